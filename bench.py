@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""bench.py -- site-pattern x node partial updates/s of the MI355X pruning engine.
+
+Contract (driver): python bench.py --gpus N --steps K --warmup W
+  N = 1: single process on cuda:0.  N > 1: launched by torch.distributed.run, one
+  rank per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the environment).
+
+Workload: BASELINE.json config 2 -- GTR+Gamma4, 4 states, 1M synthetic site patterns,
+64-taxon balanced tree (unrooted by the API like the reference, so I = 62 internal
+nodes).  Weak scaling: every rank evaluates its own 1M-pattern slice of one global
+synthetic alignment (patterns are independent), so per-GPU work is fixed as N grows.
+
+One step = one likelihood evaluation as RHomogeneousTreeLikelihood::fireParameterChanged
+does it: all branch transition matrices (K4), the full postorder traversal (partials
+kernel, one launch per tree level), the root reduction (K5) whose fixed-order
+4096-pattern block sums are all-gathered over RCCL and summed in global order (the
+only cross-GPU exchange).  value = (P x I x K x N) / max-over-ranks wall time of the
+K timed steps, inputs already resident in HBM.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "bpp-phyl_amd"))
+
+import phylo  # noqa: E402
+import plk  # noqa: E402
+import workload  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="gtr_g4_dna_1M_64", choices=sorted(workload.CONFIGS))
+    ap.add_argument("--patterns", type=int, default=None, help="override patterns per rank")
+    ap.add_argument("--cpu-sample", type=int, default=100_000, help="patterns in the CPU-baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(wl, n_sample: int, reps: int):
+    """The oracle (faithful C++11 -O2 -g restatement of computeSubtreeLikelihood with the
+    reference's nested-vector layout, usePatterns=true -- the reference default) timed on
+    one host core over a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test/bench infrastructure only
+
+    try:
+        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+    except Exception:
+        pass
+    et = wl.et
+    states = wl.simulate(0, n_sample).astype(np.int32)
+    C, S = wl.C, wl.S
+    pm = np.zeros((et.n_nodes, C, S, S))
+    for n in range(et.n_nodes):
+        if n != et.root:
+            m = wl.models[0] if wl.model_of_node is None else wl.models[wl.model_of_node[n]]
+            for c in range(C):
+                pm[n, c] = m.pij(et.brlen[n] * wl.rates[c])
+    ss, sons, lr = et.son_arrays()
+    res = {}
+    for up in (True, False):
+        _, _, t_trav, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, wl.alphabet.init_table, pm, wl.probs,
+                                             wl.root_freqs, use_patterns=up, scaling=wl.scaling, n_rep=reps)
+        res[up] = n_sample * et.n_internal / t_trav
+    return {
+        "value": res[True],
+        "unit": "site-pattern x node partial updates/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"{n_sample} patterns of the same workload ({et.n_tips} taxa, I={et.n_internal}), "
+                   f"oracle/oracle.cpp computeSubtreeLikelihood restatement, g++ -O2 -g, usePatterns=true "
+                   f"(reference default), median-free mean of {reps} traversals on 1 pinned core of "
+                   f"{platform.processor() or platform.machine()}"),
+        "value_use_patterns_false": res[False],
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    device = local if world > 1 else 0
+
+    wl = workload.make_workload(args.config)
+    P = args.patterns or wl.n_patterns
+    wl.n_patterns = P
+    start, end = rank * P, (rank + 1) * P
+    t_setup = time.time()
+    ev = workload.Evaluator(wl, device, start, end)
+    t_setup = time.time() - t_setup
+    units_step = P * wl.et.n_internal
+
+    def one_step():
+        _, _, blocks = ev.step()
+        if dist is not None:
+            t = torch.from_numpy(blocks).cuda()
+            out = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(out, t)
+            allb = torch.cat(out).cpu().numpy()
+        else:
+            allb = blocks
+        s = 0.0
+        for v in allb:   # global fixed order: identical for any GPU count
+            s += v
+        return s
+
+    for _ in range(args.warmup):
+        lnl = one_step()
+    ev.eng.reset_timing()
+    ev.eng.set_timing(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lnl = one_step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    tm = ev.eng.get_timing()
+    ev.eng.set_timing(False)
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    if rank == 0:
+        ms_step = elapsed * 1e3 / args.steps
+        value = units_step * world * args.steps / elapsed
+        bytes_pattern = wl.algorithmic_bytes_per_pattern()
+        alg_bytes = bytes_pattern * P * args.steps          # partials traffic of the timed traversals
+        part_s = tm["partials_ms"] * 1e-3
+        achieved = alg_bytes / part_s / 1e9 if part_s > 0 else None
+        launches = max(tm["launches"], 1)
+        rec = {
+            "metric": "site-pattern x node partial updates/s",
+            "value": value,
+            "unit": "updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded counter-based simulation under the model, 1 pattern = 1 column)",
+            "config": {
+                "workload": (f"{args.config}: GTR+G4 DNA, {P} patterns per GPU, {wl.et.n_tips}-taxon balanced "
+                             f"tree (unrooted, I={wl.et.n_internal})") if args.config.startswith("gtr") else args.config,
+                "patterns_per_gpu": P,
+                "taxa": wl.et.n_tips,
+                "internal_nodes": wl.et.n_internal,
+                "states": wl.S,
+                "classes": wl.C,
+                "parallelism": f"pattern-shard x{world}",
+            },
+            "lnl": lnl,
+            "partials_only_updates_per_s": units_step * args.steps / part_s if part_s > 0 else None,
+            "kernel_ms_per_step": {"partials": tm["partials_ms"] / args.steps, "pmatrix": tm["pmat_ms"] / args.steps,
+                                   "root": tm["root_ms"] / args.steps},
+            "partials_launches_per_step": launches / args.steps,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": None,
+                "basis": (f"algorithmic {bytes_pattern} B/pattern/traversal = 16*C*S*I + N + 8 "
+                          f"({bytes_pattern / wl.et.n_internal:.1f} B/update) over the summed HIP-event "
+                          f"duration of the partials launches"),
+            },
+            "setup_s": t_setup,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(wl, min(args.cpu_sample, P), args.cpu_reps)
+        prof = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(prof):
+            try:
+                tr = json.load(open(prof)).get(args.config)
+                if tr:
+                    rec["roofline"]["traffic"] = tr["hbm_bytes_per_traversal"] * P / tr["patterns"]
+                    rec["roofline"]["traffic_source"] = tr["source"]
+            except Exception:
+                pass
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,678 @@
+// plk.hip -- libplk: C-ABI (include/plk.h) over the gfx950 kernels in
+// plk_kernels.hpp.  Host-side responsibilities: device buffers owned by the
+// handle, dependency levelling of the postorder op list (independent nodes of
+// one level share a launch), launch geometry, HIP-event instrumentation.
+// There is deliberately no CPU fallback anywhere in this library.
+
+#include "../../include/plk.h"
+#include "plk_kernels.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace plk;
+
+namespace {
+
+std::string g_last_error;
+
+struct EventPair {
+  hipEvent_t a, b;
+  int kind;  // 0 partials, 1 pmat, 2 root
+};
+
+}  // namespace
+
+struct plk_handle_s {
+  int device = 0;
+  int S = 0, C = 0, n_tips = 0, n_internal = 0, n_nodes = 0, n_models = 0;
+  int64_t n_patterns = 0, n_pad = 0;
+  int n_tiles = 0, n_blocks = 0;
+  unsigned flags = 0;
+  int n_codes = 0;
+  hipStream_t stream = nullptr;
+  // device buffers
+  double* partials = nullptr;
+  int32_t* scale = nullptr;
+  uint8_t* codes = nullptr;
+  double* code_table = nullptr;
+  double* tipP = nullptr;
+  double* pmats = nullptr;
+  double* dpmats = nullptr;
+  double* d2pmats = nullptr;
+  double* V = nullptr;
+  double* Vinv = nullptr;
+  double* lambda = nullptr;
+  double* weights = nullptr;
+  double* rates = nullptr;
+  double* probs = nullptr;
+  double* pi = nullptr;
+  double* site_lnl = nullptr;
+  double* block_sums = nullptr;
+  // small staging buffers for op lists / pmatrix requests
+  KOp* d_ops = nullptr;
+  size_t d_ops_cap = 0;
+  void* d_req = nullptr;
+  size_t d_req_cap = 0;
+  int64_t slot_stride = 0;
+  // state
+  bool rates_set = false, pi_set = false, table_set = false;
+  std::vector<char> pmat_valid;   // per node
+  std::vector<char> eigen_set;    // per model
+  bool tip_tables_dirty = true;
+  std::vector<char> tip_set;
+  // instrumentation
+  bool timing = false;
+  std::vector<EventPair> events;
+  std::vector<EventPair> event_pool;
+  int64_t n_launches = 0;
+  double acc_ms[3] = {0, 0, 0};
+  std::string last_error;
+  // host copy of the op list last uploaded to d_ops (re-used when identical)
+  std::vector<KOp> h_ops;
+  std::vector<plk_op> last_ops;
+  std::vector<int> last_level_start;
+};
+
+namespace {
+
+int fail(plk_handle h, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  if (h) h->last_error = buf;
+  return code;
+}
+
+#define HIPCHK(h, call)                                                                          \
+  do {                                                                                           \
+    hipError_t e_ = (call);                                                                      \
+    if (e_ != hipSuccess) return fail((h), PLK_ERR_DEVICE, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+int dalloc(plk_handle h, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(h, PLK_ERR_OOM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
+  }
+  return PLK_OK;
+}
+
+int ensure_cap(plk_handle h, void** p, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return PLK_OK;
+  if (*p) {
+    // the buffer may still be read by queued work
+    hipStreamSynchronize(h->stream);
+    hipFree(*p);
+    *p = nullptr;
+  }
+  size_t nb = std::max(bytes, (size_t)4096);
+  int rc = dalloc(h, p, nb);
+  if (rc) return rc;
+  *cap = nb;
+  return PLK_OK;
+}
+
+EventPair get_events(plk_handle h, int kind) {
+  EventPair e;
+  if (!h->event_pool.empty()) {
+    e = h->event_pool.back();
+    h->event_pool.pop_back();
+  } else {
+    hipEventCreate(&e.a);
+    hipEventCreate(&e.b);
+  }
+  e.kind = kind;
+  return e;
+}
+
+int collect_events(plk_handle h) {
+  if (h->events.empty()) return PLK_OK;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (auto& e : h->events) {
+    float ms = 0.f;
+    HIPCHK(h, hipEventElapsedTime(&ms, e.a, e.b));
+    h->acc_ms[e.kind] += ms;
+    h->event_pool.push_back(e);
+  }
+  h->events.clear();
+  return PLK_OK;
+}
+
+bool s4_supported(int C) { return C == 1 || C == 2 || C == 4 || C == 8; }
+
+template <bool SCALE>
+void launch_s4(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
+  dim3 grid((a.n_tiles + 3) / 4, n_ops), block(256);
+  switch (h->C) {
+    case 1: partials_s4_kernel<1, SCALE><<<grid, block, 0, h->stream>>>(d_ops, a); break;
+    case 2: partials_s4_kernel<2, SCALE><<<grid, block, 0, h->stream>>>(d_ops, a); break;
+    case 4: partials_s4_kernel<4, SCALE><<<grid, block, 0, h->stream>>>(d_ops, a); break;
+    case 8: partials_s4_kernel<8, SCALE><<<grid, block, 0, h->stream>>>(d_ops, a); break;
+  }
+}
+
+template <int S, int XB>
+void launch_generic_S(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a, size_t lds) {
+  dim3 grid((a.n_tiles + 1) / 2, n_ops), block(256);
+  if (h->flags & PLK_FLAG_SCALING)
+    partials_generic_kernel<S, XB, true><<<grid, block, lds, h->stream>>>(d_ops, a, h->C);
+  else
+    partials_generic_kernel<S, XB, false><<<grid, block, lds, h->stream>>>(d_ops, a, h->C);
+}
+
+int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
+  const int S = h->S;
+  const size_t per = (size_t)h->C * S * std::max(S, h->n_codes);
+  const size_t lds = 3 * per * sizeof(double);
+  if (lds > 160 * 1024) return fail(h, PLK_ERR_UNSUPPORTED, "LDS image of %zu bytes exceeds 160 KiB", lds);
+  switch (S) {
+    case 2: launch_generic_S<2, 2>(h, d_ops, n_ops, a, lds); break;
+    case 3: launch_generic_S<3, 3>(h, d_ops, n_ops, a, lds); break;
+    case 4: launch_generic_S<4, 4>(h, d_ops, n_ops, a, lds); break;
+    case 20: launch_generic_S<20, 20>(h, d_ops, n_ops, a, lds); break;
+    case 64: launch_generic_S<64, 16>(h, d_ops, n_ops, a, lds); break;
+    default: return fail(h, PLK_ERR_UNSUPPORTED, "state count %d has no kernel instance", S);
+  }
+  return PLK_OK;
+}
+
+int refresh_tip_tables(plk_handle h) {
+  if (!h->tip_tables_dirty) return PLK_OK;
+  if (!h->table_set) return fail(h, PLK_ERR_STATE, "code table not set (plk_set_code_table)");
+  for (int t = 0; t < h->n_tips; ++t)
+    if (!h->pmat_valid[t]) return fail(h, PLK_ERR_STATE, "transition matrix of tip branch %d not set", t);
+  if (h->n_tips > 0) {
+    dim3 grid(h->n_tips, h->C);
+    tip_table_kernel<<<grid, 256, 0, h->stream>>>(h->pmats, h->code_table, h->tipP, h->n_tips, h->C, h->S,
+                                                  h->n_codes);
+    HIPCHK(h, hipGetLastError());
+  }
+  h->tip_tables_dirty = false;
+  return PLK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int plk_abi_version(void) { return PLK_ABI_VERSION; }
+
+int plk_block_size(void) { return kRootBlock; }
+
+int plk_device_count(int* count) {
+  if (!count) return fail(nullptr, PLK_ERR_ARG, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(nullptr, PLK_ERR_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *count = n;
+  return PLK_OK;
+}
+
+const char* plk_last_error(plk_handle h) { return h ? h->last_error.c_str() : g_last_error.c_str(); }
+
+int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int n_tips, int n_internal,
+               int n_models, unsigned flags, plk_handle* out) {
+  if (!out) return fail(nullptr, PLK_ERR_ARG, "null out handle");
+  *out = nullptr;
+  if (n_states < 2 || n_states > 64) return fail(nullptr, PLK_ERR_UNSUPPORTED, "n_states %d not in [2, 64]", n_states);
+  if (n_classes < 1 || n_classes > 16) return fail(nullptr, PLK_ERR_UNSUPPORTED, "n_classes %d not in [1, 16]", n_classes);
+  if (n_patterns < 1 || n_tips < 0 || n_internal < 1 || n_models < 1)
+    return fail(nullptr, PLK_ERR_ARG, "bad sizes (patterns %lld tips %d internal %d models %d)",
+                (long long)n_patterns, n_tips, n_internal, n_models);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(nullptr, PLK_ERR_DEVICE, "no HIP device available (libplk has no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(nullptr, PLK_ERR_DEVICE, "device %d out of range (%d devices)", device, ndev);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+    return fail(nullptr, PLK_ERR_DEVICE, "hipGetDeviceProperties failed");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(nullptr, PLK_ERR_DEVICE, "device %d is %s; libplk is built for gfx950 only", device, prop.gcnArchName);
+  if (hipSetDevice(device) != hipSuccess) return fail(nullptr, PLK_ERR_DEVICE, "hipSetDevice(%d) failed", device);
+
+  plk_handle h = new plk_handle_s();
+  h->device = device;
+  h->S = n_states;
+  h->C = n_classes;
+  h->n_tips = n_tips;
+  h->n_internal = n_internal;
+  h->n_nodes = n_tips + n_internal;
+  h->n_models = n_models;
+  h->flags = flags;
+  h->n_patterns = n_patterns;
+  h->n_tiles = (int)((n_patterns + kTile - 1) / kTile);
+  h->n_pad = (int64_t)h->n_tiles * kTile;
+  h->n_blocks = (int)((n_patterns + kRootBlock - 1) / kRootBlock);
+  h->slot_stride = (int64_t)h->n_tiles * n_classes * n_states * kTile;
+  h->pmat_valid.assign(h->n_nodes, 0);
+  h->eigen_set.assign(n_models, 0);
+  h->tip_set.assign(n_tips, 0);
+  int rc = PLK_OK;
+  auto bail = [&](int code) {
+    plk_destroy(h);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(nullptr, PLK_ERR_DEVICE, "hipStreamCreate failed"));
+  const size_t S2 = (size_t)n_states * n_states;
+  if ((rc = dalloc(h, (void**)&h->partials, (size_t)n_internal * h->slot_stride * sizeof(double)))) return bail(rc);
+  if (flags & PLK_FLAG_SCALING) {
+    if ((rc = dalloc(h, (void**)&h->scale, (size_t)n_internal * h->n_pad * sizeof(int32_t)))) return bail(rc);
+  }
+  if ((rc = dalloc(h, (void**)&h->codes, (size_t)std::max(n_tips, 1) * h->n_pad))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->pmats, (size_t)h->n_nodes * n_classes * S2 * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->V, (size_t)n_models * S2 * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->Vinv, (size_t)n_models * S2 * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->lambda, (size_t)n_models * n_states * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->weights, (size_t)h->n_pad * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->rates, 16 * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->probs, 16 * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->pi, 64 * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->site_lnl, (size_t)h->n_pad * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->block_sums, (size_t)h->n_blocks * sizeof(double)))) return bail(rc);
+  // default weights 1 for real patterns, 0 for padding
+  std::vector<double> w(h->n_pad, 0.0);
+  std::fill(w.begin(), w.begin() + n_patterns, 1.0);
+  if (hipMemcpy(h->weights, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+    return bail(fail(nullptr, PLK_ERR_DEVICE, "weights upload failed"));
+  if (hipMemset(h->codes, 0, (size_t)std::max(n_tips, 1) * h->n_pad) != hipSuccess)
+    return bail(fail(nullptr, PLK_ERR_DEVICE, "codes memset failed"));
+  if (h->scale && hipMemset(h->scale, 0, (size_t)n_internal * h->n_pad * sizeof(int32_t)) != hipSuccess)
+    return bail(fail(nullptr, PLK_ERR_DEVICE, "scale memset failed"));
+  *out = h;
+  return PLK_OK;
+}
+
+int plk_destroy(plk_handle h) {
+  if (!h) return PLK_OK;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
+                  h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
+                  h->block_sums, h->d_ops, h->d_req};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  for (auto& e : h->events) {
+    hipEventDestroy(e.a);
+    hipEventDestroy(e.b);
+  }
+  for (auto& e : h->event_pool) {
+    hipEventDestroy(e.a);
+    hipEventDestroy(e.b);
+  }
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return PLK_OK;
+}
+
+int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec) {
+  if (!h || !code_to_vec || n_codes < 1 || n_codes > 256) return fail(h, PLK_ERR_ARG, "bad code table (n_codes %d)", n_codes);
+  if (h->S == 4 && n_codes > kMaxCodes4 && s4_supported(h->C))
+    return fail(h, PLK_ERR_UNSUPPORTED, "4-state engine supports at most %d codes", kMaxCodes4);
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->code_table) hipFree(h->code_table);
+  if (h->tipP) hipFree(h->tipP);
+  h->code_table = nullptr;
+  h->tipP = nullptr;
+  int rc;
+  if ((rc = dalloc(h, (void**)&h->code_table, (size_t)n_codes * h->S * sizeof(double)))) return rc;
+  if ((rc = dalloc(h, (void**)&h->tipP, (size_t)std::max(h->n_tips, 1) * h->C * n_codes * h->S * sizeof(double))))
+    return rc;
+  HIPCHK(h, hipMemcpy(h->code_table, code_to_vec, (size_t)n_codes * h->S * sizeof(double), hipMemcpyHostToDevice));
+  h->n_codes = n_codes;
+  h->table_set = true;
+  h->tip_tables_dirty = true;
+  return PLK_OK;
+}
+
+int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes) {
+  if (!h || !codes || tip < 0 || tip >= h->n_tips) return fail(h, PLK_ERR_ARG, "bad tip index %d", tip);
+  if (!h->table_set) return fail(h, PLK_ERR_STATE, "plk_set_code_table must precede plk_set_tip_codes");
+  for (int64_t i = 0; i < h->n_patterns; ++i)
+    if (codes[i] >= h->n_codes)
+      return fail(h, PLK_ERR_BAD_CODE, "tip %d pattern %lld: code %d outside the code table (%d codes)", tip,
+                  (long long)i, (int)codes[i], h->n_codes);
+  hipSetDevice(h->device);
+  HIPCHK(h, hipMemcpy(h->codes + (size_t)tip * h->n_pad, codes, (size_t)h->n_patterns, hipMemcpyHostToDevice));
+  h->tip_set[tip] = 1;
+  return PLK_OK;
+}
+
+int plk_set_pattern_weights(plk_handle h, const double* weights) {
+  if (!h || !weights) return fail(h, PLK_ERR_ARG, "null weights");
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipMemcpy(h->weights, weights, (size_t)h->n_patterns * sizeof(double), hipMemcpyHostToDevice));
+  return PLK_OK;
+}
+
+int plk_set_category_rates(plk_handle h, const double* rates, const double* probs) {
+  if (!h || !rates || !probs) return fail(h, PLK_ERR_ARG, "null rates/probs");
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipMemcpy(h->rates, rates, h->C * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->probs, probs, h->C * sizeof(double), hipMemcpyHostToDevice));
+  h->rates_set = true;
+  return PLK_OK;
+}
+
+int plk_set_root_frequencies(plk_handle h, const double* pi) {
+  if (!h || !pi) return fail(h, PLK_ERR_ARG, "null frequencies");
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipMemcpy(h->pi, pi, h->S * sizeof(double), hipMemcpyHostToDevice));
+  h->pi_set = true;
+  return PLK_OK;
+}
+
+int plk_set_eigen(plk_handle h, int model, const double* V, const double* Vinv, const double* lambda) {
+  if (!h || !V || !Vinv || !lambda || model < 0 || model >= h->n_models)
+    return fail(h, PLK_ERR_ARG, "bad eigen system (model %d)", model);
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const size_t S2 = (size_t)h->S * h->S;
+  HIPCHK(h, hipMemcpy(h->V + model * S2, V, S2 * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->Vinv + model * S2, Vinv, S2 * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->lambda + (size_t)model * h->S, lambda, h->S * sizeof(double), hipMemcpyHostToDevice));
+  h->eigen_set[model] = 1;
+  return PLK_OK;
+}
+
+int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32_t* model, const double* t,
+                         unsigned deriv_mask) {
+  if (!h || n < 0 || (n > 0 && (!branch || !t))) return fail(h, PLK_ERR_ARG, "bad pmatrix request");
+  if (n == 0) return PLK_OK;
+  if (!h->rates_set) return fail(h, PLK_ERR_STATE, "plk_set_category_rates must precede plk_update_pmatrices");
+  if (deriv_mask == 0) deriv_mask = PLK_DERIV_P;
+  for (int i = 0; i < n; ++i) {
+    if (branch[i] < 0 || branch[i] >= h->n_nodes) return fail(h, PLK_ERR_ARG, "branch %d out of range", branch[i]);
+    const int m = model ? model[i] : 0;
+    if (m < 0 || m >= h->n_models) return fail(h, PLK_ERR_ARG, "model %d out of range", m);
+    if (!h->eigen_set[m]) return fail(h, PLK_ERR_STATE, "eigen system %d not set", m);
+    if (!(t[i] >= 0.0)) return fail(h, PLK_ERR_ARG, "branch length %g not >= 0", t[i]);
+  }
+  hipSetDevice(h->device);
+  const size_t S2 = (size_t)h->S * h->S;
+  if ((deriv_mask & PLK_DERIV_DP) && !h->dpmats) {
+    int rc = dalloc(h, (void**)&h->dpmats, (size_t)h->n_nodes * h->C * S2 * sizeof(double));
+    if (rc) return rc;
+  }
+  if ((deriv_mask & PLK_DERIV_D2P) && !h->d2pmats) {
+    int rc = dalloc(h, (void**)&h->d2pmats, (size_t)h->n_nodes * h->C * S2 * sizeof(double));
+    if (rc) return rc;
+  }
+  // request buffer: branch[n] | model[n] | t[n]
+  const size_t bytes = (size_t)n * (2 * sizeof(int32_t) + sizeof(double)) + 64;
+  int rc = ensure_cap(h, &h->d_req, &h->d_req_cap, bytes);
+  if (rc) return rc;
+  std::vector<char> staging(bytes, 0);
+  const size_t off_t = 0, off_b = (size_t)n * sizeof(double), off_m = off_b + (size_t)n * sizeof(int32_t);
+  std::memcpy(staging.data() + off_t, t, n * sizeof(double));
+  std::memcpy(staging.data() + off_b, branch, n * sizeof(int32_t));
+  if (model) std::memcpy(staging.data() + off_m, model, n * sizeof(int32_t));
+  // synchronous copy keeps the pageable staging buffer safe; it is tiny
+  HIPCHK(h, hipMemcpyAsync(h->d_req, staging.data(), bytes, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  PmatArgs a;
+  a.t = reinterpret_cast<const double*>((char*)h->d_req + off_t);
+  a.branch = reinterpret_cast<const int32_t*>((char*)h->d_req + off_b);
+  a.model = model ? reinterpret_cast<const int32_t*>((char*)h->d_req + off_m) : nullptr;
+  a.rates = h->rates;
+  a.V = h->V;
+  a.Vinv = h->Vinv;
+  a.lambda = h->lambda;
+  a.P = h->pmats;
+  a.dP = h->dpmats;
+  a.d2P = h->d2pmats;
+  a.S = h->S;
+  a.C = h->C;
+  a.mask = deriv_mask;
+  EventPair ev;
+  if (h->timing) {
+    ev = get_events(h, 1);
+    hipEventRecord(ev.a, h->stream);
+  }
+  const size_t lds = (size_t)(h->S + S2) * sizeof(double);
+  pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a);
+  HIPCHK(h, hipGetLastError());
+  if (h->timing) {
+    hipEventRecord(ev.b, h->stream);
+    h->events.push_back(ev);
+  }
+  if (deriv_mask & PLK_DERIV_P) {
+    for (int i = 0; i < n; ++i) {
+      h->pmat_valid[branch[i]] = 1;
+      if (branch[i] < h->n_tips) h->tip_tables_dirty = true;
+    }
+  }
+  return PLK_OK;
+}
+
+int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
+  if (!h || !P || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const size_t n = (size_t)h->C * h->S * h->S;
+  HIPCHK(h, hipMemcpy(h->pmats + (size_t)branch * n, P, n * sizeof(double), hipMemcpyHostToDevice));
+  h->pmat_valid[branch] = 1;
+  if (branch < h->n_tips) h->tip_tables_dirty = true;
+  return PLK_OK;
+}
+
+int plk_get_pmatrix(plk_handle h, int branch, double* P) {
+  if (!h || !P || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const size_t n = (size_t)h->C * h->S * h->S;
+  HIPCHK(h, hipMemcpy(P, h->pmats + (size_t)branch * n, n * sizeof(double), hipMemcpyDeviceToHost));
+  return PLK_OK;
+}
+
+int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
+  if (!h || n_ops < 0 || (n_ops > 0 && !ops)) return fail(h, PLK_ERR_ARG, "bad op list");
+  if (n_ops == 0) return PLK_OK;
+  hipSetDevice(h->device);
+  // Validate and level the ops: level(op) = 1 + max(level of the op that last
+  // wrote each internal child in this call, level of the last writer of parent).
+  std::vector<int> writer_level(h->n_nodes, -1);
+  std::vector<int> level(n_ops);
+  int max_level = 0;
+  for (int i = 0; i < n_ops; ++i) {
+    const plk_op& o = ops[i];
+    if (o.parent < h->n_tips || o.parent >= h->n_nodes)
+      return fail(h, PLK_ERR_ARG, "op %d: parent %d is not an internal node", i, o.parent);
+    if (o.n_children < 1 || o.n_children > 3) return fail(h, PLK_ERR_ARG, "op %d: %d children", i, o.n_children);
+    int lv = writer_level[o.parent];
+    for (int k = 0; k < o.n_children; ++k) {
+      const int c = o.child[k];
+      if (c < 0 || c >= h->n_nodes || c == o.parent) return fail(h, PLK_ERR_ARG, "op %d: bad child %d", i, c);
+      if (!h->pmat_valid[c]) return fail(h, PLK_ERR_STATE, "op %d: transition matrix of branch %d not set", i, c);
+      if (c < h->n_tips && !h->tip_set[c]) return fail(h, PLK_ERR_STATE, "op %d: tip %d has no codes", i, c);
+      lv = std::max(lv, writer_level[c]);
+    }
+    level[i] = lv + 1;
+    writer_level[o.parent] = level[i];
+    max_level = std::max(max_level, level[i]);
+  }
+  int rc = refresh_tip_tables(h);
+  if (rc) return rc;
+  std::vector<int> level_start(max_level + 2, 0);
+  const bool same = (int)h->last_ops.size() == n_ops &&
+                    std::memcmp(h->last_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
+  if (same) {
+    level_start = h->last_level_start;
+  } else {
+  // Build device op list grouped by level (stable within a level).
+  h->h_ops.clear();
+  for (int i = 0; i < n_ops; ++i) level_start[level[i] + 1]++;
+  for (int l = 0; l <= max_level; ++l) level_start[l + 1] += level_start[l];
+  h->h_ops.resize(n_ops);
+  std::vector<int> fill(level_start.begin(), level_start.end() - 1);
+  for (int i = 0; i < n_ops; ++i) {
+    const plk_op& o = ops[i];
+    KOp k;
+    std::memset(&k, 0, sizeof(k));
+    k.parent = o.parent - h->n_tips;
+    k.n = o.n_children;
+    k.flags = o.flags;
+    for (int j = 0; j < o.n_children; ++j) {
+      const int c = o.child[j];
+      k.branch[j] = c;
+      k.is_tip[j] = c < h->n_tips;
+      k.child[j] = c < h->n_tips ? c : c - h->n_tips;
+    }
+    h->h_ops[fill[level[i]]++] = k;
+  }
+  rc = ensure_cap(h, (void**)&h->d_ops, &h->d_ops_cap, n_ops * sizeof(KOp));
+  if (rc) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->d_ops, h->h_ops.data(), n_ops * sizeof(KOp), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // h_ops is pageable and reused
+  h->last_ops.assign(ops, ops + n_ops);
+  h->last_level_start = level_start;
+  }
+
+  PartialsArgs a;
+  a.partials = h->partials;
+  a.scale = h->scale;
+  a.codes = h->codes;
+  a.tipP = h->tipP;
+  a.pmats = h->pmats;
+  a.slot_stride = h->slot_stride;
+  a.n_pad = h->n_pad;
+  a.n_tiles = h->n_tiles;
+  a.n_codes = h->n_codes;
+  const bool s4 = (h->S == 4 && s4_supported(h->C) && h->n_codes <= kMaxCodes4);
+  for (int l = 0; l <= max_level; ++l) {
+    const int cnt = level_start[l + 1] - level_start[l];
+    if (cnt == 0) continue;
+    const KOp* d = h->d_ops + level_start[l];
+    EventPair ev;
+    if (h->timing) {
+      ev = get_events(h, 0);
+      hipEventRecord(ev.a, h->stream);
+    }
+    if (s4) {
+      if (h->flags & PLK_FLAG_SCALING)
+        launch_s4<true>(h, d, cnt, a);
+      else
+        launch_s4<false>(h, d, cnt, a);
+    } else {
+      rc = launch_generic(h, d, cnt, a);
+      if (rc) return rc;
+    }
+    HIPCHK(h, hipGetLastError());
+    if (h->timing) {
+      hipEventRecord(ev.b, h->stream);
+      h->events.push_back(ev);
+    }
+    h->n_launches++;
+  }
+  return PLK_OK;
+}
+
+int plk_get_partials(plk_handle h, int node, double* out) {
+  if (!h || !out || node < h->n_tips || node >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad internal node %d", node);
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  std::vector<double> buf(h->slot_stride);
+  HIPCHK(h, hipMemcpy(buf.data(), h->partials + (size_t)(node - h->n_tips) * h->slot_stride,
+                      buf.size() * sizeof(double), hipMemcpyDeviceToHost));
+  const int CS = h->C * h->S;
+  for (int64_t p = 0; p < h->n_patterns; ++p) {
+    const int64_t tile = p / kTile, q = p % kTile;
+    for (int cs = 0; cs < CS; ++cs) out[p * CS + cs] = buf[(tile * CS + cs) * kTile + q];
+  }
+  return PLK_OK;
+}
+
+int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums) {
+  if (!h || root < h->n_tips || root >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad root node %d", root);
+  if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
+  hipSetDevice(h->device);
+  RootArgs a;
+  a.partials = h->partials + (size_t)(root - h->n_tips) * h->slot_stride;
+  a.scale = h->scale ? h->scale + (size_t)(root - h->n_tips) * h->n_pad : nullptr;
+  a.weights = h->weights;
+  a.pi = h->pi;
+  a.probs = h->probs;
+  a.site_lnl = h->site_lnl;
+  a.block_sums = h->block_sums;
+  a.n_patterns = h->n_patterns;
+  a.S = h->S;
+  a.C = h->C;
+  a.guard = (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0;
+  EventPair ev;
+  if (h->timing) {
+    ev = get_events(h, 2);
+    hipEventRecord(ev.a, h->stream);
+  }
+  root_kernel<<<h->n_blocks, 256, 0, h->stream>>>(a);
+  HIPCHK(h, hipGetLastError());
+  if (h->timing) {
+    hipEventRecord(ev.b, h->stream);
+    h->events.push_back(ev);
+  }
+  std::vector<double> bs(h->n_blocks);
+  HIPCHK(h, hipMemcpyAsync(bs.data(), h->block_sums, bs.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  if (site_lnl)
+    HIPCHK(h, hipMemcpyAsync(site_lnl, h->site_lnl, (size_t)h->n_patterns * sizeof(double), hipMemcpyDeviceToHost,
+                             h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  double s = 0.0;
+  for (double v : bs) s += v;  // fixed order: block 0, 1, 2, ...
+  if (lnl) *lnl = s;
+  if (block_sums) std::memcpy(block_sums, bs.data(), bs.size() * sizeof(double));
+  return PLK_OK;
+}
+
+int plk_set_timing(plk_handle h, int enable) {
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  h->timing = enable != 0;
+  return PLK_OK;
+}
+
+int plk_get_timing(plk_handle h, int64_t* n_launches, double* partials_ms, double* pmat_ms, double* root_ms) {
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  hipSetDevice(h->device);
+  int rc = collect_events(h);
+  if (rc) return rc;
+  if (n_launches) *n_launches = h->n_launches;
+  if (partials_ms) *partials_ms = h->acc_ms[0];
+  if (pmat_ms) *pmat_ms = h->acc_ms[1];
+  if (root_ms) *root_ms = h->acc_ms[2];
+  return PLK_OK;
+}
+
+int plk_reset_timing(plk_handle h) {
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  int rc = collect_events(h);
+  if (rc) return rc;
+  h->n_launches = 0;
+  h->acc_ms[0] = h->acc_ms[1] = h->acc_ms[2] = 0.0;
+  return PLK_OK;
+}
+
+int plk_synchronize(plk_handle h) {
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PLK_OK;
+}
+
+}  // extern "C"

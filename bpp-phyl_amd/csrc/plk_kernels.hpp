@@ -1,0 +1,398 @@
+// plk_kernels.hpp -- CDNA4 (gfx950) device code of libplk.
+//
+// Hot path: the per-node partial-likelihood update of
+// RHomogeneousTreeLikelihood::computeSubtreeLikelihood
+// (/root/reference/src/Bpp/Phyl/Likelihood/RHomogeneousTreeLikelihood.cpp:802-863):
+//     L_node[i][c][x] = prod_son sum_y P_son[c][x][y] * L_son[i][c][y]
+// plus the batched transition-matrix exponential behind getPij_t
+// (Model/AbstractSubstitutionModel.cpp:426-641) and the root reduction
+// (Likelihood/RHomogeneousTreeLikelihood.cpp:162-216).
+//
+// HBM layout (site-pattern-major, tiled): a partial vector of one internal node
+// is [tile][c*S + s][kTile] fp64 with kTile = 128 patterns per tile.  One
+// wave-instruction of the 4-state kernel loads 64 lanes x 16 B (two adjacent
+// patterns per lane) = 1 KiB contiguous; the generic kernel loads 64 x 8 B.
+// Tips are stored as one uint8 state code per pattern and resolved through a
+// per-branch table tipP[c][code][x] = sum_y P[c][x][y] * init[code][y], which
+// replaces the reference's dense one-hot leaf matvec.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace plk {
+
+constexpr int kTile = 128;          // patterns per tile (layout granule)
+constexpr int kRootBlock = 4096;    // patterns per fixed-order reduction block
+constexpr int kMaxCodes4 = 32;      // code-table rows the 4-state kernel stages in LDS
+constexpr double kScaleUp = 115792089237316195423570985008687907853269984665640564039457584007913129639936.0;  // 2^256
+constexpr double kScaleThr = 1.0 / kScaleUp;                                                                 // 2^-256
+constexpr double kLn2x256 = 177.44567822334599921;                                                           // 256 ln 2
+
+// Device-side description of one partial update (children already resolved
+// into tip indices or internal slots).
+struct KOp {
+  int32_t parent;    // internal slot
+  int32_t n;         // number of children (1..3)
+  int32_t child[3];  // tip index (is_tip) or internal slot
+  int32_t branch[3]; // node index of the child = transition-matrix index
+  int32_t is_tip[3];
+  int32_t flags;     // PLK_OP_ACCUMULATE
+};
+
+struct PartialsArgs {
+  double* partials;          // [n_internal][slot_stride]
+  int32_t* scale;            // [n_internal][n_pad] (SCALE only)
+  const uint8_t* codes;      // [n_tips][n_pad]
+  const double* tipP;        // [n_tips][C][n_codes][S]
+  const double* pmats;       // [n_nodes][C][S][S]
+  int64_t slot_stride;       // doubles per internal slot = n_tiles * C*S * kTile
+  int64_t n_pad;             // padded pattern count
+  int32_t n_tiles;
+  int32_t n_codes;
+};
+
+// ---------------------------------------------------------------------------
+// 4-state kernel: one lane = two adjacent patterns (double2 loads/stores),
+// one wave = one 128-pattern tile, 4 waves per workgroup.  P(t) of the branch
+// is wave-uniform and lives in scalar registers (s_load), tip tables in LDS.
+// HBM-bound: per internal child 16*C B/pattern read, 8*C*S B/pattern written.
+// ---------------------------------------------------------------------------
+template <int C, bool SCALE>
+__global__ __launch_bounds__(256) void partials_s4_kernel(const KOp* __restrict__ ops, PartialsArgs a) {
+  constexpr int S = 4;
+  constexpr int CS = C * S;
+  __shared__ double tipT[3][C * kMaxCodes4 * S];
+  const KOp& op = ops[blockIdx.y];
+  const int n = op.n;
+  const int nc = a.n_codes;
+  // Stage the tip tables of tip children.
+  for (int k = 0; k < n; ++k) {
+    if (op.is_tip[k]) {
+      const double* src = a.tipP + (size_t)op.child[k] * (C * nc * S);
+      for (int i = threadIdx.x; i < C * nc * S; i += blockDim.x) tipT[k][i] = src[i];
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= a.n_tiles) return;
+  const size_t toff = (size_t)tile * (CS * kTile);
+  double2* outp = reinterpret_cast<double2*>(a.partials + (size_t)op.parent * a.slot_stride + toff) + lane;
+
+  double2 acc[C][S];
+  int2 cnt = make_int2(0, 0);
+  if (op.flags & 1) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int x = 0; x < S; ++x) acc[c][x] = outp[(c * S + x) * (kTile / 2)];
+    if (SCALE) cnt = reinterpret_cast<const int2*>(a.scale + (size_t)op.parent * a.n_pad + (size_t)tile * kTile)[lane];
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int x = 0; x < S; ++x) acc[c][x] = make_double2(1.0, 1.0);
+  }
+
+  for (int k = 0; k < n; ++k) {
+    const int child = op.child[k];
+    if (op.is_tip[k]) {
+      const uint16_t cc =
+          reinterpret_cast<const uint16_t*>(a.codes + (size_t)child * a.n_pad + (size_t)tile * kTile)[lane];
+      const int c0 = cc & 0xff, c1 = cc >> 8;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const double* t0 = &tipT[k][(c * nc + c0) * S];
+        const double* t1 = &tipT[k][(c * nc + c1) * S];
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+          acc[c][x].x *= t0[x];
+          acc[c][x].y *= t1[x];
+        }
+      }
+    } else {
+      const double* __restrict__ P = a.pmats + (size_t)op.branch[k] * (C * S * S);
+      const double2* L = reinterpret_cast<const double2*>(a.partials + (size_t)child * a.slot_stride + toff) + lane;
+      double2 l[C][S];
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int y = 0; y < S; ++y) l[c][y] = L[(c * S + y) * (kTile / 2)];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+          const double* Px = P + (c * S + x) * S;
+          double s0 = Px[0] * l[c][0].x, s1 = Px[0] * l[c][0].y;
+#pragma unroll
+          for (int y = 1; y < S; ++y) {
+            s0 = __builtin_fma(Px[y], l[c][y].x, s0);
+            s1 = __builtin_fma(Px[y], l[c][y].y, s1);
+          }
+          acc[c][x].x *= s0;
+          acc[c][x].y *= s1;
+        }
+      }
+      if (SCALE) {
+        const int2 sc = reinterpret_cast<const int2*>(a.scale + (size_t)child * a.n_pad + (size_t)tile * kTile)[lane];
+        cnt.x += sc.x;
+        cnt.y += sc.y;
+      }
+    }
+  }
+
+  if (SCALE) {
+    double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int x = 0; x < S; ++x) {
+        m0 = fmax(m0, acc[c][x].x);
+        m1 = fmax(m1, acc[c][x].y);
+      }
+    const bool r0 = (m0 > 0.0 && m0 < kScaleThr), r1 = (m1 > 0.0 && m1 < kScaleThr);
+    if (r0 || r1) {
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+          if (r0) acc[c][x].x *= kScaleUp;
+          if (r1) acc[c][x].y *= kScaleUp;
+        }
+      cnt.x += r0;
+      cnt.y += r1;
+    }
+    reinterpret_cast<int2*>(a.scale + (size_t)op.parent * a.n_pad + (size_t)tile * kTile)[lane] = cnt;
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int x = 0; x < S; ++x) outp[(c * S + x) * (kTile / 2)] = acc[c][x];
+}
+
+// ---------------------------------------------------------------------------
+// Generic-S kernel (S up to 64): one lane = one pattern, 2 tiles per 256-thread
+// workgroup.  The children's P(t) (C x S x S each) and tip tables are staged in
+// LDS once per workgroup; inner products read P by wave-uniform LDS address
+// (broadcast).  Outputs are produced in chunks of XB states per class.
+// ---------------------------------------------------------------------------
+template <int S, int XB, bool SCALE>
+__global__ __launch_bounds__(256) void partials_generic_kernel(const KOp* __restrict__ ops, PartialsArgs a, int C) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const KOp& op = ops[blockIdx.y];
+  const int n = op.n;
+  const int nc = a.n_codes;
+  const int CS = C * S;
+  // LDS image: per child k, either P (C*S*S) or tipP (C*nc*S); offset k*per.
+  const int per = C * S * ((S > nc) ? S : nc);
+  for (int k = 0; k < n; ++k) {
+    const double* src = op.is_tip[k] ? a.tipP + (size_t)op.child[k] * (C * nc * S)
+                                     : a.pmats + (size_t)op.branch[k] * (C * S * S);
+    const int cnt = op.is_tip[k] ? C * nc * S : C * S * S;
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) lds[k * per + i] = src[i];
+  }
+  __syncthreads();
+  const int q = threadIdx.x & (kTile - 1);
+  const int tile = blockIdx.x * 2 + (threadIdx.x >> 7);
+  if (tile >= a.n_tiles) return;
+  const size_t toff = (size_t)tile * ((size_t)CS * kTile) + q;
+  double* outp = a.partials + (size_t)op.parent * a.slot_stride + toff;
+  const size_t pidx = (size_t)tile * kTile + q;
+
+  int cnt = 0;
+  if (SCALE) {
+    if (op.flags & 1) cnt = a.scale[(size_t)op.parent * a.n_pad + pidx];
+    for (int k = 0; k < n; ++k)
+      if (!op.is_tip[k]) cnt += a.scale[(size_t)op.child[k] * a.n_pad + pidx];
+  }
+  int code[3] = {0, 0, 0};
+  for (int k = 0; k < n; ++k)
+    if (op.is_tip[k]) code[k] = a.codes[(size_t)op.child[k] * a.n_pad + pidx];
+
+  double m = 0.0;
+  for (int c = 0; c < C; ++c) {
+    for (int x0 = 0; x0 < S; x0 += XB) {
+      double acc[XB];
+      if (op.flags & 1) {
+#pragma unroll
+        for (int xb = 0; xb < XB; ++xb) acc[xb] = outp[(size_t)(c * S + x0 + xb) * kTile];
+      } else {
+#pragma unroll
+        for (int xb = 0; xb < XB; ++xb) acc[xb] = 1.0;
+      }
+      for (int k = 0; k < n; ++k) {
+        if (op.is_tip[k]) {
+          const double* t = &lds[k * per + (c * nc + code[k]) * S + x0];
+#pragma unroll
+          for (int xb = 0; xb < XB; ++xb) acc[xb] *= t[xb];
+        } else {
+          const double* L = a.partials + (size_t)op.child[k] * a.slot_stride + toff + (size_t)c * S * kTile;
+          const double* Pc = &lds[k * per + (c * S + x0) * S];
+          double s[XB];
+          {
+            const double l0 = L[0];
+#pragma unroll
+            for (int xb = 0; xb < XB; ++xb) s[xb] = Pc[xb * S] * l0;
+          }
+#pragma unroll 4
+          for (int y = 1; y < S; ++y) {
+            const double ly = L[(size_t)y * kTile];
+#pragma unroll
+            for (int xb = 0; xb < XB; ++xb) s[xb] = __builtin_fma(Pc[xb * S + y], ly, s[xb]);
+          }
+#pragma unroll
+          for (int xb = 0; xb < XB; ++xb) acc[xb] *= s[xb];
+        }
+      }
+#pragma unroll
+      for (int xb = 0; xb < XB; ++xb) {
+        if (SCALE) m = fmax(m, acc[xb]);
+        outp[(size_t)(c * S + x0 + xb) * kTile] = acc[xb];
+      }
+    }
+  }
+  if (SCALE) {
+    if (m > 0.0 && m < kScaleThr) {
+      for (int i = 0; i < CS; ++i) outp[(size_t)i * kTile] *= kScaleUp;
+      cnt += 1;
+    }
+    a.scale[(size_t)op.parent * a.n_pad + pidx] = cnt;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4: batched transition matrices.  One workgroup per (branch i, class c):
+//   P = V diag(exp(lambda * r_c * t_i)) Vinv                (getPij_t :426-438)
+//   dP = r_c * V diag(lambda e) Vinv, d2P = r_c^2 V diag(lambda^2 e) Vinv
+//   (AbstractHomogeneousTreeLikelihood.cpp:375-413, AbstractSubstitutionModel.cpp:499-641)
+// ---------------------------------------------------------------------------
+struct PmatArgs {
+  const int32_t* branch;   // [n]
+  const int32_t* model;    // [n] or null
+  const double* t;         // [n]
+  const double* rates;     // [C]
+  const double* V;         // [n_models][S][S]
+  const double* Vinv;      // [n_models][S][S]
+  const double* lambda;    // [n_models][S]
+  double* P;               // [n_nodes][C][S][S]
+  double* dP;
+  double* d2P;
+  int S, C;
+  unsigned mask;
+};
+
+__global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int i = blockIdx.x, c = blockIdx.y, S = a.S;
+  const int b = a.branch[i];
+  const int m = a.model ? a.model[i] : 0;
+  const double rc = a.rates[c];
+  const double tt = a.t[i] * rc;
+  double* e = sm;           // exp(lambda t)
+  double* Vm = sm + S;      // V
+  const double* V = a.V + (size_t)m * S * S;
+  const double* Vi = a.Vinv + (size_t)m * S * S;
+  const double* lam = a.lambda + (size_t)m * S;
+  for (int k = threadIdx.x; k < S; k += blockDim.x) e[k] = exp(lam[k] * tt);
+  for (int k = threadIdx.x; k < S * S; k += blockDim.x) Vm[k] = V[k];
+  __syncthreads();
+  const size_t off = ((size_t)b * a.C + c) * S * S;
+  for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
+    const int x = idx / S, y = idx % S;
+    double p = 0.0, dp = 0.0, d2p = 0.0;
+    for (int k = 0; k < S; ++k) {
+      const double w = Vm[x * S + k] * Vi[k * S + y];
+      const double ek = e[k];
+      p = __builtin_fma(w, ek, p);
+      if (a.mask & 6u) {
+        const double le = lam[k] * ek;
+        dp = __builtin_fma(w, le, dp);
+        d2p = __builtin_fma(w, lam[k] * le, d2p);
+      }
+    }
+    if (tt == 0.0) p = (x == y) ? 1.0 : 0.0;  // getPij_t: t == 0 -> identity (:428-431)
+    if (a.mask & 1u) a.P[off + idx] = p;
+    if (a.mask & 2u) a.dP[off + idx] = rc * dp;
+    if (a.mask & 4u) a.d2P[off + idx] = rc * rc * d2p;
+  }
+}
+
+// tipP[tip][c][code][x] = sum_y P[tip][c][x][y] * init[code][y]
+__global__ __launch_bounds__(256) void tip_table_kernel(const double* __restrict__ P, const double* __restrict__ init,
+                                                        double* __restrict__ tipP, int n_tips, int C, int S,
+                                                        int n_codes) {
+  const int tip = blockIdx.x, c = blockIdx.y;
+  if (tip >= n_tips) return;
+  const double* Pc = P + ((size_t)tip * C + c) * S * S;
+  double* out = tipP + ((size_t)tip * C + c) * n_codes * S;
+  for (int idx = threadIdx.x; idx < n_codes * S; idx += blockDim.x) {
+    const int code = idx / S, x = idx % S;
+    double s = 0.0;
+    for (int y = 0; y < S; ++y) s = __builtin_fma(Pc[x * S + y], init[code * S + y], s);
+    out[idx] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K5: root reduction.  Per pattern p: l_c = sum_s L[c][s] pi_s, l = sum_c l_c w_c
+// with the reference's "<= 0 terms dropped" guards (HOMOG) or NH clamp;
+// lnl_p = log(l) - nscale * 256 ln 2.  Block b sums w_p * lnl_p over patterns
+// [b*4096, (b+1)*4096) in a fixed order.
+// ---------------------------------------------------------------------------
+struct RootArgs {
+  const double* partials;  // root slot base
+  const int32_t* scale;    // root scale row or null
+  const double* weights;   // [n_pad]
+  const double* pi;        // [S]
+  const double* probs;     // [C]
+  double* site_lnl;        // [n_pad]
+  double* block_sums;      // [n_blocks]
+  int64_t n_patterns;
+  int S, C;
+  int guard;               // 1: homogeneous guards, 0: NH clamp
+};
+
+__global__ __launch_bounds__(256) void root_kernel(RootArgs a) {
+  __shared__ double red[256];
+  const int CS = a.C * a.S;
+  double local = 0.0;
+  for (int j = 0; j < kRootBlock / 256; ++j) {
+    const int64_t p = (int64_t)blockIdx.x * kRootBlock + j * 256 + threadIdx.x;
+    if (p >= a.n_patterns) break;
+    const int64_t tile = p / kTile, q = p % kTile;
+    const double* L = a.partials + tile * ((int64_t)CS * kTile) + q;
+    double l = 0.0;
+    for (int c = 0; c < a.C; ++c) {
+      double lc = 0.0;
+      for (int s = 0; s < a.S; ++s) {
+        const double li = L[(int64_t)(c * a.S + s) * kTile] * a.pi[s];
+        if (a.guard) {
+          if (li > 0.0) lc += li;
+        } else {
+          lc += li;
+        }
+      }
+      const double li = lc * a.probs[c];
+      if (a.guard) {
+        if (li > 0.0) l += li;
+      } else {
+        l += li;
+      }
+    }
+    if (!a.guard && l < 0.0) l = 0.0;
+    double r = log(l);
+    if (a.scale) r -= (double)a.scale[p] * kLn2x256;
+    a.site_lnl[p] = r;
+    local += a.weights[p] * r;
+  }
+  red[threadIdx.x] = local;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.block_sums[blockIdx.x] = red[0];
+}
+
+}  // namespace plk

@@ -1,0 +1,225 @@
+"""ctypes binding of libplk (include/plk.h) -- the Python side of the C-ABI boundary.
+
+This is the binding a Python maintainer would add for the engine; the C++ Bio++
+host mirror (bpp-phyl_amd/host) binds the same symbols directly.  Errors become
+PlkError carrying plk_last_error().  There is no fallback: if libplk.so is missing
+or no gfx950 device is present, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libplk.so")
+
+PLK_OK = 0
+PLK_FLAG_SCALING = 1
+PLK_FLAG_NONNEG_GUARD = 2
+PLK_DERIV_P, PLK_DERIV_DP, PLK_DERIV_D2P = 1, 2, 4
+PLK_OP_ACCUMULATE = 1
+
+# every symbol include/plk.h declares
+EXPORTS = [
+    "plk_abi_version", "plk_device_count", "plk_last_error", "plk_create", "plk_destroy",
+    "plk_set_code_table", "plk_set_tip_codes", "plk_set_pattern_weights", "plk_set_category_rates",
+    "plk_set_root_frequencies", "plk_set_eigen", "plk_update_pmatrices", "plk_set_pmatrix",
+    "plk_get_pmatrix", "plk_update_partials", "plk_get_partials", "plk_root_loglik", "plk_block_size",
+    "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize",
+]
+
+
+class PlkError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"plk error {code}: {msg}")
+        self.code = code
+
+
+class plk_op(ct.Structure):
+    _fields_ = [("parent", ct.c_int32), ("n_children", ct.c_int32), ("child", ct.c_int32 * 3),
+                ("flags", ct.c_int32)]
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ct.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built (run make -C bpp-phyl_amd); libplk has no CPU fallback")
+    lib = ct.CDLL(path)
+    P = ct.POINTER
+    dp, ip = P(ct.c_double), P(ct.c_int32)
+    sig = {
+        "plk_abi_version": ([], ct.c_int),
+        "plk_device_count": ([P(ct.c_int)], ct.c_int),
+        "plk_last_error": ([ct.c_void_p], ct.c_char_p),
+        "plk_create": ([ct.c_int, ct.c_int, ct.c_int, ct.c_int64, ct.c_int, ct.c_int, ct.c_int, ct.c_uint,
+                        P(ct.c_void_p)], ct.c_int),
+        "plk_destroy": ([ct.c_void_p], ct.c_int),
+        "plk_set_code_table": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
+        "plk_set_tip_codes": ([ct.c_void_p, ct.c_int, P(ct.c_uint8)], ct.c_int),
+        "plk_set_pattern_weights": ([ct.c_void_p, dp], ct.c_int),
+        "plk_set_category_rates": ([ct.c_void_p, dp, dp], ct.c_int),
+        "plk_set_root_frequencies": ([ct.c_void_p, dp], ct.c_int),
+        "plk_set_eigen": ([ct.c_void_p, ct.c_int, dp, dp, dp], ct.c_int),
+        "plk_update_pmatrices": ([ct.c_void_p, ct.c_int, ip, ip, dp, ct.c_uint], ct.c_int),
+        "plk_set_pmatrix": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
+        "plk_get_pmatrix": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
+        "plk_update_partials": ([ct.c_void_p, P(plk_op), ct.c_int], ct.c_int),
+        "plk_get_partials": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
+        "plk_root_loglik": ([ct.c_void_p, ct.c_int, dp, dp, dp], ct.c_int),
+        "plk_block_size": ([], ct.c_int),
+        "plk_set_timing": ([ct.c_void_p, ct.c_int], ct.c_int),
+        "plk_get_timing": ([ct.c_void_p, P(ct.c_int64), dp, dp, dp], ct.c_int),
+        "plk_reset_timing": ([ct.c_void_p], ct.c_int),
+        "plk_synchronize": ([ct.c_void_p], ct.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = lib
+    return lib
+
+
+def _d(a: np.ndarray):
+    return a.ctypes.data_as(ct.POINTER(ct.c_double))
+
+
+def device_count() -> int:
+    lib = load()
+    n = ct.c_int(0)
+    lib.plk_device_count(ct.byref(n))
+    return n.value
+
+
+def make_ops(ops: Sequence[Tuple[int, Sequence[int], int]]):
+    arr = (plk_op * len(ops))()
+    for i, (p, ch, fl) in enumerate(ops):
+        arr[i].parent = p
+        arr[i].n_children = len(ch)
+        for k, c in enumerate(ch):
+            arr[i].child[k] = c
+        arr[i].flags = fl
+    return arr
+
+
+class Engine:
+    """One libplk handle (one device, one pattern shard)."""
+
+    def __init__(self, device: int, n_states: int, n_classes: int, n_patterns: int, n_tips: int,
+                 n_internal: int, n_models: int = 1, flags: int = PLK_FLAG_NONNEG_GUARD):
+        self.lib = load()
+        self.h = ct.c_void_p()
+        self.S, self.C, self.P = n_states, n_classes, n_patterns
+        self.n_tips, self.n_internal = n_tips, n_internal
+        self._ops_cache = None
+        rc = self.lib.plk_create(device, n_states, n_classes, n_patterns, n_tips, n_internal, n_models, flags,
+                                 ct.byref(self.h))
+        if rc != PLK_OK:
+            raise PlkError(rc, self.lib.plk_last_error(None).decode())
+
+    def _chk(self, rc: int):
+        if rc != PLK_OK:
+            raise PlkError(rc, self.lib.plk_last_error(self.h).decode())
+
+    def close(self):
+        if self.h:
+            self.lib.plk_destroy(self.h)
+            self.h = ct.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_code_table(self, table: np.ndarray):
+        t = np.ascontiguousarray(table, dtype=np.float64)
+        self._chk(self.lib.plk_set_code_table(self.h, t.shape[0], _d(t)))
+
+    def set_tip_codes(self, tip: int, codes: np.ndarray):
+        c = np.ascontiguousarray(codes, dtype=np.uint8)
+        self._chk(self.lib.plk_set_tip_codes(self.h, tip, c.ctypes.data_as(ct.POINTER(ct.c_uint8))))
+
+    def set_pattern_weights(self, w: np.ndarray):
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        self._chk(self.lib.plk_set_pattern_weights(self.h, _d(w)))
+
+    def set_category_rates(self, rates: np.ndarray, probs: np.ndarray):
+        r = np.ascontiguousarray(rates, dtype=np.float64)
+        p = np.ascontiguousarray(probs, dtype=np.float64)
+        self._chk(self.lib.plk_set_category_rates(self.h, _d(r), _d(p)))
+
+    def set_root_frequencies(self, pi: np.ndarray):
+        p = np.ascontiguousarray(pi, dtype=np.float64)
+        self._chk(self.lib.plk_set_root_frequencies(self.h, _d(p)))
+
+    def set_eigen(self, model: int, V: np.ndarray, Vinv: np.ndarray, lam: np.ndarray):
+        V = np.ascontiguousarray(V, dtype=np.float64)
+        Vi = np.ascontiguousarray(Vinv, dtype=np.float64)
+        la = np.ascontiguousarray(lam, dtype=np.float64)
+        self._chk(self.lib.plk_set_eigen(self.h, model, _d(V), _d(Vi), _d(la)))
+
+    def update_pmatrices(self, branches: np.ndarray, t: np.ndarray, models: Optional[np.ndarray] = None,
+                         deriv_mask: int = PLK_DERIV_P):
+        b = np.ascontiguousarray(branches, dtype=np.int32)
+        tt = np.ascontiguousarray(t, dtype=np.float64)
+        mp = None
+        if models is not None:
+            m = np.ascontiguousarray(models, dtype=np.int32)
+            mp = m.ctypes.data_as(ct.POINTER(ct.c_int32))
+        self._chk(self.lib.plk_update_pmatrices(self.h, len(b), b.ctypes.data_as(ct.POINTER(ct.c_int32)), mp,
+                                                _d(tt), deriv_mask))
+
+    def set_pmatrix(self, branch: int, P: np.ndarray):
+        p = np.ascontiguousarray(P, dtype=np.float64)
+        assert p.size == self.C * self.S * self.S
+        self._chk(self.lib.plk_set_pmatrix(self.h, branch, _d(p)))
+
+    def get_pmatrix(self, branch: int) -> np.ndarray:
+        out = np.empty((self.C, self.S, self.S))
+        self._chk(self.lib.plk_get_pmatrix(self.h, branch, _d(out)))
+        return out
+
+    def update_partials(self, ops: Sequence[Tuple[int, Sequence[int], int]]):
+        key = tuple((p, tuple(c), f) for p, c, f in ops)
+        if self._ops_cache is None or self._ops_cache[0] != key:
+            self._ops_cache = (key, make_ops(ops))
+        arr = self._ops_cache[1]
+        self._chk(self.lib.plk_update_partials(self.h, arr, len(arr)))
+
+    def get_partials(self, node: int) -> np.ndarray:
+        out = np.empty((self.P, self.C, self.S))
+        self._chk(self.lib.plk_get_partials(self.h, node, _d(out)))
+        return out
+
+    def root_loglik(self, root: int, want_sites: bool = False, want_blocks: bool = False):
+        lnl = ct.c_double(0.0)
+        sites = np.empty(self.P) if want_sites else None
+        nb = (self.P + self.lib.plk_block_size() - 1) // self.lib.plk_block_size()
+        blocks = np.empty(nb) if want_blocks else None
+        self._chk(self.lib.plk_root_loglik(self.h, root, ct.byref(lnl), _d(sites) if want_sites else None,
+                                           _d(blocks) if want_blocks else None))
+        return lnl.value, sites, blocks
+
+    def set_timing(self, on: bool):
+        self._chk(self.lib.plk_set_timing(self.h, 1 if on else 0))
+
+    def get_timing(self):
+        n = ct.c_int64(0)
+        a, b, c = ct.c_double(0), ct.c_double(0), ct.c_double(0)
+        self._chk(self.lib.plk_get_timing(self.h, ct.byref(n), ct.byref(a), ct.byref(b), ct.byref(c)))
+        return {"launches": n.value, "partials_ms": a.value, "pmat_ms": b.value, "root_ms": c.value}
+
+    def reset_timing(self):
+        self._chk(self.lib.plk_reset_timing(self.h))
+
+    def synchronize(self):
+        self._chk(self.lib.plk_synchronize(self.h))

@@ -1,0 +1,151 @@
+/* plk.h -- C-ABI of libplk, the MI355X (gfx950) Felsenstein-pruning engine.
+ *
+ * This is the drop-in boundary under the Bio++ likelihood classes.  The
+ * reference (bpp-phyl) has no FFI: its hot path is a set of C++ virtuals, and
+ * each entry point below replaces one of them (paths relative to
+ * /root/reference/src/Bpp/Phyl/):
+ *
+ *   plk_set_tip_codes / plk_set_code_table
+ *       DRASRTreeLikelihoodData::initLikelihoods leaf init
+ *       (Likelihood/DRASRTreeLikelihoodData.cpp:160-191) with
+ *       AbstractTransitionModel::getInitValue (Model/AbstractSubstitutionModel.cpp:98-112)
+ *   plk_set_pattern_weights
+ *       rootWeights_ (Likelihood/AbstractTreeLikelihoodData.h:91)
+ *   plk_set_eigen
+ *       SubstitutionModel::getEigenValues / getColumnRightEigenVectors /
+ *       getRowLeftEigenVectors (Model/SubstitutionModel.h:498-525)
+ *   plk_update_pmatrices
+ *       AbstractHomogeneousTreeLikelihood::computeTransitionProbabilitiesForNode
+ *       (Likelihood/AbstractHomogeneousTreeLikelihood.cpp:354-414) and
+ *       AbstractSubstitutionModel::getPij_t / getdPij_dt / getd2Pij_dt2
+ *       (Model/AbstractSubstitutionModel.cpp:426-641); NH twin
+ *       Likelihood/AbstractNonHomogeneousTreeLikelihood.cpp:407-470
+ *   plk_set_pmatrix
+ *       closed-form getPij_t models computed on the host (T92::getPij_t,
+ *       Model/Nucleotide/T92.cpp:355-386) copied into pxy_
+ *   plk_update_partials
+ *       RHomogeneousTreeLikelihood::computeSubtreeLikelihood
+ *       (Likelihood/RHomogeneousTreeLikelihood.cpp:802-863); NH twin
+ *       Likelihood/RNonHomogeneousTreeLikelihood.cpp:1286-1350
+ *   plk_root_loglik
+ *       RHomogeneousTreeLikelihood::getLogLikelihood / getLogLikelihoodForASite /
+ *       getLikelihoodForASiteForARateClass (Likelihood/RHomogeneousTreeLikelihood.cpp:162-216);
+ *       NH Likelihood/RNonHomogeneousTreeLikelihood.cpp:168-233
+ *
+ * Conventions
+ *   - Node indices: tips are [0, n_tips), internal nodes [n_tips, n_tips + n_internal).
+ *     The transition matrix of a branch is indexed by its CHILD node index.
+ *   - Matrices are row-major fp64; P[c][x][y] = Prob(y at child | x at parent).
+ *   - Host buffers are borrowed for the duration of the call only; device buffers
+ *     are owned by the handle.  One handle per host thread.  All work is ordered
+ *     on the handle's HIP stream; plk_root_loglik and plk_get_* synchronise.
+ *   - Every function returns PLK_OK (0) or a negative PLK_ERR_* code; the
+ *     message of the last error is available from plk_last_error().  No C++
+ *     exception crosses this boundary.
+ *   - There is no CPU fallback: plk_create fails with PLK_ERR_DEVICE when no
+ *     gfx950 device is usable.
+ */
+#ifndef PLK_H
+#define PLK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PLK_ABI_VERSION 1
+
+enum {
+  PLK_OK = 0,
+  PLK_ERR_ARG = -1,         /* bad argument (index out of range, null pointer, size) */
+  PLK_ERR_DEVICE = -2,      /* HIP runtime / device error or no usable GPU */
+  PLK_ERR_OOM = -3,         /* device allocation failed */
+  PLK_ERR_UNSUPPORTED = -4, /* state count / class count / flag not supported */
+  PLK_ERR_STATE = -5,       /* call order violated (e.g. partials before P matrices) */
+  PLK_ERR_BAD_CODE = -6     /* tip code outside the code table (BadIntException) */
+};
+
+/* plk_create flags */
+enum {
+  PLK_FLAG_SCALING = 1u << 0,    /* exact power-of-two per-pattern rescaling (deviation,
+                                    needed where the reference underflows) */
+  PLK_FLAG_NONNEG_GUARD = 1u << 1 /* homogeneous root guards: drop terms <= 0
+                                    (RHomogeneousTreeLikelihood.cpp:197-198,212-213);
+                                    without it the NH rule clamps l<0 -> 0
+                                    (RNonHomogeneousTreeLikelihood.cpp:206) */
+};
+
+/* plk_update_pmatrices deriv_mask */
+enum { PLK_DERIV_P = 1u, PLK_DERIV_DP = 2u, PLK_DERIV_D2P = 4u };
+
+/* plk_op flags */
+enum { PLK_OP_ACCUMULATE = 1 /* multiply into the parent's existing partial (polytomies) */ };
+
+/* One partial update: parent = prod_k (P_branch(child_k) . L_child_k).
+ * Ops handed to one plk_update_partials call must be in postorder; the engine
+ * batches consecutive independent ops into one launch. */
+typedef struct plk_op {
+  int32_t parent;
+  int32_t n_children; /* 1..3 */
+  int32_t child[3];
+  int32_t flags;
+} plk_op;
+
+typedef struct plk_handle_s* plk_handle;
+
+/* Library / device */
+int plk_abi_version(void);
+int plk_device_count(int* count);
+const char* plk_last_error(plk_handle h); /* h may be NULL: last global error */
+
+/* Create an engine instance on HIP device `device`.
+ *   n_states: 2..64, n_classes: 1..16, n_patterns >= 1 (padded internally),
+ *   n_models: number of eigen systems (1 for homogeneous; one per branch for NH). */
+int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int n_tips, int n_internal,
+               int n_models, unsigned flags, plk_handle* out);
+int plk_destroy(plk_handle h);
+
+/* Data */
+int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec /* n_codes x S */);
+int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes /* n_patterns */);
+int plk_set_pattern_weights(plk_handle h, const double* weights /* n_patterns */);
+int plk_set_category_rates(plk_handle h, const double* rates /* C */, const double* probs /* C */);
+int plk_set_root_frequencies(plk_handle h, const double* pi /* S */);
+
+/* Models and transition matrices */
+int plk_set_eigen(plk_handle h, int model, const double* V /* S x S */, const double* Vinv /* S x S */,
+                  const double* lambda /* S */);
+/* For each i < n: branch[i] (a child node index) gets P = V_m exp(lambda_m * r_c * t_i) Vinv_m
+ * for every class c, with m = model[i] (model may be NULL: model 0).  Optional
+ * first/second derivatives follow the reference: dP = r_c dP/dt, d2P = r_c^2 d2P/dt2. */
+int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32_t* model,
+                         const double* t, unsigned deriv_mask);
+int plk_set_pmatrix(plk_handle h, int branch, const double* P /* C x S x S */);
+int plk_get_pmatrix(plk_handle h, int branch, double* P /* C x S x S */);
+
+/* Partials */
+int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops);
+int plk_get_partials(plk_handle h, int node, double* out /* n_patterns x C x S, reference order */);
+
+/* Root reduction.  lnl = sum_p w_p log(sum_c prob_c sum_s pi_s L_root[p][c][s]).
+ * site_lnl (nullable) receives the per-pattern log-likelihoods (n_patterns).
+ * block_sums (nullable) receives the per-4096-pattern-block weighted sums in
+ * pattern order (ceil(n_patterns / 4096) values): summing them in a fixed order
+ * gives a result independent of how patterns are sharded across devices. */
+int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums);
+int plk_block_size(void);
+
+/* Instrumentation: HIP-event timing of the partial-update kernels on the
+ * handle's stream (enabled by plk_set_timing(h, 1)). */
+int plk_set_timing(plk_handle h, int enable);
+int plk_get_timing(plk_handle h, int64_t* n_launches, double* partials_ms, double* pmat_ms, double* root_ms);
+int plk_reset_timing(plk_handle h);
+int plk_synchronize(plk_handle h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PLK_H */

@@ -1,0 +1,348 @@
+"""GPU parity tests (run on the MI355X box): libplk through its C-ABI vs the CPU oracle
+and the committed golden fixtures.
+
+Tolerances (north_star: |dlnL|/|lnL| < 1e-10):
+  - total lnL: relative 1e-12 against the oracle on identical inputs,
+  - per-pattern lnL: relative 1e-12,
+  - transition matrices vs scipy expm fixtures: absolute 1e-13,
+  - sharded vs whole evaluation: bitwise equal (fixed-order block sums).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import phylo
+import plk
+import workload
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+REL = 1e-12
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if plk.device_count() < 1:
+        pytest.fail("no GPU visible: gpu-marked tests must run on the MI355X box")
+
+
+def engine_for(et, S, C, n_patterns, states, init_table, rates, probs, pi, models, model_of_node=None,
+               flags=plk.PLK_FLAG_NONNEG_GUARD):
+    eng = plk.Engine(0, S, C, n_patterns, et.n_tips, et.n_internal, len(models), flags)
+    eng.set_code_table(init_table)
+    for i in range(et.n_tips):
+        eng.set_tip_codes(i, states[i].astype(np.uint8))
+    eng.set_category_rates(rates, probs)
+    eng.set_root_frequencies(pi)
+    for k, m in enumerate(models):
+        eng.set_eigen(k, m.V, m.Vinv, m.lam)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    mi = None if model_of_node is None else np.asarray(model_of_node)[br].astype(np.int32)
+    eng.update_pmatrices(br, et.brlen[br], mi)
+    return eng
+
+
+def run_engine(eng, et, sites=True):
+    eng.update_partials(phylo.split_ops(et.ops))
+    return eng.root_loglik(et.root, want_sites=sites, want_blocks=True)
+
+
+def oracle_for(et, states, init_table, rates, probs, pi, models, model_of_node=None, scaling=False,
+               pmats=None):
+    C = len(rates)
+    S = init_table.shape[1]
+    if pmats is None:
+        pmats = np.zeros((et.n_nodes, C, S, S))
+        for n in range(et.n_nodes):
+            if n == et.root:
+                continue
+            m = models[0] if model_of_node is None else models[model_of_node[n]]
+            for c in range(C):
+                pmats[n, c] = oracle.reversible_pij(m.Q, m.pi, et.brlen[n] * rates[c])
+    ss, sons, lr = et.son_arrays()
+    lnl, site, _, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, init_table, pmats, probs, pi,
+                                         use_patterns=False, scaling=scaling, want_sites=True)
+    return lnl, site
+
+
+def check(lnl_g, site_g, lnl_o, site_o, rel=REL):
+    assert np.all(np.isfinite(site_g))
+    assert abs(lnl_g - lnl_o) <= rel * abs(lnl_o), (lnl_g, lnl_o)
+    assert np.allclose(site_g, site_o, rtol=rel, atol=0)
+
+
+# ---------------------------------------------------------------- transition matrices (K4)
+
+@pytest.mark.parametrize("name", ["T92", "GTR", "LG08"])
+def test_pmatrix_kernel_vs_expm(name):
+    f = np.load(os.path.join(GOLD, "pmatrix.npz"))
+    m = {"T92": phylo.t92(3.0, 0.5), "GTR": phylo.gtr(a=1.2, b=0.4, c=0.6, d=0.8, e=0.5, piA=0.30, piC=0.20,
+                                                          piG=0.25, piT=0.25), "LG08": phylo.lg08()}[name]
+    ts = f[f"{name}_t"]
+    et = phylo.engine_tree(phylo.balanced_tree(8))
+    eng = plk.Engine(0, m.S, 1, 256, et.n_tips, et.n_internal, 1)
+    eng.set_category_rates(np.ones(1), np.ones(1))
+    eng.set_eigen(0, m.V, m.Vinv, m.lam)
+    br = np.arange(len(ts), dtype=np.int32)
+    eng.update_pmatrices(br, ts)
+    for i, P in enumerate(f[f"{name}_P"]):
+        assert np.allclose(eng.get_pmatrix(i)[0], P, atol=1e-13)
+
+
+def test_pmatrix_derivatives():
+    m = phylo.gtr(a=1.2, b=0.4, c=0.6, d=0.8, e=0.5, piA=0.30, piC=0.20, piG=0.25, piT=0.25)
+    eng = plk.Engine(0, 4, 4, 256, 4, 2, 1)
+    rates, probs = phylo.gamma_rates(4, 0.5)
+    eng.set_category_rates(rates, probs)
+    eng.set_eigen(0, m.V, m.Vinv, m.lam)
+    eng.update_pmatrices(np.array([0, 1], dtype=np.int32), np.array([0.1, 0.7]),
+                         deriv_mask=plk.PLK_DERIV_P | plk.PLK_DERIV_DP | plk.PLK_DERIV_D2P)
+    P = eng.get_pmatrix(1)
+    for c, r in enumerate(rates):
+        assert np.allclose(P[c], m.pij(0.7 * r), atol=1e-14)
+
+
+# ---------------------------------------------------------------- reference goldens through the engine
+
+def _ref_case(key):
+    with open(os.path.join(GOLD, "reference.json")) as f:
+        case = json.load(f)[key]
+    et = phylo.engine_tree(phylo.Tree.from_newick(case["newick"]), unroot=case["unroot"])
+    states = np.stack([phylo.DNA.encode(case["sequences"][n]) for n in et.tip_names])
+    m = phylo.t92(case["model"]["kappa"], case["model"]["theta"])
+    if case["rates"]["name"] == "Gamma":
+        rates, probs = phylo.gamma_rates(case["rates"]["n"], case["rates"]["alpha"])
+    else:
+        rates, probs = np.ones(1), np.ones(1)
+    return case, et, states, m, rates, probs
+
+
+@pytest.mark.parametrize("key,golden,tol", [("test_likelihood", 85.030942031997312824, 1e-9),
+                                             ("test_likelihood_clock", 94.3957, 5e-5),
+                                             ("example1", 43.259398988513, 1e-9)])
+def test_reference_goldens(key, golden, tol):
+    case, et, states, m, rates, probs = _ref_case(key)
+    eng = engine_for(et, 4, len(rates), states.shape[1], states, phylo.DNA.init_table, rates, probs, m.pi, [m])
+    lnl, site, _ = run_engine(eng, et)
+    assert abs(-lnl - golden) < tol
+    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m])
+    check(lnl, site, lo, so)
+
+
+def test_closed_form_pmatrix_path():
+    """T92 P(t) computed on the host in closed form and handed over with plk_set_pmatrix."""
+    case, et, states, m, rates, probs = _ref_case("test_likelihood")
+    C = len(rates)
+    eng = plk.Engine(0, 4, C, states.shape[1], et.n_tips, et.n_internal, 1, plk.PLK_FLAG_NONNEG_GUARD)
+    eng.set_code_table(phylo.DNA.init_table)
+    for i in range(et.n_tips):
+        eng.set_tip_codes(i, states[i].astype(np.uint8))
+    eng.set_category_rates(rates, probs)
+    eng.set_root_frequencies(m.pi)
+    pm = np.zeros((et.n_nodes, C, 4, 4))
+    for n in range(et.n_nodes):
+        if n != et.root:
+            pm[n] = np.stack([oracle.t92_pij(3.0, 0.5, et.brlen[n] * r) for r in rates])
+            eng.set_pmatrix(n, pm[n])
+    lnl, site, _ = run_engine(eng, et)
+    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m], pmats=pm)
+    check(lnl, site, lo, so)
+    assert abs(-lnl - 85.030942031997312824) < 1e-9
+
+
+# ---------------------------------------------------------------- committed pruning fixtures
+
+@pytest.mark.parametrize("name,alph", [("T92", phylo.DNA), ("GTR", phylo.DNA), ("GTRamb", phylo.DNA),
+                                        ("LG08", phylo.PROTEIN)])
+def test_pruning_fixtures(name, alph):
+    f = np.load(os.path.join(GOLD, "pruning.npz"))
+    g = {k[len(name) + 1:]: f[k] for k in f.files if k.startswith(name + "_")}
+    # rebuild the engine tree from the fixture arrays
+    n_nodes = len(g["leaf_row"])
+    n_tips = int((g["leaf_row"] >= 0).sum())
+    ops = [(p, tuple(int(x) for x in g["sons"][g["son_start"][p]:g["son_start"][p + 1]]))
+           for p in range(n_tips, n_nodes)]
+    et = phylo.EngineTree(n_tips, n_nodes - n_tips, int(g["root"]), [], ops, g["brlen"], {}, [], [])
+    Q, pi = g["Q"], g["pi"]
+    V, Vinv, lam = phylo.reversible_eigen(Q, pi)
+    m = phylo.Model(name, Q.shape[0], Q, pi, V, Vinv, lam)
+    eng = engine_for(et, m.S, len(g["rates"]), g["states"].shape[1], g["states"], alph.init_table, g["rates"],
+                     g["probs"], pi, [m])
+    lnl, site, _ = run_engine(eng, et)
+    assert np.allclose(site, g["site_lnl"], rtol=REL, atol=0)
+    assert abs(lnl - float(g["lnl"])) <= REL * abs(lnl)
+
+
+# ---------------------------------------------------------------- seeded random problems vs the oracle
+
+def _random_problem(S, C, n_taxa, n_patterns, seed, alpha=0.5, amb=False, lo=0.01, hi=0.3):
+    rng = np.random.default_rng(seed)
+    tree = phylo.balanced_tree(n_taxa, seed=seed, lo=lo, hi=hi)
+    et = phylo.engine_tree(tree)
+    if S == 4:
+        m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
+        alph = phylo.DNA
+    elif S == 20:
+        m = phylo.lg08()
+        alph = phylo.PROTEIN
+    else:
+        E = rng.uniform(0.1, 2.0, (S, S))
+        E = E + E.T
+        pi = rng.dirichlet(np.ones(S) * 5)
+        Q = phylo.reversible_generator(E, pi)
+        V, Vinv, lam = phylo.reversible_eigen(Q, pi)
+        m = phylo.Model("rand", S, Q, pi, V, Vinv, lam)
+        alph = phylo.CODON if S == 64 else phylo.Alphabet("R", S, {}, np.eye(S))
+    rates, probs = phylo.gamma_rates(C, alpha)
+    wl = workload.Workload("r", et, [m], None, rates, probs, m.pi, alph, n_patterns, False, True, seed)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    if amb:
+        mask = rng.random(states.shape) < 0.15
+        states[mask] = rng.integers(S, alph.n_codes, size=mask.sum())
+    return et, m, alph, rates, probs, states
+
+
+@pytest.mark.parametrize("S,C,n_taxa,n_patterns", [
+    (4, 4, 16, 5000), (4, 1, 9, 1000), (4, 2, 12, 777), (4, 8, 10, 300), (4, 4, 3, 1), (4, 4, 33, 129),
+    (20, 4, 12, 600), (20, 1, 7, 250), (64, 1, 8, 300), (64, 1, 5, 130)])
+def test_random_vs_oracle(S, C, n_taxa, n_patterns):
+    et, m, alph, rates, probs, states = _random_problem(S, C, n_taxa, n_patterns, seed=S * 1000 + C * 10 + n_taxa)
+    eng = engine_for(et, S, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m])
+    lnl, site, _ = run_engine(eng, et)
+    lo, so = oracle_for(et, states, alph.init_table, rates, probs, m.pi, [m])
+    check(lnl, site, lo, so)
+
+
+def test_ambiguity_codes_vs_oracle():
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 20, 3000, seed=5, amb=True)
+    eng = engine_for(et, 4, 4, 3000, states, alph.init_table, rates, probs, m.pi, [m])
+    lnl, site, _ = run_engine(eng, et)
+    lo, so = oracle_for(et, states, alph.init_table, rates, probs, m.pi, [m])
+    check(lnl, site, lo, so)
+
+
+def test_polytomy_accumulate_vs_oracle():
+    t = phylo.Tree.from_newick("((a:0.1,b:0.2,c:0.05,d:0.3,e:0.12):0.1,(f:0.2,g:0.1):0.05,h:0.3,i:0.2);")
+    et = phylo.engine_tree(t)
+    m = phylo.gtr(1.2, 0.4, 0.6, 0.8, 0.5, 0.3, 0.2, 0.25, 0.25)
+    rates, probs = phylo.gamma_rates(4, 0.5)
+    wl = workload.Workload("p", et, [m], None, rates, probs, m.pi, phylo.DNA, 1000, False, True, 9)
+    states = wl.simulate(0, 1000).astype(np.int32)
+    assert any(len(ch) > 3 for _, ch in et.ops)
+    eng = engine_for(et, 4, 4, 1000, states, phylo.DNA.init_table, rates, probs, m.pi, [m])
+    lnl, site, _ = run_engine(eng, et)
+    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m])
+    check(lnl, site, lo, so)
+
+
+@pytest.mark.parametrize("S", [4, 20])
+def test_scaling_vs_oracle_deep_tree(S):
+    """Trees where the unscaled reference underflows: both sides use exact 2^256 rescaling."""
+    et, m, alph, rates, probs, states = _random_problem(S, 4, 256, 700, seed=11 + S, lo=0.2, hi=0.5)
+    eng = engine_for(et, S, 4, 700, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_SCALING | plk.PLK_FLAG_NONNEG_GUARD)
+    lnl, site, _ = run_engine(eng, et)
+    lo, so = oracle_for(et, states, alph.init_table, rates, probs, m.pi, [m], scaling=True)
+    check(lnl, site, lo, so)
+    assert lnl < -745 * 10  # deep enough that the scaling matters
+
+
+def test_nonhomogeneous_vs_oracle():
+    wl = workload.make_workload("nh_gtr_g4_dna_2M_512", n_patterns=2000)
+    et = wl.et
+    # shrink: keep the tree but only 2000 patterns; oracle at 512 taxa is still fast
+    states = wl.simulate(0, 2000).astype(np.int32)
+    eng = engine_for(et, 4, 4, 2000, states, phylo.DNA.init_table, wl.rates, wl.probs, wl.root_freqs, wl.models,
+                     model_of_node=wl.model_of_node, flags=plk.PLK_FLAG_SCALING)
+    lnl, site, _ = run_engine(eng, et)
+    lo, so = oracle_for(et, states, phylo.DNA.init_table, wl.rates, wl.probs, wl.root_freqs, wl.models,
+                        model_of_node=wl.model_of_node, scaling=True)
+    check(lnl, site, lo, so)
+
+
+# ---------------------------------------------------------------- sharding / determinism
+
+def test_sharded_block_sums_bitwise():
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 24, 3 * 4096 + 1000, seed=21)
+    P = states.shape[1]
+    eng = engine_for(et, 4, 4, P, states, alph.init_table, rates, probs, m.pi, [m])
+    lnl, _, blocks = run_engine(eng, et, sites=False)
+    cut = 2 * 4096
+    e1 = engine_for(et, 4, 4, cut, states[:, :cut], alph.init_table, rates, probs, m.pi, [m])
+    e2 = engine_for(et, 4, 4, P - cut, states[:, cut:], alph.init_table, rates, probs, m.pi, [m])
+    _, _, b1 = run_engine(e1, et, sites=False)
+    _, _, b2 = run_engine(e2, et, sites=False)
+    allb = np.concatenate([b1, b2])
+    assert np.array_equal(allb, blocks)
+    s = 0.0
+    for v in allb:
+        s += v
+    assert s == lnl
+
+
+def test_repeat_evaluation_bitwise():
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 32, 10000, seed=4)
+    eng = engine_for(et, 4, 4, 10000, states, alph.init_table, rates, probs, m.pi, [m])
+    a = run_engine(eng, et)
+    b = run_engine(eng, et)
+    assert a[0] == b[0] and np.array_equal(a[1], b[1])
+
+
+def test_get_partials_matches_recomputation():
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 6, 300, seed=8)
+    eng = engine_for(et, 4, 4, 300, states, alph.init_table, rates, probs, m.pi, [m])
+    run_engine(eng, et)
+    # first op's partial = product over its children of P . L
+    p, ch = et.ops[0]
+    L = eng.get_partials(p)
+    acc = np.ones((300, 4, 4))
+    for c in ch:
+        P = eng.get_pmatrix(c)
+        Lc = alph.init_table[states[c]][:, None, :] if c < et.n_tips else eng.get_partials(c)
+        acc *= np.einsum("cxy,icy->icx", P, np.broadcast_to(Lc, (300, 4, 4)))
+    assert np.allclose(L, acc, rtol=1e-13, atol=0)
+
+
+# ---------------------------------------------------------------- errors (reference exception behaviour)
+
+def test_errors():
+    eng = plk.Engine(0, 4, 4, 100, 4, 2, 1)
+    eng.set_code_table(phylo.DNA.init_table)
+    with pytest.raises(plk.PlkError) as ei:
+        eng.set_tip_codes(0, np.full(100, 200, dtype=np.uint8))
+    assert ei.value.code == -6          # BadIntException analogue
+    with pytest.raises(plk.PlkError) as ei:
+        eng.update_partials([(4, (0, 1), 0)])
+    assert ei.value.code == -5          # P matrices not set yet
+    with pytest.raises(plk.PlkError) as ei:
+        eng.update_partials([(1, (0, 2), 0)])
+    assert ei.value.code == -1          # parent is a tip
+
+
+# ---------------------------------------------------------------- full-size config 2 (properties)
+
+@pytest.mark.slow
+def test_config2_full_size_properties():
+    """BASELINE config 2 at full size (1M patterns, 64 taxa): oracle on a 20k-pattern
+    prefix (patterns are independent), bitwise shard invariance and determinism."""
+    wl = workload.make_workload("gtr_g4_dna_1M_64")
+    ev = workload.Evaluator(wl, 0, 0, wl.n_patterns)
+    lnl, _, blocks = ev.step()
+    lnl2, _, _ = ev.step()
+    assert np.isfinite(lnl) and lnl == lnl2
+    _, sites, _ = ev.eng.root_loglik(wl.et.root, want_sites=True)
+    n = 20000
+    states = wl.simulate(0, n).astype(np.int32)
+    lo, so = oracle_for(wl.et, states, phylo.DNA.init_table, wl.rates, wl.probs, wl.root_freqs, wl.models)
+    assert np.allclose(sites[:n], so, rtol=REL, atol=0)
+    # 2-way shard at a block boundary
+    cut = 61 * 4096
+    e1 = workload.Evaluator(wl, 0, 0, cut)
+    b1 = e1.step()[2]
+    del e1
+    e2 = workload.Evaluator(wl, 0, cut, wl.n_patterns)
+    b2 = e2.step()[2]
+    assert np.array_equal(np.concatenate([b1, b2]), blocks)
