@@ -33,6 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "bpp-phyl_amd"))
 
 import phylo  # noqa: E402
 import plk  # noqa: E402
+import shard  # noqa: E402
 import workload  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
@@ -117,17 +118,8 @@ def main():
 
     def one_step():
         _, _, blocks = ev.step()
-        if dist is not None:
-            t = torch.from_numpy(blocks).cuda()
-            out = [torch.empty_like(t) for _ in range(world)]
-            dist.all_gather(out, t)
-            allb = torch.cat(out).cpu().numpy()
-        else:
-            allb = blocks
-        s = 0.0
-        for v in allb:   # global fixed order: identical for any GPU count
-            s += v
-        return s
+        # the one cross-GPU exchange: RCCL all-gather of fixed-order block sums
+        return shard.allgather_lnl(blocks, dist, device="cuda" if dist is not None else None)
 
     for _ in range(args.warmup):
         lnl = one_step()

@@ -1,0 +1,52 @@
+"""Site-pattern sharding across GPUs (one process per GPU, torch.distributed over RCCL).
+
+Patterns are independent, so each rank evaluates a contiguous pattern range with no
+data-path communication.  The single exchange of an evaluation is the final
+log-likelihood: every rank contributes its fixed-order 4096-pattern block sums
+(plk_root_loglik's block_sums), they are all-gathered and summed in global block
+order, so the total is bitwise identical for any GPU count as long as shard
+boundaries fall on block boundaries.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+
+BLOCK = 4096  # plk_block_size()
+
+
+def shard_range(rank: int, world: int, n_patterns: int, align: int = BLOCK) -> Tuple[int, int]:
+    """Strong-scaling split of [0, n_patterns) into `world` contiguous ranges whose
+    boundaries are multiples of `align` (the last range takes the remainder)."""
+    n_blocks = (n_patterns + align - 1) // align
+    per, extra = divmod(n_blocks, world)
+    b0 = rank * per + min(rank, extra)
+    b1 = b0 + per + (1 if rank < extra else 0)
+    return min(b0 * align, n_patterns), min(b1 * align, n_patterns)
+
+
+def fixed_order_sum(blocks: np.ndarray) -> float:
+    s = 0.0
+    for v in blocks:
+        s += float(v)
+    return s
+
+
+def allgather_lnl(blocks: np.ndarray, dist=None, device=None) -> float:
+    """All-gather per-rank block sums (variable counts allowed) and sum in global order."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return fixed_order_sum(blocks)
+    import torch
+
+    world = dist.get_world_size()
+    n = torch.tensor([len(blocks)], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n)
+    cmax = int(max(int(c.item()) for c in counts))
+    buf = torch.zeros(cmax, dtype=torch.float64, device=device)
+    buf[: len(blocks)] = torch.from_numpy(np.asarray(blocks, dtype=np.float64)).to(buf.device)
+    out = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf)
+    allb = np.concatenate([o[: int(c.item())].cpu().numpy() for o, c in zip(out, counts)])
+    return fixed_order_sum(allb)
