@@ -1,0 +1,224 @@
+// Parameters, constraints and parameter lists with bpp-core 2.4 semantics, as far
+// as the likelihood classes and their callers use them.
+#ifndef BPP_AMD_PARAMETER_H
+#define BPP_AMD_PARAMETER_H
+
+#include <cmath>
+#include <iostream>
+#include <limits>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../Exceptions.h"
+
+namespace bpp {
+
+class Constraint {
+ public:
+  virtual ~Constraint() {}
+  virtual Constraint* clone() const = 0;
+  virtual bool isCorrect(double value) const = 0;
+  virtual double getAcceptedLimit(double value) const = 0;
+  virtual double getLowerBound() const = 0;
+  virtual double getUpperBound() const = 0;
+  virtual bool strictLowerBound() const = 0;
+  virtual bool strictUpperBound() const = 0;
+};
+
+class IntervalConstraint : public Constraint {
+  double lower_, upper_;
+  bool inclLower_, inclUpper_;
+  double precision_;
+
+ public:
+  IntervalConstraint(double lower, double upper, bool inclLower, bool inclUpper, double precision = 1e-7)
+      : lower_(lower), upper_(upper), inclLower_(inclLower), inclUpper_(inclUpper), precision_(precision) {}
+  IntervalConstraint* clone() const override { return new IntervalConstraint(*this); }
+  bool isCorrect(double v) const override {
+    bool lo = inclLower_ ? v >= lower_ : v > lower_;
+    bool hi = inclUpper_ ? v <= upper_ : v < upper_;
+    return lo && hi;
+  }
+  double getAcceptedLimit(double v) const override {
+    if (!(inclLower_ ? v >= lower_ : v > lower_)) return inclLower_ ? lower_ : lower_ + precision_;
+    if (!(inclUpper_ ? v <= upper_ : v < upper_)) return inclUpper_ ? upper_ : upper_ - precision_;
+    return v;
+  }
+  double getLowerBound() const override { return lower_; }
+  double getUpperBound() const override { return upper_; }
+  bool strictLowerBound() const override { return !inclLower_; }
+  bool strictUpperBound() const override { return !inclUpper_; }
+};
+
+class Parameter {
+  std::string name_;
+  double value_;
+  std::shared_ptr<Constraint> constraint_;
+
+ public:
+  static const std::shared_ptr<IntervalConstraint> R_PLUS;
+  static const std::shared_ptr<IntervalConstraint> R_PLUS_STAR;
+  static const std::shared_ptr<IntervalConstraint> PROP_CONSTRAINT_IN;
+  static const std::shared_ptr<IntervalConstraint> PROP_CONSTRAINT_EX;
+
+  Parameter() : name_(), value_(0.), constraint_() {}
+  Parameter(const std::string& name, double value, std::shared_ptr<Constraint> c = nullptr)
+      : name_(name), value_(value), constraint_(c) {
+    if (constraint_ && !constraint_->isCorrect(value))
+      throw ConstraintException("Parameter::Parameter: value out of constraint", name, value);
+  }
+  const std::string& getName() const { return name_; }
+  void setName(const std::string& n) { name_ = n; }
+  double getValue() const { return value_; }
+  void setValue(double v) {
+    if (constraint_ && !constraint_->isCorrect(v))
+      throw ConstraintException("Parameter::setValue", name_, v);
+    value_ = v;
+  }
+  bool hasConstraint() const { return (bool)constraint_; }
+  std::shared_ptr<Constraint> getConstraint() const { return constraint_; }
+  void setConstraint(std::shared_ptr<Constraint> c) { constraint_ = c; }
+};
+
+class ParameterList {
+  std::vector<Parameter> params_;
+
+ public:
+  size_t size() const { return params_.size(); }
+  const Parameter& operator[](size_t i) const { return params_[i]; }
+  Parameter& operator[](size_t i) { return params_[i]; }
+  std::vector<std::string> getParameterNames() const {
+    std::vector<std::string> v;
+    for (auto& p : params_) v.push_back(p.getName());
+    return v;
+  }
+  bool hasParameter(const std::string& name) const {
+    for (auto& p : params_)
+      if (p.getName() == name) return true;
+    return false;
+  }
+  size_t whichParameterHasName(const std::string& name) const {
+    for (size_t i = 0; i < params_.size(); i++)
+      if (params_[i].getName() == name) return i;
+    throw ParameterNotFoundException("ParameterList::whichParameterHasName", name);
+  }
+  const Parameter& getParameter(const std::string& name) const { return params_[whichParameterHasName(name)]; }
+  double getParameterValue(const std::string& name) const { return getParameter(name).getValue(); }
+  void addParameter(const Parameter& p) {
+    if (hasParameter(p.getName())) throw Exception("ParameterList::addParameter: duplicate " + p.getName());
+    params_.push_back(p);
+  }
+  void addParameters(const ParameterList& pl) {
+    for (size_t i = 0; i < pl.size(); i++) addParameter(pl[i]);
+  }
+  void includeParameters(const ParameterList& pl) {
+    for (size_t i = 0; i < pl.size(); i++) {
+      if (hasParameter(pl[i].getName()))
+        params_[whichParameterHasName(pl[i].getName())].setValue(pl[i].getValue());
+      else
+        params_.push_back(pl[i]);
+    }
+  }
+  void setParameterValue(const std::string& name, double v) { params_[whichParameterHasName(name)].setValue(v); }
+  // Update values of parameters present in both lists; returns true if any changed.
+  bool matchParametersValues(const ParameterList& pl, std::vector<size_t>* changed = nullptr) {
+    bool any = false;
+    for (size_t i = 0; i < params_.size(); i++) {
+      for (size_t j = 0; j < pl.size(); j++) {
+        if (pl[j].getName() == params_[i].getName()) {
+          if (params_[i].getValue() != pl[j].getValue()) {
+            params_[i].setValue(pl[j].getValue());
+            any = true;
+            if (changed) changed->push_back(i);
+          }
+          break;
+        }
+      }
+    }
+    return any;
+  }
+  ParameterList getCommonParametersWith(const ParameterList& pl) const {
+    ParameterList out;
+    for (auto& p : params_)
+      if (pl.hasParameter(p.getName())) out.params_.push_back(p);
+    return out;
+  }
+  ParameterList createSubList(const std::vector<std::string>& names) const {
+    ParameterList out;
+    for (auto& n : names) out.params_.push_back(getParameter(n));
+    return out;
+  }
+  void deleteParameter(const std::string& name) { params_.erase(params_.begin() + whichParameterHasName(name)); }
+  void reset() { params_.clear(); }
+  void printParameters(std::ostream& out) const {
+    for (auto& p : params_) out << p.getName() << "=" << p.getValue() << std::endl;
+  }
+};
+
+// Parametrizable objects with a namespace prefix ("T92.", "GTR.", ...).
+class Parametrizable {
+ public:
+  virtual ~Parametrizable() {}
+  virtual const ParameterList& getParameters() const = 0;
+  virtual bool matchParametersValues(const ParameterList& pl) = 0;
+};
+
+class AbstractParametrizable : public virtual Parametrizable {
+ protected:
+  ParameterList parameters_;
+  std::string prefix_;
+
+ public:
+  explicit AbstractParametrizable(const std::string& prefix = "") : parameters_(), prefix_(prefix) {}
+  virtual ~AbstractParametrizable() {}
+  const ParameterList& getParameters() const override { return parameters_; }
+  virtual ParameterList getIndependentParameters() const { return parameters_; }
+  const std::string& getNamespace() const { return prefix_; }
+  virtual void setNamespace(const std::string& prefix) {
+    for (size_t i = 0; i < parameters_.size(); i++) {
+      std::string n = parameters_[i].getName();
+      if (n.compare(0, prefix_.size(), prefix_) == 0) n = n.substr(prefix_.size());
+      parameters_[i].setName(prefix + n);
+    }
+    prefix_ = prefix;
+  }
+  std::string getParameterNameWithoutNamespace(const std::string& name) const {
+    if (name.compare(0, prefix_.size(), prefix_) == 0) return name.substr(prefix_.size());
+    return name;
+  }
+  bool hasParameter(const std::string& name) const { return parameters_.hasParameter(prefix_ + name); }
+  const Parameter& getParameter(const std::string& name) const { return parameters_.getParameter(prefix_ + name); }
+  double getParameterValue(const std::string& name) const { return parameters_.getParameterValue(prefix_ + name); }
+  virtual void setParameterValue(const std::string& name, double v) {
+    ParameterList pl;
+    Parameter p = parameters_.getParameter(prefix_ + name);
+    p.setValue(v);
+    pl.addParameter(p);
+    matchParametersValues(pl);
+  }
+  bool matchParametersValues(const ParameterList& pl) override {
+    std::vector<size_t> changed;
+    bool any = parameters_.matchParametersValues(pl, &changed);
+    if (any) {
+      ParameterList ch;
+      for (size_t i : changed) ch.addParameter(parameters_[i]);
+      fireParameterChanged(ch);
+    }
+    return any;
+  }
+  virtual void setParametersValues(const ParameterList& pl) {
+    parameters_.matchParametersValues(pl);
+    fireParameterChanged(pl);
+  }
+  virtual void fireParameterChanged(const ParameterList&) {}
+
+ protected:
+  void addParameter_(const Parameter& p) { parameters_.addParameter(p); }
+  void addParameters_(const ParameterList& pl) { parameters_.addParameters(pl); }
+  void resetParameters_() { parameters_.reset(); }
+};
+
+}  // namespace bpp
+
+#endif

@@ -1,0 +1,177 @@
+// Likelihood classes of the host mirror: the Bio++ TreeLikelihood API surface the
+// reference's tests use (Likelihood/TreeLikelihood.h:66-442,
+// Likelihood/RHomogeneousTreeLikelihood.h:131-138, RNonHomogeneousTreeLikelihood.h),
+// implemented over libplk (include/plk.h).  The hot path
+// (computeTransitionProbabilities*, computeTreeLikelihood, getLogLikelihood) runs on
+// the GPU; the host keeps parameters, tree, patterns and the dispatch logic of
+// fireParameterChanged (Likelihood/RHomogeneousTreeLikelihood.cpp:255-283).
+#ifndef BPP_AMD_TREELIKELIHOOD_H
+#define BPP_AMD_TREELIKELIHOOD_H
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../Numeric/Prob/DiscreteDistribution.h"
+#include "../../Seq/Container/SiteContainer.h"
+#include "../Model/Models.h"
+#include "../Model/SubstitutionModelSet.h"
+#include "../TreeTemplate.h"
+
+struct plk_handle_s;
+
+namespace bpp {
+
+class TreeLikelihood : public AbstractParametrizable {
+ public:
+  virtual ~TreeLikelihood() {}
+  virtual void initialize() = 0;
+  virtual bool isInitialized() const = 0;
+  virtual double getValue() const = 0;            // -lnL
+  virtual double getLogLikelihood() const = 0;
+  virtual double getLikelihood() const = 0;
+  virtual double getLogLikelihoodForASite(size_t site) const = 0;
+  virtual double getLikelihoodForASite(size_t site) const = 0;
+  virtual size_t getNumberOfSites() const = 0;
+  virtual size_t getNumberOfStates() const = 0;
+  virtual size_t getNumberOfClasses() const = 0;
+  virtual const Tree& getTree() const = 0;
+  virtual ParameterList getBranchLengthsParameters() const = 0;
+  virtual ParameterList getSubstitutionModelParameters() const = 0;
+  virtual ParameterList getRateDistributionParameters() const = 0;
+  virtual void setParameters(const ParameterList& pl) = 0;
+  virtual double f(const ParameterList& pl) = 0;
+  virtual double getFirstOrderDerivative(const std::string& variable) const = 0;
+  virtual double getSecondOrderDerivative(const std::string& variable) const = 0;
+  virtual void enableDerivatives(bool yn) = 0;
+  virtual void enableFirstOrderDerivatives(bool yn) = 0;
+  virtual void enableSecondOrderDerivatives(bool yn) = 0;
+};
+
+// Common engine plumbing of the R-likelihoods: tree copy, node order, root site
+// patterns, the libplk handle and the postorder op list.
+class AbstractPlkTreeLikelihood : public TreeLikelihood {
+ protected:
+  TreeTemplate<Node>* tree_ = nullptr;
+  std::vector<Node*> nodes_;                 // postorder minus root (BrLen<i> = nodes_[i])
+  DiscreteDistribution* rateDistribution_;   // not owned
+  size_t nbClasses_ = 1, nbStates_ = 0;
+  // data
+  std::unique_ptr<SiteContainer> data_;
+  size_t nbSites_ = 0, nbDistinctSites_ = 0;
+  std::vector<size_t> rootPatternLinks_;     // site -> pattern
+  std::vector<unsigned int> rootWeights_;    // pattern -> number of sites
+  std::vector<std::vector<int> > patternStates_;  // [tip engine index][pattern]
+  // engine mapping: tips first, internal nodes after
+  std::map<const Node*, int> engineIndex_;
+  int nTips_ = 0, nInternal_ = 0, rootEngine_ = -1;
+  std::vector<int> opParent_, opFlags_;
+  std::vector<std::vector<int> > opChildren_;
+  plk_handle_s* engine_ = nullptr;
+  bool usePatterns_ = true;
+  bool verbose_ = true;
+  bool initialized_ = false;
+  bool scaling_ = true;
+  bool derivFirst_ = true, derivSecond_ = true;
+  double minimumBrLen_ = 0.000001, maximumBrLen_ = 10000.;
+  std::shared_ptr<IntervalConstraint> brLenConstraint_;
+  ParameterList brLenParameters_;
+  mutable double minusLogLik_ = -1.;
+  mutable std::vector<double> siteLnl_;      // per pattern (fetched lazily)
+  mutable bool siteLnlValid_ = false;
+  Vdouble rootFreqs_;
+
+  AbstractPlkTreeLikelihood(const Tree& tree, DiscreteDistribution* rDist, bool checkRooted, bool verbose,
+                            bool usePatterns);
+  AbstractPlkTreeLikelihood(const AbstractPlkTreeLikelihood&) = delete;
+  AbstractPlkTreeLikelihood& operator=(const AbstractPlkTreeLikelihood&) = delete;
+
+  void buildEngineLayout();
+  void setDataImpl(const SiteContainer& sites, const Alphabet* alphabet, const SubstitutionModel& model);
+  void createEngine(size_t nModels, bool nonNegGuard);
+  void initBranchLengthsParameters();
+  void applyBranchLengths();
+  // Upload transition matrices for the given branches (nodes) of model m(node).
+  void updatePmatrices(const std::vector<const Node*>& nodes);
+  virtual int modelIndexForNode(const Node*) const { return 0; }
+  void uploadEigen(int modelIndex, const SubstitutionModel& model);
+  void uploadRates();
+  void computeTreeLikelihood();
+  double reduceRoot() const;
+  void fetchSiteLnl() const;
+  void check(int rc, const char* what) const;
+
+ public:
+  ~AbstractPlkTreeLikelihood() override;
+  bool isInitialized() const override { return initialized_; }
+  double getValue() const override;
+  double getLogLikelihood() const override;
+  double getLikelihood() const override;
+  double getLogLikelihoodForASite(size_t site) const override;
+  double getLikelihoodForASite(size_t site) const override;
+  size_t getNumberOfSites() const override { return nbSites_; }
+  size_t getNumberOfDistinctSites() const { return nbDistinctSites_; }
+  size_t getNumberOfStates() const override { return nbStates_; }
+  size_t getNumberOfClasses() const override { return nbClasses_; }
+  const Tree& getTree() const override { return *tree_; }
+  ParameterList getBranchLengthsParameters() const override;
+  ParameterList getRateDistributionParameters() const override;
+  void setParameters(const ParameterList& pl) override;
+  double f(const ParameterList& pl) override {
+    setParameters(pl);
+    return getValue();
+  }
+  double getFirstOrderDerivative(const std::string& variable) const override;
+  double getSecondOrderDerivative(const std::string& variable) const override;
+  void enableDerivatives(bool yn) override { derivFirst_ = derivSecond_ = yn; }
+  void enableFirstOrderDerivatives(bool yn) override { derivFirst_ = yn; }
+  void enableSecondOrderDerivatives(bool yn) override { derivSecond_ = yn; }
+  const std::vector<unsigned int>& getWeights() const { return rootWeights_; }
+  size_t getRootArrayPosition(size_t site) const { return rootPatternLinks_[site]; }
+  // Exact power-of-two rescaling of partials (a deviation from the reference, which
+  // has none and underflows on large trees); bit-identical when it never triggers.
+  void setUnderflowScaling(bool yn) { scaling_ = yn; }
+  // Partial likelihoods of a node in the reference's [pattern][class][state] order.
+  VVVdouble getLikelihoodArray(int nodeId) const;
+  plk_handle_s* getEngine() const { return engine_; }
+};
+
+class RHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
+  SubstitutionModel* model_;  // not owned
+
+ public:
+  RHomogeneousTreeLikelihood(const Tree& tree, SubstitutionModel* model, DiscreteDistribution* rDist,
+                             bool checkRooted = true, bool verbose = true, bool usePatterns = true);
+  RHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data, SubstitutionModel* model,
+                             DiscreteDistribution* rDist, bool checkRooted = true, bool verbose = true,
+                             bool usePatterns = true);
+  void setData(const SiteContainer& sites);
+  void initialize() override;
+  void fireParameterChanged(const ParameterList& params) override;
+  ParameterList getSubstitutionModelParameters() const override;
+  const SubstitutionModel* getModel() const { return model_; }
+  SubstitutionModel* getModel() { return model_; }
+  void computeAllTransitionProbabilities();
+};
+
+class RNonHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
+  SubstitutionModelSet* modelSet_;  // not owned
+  std::map<int, int> modelOfNodeId_;
+
+  int modelIndexForNode(const Node* n) const override;
+
+ public:
+  RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data, SubstitutionModelSet* modelSet,
+                                DiscreteDistribution* rDist, bool verbose = true, bool usePatterns = true,
+                                bool reparametrizeRoot = false);
+  void setData(const SiteContainer& sites);
+  void initialize() override;
+  void fireParameterChanged(const ParameterList& params) override;
+  ParameterList getSubstitutionModelParameters() const override;
+  void computeAllTransitionProbabilities();
+};
+
+}  // namespace bpp
+
+#endif

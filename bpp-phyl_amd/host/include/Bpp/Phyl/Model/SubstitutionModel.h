@@ -1,0 +1,109 @@
+// Substitution models of the host mirror.  Interface after the reference's
+// SubstitutionModel (Model/SubstitutionModel.h:122-602): generator, frequencies,
+// eigen-system (getEigenValues / getRowLeftEigenVectors = V^-1 /
+// getColumnRightEigenVectors = V, :498-525), getPij_t & derivatives (:233-247),
+// getInitValue (:277).  The likelihood classes hand the eigen-system (or, for
+// closed-form models, P(t) itself) to libplk, which builds every branch's
+// transition matrices on the GPU.
+#ifndef BPP_AMD_SUBSTITUTIONMODEL_H
+#define BPP_AMD_SUBSTITUTIONMODEL_H
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../Numeric/Matrix/Matrix.h"
+#include "../../Numeric/NumConstants.h"
+#include "../../Numeric/Parameter.h"
+#include "../../Seq/Alphabet/Alphabet.h"
+
+namespace bpp {
+
+class FrequencySet;
+
+class SubstitutionModel : public AbstractParametrizable {
+ protected:
+  const Alphabet* alphabet_;
+  size_t size_;
+  double rate_ = 1.;
+  RowMatrix<double> generator_;
+  RowMatrix<double> exchangeability_;
+  Vdouble freq_;
+  Vdouble eigenValues_;
+  RowMatrix<double> leftEigenVectors_;   // V^-1 (rows)
+  RowMatrix<double> rightEigenVectors_;  // V (columns)
+  bool isDiagonalizable_ = true;
+  bool isNonSingular_ = true;
+  bool isScalable_ = true;
+  mutable RowMatrix<double> pijt_, dpijt_, d2pijt_;
+
+ public:
+  SubstitutionModel(const Alphabet* alpha, size_t size, const std::string& prefix)
+      : AbstractParametrizable(prefix), alphabet_(alpha), size_(size), generator_(size, size),
+        exchangeability_(size, size), freq_(size, 1. / size), eigenValues_(size, 0.),
+        leftEigenVectors_(size, size), rightEigenVectors_(size, size), pijt_(size, size), dpijt_(size, size),
+        d2pijt_(size, size) {}
+  virtual ~SubstitutionModel() {}
+  virtual SubstitutionModel* clone() const = 0;
+  virtual std::string getName() const = 0;
+
+  const Alphabet* getAlphabet() const { return alphabet_; }
+  size_t getNumberOfStates() const { return size_; }
+  const Vdouble& getFrequencies() const { return freq_; }
+  double freq(size_t i) const { return freq_[i]; }
+  const RowMatrix<double>& getGenerator() const { return generator_; }
+  const RowMatrix<double>& getExchangeabilityMatrix() const { return exchangeability_; }
+  const Vdouble& getEigenValues() const { return eigenValues_; }
+  const RowMatrix<double>& getRowLeftEigenVectors() const { return leftEigenVectors_; }
+  const RowMatrix<double>& getColumnRightEigenVectors() const { return rightEigenVectors_; }
+  bool isDiagonalizable() const { return isDiagonalizable_; }
+  bool isNonSingular() const { return isNonSingular_; }
+  double getRate() const { return rate_; }
+  void setRate(double r) { rate_ = r; }
+  bool isScalable() const { return isScalable_; }
+  void setScalable(bool s) { isScalable_ = s; }
+  int getAlphabetStateAsInt(size_t i) const { return (int)i; }
+
+  // Closed-form models (T92) expose P(t) directly; the likelihood then hands the
+  // host-computed matrices to the engine with plk_set_pmatrix.
+  virtual bool hasClosedFormPij() const { return false; }
+
+  // P(t) = V diag(exp(lambda rate t)) V^-1 (Model/AbstractSubstitutionModel.cpp:426-438)
+  virtual const RowMatrix<double>& getPij_t(double t) const;
+  virtual const RowMatrix<double>& getdPij_dt(double t) const;
+  virtual const RowMatrix<double>& getd2Pij_dt2(double t) const;
+
+  // Leaf init value: 1 if resolved state i is in the alias set of `state`
+  // (Model/AbstractSubstitutionModel.cpp:98-112); throws BadIntException for gaps.
+  double getInitValue(size_t i, int state) const;
+
+  // -sum_i pi_i Q_ii (:645-650) and normalisation to 1 (:686-690)
+  double getScale() const;
+  void setScale(double scale);
+  void normalize() {
+    if (isScalable_) setScale(1. / getScale());
+  }
+  void setDiagonal();
+
+  void fireParameterChanged(const ParameterList&) override { updateMatrices(); }
+  virtual void updateMatrices() = 0;
+
+ protected:
+  // Eigen-system of the current generator (reversible: symmetric form); strips
+  // null (stop) states like Model/AbstractSubstitutionModel.cpp:184-273.
+  void computeEigen();
+};
+
+typedef SubstitutionModel TransitionModel;
+
+// Q = S o pi, diagonal, normalise, eigen (Model/AbstractSubstitutionModel.cpp:694-703)
+class AbstractReversibleSubstitutionModel : public SubstitutionModel {
+ public:
+  AbstractReversibleSubstitutionModel(const Alphabet* alpha, size_t size, const std::string& prefix)
+      : SubstitutionModel(alpha, size, prefix) {}
+  void updateMatrices() override;
+};
+
+}  // namespace bpp
+
+#endif

@@ -1,0 +1,53 @@
+// Host-side optimisers driving repeated likelihood evaluations (the callers of the
+// hot path): optimizeTreeScale (OptimizationTools.cpp:119-143) and
+// optimizeNumericalParameters2 (:266-353).  Every function evaluation is one GPU
+// evaluation through fireParameterChanged.  The search is a bounded Brent line
+// search per parameter, cycled to convergence; it reaches the same optimum as the
+// reference's PseudoNewton/BFGS combination (the test goldens are optima).
+#ifndef BPP_AMD_OPTIMIZATIONTOOLS_H
+#define BPP_AMD_OPTIMIZATIONTOOLS_H
+
+#include <string>
+
+#include "Likelihood/TreeLikelihood.h"
+
+namespace bpp {
+
+class OutputStream {
+ public:
+  virtual ~OutputStream() {}
+};
+class OptimizationListener {
+ public:
+  virtual ~OptimizationListener() {}
+};
+
+struct OptimizationTools {
+  static const std::string OPTIMIZATION_NEWTON;
+  static const std::string OPTIMIZATION_GRADIENT;
+  static const std::string OPTIMIZATION_BRENT;
+  static const std::string OPTIMIZATION_BFGS;
+
+  static unsigned int optimizeTreeScale(TreeLikelihood* tl, double tolerance = 0.000001,
+                                        unsigned int tlEvalMax = 1000000, OutputStream* messageHandler = nullptr,
+                                        OutputStream* profiler = nullptr, unsigned int verbose = 1);
+
+  static unsigned int optimizeNumericalParameters2(TreeLikelihood* tl, const ParameterList& parameters,
+                                                   OptimizationListener* listener = nullptr,
+                                                   double tolerance = 0.000001, unsigned int tlEvalMax = 1000000,
+                                                   OutputStream* messageHandler = nullptr,
+                                                   OutputStream* profiler = nullptr, bool reparametrization = false,
+                                                   bool useClock = false, unsigned int verbose = 1,
+                                                   const std::string& optMethodDeriv = OPTIMIZATION_NEWTON);
+
+  // Bounded 1-D Brent minimisation of f on [a, b]; returns the argmin, *fmin the value.
+  template <class F>
+  static double brent(F f, double a, double b, double x0, double tol, unsigned int maxEval, double* fmin,
+                      unsigned int* nEval);
+};
+
+}  // namespace bpp
+
+#include "OptimizationTools.tpp"
+
+#endif

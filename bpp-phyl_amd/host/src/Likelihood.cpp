@@ -1,0 +1,491 @@
+// Host mirror: R-likelihood classes over libplk.
+//
+// What stays on the host (as in the reference): parameters and their dispatch
+// (fireParameterChanged, Likelihood/RHomogeneousTreeLikelihood.cpp:255-283), the
+// tree copy / unroot / postorder node list (Likelihood/AbstractHomogeneousTreeLikelihood.cpp:140-166),
+// root site patterns (SitePatterns.cpp:51-100), model eigen-systems.
+// What runs on the MI355X: every branch transition matrix (plk_update_pmatrices),
+// the full postorder traversal (plk_update_partials) and the root reduction
+// (plk_root_loglik).  Only one scalar comes back per evaluation.
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <unordered_map>
+
+#include "Bpp/App/ApplicationTools.h"
+#include "Bpp/Phyl/Likelihood/TreeLikelihood.h"
+#include "plk.h"
+
+namespace bpp {
+
+namespace {
+int deviceFromEnv() {
+  const char* e = std::getenv("BPP_AMD_DEVICE");
+  return e ? std::atoi(e) : 0;
+}
+}  // namespace
+
+void AbstractPlkTreeLikelihood::check(int rc, const char* what) const {
+  if (rc != PLK_OK) throw DeviceException(rc, std::string(what) + ": " + plk_last_error(engine_));
+}
+
+AbstractPlkTreeLikelihood::AbstractPlkTreeLikelihood(const Tree& tree, DiscreteDistribution* rDist, bool checkRooted,
+                                                     bool verbose, bool usePatterns)
+    : rateDistribution_(rDist), usePatterns_(usePatterns), verbose_(verbose) {
+  if (!rDist) throw NullPointerException("AbstractPlkTreeLikelihood: null rate distribution");
+  tree_ = new TreeTemplate<Node>(tree);
+  if (checkRooted && tree_->isRooted()) {
+    if (verbose) ApplicationTools::displayWarning("Tree has been unrooted.");
+    tree_->unroot();
+  }
+  nodes_ = tree_->getNodes();
+  nodes_.pop_back();  // the root is last in postorder
+  nbClasses_ = rateDistribution_->getNumberOfCategories();
+  brLenConstraint_ = std::make_shared<IntervalConstraint>(minimumBrLen_, maximumBrLen_, true, true);
+  buildEngineLayout();
+}
+
+AbstractPlkTreeLikelihood::~AbstractPlkTreeLikelihood() {
+  if (engine_) plk_destroy(engine_);
+  delete tree_;
+}
+
+void AbstractPlkTreeLikelihood::buildEngineLayout() {
+  std::vector<Node*> all = tree_->getNodes();
+  engineIndex_.clear();
+  nTips_ = nInternal_ = 0;
+  for (Node* n : all)
+    if (n->isLeaf()) engineIndex_[n] = nTips_++;
+  for (Node* n : all)
+    if (!n->isLeaf()) engineIndex_[n] = nTips_ + nInternal_++;
+  rootEngine_ = engineIndex_[tree_->getRootNode()];
+  opParent_.clear();
+  opChildren_.clear();
+  opFlags_.clear();
+  for (Node* n : all) {
+    if (n->isLeaf()) continue;
+    for (size_t k = 0; k < n->getNumberOfSons(); k += 3) {
+      std::vector<int> ch;
+      for (size_t j = k; j < std::min(k + 3, n->getNumberOfSons()); j++) ch.push_back(engineIndex_[n->getSon(j)]);
+      opParent_.push_back(engineIndex_[n]);
+      opChildren_.push_back(ch);
+      opFlags_.push_back(k == 0 ? 0 : PLK_OP_ACCUMULATE);
+    }
+  }
+}
+
+// DRASRTreeLikelihoodData::initLikelihoods (Likelihood/DRASRTreeLikelihoodData.cpp:55-90):
+// checks, root site patterns, leaf states.  The engine always evaluates the root
+// patterns; per-subtree compression (usePatterns) changes nothing in the result.
+void AbstractPlkTreeLikelihood::setDataImpl(const SiteContainer& sites, const Alphabet* alphabet,
+                                            const SubstitutionModel& model) {
+  if (sites.getNumberOfSequences() == 1) throw Exception("Error, only 1 sequence!");
+  if (sites.getNumberOfSequences() == 0) throw Exception("Error, no sequence!");
+  if (sites.getAlphabet()->getAlphabetType() != alphabet->getAlphabetType())
+    throw AlphabetMismatchException("Data and model must have the same alphabet type.");
+  std::vector<const Node*> leaves(nTips_);
+  for (auto& kv : engineIndex_)
+    if (kv.second < nTips_) leaves[kv.second] = kv.first;
+  std::vector<const Sequence*> seqs(nTips_);
+  for (int t = 0; t < nTips_; t++) {
+    if (!sites.hasSequence(leaves[t]->getName()))
+      throw SequenceNotFoundException("Leaf name in tree not found in site container", leaves[t]->getName());
+    seqs[t] = &sites.getSequence(leaves[t]->getName());
+  }
+  nbSites_ = sites.getNumberOfSites();
+  // leaf states must be allowed by the model (getInitValue throws BadIntException)
+  for (int t = 0; t < nTips_; t++)
+    for (size_t i = 0; i < nbSites_; i++) {
+      const int s = seqs[t]->getValue(i);
+      if (s < 0 || !alphabet->isIntInAlphabet(s)) model.getInitValue(0, s);
+    }
+  // root patterns (first-occurrence order; SitePatterns sorts, which only permutes them)
+  std::unordered_map<std::string, size_t> seen;
+  rootPatternLinks_.assign(nbSites_, 0);
+  rootWeights_.clear();
+  std::vector<size_t> repr;
+  std::string key(nTips_ * sizeof(int), '\0');
+  for (size_t i = 0; i < nbSites_; i++) {
+    for (int t = 0; t < nTips_; t++) {
+      const int s = seqs[t]->getValue(i);
+      std::memcpy(&key[t * sizeof(int)], &s, sizeof(int));
+    }
+    auto it = seen.find(key);
+    if (it == seen.end()) {
+      it = seen.emplace(key, rootWeights_.size()).first;
+      rootWeights_.push_back(0);
+      repr.push_back(i);
+    }
+    rootPatternLinks_[i] = it->second;
+    rootWeights_[it->second]++;
+  }
+  nbDistinctSites_ = rootWeights_.size();
+  patternStates_.assign(nTips_, std::vector<int>(nbDistinctSites_));
+  for (int t = 0; t < nTips_; t++)
+    for (size_t p = 0; p < nbDistinctSites_; p++) patternStates_[t][p] = seqs[t]->getValue(repr[p]);
+  data_.reset(sites.clone());
+  nbStates_ = model.getNumberOfStates();
+  initialized_ = false;
+}
+
+void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
+  if (engine_) {
+    plk_destroy(engine_);
+    engine_ = nullptr;
+  }
+  unsigned flags = (scaling_ ? (unsigned)PLK_FLAG_SCALING : 0u) | (nonNegGuard ? (unsigned)PLK_FLAG_NONNEG_GUARD : 0u);
+  plk_handle h = nullptr;
+  int rc = plk_create(deviceFromEnv(), (int)nbStates_, (int)nbClasses_, (int64_t)nbDistinctSites_, nTips_, nInternal_,
+                      (int)nModels, flags, &h);
+  if (rc != PLK_OK) throw DeviceException(rc, std::string("plk_create: ") + plk_last_error(nullptr));
+  engine_ = h;
+}
+
+void AbstractPlkTreeLikelihood::initBranchLengthsParameters() {
+  brLenParameters_.reset();
+  for (size_t i = 0; i < nodes_.size(); i++) {
+    double d = minimumBrLen_;
+    if (!nodes_[i]->hasDistanceToFather()) {
+      if (verbose_)
+        ApplicationTools::displayWarning("Missing branch length " + std::to_string(i) + ". Value is set to " +
+                                         std::to_string(minimumBrLen_));
+      nodes_[i]->setDistanceToFather(minimumBrLen_);
+    } else {
+      d = nodes_[i]->getDistanceToFather();
+      if (d < minimumBrLen_) {
+        nodes_[i]->setDistanceToFather(minimumBrLen_);
+        d = minimumBrLen_;
+      }
+      if (d > maximumBrLen_) {
+        nodes_[i]->setDistanceToFather(maximumBrLen_);
+        d = maximumBrLen_;
+      }
+    }
+    brLenParameters_.addParameter(Parameter("BrLen" + std::to_string(i), d, brLenConstraint_));
+  }
+}
+
+void AbstractPlkTreeLikelihood::applyBranchLengths() {
+  for (size_t i = 0; i < nodes_.size(); i++) {
+    const std::string n = "BrLen" + std::to_string(i);
+    if (parameters_.hasParameter(n)) nodes_[i]->setDistanceToFather(parameters_.getParameterValue(n));
+  }
+}
+
+void AbstractPlkTreeLikelihood::uploadEigen(int m, const SubstitutionModel& model) {
+  const size_t S = nbStates_;
+  std::vector<double> lam(S);
+  for (size_t k = 0; k < S; k++) lam[k] = model.getEigenValues()[k] * model.getRate();
+  check(plk_set_eigen(engine_, m, model.getColumnRightEigenVectors().data(), model.getRowLeftEigenVectors().data(),
+                      lam.data()),
+        "plk_set_eigen");
+}
+
+void AbstractPlkTreeLikelihood::uploadRates() {
+  check(plk_set_category_rates(engine_, rateDistribution_->getCategories().data(),
+                               rateDistribution_->getProbabilities().data()),
+        "plk_set_category_rates");
+}
+
+void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& nodes) {
+  if (nodes.empty()) return;
+  std::vector<int32_t> br, mod;
+  std::vector<double> t;
+  for (const Node* n : nodes) {
+    br.push_back(engineIndex_.at(n));
+    mod.push_back(modelIndexForNode(n));
+    t.push_back(n->getDistanceToFather());
+  }
+  check(plk_update_pmatrices(engine_, (int)br.size(), br.data(), mod.data(), t.data(), PLK_DERIV_P),
+        "plk_update_pmatrices");
+}
+
+void AbstractPlkTreeLikelihood::computeTreeLikelihood() {
+  std::vector<plk_op> ops(opParent_.size());
+  for (size_t i = 0; i < ops.size(); i++) {
+    ops[i].parent = opParent_[i];
+    ops[i].n_children = (int)opChildren_[i].size();
+    for (size_t k = 0; k < 3; k++) ops[i].child[k] = k < opChildren_[i].size() ? opChildren_[i][k] : -1;
+    ops[i].flags = opFlags_[i];
+  }
+  check(plk_update_partials(engine_, ops.data(), (int)ops.size()), "plk_update_partials");
+  siteLnlValid_ = false;
+}
+
+double AbstractPlkTreeLikelihood::reduceRoot() const {
+  double lnl = 0.;
+  check(plk_root_loglik(engine_, rootEngine_, &lnl, nullptr, nullptr), "plk_root_loglik");
+  return lnl;
+}
+
+void AbstractPlkTreeLikelihood::fetchSiteLnl() const {
+  if (siteLnlValid_) return;
+  siteLnl_.resize(nbDistinctSites_);
+  double lnl = 0.;
+  check(plk_root_loglik(engine_, rootEngine_, &lnl, siteLnl_.data(), nullptr), "plk_root_loglik");
+  siteLnlValid_ = true;
+}
+
+double AbstractPlkTreeLikelihood::getValue() const {
+  if (!initialized_) throw Exception("TreeLikelihood::getValue(). Instance is not initialized.");
+  return minusLogLik_;
+}
+
+double AbstractPlkTreeLikelihood::getLogLikelihood() const { return -getValue(); }
+
+double AbstractPlkTreeLikelihood::getLikelihood() const {
+  double l = 1.;
+  for (size_t i = 0; i < nbSites_; i++) l *= getLikelihoodForASite(i);
+  return l;
+}
+
+double AbstractPlkTreeLikelihood::getLogLikelihoodForASite(size_t site) const {
+  fetchSiteLnl();
+  return siteLnl_.at(rootPatternLinks_.at(site));
+}
+
+double AbstractPlkTreeLikelihood::getLikelihoodForASite(size_t site) const {
+  return std::exp(getLogLikelihoodForASite(site));
+}
+
+ParameterList AbstractPlkTreeLikelihood::getBranchLengthsParameters() const {
+  if (!initialized_) throw Exception("getBranchLengthsParameters(). Object is not initialized.");
+  return brLenParameters_.getCommonParametersWith(getParameters());
+}
+
+ParameterList AbstractPlkTreeLikelihood::getRateDistributionParameters() const {
+  if (!initialized_) throw Exception("getRateDistributionParameters(). Object is not initialized.");
+  return rateDistribution_->getIndependentParameters().getCommonParametersWith(getParameters());
+}
+
+void AbstractPlkTreeLikelihood::setParameters(const ParameterList& pl) { setParametersValues(pl); }
+
+VVVdouble AbstractPlkTreeLikelihood::getLikelihoodArray(int nodeId) const {
+  const Node* node = tree_->getNode(nodeId);
+  const int e = engineIndex_.at(node);
+  VVVdouble out(nbDistinctSites_, VVdouble(nbClasses_, Vdouble(nbStates_)));
+  if (e < nTips_) {
+    throw Exception("getLikelihoodArray: leaf arrays are held as state codes on the device");
+  }
+  std::vector<double> buf(nbDistinctSites_ * nbClasses_ * nbStates_);
+  check(plk_get_partials(engine_, e, buf.data()), "plk_get_partials");
+  for (size_t i = 0; i < nbDistinctSites_; i++)
+    for (size_t c = 0; c < nbClasses_; c++)
+      for (size_t s = 0; s < nbStates_; s++) out[i][c][s] = buf[(i * nbClasses_ + c) * nbStates_ + s];
+  return out;
+}
+
+// Branch-length derivatives: central differences of the device log-likelihood
+// (analytic dP propagation, Likelihood/RHomogeneousTreeLikelihood.cpp:346-541, is
+// the next row of SURVEY.md 8f).
+double AbstractPlkTreeLikelihood::getFirstOrderDerivative(const std::string& variable) const {
+  if (!parameters_.hasParameter(variable)) throw ParameterNotFoundException("getFirstOrderDerivative().", variable);
+  if (variable.compare(0, 5, "BrLen") != 0)
+    throw Exception("Derivatives are only implemented for branch length parameters.");
+  AbstractPlkTreeLikelihood* self = const_cast<AbstractPlkTreeLikelihood*>(this);
+  const double t = parameters_.getParameterValue(variable);
+  const double h = 1e-5 * std::max(t, 1e-3);
+  ParameterList pl = parameters_.createSubList(std::vector<std::string>(1, variable));
+  pl[0].setValue(t + h);
+  self->setParameters(pl);
+  const double fp = minusLogLik_;
+  pl[0].setValue(std::max(t - h, minimumBrLen_));
+  const double tm = pl[0].getValue();
+  self->setParameters(pl);
+  const double fm = minusLogLik_;
+  pl[0].setValue(t);
+  self->setParameters(pl);
+  return (fp - fm) / (t + h - tm);
+}
+
+double AbstractPlkTreeLikelihood::getSecondOrderDerivative(const std::string& variable) const {
+  if (!parameters_.hasParameter(variable)) throw ParameterNotFoundException("getSecondOrderDerivative().", variable);
+  AbstractPlkTreeLikelihood* self = const_cast<AbstractPlkTreeLikelihood*>(this);
+  const double t = parameters_.getParameterValue(variable);
+  const double h = 1e-4 * std::max(t, 1e-2);
+  ParameterList pl = parameters_.createSubList(std::vector<std::string>(1, variable));
+  const double f0 = minusLogLik_;
+  pl[0].setValue(t + h);
+  self->setParameters(pl);
+  const double fp = minusLogLik_;
+  pl[0].setValue(std::max(t - h, minimumBrLen_));
+  self->setParameters(pl);
+  const double fm = minusLogLik_;
+  pl[0].setValue(t);
+  self->setParameters(pl);
+  return (fp - 2. * f0 + fm) / (h * h);
+}
+
+// ---------------------------------------------------------------------------
+// RHomogeneousTreeLikelihood
+// ---------------------------------------------------------------------------
+
+RHomogeneousTreeLikelihood::RHomogeneousTreeLikelihood(const Tree& tree, SubstitutionModel* model,
+                                                       DiscreteDistribution* rDist, bool checkRooted, bool verbose,
+                                                       bool usePatterns)
+    : AbstractPlkTreeLikelihood(tree, rDist, checkRooted, verbose, usePatterns), model_(model) {
+  if (!model) throw NullPointerException("RHomogeneousTreeLikelihood: null model");
+  nbStates_ = model->getNumberOfStates();
+}
+
+RHomogeneousTreeLikelihood::RHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data,
+                                                       SubstitutionModel* model, DiscreteDistribution* rDist,
+                                                       bool checkRooted, bool verbose, bool usePatterns)
+    : RHomogeneousTreeLikelihood(tree, model, rDist, checkRooted, verbose, usePatterns) {
+  setData(data);
+}
+
+void RHomogeneousTreeLikelihood::setData(const SiteContainer& sites) {
+  if (verbose_) ApplicationTools::displayTask("Initializing data structure");
+  setDataImpl(sites, model_->getAlphabet(), *model_);
+  createEngine(1, true);
+  // leaf codes and init values (getInitValue) on the device
+  const Alphabet* a = model_->getAlphabet();
+  const int nc = a->getNumberOfCodes();
+  std::vector<double> table((size_t)nc * nbStates_);
+  for (int c = 0; c < nc; c++)
+    for (size_t s = 0; s < nbStates_; s++) table[c * nbStates_ + s] = model_->getInitValue(s, c);
+  check(plk_set_code_table(engine_, nc, table.data()), "plk_set_code_table");
+  std::vector<uint8_t> codes(nbDistinctSites_);
+  for (int t = 0; t < nTips_; t++) {
+    for (size_t p = 0; p < nbDistinctSites_; p++) codes[p] = (uint8_t)patternStates_[t][p];
+    check(plk_set_tip_codes(engine_, t, codes.data()), "plk_set_tip_codes");
+  }
+  std::vector<double> w(rootWeights_.begin(), rootWeights_.end());
+  check(plk_set_pattern_weights(engine_, w.data()), "plk_set_pattern_weights");
+  if (verbose_) {
+    ApplicationTools::displayTaskDone();
+    ApplicationTools::displayResult("Number of distinct sites", nbDistinctSites_);
+  }
+}
+
+void RHomogeneousTreeLikelihood::initialize() {
+  if (initialized_) throw Exception("RHomogeneousTreeLikelihood::initialize(). Object is already initialized.");
+  if (!data_) throw Exception("RHomogeneousTreeLikelihood::initialize(). Data are no set.");
+  resetParameters_();
+  initBranchLengthsParameters();
+  addParameters_(brLenParameters_);
+  addParameters_(model_->getIndependentParameters());
+  addParameters_(rateDistribution_->getIndependentParameters());
+  initialized_ = true;
+  fireParameterChanged(getParameters());
+}
+
+ParameterList RHomogeneousTreeLikelihood::getSubstitutionModelParameters() const {
+  if (!initialized_) throw Exception("getSubstitutionModelParameters(). Object is not initialized.");
+  return model_->getParameters().getCommonParametersWith(getParameters());
+}
+
+void RHomogeneousTreeLikelihood::computeAllTransitionProbabilities() {
+  uploadEigen(0, *model_);
+  uploadRates();
+  std::vector<const Node*> all(nodes_.begin(), nodes_.end());
+  updatePmatrices(all);
+  rootFreqs_ = model_->getFrequencies();
+  check(plk_set_root_frequencies(engine_, rootFreqs_.data()), "plk_set_root_frequencies");
+}
+
+// Likelihood/RHomogeneousTreeLikelihood.cpp:255-283
+void RHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList& params) {
+  if (!initialized_) throw Exception("RHomogeneousTreeLikelihood::fireParameterChanged(). Object not initialized.");
+  applyBranchLengths();
+  model_->matchParametersValues(getParameters());
+  rateDistribution_->matchParametersValues(getParameters());
+  if (rateDistribution_->getParameters().getCommonParametersWith(params).size() > 0 ||
+      model_->getParameters().getCommonParametersWith(params).size() > 0) {
+    computeAllTransitionProbabilities();
+  } else if (params.size() > 0) {
+    std::vector<const Node*> changed;
+    for (size_t i = 0; i < params.size(); i++) {
+      const std::string& s = params[i].getName();
+      if (s.compare(0, 5, "BrLen") == 0) changed.push_back(nodes_[TextTools::to<size_t>(s.substr(5))]);
+    }
+    updatePmatrices(changed);
+  }
+  computeTreeLikelihood();
+  minusLogLik_ = -reduceRoot();
+}
+
+// ---------------------------------------------------------------------------
+// RNonHomogeneousTreeLikelihood (rooted; one eigen-system per branch model)
+// ---------------------------------------------------------------------------
+
+RNonHomogeneousTreeLikelihood::RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data,
+                                                             SubstitutionModelSet* modelSet,
+                                                             DiscreteDistribution* rDist, bool verbose,
+                                                             bool usePatterns, bool)
+    : AbstractPlkTreeLikelihood(tree, rDist, false, verbose, usePatterns), modelSet_(modelSet) {
+  if (!modelSet) throw NullPointerException("RNonHomogeneousTreeLikelihood: null model set");
+  nbStates_ = modelSet->getNumberOfStates();
+  for (const Node* n : nodes_) modelOfNodeId_[n->getId()] = (int)modelSet_->getModelIndexForNode(n->getId());
+  setData(data);
+}
+
+int RNonHomogeneousTreeLikelihood::modelIndexForNode(const Node* n) const { return modelOfNodeId_.at(n->getId()); }
+
+void RNonHomogeneousTreeLikelihood::setData(const SiteContainer& sites) {
+  const SubstitutionModel& m0 = *modelSet_->getModel(0);
+  setDataImpl(sites, modelSet_->getAlphabet(), m0);
+  createEngine(modelSet_->getNumberOfModels(), false);
+  const Alphabet* a = modelSet_->getAlphabet();
+  const int nc = a->getNumberOfCodes();
+  std::vector<double> table((size_t)nc * nbStates_);
+  for (int c = 0; c < nc; c++)
+    for (size_t s = 0; s < nbStates_; s++) table[c * nbStates_ + s] = m0.getInitValue(s, c);
+  check(plk_set_code_table(engine_, nc, table.data()), "plk_set_code_table");
+  std::vector<uint8_t> codes(nbDistinctSites_);
+  for (int t = 0; t < nTips_; t++) {
+    for (size_t p = 0; p < nbDistinctSites_; p++) codes[p] = (uint8_t)patternStates_[t][p];
+    check(plk_set_tip_codes(engine_, t, codes.data()), "plk_set_tip_codes");
+  }
+  std::vector<double> w(rootWeights_.begin(), rootWeights_.end());
+  check(plk_set_pattern_weights(engine_, w.data()), "plk_set_pattern_weights");
+}
+
+void RNonHomogeneousTreeLikelihood::initialize() {
+  if (initialized_) throw Exception("RNonHomogeneousTreeLikelihood::initialize(). Object is already initialized.");
+  resetParameters_();
+  initBranchLengthsParameters();
+  addParameters_(brLenParameters_);
+  addParameters_(modelSet_->getParameters());
+  addParameters_(rateDistribution_->getIndependentParameters());
+  initialized_ = true;
+  fireParameterChanged(getParameters());
+}
+
+ParameterList RNonHomogeneousTreeLikelihood::getSubstitutionModelParameters() const {
+  if (!initialized_) throw Exception("getSubstitutionModelParameters(). Object is not initialized.");
+  return modelSet_->getParameters().getCommonParametersWith(getParameters());
+}
+
+void RNonHomogeneousTreeLikelihood::computeAllTransitionProbabilities() {
+  for (size_t m = 0; m < modelSet_->getNumberOfModels(); m++) uploadEigen((int)m, *modelSet_->getModel(m));
+  uploadRates();
+  std::vector<const Node*> all(nodes_.begin(), nodes_.end());
+  updatePmatrices(all);
+  rootFreqs_ = modelSet_->getRootFrequencies();
+  check(plk_set_root_frequencies(engine_, rootFreqs_.data()), "plk_set_root_frequencies");
+}
+
+// Likelihood/RNonHomogeneousTreeLikelihood.cpp:259-311
+void RNonHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList& params) {
+  if (!initialized_) throw Exception("RNonHomogeneousTreeLikelihood::fireParameterChanged(). Object not initialized.");
+  applyBranchLengths();
+  modelSet_->matchParametersValues(getParameters());
+  rateDistribution_->matchParametersValues(getParameters());
+  if (rateDistribution_->getParameters().getCommonParametersWith(params).size() > 0 ||
+      modelSet_->getParameters().getCommonParametersWith(params).size() > 0) {
+    computeAllTransitionProbabilities();
+  } else if (params.size() > 0) {
+    std::vector<const Node*> changed;
+    for (size_t i = 0; i < params.size(); i++) {
+      const std::string& s = params[i].getName();
+      if (s.compare(0, 5, "BrLen") == 0) changed.push_back(nodes_[TextTools::to<size_t>(s.substr(5))]);
+    }
+    updatePmatrices(changed);
+  }
+  computeTreeLikelihood();
+  minusLogLik_ = -reduceRoot();
+}
+
+}  // namespace bpp

@@ -1,0 +1,419 @@
+// Host mirror: substitution models (generator, frequencies, eigen-system, P(t)) and
+// non-homogeneous model sets.
+#include <cmath>
+
+#include "Bpp/Phyl/Model/Models.h"
+#include "Bpp/Phyl/Model/SubstitutionModelSet.h"
+
+namespace bpp {
+
+#include "lg08_data.inc"
+
+const std::shared_ptr<IntervalConstraint> FrequencySet::FREQUENCE_CONSTRAINT_SMALL =
+    std::make_shared<IntervalConstraint>(NumConstants::SMALL(), 1. - NumConstants::SMALL(), true, true);
+
+// ---------------------------------------------------------------------------
+// SubstitutionModel
+// ---------------------------------------------------------------------------
+
+double SubstitutionModel::getInitValue(size_t i, int state) const {
+  if (i >= size_) throw IndexOutOfBoundsException("SubstitutionModel::getInitValue", i, 0, size_ - 1);
+  if (state < 0 || !alphabet_->isIntInAlphabet(state))
+    throw BadIntException(state, "SubstitutionModel::getInitValue. Character " + alphabet_->intToChar(state) +
+                                     " is not allowed in model.");
+  for (int s : alphabet_->getAlias(state))
+    if (s == (int)i) return 1.;
+  return 0.;
+}
+
+double SubstitutionModel::getScale() const {
+  double s = 0.;
+  for (size_t i = 0; i < size_; i++) s += generator_(i, i) * freq_[i];
+  return -s;
+}
+
+void SubstitutionModel::setScale(double scale) {
+  if (!isScalable_) return;
+  for (size_t i = 0; i < size_; i++)
+    for (size_t j = 0; j < size_; j++) generator_(i, j) *= scale;
+  for (double& l : eigenValues_) l *= scale;
+}
+
+void SubstitutionModel::setDiagonal() {
+  for (size_t i = 0; i < size_; i++) {
+    double lambda = 0.;
+    for (size_t j = 0; j < size_; j++)
+      if (j != i) lambda += generator_(i, j);
+    generator_(i, i) = -lambda;
+  }
+}
+
+namespace {
+// out = V diag(w) Vinv
+void eigenProduct(const RowMatrix<double>& V, const Vdouble& w, const RowMatrix<double>& Vi, RowMatrix<double>& out) {
+  const size_t n = w.size();
+  for (size_t i = 0; i < n; i++)
+    for (size_t j = 0; j < n; j++) {
+      double s = 0.;
+      for (size_t k = 0; k < n; k++) s += V(i, k) * w[k] * Vi(k, j);
+      out(i, j) = s;
+    }
+}
+}  // namespace
+
+const RowMatrix<double>& SubstitutionModel::getPij_t(double t) const {
+  if (t == 0.) {
+    for (size_t i = 0; i < size_; i++)
+      for (size_t j = 0; j < size_; j++) pijt_(i, j) = (i == j) ? 1. : 0.;
+    return pijt_;
+  }
+  Vdouble w(size_);
+  for (size_t k = 0; k < size_; k++) w[k] = std::exp(eigenValues_[k] * rate_ * t);
+  eigenProduct(rightEigenVectors_, w, leftEigenVectors_, pijt_);
+  return pijt_;
+}
+
+const RowMatrix<double>& SubstitutionModel::getdPij_dt(double t) const {
+  Vdouble w(size_);
+  for (size_t k = 0; k < size_; k++) w[k] = rate_ * eigenValues_[k] * std::exp(eigenValues_[k] * rate_ * t);
+  eigenProduct(rightEigenVectors_, w, leftEigenVectors_, dpijt_);
+  return dpijt_;
+}
+
+const RowMatrix<double>& SubstitutionModel::getd2Pij_dt2(double t) const {
+  Vdouble w(size_);
+  for (size_t k = 0; k < size_; k++) {
+    const double l = rate_ * eigenValues_[k];
+    w[k] = l * l * std::exp(eigenValues_[k] * rate_ * t);
+  }
+  eigenProduct(rightEigenVectors_, w, leftEigenVectors_, d2pijt_);
+  return d2pijt_;
+}
+
+// Reversible eigen-system via the symmetric form B = D^1/2 Q D^-1/2 (D = diag(pi)):
+// B = U L U^T  =>  Q = (D^-1/2 U) L (U^T D^1/2), i.e. V = D^-1/2 U, V^-1 = U^T D^1/2.
+// Null states (zero generator row and column: codon stops) are excluded from the
+// decomposition and receive unit eigenvectors with eigenvalue 0, placed after the
+// live ones (Model/AbstractSubstitutionModel.cpp:184-273).
+void SubstitutionModel::computeEigen() {
+  std::vector<size_t> live, null;
+  for (size_t i = 0; i < size_; i++) {
+    bool isNull = std::fabs(generator_(i, i)) < NumConstants::TINY();
+    for (size_t j = 0; j < size_ && isNull; j++)
+      if (std::fabs(generator_(j, i)) >= NumConstants::TINY()) isNull = false;
+    (isNull ? null : live).push_back(i);
+  }
+  const size_t n = live.size();
+  std::vector<double> B(n * n), d, U;
+  std::vector<double> sq(n);
+  for (size_t a = 0; a < n; a++) sq[a] = std::sqrt(freq_[live[a]]);
+  for (size_t a = 0; a < n; a++)
+    for (size_t b = 0; b < n; b++) B[a * n + b] = sq[a] * generator_(live[a], live[b]) / sq[b];
+  for (size_t a = 0; a < n; a++)
+    for (size_t b = a + 1; b < n; b++) {
+      const double m = 0.5 * (B[a * n + b] + B[b * n + a]);
+      B[a * n + b] = B[b * n + a] = m;
+    }
+  symmetricEigen(n, B, d, U);
+  rightEigenVectors_.resize(size_, size_);
+  leftEigenVectors_.resize(size_, size_);
+  eigenValues_.assign(size_, 0.);
+  size_t nullEig = 0;
+  for (size_t k = 0; k < n; k++) {
+    eigenValues_[k] = d[k];
+    if (std::fabs(d[k]) < std::fabs(d[nullEig])) nullEig = k;
+    for (size_t a = 0; a < n; a++) {
+      rightEigenVectors_(live[a], k) = U[a * n + k] / sq[a];
+      leftEigenVectors_(k, live[a]) = U[a * n + k] * sq[a];
+    }
+  }
+  if (n > 0) eigenValues_[nullEig] = 0.;  // exact stationary eigenvalue (:358-361)
+  for (size_t s = 0; s < null.size(); s++) {
+    rightEigenVectors_(null[s], n + s) = 1.;
+    leftEigenVectors_(n + s, null[s]) = 1.;
+  }
+  isDiagonalizable_ = true;
+  isNonSingular_ = true;
+}
+
+void AbstractReversibleSubstitutionModel::updateMatrices() {
+  for (size_t i = 0; i < size_; i++)
+    for (size_t j = 0; j < size_; j++) generator_(i, j) = exchangeability_(i, j) * freq_[j];
+  setDiagonal();
+  normalize();
+  computeEigen();
+}
+
+// ---------------------------------------------------------------------------
+// T92
+// ---------------------------------------------------------------------------
+
+T92::T92(const NucleicAlphabet* alpha, double kappa, double theta)
+    : AbstractReversibleSubstitutionModel(alpha, 4, "T92."), kappa_(kappa), theta_(theta), k_(0.), r_(0.) {
+  addParameter_(Parameter("T92.kappa", kappa, Parameter::R_PLUS_STAR));
+  addParameter_(Parameter("T92.theta", theta, FrequencySet::FREQUENCE_CONSTRAINT_SMALL));
+  updateMatrices();
+}
+
+void T92::updateMatrices() {
+  kappa_ = getParameterValue("kappa");
+  theta_ = getParameterValue("theta");
+  const double th = theta_, ka = kappa_;
+  const double piAT = (1. - th) / 2., piCG = th / 2.;
+  k_ = (ka + 1.) / 2.;
+  r_ = isScalable_ ? 2. / (1. + 2. * th * ka - 2. * th * th * ka) : 1.;
+  freq_ = {piAT, piCG, piCG, piAT};
+  // unscaled generator (Model/Nucleotide/T92.cpp:100-121), then scaled by r
+  const double Qu[4][4] = {{-(1. + th * ka) / 2., th / 2., ka * th / 2., (1. - th) / 2.},
+                           {(1. - th) / 2., -(1. + (1. - th) * ka) / 2., th / 2., ka * (1. - th) / 2.},
+                           {ka * (1. - th) / 2., th / 2., -(1. + (1. - th) * ka) / 2., (1. - th) / 2.},
+                           {(1. - th) / 2., ka * th / 2., th / 2., -(1. + th * ka) / 2.}};
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) generator_(i, j) = Qu[i][j] * r_;
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) exchangeability_(i, j) = generator_(i, j) / freq_[j];
+  // analytic eigen-system (:140-186)
+  eigenValues_ = {0., -r_ * (1. + ka) / 2., -r_ * (1. + ka) / 2., -r_};
+  const double Vi[4][4] = {{(1. - th) / 2., th / 2., th / 2., (1. - th) / 2.},
+                           {0., 1. - th, 0., th - 1.},
+                           {th, 0., -th, 0.},
+                           {(1. - th) / 2., -th / 2., th / 2., (th - 1.) / 2.}};
+  const double V[4][4] = {{1., 0., 1., 1.},
+                          {1., 1., 0., -1.},
+                          {1., 0., (th - 1.) / th, 1.},
+                          {1., th / (th - 1.), 0., -1.}};
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) {
+      leftEigenVectors_(i, j) = Vi[i][j];
+      rightEigenVectors_(i, j) = V[i][j];
+    }
+}
+
+const RowMatrix<double>& T92::getPij_t(double d) const {
+  // closed form, Model/Nucleotide/T92.cpp:355-386
+  const double l = rate_ * r_ * d;
+  const double e1 = std::exp(-l), e2 = std::exp(-k_ * l);
+  const double th = theta_;
+  const double piA = (1. - th) / 2., piC = th / 2., piG = th / 2., piT = (1. - th) / 2.;
+  const double P[4][4] = {
+      {piA * (1. + e1) + th * e2, piC * (1. - e1), piG * (1. + e1) - th * e2, piT * (1. - e1)},
+      {piA * (1. - e1), piC * (1. + e1) + (1. - th) * e2, piG * (1. - e1), piT * (1. + e1) - (1. - th) * e2},
+      {piA * (1. + e1) - (1. - th) * e2, piC * (1. - e1), piG * (1. + e1) + (1. - th) * e2, piT * (1. - e1)},
+      {piA * (1. - e1), piC * (1. + e1) - th * e2, piG * (1. - e1), piT * (1. + e1) + th * e2}};
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) pijt_(i, j) = P[i][j];
+  return pijt_;
+}
+
+const RowMatrix<double>& T92::getdPij_dt(double d) const { return SubstitutionModel::getdPij_dt(d); }
+const RowMatrix<double>& T92::getd2Pij_dt2(double d) const { return SubstitutionModel::getd2Pij_dt2(d); }
+
+// ---------------------------------------------------------------------------
+// GTR
+// ---------------------------------------------------------------------------
+
+GTR::GTR(const NucleicAlphabet* alpha, double a, double b, double c, double d, double e, double piA, double piC,
+         double piG, double piT)
+    : AbstractReversibleSubstitutionModel(alpha, 4, "GTR.") {
+  const double theta = piG + piC;
+  addParameter_(Parameter("GTR.a", a, Parameter::R_PLUS_STAR));
+  addParameter_(Parameter("GTR.b", b, Parameter::R_PLUS_STAR));
+  addParameter_(Parameter("GTR.c", c, Parameter::R_PLUS_STAR));
+  addParameter_(Parameter("GTR.d", d, Parameter::R_PLUS_STAR));
+  addParameter_(Parameter("GTR.e", e, Parameter::R_PLUS_STAR));
+  addParameter_(Parameter("GTR.theta", theta, FrequencySet::FREQUENCE_CONSTRAINT_SMALL));
+  addParameter_(Parameter("GTR.theta1", piA / (1. - theta), FrequencySet::FREQUENCE_CONSTRAINT_SMALL));
+  addParameter_(Parameter("GTR.theta2", piG / theta, FrequencySet::FREQUENCE_CONSTRAINT_SMALL));
+  updateMatrices();
+}
+
+void GTR::updateMatrices() {
+  const double a = getParameterValue("a"), b = getParameterValue("b"), c = getParameterValue("c");
+  const double d = getParameterValue("d"), e = getParameterValue("e");
+  const double theta = getParameterValue("theta"), t1 = getParameterValue("theta1"), t2 = getParameterValue("theta2");
+  const double pA = t1 * (1. - theta), pC = (1. - t2) * theta, pG = t2 * theta, pT = (1. - t1) * (1. - theta);
+  const double p = 2. * (a * pC * pT + b * pA * pT + c * pG * pT + d * pA * pC + e * pC * pG + pA * pG);
+  freq_ = {pA, pC, pG, pT};
+  // A<->G = 1, a = C<->T, b = A<->T, c = G<->T, d = A<->C, e = C<->G (GTR.cpp:104-120)
+  const double S[4][4] = {{0., d, 1., b}, {d, 0., e, a}, {1., e, 0., c}, {b, a, c, 0.}};
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) exchangeability_(i, j) = S[i][j] / p;
+  AbstractReversibleSubstitutionModel::updateMatrices();
+}
+
+// ---------------------------------------------------------------------------
+// LG08
+// ---------------------------------------------------------------------------
+
+LG08::LG08(const ProteicAlphabet* alpha) : AbstractReversibleSubstitutionModel(alpha, 20, "LG08.") {
+  for (int i = 0; i < 20; i++) {
+    freq_[i] = kLG08Frequencies[i];
+    for (int j = 0; j < 20; j++) exchangeability_(i, j) = kLG08Exchangeability[i][j];
+  }
+  updateMatrices();
+}
+
+void LG08::updateMatrices() { AbstractReversibleSubstitutionModel::updateMatrices(); }
+
+// ---------------------------------------------------------------------------
+// YN98
+// ---------------------------------------------------------------------------
+
+YN98::YN98(const GeneticCode* gc, const Vdouble& codonFreqs, double kappa, double omega)
+    : AbstractReversibleSubstitutionModel(gc->getSourceAlphabet(), 64, "YN98."), gc_(gc), codonFreqs_(codonFreqs) {
+  addParameter_(Parameter("YN98.kappa", kappa, Parameter::R_PLUS_STAR));
+  addParameter_(Parameter("YN98.omega", omega,
+                          std::make_shared<IntervalConstraint>(NumConstants::MILLI(), 999., true, true)));
+  if (codonFreqs_.empty()) codonFreqs_.assign(64, 1.);  // F3X4, equal nucleotide frequencies
+  double s = 0.;
+  for (int i = 0; i < 64; i++) {
+    if (gc_->isStop(i)) codonFreqs_[i] = 0.;
+    s += codonFreqs_[i];
+  }
+  for (double& f : codonFreqs_) f /= s;
+  updateMatrices();
+}
+
+void YN98::updateMatrices() {
+  const double kappa = getParameterValue("kappa"), omega = getParameterValue("omega");
+  freq_ = codonFreqs_;
+  auto isTransition = [](int x, int y) { return (x == 0 && y == 2) || (x == 2 && y == 0) || (x == 1 && y == 3) || (x == 3 && y == 1); };
+  for (int i = 0; i < 64; i++)
+    for (int j = 0; j < 64; j++) {
+      generator_(i, j) = 0.;
+      if (i == j || gc_->isStop(i) || gc_->isStop(j)) continue;
+      int diff = 0, from = 0, to = 0;
+      for (int pos = 0; pos < 3; pos++) {
+        const int div = pos == 0 ? 16 : (pos == 1 ? 4 : 1);
+        const int a = (i / div) % 4, b = (j / div) % 4;
+        if (a != b) {
+          diff++;
+          from = a;
+          to = b;
+        }
+      }
+      if (diff != 1) continue;
+      double q = isTransition(from, to) ? kappa : 1.;
+      if (!gc_->areSynonymous(i, j)) q *= omega;
+      generator_(i, j) = q * freq_[j];
+    }
+  setDiagonal();
+  normalize();
+  for (int i = 0; i < 64; i++)
+    for (int j = 0; j < 64; j++) exchangeability_(i, j) = freq_[j] > 0. ? generator_(i, j) / freq_[j] : 0.;
+  computeEigen();
+}
+
+// ---------------------------------------------------------------------------
+// Frequency sets
+// ---------------------------------------------------------------------------
+
+GCFrequencySet::GCFrequencySet(const NucleicAlphabet* alpha, double theta) : FrequencySet(alpha, 4, "GC.") {
+  addParameter_(Parameter("GC.theta", theta, FREQUENCE_CONSTRAINT_SMALL));
+  fireParameterChanged(ParameterList());
+}
+
+void GCFrequencySet::fireParameterChanged(const ParameterList&) {
+  const double th = getParameterValue("theta");
+  freq_ = {(1. - th) / 2., th / 2., th / 2., (1. - th) / 2.};
+}
+
+// ---------------------------------------------------------------------------
+// SubstitutionModelSet
+// ---------------------------------------------------------------------------
+
+SubstitutionModelSet::SubstitutionModelSet(const SubstitutionModelSet& s)
+    : AbstractParametrizable(s), alphabet_(s.alphabet_), nodesOfModel_(s.nodesOfModel_),
+      modelOfNode_(s.modelOfNode_), globalNames_(s.globalNames_) {
+  for (auto& m : s.models_) models_.push_back(std::shared_ptr<SubstitutionModel>(m->clone()));
+  if (s.rootFreqs_) rootFreqs_.reset(s.rootFreqs_->clone());
+}
+
+void SubstitutionModelSet::setRootFrequencies(FrequencySet* rootFreqs) {
+  rootFreqs_.reset(rootFreqs);
+  if (rootFreqs_) addParameters_(rootFreqs_->getParameters());
+}
+
+void SubstitutionModelSet::addModel(SubstitutionModel* model, const std::vector<int>& nodesId,
+                                    const std::vector<std::string>& globalNames) {
+  const size_t k = models_.size() + 1;
+  models_.push_back(std::shared_ptr<SubstitutionModel>(model));
+  nodesOfModel_.push_back(nodesId);
+  for (int id : nodesId) modelOfNode_[id] = k - 1;
+  globalNames_ = globalNames;
+  const ParameterList& pl = model->getParameters();
+  for (size_t i = 0; i < pl.size(); i++) {
+    const std::string& n = pl[i].getName();
+    bool global = false;
+    for (auto& g : globalNames_)
+      if (g == n) global = true;
+    if (global) {
+      if (!parameters_.hasParameter(n)) addParameter_(pl[i]);
+    } else {
+      Parameter p(pl[i]);
+      p.setName(n + "_" + std::to_string(k));
+      addParameter_(p);
+    }
+  }
+}
+
+ParameterList SubstitutionModelSet::getModelParameters() const {
+  ParameterList out;
+  ParameterList rf = getRootFrequenciesParameters();
+  for (size_t i = 0; i < parameters_.size(); i++)
+    if (!rf.hasParameter(parameters_[i].getName())) out.addParameter(parameters_[i]);
+  return out;
+}
+
+void SubstitutionModelSet::fireParameterChanged(const ParameterList&) {
+  for (size_t k = 0; k < models_.size(); k++) {
+    ParameterList own;
+    const ParameterList& pl = models_[k]->getParameters();
+    for (size_t i = 0; i < pl.size(); i++) {
+      const std::string& n = pl[i].getName();
+      const std::string local = n + "_" + std::to_string(k + 1);
+      Parameter p(pl[i]);
+      if (parameters_.hasParameter(local))
+        p.setValue(parameters_.getParameterValue(local));
+      else if (parameters_.hasParameter(n))
+        p.setValue(parameters_.getParameterValue(n));
+      own.addParameter(p);
+    }
+    models_[k]->matchParametersValues(own);
+  }
+  if (rootFreqs_) rootFreqs_->matchParametersValues(parameters_);
+}
+
+SubstitutionModelSet* SubstitutionModelSetTools::createNonHomogeneousModelSet(
+    SubstitutionModel* model, FrequencySet* rootFreqs, const Tree* tree, const std::map<std::string, std::string>&,
+    std::map<std::string, std::vector<Vint> >& globalParameterNames) {
+  const TreeTemplate<Node>* tt = dynamic_cast<const TreeTemplate<Node>*>(tree);
+  if (!tt) throw Exception("createNonHomogeneousModelSet: unsupported tree implementation");
+  std::vector<std::string> globals;
+  for (auto& kv : globalParameterNames) globals.push_back(kv.first);
+  SubstitutionModelSet* set = new SubstitutionModelSet(model->getAlphabet());
+  for (const Node* n : tt->getNodes()) {
+    if (n == tt->getRootNode()) continue;
+    set->addModel(model->clone(), std::vector<int>(1, n->getId()), globals);
+  }
+  set->setRootFrequencies(rootFreqs);
+  delete model;
+  return set;
+}
+
+SubstitutionModelSet* SubstitutionModelSetTools::createHomogeneousModelSet(SubstitutionModel* model,
+                                                                           FrequencySet* rootFreqs,
+                                                                           const Tree* tree) {
+  const TreeTemplate<Node>* tt = dynamic_cast<const TreeTemplate<Node>*>(tree);
+  if (!tt) throw Exception("createHomogeneousModelSet: unsupported tree implementation");
+  std::vector<int> ids;
+  for (const Node* n : tt->getNodes())
+    if (n != tt->getRootNode()) ids.push_back(n->getId());
+  SubstitutionModelSet* set = new SubstitutionModelSet(model->getAlphabet());
+  std::vector<std::string> globals = model->getParameters().getParameterNames();
+  set->addModel(model, ids, globals);
+  set->setRootFrequencies(rootFreqs);
+  return set;
+}
+
+}  // namespace bpp

@@ -1,0 +1,101 @@
+// CPU-only checks of the host mirror (no GPU): prints JSON records that
+// tests/test_host.py compares with the oracle and the golden fixtures.
+#include <Bpp/Phyl/Model/Codon/YN98.h>
+#include <Bpp/Phyl/Model/Nucleotide/GTR.h>
+#include <Bpp/Phyl/Model/Nucleotide/T92.h>
+#include <Bpp/Phyl/Model/Protein/LG08.h>
+#include <Bpp/Phyl/Model/RateDistribution/GammaDiscreteRateDistribution.h>
+#include <Bpp/Phyl/Model/SubstitutionModelSet.h>
+#include <Bpp/Phyl/TreeTemplate.h>
+#include <Bpp/Seq/Alphabet/AlphabetTools.h>
+
+#include <cstdio>
+#include <memory>
+#include <string>
+#include <vector>
+
+using namespace bpp;
+
+static void printVec(const char* key, const std::vector<double>& v) {
+  std::printf("\"%s\": [", key);
+  for (size_t i = 0; i < v.size(); i++) std::printf("%s%.17g", i ? ", " : "", v[i]);
+  std::printf("]");
+}
+
+static void printModel(const char* name, const SubstitutionModel& m, const std::vector<double>& ts) {
+  const size_t S = m.getNumberOfStates();
+  std::printf("{\"kind\": \"model\", \"name\": \"%s\", \"S\": %zu, ", name, S);
+  std::vector<double> Q(m.getGenerator().data(), m.getGenerator().data() + S * S);
+  printVec("Q", Q);
+  std::printf(", ");
+  printVec("pi", m.getFrequencies());
+  std::printf(", ");
+  printVec("t", ts);
+  std::printf(", \"P\": [");
+  for (size_t k = 0; k < ts.size(); k++) {
+    const RowMatrix<double>& P = m.getPij_t(ts[k]);
+    std::vector<double> p(P.data(), P.data() + S * S);
+    std::printf("%s[", k ? ", " : "");
+    for (size_t i = 0; i < p.size(); i++) std::printf("%s%.17g", i ? ", " : "", p[i]);
+    std::printf("]");
+  }
+  std::printf("], \"P_eigen\": [");
+  for (size_t k = 0; k < ts.size(); k++) {
+    const RowMatrix<double>& P = m.SubstitutionModel::getPij_t(ts[k]);
+    std::vector<double> p(P.data(), P.data() + S * S);
+    std::printf("%s[", k ? ", " : "");
+    for (size_t i = 0; i < p.size(); i++) std::printf("%s%.17g", i ? ", " : "", p[i]);
+    std::printf("]");
+  }
+  std::printf("]}\n");
+}
+
+int main() {
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  std::vector<double> ts = {1e-6, 0.01, 0.1, 0.5, 2.0, 10.0};
+  // gamma rates
+  for (double a : {0.2, 0.5, 1.0, 2.0, 7.5}) {
+    GammaDiscreteRateDistribution g(4, a);
+    std::printf("{\"kind\": \"gamma\", \"alpha\": %.17g, ", a);
+    printVec("rates", g.getCategories());
+    std::printf("}\n");
+  }
+  printModel("T92", T92(dna, 3.0, 0.5), ts);
+  printModel("T92_k2_t03", T92(dna, 2.0, 0.3), ts);
+  printModel("GTR", GTR(dna, 1.2, 0.4, 0.6, 0.8, 0.5, 0.30, 0.20, 0.25, 0.25), ts);
+  printModel("LG08", LG08(&AlphabetTools::PROTEIN_ALPHABET), ts);
+  StandardGeneticCode gc(dna);
+  printModel("YN98", YN98(&gc, std::vector<double>(), 2.0, 0.3), ts);
+  // trees: postorder ids, unroot
+  const char* newicks[] = {"((A:0.01, B:0.02):0.03,C:0.01,D:0.1);", "(((A:0.01, B:0.01):0.02,C:0.03):0.01,D:0.04);",
+                           "((a:1,b:2):3,(c:4,d:5):6);"};
+  for (const char* nw : newicks) {
+    std::unique_ptr<TreeTemplate<Node> > t(TreeTemplateTools::parenthesisToTree(nw));
+    std::printf("{\"kind\": \"tree\", \"newick\": \"%s\", \"rooted\": %s, \"leaves\": [", nw, t->isRooted() ? "true" : "false");
+    std::vector<std::string> ln = t->getLeavesNames();
+    for (size_t i = 0; i < ln.size(); i++) std::printf("%s\"%s\"", i ? ", " : "", ln[i].c_str());
+    std::printf("], \"ids\": [");
+    std::vector<int> ids = t->getNodesId();
+    for (size_t i = 0; i < ids.size(); i++) std::printf("%s%d", i ? ", " : "", ids[i]);
+    std::printf("]");
+    if (t->isRooted()) {
+      t->unroot();
+      std::printf(", \"unrooted\": \"%s\"", TreeTemplateTools::treeToParenthesis(*t).c_str());
+    }
+    std::printf("}\n");
+  }
+  // NH model set parameter naming
+  std::unique_ptr<TreeTemplate<Node> > t(TreeTemplateTools::parenthesisToTree("((A:0.1,B:0.2):0.3,(C:0.1,D:0.2):0.1);"));
+  std::map<std::string, std::vector<Vint> > globals;
+  globals["T92.kappa"] = {};
+  std::map<std::string, std::string> alias;
+  std::unique_ptr<SubstitutionModelSet> set(SubstitutionModelSetTools::createNonHomogeneousModelSet(
+      new T92(dna, 3.), new GCFrequencySet(dna), t.get(), alias, globals));
+  set->setParameterValue("T92.theta_2", 0.7);
+  std::printf("{\"kind\": \"modelset\", \"n\": %zu, \"names\": [", set->getNumberOfModels());
+  std::vector<std::string> pn = set->getParameters().getParameterNames();
+  for (size_t i = 0; i < pn.size(); i++) std::printf("%s\"%s\"", i ? ", " : "", pn[i].c_str());
+  std::printf("], \"theta2\": %.17g, \"theta1\": %.17g}\n", set->getModel(1)->getParameterValue("theta"),
+              set->getModel(0)->getParameterValue("theta"));
+  return 0;
+}

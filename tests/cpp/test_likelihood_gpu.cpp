@@ -1,0 +1,110 @@
+// Drop-in check of the Bio++ API mirror on the MI355X: the same calls the
+// reference's test/test_likelihood.cpp and test/test_likelihood_clock.cpp make
+// (tree from Newick, DNA site container, T92 + discrete Gamma, RHomogeneousTreeLikelihood,
+// initialize / getValue, optimizeTreeScale + optimizeNumericalParameters2), checked
+// against the goldens those tests hold.  Exit code 0 = pass (reference convention).
+#include <Bpp/Numeric/Prob/GammaDiscreteDistribution.h>
+#include <Bpp/Phyl/Likelihood/RHomogeneousTreeLikelihood.h>
+#include <Bpp/Phyl/Model/Nucleotide/T92.h>
+#include <Bpp/Phyl/Model/RateDistribution/GammaDiscreteRateDistribution.h>
+#include <Bpp/Phyl/OptimizationTools.h>
+#include <Bpp/Phyl/TreeTemplate.h>
+#include <Bpp/Seq/Alphabet/AlphabetTools.h>
+#include <Bpp/Seq/Container/VectorSiteContainer.h>
+
+#include <cmath>
+#include <iomanip>
+#include <iostream>
+#include <memory>
+
+using namespace bpp;
+
+static int failures = 0;
+
+static void expectNear(const char* what, double got, double want, double tol) {
+  const bool ok = std::fabs(got - want) <= tol;
+  std::cout << std::setprecision(20) << what << " = " << got << " (expected " << want << ", tol " << tol << ") "
+            << (ok ? "ok" : "FAIL") << std::endl;
+  if (!ok) failures++;
+}
+
+// test/test_likelihood.cpp:91-108 inputs and goldens
+static void unrootedGammaCase() {
+  std::unique_ptr<TreeTemplate<Node> > tree(
+      TreeTemplateTools::parenthesisToTree("((A:0.01, B:0.02):0.03,C:0.01,D:0.1);"));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  const char* names[] = {"A", "B", "C", "D"};
+  const char* seqs[] = {"AAATGGCTGTGCACGTC", "GACTGGATCTGCACGTC", "CTCTGGATGTGCACGTG", "AAATGGCGGTGCGCCTA"};
+  for (int i = 0; i < 4; i++) aln.addSequence(BasicSequence(names[i], seqs[i], dna));
+  T92 model(dna, 3.);
+  GammaDiscreteRateDistribution rdist(4, 1.0);
+  RHomogeneousTreeLikelihood tl(*tree, aln, &model, &rdist, true, false);
+  tl.initialize();
+  expectNear("T92+G4 initial -lnL", tl.getValue(), 85.030942031997312824, 1e-9);
+  std::cout << "distinct sites: " << tl.getNumberOfDistinctSites() << " of " << tl.getNumberOfSites() << std::endl;
+  // per-site log-likelihoods sum to the total
+  double s = 0.;
+  for (size_t i = 0; i < tl.getNumberOfSites(); i++) s += tl.getLogLikelihoodForASite(i);
+  expectNear("sum of site lnL", s, tl.getLogLikelihood(), 1e-10);
+  // branch-length parameters are BrLen<postorder index>, 5 branches once unrooted
+  ParameterList bl = tl.getBranchLengthsParameters();
+  expectNear("number of BrLen parameters", (double)bl.size(), 5., 0.);
+  OptimizationTools::optimizeTreeScale(&tl);
+  std::cout << "after tree scale: " << tl.getValue() << std::endl;
+  OptimizationTools::optimizeNumericalParameters2(&tl, tl.getParameters(), 0, 0.000001, 10000, 0, 0);
+  expectNear("T92+G4 optimised -lnL", tl.getValue(), 65.72293577214308868406, 1e-3);
+}
+
+// test/test_likelihood_clock.cpp:99-115: rooted tree kept rooted, constant rate
+static void rootedConstantCase() {
+  std::unique_ptr<TreeTemplate<Node> > tree(
+      TreeTemplateTools::parenthesisToTree("(((A:0.01, B:0.01):0.02,C:0.03):0.01,D:0.04);"));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  const char* names[] = {"A", "B", "C", "D"};
+  const char* seqs[] = {"AAATGGCTGTGCACGTC", "AACTGGATCTGCATGTC", "ATCTGGACGTGCACGTG", "CAACGGGAGTGCGCCTA"};
+  for (int i = 0; i < 4; i++) aln.addSequence(BasicSequence(names[i], seqs[i], dna));
+  T92 model(dna, 3.);
+  ConstantRateDistribution rdist;
+  RHomogeneousTreeLikelihood tl(*tree, aln, &model, &rdist, false, false);
+  tl.enableFirstOrderDerivatives(false);
+  tl.enableSecondOrderDerivatives(false);
+  tl.initialize();
+  expectNear("T92 rooted initial -lnL", tl.getValue(), 94.3957, 5e-5);
+  OptimizationTools::optimizeNumericalParameters2(&tl, tl.getParameters(), 0, 0.000001, 10000, 0, 0);
+  expectNear("T92 rooted optimised -lnL", tl.getValue(), 71.2657, 1e-3);
+}
+
+// gaps are not allowed by the model: BadIntException like getInitValue
+static void gapCase() {
+  std::unique_ptr<TreeTemplate<Node> > tree(TreeTemplateTools::parenthesisToTree("((A:0.1,B:0.2):0.1,C:0.3);"));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  aln.addSequence(BasicSequence("A", "AC-T", dna));
+  aln.addSequence(BasicSequence("B", "ACGT", dna));
+  aln.addSequence(BasicSequence("C", "ACGA", dna));
+  T92 model(dna, 2.);
+  ConstantRateDistribution rdist;
+  bool thrown = false;
+  try {
+    RHomogeneousTreeLikelihood tl(*tree, aln, &model, &rdist, true, false);
+  } catch (BadIntException&) {
+    thrown = true;
+  }
+  std::cout << "gap -> BadIntException: " << (thrown ? "ok" : "FAIL") << std::endl;
+  if (!thrown) failures++;
+}
+
+int main() {
+  try {
+    unrootedGammaCase();
+    rootedConstantCase();
+    gapCase();
+  } catch (Exception& e) {
+    std::cerr << e.what() << std::endl;
+    return 1;
+  }
+  std::cout << (failures ? "FAILED" : "PASSED") << std::endl;
+  return failures ? 1 : 0;
+}

@@ -1,0 +1,139 @@
+"""CPU tests of the host-side logic: the Python helpers (bpp-phyl_amd/phylo.py,
+workload.py) and the C++ Bio++ mirror (bpp-phyl_amd/host) against the oracle and
+the golden fixtures.  No GPU."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+from scipy.linalg import expm
+
+import oracle
+import phylo
+import workload
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+HOST = os.path.join(ROOT, "bpp-phyl_amd", "host")
+
+
+@pytest.fixture(scope="module")
+def host_records():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "bpp-phyl_amd")], check=True)
+    subprocess.run(["make", "-s", "-j8", "-C", HOST], check=True)
+    out = subprocess.run([os.path.join(HOST, "bin", "test_host_cpu")], check=True, capture_output=True,
+                         text=True).stdout
+    return [json.loads(line) for line in out.splitlines() if line.strip()]
+
+
+def _models(recs):
+    return {r["name"]: r for r in recs if r["kind"] == "model"}
+
+
+# ------------------------------------------------------------------ C++ host mirror
+
+def test_host_gamma_matches_oracle(host_records):
+    for r in (x for x in host_records if x["kind"] == "gamma"):
+        ro, _ = oracle.gamma_rates(4, r["alpha"])
+        assert np.allclose(r["rates"], ro, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("name", ["T92", "T92_k2_t03", "GTR", "LG08"])
+def test_host_pmatrix_vs_expm_fixture(host_records, name):
+    f = np.load(os.path.join(GOLD, "pmatrix.npz"))
+    r = _models(host_records)[name]
+    S = r["S"]
+    assert np.allclose(np.array(r["Q"]).reshape(S, S), f[f"{name}_Q"], atol=1e-14)
+    for P, Pe, Pf in zip(r["P"], r["P_eigen"], f[f"{name}_P"]):
+        assert np.allclose(np.array(P).reshape(S, S), Pf, atol=1e-13)
+        assert np.allclose(np.array(Pe).reshape(S, S), Pf, atol=1e-13)
+
+
+def test_host_yn98_properties(host_records):
+    r = _models(host_records)["YN98"]
+    Q = np.array(r["Q"]).reshape(64, 64)
+    pi = np.array(r["pi"])
+    stops = [48, 50, 56]  # TAA TAG TGA
+    assert np.all(pi[stops] == 0) and abs(pi.sum() - 1) < 1e-14
+    assert abs(-np.dot(np.diag(Q), pi) - 1) < 1e-13
+    for t, P in zip(r["t"], r["P"]):
+        P = np.array(P).reshape(64, 64)
+        assert np.allclose(P[stops][:, stops], np.eye(3))
+        live = [i for i in range(64) if i not in stops]
+        assert np.allclose(P[live].sum(1), 1, atol=1e-12)
+        D = pi[:, None] * P
+        assert np.allclose(D, D.T, atol=1e-14)
+        assert np.allclose(P[np.ix_(live, live)], expm(Q[np.ix_(live, live)] * t), atol=1e-12)
+        # the oracle's independent Jacobi path
+        assert np.allclose(P, oracle.reversible_pij(Q, pi, t), atol=1e-12)
+
+
+def test_host_trees(host_records):
+    trees = [r for r in host_records if r["kind"] == "tree"]
+    assert trees[0]["leaves"] == ["A", "B", "C", "D"] and not trees[0]["rooted"]
+    assert trees[1]["ids"] == list(range(7))
+    assert trees[2]["unrooted"] == "(a:1,b:2,(c:4,d:5):9);"
+    # same unroot semantics in the Python helper
+    t = phylo.Tree.from_newick(trees[2]["newick"])
+    t.unroot()
+    assert [n.name for n in t.root.sons[:2]] == ["a", "b"] and abs(t.root.sons[2].dist - 9.0) < 1e-15
+
+
+def test_host_model_set_naming(host_records):
+    r = next(x for x in host_records if x["kind"] == "modelset")
+    assert r["n"] == 6
+    assert r["names"][0] == "T92.kappa" and "T92.theta_6" in r["names"] and r["names"][-1] == "GC.theta"
+    assert r["theta2"] == 0.7 and r["theta1"] == 0.5
+
+
+# ------------------------------------------------------------------ Python host helpers
+
+def test_newick_postorder_ids():
+    t = phylo.Tree.from_newick("((A:0.01, B:0.02):0.03,C:0.01,D:0.1);")
+    assert [n.id for n in t.nodes()] == list(range(6))
+    assert t.leaf_names() == ["A", "B", "C", "D"]
+    et = phylo.engine_tree(t)
+    assert et.n_tips == 4 and et.n_internal == 2
+    assert et.brlen_names == [f"BrLen{i}" for i in range(5)]
+
+
+def test_engine_tree_unroots_and_clamps():
+    t = phylo.Tree.from_newick("(((s05:0.1,s04:0.0):0.3,s03:0.0):0.26667,s02:0.06667,s01:0.16667);")
+    et = phylo.engine_tree(t)
+    assert et.brlen.min() == 0.0  # the root entry
+    assert sorted(et.brlen)[1] == phylo.MIN_BRLEN  # zero lengths clamped to 1e-6
+    t2 = phylo.balanced_tree(64)
+    et2 = phylo.engine_tree(t2)
+    assert et2.n_internal == 62 and len(et.ops) == et.n_internal
+
+
+@pytest.mark.parametrize("name", ["T92", "GTR", "LG08"])
+def test_python_models_vs_expm(name):
+    f = np.load(os.path.join(GOLD, "pmatrix.npz"))
+    m = {"T92": phylo.t92(3.0, 0.5), "GTR": phylo.gtr(1.2, 0.4, 0.6, 0.8, 0.5, 0.30, 0.20, 0.25, 0.25),
+         "LG08": phylo.lg08()}[name]
+    for t, P in zip(f[f"{name}_t"], f[f"{name}_P"]):
+        assert np.allclose(m.pij(t), P, atol=1e-13)
+
+
+def test_split_ops_polytomy():
+    ops = phylo.split_ops([(10, (0, 1, 2, 3, 4))])
+    assert ops == [(10, (0, 1, 2), 0), (10, (3, 4), 1)]
+
+
+def test_simulation_is_shard_invariant():
+    wl = workload.make_workload("gtr_g4_dna_1M_64", n_patterns=5000)
+    a = wl.simulate(0, 5000)
+    b = np.concatenate([wl.simulate(0, 1234), wl.simulate(1234, 5000)], axis=1)
+    assert np.array_equal(a, b)
+    assert a.min() >= 0 and a.max() <= 3
+    # empirical base composition close to the model's stationary frequencies
+    freq = np.bincount(a.ravel(), minlength=4) / a.size
+    assert np.allclose(freq, wl.models[0].pi, atol=0.02)
+
+
+def test_algorithmic_bytes_cfg2():
+    wl = workload.make_workload("gtr_g4_dna_1M_64", n_patterns=10)
+    assert wl.algorithmic_bytes_per_pattern() == 15944
+    assert abs(wl.algorithmic_bytes_per_pattern() / wl.et.n_internal - 257.16) < 0.01
