@@ -3,6 +3,8 @@
 
 #include <cmath>
 #include <limits>
+#include <map>
+#include <memory>
 
 namespace bpp {
 
@@ -71,12 +73,86 @@ unsigned int OptimizationTools::optimizeTreeScale(TreeLikelihood* tl, double tol
   return nEval;
 }
 
+namespace {
+
+// Global molecular clock (OptimizationTools.cpp:266-353 with useClock = true, i.e.
+// GlobalClockTreeLikelihoodFunctionWrapper): branch lengths of a rooted tree are
+// derived from node heights, h(leaf) = 0, h(root) = TotalHeight and, for every
+// other internal node v, h(v) = HeightP_v * h(father(v)) with HeightP_v in (0, 1).
+struct ClockMap {
+  std::vector<const Node*> nodes;       // postorder, root last: BrLen<i> = nodes[i]
+  std::map<const Node*, size_t> index;
+  std::vector<int> internalNonRoot;     // indices into nodes
+  double totalHeight = 0.;
+  std::vector<double> heightP;          // per internalNonRoot
+
+  explicit ClockMap(const TreeTemplate<Node>& tree) {
+    nodes = tree.getNodes();
+    for (size_t i = 0; i < nodes.size(); i++) index[nodes[i]] = i;
+    if (nodes.back()->getNumberOfSons() != 2)
+      throw Exception("optimizeNumericalParameters2(useClock = true): the tree must be rooted");
+    std::vector<double> h(nodes.size(), 0.);
+    for (size_t i = 0; i < nodes.size(); i++) {
+      const Node* n = nodes[i];
+      double m = 0.;
+      for (size_t k = 0; k < n->getNumberOfSons(); k++) {
+        const Node* c = n->getSon(k);
+        m = std::max(m, h[index[c]] + c->getDistanceToFather());
+      }
+      h[i] = n->isLeaf() ? 0. : m;
+    }
+    totalHeight = h.back();
+    for (size_t i = 0; i + 1 < nodes.size(); i++)
+      if (!nodes[i]->isLeaf()) {
+        internalNonRoot.push_back((int)i);
+        heightP.push_back(std::min(std::max(h[i] / h[index[nodes[i]->getFather()]], 1e-6), 1. - 1e-6));
+      }
+  }
+  std::vector<double> branchLengths() const {
+    std::vector<double> h(nodes.size(), 0.);
+    h.back() = totalHeight;
+    // heights top-down (reverse postorder)
+    std::map<int, double> p;
+    for (size_t k = 0; k < internalNonRoot.size(); k++) p[internalNonRoot[k]] = heightP[k];
+    for (size_t i = nodes.size() - 1; i-- > 0;) {
+      const Node* n = nodes[i];
+      h[i] = n->isLeaf() ? 0. : p[(int)i] * h[index.at(n->getFather())];
+    }
+    std::vector<double> bl(nodes.size() - 1);
+    for (size_t i = 0; i + 1 < nodes.size(); i++)
+      bl[i] = std::min(std::max(h[index.at(nodes[i]->getFather())] - h[i], 0.000001), 10000.);
+    return bl;
+  }
+};
+
+}  // namespace
+
 unsigned int OptimizationTools::optimizeNumericalParameters2(TreeLikelihood* tl, const ParameterList& parameters,
                                                              OptimizationListener*, double tolerance,
                                                              unsigned int tlEvalMax, OutputStream*, OutputStream*,
-                                                             bool, bool, unsigned int, const std::string&) {
+                                                             bool, bool useClock, unsigned int, const std::string&) {
   ParameterList pl = tl->getParameters().getCommonParametersWith(parameters);
   unsigned int nEval = 0;
+  std::unique_ptr<ClockMap> clock;
+  ParameterList brl;
+  if (useClock) {
+    const TreeTemplate<Node>* tree = dynamic_cast<const TreeTemplate<Node>*>(&tl->getTree());
+    clock.reset(new ClockMap(*tree));
+    brl = tl->getBranchLengthsParameters();
+    // branch lengths are replaced by the clock parameters
+    ParameterList rest;
+    for (size_t i = 0; i < pl.size(); i++)
+      if (pl[i].getName().compare(0, 5, "BrLen") != 0) rest.addParameter(pl[i]);
+    pl = rest;
+    for (size_t i = 0; i < brl.size(); i++) brl[i].setValue(clock->branchLengths()[i]);
+    tl->setParameters(brl);
+  }
+  auto applyClock = [&]() {
+    std::vector<double> bl = clock->branchLengths();
+    for (size_t i = 0; i < brl.size(); i++) brl[i].setValue(bl[i]);
+    tl->setParameters(brl);
+    return tl->getValue();
+  };
   double fcur = tl->getValue();
   for (int round = 0; round < 200 && nEval < tlEvalMax; round++) {
     const double fstart = fcur;
@@ -95,6 +171,33 @@ unsigned int OptimizationTools::optimizeNumericalParameters2(TreeLikelihood* tl,
       double fu = f(u);
       if (fu > fcur) fu = f(x0);  // never accept a worse point
       fcur = fu;
+    }
+    if (clock) {
+      // TotalHeight on a log scale, then every HeightP in (0, 1)
+      {
+        const double x0 = std::log(clock->totalHeight);
+        auto f = [&](double u) {
+          clock->totalHeight = std::exp(u);
+          return applyClock();
+        };
+        double fmin = 0.;
+        const double u = brent(f, x0 - 4., x0 + 4., x0, 1e-8, 200, &fmin, &nEval);
+        double fu = f(u);
+        if (fu > fcur) fu = f(x0);
+        fcur = fu;
+      }
+      for (size_t k = 0; k < clock->heightP.size(); k++) {
+        const double x0 = clock->heightP[k];
+        auto f = [&](double v) {
+          clock->heightP[k] = v;
+          return applyClock();
+        };
+        double fmin = 0.;
+        const double u = brent(f, 1e-6, 1. - 1e-6, x0, 1e-8, 200, &fmin, &nEval);
+        double fu = f(u);
+        if (fu > fcur) fu = f(x0);
+        fcur = fu;
+      }
     }
     if (fstart - fcur < tolerance) break;
   }

@@ -72,8 +72,10 @@ static void rootedConstantCase() {
   tl.enableSecondOrderDerivatives(false);
   tl.initialize();
   expectNear("T92 rooted initial -lnL", tl.getValue(), 94.3957, 5e-5);
-  OptimizationTools::optimizeNumericalParameters2(&tl, tl.getParameters(), 0, 0.000001, 10000, 0, 0);
-  expectNear("T92 rooted optimised -lnL", tl.getValue(), 71.2657, 1e-3);
+  // global molecular clock, as test_likelihood_clock.cpp:67 (useClock = true)
+  OptimizationTools::optimizeNumericalParameters2(&tl, tl.getParameters(), 0, 0.000001, 10000, 0, 0, false, true, 2,
+                                                  OptimizationTools::OPTIMIZATION_NEWTON);
+  expectNear("T92 rooted clock-optimised -lnL", tl.getValue(), 71.2657, 1e-3);
 }
 
 // gaps are not allowed by the model: BadIntException like getInitValue
