@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="gtr_g4_dna_1M_64", choices=sorted(workload.CONFIGS))
     ap.add_argument("--patterns", type=int, default=None, help="override patterns per rank")
-    ap.add_argument("--cpu-sample", type=int, default=100_000, help="patterns in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=None, help="patterns in the CPU-baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -164,8 +164,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded counter-based simulation under the model, 1 pattern = 1 column)",
             "config": {
-                "workload": (f"{args.config}: GTR+G4 DNA, {P} patterns per GPU, {wl.et.n_tips}-taxon balanced "
-                             f"tree (unrooted, I={wl.et.n_internal})") if args.config.startswith("gtr") else args.config,
+                "workload": (f"{args.config}: {wl.models[0].name}{'+G%d' % wl.C if wl.C > 1 else ''} "
+                             f"{wl.alphabet.name}, {P} patterns per GPU, {wl.et.n_tips}-taxon balanced tree "
+                             f"({'rooted' if wl.model_of_node is not None else 'unrooted'}, I={wl.et.n_internal})"),
                 "patterns_per_gpu": P,
                 "taxa": wl.et.n_tips,
                 "internal_nodes": wl.et.n_internal,
@@ -192,7 +193,8 @@ def main():
             "setup_s": t_setup,
         }
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(wl, min(args.cpu_sample, P), args.cpu_reps)
+            ns = args.cpu_sample or workload.CONFIGS[args.config]["cpu_sample"]
+            rec["cpu_baseline"] = cpu_baseline(wl, min(ns, P), args.cpu_reps)
         prof = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(prof):
             try:

@@ -447,6 +447,39 @@ def lg08() -> Model:
     return Model("LG08", 20, Q, pi, V, Vinv, lam)
 
 
+STOP_CODONS = [i for i, a in enumerate(_STD_CODE_AA) if a == "*"]
+
+
+def yn98(kappa: float = 2.0, omega: float = 0.3, codon_freqs: Optional[np.ndarray] = None) -> Model:
+    """YN98 on the 64-codon state space, stop codons as null states
+    (Model/Codon/YN98.cpp:51-78 -> AbstractWordSubstitutionModel::fillBasicGenerator :355-390,
+    AbstractCodonSubstitutionModel::completeMatrices :174-190): for codons differing at
+    one position, Q_ij = (kappa if transition) * (omega if non-synonymous) * pi_j."""
+    pi = np.ones(64) if codon_freqs is None else np.array(codon_freqs, dtype=float)
+    pi[STOP_CODONS] = 0.0
+    pi /= pi.sum()
+    Q = np.zeros((64, 64))
+    ts = {(0, 2), (2, 0), (1, 3), (3, 1)}
+    for i in range(64):
+        for j in range(64):
+            if i == j or i in STOP_CODONS or j in STOP_CODONS:
+                continue
+            a = (i // 16, (i // 4) % 4, i % 4)
+            b = (j // 16, (j // 4) % 4, j % 4)
+            diff = [k for k in range(3) if a[k] != b[k]]
+            if len(diff) != 1:
+                continue
+            k = diff[0]
+            q = kappa if (a[k], b[k]) in ts else 1.0
+            if _STD_CODE_AA[i] != _STD_CODE_AA[j]:
+                q *= omega
+            Q[i, j] = q * pi[j]
+    np.fill_diagonal(Q, -Q.sum(axis=1))
+    Q /= -np.dot(np.diag(Q), pi)
+    V, Vinv, lam = reversible_eigen(Q, pi)
+    return Model("YN98", 64, Q, pi, V, Vinv, lam)
+
+
 # ---------------------------------------------------------------------------
 # Seeded simulation (NonHomogeneousSequenceSimulator::simulate semantics,
 # Simulation/NonHomogeneousSequenceSimulator.cpp:306-353): root ~ pi, class

@@ -95,18 +95,20 @@ def _gtr_cfg2() -> phylo.Model:
 
 CONFIGS = {
     # config 2: "DNA GTR+G4, 4 states, 1M synthetic site patterns, 64-taxon balanced tree, 1 MI355X"
-    "gtr_g4_dna_1M_64": dict(model="GTR", alpha=0.5, C=4, n_taxa=64, n_patterns=1_000_000, scaling=False),
+    "gtr_g4_dna_1M_64": dict(model="GTR", alpha=0.5, C=4, n_taxa=64, n_patterns=1_000_000, scaling=False, cpu_sample=100_000),
     # config 3: "Protein LG+G4, 20 states, 200k patterns, 256 taxa"
-    "lg08_g4_protein_200k_256": dict(model="LG08", alpha=0.5, C=4, n_taxa=256, n_patterns=200_000, scaling=True),
-    # config 5 (per GPU shard of the NH run): per-branch GTR, 512 taxa, rooted
-    "nh_gtr_g4_dna_2M_512": dict(model="NHGTR", alpha=1.0, C=4, n_taxa=512, n_patterns=2_000_000, scaling=True),
+    "lg08_g4_protein_200k_256": dict(model="LG08", alpha=0.5, C=4, n_taxa=256, n_patterns=200_000, scaling=True, cpu_sample=8_000),
+    # config 4: "Codon YN98, 61 states, 50k patterns, 128 taxa" (64 stored states, 3 null stops)
+    "yn98_codon_50k_128": dict(model="YN98", alpha=None, C=1, n_taxa=128, n_patterns=50_000, scaling=False, cpu_sample=2_000),
+    # config 5: per-branch GTR, 512 taxa, rooted; 2M patterns = 250k per GPU x 8 (weak-scaled per GPU)
+    "nh_gtr_g4_dna_2M_512": dict(model="NHGTR", alpha=1.0, C=4, n_taxa=512, n_patterns=250_000, scaling=True, cpu_sample=10_000),
 }
 
 
 def make_workload(name: str, n_patterns: Optional[int] = None, seed: int = 42) -> Workload:
     cfg = CONFIGS[name]
     tree = phylo.balanced_tree(cfg["n_taxa"], seed=seed)
-    rates, probs = phylo.gamma_rates(cfg["C"], cfg["alpha"])
+    rates, probs = phylo.gamma_rates(cfg["C"], cfg["alpha"]) if cfg["C"] > 1 else (np.ones(1), np.ones(1))
     P = cfg["n_patterns"] if n_patterns is None else n_patterns
     if cfg["model"] == "GTR":
         m = _gtr_cfg2()
@@ -116,6 +118,10 @@ def make_workload(name: str, n_patterns: Optional[int] = None, seed: int = 42) -
         m = phylo.lg08()
         et = phylo.engine_tree(tree, unroot=True)
         return Workload(name, et, [m], None, rates, probs, m.pi, phylo.PROTEIN, P, cfg["scaling"], True, seed)
+    if cfg["model"] == "YN98":
+        m = phylo.yn98(2.0, 0.3)
+        et = phylo.engine_tree(tree, unroot=True)
+        return Workload(name, et, [m], None, rates, probs, m.pi, phylo.CODON, P, cfg["scaling"], True, seed)
     if cfg["model"] == "NHGTR":
         et = phylo.engine_tree(tree, unroot=False)
         u = uniforms(seed, 7, 0, et.n_nodes)
