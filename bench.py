@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=None, help="patterns in the CPU-baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="lnl", choices=["lnl", "materialize", "levelwise"],
+                    help="lnl: fused traversal, interior partials kept in registers (recomputed on demand); "
+                         "materialize: fused traversal writing every partial; levelwise: one launch per level")
     return ap.parse_args()
 
 
@@ -112,7 +115,8 @@ def main():
     wl.n_patterns = P
     start, end = rank * P, (rank + 1) * P
     t_setup = time.time()
-    ev = workload.Evaluator(wl, device, start, end)
+    extra = {"lnl": plk.PLK_FLAG_LNL_ONLY, "materialize": 0, "levelwise": plk.PLK_FLAG_LEVELWISE}[args.mode]
+    ev = workload.Evaluator(wl, device, start, end, extra_flags=extra)
     t_setup = time.time() - t_setup
     units_step = P * wl.et.n_internal
 

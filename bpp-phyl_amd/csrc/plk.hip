@@ -6,10 +6,12 @@
 
 #include "../../include/plk.h"
 #include "plk_kernels.hpp"
+#include "plk_tree4.hpp"
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -78,6 +80,21 @@ struct plk_handle_s {
   std::vector<KOp> h_ops;
   std::vector<plk_op> last_ops;
   std::vector<int> last_level_start;
+  // fused 4-state traversal (plk_tree4.hpp)
+  double* wave_sums = nullptr;
+  TInstr* d_prog = nullptr;
+  size_t d_prog_cap = 0;
+  int32_t* d_frag = nullptr;
+  size_t d_frag_cap = 0;
+  std::vector<plk_op> prog_ops;           // op list the cached program was built from
+  bool prog_materialize = false;
+  bool prog_reduce = false;
+  std::vector<std::vector<int> > prog_tiers;  // fragment ids per tier
+  int prog_root = -1;                     // node whose lnL the program reduces (-1: none)
+  std::vector<char> materialized;         // per internal slot: partial present in HBM
+  std::vector<int> prog_mat_after;        // per internal slot after the cached program (-1 untouched)
+  bool fused_lnl_valid = false;
+  int fused_lnl_root = -1;
 };
 
 namespace {
@@ -255,7 +272,7 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   h->n_models = n_models;
   h->flags = flags;
   h->n_patterns = n_patterns;
-  h->n_tiles = (int)((n_patterns + kTile - 1) / kTile);
+  h->n_tiles = (int)(((n_patterns + 255) / 256) * 2);  // n_pad multiple of 256 (fused kernel blocks)
   h->n_pad = (int64_t)h->n_tiles * kTile;
   h->n_blocks = (int)((n_patterns + kRootBlock - 1) / kRootBlock);
   h->slot_stride = (int64_t)h->n_tiles * n_classes * n_states * kTile;
@@ -285,6 +302,8 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   if ((rc = dalloc(h, (void**)&h->pi, 64 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->site_lnl, (size_t)h->n_pad * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->block_sums, (size_t)h->n_blocks * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->wave_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return bail(rc);
+  h->materialized.assign(n_internal, 0);
   // default weights 1 for real patterns, 0 for padding
   std::vector<double> w(h->n_pad, 0.0);
   std::fill(w.begin(), w.begin() + n_patterns, 1.0);
@@ -304,7 +323,7 @@ int plk_destroy(plk_handle h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
-                  h->block_sums, h->d_ops, h->d_req};
+                  h->block_sums, h->d_ops, h->d_req, h->wave_sums, h->d_prog, h->d_frag};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (auto& e : h->events) {
@@ -484,10 +503,217 @@ int plk_get_pmatrix(plk_handle h, int branch, double* P) {
   return PLK_OK;
 }
 
-int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
-  if (!h || n_ops < 0 || (n_ops > 0 && !ops)) return fail(h, PLK_ERR_ARG, "bad op list");
-  if (n_ops == 0) return PLK_OK;
-  hipSetDevice(h->device);
+}  // extern "C"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Fused 4-state traversal: program builder + launches (kernel in plk_tree4.hpp).
+// ---------------------------------------------------------------------------
+constexpr int kTree4Levels(int C) { return C >= 4 ? 6 : 8; }
+
+bool tree4_supported(plk_handle h) {
+  return h->S == 4 && (h->C == 1 || h->C == 2 || h->C == 4) && !(h->flags & PLK_FLAG_LEVELWISE);
+}
+
+// Build the fragment programs for `ops` (validated, postorder).  Every produced node
+// is emitted inside exactly one fragment; a produced internal child deeper than the
+// register levels allow becomes the root of its own fragment (materialised and
+// LOADed by its parent's fragment).  Fragments are grouped into tiers so that a
+// fragment only reads partials written by earlier tiers.
+int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materialize, bool reduce) {
+  const int DM = kTree4Levels(h->C);
+  const int nt = h->n_tips;
+  std::vector<std::vector<int> > kids(h->n_nodes);
+  std::vector<char> produced(h->n_nodes, 0), is_child(h->n_nodes, 0);
+  for (int i = 0; i < n_ops; ++i) {
+    produced[ops[i].parent] = 1;
+    for (int k = 0; k < ops[i].n_children; ++k) {
+      kids[ops[i].parent].push_back(ops[i].child[k]);
+      is_child[ops[i].child[k]] = 1;
+    }
+  }
+  // produced internal children that have not been produced by an earlier op must
+  // be materialised already
+  std::vector<int> tops;
+  for (int i = 0; i < n_ops; ++i) {
+    const int n = ops[i].parent;
+    if (!is_child[n] && (tops.empty() || tops.back() != n)) tops.push_back(n);
+    for (int k = 0; k < ops[i].n_children; ++k) {
+      const int c = ops[i].child[k];
+      if (c >= nt && !produced[c] && !h->materialized[c - nt])
+        return fail(h, PLK_ERR_STATE, "child %d of node %d has no partial in HBM (not computed by this call)", c,
+                    n);
+    }
+  }
+  std::sort(tops.begin(), tops.end());
+  tops.erase(std::unique(tops.begin(), tops.end()), tops.end());
+  // assign fragments top-down
+  std::vector<int> frag_of(h->n_nodes, -1), depth(h->n_nodes, 0);
+  std::vector<int> frag_roots;
+  std::vector<int> stack;
+  for (int t : tops) {
+    frag_of[t] = (int)frag_roots.size();
+    frag_roots.push_back(t);
+    stack.push_back(t);
+  }
+  while (!stack.empty()) {
+    const int n = stack.back();
+    stack.pop_back();
+    for (int c : kids[n]) {
+      if (c < nt || !produced[c]) continue;
+      if (depth[n] + 1 <= DM - 1) {
+        frag_of[c] = frag_of[n];
+        depth[c] = depth[n] + 1;
+      } else {
+        frag_of[c] = (int)frag_roots.size();
+        frag_roots.push_back(c);
+        depth[c] = 0;
+      }
+      stack.push_back(c);
+    }
+  }
+  const int nf = (int)frag_roots.size();
+  // tiers: a fragment depends on the fragments of the cut nodes it loads
+  std::vector<int> tier(nf, 0);
+  bool changed = true;
+  while (changed) {
+    changed = false;
+    for (int n = nt; n < h->n_nodes; ++n) {
+      if (!produced[n]) continue;
+      for (int c : kids[n])
+        if (c >= nt && produced[c] && frag_of[c] != frag_of[n] && tier[frag_of[n]] < tier[frag_of[c]] + 1) {
+          tier[frag_of[n]] = tier[frag_of[c]] + 1;
+          changed = true;
+        }
+    }
+  }
+  // emit
+  std::vector<TInstr> prog;
+  std::vector<int32_t> start(nf);
+  const int root_reduce = (reduce && tops.size() == 1) ? tops[0] : -1;
+  std::function<void(int, int)> emit = [&](int n, int d) {
+    prog.push_back({T_ENTER, d, 0, 0});
+    for (int c : kids[n]) {
+      if (c < nt) {
+        prog.push_back({T_TIP, d, c, c});
+      } else if (produced[c] && frag_of[c] == frag_of[n]) {
+        emit(c, d + 1);
+        prog.push_back({T_EXIT, d, materialize ? c - nt : -1, c});
+      } else {
+        prog.push_back({T_LOAD, d, c - nt, c});
+      }
+    }
+  };
+  for (int f = 0; f < nf; ++f) {
+    start[f] = (int32_t)prog.size();
+    const int r = frag_roots[f];
+    emit(r, 0);
+    const bool cut = r != root_reduce && std::find(tops.begin(), tops.end(), r) == tops.end();
+    prog.push_back({T_ROOT, 0, (materialize || cut) ? r - nt : -1, r == root_reduce ? 1 : 0});
+    prog.push_back({T_END, 0, 0, 0});
+  }
+  int rc = ensure_cap(h, (void**)&h->d_prog, &h->d_prog_cap, prog.size() * sizeof(TInstr));
+  if (rc) return rc;
+  rc = ensure_cap(h, (void**)&h->d_frag, &h->d_frag_cap, std::max(nf, 1) * sizeof(int32_t));
+  if (rc) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->d_prog, prog.data(), prog.size() * sizeof(TInstr), hipMemcpyHostToDevice, h->stream));
+  // fragments sorted by tier so that each tier is a contiguous range of blockIdx.y
+  std::vector<int> order(nf);
+  for (int f = 0; f < nf; ++f) order[f] = f;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return tier[x] < tier[y]; });
+  std::vector<int32_t> start_sorted(nf);
+  h->prog_tiers.clear();
+  for (int i = 0; i < nf; ++i) {
+    start_sorted[i] = start[order[i]];
+    if (h->prog_tiers.empty() || tier[order[i]] != tier[order[i - 1]]) h->prog_tiers.push_back({});
+    h->prog_tiers.back().push_back(i);
+  }
+  HIPCHK(h, hipMemcpyAsync(h->d_frag, start_sorted.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // host staging vectors go out of scope
+  h->prog_ops.assign(ops, ops + n_ops);
+  h->prog_materialize = materialize;
+  h->prog_reduce = reduce;
+  h->prog_root = root_reduce;
+  // bookkeeping: which partials will be in HBM after the launch (-1: untouched)
+  h->prog_mat_after.assign(h->n_internal, -1);
+  for (int n = nt; n < h->n_nodes; ++n)
+    if (produced[n]) {
+      const bool cut = frag_of[n] >= 0 && frag_roots[frag_of[n]] == n;
+      h->prog_mat_after[n - nt] = (materialize || (cut && n != root_reduce)) ? 1 : 0;
+      h->materialized[n - nt] = (char)h->prog_mat_after[n - nt];
+    }
+  return PLK_OK;
+}
+
+template <int C, int DM>
+void launch_tree4_C(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
+  if (h->flags & PLK_FLAG_SCALING)
+    tree4_kernel<C, DM, true><<<grid, 256, lds, h->stream>>>(a);
+  else
+    tree4_kernel<C, DM, false><<<grid, 256, lds, h->stream>>>(a);
+}
+
+int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
+  const bool materialize = !(h->flags & PLK_FLAG_LNL_ONLY);
+  const bool reduce = h->pi_set && h->rates_set;
+  const bool same = h->prog_ops.size() == (size_t)n_ops && h->prog_materialize == materialize &&
+                    h->prog_reduce == reduce &&
+                    std::memcmp(h->prog_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
+  if (!same) {
+    int rc = build_tree4_program(h, ops, n_ops, materialize, reduce);
+    if (rc) return rc;
+  } else {
+    for (size_t i = 0; i < h->prog_mat_after.size(); ++i)
+      if (h->prog_mat_after[i] >= 0) h->materialized[i] = (char)h->prog_mat_after[i];
+  }
+  if (!h->table_set) return fail(h, PLK_ERR_STATE, "code table not set (plk_set_code_table)");
+  TreeArgs a;
+  a.prog = h->d_prog;
+  a.partials = h->partials;
+  a.scale = h->scale;
+  a.codes = h->codes;
+  a.pmats = h->pmats;
+  a.init = h->code_table;
+  a.weights = h->weights;
+  a.pi = h->pi;
+  a.probs = h->probs;
+  a.site_lnl = h->site_lnl;
+  a.wave_sums = h->wave_sums;
+  a.slot_stride = h->slot_stride;
+  a.n_pad = h->n_pad;
+  a.n_patterns = h->n_patterns;
+  a.n_codes = h->n_codes;
+  a.guard = (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0;
+  const size_t lds = (size_t)h->n_codes * 4 * sizeof(double);
+  int first = 0;
+  for (const auto& t : h->prog_tiers) {
+    a.frag_start = h->d_frag + first;
+    dim3 grid((unsigned)(h->n_pad / 256), (unsigned)t.size());
+    EventPair ev;
+    if (h->timing) {
+      ev = get_events(h, 0);
+      hipEventRecord(ev.a, h->stream);
+    }
+    switch (h->C) {
+      case 1: launch_tree4_C<1, kTree4Levels(1)>(h, a, grid, lds); break;
+      case 2: launch_tree4_C<2, kTree4Levels(2)>(h, a, grid, lds); break;
+      case 4: launch_tree4_C<4, kTree4Levels(4)>(h, a, grid, lds); break;
+    }
+    HIPCHK(h, hipGetLastError());
+    if (h->timing) {
+      hipEventRecord(ev.b, h->stream);
+      h->events.push_back(ev);
+    }
+    h->n_launches++;
+    first += (int)t.size();
+  }
+  h->fused_lnl_valid = h->prog_root >= 0;
+  h->fused_lnl_root = h->prog_root;
+  return PLK_OK;
+}
+
+int update_levelwise(plk_handle h, const plk_op* ops, int n_ops) {
   // Validate and level the ops: level(op) = 1 + max(level of the op that last
   // wrote each internal child in this call, level of the last writer of parent).
   std::vector<int> writer_level(h->n_nodes, -1);
@@ -583,12 +809,69 @@ int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
     }
     h->n_launches++;
   }
+  for (int i = 0; i < n_ops; ++i) h->materialized[ops[i].parent - h->n_tips] = 1;
+  h->fused_lnl_valid = false;
   return PLK_OK;
+}
+
+int validate_ops(plk_handle h, const plk_op* ops, int n_ops) {
+  std::vector<char> done(h->n_nodes, 0);
+  for (int i = 0; i < n_ops; ++i) {
+    const plk_op& o = ops[i];
+    if (o.parent < h->n_tips || o.parent >= h->n_nodes)
+      return fail(h, PLK_ERR_ARG, "op %d: parent %d is not an internal node", i, o.parent);
+    if (o.n_children < 1 || o.n_children > 3) return fail(h, PLK_ERR_ARG, "op %d: %d children", i, o.n_children);
+    if ((o.flags & PLK_OP_ACCUMULATE) && !done[o.parent] && !h->materialized[o.parent - h->n_tips])
+      return fail(h, PLK_ERR_STATE, "op %d: accumulate into node %d that has no partial", i, o.parent);
+    for (int k = 0; k < o.n_children; ++k) {
+      const int c = o.child[k];
+      if (c < 0 || c >= h->n_nodes || c == o.parent) return fail(h, PLK_ERR_ARG, "op %d: bad child %d", i, c);
+      if (!h->pmat_valid[c]) return fail(h, PLK_ERR_STATE, "op %d: transition matrix of branch %d not set", i, c);
+      if (c < h->n_tips && !h->tip_set[c]) return fail(h, PLK_ERR_STATE, "op %d: tip %d has no codes", i, c);
+    }
+    done[o.parent] = 1;
+  }
+  return PLK_OK;
+}
+
+// An op list is fusable when every ACCUMULATE op continues the node of the op
+// just before it (the polytomy split produced by the host) -- then the program
+// treats the node as one multi-child node.
+bool fusable(const plk_op* ops, int n_ops) {
+  for (int i = 0; i < n_ops; ++i)
+    if ((ops[i].flags & PLK_OP_ACCUMULATE) && (i == 0 || ops[i - 1].parent != ops[i].parent)) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
+  if (!h || n_ops < 0 || (n_ops > 0 && !ops)) return fail(h, PLK_ERR_ARG, "bad op list");
+  if (n_ops == 0) return PLK_OK;
+  hipSetDevice(h->device);
+  int rc = validate_ops(h, ops, n_ops);
+  if (rc) return rc;
+  if (tree4_supported(h) && fusable(ops, n_ops)) return update_tree4(h, ops, n_ops);
+  return update_levelwise(h, ops, n_ops);
 }
 
 int plk_get_partials(plk_handle h, int node, double* out) {
   if (!h || !out || node < h->n_tips || node >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad internal node %d", node);
   hipSetDevice(h->device);
+  if (!h->materialized[node - h->n_tips]) {
+    // lnL-only traversal kept this partial in registers: re-run the last traversal
+    // materialising every node (same arithmetic, so the values are identical).
+    if (h->prog_ops.empty()) return fail(h, PLK_ERR_STATE, "node %d has no partial yet", node);
+    const unsigned saved = h->flags;
+    const std::vector<plk_op> ops = h->prog_ops;
+    h->flags &= ~(unsigned)PLK_FLAG_LNL_ONLY;
+    const int rc = update_tree4(h, ops.data(), (int)ops.size());
+    h->flags = saved;
+    if (rc) return rc;
+    if (!h->materialized[node - h->n_tips]) return fail(h, PLK_ERR_STATE, "node %d has no partial", node);
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   std::vector<double> buf(h->slot_stride);
   HIPCHK(h, hipMemcpy(buf.data(), h->partials + (size_t)(node - h->n_tips) * h->slot_stride,
@@ -601,10 +884,37 @@ int plk_get_partials(plk_handle h, int node, double* out) {
   return PLK_OK;
 }
 
+static int launch_root(plk_handle h, int root);
+
 int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums) {
   if (!h || root < h->n_tips || root >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad root node %d", root);
   if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
   hipSetDevice(h->device);
+  if (h->fused_lnl_valid && h->fused_lnl_root == root) {
+    // the fused traversal already reduced the root: only the block sums remain
+    const int n_waves = (int)((h->n_patterns + 63) / 64);
+    wave_sums_to_blocks<<<(h->n_blocks + 255) / 256, 256, 0, h->stream>>>(h->wave_sums, h->block_sums, n_waves,
+                                                                          h->n_blocks);
+    HIPCHK(h, hipGetLastError());
+  } else {
+    if (!h->materialized[root - h->n_tips]) return fail(h, PLK_ERR_STATE, "root %d has no partial", root);
+    int rc = launch_root(h, root);
+    if (rc) return rc;
+  }
+  std::vector<double> bs(h->n_blocks);
+  HIPCHK(h, hipMemcpyAsync(bs.data(), h->block_sums, bs.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  if (site_lnl)
+    HIPCHK(h, hipMemcpyAsync(site_lnl, h->site_lnl, (size_t)h->n_patterns * sizeof(double), hipMemcpyDeviceToHost,
+                             h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  double s = 0.0;
+  for (double v : bs) s += v;  // fixed order: block 0, 1, 2, ...
+  if (lnl) *lnl = s;
+  if (block_sums) std::memcpy(block_sums, bs.data(), bs.size() * sizeof(double));
+  return PLK_OK;
+}
+
+static int launch_root(plk_handle h, int root) {
   RootArgs a;
   a.partials = h->partials + (size_t)(root - h->n_tips) * h->slot_stride;
   a.scale = h->scale ? h->scale + (size_t)(root - h->n_tips) * h->n_pad : nullptr;
@@ -628,16 +938,6 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
     hipEventRecord(ev.b, h->stream);
     h->events.push_back(ev);
   }
-  std::vector<double> bs(h->n_blocks);
-  HIPCHK(h, hipMemcpyAsync(bs.data(), h->block_sums, bs.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-  if (site_lnl)
-    HIPCHK(h, hipMemcpyAsync(site_lnl, h->site_lnl, (size_t)h->n_patterns * sizeof(double), hipMemcpyDeviceToHost,
-                             h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  double s = 0.0;
-  for (double v : bs) s += v;  // fixed order: block 0, 1, 2, ...
-  if (lnl) *lnl = s;
-  if (block_sums) std::memcpy(block_sums, bs.data(), bs.size() * sizeof(double));
   return PLK_OK;
 }
 

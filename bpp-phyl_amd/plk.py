@@ -19,6 +19,8 @@ LIB_PATH = os.path.join(_HERE, "libplk.so")
 PLK_OK = 0
 PLK_FLAG_SCALING = 1
 PLK_FLAG_NONNEG_GUARD = 2
+PLK_FLAG_LNL_ONLY = 4
+PLK_FLAG_LEVELWISE = 8
 PLK_DERIV_P, PLK_DERIV_DP, PLK_DERIV_D2P = 1, 2, 4
 PLK_OP_ACCUMULATE = 1
 

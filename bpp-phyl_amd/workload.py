@@ -139,11 +139,12 @@ def make_workload(name: str, n_patterns: Optional[int] = None, seed: int = 42) -
 class Evaluator:
     """One libplk engine holding the patterns [start, end) of a workload."""
 
-    def __init__(self, wl: Workload, device: int, start: int, end: int, states: Optional[np.ndarray] = None):
+    def __init__(self, wl: Workload, device: int, start: int, end: int, states: Optional[np.ndarray] = None,
+                 extra_flags: int = 0):
         self.wl = wl
         self.start, self.end = start, end
         et = wl.et
-        flags = (plk.PLK_FLAG_SCALING if wl.scaling else 0) | (plk.PLK_FLAG_NONNEG_GUARD if wl.guard else 0)
+        flags = (plk.PLK_FLAG_SCALING if wl.scaling else 0) | (plk.PLK_FLAG_NONNEG_GUARD if wl.guard else 0) | extra_flags
         self.eng = plk.Engine(device, wl.S, wl.C, end - start, et.n_tips, et.n_internal, len(wl.models), flags)
         self.eng.set_code_table(wl.alphabet.init_table)
         st = wl.simulate(start, end) if states is None else states

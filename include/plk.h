@@ -74,7 +74,12 @@ enum {
   PLK_FLAG_NONNEG_GUARD = 1u << 1 /* homogeneous root guards: drop terms <= 0
                                     (RHomogeneousTreeLikelihood.cpp:197-198,212-213);
                                     without it the NH rule clamps l<0 -> 0
-                                    (RNonHomogeneousTreeLikelihood.cpp:206) */
+                                    (RNonHomogeneousTreeLikelihood.cpp:206) */,
+  PLK_FLAG_LNL_ONLY = 1u << 2,   /* 4-state fused traversal keeps interior partials in
+                                    registers and materialises only fragment roots; other
+                                    partials are recomputed on demand by plk_get_partials */
+  PLK_FLAG_LEVELWISE = 1u << 3   /* force one launch per tree level (every child partial
+                                    re-read from HBM); for A/B measurements */
 };
 
 /* plk_update_pmatrices deriv_mask */

@@ -346,3 +346,60 @@ def test_config2_full_size_properties():
     e2 = workload.Evaluator(wl, 0, cut, wl.n_patterns)
     b2 = e2.step()[2]
     assert np.array_equal(np.concatenate([b1, b2]), blocks)
+
+
+# ---------------------------------------------------------------- fused 4-state traversal modes
+
+MODES = {"materialize": 0, "lnl_only": plk.PLK_FLAG_LNL_ONLY, "levelwise": plk.PLK_FLAG_LEVELWISE}
+
+
+def _caterpillar(n, seed=3):
+    rng = np.random.default_rng(seed)
+    s = "t0:%.4f" % rng.uniform(0.02, 0.2)
+    for i in range(1, n - 1):
+        s = "(%s,t%d:%.4f):%.4f" % (s, i, rng.uniform(0.02, 0.2), rng.uniform(0.02, 0.2))
+    return phylo.Tree.from_newick("(%s,t%d:%.4f);" % (s, n - 1, rng.uniform(0.02, 0.2)))
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
+@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling", [
+    (4, "balanced64", 3000, False), (1, "balanced64", 777, False), (2, "balanced64", 1000, True),
+    (4, "caterpillar40", 900, False), (4, "caterpillar40", 900, True), (1, "caterpillar40", 300, True),
+    (4, "balanced300", 513, True)])
+def test_s4_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling):
+    if tree_kind.startswith("balanced"):
+        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=17, lo=0.05, hi=0.4)
+    else:
+        tree = _caterpillar(int(tree_kind[11:]))
+    et = phylo.engine_tree(tree)
+    rng = np.random.default_rng(C * 7 + n_patterns)
+    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
+    rates, probs = phylo.gamma_rates(C, 0.5) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, scaling, True, 5)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    mask = rng.random(states.shape) < 0.05
+    states[mask] = rng.integers(4, 15, size=mask.sum())       # ambiguity codes
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, 4, C, n_patterns, states, phylo.DNA.init_table, rates, probs, m.pi, [m], flags=flags)
+    lnl, site, blocks = run_engine(eng, et)
+    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m], scaling=scaling)
+    check(lnl, site, lo, so)
+    # partials of an interior node are available in every mode (recomputed on demand)
+    p, ch = et.ops[len(et.ops) // 2]
+    L = eng.get_partials(p)
+    assert np.all(np.isfinite(L)) and L.shape == (n_patterns, C, 4)
+    # a second evaluation is bitwise identical
+    lnl2, site2, _ = run_engine(eng, et)
+    assert lnl2 == lnl and np.array_equal(site2, site)
+
+
+def test_fused_partials_equal_levelwise():
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 24, 1000, seed=31)
+    outs = []
+    for mode in ("materialize", "levelwise", "lnl_only"):
+        eng = engine_for(et, 4, 4, 1000, states, alph.init_table, rates, probs, m.pi, [m],
+                         flags=plk.PLK_FLAG_NONNEG_GUARD | MODES[mode])
+        run_engine(eng, et)
+        outs.append(np.stack([eng.get_partials(p) for p, _ in et.ops]))
+    assert np.allclose(outs[0], outs[1], rtol=1e-13, atol=0)
+    assert np.array_equal(outs[0], outs[2])
