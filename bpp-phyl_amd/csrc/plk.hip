@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <functional>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -510,7 +511,16 @@ namespace {
 // ---------------------------------------------------------------------------
 // Fused 4-state traversal: program builder + launches (kernel in plk_tree4.hpp).
 // ---------------------------------------------------------------------------
-constexpr int kTree4Levels(int C) { return C >= 4 ? 6 : 8; }
+constexpr int kTree4Levels(int CW) { return CW >= 4 ? 6 : 8; }
+
+// classes per wave of the fused kernel (PLK_TREE4_CW overrides; default 1 = one
+// wave per rate class, the smallest register footprint and the highest occupancy)
+int tree4_cw(plk_handle h) {
+  int cw = 1;
+  if (const char* e = std::getenv("PLK_TREE4_CW")) cw = std::atoi(e);
+  if (cw != 1 && cw != 2 && cw != 4) cw = 1;
+  return std::min(cw, h->C);
+}
 
 bool tree4_supported(plk_handle h) {
   return h->S == 4 && (h->C == 1 || h->C == 2 || h->C == 4) && !(h->flags & PLK_FLAG_LEVELWISE);
@@ -522,7 +532,7 @@ bool tree4_supported(plk_handle h) {
 // LOADed by its parent's fragment).  Fragments are grouped into tiers so that a
 // fragment only reads partials written by earlier tiers.
 int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materialize, bool reduce) {
-  const int DM = kTree4Levels(h->C);
+  const int DM = kTree4Levels(tree4_cw(h));
   const int nt = h->n_tips;
   std::vector<std::vector<int> > kids(h->n_nodes);
   std::vector<char> produced(h->n_nodes, 0), is_child(h->n_nodes, 0);
@@ -646,12 +656,14 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   return PLK_OK;
 }
 
-template <int C, int DM>
-void launch_tree4_C(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
+template <int CW>
+void launch_tree4_cw(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
+  constexpr int DM = kTree4Levels(CW);
+  const dim3 block(64 * (h->C / CW));
   if (h->flags & PLK_FLAG_SCALING)
-    tree4_kernel<C, DM, true><<<grid, 256, lds, h->stream>>>(a);
+    tree4_kernel<CW, DM, true><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
   else
-    tree4_kernel<C, DM, false><<<grid, 256, lds, h->stream>>>(a);
+    tree4_kernel<CW, DM, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
 }
 
 int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
@@ -685,20 +697,25 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   a.n_patterns = h->n_patterns;
   a.n_codes = h->n_codes;
   a.guard = (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0;
-  const size_t lds = (size_t)h->n_codes * 4 * sizeof(double);
+  a.n_tips = h->n_tips;
+  a.C = h->C;
+  a.stage_codes = (h->n_tips * 64 <= 64 * 1024) ? 1 : 0;
+  const size_t lds = (size_t)((h->n_codes * 4 + 1) & ~1) * sizeof(double) + kTreeMaxWaves * 64 * sizeof(double) +
+                     (a.stage_codes ? (size_t)h->n_tips * 64 : 0);
+  const int cw = tree4_cw(h);
   int first = 0;
   for (const auto& t : h->prog_tiers) {
     a.frag_start = h->d_frag + first;
-    dim3 grid((unsigned)(h->n_pad / 256), (unsigned)t.size());
+    dim3 grid((unsigned)(h->n_pad / 64), (unsigned)t.size());
     EventPair ev;
     if (h->timing) {
       ev = get_events(h, 0);
       hipEventRecord(ev.a, h->stream);
     }
-    switch (h->C) {
-      case 1: launch_tree4_C<1, kTree4Levels(1)>(h, a, grid, lds); break;
-      case 2: launch_tree4_C<2, kTree4Levels(2)>(h, a, grid, lds); break;
-      case 4: launch_tree4_C<4, kTree4Levels(4)>(h, a, grid, lds); break;
+    switch (cw) {
+      case 1: launch_tree4_cw<1>(h, a, grid, lds); break;
+      case 2: launch_tree4_cw<2>(h, a, grid, lds); break;
+      case 4: launch_tree4_cw<4>(h, a, grid, lds); break;
     }
     HIPCHK(h, hipGetLastError());
     if (h->timing) {

@@ -1,22 +1,26 @@
 // plk_tree4.hpp -- fused postorder traversal for 4-state models (gfx950).
 //
-// One lane = one site pattern, one wave = 64 consecutive patterns.  A wave walks a
-// small "tree program" (postorder events, wave-uniform, read with scalar loads) and
-// keeps the pending product of every open ancestor in registers: level d of the
-// current root-to-node path owns acc[d][C*4].  All register indices are compile
-// time constants (the runtime level selects a template instance through a switch),
-// so nothing spills.  A child's contribution is multiplied into its parent's level
-// as soon as the child completes, in the reference's son order:
+// A workgroup owns 64 consecutive site patterns (one per lane) and C/CW waves: wave
+// w evaluates rate classes [w*CW, (w+1)*CW) for those patterns.  Every wave walks
+// the same small "tree program" (postorder events, wave-uniform, fetched one word
+// ahead with scalar loads) and keeps the pending product of every open ancestor in
+// registers: level d of the current root-to-node path owns acc[d][CW*4].  Register
+// indices are compile-time constants (the runtime level selects a template instance
+// through a switch), so nothing spills, and the per-wave footprint is small enough
+// for several waves per SIMD to hide the scalar-load and LDS latencies.  A child's
+// contribution is multiplied into its parent's level as soon as the child completes,
+// in the reference's son order:
 //     L_node[c][x] = prod_son sum_y P_son[c][x][y] L_son[c][y]
 // (Likelihood/RHomogeneousTreeLikelihood.cpp:839-861).
 //
-// Compared with one launch per tree level (partials_s4_kernel), child partials are
+// Compared with one launch per tree level (partials_s4_kernel) child partials are
 // never re-read from HBM: a materialising traversal only WRITES each internal
-// partial once (half the HBM traffic), and an lnL-only traversal writes nothing but
-// the fragment roots.  Tips enter as uint8 codes through the getInitValue table
-// (n_codes x 4 in LDS), which covers ambiguity codes exactly like the reference's
-// dense leaf vectors.  The root reduction (RHomogeneousTreeLikelihood.cpp:162-216)
-// is fused into the program's ROOT event.
+// partial once, an lnL-only traversal writes nothing but fragment roots.  Tips enter
+// as uint8 codes (staged in LDS) through the getInitValue table, which covers
+// ambiguity codes exactly like the reference's dense leaf vectors.  Power-of-two
+// rescaling uses the max over ALL classes of a pattern (waves exchange their maxima
+// through LDS), i.e. the same rule as the levelwise kernels and the oracle.  The
+// root reduction (RHomogeneousTreeLikelihood.cpp:162-216) is fused into ROOT.
 #pragma once
 
 #include "plk_kernels.hpp"
@@ -50,20 +54,20 @@ struct TreeArgs {
   int64_t n_pad;
   int64_t n_patterns;
   int32_t n_codes;
+  int32_t n_tips;
+  int32_t C;
   int32_t guard;
+  int32_t stage_codes;        // 1: tip codes staged in LDS
 };
 
-template <int C>
-struct Acc {
-  double v[C * 4];
-};
+constexpr int kTreeMaxWaves = 4;
 
-// acc[D][c][x] *= sum_y P[c][x][y] * src[c][y]
-template <int C>
-__device__ __forceinline__ void contribute(double (&dst)[C * 4], const double (&src)[C * 4],
+// dst[c][x] *= sum_y P[c][x][y] * src[c][y]   (P = this wave's classes, 16 doubles each)
+template <int CW>
+__device__ __forceinline__ void contribute(double (&dst)[CW * 4], const double (&src)[CW * 4],
                                            const double* __restrict__ P) {
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
+  for (int c = 0; c < CW; ++c) {
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const double* Px = P + (c * 4 + x) * 4;
@@ -76,73 +80,107 @@ __device__ __forceinline__ void contribute(double (&dst)[C * 4], const double (&
   }
 }
 
-// Exact power-of-two rescaling of one pattern's partial (max < 2^-256 -> x 2^256).
-template <int C>
-__device__ __forceinline__ void rescale(double (&v)[C * 4], int& cnt) {
+// Joint (all-class) exact power-of-two rescaling of one pattern's partial.
+template <int CW>
+__device__ __forceinline__ void rescale(double (&v)[CW * 4], int& cnt, double* xmax, int nw) {
   double m = 0.0;
 #pragma unroll
-  for (int i = 0; i < C * 4; ++i) m = fmax(m, v[i]);
+  for (int i = 0; i < CW * 4; ++i) m = fmax(m, v[i]);
+  if (nw > 1) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    xmax[w * 64 + lane] = m;
+    __syncthreads();
+    m = 0.0;
+    for (int k = 0; k < nw; ++k) m = fmax(m, xmax[k * 64 + lane]);
+    __syncthreads();
+  }
   if (m > 0.0 && m < kScaleThr) {
 #pragma unroll
-    for (int i = 0; i < C * 4; ++i) v[i] *= kScaleUp;
+    for (int i = 0; i < CW * 4; ++i) v[i] *= kScaleUp;
     cnt += 1;
   }
 }
 
-template <int C, bool SCALE>
-__device__ __forceinline__ void store_partial(const TreeArgs& a, int slot, int64_t p, const double (&v)[C * 4],
-                                              int cnt) {
+template <int CW, bool SCALE>
+__device__ __forceinline__ void store_partial(const TreeArgs& a, int slot, int64_t p, int c0,
+                                              const double (&v)[CW * 4], int cnt) {
   const int64_t tile = p >> 7, q = p & (kTile - 1);
-  double* dst = a.partials + (size_t)slot * a.slot_stride + tile * (C * 4 * kTile) + q;
+  double* dst = a.partials + (size_t)slot * a.slot_stride + tile * ((int64_t)a.C * 4 * kTile) + (size_t)c0 * 4 * kTile + q;
 #pragma unroll
-  for (int i = 0; i < C * 4; ++i) __builtin_nontemporal_store(v[i], dst + (size_t)i * kTile);
-  if (SCALE) a.scale[(size_t)slot * a.n_pad + p] = cnt;
+  for (int i = 0; i < CW * 4; ++i) __builtin_nontemporal_store(v[i], dst + (size_t)i * kTile);
+  if (SCALE && c0 == 0) a.scale[(size_t)slot * a.n_pad + p] = cnt;
 }
 
-template <int C, int DM, bool SCALE>
-__global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double init_lds[];  // [n_codes][4]
+// prog / frag_start / pmats are separate __restrict__ kernel arguments: the compiler
+// can then prove they are never written in the kernel and fetches the wave-uniform
+// program words and P(t) entries with scalar loads into SGPRs.
+template <int CW, int DM, bool SCALE>
+__global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a, const TInstr* __restrict__ prog,
+                                                    const int32_t* __restrict__ frag_start,
+                                                    const double* __restrict__ pmats) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  // LDS: init table [n_codes][4] | class exchange [4][64] | codes [n_tips][64] (if staged)
+  double* init_lds = lds;
+  double* xch = lds + ((a.n_codes * 4 + 1) & ~1);
+  uint8_t* code_lds = reinterpret_cast<uint8_t*>(xch + kTreeMaxWaves * 64);
+  const int nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63;
+  // wave index as a scalar: keeps P(t) addresses uniform -> s_load into SGPRs
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = w * CW;
+  const int64_t p0 = (int64_t)blockIdx.x * 64;
+  const int64_t p = p0 + lane;
   for (int i = threadIdx.x; i < a.n_codes * 4; i += blockDim.x) init_lds[i] = a.init[i];
+  if (a.stage_codes) {
+    // 16 B per thread: tip t, bytes [16*j, 16*j + 16) of the 64-pattern row
+    for (int i = threadIdx.x; i < a.n_tips * 4; i += blockDim.x) {
+      const int t = i >> 2, j = i & 3;
+      reinterpret_cast<uint4*>(code_lds)[i] =
+          *reinterpret_cast<const uint4*>(a.codes + (size_t)t * a.n_pad + p0 + 16 * j);
+    }
+  }
   __syncthreads();
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // pattern (< n_pad always)
-  double acc[DM][C * 4];
+
+  double acc[DM][CW * 4];
   int cnt[DM];
 #pragma unroll
   for (int d = 0; d < DM; ++d) cnt[d] = 0;
-  const TInstr* pc = a.prog + a.frag_start[blockIdx.y];
-
-  for (;;) {
-    const TInstr in = *pc++;
-    if (in.op == T_END) break;
+  const TInstr* __restrict__ pc = prog + frag_start[blockIdx.y];
+  TInstr in = pc[0];
+  while (in.op != T_END) {
+    const TInstr nx = pc[1];  // fetched one word ahead
+    ++pc;
+    const double* __restrict__ P = pmats + ((size_t)in.b * a.C + c0) * 16;
     switch (in.op) {
       case T_ENTER:
         switch (in.d) {
-#define PLK_ENTER(D)                                          \
-  case D:                                                     \
-    _Pragma("unroll") for (int i = 0; i < C * 4; ++i) acc[D][i] = 1.0; \
-    cnt[D] = 0;                                               \
+#define PLK_ENTER(D)                                                           \
+  case D:                                                                      \
+    if (D < DM) {                                                              \
+      _Pragma("unroll") for (int i = 0; i < CW * 4; ++i) acc[D < DM ? D : 0][i] = 1.0; \
+      cnt[D < DM ? D : 0] = 0;                                                 \
+    }                                                                          \
     break;
           PLK_ENTER(0) PLK_ENTER(1) PLK_ENTER(2) PLK_ENTER(3) PLK_ENTER(4) PLK_ENTER(5) PLK_ENTER(6) PLK_ENTER(7)
 #undef PLK_ENTER
         }
         break;
       case T_TIP: {
-        const int code = a.codes[(size_t)in.a * a.n_pad + p];
-        double src[C * 4];
-        const double* iv = init_lds + code * 4;
-        const double i0 = iv[0], i1 = iv[1], i2 = iv[2], i3 = iv[3];
+        const int code = a.stage_codes ? code_lds[in.a * 64 + lane] : a.codes[(size_t)in.a * a.n_pad + p];
+        const double2* iv = reinterpret_cast<const double2*>(init_lds + code * 4);
+        const double2 i01 = iv[0], i23 = iv[1];
+        double src[CW * 4];
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          src[c * 4 + 0] = i0;
-          src[c * 4 + 1] = i1;
-          src[c * 4 + 2] = i2;
-          src[c * 4 + 3] = i3;
+        for (int c = 0; c < CW; ++c) {
+          src[c * 4 + 0] = i01.x;
+          src[c * 4 + 1] = i01.y;
+          src[c * 4 + 2] = i23.x;
+          src[c * 4 + 3] = i23.y;
         }
-        const double* __restrict__ P = a.pmats + (size_t)in.b * (C * 16);
         switch (in.d) {
-#define PLK_TIP(D) \
-  case D:          \
-    if (D < DM) contribute<C>(acc[D < DM ? D : 0], src, P); \
+#define PLK_TIP(D)                                                  \
+  case D:                                                           \
+    if (D < DM) contribute<CW>(acc[D < DM ? D : 0], src, P);        \
     break;
           PLK_TIP(0) PLK_TIP(1) PLK_TIP(2) PLK_TIP(3) PLK_TIP(4) PLK_TIP(5) PLK_TIP(6) PLK_TIP(7)
 #undef PLK_TIP
@@ -151,19 +189,19 @@ __global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a) {
       }
       case T_LOAD: {
         const int64_t tile = p >> 7, q = p & (kTile - 1);
-        const double* L = a.partials + (size_t)in.a * a.slot_stride + tile * (C * 4 * kTile) + q;
-        double src[C * 4];
+        const double* L = a.partials + (size_t)in.a * a.slot_stride + tile * ((int64_t)a.C * 4 * kTile) +
+                          (size_t)c0 * 4 * kTile + q;
+        double src[CW * 4];
 #pragma unroll
-        for (int i = 0; i < C * 4; ++i) src[i] = L[(size_t)i * kTile];
-        int sc = SCALE ? a.scale[(size_t)in.a * a.n_pad + p] : 0;
-        const double* __restrict__ P = a.pmats + (size_t)in.b * (C * 16);
+        for (int i = 0; i < CW * 4; ++i) src[i] = L[(size_t)i * kTile];
+        const int sc = SCALE ? a.scale[(size_t)in.a * a.n_pad + p] : 0;
         switch (in.d) {
-#define PLK_LOAD(D)                                            \
-  case D:                                                      \
-    if (D < DM) {                                              \
-      contribute<C>(acc[D < DM ? D : 0], src, P);              \
-      if (SCALE) cnt[D < DM ? D : 0] += sc;                    \
-    }                                                          \
+#define PLK_LOAD(D)                                              \
+  case D:                                                        \
+    if (D < DM) {                                                \
+      contribute<CW>(acc[D < DM ? D : 0], src, P);               \
+      if (SCALE) cnt[D < DM ? D : 0] += sc;                      \
+    }                                                            \
     break;
           PLK_LOAD(0) PLK_LOAD(1) PLK_LOAD(2) PLK_LOAD(3) PLK_LOAD(4) PLK_LOAD(5) PLK_LOAD(6) PLK_LOAD(7)
 #undef PLK_LOAD
@@ -172,18 +210,17 @@ __global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a) {
       }
       case T_EXIT: {
         // child complete at level d+1: rescale, optionally store, multiply into level d
-        const double* __restrict__ P = a.pmats + (size_t)in.b * (C * 16);
         switch (in.d) {
-#define PLK_EXIT(D)                                                                  \
-  case D:                                                                            \
-    if (D + 1 < DM) {                                                                \
-      constexpr int K = (D + 1 < DM) ? D + 1 : 0;                                    \
-      constexpr int J = (D + 1 < DM) ? D : 0;                                        \
-      if (SCALE) rescale<C>(acc[K], cnt[K]);                                         \
-      if (in.a >= 0) store_partial<C, SCALE>(a, in.a, p, acc[K], cnt[K]);            \
-      contribute<C>(acc[J], acc[K], P);                                              \
-      if (SCALE) cnt[J] += cnt[K];                                                   \
-    }                                                                                \
+#define PLK_EXIT(D)                                                         \
+  case D:                                                                   \
+    if (D + 1 < DM) {                                                       \
+      constexpr int K = (D + 1 < DM) ? D + 1 : 0;                           \
+      constexpr int J = (D + 1 < DM) ? D : 0;                               \
+      if (SCALE) rescale<CW>(acc[K], cnt[K], xch, nw);                      \
+      if (in.a >= 0) store_partial<CW, SCALE>(a, in.a, p, c0, acc[K], cnt[K]); \
+      contribute<CW>(acc[J], acc[K], P);                                    \
+      if (SCALE) cnt[J] += cnt[K];                                          \
+    }                                                                       \
     break;
           PLK_EXIT(0) PLK_EXIT(1) PLK_EXIT(2) PLK_EXIT(3) PLK_EXIT(4) PLK_EXIT(5) PLK_EXIT(6)
 #undef PLK_EXIT
@@ -192,12 +229,13 @@ __global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a) {
       }
       case T_ROOT: {
         // fragment root at level 0: rescale, optionally store, optionally reduce lnL
-        if (SCALE) rescale<C>(acc[0], cnt[0]);
-        if (in.a >= 0) store_partial<C, SCALE>(a, in.a, p, acc[0], cnt[0]);
+        if (SCALE) rescale<CW>(acc[0], cnt[0], xch, nw);
+        if (in.a >= 0) store_partial<CW, SCALE>(a, in.a, p, c0, acc[0], cnt[0]);
         if (in.b) {
-          double l = 0.0;
+          // per class: l_c = sum_s L[c][s] pi_s, t_c = l_c * prob_c  (guards: drop <= 0)
+          double t[CW];
 #pragma unroll
-          for (int c = 0; c < C; ++c) {
+          for (int c = 0; c < CW; ++c) {
             double lc = 0.0;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
@@ -208,30 +246,40 @@ __global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a) {
                 lc += li;
               }
             }
-            const double li = lc * a.probs[c];
-            if (a.guard) {
-              if (li > 0.0) l += li;
-            } else {
-              l += li;
-            }
+            t[c] = lc * a.probs[c0 + c];
           }
-          if (!a.guard && l < 0.0) l = 0.0;
-          double r = log(l);
-          if (SCALE) r -= (double)cnt[0] * kLn2x256;
-          const bool valid = p < a.n_patterns;
-          double wr = 0.0;
-          if (valid) {
-            a.site_lnl[p] = r;
-            wr = a.weights[p] * r;
-          }
-          // fixed-order wave reduction (xor butterfly, same order for every wave)
+          __syncthreads();
 #pragma unroll
-          for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
-          if ((threadIdx.x & 63) == 0) a.wave_sums[p >> 6] = wr;
+          for (int c = 0; c < CW; ++c) xch[(c0 + c) * 64 + lane] = t[c];  // C <= 4 classes fit in xch
+          __syncthreads();
+          if (w == 0) {
+            double l = 0.0;
+            for (int c = 0; c < a.C; ++c) {
+              const double li = xch[c * 64 + lane];
+              if (a.guard) {
+                if (li > 0.0) l += li;
+              } else {
+                l += li;
+              }
+            }
+            if (!a.guard && l < 0.0) l = 0.0;
+            double r = log(l);
+            if (SCALE) r -= (double)cnt[0] * kLn2x256;
+            double wr = 0.0;
+            if (p < a.n_patterns) {
+              a.site_lnl[p] = r;
+              wr = a.weights[p] * r;
+            }
+            // fixed-order butterfly: the same summation order for every wave
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+            if (lane == 0) a.wave_sums[p0 >> 6] = wr;
+          }
         }
         break;
       }
     }
+    in = nx;
   }
 }
 
