@@ -7,6 +7,7 @@
 #include "../../include/plk.h"
 #include "plk_kernels.hpp"
 #include "plk_tree4.hpp"
+#include "plk_deriv.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -94,6 +95,13 @@ struct plk_handle_s {
   int prog_root = -1;                     // node whose lnL the program reduces (-1: none)
   std::vector<char> materialized;         // per internal slot: partial present in HBM
   std::vector<int> prog_mat_after;        // per internal slot after the cached program (-1 untouched)
+  // last traversal (for derivative paths) and derivative buffers
+  std::vector<plk_op> trav_ops;
+  std::vector<char> deriv_valid;          // per node: dP and d2P present
+  double* d1_sums = nullptr;
+  double* d2_sums = nullptr;
+  DInstr* d_dprog = nullptr;
+  size_t d_dprog_cap = 0;
   bool fused_lnl_valid = false;
   int fused_lnl_root = -1;
 };
@@ -324,7 +332,8 @@ int plk_destroy(plk_handle h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
-                  h->block_sums, h->d_ops, h->d_req, h->wave_sums, h->d_prog, h->d_frag};
+                  h->block_sums, h->d_ops, h->d_req, h->wave_sums, h->d_prog, h->d_frag, h->d1_sums,
+                  h->d2_sums, h->d_dprog};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (auto& e : h->events) {
@@ -481,6 +490,11 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
       if (branch[i] < h->n_tips) h->tip_tables_dirty = true;
     }
   }
+  if (h->deriv_valid.empty()) h->deriv_valid.assign(h->n_nodes, 0);
+  // dP/d2P stay consistent with P only when all three come from the same call
+  const bool both = (deriv_mask & (PLK_DERIV_P | PLK_DERIV_DP | PLK_DERIV_D2P)) ==
+                    (PLK_DERIV_P | PLK_DERIV_DP | PLK_DERIV_D2P);
+  for (int i = 0; i < n; ++i) h->deriv_valid[branch[i]] = both ? 1 : 0;
   return PLK_OK;
 }
 
@@ -491,6 +505,7 @@ int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
   const size_t n = (size_t)h->C * h->S * h->S;
   HIPCHK(h, hipMemcpy(h->pmats + (size_t)branch * n, P, n * sizeof(double), hipMemcpyHostToDevice));
   h->pmat_valid[branch] = 1;
+  if (!h->deriv_valid.empty()) h->deriv_valid[branch] = 0;
   if (branch < h->n_tips) h->tip_tables_dirty = true;
   return PLK_OK;
 }
@@ -602,26 +617,30 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   std::vector<TInstr> prog;
   std::vector<int32_t> start(nf);
   const int root_reduce = (reduce && tops.size() == 1) ? tops[0] : -1;
-  std::function<void(int, int)> emit = [&](int n, int d) {
-    prog.push_back({T_ENTER, d, 0, 0});
+  // node n at register level d: child events in son order, then ASCEND carrying the
+  // node's own store slot and branch (the parent contributes it through that branch)
+  std::function<void(int, int, bool)> emit = [&](int n, int d, bool frag_root) {
     for (int c : kids[n]) {
       if (c < nt) {
         prog.push_back({T_TIP, d, c, c});
       } else if (produced[c] && frag_of[c] == frag_of[n]) {
-        emit(c, d + 1);
-        prog.push_back({T_EXIT, d, materialize ? c - nt : -1, c});
+        prog.push_back({T_DESCEND, d, 0, 0});
+        emit(c, d + 1, false);
       } else {
         prog.push_back({T_LOAD, d, c - nt, c});
       }
     }
+    if (frag_root)
+      prog.push_back({T_ASCEND, d, -1, -1});
+    else
+      prog.push_back({T_ASCEND, d, materialize ? n - nt : -1, n});
   };
   for (int f = 0; f < nf; ++f) {
     start[f] = (int32_t)prog.size();
     const int r = frag_roots[f];
-    emit(r, 0);
+    emit(r, 0, true);
     const bool cut = r != root_reduce && std::find(tops.begin(), tops.end(), r) == tops.end();
     prog.push_back({T_ROOT, 0, (materialize || cut) ? r - nt : -1, r == root_reduce ? 1 : 0});
-    prog.push_back({T_END, 0, 0, 0});
   }
   int rc = ensure_cap(h, (void**)&h->d_prog, &h->d_prog_cap, prog.size() * sizeof(TInstr));
   if (rc) return rc;
@@ -870,6 +889,7 @@ int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
   hipSetDevice(h->device);
   int rc = validate_ops(h, ops, n_ops);
   if (rc) return rc;
+  h->trav_ops.assign(ops, ops + n_ops);
   if (tree4_supported(h) && fusable(ops, n_ops)) return update_tree4(h, ops, n_ops);
   return update_levelwise(h, ops, n_ops);
 }
@@ -955,6 +975,104 @@ static int launch_root(plk_handle h, int root) {
     hipEventRecord(ev.b, h->stream);
     h->events.push_back(ev);
   }
+  return PLK_OK;
+}
+
+int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
+  if (!h || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
+  if (h->S != 4 || !(h->C == 1 || h->C == 2 || h->C == 4))
+    return fail(h, PLK_ERR_UNSUPPORTED, "branch derivatives need S = 4 and C in {1, 2, 4}");
+  if (h->trav_ops.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet (plk_update_partials)");
+  if (h->deriv_valid.empty() || !h->deriv_valid[branch])
+    return fail(h, PLK_ERR_STATE, "dP/d2P of branch %d not computed (PLK_DERIV_DP | PLK_DERIV_D2P)", branch);
+  if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
+  hipSetDevice(h->device);
+  const int nt = h->n_tips;
+  // tree of the last traversal: sons per node (ops merged), parent map
+  std::vector<std::vector<int> > kids(h->n_nodes);
+  std::vector<int> parent(h->n_nodes, -1);
+  for (const plk_op& o : h->trav_ops)
+    for (int k = 0; k < o.n_children; ++k) {
+      kids[o.parent].push_back(o.child[k]);
+      parent[o.child[k]] = o.parent;
+    }
+  if (parent[branch] < 0) return fail(h, PLK_ERR_ARG, "branch %d is not below any node of the last traversal", branch);
+  // every partial read along the path must be in HBM: re-materialise if needed
+  bool need = false;
+  for (int n = parent[branch]; n >= 0; n = parent[n])
+    for (int c : kids[n])
+      if (c >= nt && !h->materialized[c - nt]) need = true;
+  if (need) {
+    const unsigned saved = h->flags;
+    const std::vector<plk_op> ops = h->trav_ops;
+    h->flags &= ~(unsigned)PLK_FLAG_LNL_ONLY;
+    int rc = tree4_supported(h) && fusable(ops.data(), (int)ops.size())
+                 ? update_tree4(h, ops.data(), (int)ops.size())
+                 : update_levelwise(h, ops.data(), (int)ops.size());
+    h->flags = saved;
+    if (rc) return rc;
+  }
+  // path program: father of the branch first, then every ancestor up to the root
+  std::vector<DInstr> prog;
+  int path = branch;
+  for (int n = parent[branch]; n >= 0; path = n, n = parent[n]) {
+    for (int c : kids[n]) {
+      if (c == path) {
+        if (path == branch)
+          prog.push_back({D_PATH, c < nt ? 1 : 0, c < nt ? c : c - nt, c});
+        else
+          prog.push_back({D_PATH, 0, 0, c});
+      } else if (c < nt) {
+        prog.push_back({D_TIP, 0, c, c});
+      } else {
+        prog.push_back({D_LOAD, 0, c - nt, c});
+      }
+    }
+    prog.push_back({D_STEP, 0, 0, 0});
+  }
+  prog.push_back({D_END, 0, 0, 0});
+  int rc = ensure_cap(h, (void**)&h->d_dprog, &h->d_dprog_cap, prog.size() * sizeof(DInstr));
+  if (rc) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->d_dprog, prog.data(), prog.size() * sizeof(DInstr), hipMemcpyHostToDevice,
+                           h->stream));
+  if (!h->d1_sums) {
+    if ((rc = dalloc(h, (void**)&h->d1_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return rc;
+    if ((rc = dalloc(h, (void**)&h->d2_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return rc;
+  }
+  DerivArgs a;
+  a.partials = h->partials;
+  a.codes = h->codes;
+  a.init = h->code_table;
+  a.pi = h->pi;
+  a.probs = h->probs;
+  a.weights = h->weights;
+  a.d1_sums = h->d1_sums;
+  a.d2_sums = h->d2_sums;
+  a.slot_stride = h->slot_stride;
+  a.n_pad = h->n_pad;
+  a.n_patterns = h->n_patterns;
+  a.n_codes = h->n_codes;
+  const int guard = (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0;
+  const dim3 grid((unsigned)(h->n_pad / 256));
+  switch (h->C) {
+    case 1: deriv_kernel<4, 1><<<grid, 256, 0, h->stream>>>(a, h->d_dprog, h->pmats, h->dpmats, h->d2pmats, guard); break;
+    case 2: deriv_kernel<4, 2><<<grid, 256, 0, h->stream>>>(a, h->d_dprog, h->pmats, h->dpmats, h->d2pmats, guard); break;
+    case 4: deriv_kernel<4, 4><<<grid, 256, 0, h->stream>>>(a, h->d_dprog, h->pmats, h->dpmats, h->d2pmats, guard); break;
+  }
+  HIPCHK(h, hipGetLastError());
+  // fixed-order host sum of the wave sums (same order for any run)
+  const int n_waves = (int)((h->n_patterns + 63) / 64);
+  std::vector<double> w1(n_waves), w2(n_waves);
+  HIPCHK(h, hipMemcpyAsync(w1.data(), h->d1_sums, n_waves * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(w2.data(), h->d2_sums, n_waves * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = 0; i < n_waves; ++i) {
+    s1 += w1[i];
+    s2 += w2[i];
+  }
+  if (d1) *d1 = s1;
+  if (d2) *d2 = s2;
   return PLK_OK;
 }
 

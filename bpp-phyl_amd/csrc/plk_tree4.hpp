@@ -27,14 +27,16 @@
 
 namespace plk {
 
-enum TreeOp : int32_t { T_ENTER = 0, T_TIP = 1, T_LOAD = 2, T_EXIT = 3, T_ROOT = 4, T_END = 5 };
+enum TreeOp : int32_t { T_TIP = 1, T_LOAD = 2, T_DESCEND = 3, T_ASCEND = 4, T_ROOT = 5 };
 
 // 16-byte program word: wave-uniform, fetched with s_load_dwordx4.
+// Per node: its child events in son order -- TIP / LOAD / DESCEND (followed by the
+// child's own events) -- then ASCEND.  A fragment ends with ROOT.
 struct TInstr {
   int32_t op;
-  int32_t d;  // level of the accumulator the event writes
-  int32_t a;  // TIP: tip index; LOAD: internal slot; EXIT/ROOT: store slot or -1
-  int32_t b;  // TIP/LOAD/EXIT: branch (child node index); ROOT: 1 = reduce lnL
+  int32_t d;  // register level (informational)
+  int32_t a;  // TIP: tip index; LOAD: internal slot; ASCEND/ROOT: store slot or -1
+  int32_t b;  // TIP/LOAD/ASCEND: branch (node index of the child; -1 for a fragment root); ROOT: 1 = reduce lnL
 };
 
 struct TreeArgs {
@@ -111,6 +113,66 @@ __device__ __forceinline__ void store_partial(const TreeArgs& a, int slot, int64
   if (SCALE && c0 == 0) a.scale[(size_t)slot * a.n_pad + p] = cnt;
 }
 
+// Evaluate one node at register level D: consume its child events until ASCEND.
+// Each level is its own inlined loop with its own accumulator, so the ancestors'
+// products stay in fixed registers without any phi copies.
+template <int CW, int D, int DM, bool SCALE>
+__device__ __forceinline__ void eval_node(const TreeArgs& a, const TInstr* __restrict__& pc,
+                                          const double* __restrict__ pmats, const double* init_lds,
+                                          const uint8_t* code_lds, double* xch, int nw, int c0, int64_t p,
+                                          double (&acc)[CW * 4], int& cnt) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < CW * 4; ++i) acc[i] = 1.0;
+  cnt = 0;
+  for (;;) {
+    const TInstr in = *pc++;
+    if (in.op == T_ASCEND) {
+      // node complete: rescale, optionally store (its parent contributes it)
+      if (in.b >= 0) {
+        if (SCALE) rescale<CW>(acc, cnt, xch, nw);
+        if (in.a >= 0) store_partial<CW, SCALE>(a, in.a, p, c0, acc, cnt);
+      }
+      return;
+    }
+    const double* __restrict__ P = pmats + ((size_t)in.b * a.C + c0) * 16;
+    if (in.op == T_TIP) {
+      const int code = a.stage_codes ? code_lds[in.a * 64 + lane] : a.codes[(size_t)in.a * a.n_pad + p];
+      const double2* iv = reinterpret_cast<const double2*>(init_lds + code * 4);
+      const double2 i01 = iv[0], i23 = iv[1];
+      double src[CW * 4];
+#pragma unroll
+      for (int c = 0; c < CW; ++c) {
+        src[c * 4 + 0] = i01.x;
+        src[c * 4 + 1] = i01.y;
+        src[c * 4 + 2] = i23.x;
+        src[c * 4 + 3] = i23.y;
+      }
+      contribute<CW>(acc, src, P);
+    } else if (in.op == T_LOAD) {
+      const int64_t tile = p >> 7, q = p & (kTile - 1);
+      const double* L = a.partials + (size_t)in.a * a.slot_stride + tile * ((int64_t)a.C * 4 * kTile) +
+                        (size_t)c0 * 4 * kTile + q;
+      double src[CW * 4];
+#pragma unroll
+      for (int i = 0; i < CW * 4; ++i) src[i] = L[(size_t)i * kTile];
+      if (SCALE) cnt += a.scale[(size_t)in.a * a.n_pad + p];
+      contribute<CW>(acc, src, P);
+    } else {  // T_DESCEND: an internal child evaluated one register level down
+      if constexpr (D + 1 < DM) {
+        double child[CW * 4];
+        int ccnt;
+        eval_node<CW, D + 1, DM, SCALE>(a, pc, pmats, init_lds, code_lds, xch, nw, c0, p, child, ccnt);
+        // the child's ASCEND word carried its branch; re-read it (uniform, cached)
+        const TInstr up = pc[-1];
+        const double* __restrict__ Pc = pmats + ((size_t)up.b * a.C + c0) * 16;
+        contribute<CW>(acc, child, Pc);
+        if (SCALE) cnt += ccnt;
+      }
+    }
+  }
+}
+
 // prog / frag_start / pmats are separate __restrict__ kernel arguments: the compiler
 // can then prove they are never written in the kernel and fetches the wave-uniform
 // program words and P(t) entries with scalar loads into SGPRs.
@@ -141,145 +203,58 @@ __global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a, const TInstr* __
   }
   __syncthreads();
 
-  double acc[DM][CW * 4];
-  int cnt[DM];
-#pragma unroll
-  for (int d = 0; d < DM; ++d) cnt[d] = 0;
   const TInstr* __restrict__ pc = prog + frag_start[blockIdx.y];
-  TInstr in = pc[0];
-  while (in.op != T_END) {
-    const TInstr nx = pc[1];  // fetched one word ahead
-    ++pc;
-    const double* __restrict__ P = pmats + ((size_t)in.b * a.C + c0) * 16;
-    switch (in.op) {
-      case T_ENTER:
-        switch (in.d) {
-#define PLK_ENTER(D)                                                           \
-  case D:                                                                      \
-    if (D < DM) {                                                              \
-      _Pragma("unroll") for (int i = 0; i < CW * 4; ++i) acc[D < DM ? D : 0][i] = 1.0; \
-      cnt[D < DM ? D : 0] = 0;                                                 \
-    }                                                                          \
-    break;
-          PLK_ENTER(0) PLK_ENTER(1) PLK_ENTER(2) PLK_ENTER(3) PLK_ENTER(4) PLK_ENTER(5) PLK_ENTER(6) PLK_ENTER(7)
-#undef PLK_ENTER
-        }
-        break;
-      case T_TIP: {
-        const int code = a.stage_codes ? code_lds[in.a * 64 + lane] : a.codes[(size_t)in.a * a.n_pad + p];
-        const double2* iv = reinterpret_cast<const double2*>(init_lds + code * 4);
-        const double2 i01 = iv[0], i23 = iv[1];
-        double src[CW * 4];
+  double acc[CW * 4];
+  int cnt;
+  eval_node<CW, 0, DM, SCALE>(a, pc, pmats, init_lds, code_lds, xch, nw, c0, p, acc, cnt);
+  const TInstr in = *pc;  // T_ROOT
+  // fragment root: rescale, optionally store, optionally reduce lnL
+  if (SCALE) rescale<CW>(acc, cnt, xch, nw);
+  if (in.a >= 0) store_partial<CW, SCALE>(a, in.a, p, c0, acc, cnt);
+  if (in.b) {
+    // per class: l_c = sum_s L[c][s] pi_s, t_c = l_c * prob_c  (guards: drop <= 0)
+    double t[CW];
 #pragma unroll
-        for (int c = 0; c < CW; ++c) {
-          src[c * 4 + 0] = i01.x;
-          src[c * 4 + 1] = i01.y;
-          src[c * 4 + 2] = i23.x;
-          src[c * 4 + 3] = i23.y;
+    for (int c = 0; c < CW; ++c) {
+      double lc = 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double li = acc[c * 4 + s] * a.pi[s];
+        if (a.guard) {
+          if (li > 0.0) lc += li;
+        } else {
+          lc += li;
         }
-        switch (in.d) {
-#define PLK_TIP(D)                                                  \
-  case D:                                                           \
-    if (D < DM) contribute<CW>(acc[D < DM ? D : 0], src, P);        \
-    break;
-          PLK_TIP(0) PLK_TIP(1) PLK_TIP(2) PLK_TIP(3) PLK_TIP(4) PLK_TIP(5) PLK_TIP(6) PLK_TIP(7)
-#undef PLK_TIP
-        }
-        break;
       }
-      case T_LOAD: {
-        const int64_t tile = p >> 7, q = p & (kTile - 1);
-        const double* L = a.partials + (size_t)in.a * a.slot_stride + tile * ((int64_t)a.C * 4 * kTile) +
-                          (size_t)c0 * 4 * kTile + q;
-        double src[CW * 4];
-#pragma unroll
-        for (int i = 0; i < CW * 4; ++i) src[i] = L[(size_t)i * kTile];
-        const int sc = SCALE ? a.scale[(size_t)in.a * a.n_pad + p] : 0;
-        switch (in.d) {
-#define PLK_LOAD(D)                                              \
-  case D:                                                        \
-    if (D < DM) {                                                \
-      contribute<CW>(acc[D < DM ? D : 0], src, P);               \
-      if (SCALE) cnt[D < DM ? D : 0] += sc;                      \
-    }                                                            \
-    break;
-          PLK_LOAD(0) PLK_LOAD(1) PLK_LOAD(2) PLK_LOAD(3) PLK_LOAD(4) PLK_LOAD(5) PLK_LOAD(6) PLK_LOAD(7)
-#undef PLK_LOAD
-        }
-        break;
-      }
-      case T_EXIT: {
-        // child complete at level d+1: rescale, optionally store, multiply into level d
-        switch (in.d) {
-#define PLK_EXIT(D)                                                         \
-  case D:                                                                   \
-    if (D + 1 < DM) {                                                       \
-      constexpr int K = (D + 1 < DM) ? D + 1 : 0;                           \
-      constexpr int J = (D + 1 < DM) ? D : 0;                               \
-      if (SCALE) rescale<CW>(acc[K], cnt[K], xch, nw);                      \
-      if (in.a >= 0) store_partial<CW, SCALE>(a, in.a, p, c0, acc[K], cnt[K]); \
-      contribute<CW>(acc[J], acc[K], P);                                    \
-      if (SCALE) cnt[J] += cnt[K];                                          \
-    }                                                                       \
-    break;
-          PLK_EXIT(0) PLK_EXIT(1) PLK_EXIT(2) PLK_EXIT(3) PLK_EXIT(4) PLK_EXIT(5) PLK_EXIT(6)
-#undef PLK_EXIT
-        }
-        break;
-      }
-      case T_ROOT: {
-        // fragment root at level 0: rescale, optionally store, optionally reduce lnL
-        if (SCALE) rescale<CW>(acc[0], cnt[0], xch, nw);
-        if (in.a >= 0) store_partial<CW, SCALE>(a, in.a, p, c0, acc[0], cnt[0]);
-        if (in.b) {
-          // per class: l_c = sum_s L[c][s] pi_s, t_c = l_c * prob_c  (guards: drop <= 0)
-          double t[CW];
-#pragma unroll
-          for (int c = 0; c < CW; ++c) {
-            double lc = 0.0;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              const double li = acc[0][c * 4 + s] * a.pi[s];
-              if (a.guard) {
-                if (li > 0.0) lc += li;
-              } else {
-                lc += li;
-              }
-            }
-            t[c] = lc * a.probs[c0 + c];
-          }
-          __syncthreads();
-#pragma unroll
-          for (int c = 0; c < CW; ++c) xch[(c0 + c) * 64 + lane] = t[c];  // C <= 4 classes fit in xch
-          __syncthreads();
-          if (w == 0) {
-            double l = 0.0;
-            for (int c = 0; c < a.C; ++c) {
-              const double li = xch[c * 64 + lane];
-              if (a.guard) {
-                if (li > 0.0) l += li;
-              } else {
-                l += li;
-              }
-            }
-            if (!a.guard && l < 0.0) l = 0.0;
-            double r = log(l);
-            if (SCALE) r -= (double)cnt[0] * kLn2x256;
-            double wr = 0.0;
-            if (p < a.n_patterns) {
-              a.site_lnl[p] = r;
-              wr = a.weights[p] * r;
-            }
-            // fixed-order butterfly: the same summation order for every wave
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
-            if (lane == 0) a.wave_sums[p0 >> 6] = wr;
-          }
-        }
-        break;
-      }
+      t[c] = lc * a.probs[c0 + c];
     }
-    in = nx;
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < CW; ++c) xch[(c0 + c) * 64 + lane] = t[c];  // C <= 4 classes fit in xch
+    __syncthreads();
+    if (w == 0) {
+      double l = 0.0;
+      for (int c = 0; c < a.C; ++c) {
+        const double li = xch[c * 64 + lane];
+        if (a.guard) {
+          if (li > 0.0) l += li;
+        } else {
+          l += li;
+        }
+      }
+      if (!a.guard && l < 0.0) l = 0.0;
+      double r = log(l);
+      if (SCALE) r -= (double)cnt * kLn2x256;
+      double wr = 0.0;
+      if (p < a.n_patterns) {
+        a.site_lnl[p] = r;
+        wr = a.weights[p] * r;
+      }
+      // fixed-order butterfly: the same summation order for every wave
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+      if (lane == 0) a.wave_sums[p0 >> 6] = wr;
+    }
   }
 }
 

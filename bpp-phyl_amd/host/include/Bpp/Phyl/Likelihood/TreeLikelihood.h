@@ -101,6 +101,7 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   double reduceRoot() const;
   void fetchSiteLnl() const;
   void check(int rc, const char* what) const;
+  bool analyticDerivatives(const std::string& variable, double* d1, double* d2) const;
 
  public:
   ~AbstractPlkTreeLikelihood() override;

@@ -196,7 +196,10 @@ void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& 
     mod.push_back(modelIndexForNode(n));
     t.push_back(n->getDistanceToFather());
   }
-  check(plk_update_pmatrices(engine_, (int)br.size(), br.data(), mod.data(), t.data(), PLK_DERIV_P),
+  // dP and d2P ride along when derivatives are enabled (the reference computes them
+  // with every P, AbstractHomogeneousTreeLikelihood.cpp:375-413)
+  const unsigned mask = (derivFirst_ || derivSecond_) ? (PLK_DERIV_P | PLK_DERIV_DP | PLK_DERIV_D2P) : PLK_DERIV_P;
+  check(plk_update_pmatrices(engine_, (int)br.size(), br.data(), mod.data(), t.data(), mask),
         "plk_update_pmatrices");
 }
 
@@ -275,13 +278,25 @@ VVVdouble AbstractPlkTreeLikelihood::getLikelihoodArray(int nodeId) const {
   return out;
 }
 
-// Branch-length derivatives: central differences of the device log-likelihood
-// (analytic dP propagation, Likelihood/RHomogeneousTreeLikelihood.cpp:346-541, is
-// the next row of SURVEY.md 8f).
+// Branch-length derivatives: analytic on the device (plk_branch_derivatives, the
+// dL / d2L propagation of Likelihood/RHomogeneousTreeLikelihood.cpp:346-541, 596-791);
+// central differences of the device log-likelihood where the engine has no
+// derivative kernel (state counts other than 4).
+bool AbstractPlkTreeLikelihood::analyticDerivatives(const std::string& variable, double* d1, double* d2) const {
+  if (!(derivFirst_ || derivSecond_)) return false;
+  const Node* n = nodes_.at(TextTools::to<size_t>(variable.substr(5)));
+  const int rc = plk_branch_derivatives(engine_, engineIndex_.at(n), d1, d2);
+  if (rc == PLK_ERR_UNSUPPORTED) return false;
+  check(rc, "plk_branch_derivatives");
+  return true;
+}
+
 double AbstractPlkTreeLikelihood::getFirstOrderDerivative(const std::string& variable) const {
   if (!parameters_.hasParameter(variable)) throw ParameterNotFoundException("getFirstOrderDerivative().", variable);
   if (variable.compare(0, 5, "BrLen") != 0)
     throw Exception("Derivatives are only implemented for branch length parameters.");
+  double d1, d2;
+  if (analyticDerivatives(variable, &d1, &d2)) return -d1;
   AbstractPlkTreeLikelihood* self = const_cast<AbstractPlkTreeLikelihood*>(this);
   const double t = parameters_.getParameterValue(variable);
   const double h = 1e-5 * std::max(t, 1e-3);
@@ -300,6 +315,10 @@ double AbstractPlkTreeLikelihood::getFirstOrderDerivative(const std::string& var
 
 double AbstractPlkTreeLikelihood::getSecondOrderDerivative(const std::string& variable) const {
   if (!parameters_.hasParameter(variable)) throw ParameterNotFoundException("getSecondOrderDerivative().", variable);
+  if (variable.compare(0, 5, "BrLen") != 0)
+    throw Exception("Derivatives are only implemented for branch length parameters.");
+  double d1, d2;
+  if (analyticDerivatives(variable, &d1, &d2)) return -d2;
   AbstractPlkTreeLikelihood* self = const_cast<AbstractPlkTreeLikelihood*>(this);
   const double t = parameters_.getParameterValue(variable);
   const double h = 1e-4 * std::max(t, 1e-2);

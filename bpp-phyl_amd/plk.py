@@ -30,7 +30,7 @@ EXPORTS = [
     "plk_set_code_table", "plk_set_tip_codes", "plk_set_pattern_weights", "plk_set_category_rates",
     "plk_set_root_frequencies", "plk_set_eigen", "plk_update_pmatrices", "plk_set_pmatrix",
     "plk_get_pmatrix", "plk_update_partials", "plk_get_partials", "plk_root_loglik", "plk_block_size",
-    "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize",
+    "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
 ]
 
 
@@ -81,6 +81,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_get_timing": ([ct.c_void_p, P(ct.c_int64), dp, dp, dp], ct.c_int),
         "plk_reset_timing": ([ct.c_void_p], ct.c_int),
         "plk_synchronize": ([ct.c_void_p], ct.c_int),
+        "plk_branch_derivatives": ([ct.c_void_p, ct.c_int, dp, dp], ct.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -210,6 +211,12 @@ class Engine:
         self._chk(self.lib.plk_root_loglik(self.h, root, ct.byref(lnl), _d(sites) if want_sites else None,
                                            _d(blocks) if want_blocks else None))
         return lnl.value, sites, blocks
+
+    def branch_derivatives(self, branch: int):
+        """(d lnL/dt, d2 lnL/dt2) for the branch above node `branch`."""
+        d1, d2 = ct.c_double(0), ct.c_double(0)
+        self._chk(self.lib.plk_branch_derivatives(self.h, branch, ct.byref(d1), ct.byref(d2)))
+        return d1.value, d2.value
 
     def set_timing(self, on: bool):
         self._chk(self.lib.plk_set_timing(self.h, 1 if on else 0))

@@ -140,6 +140,15 @@ int plk_get_partials(plk_handle h, int node, double* out /* n_patterns x C x S, 
  * pattern order (ceil(n_patterns / 4096) values): summing them in a fixed order
  * gives a result independent of how patterns are sharded across devices. */
 int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums);
+
+/* First and second derivatives of lnL with respect to the length of `branch` (a child
+ * node index) for the tree of the last plk_update_partials call:
+ *   d1 = d lnL / dt,  d2 = d2 lnL / dt2   (the reference's getFirstOrderDerivative
+ *   returns -d1, RHomogeneousTreeLikelihood.cpp:346-360, 596-610).
+ * Requires dP and d2P of the branch (plk_update_pmatrices with PLK_DERIV_DP | PLK_DERIV_D2P).
+ * Replaces computeTreeDLikelihood / computeTreeD2Likelihood (:365-541, :615-791).
+ * Supported for 4-state models with 1, 2 or 4 classes (PLK_ERR_UNSUPPORTED otherwise). */
+int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2);
 int plk_block_size(void);
 
 /* Instrumentation: HIP-event timing of the partial-update kernels on the

@@ -50,6 +50,22 @@ static void unrootedGammaCase() {
   // branch-length parameters are BrLen<postorder index>, 5 branches once unrooted
   ParameterList bl = tl.getBranchLengthsParameters();
   expectNear("number of BrLen parameters", (double)bl.size(), 5., 0.);
+  // analytic dlnL/dBrLen (GPU path propagation) vs a central difference of -lnL; the
+  // reference checks its R and DR derivatives against each other to 1e-6
+  // (test/test_likelihood.cpp:122-135)
+  for (const std::string& name : bl.getParameterNames()) {
+    const double d1 = tl.getFirstOrderDerivative(name);
+    const double t = tl.getParameters().getParameterValue(name);
+    const double h = 1e-6;
+    ParameterList one = tl.getParameters().createSubList(std::vector<std::string>(1, name));
+    one[0].setValue(t + h);
+    const double fp = tl.f(one);
+    one[0].setValue(t - h);
+    const double fm = tl.f(one);
+    one[0].setValue(t);
+    tl.f(one);
+    expectNear((std::string("dlnL/d") + name).c_str(), d1, (fp - fm) / (2 * h), 1e-6);
+  }
   OptimizationTools::optimizeTreeScale(&tl);
   std::cout << "after tree scale: " << tl.getValue() << std::endl;
   OptimizationTools::optimizeNumericalParameters2(&tl, tl.getParameters(), 0, 0.000001, 10000, 0, 0);

@@ -403,3 +403,40 @@ def test_fused_partials_equal_levelwise():
         outs.append(np.stack([eng.get_partials(p) for p, _ in et.ops]))
     assert np.allclose(outs[0], outs[1], rtol=1e-13, atol=0)
     assert np.array_equal(outs[0], outs[2])
+
+
+# ---------------------------------------------------------------- analytic branch derivatives (row f1)
+
+@pytest.mark.parametrize("C,mode", [(4, "materialize"), (4, "lnl_only"), (1, "levelwise"), (2, "materialize")])
+def test_branch_derivatives_vs_oracle_finite_differences(C, mode):
+    et, m, alph, rates, probs, states = _random_problem(4, C, 12, 700, seed=40 + C)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode]
+    eng = engine_for(et, 4, C, 700, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    for b in (0, et.n_tips, et.ops[0][0], br[-1]):
+        d1, d2 = eng.branch_derivatives(int(b))
+
+        def lnl_at(t):
+            bl = et.brlen.copy()
+            bl[b] = t
+            e2 = phylo.EngineTree(et.n_tips, et.n_internal, et.root, et.tip_names, et.ops, bl, {}, [], [])
+            return oracle_for(e2, states, alph.init_table, rates, probs, m.pi, [m])[0]
+
+        t = et.brlen[b]
+        h = 1e-5
+        fd1 = (lnl_at(t + h) - lnl_at(t - h)) / (2 * h)
+        h2 = 1e-4
+        fd2 = (lnl_at(t + h2) - 2 * lnl_at(t) + lnl_at(t - h2)) / h2 ** 2
+        assert abs(d1 - fd1) <= 1e-6 * max(1.0, abs(fd1)), (b, d1, fd1)
+        assert abs(d2 - fd2) <= 2e-4 * max(1.0, abs(fd2)), (b, d2, fd2)
+
+
+def test_branch_derivatives_require_dp():
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 6, 100, seed=3)
+    eng = engine_for(et, 4, 4, 100, states, alph.init_table, rates, probs, m.pi, [m])
+    run_engine(eng, et)
+    with pytest.raises(plk.PlkError) as ei:
+        eng.branch_derivatives(0)
+    assert ei.value.code == -5
