@@ -200,6 +200,18 @@ void launch_generic_S(plk_handle h, const KOp* d_ops, int n_ops, const PartialsA
 
 int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
   const int S = h->S;
+  if (S == 20 && !std::getenv("PLK_GENERIC20")) {
+    // K2: P rows through scalar loads, tip tables in LDS
+    const size_t lds = 3 * (size_t)h->C * h->n_codes * S * sizeof(double);
+    if (lds <= 160 * 1024) {
+      dim3 grid((a.n_tiles + 1) / 2, n_ops), block(256);
+      if (h->flags & PLK_FLAG_SCALING)
+        partials_sgpr_kernel<20, true><<<grid, block, lds, h->stream>>>(d_ops, a, h->pmats, h->C);
+      else
+        partials_sgpr_kernel<20, false><<<grid, block, lds, h->stream>>>(d_ops, a, h->pmats, h->C);
+      return PLK_OK;
+    }
+  }
   const size_t per = (size_t)h->C * S * std::max(S, h->n_codes);
   const size_t lds = 3 * per * sizeof(double);
   if (lds > 160 * 1024) return fail(h, PLK_ERR_UNSUPPORTED, "LDS image of %zu bytes exceeds 160 KiB", lds);

@@ -262,6 +262,89 @@ __global__ __launch_bounds__(256) void partials_generic_kernel(const KOp* __rest
 }
 
 // ---------------------------------------------------------------------------
+// K2: medium state counts (S = 20 amino acids).  One lane = one pattern; classes
+// outer.  P(t) rows are wave-uniform and come from scalar loads straight into SGPRs
+// (pmats is a separate __restrict__ argument so the compiler may use s_load), so each
+// v_fma_f64 takes its P operand from an SGPR pair: no LDS traffic per FMA.  Tip
+// children use the per-branch tip tables staged in LDS.  Child partials are read
+// once per (class, child) into VGPRs (20 coalesced 512-B loads per wave).
+// ---------------------------------------------------------------------------
+template <int S, bool SCALE>
+__global__ __launch_bounds__(256) void partials_sgpr_kernel(const KOp* __restrict__ ops, PartialsArgs a,
+                                                            const double* __restrict__ pmats, int C) {
+  extern __shared__ __attribute__((aligned(16))) double tipT[];  // [3][C][n_codes][S]
+  const KOp& op = ops[blockIdx.y];
+  const int n = op.n;
+  const int nc = a.n_codes;
+  const int per = C * nc * S;
+  for (int k = 0; k < n; ++k)
+    if (op.is_tip[k]) {
+      const double* src = a.tipP + (size_t)op.child[k] * per;
+      for (int i = threadIdx.x; i < per; i += blockDim.x) tipT[k * per + i] = src[i];
+    }
+  __syncthreads();
+  const int q = threadIdx.x & (kTile - 1);
+  const int tile = blockIdx.x * 2 + (threadIdx.x >> 7);
+  if (tile >= a.n_tiles) return;
+  const int CS = C * S;
+  const size_t toff = (size_t)tile * ((size_t)CS * kTile) + q;
+  double* outp = a.partials + (size_t)op.parent * a.slot_stride + toff;
+  const size_t pidx = (size_t)tile * kTile + q;
+  int code[3] = {0, 0, 0};
+  for (int k = 0; k < n; ++k)
+    if (op.is_tip[k]) code[k] = a.codes[(size_t)op.child[k] * a.n_pad + pidx];
+  int cnt = 0;
+  if (SCALE) {
+    if (op.flags & 1) cnt = a.scale[(size_t)op.parent * a.n_pad + pidx];
+    for (int k = 0; k < n; ++k)
+      if (!op.is_tip[k]) cnt += a.scale[(size_t)op.child[k] * a.n_pad + pidx];
+  }
+  double m = 0.0;
+  for (int c = 0; c < C; ++c) {
+    double acc[S];
+    if (op.flags & 1) {
+#pragma unroll
+      for (int x = 0; x < S; ++x) acc[x] = outp[(size_t)(c * S + x) * kTile];
+    } else {
+#pragma unroll
+      for (int x = 0; x < S; ++x) acc[x] = 1.0;
+    }
+    for (int k = 0; k < n; ++k) {
+      if (op.is_tip[k]) {
+        const double* t = &tipT[k * per + (c * nc + code[k]) * S];
+#pragma unroll
+        for (int x = 0; x < S; ++x) acc[x] *= t[x];
+      } else {
+        const double* L = a.partials + (size_t)op.child[k] * a.slot_stride + toff + (size_t)c * S * kTile;
+        double l[S];
+#pragma unroll
+        for (int y = 0; y < S; ++y) l[y] = __builtin_nontemporal_load(L + (size_t)y * kTile);
+        const double* __restrict__ P = pmats + ((size_t)op.branch[k] * C + c) * S * S;
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+          double s = P[x * S] * l[0];
+#pragma unroll
+          for (int y = 1; y < S; ++y) s = __builtin_fma(P[x * S + y], l[y], s);
+          acc[x] *= s;
+        }
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < S; ++x) {
+      if (SCALE) m = fmax(m, acc[x]);
+      outp[(size_t)(c * S + x) * kTile] = acc[x];
+    }
+  }
+  if (SCALE) {
+    if (m > 0.0 && m < kScaleThr) {
+      for (int i = 0; i < CS; ++i) outp[(size_t)i * kTile] *= kScaleUp;
+      cnt += 1;
+    }
+    a.scale[(size_t)op.parent * a.n_pad + pidx] = cnt;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K4: batched transition matrices.  One workgroup per (branch i, class c):
 //   P = V diag(exp(lambda * r_c * t_i)) Vinv                (getPij_t :426-438)
 //   dP = r_c * V diag(lambda e) Vinv, d2P = r_c^2 V diag(lambda^2 e) Vinv
