@@ -8,6 +8,7 @@
 #include "plk_kernels.hpp"
 #include "plk_tree4.hpp"
 #include "plk_deriv.hpp"
+#include "plk_mfma64.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -98,6 +99,8 @@ struct plk_handle_s {
   // last traversal (for derivative paths) and derivative buffers
   std::vector<plk_op> trav_ops;
   std::vector<char> deriv_valid;          // per node: dP and d2P present
+  double* pmatsT = nullptr;               // S = 64: transposed copy for the MFMA kernel
+  bool pmatsT_dirty = true;
   double* d1_sums = nullptr;
   double* d2_sums = nullptr;
   DInstr* d_dprog = nullptr;
@@ -200,6 +203,25 @@ void launch_generic_S(plk_handle h, const KOp* d_ops, int n_ops, const PartialsA
 
 int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
   const int S = h->S;
+  if (S == 64 && !std::getenv("PLK_GENERIC64")) {
+    // K3: fp64 MFMA, P^T staged in LDS
+    if (!h->pmatsT) {
+      int rc = dalloc(h, (void**)&h->pmatsT, (size_t)h->n_nodes * h->C * 64 * 64 * sizeof(double));
+      if (rc) return rc;
+      h->pmatsT_dirty = true;
+    }
+    if (h->pmatsT_dirty) {
+      transpose_pmats64<<<dim3(h->n_nodes, h->C), 256, 0, h->stream>>>(h->pmats, h->pmatsT, h->C);
+      h->pmatsT_dirty = false;
+    }
+    const size_t lds = (size_t)std::max(64 * kM64Ld, h->n_codes * 64) * sizeof(double);
+    dim3 grid(a.n_tiles, n_ops), block(256);
+    if (h->flags & PLK_FLAG_SCALING)
+      partials_mfma64_kernel<true><<<grid, block, lds, h->stream>>>(d_ops, a, h->pmatsT, h->C);
+    else
+      partials_mfma64_kernel<false><<<grid, block, lds, h->stream>>>(d_ops, a, h->pmatsT, h->C);
+    return PLK_OK;
+  }
   if (S == 20 && !std::getenv("PLK_GENERIC20")) {
     // K2: P rows through scalar loads, tip tables in LDS
     const size_t lds = 3 * (size_t)h->C * h->n_codes * S * sizeof(double);
@@ -345,7 +367,7 @@ int plk_destroy(plk_handle h) {
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->block_sums, h->d_ops, h->d_req, h->wave_sums, h->d_prog, h->d_frag, h->d1_sums,
-                  h->d2_sums, h->d_dprog};
+                  h->d2_sums, h->d_dprog, h->pmatsT};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (auto& e : h->events) {
@@ -499,6 +521,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   if (deriv_mask & PLK_DERIV_P) {
     for (int i = 0; i < n; ++i) {
       h->pmat_valid[branch[i]] = 1;
+      h->pmatsT_dirty = true;
       if (branch[i] < h->n_tips) h->tip_tables_dirty = true;
     }
   }
@@ -517,6 +540,7 @@ int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
   const size_t n = (size_t)h->C * h->S * h->S;
   HIPCHK(h, hipMemcpy(h->pmats + (size_t)branch * n, P, n * sizeof(double), hipMemcpyHostToDevice));
   h->pmat_valid[branch] = 1;
+  h->pmatsT_dirty = true;
   if (!h->deriv_valid.empty()) h->deriv_valid[branch] = 0;
   if (branch < h->n_tips) h->tip_tables_dirty = true;
   return PLK_OK;
