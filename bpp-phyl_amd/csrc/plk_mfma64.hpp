@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void partials_mfma64_kernel(const KOp* __restr
         for (int xt = 0; xt < 4; ++xt)
 #pragma unroll
           for (int pt = 0; pt < 2; ++pt) d[xt][pt] = (f64x4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
+#pragma unroll 2
         for (int ks = 0; ks < 16; ++ks) {
           const int y = 4 * ks + lr;
           double bf[2];

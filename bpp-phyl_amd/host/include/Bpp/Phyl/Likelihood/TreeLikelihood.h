@@ -73,6 +73,7 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   bool verbose_ = true;
   bool initialized_ = false;
   bool scaling_ = true;
+  bool incremental_ = true;
   bool derivFirst_ = true, derivSecond_ = true;
   double minimumBrLen_ = 0.000001, maximumBrLen_ = 10000.;
   std::shared_ptr<IntervalConstraint> brLenConstraint_;
@@ -97,7 +98,7 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   virtual int modelIndexForNode(const Node*) const { return 0; }
   void uploadEigen(int modelIndex, const SubstitutionModel& model);
   void uploadRates();
-  void computeTreeLikelihood();
+  void computeTreeLikelihood(const std::vector<const Node*>* changed = nullptr);
   double reduceRoot() const;
   void fetchSiteLnl() const;
   void check(int rc, const char* what) const;
@@ -133,6 +134,9 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   // Exact power-of-two rescaling of partials (a deviation from the reference, which
   // has none and underflows on large trees); bit-identical when it never triggers.
   void setUnderflowScaling(bool yn) { scaling_ = yn; }
+  // Branch-length-only changes re-evaluate just the ancestors of the changed branches
+  // (default); false restores the reference's full traversal on every change.
+  void setIncrementalRecompute(bool yn) { incremental_ = yn; }
   // Partial likelihoods of a node in the reference's [pattern][class][state] order.
   VVVdouble getLikelihoodArray(int nodeId) const;
   plk_handle_s* getEngine() const { return engine_; }

@@ -203,13 +203,36 @@ void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& 
         "plk_update_pmatrices");
 }
 
-void AbstractPlkTreeLikelihood::computeTreeLikelihood() {
-  std::vector<plk_op> ops(opParent_.size());
-  for (size_t i = 0; i < ops.size(); i++) {
-    ops[i].parent = opParent_[i];
-    ops[i].n_children = (int)opChildren_[i].size();
-    for (size_t k = 0; k < 3; k++) ops[i].child[k] = k < opChildren_[i].size() ? opChildren_[i][k] : -1;
-    ops[i].flags = opFlags_[i];
+// Full postorder traversal (Likelihood/RHomogeneousTreeLikelihood.cpp:795-798), or,
+// when only branch lengths changed, the traversal restricted to the ancestors of
+// the changed branches: every other partial is still resident in HBM and the engine
+// LOADs it (the reference always re-traverses, :280).  Same per-node arithmetic, so
+// the result is bit-identical to a full traversal.
+void AbstractPlkTreeLikelihood::computeTreeLikelihood(const std::vector<const Node*>* changed) {
+  std::vector<char> need;
+  if (changed && incremental_) {
+    need.assign((size_t)(nTips_ + nInternal_), 0);
+    for (const Node* n : *changed)
+      for (const Node* p = n->getFather(); p; p = p->getFather()) {
+        char& f = need[(size_t)engineIndex_.at(p)];
+        if (f) break;  // the rest of the path is already marked
+        f = 1;
+      }
+  }
+  std::vector<plk_op> ops;
+  ops.reserve(opParent_.size());
+  for (size_t i = 0; i < opParent_.size(); i++) {
+    if (!need.empty() && !need[(size_t)opParent_[i]]) continue;
+    ops.emplace_back();
+    plk_op& o = ops.back();
+    o.parent = opParent_[i];
+    o.n_children = (int)opChildren_[i].size();
+    for (size_t k = 0; k < 3; k++) o.child[k] = k < opChildren_[i].size() ? opChildren_[i][k] : -1;
+    o.flags = opFlags_[i];
+  }
+  if (ops.empty()) {
+    siteLnlValid_ = false;
+    return;
   }
   check(plk_update_partials(engine_, ops.data(), (int)ops.size()), "plk_update_partials");
   siteLnlValid_ = false;
@@ -420,6 +443,9 @@ void RHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList& param
       if (s.compare(0, 5, "BrLen") == 0) changed.push_back(nodes_[TextTools::to<size_t>(s.substr(5))]);
     }
     updatePmatrices(changed);
+    computeTreeLikelihood(&changed);
+    minusLogLik_ = -reduceRoot();
+    return;
   }
   computeTreeLikelihood();
   minusLogLik_ = -reduceRoot();
@@ -502,6 +528,9 @@ void RNonHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList& pa
       if (s.compare(0, 5, "BrLen") == 0) changed.push_back(nodes_[TextTools::to<size_t>(s.substr(5))]);
     }
     updatePmatrices(changed);
+    computeTreeLikelihood(&changed);
+    minusLogLik_ = -reduceRoot();
+    return;
   }
   computeTreeLikelihood();
   minusLogLik_ = -reduceRoot();

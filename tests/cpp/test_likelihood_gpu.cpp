@@ -66,6 +66,23 @@ static void unrootedGammaCase() {
     tl.f(one);
     expectNear((std::string("dlnL/d") + name).c_str(), d1, (fp - fm) / (2 * h), 1e-6);
   }
+  // incremental re-evaluation (ancestors of the changed branch only) is bit-identical
+  // to the reference's full traversal
+  {
+    const ParameterList orig = tl.getParameters();
+    const double v0 = tl.getValue();
+    RHomogeneousTreeLikelihood full(*tree, aln, &model, &rdist, true, false);
+    full.setIncrementalRecompute(false);
+    full.initialize();
+    for (const std::string& name : bl.getParameterNames()) {
+      ParameterList one = tl.getParameters().createSubList(std::vector<std::string>(1, name));
+      one[0].setValue(one[0].getValue() * 1.7 + 0.003);
+      const double a = tl.f(one), b = full.f(one);
+      expectNear((std::string("incremental == full after ") + name).c_str(), a, b, 0.);
+    }
+    tl.setParameters(orig);
+    expectNear("restored", tl.getValue(), v0, 0.);
+  }
   OptimizationTools::optimizeTreeScale(&tl);
   std::cout << "after tree scale: " << tl.getValue() << std::endl;
   OptimizationTools::optimizeNumericalParameters2(&tl, tl.getParameters(), 0, 0.000001, 10000, 0, 0);

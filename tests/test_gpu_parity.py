@@ -207,7 +207,7 @@ def _random_problem(S, C, n_taxa, n_patterns, seed, alpha=0.5, amb=False, lo=0.0
 
 @pytest.mark.parametrize("S,C,n_taxa,n_patterns", [
     (4, 4, 16, 5000), (4, 1, 9, 1000), (4, 2, 12, 777), (4, 8, 10, 300), (4, 4, 3, 1), (4, 4, 33, 129),
-    (20, 4, 12, 600), (20, 1, 7, 250), (64, 1, 8, 300), (64, 1, 5, 130)])
+    (20, 4, 12, 600), (20, 1, 7, 250), (64, 1, 8, 300), (64, 1, 5, 130), (64, 2, 10, 400), (64, 4, 3, 1)])
 def test_random_vs_oracle(S, C, n_taxa, n_patterns):
     et, m, alph, rates, probs, states = _random_problem(S, C, n_taxa, n_patterns, seed=S * 1000 + C * 10 + n_taxa)
     eng = engine_for(et, S, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m])
@@ -238,7 +238,7 @@ def test_polytomy_accumulate_vs_oracle():
     check(lnl, site, lo, so)
 
 
-@pytest.mark.parametrize("S", [4, 20])
+@pytest.mark.parametrize("S", [4, 20, 64])
 def test_scaling_vs_oracle_deep_tree(S):
     """Trees where the unscaled reference underflows: both sides use exact 2^256 rescaling."""
     et, m, alph, rates, probs, states = _random_problem(S, 4, 256, 700, seed=11 + S, lo=0.2, hi=0.5)
