@@ -94,6 +94,60 @@ def cpu_baseline(wl, n_sample: int, reps: int):
     }
 
 
+FP64_PEAK_TFS = 78.6   # MI355X fp64 peak, vector and matrix alike (AMD spec sheet; the guide lists no fp64 row)
+RIDGE = FP64_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop/B
+
+
+def measured_traffic(config, mode, P, launches_per_step):
+    """HBM bytes per partials launch from the committed PMC passes (profiles/traffic.json,
+    keyed config/mode), rescaled to this run's pattern count."""
+    prof = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        tr = json.load(open(prof)).get(f"{config}/{mode}")
+    except Exception:
+        return None, None
+    if not tr:
+        return None, None
+    per_traversal = tr["hbm_bytes_per_traversal"] * P / tr["patterns"]
+    return per_traversal / launches_per_step, tr["source"]
+
+
+def roofline(wl, mode, P, steps, part_s, launches, bytes_pattern, flops_pattern, traffic):
+    """Roofline of the partials kernel.  achieved = algorithmic bytes (or flops) per launch
+    (SURVEY 8(d) per-pattern figures x patterns) / mean launch duration (HIP events).
+    The binding ceiling follows the bytes the design actually moves: the fused traversal
+    (mode lnl, 4 states) keeps interior partials in registers, so it moves ~N+8 B/pattern
+    and is fp64-compute bound; the materialising paths stream every partial through HBM
+    (intensity <= 7.6 flop/B < the 9.8 flop/B ridge) and are HBM bound."""
+    if part_s <= 0:
+        return None
+    per_launch_s = part_s / launches
+    pat_per_launch = P * steps / launches
+    gbs = bytes_pattern * pat_per_launch / per_launch_s / 1e9
+    tfs = flops_pattern * pat_per_launch / per_launch_s / 1e12
+    fused = mode == "lnl" and wl.S == 4 and wl.model_of_node is None
+    if traffic:
+        intensity = flops_pattern * pat_per_launch / traffic
+        compute_bound = intensity > RIDGE
+    else:
+        compute_bound = fused
+    hbm = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+           "traffic": traffic,
+           "basis": (f"algorithmic {bytes_pattern} B/pattern/traversal = 16*C*S*I + N + 8 "
+                     f"({bytes_pattern / wl.et.n_internal:.1f} B/update) x {pat_per_launch:.0f} patterns per launch "
+                     f"/ mean HIP-event launch duration")}
+    mf = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / FP64_PEAK_TFS,
+          "traffic": traffic,
+          "basis": (f"algorithmic {flops_pattern} flop/pattern/traversal = 2*C*S^2 per internal child + (k-1)*C*S "
+                    f"per combine ({flops_pattern / wl.et.n_internal:.1f} flop/update) x {pat_per_launch:.0f} "
+                    f"patterns per launch / mean HIP-event launch duration; peak = fp64 (vector = matrix) spec")}
+    main, alt = (mf, hbm) if compute_bound else (hbm, mf)
+    main = dict(main)
+    main["other_ceiling"] = {k: alt[k] for k in ("bound", "achieved", "peak", "unit", "frac")}
+    main["launch_ms"] = per_launch_s * 1e3
+    return main
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,10 +204,13 @@ def main():
         ms_step = elapsed * 1e3 / args.steps
         value = units_step * world * args.steps / elapsed
         bytes_pattern = wl.algorithmic_bytes_per_pattern()
-        alg_bytes = bytes_pattern * P * args.steps          # partials traffic of the timed traversals
+        flops_pattern = wl.algorithmic_flops_per_pattern()
         part_s = tm["partials_ms"] * 1e-3
-        achieved = alg_bytes / part_s / 1e9 if part_s > 0 else None
         launches = max(tm["launches"], 1)
+        traffic, traffic_src = measured_traffic(args.config, args.mode, P, launches / args.steps)
+        roof = roofline(wl, args.mode, P, args.steps, part_s, launches, bytes_pattern, flops_pattern, traffic)
+        if traffic_src:
+            roof["traffic_source"] = traffic_src
         rec = {
             "metric": "site-pattern x node partial updates/s",
             "value": value,
@@ -176,6 +233,7 @@ def main():
                 "internal_nodes": wl.et.n_internal,
                 "states": wl.S,
                 "classes": wl.C,
+                "mode": args.mode,
                 "parallelism": f"pattern-shard x{world}",
             },
             "lnl": lnl,
@@ -183,31 +241,12 @@ def main():
             "kernel_ms_per_step": {"partials": tm["partials_ms"] / args.steps, "pmatrix": tm["pmat_ms"] / args.steps,
                                    "root": tm["root_ms"] / args.steps},
             "partials_launches_per_step": launches / args.steps,
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": None,
-                "basis": (f"algorithmic {bytes_pattern} B/pattern/traversal = 16*C*S*I + N + 8 "
-                          f"({bytes_pattern / wl.et.n_internal:.1f} B/update) over the summed HIP-event "
-                          f"duration of the partials launches"),
-            },
+            "roofline": roof,
             "setup_s": t_setup,
         }
         if world == 1 and not args.no_cpu_baseline:
             ns = args.cpu_sample or workload.CONFIGS[args.config]["cpu_sample"]
             rec["cpu_baseline"] = cpu_baseline(wl, min(ns, P), args.cpu_reps)
-        prof = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(prof):
-            try:
-                tr = json.load(open(prof)).get(args.config)
-                if tr:
-                    rec["roofline"]["traffic"] = tr["hbm_bytes_per_traversal"] * P / tr["patterns"]
-                    rec["roofline"]["traffic_source"] = tr["source"]
-            except Exception:
-                pass
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.destroy_process_group()

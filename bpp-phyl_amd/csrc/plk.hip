@@ -995,7 +995,7 @@ static int launch_root(plk_handle h, int root) {
   a.pi = h->pi;
   a.probs = h->probs;
   a.site_lnl = h->site_lnl;
-  a.block_sums = h->block_sums;
+  a.wave_sums = h->wave_sums;
   a.n_patterns = h->n_patterns;
   a.S = h->S;
   a.C = h->C;
@@ -1005,7 +1005,11 @@ static int launch_root(plk_handle h, int root) {
     ev = get_events(h, 2);
     hipEventRecord(ev.a, h->stream);
   }
-  root_kernel<<<h->n_blocks, 256, 0, h->stream>>>(a);
+  root_kernel<<<(unsigned)(h->n_pad / 64), 64, 0, h->stream>>>(a);
+  HIPCHK(h, hipGetLastError());
+  const int n_waves = (int)((h->n_patterns + 63) / 64);
+  wave_sums_to_blocks<<<(h->n_blocks + 255) / 256, 256, 0, h->stream>>>(h->wave_sums, h->block_sums, n_waves,
+                                                                        h->n_blocks);
   HIPCHK(h, hipGetLastError());
   if (h->timing) {
     hipEventRecord(ev.b, h->stream);

@@ -420,8 +420,11 @@ __global__ __launch_bounds__(256) void tip_table_kernel(const double* __restrict
 // ---------------------------------------------------------------------------
 // K5: root reduction.  Per pattern p: l_c = sum_s L[c][s] pi_s, l = sum_c l_c w_c
 // with the reference's "<= 0 terms dropped" guards (HOMOG) or NH clamp;
-// lnl_p = log(l) - nscale * 256 ln 2.  Block b sums w_p * lnl_p over patterns
-// [b*4096, (b+1)*4096) in a fixed order.
+// lnl_p = log(l) - nscale * 256 ln 2.  One wave per 64 patterns (a grid of n_pad/64
+// single-wave blocks fills the chip even at 50k patterns); each wave sums w_p * lnl_p
+// with the same fixed butterfly as the fused traversal's root (plk_tree4.hpp), and
+// wave_sums_to_blocks then forms the fixed-order 4096-pattern block sums, so both
+// paths give bit-identical lnL from bit-identical root partials.
 // ---------------------------------------------------------------------------
 struct RootArgs {
   const double* partials;  // root slot base
@@ -430,52 +433,47 @@ struct RootArgs {
   const double* pi;        // [S]
   const double* probs;     // [C]
   double* site_lnl;        // [n_pad]
-  double* block_sums;      // [n_blocks]
+  double* wave_sums;       // [n_pad / 64]
   int64_t n_patterns;
   int S, C;
   int guard;               // 1: homogeneous guards, 0: NH clamp
 };
 
-__global__ __launch_bounds__(256) void root_kernel(RootArgs a) {
-  __shared__ double red[256];
-  const int CS = a.C * a.S;
-  double local = 0.0;
-  for (int j = 0; j < kRootBlock / 256; ++j) {
-    const int64_t p = (int64_t)blockIdx.x * kRootBlock + j * 256 + threadIdx.x;
-    if (p >= a.n_patterns) break;
-    const int64_t tile = p / kTile, q = p % kTile;
-    const double* L = a.partials + tile * ((int64_t)CS * kTile) + q;
-    double l = 0.0;
-    for (int c = 0; c < a.C; ++c) {
-      double lc = 0.0;
-      for (int s = 0; s < a.S; ++s) {
-        const double li = L[(int64_t)(c * a.S + s) * kTile] * a.pi[s];
-        if (a.guard) {
-          if (li > 0.0) lc += li;
-        } else {
-          lc += li;
-        }
-      }
-      const double li = lc * a.probs[c];
+__global__ __launch_bounds__(64) void root_kernel(RootArgs a) {
+  const int lane = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * 64;
+  const int64_t p = p0 + lane;
+  const int64_t tile = p / kTile, q = p % kTile;
+  const double* L = a.partials + tile * ((int64_t)a.C * a.S * kTile) + q;
+  double l = 0.0;
+  for (int c = 0; c < a.C; ++c) {
+    double lc = 0.0;
+    for (int s = 0; s < a.S; ++s) {
+      const double li = L[(int64_t)(c * a.S + s) * kTile] * a.pi[s];
       if (a.guard) {
-        if (li > 0.0) l += li;
+        if (li > 0.0) lc += li;
       } else {
-        l += li;
+        lc += li;
       }
     }
-    if (!a.guard && l < 0.0) l = 0.0;
-    double r = log(l);
-    if (a.scale) r -= (double)a.scale[p] * kLn2x256;
+    const double li = lc * a.probs[c];
+    if (a.guard) {
+      if (li > 0.0) l += li;
+    } else {
+      l += li;
+    }
+  }
+  if (!a.guard && l < 0.0) l = 0.0;
+  double r = log(l);
+  if (a.scale) r -= (double)a.scale[p] * kLn2x256;
+  double wr = 0.0;
+  if (p < a.n_patterns) {
     a.site_lnl[p] = r;
-    local += a.weights[p] * r;
+    wr = a.weights[p] * r;
   }
-  red[threadIdx.x] = local;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) a.block_sums[blockIdx.x] = red[0];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+  if (lane == 0) a.wave_sums[p0 >> 6] = wr;
 }
 
 }  // namespace plk

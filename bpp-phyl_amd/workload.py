@@ -71,6 +71,16 @@ class Workload:
         S_live = self.S if self.alphabet.name != "Codon" else 61
         return 16 * self.C * S_live * self.et.n_internal + self.et.n_tips + 8
 
+    def algorithmic_flops_per_pattern(self) -> int:
+        """2*C*S^2 per internal child, 0 per leaf child (code lookup),
+        (k-1)*C*S to combine k children."""
+        S_live = self.S if self.alphabet.name != "Codon" else 61
+        nt = self.et.n_tips
+        f = 0
+        for _, ch in self.et.ops:
+            f += sum(2 * self.C * S_live * S_live for c in ch if c >= nt) + (len(ch) - 1) * self.C * S_live
+        return f
+
     def simulate(self, start: int, end: int) -> np.ndarray:
         """States [n_tips][end-start] for sites [start, end)."""
         et, S = self.et, self.S
