@@ -125,7 +125,7 @@ def roofline(wl, mode, P, steps, part_s, launches, bytes_pattern, flops_pattern,
     pat_per_launch = P * steps / launches
     gbs = bytes_pattern * pat_per_launch / per_launch_s / 1e9
     tfs = flops_pattern * pat_per_launch / per_launch_s / 1e12
-    fused = mode == "lnl" and wl.S == 4 and wl.model_of_node is None
+    fused = mode == "lnl" and wl.S == 4 and wl.C in (1, 2, 4)  # tree4_supported() in plk.hip
     if traffic:
         intensity = flops_pattern * pat_per_launch / traffic
         compute_bound = intensity > RIDGE

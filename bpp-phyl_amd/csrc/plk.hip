@@ -9,6 +9,7 @@
 #include "plk_tree4.hpp"
 #include "plk_deriv.hpp"
 #include "plk_mfma64.hpp"
+#include "plk_treeS.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -92,6 +93,7 @@ struct plk_handle_s {
   std::vector<plk_op> prog_ops;           // op list the cached program was built from
   bool prog_materialize = false;
   bool prog_reduce = false;
+  int prog_dm = 0;                        // register levels the program was cut for
   std::vector<std::vector<int> > prog_tiers;  // fragment ids per tier
   int prog_root = -1;                     // node whose lnL the program reduces (-1: none)
   std::vector<char> materialized;         // per internal slot: partial present in HBM
@@ -215,7 +217,7 @@ int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs
       h->pmatsT_dirty = false;
     }
     const size_t lds = (size_t)std::max(64 * kM64Ld, h->n_codes * 64) * sizeof(double);
-    dim3 grid(a.n_tiles, n_ops), block(256);
+    dim3 grid(a.n_tiles, n_ops), block(kM64Threads);
     if (h->flags & PLK_FLAG_SCALING)
       partials_mfma64_kernel<true><<<grid, block, lds, h->stream>>>(d_ops, a, h->pmatsT, h->C);
     else
@@ -573,8 +575,25 @@ int tree4_cw(plk_handle h) {
   return std::min(cw, h->C);
 }
 
+// register levels of the fused 20-state kernel (PLK_TREES_DM overrides: 2, 3 or 4)
+int trees_dm() {
+  int dm = 2;
+  if (const char* e = std::getenv("PLK_TREES_DM")) dm = std::atoi(e);
+  return (dm >= 2 && dm <= 4) ? dm : 2;
+}
+
+int tree_levels(plk_handle h) { return h->S == 4 ? kTree4Levels(tree4_cw(h)) : trees_dm(); }
+
+// Fused traversal: 4 states (tree4_kernel) or 20 states (treeS_kernel, one wave per
+// class, C <= 4); PLK_FUSED20=0 keeps 20-state models on the levelwise K2 path.
 bool tree4_supported(plk_handle h) {
-  return h->S == 4 && (h->C == 1 || h->C == 2 || h->C == 4) && !(h->flags & PLK_FLAG_LEVELWISE);
+  if (h->flags & PLK_FLAG_LEVELWISE) return false;
+  if (h->S == 4) return h->C == 1 || h->C == 2 || h->C == 4;
+  if (h->S == 20) {
+    const char* e = std::getenv("PLK_FUSED20");
+    return h->C <= kTreeMaxWaves && !(e && e[0] == '0');
+  }
+  return false;
 }
 
 // Build the fragment programs for `ops` (validated, postorder).  Every produced node
@@ -583,7 +602,7 @@ bool tree4_supported(plk_handle h) {
 // LOADed by its parent's fragment).  Fragments are grouped into tiers so that a
 // fragment only reads partials written by earlier tiers.
 int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materialize, bool reduce) {
-  const int DM = kTree4Levels(tree4_cw(h));
+  const int DM = tree_levels(h);
   const int nt = h->n_tips;
   std::vector<std::vector<int> > kids(h->n_nodes);
   std::vector<char> produced(h->n_nodes, 0), is_child(h->n_nodes, 0);
@@ -609,8 +628,25 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   }
   std::sort(tops.begin(), tops.end());
   tops.erase(std::unique(tops.begin(), tops.end()), tops.end());
-  // assign fragments top-down
-  std::vector<int> frag_of(h->n_nodes, -1), depth(h->n_nodes, 0);
+  // Fragments, bottom-up: the register height of a node is 1 + the largest height of
+  // the produced children kept in its fragment; when that would exceed DM the
+  // tallest children are cut (they become fragment roots, materialised and LOADed).
+  // Cherries cost one level, so a fragment is as large a subtree as the registers
+  // allow and the cut partials sit as high in the tree as possible.
+  std::vector<int> rh(h->n_nodes, 0);
+  std::vector<char> cut_node(h->n_nodes, 0);
+  for (int i = 0; i < n_ops; ++i) {
+    const int n = ops[i].parent;
+    if (i + 1 < n_ops && ops[i + 1].parent == n) continue;  // polytomy: handle the node at its last op
+    std::vector<int> in;
+    for (int c : kids[n])
+      if (c >= nt && produced[c]) in.push_back(c);
+    std::sort(in.begin(), in.end(), [&](int x, int y) { return rh[x] > rh[y]; });
+    size_t first = 0;
+    while (first < in.size() && 1 + rh[in[first]] > DM) cut_node[in[first++]] = 1;
+    rh[n] = 1 + (first < in.size() ? rh[in[first]] : 0);
+  }
+  std::vector<int> frag_of(h->n_nodes, -1);
   std::vector<int> frag_roots;
   std::vector<int> stack;
   for (int t : tops) {
@@ -623,13 +659,11 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
     stack.pop_back();
     for (int c : kids[n]) {
       if (c < nt || !produced[c]) continue;
-      if (depth[n] + 1 <= DM - 1) {
-        frag_of[c] = frag_of[n];
-        depth[c] = depth[n] + 1;
-      } else {
+      if (cut_node[c]) {
         frag_of[c] = (int)frag_roots.size();
         frag_roots.push_back(c);
-        depth[c] = 0;
+      } else {
+        frag_of[c] = frag_of[n];
       }
       stack.push_back(c);
     }
@@ -699,6 +733,7 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   h->prog_ops.assign(ops, ops + n_ops);
   h->prog_materialize = materialize;
   h->prog_reduce = reduce;
+  h->prog_dm = DM;
   h->prog_root = root_reduce;
   // bookkeeping: which partials will be in HBM after the launch (-1: untouched)
   h->prog_mat_after.assign(h->n_internal, -1);
@@ -721,11 +756,29 @@ void launch_tree4_cw(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
     tree4_kernel<CW, DM, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
 }
 
+template <int S, int DM>
+void launch_treeS_dm(plk_handle h, const TreeArgs& a, dim3 grid) {
+  const dim3 block(64 * h->C);
+  if (h->flags & PLK_FLAG_SCALING)
+    treeS_kernel<S, DM, true><<<grid, block, 0, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
+  else
+    treeS_kernel<S, DM, false><<<grid, block, 0, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
+}
+
+template <int S>
+void launch_treeS(plk_handle h, const TreeArgs& a, dim3 grid) {
+  switch (h->prog_dm) {  // the depth the cached program was cut for
+    case 4: launch_treeS_dm<S, 4>(h, a, grid); break;
+    case 3: launch_treeS_dm<S, 3>(h, a, grid); break;
+    default: launch_treeS_dm<S, 2>(h, a, grid); break;
+  }
+}
+
 int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const bool materialize = !(h->flags & PLK_FLAG_LNL_ONLY);
   const bool reduce = h->pi_set && h->rates_set;
   const bool same = h->prog_ops.size() == (size_t)n_ops && h->prog_materialize == materialize &&
-                    h->prog_reduce == reduce &&
+                    h->prog_reduce == reduce && h->prog_dm == tree_levels(h) &&
                     std::memcmp(h->prog_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
   if (!same) {
     int rc = build_tree4_program(h, ops, n_ops, materialize, reduce);
@@ -735,6 +788,10 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       if (h->prog_mat_after[i] >= 0) h->materialized[i] = (char)h->prog_mat_after[i];
   }
   if (!h->table_set) return fail(h, PLK_ERR_STATE, "code table not set (plk_set_code_table)");
+  if (h->S != 4) {
+    int rc = refresh_tip_tables(h);
+    if (rc) return rc;
+  }
   TreeArgs a;
   a.prog = h->d_prog;
   a.partials = h->partials;
@@ -742,6 +799,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   a.codes = h->codes;
   a.pmats = h->pmats;
   a.init = h->code_table;
+  a.tipP = h->tipP;
   a.weights = h->weights;
   a.pi = h->pi;
   a.probs = h->probs;
@@ -767,10 +825,14 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       ev = get_events(h, 0);
       hipEventRecord(ev.a, h->stream);
     }
-    switch (cw) {
-      case 1: launch_tree4_cw<1>(h, a, grid, lds); break;
-      case 2: launch_tree4_cw<2>(h, a, grid, lds); break;
-      case 4: launch_tree4_cw<4>(h, a, grid, lds); break;
+    if (h->S == 20) {
+      launch_treeS<20>(h, a, grid);
+    } else {
+      switch (cw) {
+        case 1: launch_tree4_cw<1>(h, a, grid, lds); break;
+        case 2: launch_tree4_cw<2>(h, a, grid, lds); break;
+        case 4: launch_tree4_cw<4>(h, a, grid, lds); break;
+      }
     }
     HIPCHK(h, hipGetLastError());
     if (h->timing) {

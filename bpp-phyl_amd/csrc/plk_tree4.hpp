@@ -47,6 +47,7 @@ struct TreeArgs {
   const uint8_t* codes;       // [n_tips][n_pad]
   const double* pmats;        // [n_nodes][C][4][4]
   const double* init;         // [n_codes][4]
+  const double* tipP;         // [n_tips][C][n_codes][S] (S > 4 kernels)
   const double* weights;      // [n_pad]
   const double* pi;           // [4]
   const double* probs;        // [C]

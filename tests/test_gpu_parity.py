@@ -393,6 +393,49 @@ def test_s4_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling):
     assert lnl2 == lnl and np.array_equal(site2, site)
 
 
+@pytest.mark.parametrize("mode", sorted(MODES))
+@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,dm", [
+    (4, "balanced64", 700, False, 2), (1, "balanced64", 333, True, 3), (2, "caterpillar30", 400, True, 2),
+    (4, "caterpillar30", 300, False, 4), (3, "balanced100", 257, True, 3)])
+def test_s20_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling, dm, monkeypatch):
+    """20-state fused traversal (treeS_kernel) at every register depth, against the oracle."""
+    monkeypatch.setenv("PLK_TREES_DM", str(dm))
+    if tree_kind.startswith("balanced"):
+        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=19, lo=0.05, hi=0.4)
+    else:
+        tree = _caterpillar(int(tree_kind[11:]))
+    et = phylo.engine_tree(tree)
+    m = phylo.lg08()
+    rates, probs = phylo.gamma_rates(C, 0.7) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.PROTEIN, n_patterns, scaling, True, 6)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    rng = np.random.default_rng(n_patterns)
+    mask = rng.random(states.shape) < 0.05
+    states[mask] = rng.integers(20, phylo.PROTEIN.n_codes, size=mask.sum())   # B / Z / X ...
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, 20, C, n_patterns, states, phylo.PROTEIN.init_table, rates, probs, m.pi, [m], flags=flags)
+    lnl, site, _ = run_engine(eng, et)
+    lo, so = oracle_for(et, states, phylo.PROTEIN.init_table, rates, probs, m.pi, [m], scaling=scaling)
+    check(lnl, site, lo, so)
+    p, ch = et.ops[len(et.ops) // 2]
+    L = eng.get_partials(p)
+    assert np.all(np.isfinite(L)) and L.shape == (n_patterns, C, 20)
+    lnl2, site2, _ = run_engine(eng, et)
+    assert lnl2 == lnl and np.array_equal(site2, site)
+
+
+def test_fused20_partials_equal_levelwise():
+    et, m, alph, rates, probs, states = _random_problem(20, 4, 40, 500, seed=33)
+    outs = []
+    for mode in ("materialize", "levelwise", "lnl_only"):
+        eng = engine_for(et, 20, 4, 500, states, alph.init_table, rates, probs, m.pi, [m],
+                         flags=plk.PLK_FLAG_NONNEG_GUARD | MODES[mode])
+        run_engine(eng, et)
+        outs.append(np.stack([eng.get_partials(p) for p, _ in et.ops]))
+    assert np.allclose(outs[0], outs[1], rtol=1e-12, atol=0)
+    assert np.array_equal(outs[0], outs[2])
+
+
 def test_fused_partials_equal_levelwise():
     et, m, alph, rates, probs, states = _random_problem(4, 4, 24, 1000, seed=31)
     outs = []
