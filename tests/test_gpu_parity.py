@@ -68,6 +68,16 @@ def oracle_for(et, states, init_table, rates, probs, pi, models, model_of_node=N
     return lnl, site
 
 
+def engine_pmats(eng, et):
+    """The engine's own transition matrices (K4 output), so that the oracle checks the
+    pruning on identical P(t) inputs (SURVEY 8(d) parity check)."""
+    pm = np.zeros((et.n_nodes, eng.C, eng.S, eng.S))
+    for n in range(et.n_nodes):
+        if n != et.root:
+            pm[n] = eng.get_pmatrix(n)
+    return pm
+
+
 def check(lnl_g, site_g, lnl_o, site_o, rel=REL):
     assert np.all(np.isfinite(site_g))
     assert abs(lnl_g - lnl_o) <= rel * abs(lnl_o), (lnl_g, lnl_o)
@@ -415,8 +425,14 @@ def test_s20_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling, dm, monkey
     flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
     eng = engine_for(et, 20, C, n_patterns, states, phylo.PROTEIN.init_table, rates, probs, m.pi, [m], flags=flags)
     lnl, site, _ = run_engine(eng, et)
-    lo, so = oracle_for(et, states, phylo.PROTEIN.init_table, rates, probs, m.pi, [m], scaling=scaling)
+    # pruning on identical P(t): per-pattern 1e-12
+    lo, so = oracle_for(et, states, phylo.PROTEIN.init_table, rates, probs, m.pi, [m], scaling=scaling,
+                        pmats=engine_pmats(eng, et))
     check(lnl, site, lo, so)
+    # end to end (GPU eigen-reconstructed P vs the oracle's own Jacobi P): north-star 1e-10 on lnL
+    # (small P entries of the 20-state model carry ~1e-16 absolute = up to 1e-10 relative noise)
+    lo2, _ = oracle_for(et, states, phylo.PROTEIN.init_table, rates, probs, m.pi, [m], scaling=scaling)
+    assert abs(lnl - lo2) <= 1e-10 * abs(lo2)
     p, ch = et.ops[len(et.ops) // 2]
     L = eng.get_partials(p)
     assert np.all(np.isfinite(L)) and L.shape == (n_patterns, C, 20)
