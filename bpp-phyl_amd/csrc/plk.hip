@@ -10,6 +10,7 @@
 #include "plk_deriv.hpp"
 #include "plk_mfma64.hpp"
 #include "plk_treeS.hpp"
+#include "plk_treeM.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -101,7 +102,7 @@ struct plk_handle_s {
   // last traversal (for derivative paths) and derivative buffers
   std::vector<plk_op> trav_ops;
   std::vector<char> deriv_valid;          // per node: dP and d2P present
-  double* pmatsT = nullptr;               // S = 64: transposed copy for the MFMA kernel
+  double* pmatsT = nullptr;               // S = 20 / 64: transposed copy for the MFMA kernels
   bool pmatsT_dirty = true;
   double* d1_sums = nullptr;
   double* d2_sums = nullptr;
@@ -203,19 +204,34 @@ void launch_generic_S(plk_handle h, const KOp* d_ops, int n_ops, const PartialsA
     partials_generic_kernel<S, XB, false><<<grid, block, lds, h->stream>>>(d_ops, a, h->C);
 }
 
+// P^T copy of every transition matrix for the MFMA kernels (A operand rows = y),
+// refreshed lazily after any P(t) change.
+int ensure_pmatsT(plk_handle h) {
+  if (!h->pmatsT) {
+    int rc = dalloc(h, (void**)&h->pmatsT, (size_t)h->n_nodes * h->C * h->S * h->S * sizeof(double));
+    if (rc) return rc;
+    h->pmatsT_dirty = true;
+  }
+  if (h->pmatsT_dirty) {
+    const dim3 grid(h->n_nodes, h->C);
+    if (h->S == 64)
+      transpose_pmats<64><<<grid, 256, 0, h->stream>>>(h->pmats, h->pmatsT, h->C);
+    else if (h->S == 20)
+      transpose_pmats<20><<<grid, 256, 0, h->stream>>>(h->pmats, h->pmatsT, h->C);
+    else
+      return fail(h, PLK_ERR_UNSUPPORTED, "no transposed-P path for %d states", h->S);
+    HIPCHK(h, hipGetLastError());
+    h->pmatsT_dirty = false;
+  }
+  return PLK_OK;
+}
+
 int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
   const int S = h->S;
   if (S == 64 && !std::getenv("PLK_GENERIC64")) {
     // K3: fp64 MFMA, P^T staged in LDS
-    if (!h->pmatsT) {
-      int rc = dalloc(h, (void**)&h->pmatsT, (size_t)h->n_nodes * h->C * 64 * 64 * sizeof(double));
-      if (rc) return rc;
-      h->pmatsT_dirty = true;
-    }
-    if (h->pmatsT_dirty) {
-      transpose_pmats64<<<dim3(h->n_nodes, h->C), 256, 0, h->stream>>>(h->pmats, h->pmatsT, h->C);
-      h->pmatsT_dirty = false;
-    }
+    int rc = ensure_pmatsT(h);
+    if (rc) return rc;
     const size_t lds = (size_t)std::max(64 * kM64Ld, h->n_codes * 64) * sizeof(double);
     dim3 grid(a.n_tiles, n_ops), block(kM64Threads);
     if (h->flags & PLK_FLAG_SCALING)
@@ -575,25 +591,43 @@ int tree4_cw(plk_handle h) {
   return std::min(cw, h->C);
 }
 
-// register levels of the fused 20-state kernel (PLK_TREES_DM overrides: 2, 3 or 4)
-int trees_dm() {
-  int dm = 2;
-  if (const char* e = std::getenv("PLK_TREES_DM")) dm = std::atoi(e);
-  return (dm >= 2 && dm <= 4) ? dm : 2;
+// Fused traversal kernels: 4 states -> tree4_kernel (VALU, P in SGPRs); 20 and 64
+// states -> treeM_kernel (fp64 MFMA, register-chained layouts), or for 20 states the
+// VALU treeS_kernel when PLK_TREES=1.  PLK_FUSED20=0 / PLK_FUSED64=0 keep those state
+// counts on the levelwise kernels (K2 / K3).
+enum FusedKind { FK_NONE = 0, FK_TREE4, FK_TREES, FK_TREEM };
+
+bool env_is(const char* name, char v) {
+  const char* e = std::getenv(name);
+  return e && e[0] == v;
 }
 
-int tree_levels(plk_handle h) { return h->S == 4 ? kTree4Levels(tree4_cw(h)) : trees_dm(); }
+FusedKind fused_kind(plk_handle h) {
+  if (h->flags & PLK_FLAG_LEVELWISE) return FK_NONE;
+  if (h->S == 4) return (h->C == 1 || h->C == 2 || h->C == 4) ? FK_TREE4 : FK_NONE;
+  if (h->C > kTreeMaxWaves) return FK_NONE;
+  if (h->S == 20 && !env_is("PLK_FUSED20", '0')) return env_is("PLK_TREES", '1') ? FK_TREES : FK_TREEM;
+  if (h->S == 64 && h->C == 1 && !env_is("PLK_FUSED64", '0')) return FK_TREEM;
+  return FK_NONE;
+}
 
-// Fused traversal: 4 states (tree4_kernel) or 20 states (treeS_kernel, one wave per
-// class, C <= 4); PLK_FUSED20=0 keeps 20-state models on the levelwise K2 path.
-bool tree4_supported(plk_handle h) {
-  if (h->flags & PLK_FLAG_LEVELWISE) return false;
-  if (h->S == 4) return h->C == 1 || h->C == 2 || h->C == 4;
-  if (h->S == 20) {
-    const char* e = std::getenv("PLK_FUSED20");
-    return h->C <= kTreeMaxWaves && !(e && e[0] == '0');
+bool tree4_supported(plk_handle h) { return fused_kind(h) != FK_NONE; }
+
+int env_int(const char* name, int def, int lo, int hi) {
+  const char* e = std::getenv(name);
+  if (!e) return def;
+  const int v = std::atoi(e);
+  return (v >= lo && v <= hi) ? v : def;
+}
+
+// register levels (fragment height) of the fused program
+int tree_levels(plk_handle h) {
+  switch (fused_kind(h)) {
+    case FK_TREE4: return kTree4Levels(tree4_cw(h));
+    case FK_TREES: return env_int("PLK_TREES_DM", 2, 2, 4);
+    case FK_TREEM: return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 2, 2, 3);
+    default: return 1;
   }
-  return false;
 }
 
 // Build the fragment programs for `ops` (validated, postorder).  Every produced node
@@ -774,6 +808,32 @@ void launch_treeS(plk_handle h, const TreeArgs& a, dim3 grid) {
   }
 }
 
+template <int S, int DM>
+void launch_treeM_dm(plk_handle h, const TreeArgs& a, dim3 grid) {
+  const dim3 block(64 * kTreeMGroups * h->C);
+  if (h->flags & PLK_FLAG_SCALING)
+    treeM_kernel<S, DM, true><<<grid, block, 0, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+  else
+    treeM_kernel<S, DM, false><<<grid, block, 0, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+}
+
+void launch_treeM(plk_handle h, const TreeArgs& a, dim3 grid) {
+  if (h->S == 20) {
+    switch (h->prog_dm) {
+      case 2: launch_treeM_dm<20, 2>(h, a, grid); break;
+      case 3: launch_treeM_dm<20, 3>(h, a, grid); break;
+      case 5: launch_treeM_dm<20, 5>(h, a, grid); break;
+      case 4: launch_treeM_dm<20, 4>(h, a, grid); break;
+      default: launch_treeM_dm<20, 3>(h, a, grid); break;
+    }
+  } else {
+    switch (h->prog_dm) {
+      case 3: launch_treeM_dm<64, 3>(h, a, grid); break;
+      default: launch_treeM_dm<64, 2>(h, a, grid); break;
+    }
+  }
+}
+
 int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const bool materialize = !(h->flags & PLK_FLAG_LNL_ONLY);
   const bool reduce = h->pi_set && h->rates_set;
@@ -788,8 +848,13 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       if (h->prog_mat_after[i] >= 0) h->materialized[i] = (char)h->prog_mat_after[i];
   }
   if (!h->table_set) return fail(h, PLK_ERR_STATE, "code table not set (plk_set_code_table)");
-  if (h->S != 4) {
+  const FusedKind kind = fused_kind(h);
+  if (kind != FK_TREE4) {
     int rc = refresh_tip_tables(h);
+    if (rc) return rc;
+  }
+  if (kind == FK_TREEM) {
+    int rc = ensure_pmatsT(h);
     if (rc) return rc;
   }
   TreeArgs a;
@@ -825,7 +890,9 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       ev = get_events(h, 0);
       hipEventRecord(ev.a, h->stream);
     }
-    if (h->S == 20) {
+    if (kind == FK_TREEM) {
+      launch_treeM(h, a, grid);
+    } else if (kind == FK_TREES) {
       launch_treeS<20>(h, a, grid);
     } else {
       switch (cw) {

@@ -20,7 +20,7 @@
 // operand reuse and leaves the VALU free for the tip lookups and the product.
 #pragma once
 
-#include "plk_kernels.hpp"
+#include "plk_treeM.hpp"  // f64x4 helpers, transpose_pmats
 
 namespace plk {
 
@@ -127,17 +127,6 @@ __global__ __launch_bounds__(kM64Threads) void partials_mfma64_kernel(const KOp*
           for (int r = 0; r < 4; ++r) outp[(size_t)(c * S + 16 * xt + lr + 4 * r) * kTile] *= kScaleUp;
     }
     if (lr == 0) a.scale[(size_t)op.parent * a.n_pad + pidx] = cnt + (rs ? 1 : 0);
-  }
-}
-
-// P^T copy for the MFMA path: PT[b][c][y][x] = P[b][c][x][y]  (grid: nodes x classes)
-__global__ void transpose_pmats64(const double* __restrict__ P, double* __restrict__ PT, int C) {
-  const int b = blockIdx.x;
-  const int c = blockIdx.y;
-  const size_t off = ((size_t)b * C + c) * 64 * 64;
-  for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
-    const int y = e >> 6, x = e & 63;
-    PT[off + e] = P[off + (size_t)x * 64 + y];
   }
 }
 

@@ -1,0 +1,249 @@
+// plk_treeM.hpp -- fused postorder traversal on fp64 matrix cores for S = 20 (protein)
+// and S = 64 (codon) models (gfx950).
+//
+// Same tree programs as plk_tree4.hpp (TInstr words, fragments, tiers).  A wave owns
+// 16 consecutive site patterns of ONE rate class; a workgroup is C x 4 waves = 64
+// patterns x all classes.  The partial of a node lives in the C/D register layout of
+// v_mfma_f64_16x16x4f64: lane l holds states x = 16*xt + (l>>4) + 4*r (r = 0..3) of
+// pattern l&15, for the XT = ceil(S/16) row tiles.  A child's contribution
+//     D[x][p] = sum_y P[x][y] L[y][p]       (RHomogeneousTreeLikelihood.cpp:839-861)
+// is a chain of KS = S/4 MFMAs per row tile, and that layout is also exactly the B
+// operand layout of the next level: B for k-step ks is the register (xt, r) =
+// (ks/4, ks%4) of the same lane.  So a DESCEND child feeds its parent straight from
+// registers, with no shuffle and no LDS round trip; LOAD children come from HBM as
+// 128-byte row segments.  The A operand (P^T, per branch and class, L2/L1-resident:
+// 3.2 KB at S = 20) is read per lane straight from global memory -- every value once
+// per (wave, child), no staging barrier -- and occupancy (4 waves per SIMD) hides its
+// L2 latency behind the other waves' MFMA chains.  Padding rows x >= S (S = 20: 12 of
+// the 32 rows) have zero A rows, so they stay zero through the product.
+//
+// Leaves use the per-branch tip tables tipP[tip][c][code][x].  Rescaling is the joint
+// (all states, all classes) exact power-of-two rule of the other kernels; the fused
+// root reduction writes per-pattern lnL and the same fixed-order 64-pattern wave sums
+// as root_kernel (plk_kernels.hpp).
+#pragma once
+
+#include "plk_tree4.hpp"
+
+namespace plk {
+
+constexpr int kTreeMGroups = 4;  // 16-pattern groups per workgroup (64 patterns)
+
+template <int S>
+struct MShape {
+  static constexpr int XT = (S + 15) / 16;  // 16-row tiles of the state dimension
+  static constexpr int KS = S / 4;          // k-steps (S % 4 == 0)
+};
+
+typedef double f64x4m __attribute__((ext_vector_type(4)));
+
+template <int S>
+using MAcc = f64x4m[MShape<S>::XT];
+
+// acc[x] *= sum_y P[x][y] src[y]  for the lane's 16-pattern column; PT = P^T of the
+// child's branch and this wave's class ([y][x], row-major)
+template <int S>
+__device__ __forceinline__ void contribute_m(MAcc<S>& acc, const MAcc<S>& src, const double* __restrict__ PT,
+                                             int lr, int lc) {
+  constexpr int XT = MShape<S>::XT, KS = MShape<S>::KS;
+  f64x4m d[XT];
+#pragma unroll
+  for (int xt = 0; xt < XT; ++xt) d[xt] = (f64x4m){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const double b = src[ks >> 2][ks & 3];
+#pragma unroll
+    for (int xt = 0; xt < XT; ++xt) {
+      const int x = 16 * xt + lc;
+      const double av = (S % 16 == 0 || x < S) ? PT[(4 * ks + lr) * S + x] : 0.0;
+      d[xt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b, d[xt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int xt = 0; xt < XT; ++xt) acc[xt] *= d[xt];
+}
+
+template <int S>
+__device__ __forceinline__ bool m_valid(int xt, int r, int lr) {
+  return S % 16 == 0 || 16 * xt + lr + 4 * r < S;
+}
+
+template <int S>
+__device__ __forceinline__ void rescale_m(MAcc<S>& v, int& cnt, double* xch, int C, int c, int g, int lr, int lc) {
+  constexpr int XT = MShape<S>::XT;
+  double m = 0.0;
+#pragma unroll
+  for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m_valid<S>(xt, r, lr)) m = fmax(m, v[xt][r]);
+  m = fmax(m, __shfl_xor(m, 16, 64));
+  m = fmax(m, __shfl_xor(m, 32, 64));
+  if (C > 1) {
+    if (lr == 0) xch[(c * kTreeMGroups + g) * 16 + lc] = m;
+    __syncthreads();
+    m = 0.0;
+    for (int k = 0; k < C; ++k) m = fmax(m, xch[(k * kTreeMGroups + g) * 16 + lc]);
+    __syncthreads();
+  }
+  if (m > 0.0 && m < kScaleThr) {
+#pragma unroll
+    for (int xt = 0; xt < XT; ++xt) v[xt] *= kScaleUp;
+    cnt += 1;
+  }
+}
+
+template <int S, bool SCALE>
+__device__ __forceinline__ void store_partial_m(const TreeArgs& a, int slot, int64_t p, int c, const MAcc<S>& v,
+                                                int cnt, int lr) {
+  constexpr int XT = MShape<S>::XT;
+  const int64_t tile = p >> 7, q = p & (kTile - 1);
+  double* dst = a.partials + (size_t)slot * a.slot_stride + tile * ((int64_t)a.C * S * kTile) + (size_t)c * S * kTile + q;
+#pragma unroll
+  for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m_valid<S>(xt, r, lr)) __builtin_nontemporal_store(v[xt][r], dst + (size_t)(16 * xt + lr + 4 * r) * kTile);
+  if (SCALE && c == 0 && lr == 0) a.scale[(size_t)slot * a.n_pad + p] = cnt;
+}
+
+template <int S, int D, int DM, bool SCALE>
+__device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __restrict__& pc,
+                                            const double* __restrict__ pmatsT, double* xch, int c, int g, int lr,
+                                            int lc, int64_t p, MAcc<S>& acc, int& cnt) {
+  constexpr int XT = MShape<S>::XT;
+#pragma unroll
+  for (int xt = 0; xt < XT; ++xt) acc[xt] = (f64x4m){1.0, 1.0, 1.0, 1.0};
+  cnt = 0;
+  for (;;) {
+    const TInstr in = *pc++;
+    if (in.op == T_ASCEND) {
+      if (in.b >= 0) {
+        if (SCALE) rescale_m<S>(acc, cnt, xch, a.C, c, g, lr, lc);
+        if (in.a >= 0) store_partial_m<S, SCALE>(a, in.a, p, c, acc, cnt, lr);
+      }
+      return;
+    }
+    if (in.op == T_TIP) {
+      const int code = a.codes[(size_t)in.a * a.n_pad + p];
+      const double* t = a.tipP + (((size_t)in.a * a.C + c) * a.n_codes + code) * S;
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[xt][r] *= m_valid<S>(xt, r, lr) ? t[16 * xt + lr + 4 * r] : 0.0;
+    } else if (in.op == T_LOAD) {
+      const int64_t tile = p >> 7, q = p & (kTile - 1);
+      const double* L = a.partials + (size_t)in.a * a.slot_stride + tile * ((int64_t)a.C * S * kTile) +
+                        (size_t)c * S * kTile + q;
+      MAcc<S> src;
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          src[xt][r] = m_valid<S>(xt, r, lr) ? L[(size_t)(16 * xt + lr + 4 * r) * kTile] : 0.0;
+      if (SCALE) cnt += a.scale[(size_t)in.a * a.n_pad + p];
+      contribute_m<S>(acc, src, pmatsT + ((size_t)in.b * a.C + c) * S * S, lr, lc);
+    } else {  // T_DESCEND
+      if constexpr (D + 1 < DM) {
+        MAcc<S> child;
+        int ccnt;
+        eval_node_m<S, D + 1, DM, SCALE>(a, pc, pmatsT, xch, c, g, lr, lc, p, child, ccnt);
+        const TInstr up = pc[-1];
+        contribute_m<S>(acc, child, pmatsT + ((size_t)up.b * a.C + c) * S * S, lr, lc);
+        if (SCALE) cnt += ccnt;
+      }
+    }
+  }
+}
+
+// Workgroup = C x kTreeMGroups waves; wave w: class c = w / 4, pattern group g = w % 4.
+// S = 64 runs with one class (4 waves, up to 256 VGPRs); S = 20 with up to 4 classes
+// (16 waves, 128 VGPRs = 4 waves per SIMD).
+template <int S>
+constexpr int treeM_threads() { return S == 64 ? 64 * kTreeMGroups : 64 * kTreeMGroups * kTreeMaxWaves; }
+
+template <int S, int DM, bool SCALE>
+__global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, const TInstr* __restrict__ prog,
+                                                     const int32_t* __restrict__ frag_start,
+                                                     const double* __restrict__ pmatsT) {
+  constexpr int XT = MShape<S>::XT;
+  __shared__ double xch[kTreeMaxWaves * kTreeMGroups * 16];
+  __shared__ double red[64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = w / kTreeMGroups, g = w % kTreeMGroups;
+  const int lr = lane >> 4, lc = lane & 15;
+  const int64_t p0 = (int64_t)blockIdx.x * 64;
+  const int64_t p = p0 + 16 * g + lc;
+  const TInstr* __restrict__ pc = prog + frag_start[blockIdx.y];
+  MAcc<S> acc;
+  int cnt;
+  eval_node_m<S, 0, DM, SCALE>(a, pc, pmatsT, xch, c, g, lr, lc, p, acc, cnt);
+  const TInstr in = *pc;  // T_ROOT
+  if (SCALE) rescale_m<S>(acc, cnt, xch, a.C, c, g, lr, lc);
+  if (in.a >= 0) store_partial_m<S, SCALE>(a, in.a, p, c, acc, cnt, lr);
+  if (in.b) {
+    // l_c = sum_x L[c][x] pi_x over the lane's states, then over the 4 lanes of the pattern
+    double s = 0.0;
+#pragma unroll
+    for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (m_valid<S>(xt, r, lr)) {
+          const double li = acc[xt][r] * a.pi[16 * xt + lr + 4 * r];
+          if (a.guard) {
+            if (li > 0.0) s += li;
+          } else {
+            s += li;
+          }
+        }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const double t = s * a.probs[c];
+    __syncthreads();
+    if (lr == 0) xch[(c * kTreeMGroups + g) * 16 + lc] = t;
+    __syncthreads();
+    if (c == 0 && lr == 0) {
+      double l = 0.0;
+      for (int k = 0; k < a.C; ++k) {
+        const double li = xch[(k * kTreeMGroups + g) * 16 + lc];
+        if (a.guard) {
+          if (li > 0.0) l += li;
+        } else {
+          l += li;
+        }
+      }
+      if (!a.guard && l < 0.0) l = 0.0;
+      double rr = log(l);
+      if (SCALE) rr -= (double)cnt * kLn2x256;
+      double wr = 0.0;
+      if (p < a.n_patterns) {
+        a.site_lnl[p] = rr;
+        wr = a.weights[p] * rr;
+      }
+      red[16 * g + lc] = wr;
+    }
+    __syncthreads();
+    if (w == 0) {
+      // the 64 patterns of the workgroup in root_kernel's butterfly order
+      double wr = red[lane];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+      if (lane == 0) a.wave_sums[p0 >> 6] = wr;
+    }
+  }
+}
+
+// P^T copy: PT[b][c][y][x] = P[b][c][x][y]  (grid: nodes x classes)
+template <int S>
+__global__ void transpose_pmats(const double* __restrict__ P, double* __restrict__ PT, int C) {
+  const int b = blockIdx.x;
+  const int c = blockIdx.y;
+  const size_t off = ((size_t)b * C + c) * S * S;
+  for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
+    const int y = e / S, x = e % S;
+    PT[off + e] = P[off + (size_t)x * S + y];
+  }
+}
+
+}  // namespace plk
