@@ -95,6 +95,7 @@ struct plk_handle_s {
   bool prog_materialize = false;
   bool prog_reduce = false;
   int prog_dm = 0;                        // register levels the program was cut for
+  int prog_nf = 0;                        // fragments of the cached program
   std::vector<std::vector<int> > prog_tiers;  // fragment ids per tier
   int prog_root = -1;                     // node whose lnL the program reduces (-1: none)
   std::vector<char> materialized;         // per internal slot: partial present in HBM
@@ -746,23 +747,52 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
     const bool cut = r != root_reduce && std::find(tops.begin(), tops.end(), r) == tops.end();
     prog.push_back({T_ROOT, 0, (materialize || cut) ? r - nt : -1, r == root_reduce ? 1 : 0});
   }
+  // Staging chain for the LDS-staged kernel (treeM): the events that consume a table --
+  // TIP (its tip table), LOAD (P^T of its branch) and a non-root ASCEND (P^T of the
+  // branch its parent contributes it through) -- each carry in `d` the table of the
+  // NEXT consuming event of the fragment (prefetched while the current one computes);
+  // res_first[f] is the fragment's first table.  Codes: branch b >= 0 -> P^T(b), tip t
+  // -> -2 - t, none -> -1.  (`d` is informational for the other kernels.)
+  std::vector<int32_t> res_first(nf, -1);
+  for (int f = 0; f < nf; ++f) {
+    int prev = -1;
+    for (size_t i = (size_t)start[f]; prog[i].op != T_ROOT; ++i) {
+      TInstr& w = prog[i];
+      int res;
+      if (w.op == T_TIP)
+        res = -2 - w.a;
+      else if (w.op == T_LOAD || (w.op == T_ASCEND && w.b >= 0))
+        res = w.b;
+      else
+        continue;
+      if (prev < 0)
+        res_first[f] = res;
+      else
+        prog[(size_t)prev].d = res;
+      w.d = -1;
+      prev = (int)i;
+    }
+  }
   int rc = ensure_cap(h, (void**)&h->d_prog, &h->d_prog_cap, prog.size() * sizeof(TInstr));
   if (rc) return rc;
-  rc = ensure_cap(h, (void**)&h->d_frag, &h->d_frag_cap, std::max(nf, 1) * sizeof(int32_t));
+  rc = ensure_cap(h, (void**)&h->d_frag, &h->d_frag_cap, 2 * std::max(nf, 1) * sizeof(int32_t));
   if (rc) return rc;
   HIPCHK(h, hipMemcpyAsync(h->d_prog, prog.data(), prog.size() * sizeof(TInstr), hipMemcpyHostToDevice, h->stream));
   // fragments sorted by tier so that each tier is a contiguous range of blockIdx.y
   std::vector<int> order(nf);
   for (int f = 0; f < nf; ++f) order[f] = f;
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return tier[x] < tier[y]; });
-  std::vector<int32_t> start_sorted(nf);
+  std::vector<int32_t> start_sorted(2 * nf);  // [start offsets | first tables], tier order
   h->prog_tiers.clear();
   for (int i = 0; i < nf; ++i) {
     start_sorted[i] = start[order[i]];
+    start_sorted[nf + i] = res_first[order[i]];
     if (h->prog_tiers.empty() || tier[order[i]] != tier[order[i - 1]]) h->prog_tiers.push_back({});
     h->prog_tiers.back().push_back(i);
   }
-  HIPCHK(h, hipMemcpyAsync(h->d_frag, start_sorted.data(), nf * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->d_frag, start_sorted.data(), 2 * nf * sizeof(int32_t), hipMemcpyHostToDevice,
+                           h->stream));
+  h->prog_nf = nf;
   HIPCHK(h, hipStreamSynchronize(h->stream));  // host staging vectors go out of scope
   h->prog_ops.assign(ops, ops + n_ops);
   h->prog_materialize = materialize;
@@ -809,27 +839,27 @@ void launch_treeS(plk_handle h, const TreeArgs& a, dim3 grid) {
 }
 
 template <int S, int DM>
-void launch_treeM_dm(plk_handle h, const TreeArgs& a, dim3 grid) {
+void launch_treeM_dm(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
   const dim3 block(64 * kTreeMGroups * h->C);
   if (h->flags & PLK_FLAG_SCALING)
-    treeM_kernel<S, DM, true><<<grid, block, 0, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+    treeM_kernel<S, DM, true><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
   else
-    treeM_kernel<S, DM, false><<<grid, block, 0, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+    treeM_kernel<S, DM, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
 }
 
-void launch_treeM(plk_handle h, const TreeArgs& a, dim3 grid) {
+void launch_treeM(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
   if (h->S == 20) {
     switch (h->prog_dm) {
-      case 2: launch_treeM_dm<20, 2>(h, a, grid); break;
-      case 3: launch_treeM_dm<20, 3>(h, a, grid); break;
-      case 5: launch_treeM_dm<20, 5>(h, a, grid); break;
-      case 4: launch_treeM_dm<20, 4>(h, a, grid); break;
-      default: launch_treeM_dm<20, 3>(h, a, grid); break;
+      case 2: launch_treeM_dm<20, 2>(h, a, grid, lds); break;
+      case 3: launch_treeM_dm<20, 3>(h, a, grid, lds); break;
+      case 5: launch_treeM_dm<20, 5>(h, a, grid, lds); break;
+      case 4: launch_treeM_dm<20, 4>(h, a, grid, lds); break;
+      default: launch_treeM_dm<20, 3>(h, a, grid, lds); break;
     }
   } else {
     switch (h->prog_dm) {
-      case 3: launch_treeM_dm<64, 3>(h, a, grid); break;
-      default: launch_treeM_dm<64, 2>(h, a, grid); break;
+      case 3: launch_treeM_dm<64, 3>(h, a, grid, lds); break;
+      default: launch_treeM_dm<64, 2>(h, a, grid, lds); break;
     }
   }
 }
@@ -880,6 +910,21 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   a.stage_codes = (h->n_tips * 64 <= 64 * 1024) ? 1 : 0;
   const size_t lds = (size_t)((h->n_codes * 4 + 1) & ~1) * sizeof(double) + kTreeMaxWaves * 64 * sizeof(double) +
                      (a.stage_codes ? (size_t)h->n_tips * 64 : 0);
+  a.n_frags = h->prog_nf;
+  size_t lds_m = 0;
+  if (kind == FK_TREEM) {
+    a.buf_doubles = std::max(h->C * h->S * h->S, h->C * h->n_codes * h->S);
+    a.buf_doubles = (a.buf_doubles + 1) & ~1;
+    const int threads = 64 * kTreeMGroups * (h->S == 64 ? 1 : h->C);
+    const int pf = h->S == 64 ? treeM_pf<64>() : treeM_pf<20>();
+    if (a.buf_doubles > pf * threads)
+      return fail(h, PLK_ERR_UNSUPPORTED, "fused MFMA tables (%d doubles) exceed the staging registers",
+                  a.buf_doubles);
+    a.buf_doubles = std::max(a.buf_doubles, (pf - 1) * threads);  // unconditional stores stay inside
+    lds_m = 2 * (size_t)a.buf_doubles * sizeof(double);
+    a.stage_codes = (lds_m + (size_t)h->n_tips * 64 <= 76 * 1024) ? 1 : 0;  // two workgroups per CU
+    if (a.stage_codes) lds_m += (size_t)h->n_tips * 64;
+  }
   const int cw = tree4_cw(h);
   int first = 0;
   for (const auto& t : h->prog_tiers) {
@@ -891,7 +936,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       hipEventRecord(ev.a, h->stream);
     }
     if (kind == FK_TREEM) {
-      launch_treeM(h, a, grid);
+      launch_treeM(h, a, grid, lds_m);
     } else if (kind == FK_TREES) {
       launch_treeS<20>(h, a, grid);
     } else {

@@ -61,6 +61,8 @@ struct TreeArgs {
   int32_t C;
   int32_t guard;
   int32_t stage_codes;        // 1: tip codes staged in LDS
+  int32_t n_frags;            // fragments of the program (frag_start[n_frags + f] = first table, treeM)
+  int32_t buf_doubles;        // treeM: doubles per LDS table buffer
 };
 
 constexpr int kTreeMaxWaves = 4;

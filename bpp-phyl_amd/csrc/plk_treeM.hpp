@@ -11,16 +11,21 @@
 // operand layout of the next level: B for k-step ks is the register (xt, r) =
 // (ks/4, ks%4) of the same lane.  So a DESCEND child feeds its parent straight from
 // registers, with no shuffle and no LDS round trip; LOAD children come from HBM as
-// 128-byte row segments.  The A operand (P^T, per branch and class, L2/L1-resident:
-// 3.2 KB at S = 20) is read per lane straight from global memory -- every value once
-// per (wave, child), no staging barrier -- and occupancy (4 waves per SIMD) hides its
-// L2 latency behind the other waves' MFMA chains.  Padding rows x >= S (S = 20: 12 of
-// the 32 rows) have zero A rows, so they stay zero through the product.
+// 128-byte row segments.  Padding rows x >= S (S = 20: 12 of the 32 rows) have zero
+// A rows, so they stay zero through the product.
 //
-// Leaves use the per-branch tip tables tipP[tip][c][code][x].  Rescaling is the joint
-// (all states, all classes) exact power-of-two rule of the other kernels; the fused
-// root reduction writes per-pattern lnL and the same fixed-order 64-pattern wave sums
-// as root_kernel (plk_kernels.hpp).
+// LDS-staged tables, double-buffered: every event that needs a table -- TIP (the tip
+// table tipP[tip][c][code][x] of all classes) and LOAD / child ASCEND (P^T of the
+// branch, all classes) -- finds it already in LDS buffer `cur`.  While it computes,
+// each thread holds its slice of the NEXT event's table in registers (the builder
+// chains the tables through TInstr.d), writes it to buffer cur^1 afterwards, and one
+// workgroup barrier hands the buffers over.  The L2 latency of the tables thus hides
+// behind the MFMA chains, the A operands come from LDS (conflict-light 64-bit reads),
+// and the tip codes of the workgroup's 64 patterns are staged once at the start.
+//
+// Rescaling is the joint (all states, all classes) exact power-of-two rule of the
+// other kernels; the fused root reduction writes per-pattern lnL and the same
+// fixed-order 64-pattern wave sums as root_kernel (plk_kernels.hpp).
 #pragma once
 
 #include "plk_tree4.hpp"
@@ -41,10 +46,9 @@ template <int S>
 using MAcc = f64x4m[MShape<S>::XT];
 
 // acc[x] *= sum_y P[x][y] src[y]  for the lane's 16-pattern column; PT = P^T of the
-// child's branch and this wave's class ([y][x], row-major)
+// child's branch and this wave's class in LDS ([y][x], row stride S)
 template <int S>
-__device__ __forceinline__ void contribute_m(MAcc<S>& acc, const MAcc<S>& src, const double* __restrict__ PT,
-                                             int lr, int lc) {
+__device__ __forceinline__ void contribute_m(MAcc<S>& acc, const MAcc<S>& src, const double* PT, int lr, int lc) {
   constexpr int XT = MShape<S>::XT, KS = MShape<S>::KS;
   f64x4m d[XT];
 #pragma unroll
@@ -107,9 +111,52 @@ __device__ __forceinline__ void store_partial_m(const TreeArgs& a, int slot, int
   if (SCALE && c == 0 && lr == 0) a.scale[(size_t)slot * a.n_pad + p] = cnt;
 }
 
-template <int S, int D, int DM, bool SCALE>
+// ---- table staging (see the header): res >= 0 -> P^T of branch res, res <= -2 -> tip
+// table of tip -2-res, -1 -> nothing
+template <int S>
+__device__ __forceinline__ int table_size(const TreeArgs& a, int res) {
+  return res >= 0 ? a.C * S * S : (res <= -2 ? a.C * a.n_codes * S : 0);
+}
+
+// Every thread moves exactly PF doubles per table: loads clamp to the table (no
+// divergent predicates, no phis); a buffer holds at least (PF-1) x blockDim doubles,
+// so only the last store is predicated (the tail beyond the table is never read).
+template <int S, int PF>
+__device__ __forceinline__ void stage_load(const TreeArgs& a, const double* __restrict__ pmatsT, int res,
+                                           double (&pf)[PF]) {
+  const int n = table_size<S>(a, res);
+  const double* src = res >= 0 ? pmatsT + (size_t)res * a.C * S * S
+                               : (res <= -2 ? a.tipP + (size_t)(-2 - res) * a.C * a.n_codes * S : pmatsT);
+  const int last = n > 0 ? n - 1 : 0;
+#pragma unroll
+  for (int j = 0; j < PF; ++j) pf[j] = src[min((int)threadIdx.x + j * (int)blockDim.x, last)];
+}
+
+template <int S, int PF>
+__device__ __forceinline__ void stage_store(const TreeArgs& a, int res, const double (&pf)[PF], double* buf) {
+#pragma unroll
+  for (int j = 0; j < PF - 1; ++j) buf[threadIdx.x + j * blockDim.x] = pf[j];
+  const int i = threadIdx.x + (PF - 1) * blockDim.x;
+  if (i < a.buf_doubles) buf[i] = pf[PF - 1];
+}
+
+struct MCtx {
+  double* buf;            // two table buffers of a.buf_doubles each
+  const uint8_t* codes;   // staged codes [n_tips][64] or null
+  double* xch;
+  int cur;
+};
+
+template <int S, int PF>
+__device__ __forceinline__ void handover(const TreeArgs& a, MCtx& m, int next, const double (&pf)[PF]) {
+  stage_store<S, PF>(a, next, pf, m.buf + (m.cur ^ 1) * a.buf_doubles);
+  __syncthreads();
+  m.cur ^= 1;
+}
+
+template <int S, int PF, int D, int DM, bool SCALE>
 __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __restrict__& pc,
-                                            const double* __restrict__ pmatsT, double* xch, int c, int g, int lr,
+                                            const double* __restrict__ pmatsT, MCtx& m, int c, int g, int lr,
                                             int lc, int64_t p, MAcc<S>& acc, int& cnt) {
   constexpr int XT = MShape<S>::XT;
 #pragma unroll
@@ -119,18 +166,21 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
     const TInstr in = *pc++;
     if (in.op == T_ASCEND) {
       if (in.b >= 0) {
-        if (SCALE) rescale_m<S>(acc, cnt, xch, a.C, c, g, lr, lc);
+        if (SCALE) rescale_m<S>(acc, cnt, m.xch, a.C, c, g, lr, lc);
         if (in.a >= 0) store_partial_m<S, SCALE>(a, in.a, p, c, acc, cnt, lr);
       }
       return;
     }
     if (in.op == T_TIP) {
-      const int code = a.codes[(size_t)in.a * a.n_pad + p];
-      const double* t = a.tipP + (((size_t)in.a * a.C + c) * a.n_codes + code) * S;
+      double pf[PF];
+      stage_load<S, PF>(a, pmatsT, in.d, pf);
+      const int code = m.codes ? m.codes[in.a * 64 + 16 * g + lc] : a.codes[(size_t)in.a * a.n_pad + p];
+      const double* t = m.buf + m.cur * a.buf_doubles + (c * a.n_codes + code) * S;
 #pragma unroll
       for (int xt = 0; xt < XT; ++xt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[xt][r] *= m_valid<S>(xt, r, lr) ? t[16 * xt + lr + 4 * r] : 0.0;
+      handover<S, PF>(a, m, in.d, pf);
     } else if (in.op == T_LOAD) {
       const int64_t tile = p >> 7, q = p & (kTile - 1);
       const double* L = a.partials + (size_t)in.a * a.slot_stride + tile * ((int64_t)a.C * S * kTile) +
@@ -142,14 +192,20 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
         for (int r = 0; r < 4; ++r)
           src[xt][r] = m_valid<S>(xt, r, lr) ? L[(size_t)(16 * xt + lr + 4 * r) * kTile] : 0.0;
       if (SCALE) cnt += a.scale[(size_t)in.a * a.n_pad + p];
-      contribute_m<S>(acc, src, pmatsT + ((size_t)in.b * a.C + c) * S * S, lr, lc);
+      double pf[PF];
+      stage_load<S, PF>(a, pmatsT, in.d, pf);
+      contribute_m<S>(acc, src, m.buf + m.cur * a.buf_doubles + c * S * S, lr, lc);
+      handover<S, PF>(a, m, in.d, pf);
     } else {  // T_DESCEND
       if constexpr (D + 1 < DM) {
         MAcc<S> child;
         int ccnt;
-        eval_node_m<S, D + 1, DM, SCALE>(a, pc, pmatsT, xch, c, g, lr, lc, p, child, ccnt);
+        eval_node_m<S, PF, D + 1, DM, SCALE>(a, pc, pmatsT, m, c, g, lr, lc, p, child, ccnt);
         const TInstr up = pc[-1];
-        contribute_m<S>(acc, child, pmatsT + ((size_t)up.b * a.C + c) * S * S, lr, lc);
+        double pf[PF];
+        stage_load<S, PF>(a, pmatsT, up.d, pf);
+        contribute_m<S>(acc, child, m.buf + m.cur * a.buf_doubles + c * S * S, lr, lc);
+        handover<S, PF>(a, m, up.d, pf);
         if (SCALE) cnt += ccnt;
       }
     }
@@ -158,15 +214,19 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
 
 // Workgroup = C x kTreeMGroups waves; wave w: class c = w / 4, pattern group g = w % 4.
 // S = 64 runs with one class (4 waves, up to 256 VGPRs); S = 20 with up to 4 classes
-// (16 waves, 128 VGPRs = 4 waves per SIMD).
+// (16 waves, 128 VGPRs = 4 waves per SIMD).  PF = table doubles per thread.
 template <int S>
 constexpr int treeM_threads() { return S == 64 ? 64 * kTreeMGroups : 64 * kTreeMGroups * kTreeMaxWaves; }
+template <int S>
+constexpr int treeM_pf() { return S == 64 ? 17 : 3; }
 
 template <int S, int DM, bool SCALE>
 __global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, const TInstr* __restrict__ prog,
-                                                     const int32_t* __restrict__ frag_start,
-                                                     const double* __restrict__ pmatsT) {
+                                                                   const int32_t* __restrict__ frag_start,
+                                                                   const double* __restrict__ pmatsT) {
   constexpr int XT = MShape<S>::XT;
+  constexpr int PF = treeM_pf<S>();
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // 2 table buffers | codes
   __shared__ double xch[kTreeMaxWaves * kTreeMGroups * 16];
   __shared__ double red[64];
   const int lane = threadIdx.x & 63;
@@ -175,10 +235,30 @@ __global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, c
   const int lr = lane >> 4, lc = lane & 15;
   const int64_t p0 = (int64_t)blockIdx.x * 64;
   const int64_t p = p0 + 16 * g + lc;
+  MCtx m;
+  m.buf = lds;
+  m.xch = xch;
+  m.cur = 0;
+  m.codes = nullptr;
+  if (a.stage_codes) {
+    uint8_t* cl = reinterpret_cast<uint8_t*>(lds + 2 * a.buf_doubles);
+    for (int i = threadIdx.x; i < a.n_tips * 4; i += blockDim.x) {
+      const int t = i >> 2, j = i & 3;
+      reinterpret_cast<uint4*>(cl)[i] = *reinterpret_cast<const uint4*>(a.codes + (size_t)t * a.n_pad + p0 + 16 * j);
+    }
+    m.codes = cl;
+  }
+  {
+    const int first = frag_start[a.n_frags + blockIdx.y];
+    double pf[PF];
+    stage_load<S, PF>(a, pmatsT, first, pf);
+    stage_store<S, PF>(a, first, pf, m.buf);
+    __syncthreads();
+  }
   const TInstr* __restrict__ pc = prog + frag_start[blockIdx.y];
   MAcc<S> acc;
   int cnt;
-  eval_node_m<S, 0, DM, SCALE>(a, pc, pmatsT, xch, c, g, lr, lc, p, acc, cnt);
+  eval_node_m<S, PF, 0, DM, SCALE>(a, pc, pmatsT, m, c, g, lr, lc, p, acc, cnt);
   const TInstr in = *pc;  // T_ROOT
   if (SCALE) rescale_m<S>(acc, cnt, xch, a.C, c, g, lr, lc);
   if (in.a >= 0) store_partial_m<S, SCALE>(a, in.a, p, c, acc, cnt, lr);

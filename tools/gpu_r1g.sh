@@ -12,8 +12,6 @@ run() {  # run <tag> <config> [VAR=value ...]
 }
 run cfg3_m2 lg08_g4_protein_200k_256 PLK_TREEM_DM=2 || exit 1
 run cfg3_m3 lg08_g4_protein_200k_256 PLK_TREEM_DM=3 || exit 1
-run cfg3_m4 lg08_g4_protein_200k_256 PLK_TREEM_DM=4 || exit 1
-run cfg3_s2 lg08_g4_protein_200k_256 PLK_TREES=1 || exit 1
 run cfg4_m2 yn98_codon_50k_128 PLK_TREEM_DM=2 || exit 1
 run cfg4_m3 yn98_codon_50k_128 PLK_TREEM_DM=3 || exit 1
-run cfg4_k3 yn98_codon_50k_128 PLK_FUSED64=0 || exit 1
+bash tools/gpu_counters.sh cnt_cfg3_m2 lg08_g4_protein_200k_256 PLK_TREEM_DM=2 || exit 1
