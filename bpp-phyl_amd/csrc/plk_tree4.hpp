@@ -67,6 +67,28 @@ struct TreeArgs {
 
 constexpr int kTreeMaxWaves = 4;
 
+// Program words are wave-uniform and read-only for the whole launch: read them through
+// the constant address space so that they always come in with s_load (scalar cache,
+// SGPR result).  Through a generic pointer the compiler may pick a vector load for a
+// field it then branches on, which puts a full vector-memory round trip (and a
+// vmcnt(0) drain of every outstanding partial load) on every tree event.
+// The address itself is made provably uniform with readfirstlane (a no-op when the
+// pointer already lives in SGPRs): the nested per-level loops otherwise let the
+// divergence analysis treat the program counter as divergent.
+typedef __attribute__((address_space(4))) const TInstr* ConstProg;
+__device__ __forceinline__ TInstr fetch_instr(const TInstr* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  const ConstProg q = reinterpret_cast<ConstProg>(((uint64_t)hi << 32) | lo);
+  TInstr r;
+  r.op = q->op;
+  r.d = q->d;
+  r.a = q->a;
+  r.b = q->b;
+  return r;
+}
+
 // dst[c][x] *= sum_y P[c][x][y] * src[c][y]   (P = this wave's classes, 16 doubles each)
 template <int CW>
 __device__ __forceinline__ void contribute(double (&dst)[CW * 4], const double (&src)[CW * 4],
@@ -129,7 +151,7 @@ __device__ __forceinline__ void eval_node(const TreeArgs& a, const TInstr* __res
   for (int i = 0; i < CW * 4; ++i) acc[i] = 1.0;
   cnt = 0;
   for (;;) {
-    const TInstr in = *pc++;
+    const TInstr in = fetch_instr(pc++);
     if (in.op == T_ASCEND) {
       // node complete: rescale, optionally store (its parent contributes it)
       if (in.b >= 0) {
@@ -167,7 +189,7 @@ __device__ __forceinline__ void eval_node(const TreeArgs& a, const TInstr* __res
         int ccnt;
         eval_node<CW, D + 1, DM, SCALE>(a, pc, pmats, init_lds, code_lds, xch, nw, c0, p, child, ccnt);
         // the child's ASCEND word carried its branch; re-read it (uniform, cached)
-        const TInstr up = pc[-1];
+        const TInstr up = fetch_instr(pc - 1);
         const double* __restrict__ Pc = pmats + ((size_t)up.b * a.C + c0) * 16;
         contribute<CW>(acc, child, Pc);
         if (SCALE) cnt += ccnt;
@@ -210,7 +232,7 @@ __global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a, const TInstr* __
   double acc[CW * 4];
   int cnt;
   eval_node<CW, 0, DM, SCALE>(a, pc, pmats, init_lds, code_lds, xch, nw, c0, p, acc, cnt);
-  const TInstr in = *pc;  // T_ROOT
+  const TInstr in = fetch_instr(pc);  // T_ROOT
   // fragment root: rescale, optionally store, optionally reduce lnL
   if (SCALE) rescale<CW>(acc, cnt, xch, nw);
   if (in.a >= 0) store_partial<CW, SCALE>(a, in.a, p, c0, acc, cnt);

@@ -163,7 +163,7 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
   for (int xt = 0; xt < XT; ++xt) acc[xt] = (f64x4m){1.0, 1.0, 1.0, 1.0};
   cnt = 0;
   for (;;) {
-    const TInstr in = *pc++;
+    const TInstr in = fetch_instr(pc++);
     if (in.op == T_ASCEND) {
       if (in.b >= 0) {
         if (SCALE) rescale_m<S>(acc, cnt, m.xch, a.C, c, g, lr, lc);
@@ -201,7 +201,7 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
         MAcc<S> child;
         int ccnt;
         eval_node_m<S, PF, D + 1, DM, SCALE>(a, pc, pmatsT, m, c, g, lr, lc, p, child, ccnt);
-        const TInstr up = pc[-1];
+        const TInstr up = fetch_instr(pc - 1);
         double pf[PF];
         stage_load<S, PF>(a, pmatsT, up.d, pf);
         contribute_m<S>(acc, child, m.buf + m.cur * a.buf_doubles + c * S * S, lr, lc);
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, c
   MAcc<S> acc;
   int cnt;
   eval_node_m<S, PF, 0, DM, SCALE>(a, pc, pmatsT, m, c, g, lr, lc, p, acc, cnt);
-  const TInstr in = *pc;  // T_ROOT
+  const TInstr in = fetch_instr(pc);  // T_ROOT
   if (SCALE) rescale_m<S>(acc, cnt, xch, a.C, c, g, lr, lc);
   if (in.a >= 0) store_partial_m<S, SCALE>(a, in.a, p, c, acc, cnt, lr);
   if (in.b) {

@@ -74,7 +74,7 @@ __device__ __forceinline__ void eval_node_s(const TreeArgs& a, const TInstr* __r
   for (int i = 0; i < S; ++i) acc[i] = 1.0;
   cnt = 0;
   for (;;) {
-    const TInstr in = *pc++;
+    const TInstr in = fetch_instr(pc++);
     if (in.op == T_ASCEND) {
       if (in.b >= 0) {
         if (SCALE) rescale_s<S>(acc, cnt, xch, nw);
@@ -106,7 +106,7 @@ __device__ __forceinline__ void eval_node_s(const TreeArgs& a, const TInstr* __r
         double child[S];
         int ccnt;
         eval_node_s<S, D + 1, DM, SCALE>(a, pc, pmats, xch, nw, c0, p, child, ccnt);
-        const TInstr up = pc[-1];
+        const TInstr up = fetch_instr(pc - 1);
         contribute_s<S>(acc, child, pmats + ((size_t)up.b * a.C + c0) * S * S);
         if (SCALE) cnt += ccnt;
       }
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void treeS_kernel(TreeArgs a, const TInstr* __
   double acc[S];
   int cnt;
   eval_node_s<S, 0, DM, SCALE>(a, pc, pmats, xch, nw, c0, p, acc, cnt);
-  const TInstr in = *pc;  // T_ROOT
+  const TInstr in = fetch_instr(pc);  // T_ROOT
   if (SCALE) rescale_s<S>(acc, cnt, xch, nw);
   if (in.a >= 0) store_partial_s<S, SCALE>(a, in.a, p, c0, acc, cnt);
   if (in.b) {
