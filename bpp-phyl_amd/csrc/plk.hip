@@ -11,11 +11,15 @@
 #include "plk_mfma64.hpp"
 #include "plk_treeS.hpp"
 #include "plk_treeM.hpp"
+#include "plk_jit.hpp"
 
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 
 #include <algorithm>
 #include <functional>
+#include <map>
+#include <mutex>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -95,6 +99,7 @@ struct plk_handle_s {
   bool prog_materialize = false;
   bool prog_reduce = false;
   int prog_dm = 0;                        // register levels the program was cut for
+  bool prog_jit = false;                  // program cut for the tree-specialised kernel
   int prog_nf = 0;                        // fragments of the cached program
   std::vector<std::vector<int> > prog_tiers;  // fragment ids per tier
   int prog_root = -1;                     // node whose lnL the program reduces (-1: none)
@@ -111,6 +116,12 @@ struct plk_handle_s {
   size_t d_dprog_cap = 0;
   bool fused_lnl_valid = false;
   int fused_lnl_root = -1;
+  // tree-specialised kernel of the cached program (plk_jit.hpp); null: interpreter
+  std::vector<TInstr> prog_host;
+  std::vector<int32_t> frag_starts_host;  // fragment start offsets, tier order
+  hipFunction_t jit_fn = nullptr;
+  int jit_stage_codes = -1;
+  std::string kernel_path;                // what served the last plk_update_partials
 };
 
 namespace {
@@ -180,6 +191,47 @@ int collect_events(plk_handle h) {
     h->event_pool.push_back(e);
   }
   h->events.clear();
+  return PLK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// hiprtc compilation of the tree-specialised kernels (plk_jit.hpp), cached per
+// process by generated source.  Modules stay loaded for the life of the process.
+// ---------------------------------------------------------------------------
+std::mutex g_jit_mutex;
+std::map<std::string, hipFunction_t> g_jit_cache;
+
+int jit_function(plk_handle h, const std::string& src, const char* name, hipFunction_t* out) {
+  std::lock_guard<std::mutex> lock(g_jit_mutex);
+  auto it = g_jit_cache.find(src);
+  if (it != g_jit_cache.end()) {
+    *out = it->second;
+    return PLK_OK;
+  }
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "plk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    return fail(h, PLK_ERR_DEVICE, "hiprtcCreateProgram failed");
+  const char* opts[] = {"--offload-arch=gfx950", "-O3"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 2, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    hiprtcDestroyProgram(&prog);
+    return fail(h, PLK_ERR_DEVICE, "hiprtc compile of the tree kernel failed: %s", log.substr(0, 400).c_str());
+  }
+  size_t n = 0;
+  hiprtcGetCodeSize(prog, &n);
+  std::vector<char> code(n);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  hipModule_t mod;
+  HIPCHK(h, hipModuleLoadData(&mod, code.data()));
+  hipFunction_t fn;
+  HIPCHK(h, hipModuleGetFunction(&fn, mod, name));
+  g_jit_cache.emplace(src, fn);
+  *out = fn;
   return PLK_OK;
 }
 
@@ -621,10 +673,14 @@ int env_int(const char* name, int def, int lo, int hi) {
   return (v >= lo && v <= hi) ? v : def;
 }
 
+// 4 states, one class per wave: the tree-specialised kernel (plk_jit.hpp) serves the
+// fused traversal; PLK_JIT=0 keeps the interpreter (tree4_kernel), e.g. for A/B runs.
+bool jit_tree4(plk_handle h) { return fused_kind(h) == FK_TREE4 && tree4_cw(h) == 1 && !env_is("PLK_JIT", '0'); }
+
 // register levels (fragment height) of the fused program
 int tree_levels(plk_handle h) {
   switch (fused_kind(h)) {
-    case FK_TREE4: return kTree4Levels(tree4_cw(h));
+    case FK_TREE4: return jit_tree4(h) ? env_int("PLK_JIT_DM", 10, 2, 32) : kTree4Levels(tree4_cw(h));
     case FK_TREES: return env_int("PLK_TREES_DM", 2, 2, 4);
     case FK_TREEM: return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 2, 2, 3);
     default: return 1;
@@ -668,7 +724,11 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   // tallest children are cut (they become fragment roots, materialised and LOADed).
   // Cherries cost one level, so a fragment is as large a subtree as the registers
   // allow and the cut partials sit as high in the tree as possible.
-  std::vector<int> rh(h->n_nodes, 0);
+  // The tree-specialised kernel also bounds the code of a fragment: a workgroup runs
+  // one fragment's straight-line code, which must stay within the instruction cache,
+  // so a fragment keeps at most EMAX child edges (cutting the largest kept children).
+  const int EMAX = jit_tree4(h) ? env_int("PLK_JIT_EDGES", 160, 8, 1 << 20) : (1 << 30);
+  std::vector<int> rh(h->n_nodes, 0), ne(h->n_nodes, 0);
   std::vector<char> cut_node(h->n_nodes, 0);
   for (int i = 0; i < n_ops; ++i) {
     const int n = ops[i].parent;
@@ -680,6 +740,18 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
     size_t first = 0;
     while (first < in.size() && 1 + rh[in[first]] > DM) cut_node[in[first++]] = 1;
     rh[n] = 1 + (first < in.size() ? rh[in[first]] : 0);
+    int edges = (int)kids[n].size();
+    for (size_t k = first; k < in.size(); ++k) edges += ne[in[k]];
+    std::vector<int> kept(in.begin() + (long)first, in.end());
+    std::sort(kept.begin(), kept.end(), [&](int x, int y) { return ne[x] > ne[y]; });
+    for (size_t k = 0; k < kept.size() && edges > EMAX; ++k) {
+      cut_node[kept[k]] = 1;
+      edges -= ne[kept[k]];
+    }
+    ne[n] = edges;
+    rh[n] = 1;
+    for (int c : in)
+      if (!cut_node[c]) rh[n] = std::max(rh[n], 1 + rh[c]);
   }
   std::vector<int> frag_of(h->n_nodes, -1);
   std::vector<int> frag_roots;
@@ -793,11 +865,15 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   HIPCHK(h, hipMemcpyAsync(h->d_frag, start_sorted.data(), 2 * nf * sizeof(int32_t), hipMemcpyHostToDevice,
                            h->stream));
   h->prog_nf = nf;
+  h->prog_host = prog;
+  h->frag_starts_host.assign(start_sorted.begin(), start_sorted.begin() + nf);
+  h->jit_fn = nullptr;  // specialised kernel of the new program: compiled on first use
   HIPCHK(h, hipStreamSynchronize(h->stream));  // host staging vectors go out of scope
   h->prog_ops.assign(ops, ops + n_ops);
   h->prog_materialize = materialize;
   h->prog_reduce = reduce;
   h->prog_dm = DM;
+  h->prog_jit = jit_tree4(h);
   h->prog_root = root_reduce;
   // bookkeeping: which partials will be in HBM after the launch (-1: untouched)
   h->prog_mat_after.assign(h->n_internal, -1);
@@ -868,7 +944,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const bool materialize = !(h->flags & PLK_FLAG_LNL_ONLY);
   const bool reduce = h->pi_set && h->rates_set;
   const bool same = h->prog_ops.size() == (size_t)n_ops && h->prog_materialize == materialize &&
-                    h->prog_reduce == reduce && h->prog_dm == tree_levels(h) &&
+                    h->prog_reduce == reduce && h->prog_dm == tree_levels(h) && h->prog_jit == jit_tree4(h) &&
                     std::memcmp(h->prog_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
   if (!same) {
     int rc = build_tree4_program(h, ops, n_ops, materialize, reduce);
@@ -911,6 +987,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const size_t lds = (size_t)((h->n_codes * 4 + 1) & ~1) * sizeof(double) + kTreeMaxWaves * 64 * sizeof(double) +
                      (a.stage_codes ? (size_t)h->n_tips * 64 : 0);
   a.n_frags = h->prog_nf;
+  a.bmask = env_is("PLK_DEBUG_SAMEP", '1') ? 0 : -1;
   size_t lds_m = 0;
   if (kind == FK_TREEM) {
     a.buf_doubles = std::max(h->C * h->S * h->S, h->C * h->n_codes * h->S);
@@ -926,6 +1003,37 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     if (a.stage_codes) lds_m += (size_t)h->n_tips * 64;
   }
   const int cw = tree4_cw(h);
+  // 4 states, one class per wave: the tree-specialised kernel (PLK_JIT=0 keeps the
+  // interpreter, e.g. for A/B measurements)
+  const bool jit = jit_tree4(h);
+  JArgs ja;
+  if (jit) {
+    if (!h->jit_fn || h->jit_stage_codes != a.stage_codes) {
+      const std::string src = jit_tree4_source(h->prog_host, h->frag_starts_host, h->C,
+                                               (h->flags & PLK_FLAG_SCALING) != 0, a.stage_codes != 0,
+                                               env_int("PLK_JIT_L", 2, 1, 8));
+      int rc = jit_function(h, src, "plk_jit_tree4", &h->jit_fn);
+      if (rc) return rc;
+      h->jit_stage_codes = a.stage_codes;
+    }
+    ja.partials = a.partials;
+    ja.scale = a.scale;
+    ja.codes = a.codes;
+    ja.init = a.init;
+    ja.weights = a.weights;
+    ja.pi = a.pi;
+    ja.probs = a.probs;
+    ja.site_lnl = a.site_lnl;
+    ja.wave_sums = a.wave_sums;
+    ja.slot_stride = a.slot_stride;
+    ja.n_pad = a.n_pad;
+    ja.n_patterns = a.n_patterns;
+    ja.n_codes = a.n_codes;
+    ja.n_tips = a.n_tips;
+    ja.guard = a.guard;
+    ja.pad_ = 0;
+  }
+  h->kernel_path = jit ? "jit_tree4" : kind == FK_TREEM ? "treeM" : kind == FK_TREES ? "treeS" : "tree4";
   int first = 0;
   for (const auto& t : h->prog_tiers) {
     a.frag_start = h->d_frag + first;
@@ -935,7 +1043,13 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       ev = get_events(h, 0);
       hipEventRecord(ev.a, h->stream);
     }
-    if (kind == FK_TREEM) {
+    if (jit) {
+      const double* pm = h->pmats;
+      int base = first;
+      void* args[] = {&ja, &pm, &base};
+      HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, grid.x, grid.y, 1, 64 * h->C, 1, 1, (unsigned)lds, h->stream, args,
+                                      nullptr));
+    } else if (kind == FK_TREEM) {
       launch_treeM(h, a, grid, lds_m);
     } else if (kind == FK_TREES) {
       launch_treeS<20>(h, a, grid);
@@ -960,6 +1074,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
 }
 
 int update_levelwise(plk_handle h, const plk_op* ops, int n_ops) {
+  h->kernel_path = "levelwise";
   // Validate and level the ops: level(op) = 1 + max(level of the op that last
   // wrote each internal child in this call, level of the last writer of parent).
   std::vector<int> writer_level(h->n_nodes, -1);
@@ -1323,5 +1438,7 @@ int plk_synchronize(plk_handle h) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PLK_OK;
 }
+
+const char* plk_kernel_path(plk_handle h) { return h ? h->kernel_path.c_str() : ""; }
 
 }  // extern "C"

@@ -63,6 +63,7 @@ struct TreeArgs {
   int32_t stage_codes;        // 1: tip codes staged in LDS
   int32_t n_frags;            // fragments of the program (frag_start[n_frags + f] = first table, treeM)
   int32_t buf_doubles;        // treeM: doubles per LDS table buffer
+  int32_t bmask;              // -1 (timing experiments: 0 = every branch reads P of node 0)
 };
 
 constexpr int kTreeMaxWaves = 4;
@@ -160,7 +161,7 @@ __device__ __forceinline__ void eval_node(const TreeArgs& a, const TInstr* __res
       }
       return;
     }
-    const double* __restrict__ P = pmats + ((size_t)in.b * a.C + c0) * 16;
+    const double* __restrict__ P = pmats + ((size_t)(in.b & a.bmask) * a.C + c0) * 16;
     if (in.op == T_TIP) {
       const int code = a.stage_codes ? code_lds[in.a * 64 + lane] : a.codes[(size_t)in.a * a.n_pad + p];
       const double2* iv = reinterpret_cast<const double2*>(init_lds + code * 4);
@@ -190,7 +191,7 @@ __device__ __forceinline__ void eval_node(const TreeArgs& a, const TInstr* __res
         eval_node<CW, D + 1, DM, SCALE>(a, pc, pmats, init_lds, code_lds, xch, nw, c0, p, child, ccnt);
         // the child's ASCEND word carried its branch; re-read it (uniform, cached)
         const TInstr up = fetch_instr(pc - 1);
-        const double* __restrict__ Pc = pmats + ((size_t)up.b * a.C + c0) * 16;
+        const double* __restrict__ Pc = pmats + ((size_t)(up.b & a.bmask) * a.C + c0) * 16;
         contribute<CW>(acc, child, Pc);
         if (SCALE) cnt += ccnt;
       }

@@ -31,6 +31,7 @@ EXPORTS = [
     "plk_set_root_frequencies", "plk_set_eigen", "plk_update_pmatrices", "plk_set_pmatrix",
     "plk_get_pmatrix", "plk_update_partials", "plk_get_partials", "plk_root_loglik", "plk_block_size",
     "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
+    "plk_kernel_path",
 ]
 
 
@@ -82,6 +83,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_reset_timing": ([ct.c_void_p], ct.c_int),
         "plk_synchronize": ([ct.c_void_p], ct.c_int),
         "plk_branch_derivatives": ([ct.c_void_p, ct.c_int, dp, dp], ct.c_int),
+        "plk_kernel_path": ([ct.c_void_p], ct.c_char_p),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -232,3 +234,7 @@ class Engine:
 
     def synchronize(self):
         self._chk(self.lib.plk_synchronize(self.h))
+
+    def kernel_path(self) -> str:
+        """Kernel that served the last update_partials ("jit_tree4", "tree4", "treeS", "treeM", "levelwise")."""
+        return self.lib.plk_kernel_path(self.h).decode()

@@ -158,6 +158,10 @@ int plk_get_timing(plk_handle h, int64_t* n_launches, double* partials_ms, doubl
 int plk_reset_timing(plk_handle h);
 int plk_synchronize(plk_handle h);
 
+/* Name of the kernel that served the last plk_update_partials call ("jit_tree4",
+ * "tree4", "treeS", "treeM" or "levelwise"); "" before the first call. */
+const char* plk_kernel_path(plk_handle h);
+
 #ifdef __cplusplus
 }
 #endif

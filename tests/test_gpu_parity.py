@@ -440,6 +440,42 @@ def test_s20_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling, dm, monkey
     assert lnl2 == lnl and np.array_equal(site2, site)
 
 
+@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode", [
+    (4, "balanced64", 3000, False, "lnl_only"), (4, "balanced64", 1000, False, "materialize"),
+    (2, "balanced64", 700, True, "lnl_only"), (1, "caterpillar40", 300, True, "materialize"),
+    (4, "caterpillar40", 900, False, "lnl_only"), (4, "balanced300", 513, True, "lnl_only")])
+def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling, mode, monkeypatch):
+    """The tree-specialised kernel (plk_jit.hpp, hiprtc) against the interpreter
+    (tree4_kernel) on the same program: lnL, per-pattern lnL, block sums and every
+    interior partial bitwise; and the oracle at 1e-12."""
+    if tree_kind.startswith("balanced"):
+        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=23, lo=0.05, hi=0.4)
+    else:
+        tree = _caterpillar(int(tree_kind[11:]), seed=5)
+    et = phylo.engine_tree(tree)
+    rng = np.random.default_rng(C * 11 + n_patterns)
+    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
+    rates, probs = phylo.gamma_rates(C, 0.5) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, scaling, True, 5)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    mask = rng.random(states.shape) < 0.05
+    states[mask] = rng.integers(4, 15, size=mask.sum())
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    res = {}
+    for kernel in ("0", "1"):
+        monkeypatch.setenv("PLK_JIT", kernel)
+        eng = engine_for(et, 4, C, n_patterns, states, phylo.DNA.init_table, rates, probs, m.pi, [m], flags=flags)
+        lnl, site, blocks = run_engine(eng, et)
+        assert eng.kernel_path() == ("jit_tree4" if kernel == "1" else "tree4")
+        parts = np.stack([eng.get_partials(p) for p, _ in et.ops])
+        res[kernel] = (lnl, site, blocks, parts)
+        del eng
+    (l0, s0, b0, p0), (l1, s1, b1, p1) = res["0"], res["1"]
+    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1) and np.array_equal(p0, p1)
+    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m], scaling=scaling)
+    check(l1, s1, lo, so)
+
+
 def test_fused20_partials_equal_levelwise():
     et, m, alph, rates, probs, states = _random_problem(20, 4, 40, 500, seed=33)
     outs = []
