@@ -46,7 +46,16 @@ struct plk_handle_s {
   int64_t n_patterns = 0, n_pad = 0;
   int n_tiles = 0, n_blocks = 0;
   unsigned flags = 0;
-  int n_codes = 0;
+  int n_codes = 0;          // codes in use (compact numbering, see code_map)
+  int n_codes_table = 0;    // rows of the caller's code table
+  // Tip codes are stored on the device in a compact numbering: the codes that occur
+  // in the uploaded alignment, in order of first appearance.  The device code table
+  // and the per-tip tables then hold only those rows (an alignment of A/C/G/T uses 4
+  // of DNA's 15 codes), which is what lets the fused kernels keep the tip tables of a
+  // whole fragment in LDS.
+  std::vector<int> code_map;            // caller code -> compact code (-1: unused)
+  std::vector<int> code_orig;           // compact code -> caller code
+  std::vector<double> code_table_host;  // caller's table [n_codes_table][S]
   hipStream_t stream = nullptr;
   // device buffers
   double* partials = nullptr;
@@ -100,6 +109,7 @@ struct plk_handle_s {
   bool prog_reduce = false;
   int prog_dm = 0;                        // register levels the program was cut for
   bool prog_jit = false;                  // program cut for the tree-specialised kernel
+  int prog_tmax = 0;                      // tips per fragment the program was cut for
   int prog_nf = 0;                        // fragments of the cached program
   std::vector<std::vector<int> > prog_tiers;  // fragment ids per tier
   int prog_root = -1;                     // node whose lnL the program reduces (-1: none)
@@ -120,7 +130,7 @@ struct plk_handle_s {
   std::vector<TInstr> prog_host;
   std::vector<int32_t> frag_starts_host;  // fragment start offsets, tier order
   hipFunction_t jit_fn = nullptr;
-  int jit_stage_codes = -1;
+  JitShape jit_shape;
   std::string kernel_path;                // what served the last plk_update_partials
 };
 
@@ -334,6 +344,23 @@ int refresh_tip_tables(plk_handle h) {
   return PLK_OK;
 }
 
+// Device code table in the compact numbering (rows of the codes in use; at least one
+// row so that every kernel sees a valid table before the first tip upload).
+int upload_compact_table(plk_handle h) {
+  const int S = h->S;
+  const int U = std::max((int)h->code_orig.size(), 1);
+  std::vector<double> t((size_t)U * S, 0.0);
+  for (size_t k = 0; k < h->code_orig.size(); ++k)
+    std::copy(h->code_table_host.begin() + (size_t)h->code_orig[k] * S,
+              h->code_table_host.begin() + (size_t)(h->code_orig[k] + 1) * S, t.begin() + k * S);
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipMemcpy(h->code_table, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+  h->n_codes = U;
+  h->tip_tables_dirty = true;
+  return PLK_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -458,6 +485,9 @@ int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec) {
   if (!h || !code_to_vec || n_codes < 1 || n_codes > 256) return fail(h, PLK_ERR_ARG, "bad code table (n_codes %d)", n_codes);
   if (h->S == 4 && n_codes > kMaxCodes4 && s4_supported(h->C))
     return fail(h, PLK_ERR_UNSUPPORTED, "4-state engine supports at most %d codes", kMaxCodes4);
+  for (int c : h->code_orig)
+    if (c >= n_codes)
+      return fail(h, PLK_ERR_STATE, "uploaded tip codes use code %d, outside the new table (%d codes)", c, n_codes);
   hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->code_table) hipFree(h->code_table);
@@ -468,22 +498,40 @@ int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec) {
   if ((rc = dalloc(h, (void**)&h->code_table, (size_t)n_codes * h->S * sizeof(double)))) return rc;
   if ((rc = dalloc(h, (void**)&h->tipP, (size_t)std::max(h->n_tips, 1) * h->C * n_codes * h->S * sizeof(double))))
     return rc;
-  HIPCHK(h, hipMemcpy(h->code_table, code_to_vec, (size_t)n_codes * h->S * sizeof(double), hipMemcpyHostToDevice));
-  h->n_codes = n_codes;
+  h->code_table_host.assign(code_to_vec, code_to_vec + (size_t)n_codes * h->S);
+  h->n_codes_table = n_codes;
+  h->code_map.resize(256, -1);
   h->table_set = true;
-  h->tip_tables_dirty = true;
-  return PLK_OK;
+  return upload_compact_table(h);
 }
 
 int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes) {
   if (!h || !codes || tip < 0 || tip >= h->n_tips) return fail(h, PLK_ERR_ARG, "bad tip index %d", tip);
   if (!h->table_set) return fail(h, PLK_ERR_STATE, "plk_set_code_table must precede plk_set_tip_codes");
-  for (int64_t i = 0; i < h->n_patterns; ++i)
-    if (codes[i] >= h->n_codes)
+  bool seen[256] = {false};
+  for (int64_t i = 0; i < h->n_patterns; ++i) seen[codes[i]] = true;
+  for (int c = 0; c < 256; ++c)
+    if (seen[c] && c >= h->n_codes_table) {
+      int64_t i = 0;
+      while (codes[i] != c) ++i;
       return fail(h, PLK_ERR_BAD_CODE, "tip %d pattern %lld: code %d outside the code table (%d codes)", tip,
-                  (long long)i, (int)codes[i], h->n_codes);
+                  (long long)i, c, h->n_codes_table);
+    }
+  bool grown = false;
+  for (int c = 0; c < 256; ++c)
+    if (seen[c] && h->code_map[c] < 0) {
+      h->code_map[c] = (int)h->code_orig.size();
+      h->code_orig.push_back(c);
+      grown = true;
+    }
+  if (grown) {
+    int rc = upload_compact_table(h);
+    if (rc) return rc;
+  }
+  std::vector<uint8_t> cc((size_t)h->n_patterns);
+  for (int64_t i = 0; i < h->n_patterns; ++i) cc[(size_t)i] = (uint8_t)h->code_map[codes[i]];
   hipSetDevice(h->device);
-  HIPCHK(h, hipMemcpy(h->codes + (size_t)tip * h->n_pad, codes, (size_t)h->n_patterns, hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->codes + (size_t)tip * h->n_pad, cc.data(), (size_t)h->n_patterns, hipMemcpyHostToDevice));
   h->tip_set[tip] = 1;
   return PLK_OK;
 }
@@ -677,6 +725,12 @@ int env_int(const char* name, int def, int lo, int hi) {
 // fused traversal; PLK_JIT=0 keeps the interpreter (tree4_kernel), e.g. for A/B runs.
 bool jit_tree4(plk_handle h) { return fused_kind(h) == FK_TREE4 && tree4_cw(h) == 1 && !env_is("PLK_JIT", '0'); }
 
+// tips whose tables (C x codes-in-use x 4 doubles each) fit one fragment's LDS budget
+int jit_tip_cap(plk_handle h) {
+  const int kb = env_int("PLK_JIT_TAB_KB", 48, 4, 120);
+  return std::max(2, (kb * 1024) / (h->C * std::max(h->n_codes, 1) * 4 * (int)sizeof(double)));
+}
+
 // register levels (fragment height) of the fused program
 int tree_levels(plk_handle h) {
   switch (fused_kind(h)) {
@@ -728,7 +782,9 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   // one fragment's straight-line code, which must stay within the instruction cache,
   // so a fragment keeps at most EMAX child edges (cutting the largest kept children).
   const int EMAX = jit_tree4(h) ? env_int("PLK_JIT_EDGES", 160, 8, 1 << 20) : (1 << 30);
-  std::vector<int> rh(h->n_nodes, 0), ne(h->n_nodes, 0);
+  // ... and its tips' tables must fit the LDS budget (PLK_JIT_TAB_KB, default 48 KiB)
+  const int TMAX = jit_tree4(h) ? jit_tip_cap(h) : (1 << 30);
+  std::vector<int> rh(h->n_nodes, 0), ne(h->n_nodes, 0), ntp(h->n_nodes, 0);
   std::vector<char> cut_node(h->n_nodes, 0);
   for (int i = 0; i < n_ops; ++i) {
     const int n = ops[i].parent;
@@ -740,15 +796,21 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
     size_t first = 0;
     while (first < in.size() && 1 + rh[in[first]] > DM) cut_node[in[first++]] = 1;
     rh[n] = 1 + (first < in.size() ? rh[in[first]] : 0);
-    int edges = (int)kids[n].size();
-    for (size_t k = first; k < in.size(); ++k) edges += ne[in[k]];
+    int edges = (int)kids[n].size(), ntips = 0;
+    for (int c : kids[n]) ntips += c < nt;
+    for (size_t k = first; k < in.size(); ++k) {
+      edges += ne[in[k]];
+      ntips += ntp[in[k]];
+    }
     std::vector<int> kept(in.begin() + (long)first, in.end());
     std::sort(kept.begin(), kept.end(), [&](int x, int y) { return ne[x] > ne[y]; });
-    for (size_t k = 0; k < kept.size() && edges > EMAX; ++k) {
+    for (size_t k = 0; k < kept.size() && (edges > EMAX || ntips > TMAX); ++k) {
       cut_node[kept[k]] = 1;
       edges -= ne[kept[k]];
+      ntips -= ntp[kept[k]];
     }
     ne[n] = edges;
+    ntp[n] = ntips;
     rh[n] = 1;
     for (int c : in)
       if (!cut_node[c]) rh[n] = std::max(rh[n], 1 + rh[c]);
@@ -874,6 +936,7 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   h->prog_reduce = reduce;
   h->prog_dm = DM;
   h->prog_jit = jit_tree4(h);
+  h->prog_tmax = TMAX;
   h->prog_root = root_reduce;
   // bookkeeping: which partials will be in HBM after the launch (-1: untouched)
   h->prog_mat_after.assign(h->n_internal, -1);
@@ -945,6 +1008,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const bool reduce = h->pi_set && h->rates_set;
   const bool same = h->prog_ops.size() == (size_t)n_ops && h->prog_materialize == materialize &&
                     h->prog_reduce == reduce && h->prog_dm == tree_levels(h) && h->prog_jit == jit_tree4(h) &&
+                    (!h->prog_jit || h->prog_tmax == jit_tip_cap(h)) &&
                     std::memcmp(h->prog_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
   if (!same) {
     int rc = build_tree4_program(h, ops, n_ops, materialize, reduce);
@@ -955,7 +1019,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   }
   if (!h->table_set) return fail(h, PLK_ERR_STATE, "code table not set (plk_set_code_table)");
   const FusedKind kind = fused_kind(h);
-  if (kind != FK_TREE4) {
+  if (kind != FK_TREE4 || h->prog_jit) {
     int rc = refresh_tip_tables(h);
     if (rc) return rc;
   }
@@ -1005,21 +1069,28 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const int cw = tree4_cw(h);
   // 4 states, one class per wave: the tree-specialised kernel (PLK_JIT=0 keeps the
   // interpreter, e.g. for A/B measurements)
-  const bool jit = jit_tree4(h);
+  const bool jit = h->prog_jit;
   JArgs ja;
+  JitShape sh;
   if (jit) {
-    if (!h->jit_fn || h->jit_stage_codes != a.stage_codes) {
-      const std::string src = jit_tree4_source(h->prog_host, h->frag_starts_host, h->C,
-                                               (h->flags & PLK_FLAG_SCALING) != 0, a.stage_codes != 0,
-                                               env_int("PLK_JIT_L", 2, 1, 8));
-      int rc = jit_function(h, src, "plk_jit_tree4", &h->jit_fn);
+    sh.C = h->C;
+    sh.G = (h->n_pad % 128 == 0) ? env_int("PLK_JIT_G", 2, 1, 2) : 1;
+    sh.U = h->n_codes;
+    sh.NT = jit_max_fragment_tips(h->prog_host, h->frag_starts_host);
+    sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
+    sh.L = env_int("PLK_JIT_L", 1, 1, 8);
+    if (sh.lds_bytes() > 160 * 1024)
+      return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
+    if (!h->jit_fn || sh.C != h->jit_shape.C || sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
+        sh.NT != h->jit_shape.NT || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L) {
+      int rc = jit_function(h, jit_tree4_source(h->prog_host, h->frag_starts_host, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
-      h->jit_stage_codes = a.stage_codes;
+      h->jit_shape = sh;
     }
     ja.partials = a.partials;
     ja.scale = a.scale;
     ja.codes = a.codes;
-    ja.init = a.init;
+    ja.tipP = h->tipP;
     ja.weights = a.weights;
     ja.pi = a.pi;
     ja.probs = a.probs;
@@ -1028,10 +1099,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.slot_stride = a.slot_stride;
     ja.n_pad = a.n_pad;
     ja.n_patterns = a.n_patterns;
-    ja.n_codes = a.n_codes;
-    ja.n_tips = a.n_tips;
+    ja.n_sblocks = (int32_t)(h->n_pad / (64 * sh.G));
     ja.guard = a.guard;
-    ja.pad_ = 0;
   }
   h->kernel_path = jit ? "jit_tree4" : kind == FK_TREEM ? "treeM" : kind == FK_TREES ? "treeS" : "tree4";
   int first = 0;
@@ -1047,8 +1116,9 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       const double* pm = h->pmats;
       int base = first;
       void* args[] = {&ja, &pm, &base};
-      HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, grid.x, grid.y, 1, 64 * h->C, 1, 1, (unsigned)lds, h->stream, args,
-                                      nullptr));
+      const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, env_int("PLK_JIT_WGS", 2048, 1, 1 << 20));
+      HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * h->C * sh.G, 1, 1, (unsigned)sh.lds_bytes(),
+                                      h->stream, args, nullptr));
     } else if (kind == FK_TREEM) {
       launch_treeM(h, a, grid, lds_m);
     } else if (kind == FK_TREES) {

@@ -7,17 +7,28 @@
 // Counters on cfg2 (64 taxa, GTR+G4): per wave ~4.7k SALU + 1.4k branches next to
 // ~4.7k VALU, 42 % of wave cycles parked in s_waitcnt, VALU busy ~14 %.
 //
-// Here the same program (fragments and tiers from build_tree4_program) is emitted as
-// straight-line HIP source -- one `case` per fragment -- and compiled once per
-// (topology, C, flags) with hiprtc for gfx950.  Every P(t) address becomes a constant
-// offset from one wave-uniform base, so the compiler issues the s_loads early and
-// overlaps them with the previous events' FMAs; there is no decode, no program fetch
-// and no branch in a fragment.  The arithmetic of every event is exactly the
-// interpreter's (same helpers, same operation order), so results are bitwise those
-// of tree4_kernel<1, DM, SCALE>.  Compiled modules are cached per process, keyed by
-// the generated source (plk.hip: jit_function).
+// Here the same fragment programs (build_tree4_program: fragments and tiers) are
+// emitted as straight-line HIP source -- one `case` per fragment -- and compiled once
+// per (topology, C, codes in use, flags) with hiprtc for gfx950:
+//   * every P(t) address is a constant offset from one wave-uniform base, so P lives
+//     in SGPRs (s_load) and there is no decode, no program fetch and no branch;
+//   * a tip contributes through its table row tipP[tip][c][code][x] =
+//     sum_y P[c][x][y] init[code][y] (tip_table_kernel), staged in LDS once per
+//     workgroup for the fragment's tips: one 32-byte LDS read and 4 multiplies
+//     instead of a 4x4 matvec (16 FMAs) per tip;
+//   * the first contribution into a node's accumulator is an assignment (1 * s == s
+//     exactly), not a multiply;
+//   * workgroups are persistent over pattern super-blocks (64 * G patterns), so the
+//     tables are staged once per workgroup, not once per 64 patterns;
+//   * the operands of event i + L (tip row, or a materialised child partial) are
+//     fetched next to the compute of event i inside one scheduling region (closed by
+//     sched_barrier), which hides their latency while bounding registers.
+// Every arithmetic operation is the interpreter's, in the same order, so the results
+// are bitwise those of tree4_kernel<1, DM, SCALE>.  Modules are compiled and cached
+// per process by source (plk.hip: jit_function).
 #pragma once
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -25,28 +36,27 @@
 
 namespace plk {
 
-// Device helpers of the generated kernels (hiprtc compiles them with the program).
-// They restate contribute / rescale / store_partial / the fused root reduction of
-// plk_tree4.hpp for one class per wave.
+// Device helpers of the generated kernels.  They restate rescale / store_partial /
+// the fused root reduction of plk_tree4.hpp for one class per wave and G pattern
+// groups per workgroup (wave w: class w % C, group w / C).
 static const char* kJitPrelude = R"PLKJIT(
 typedef unsigned char u8;
 typedef long long i64;
 typedef int i32;
 typedef __attribute__((address_space(4))) const double* CPd;
 #define kTile 128
-__device__ const double kScaleUp = 115792089237316195423570985008687907853269984665640564039457584007913129639936.0;
-__device__ const double kScaleThr = 1.0 / 115792089237316195423570985008687907853269984665640564039457584007913129639936.0;
 #define kLn2x256 177.44567822334599921
+#define kScaleUp 115792089237316195423570985008687907853269984665640564039457584007913129639936.0
+#define kScaleThr (1.0 / kScaleUp)
 
 struct JArgs {
-  double* partials; i32* scale; const u8* codes; const double* init; const double* weights;
+  double* partials; i32* scale; const u8* codes; const double* tipP; const double* weights;
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
-  i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_codes; i32 n_tips; i32 guard; i32 pad_;
+  i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
 };
 
-__device__ __forceinline__ void one(double (&v)[4]) { v[0] = 1.0; v[1] = 1.0; v[2] = 1.0; v[3] = 1.0; }
-
-// dst[x] *= sum_y P[x][y] src[y]   (P row-major, this wave's class)
+// dst[x] (*)= sum_y P[x][y] src[y]   (P row-major, this wave's class); SET: dst was 1
+template <bool SET>
 __device__ __forceinline__ void contrib(double (&dst)[4], const double (&src)[4], CPd P) {
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
@@ -54,20 +64,29 @@ __device__ __forceinline__ void contrib(double (&dst)[4], const double (&src)[4]
     s = __builtin_fma(P[4 * x + 1], src[1], s);
     s = __builtin_fma(P[4 * x + 2], src[2], s);
     s = __builtin_fma(P[4 * x + 3], src[3], s);
-    dst[x] *= s;
+    if (SET) dst[x] = s; else dst[x] *= s;
   }
 }
 
-__device__ __forceinline__ void rescale(double (&v)[4], int& cnt, double* xmax, int nw) {
+template <bool SET>
+__device__ __forceinline__ void tipmul(double (&dst)[4], const double (&row)[4]) {
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    if (SET) dst[x] = row[x]; else dst[x] *= row[x];
+  }
+}
+
+template <int C>
+__device__ __forceinline__ void rescale(double (&v)[4], int& cnt, double* xch, int w, int g) {
   double m = 0.0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) m = fmax(m, v[i]);
-  if (nw > 1) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    xmax[w * 64 + lane] = m;
+  if (C > 1) {
+    const int lane = threadIdx.x & 63;
+    xch[w * 64 + lane] = m;
     __syncthreads();
     m = 0.0;
-    for (int k = 0; k < nw; ++k) m = fmax(m, xmax[k * 64 + lane]);
+    for (int k = 0; k < C; ++k) m = fmax(m, xch[(g * C + k) * 64 + lane]);
     __syncthreads();
   }
   if (m > 0.0 && m < kScaleThr) {
@@ -77,18 +96,17 @@ __device__ __forceinline__ void rescale(double (&v)[4], int& cnt, double* xmax, 
   }
 }
 
-template <int C, bool SCALE>
-__device__ __forceinline__ void store(const JArgs& a, int slot, i64 p, int c0, const double (&v)[4], int cnt) {
-  const i64 tile = p >> 7, q = p & (kTile - 1);
-  double* dst = a.partials + (i64)slot * a.slot_stride + tile * (C * 4 * kTile) + (i64)c0 * 4 * kTile + q;
+template <bool SCALE>
+__device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0, const double (&v)[4], int cnt) {
+  double* dst = a.partials + (i64)slot * a.slot_stride + off;
 #pragma unroll
   for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(v[i], dst + (i64)i * kTile);
   if (SCALE && c0 == 0) a.scale[(i64)slot * a.n_pad + p] = cnt;
 }
 
 template <int C, bool SCALE>
-__device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[4], int cnt, double* xch, int c0, i64 p0,
-                                            i64 p) {
+__device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[4], int cnt, double* xch, int w,
+                                            int g, int c0, i64 p0, i64 p) {
   const int lane = threadIdx.x & 63;
   double lc = 0.0;
 #pragma unroll
@@ -102,12 +120,12 @@ __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[
   }
   const double t = lc * a.probs[c0];
   __syncthreads();
-  xch[c0 * 64 + lane] = t;
+  xch[w * 64 + lane] = t;
   __syncthreads();
   if (c0 == 0) {
     double l = 0.0;
     for (int c = 0; c < C; ++c) {
-      const double li = xch[c * 64 + lane];
+      const double li = xch[(g * C + c) * 64 + lane];
       if (a.guard) {
         if (li > 0.0) l += li;
       } else {
@@ -134,7 +152,7 @@ struct JArgs {
   double* partials;
   int32_t* scale;
   const uint8_t* codes;
-  const double* init;
+  const double* tipP;
   const double* weights;
   const double* pi;
   const double* probs;
@@ -143,107 +161,156 @@ struct JArgs {
   int64_t slot_stride;
   int64_t n_pad;
   int64_t n_patterns;
-  int32_t n_codes;
-  int32_t n_tips;
+  int32_t n_sblocks;
   int32_t guard;
-  int32_t pad_;
 };
 
-// Emit the kernel for a tree program.  `prog` / `starts` are build_tree4_program's
-// words and fragment start offsets in tier order (fragment id = blockIdx.y + base).
-//
-// Each fragment is a list of events; an event has a FETCH part (tip code -> init row
-// from LDS, or a materialised child partial from HBM) and a COMPUTE part (the
-// contribution into its level).  The fetch of event i + L is emitted next to the
-// compute of event i, inside one scheduling region (regions are closed with
-// sched_barrier), so the LDS / HBM latency of the operands hides behind L events of
-// FMAs while the register footprint stays bounded (a ring of L + 1 operand vectors).
-// Without the regions the scheduler hoists every fetch of the fragment to its start
-// and spills.
+struct JitShape {
+  int C = 1;        // rate classes = waves per pattern group
+  int G = 1;        // 64-pattern groups per workgroup
+  int U = 1;        // codes in use (rows of a tip table)
+  int NT = 0;       // most tips of any fragment (LDS table slots)
+  bool scale = false;
+  int L = 1;        // operand fetch lookahead (events)
+  size_t lds_bytes() const {
+    const size_t nt = (size_t)std::max(NT, 1);
+    return nt * C * U * 4 * sizeof(double) + (size_t)G * C * 64 * sizeof(double) + (size_t)G * nt * 64;
+  }
+};
+
 struct JitEvent {
-  int op;     // T_TIP, T_LOAD, T_DESCEND, T_ASCEND (level >= 1), T_ROOT
+  int op;     // T_TIP (a = local tip index), T_LOAD, T_DESCEND, T_ASCEND (level >= 1), T_ROOT
   int level;  // accumulator level the event works on
   int a, b;   // program word fields
 };
 
-inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts, int C,
-                                    bool scale, bool stage_codes, int L) {
-  std::string s;
-  s.reserve(96 * prog.size() + 8192);
-  s += kJitPrelude;
-  char buf[320];
-  snprintf(buf, sizeof(buf),
-           "\nextern \"C\" __global__ __launch_bounds__(256) void plk_jit_tree4(JArgs a, const double* __restrict__ "
-           "pmats, int frag_base) {\n#define C_ %d\n#define SC_ %s\n#define STG_ %d\n",
-           C, scale ? "true" : "false", stage_codes ? 1 : 0);
-  s += buf;
-  s += R"PLKJIT(  extern __shared__ __attribute__((aligned(16))) double lds[];
-  double* init_lds = lds;
-  double* xch = lds + ((a.n_codes * 4 + 1) & ~1);
-  u8* code_lds = reinterpret_cast<u8*>(xch + 4 * 64);
-  const int nw = C_;
-  const int lane = threadIdx.x & 63;
-  const int c0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const i64 p0 = (i64)blockIdx.x * 64;
-  const i64 p = p0 + lane;
-  for (int i = threadIdx.x; i < a.n_codes * 4; i += blockDim.x) init_lds[i] = a.init[i];
-  if (STG_) {
-    for (int i = threadIdx.x; i < a.n_tips * 4; i += blockDim.x) {
-      const int t = i >> 2, j = i & 3;
-      reinterpret_cast<uint4*>(code_lds)[i] = *reinterpret_cast<const uint4*>(a.codes + (i64)t * a.n_pad + p0 + 16 * j);
-    }
-  }
-  __syncthreads();
-  const CPd pm = (CPd)(pmats + c0 * 16);
-  const i64 tile_off = (p >> 7) * (C_ * 4 * kTile) + (i64)c0 * 4 * kTile + (p & (kTile - 1));
-  (void)nw; (void)xch; (void)tile_off;
-#define TIPF(F, t) { const int code_ = STG_ ? code_lds[(t) * 64 + lane] : a.codes[(i64)(t) * a.n_pad + p]; \
-    const double2* iv_ = reinterpret_cast<const double2*>(init_lds + code_ * 4); const double2 x_ = iv_[0], y_ = iv_[1]; \
-    F[0] = x_.x; F[1] = x_.y; F[2] = y_.x; F[3] = y_.y; }
-#define LOADF(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + tile_off; \
-    F[0] = L_[0]; F[1] = L_[kTile]; F[2] = L_[2 * kTile]; F[3] = L_[3 * kTile]; \
-    if (SC_) FK = a.scale[(i64)(slot) * a.n_pad + p]; }
-#define SB __builtin_amdgcn_sched_barrier(0);
-)PLKJIT";
-  int max_level = 0;
-  {
-    int lvl = 0;
-    for (const TInstr& w : prog) {
-      if (w.op == T_DESCEND) max_level = std::max(max_level, ++lvl);
-      else if (w.op == T_ASCEND && lvl > 0) --lvl;
-      else if (w.op == T_ROOT) lvl = 0;
-    }
-  }
-  for (int d = 0; d <= max_level; ++d) {
-    snprintf(buf, sizeof(buf), "  double A%d[4]; int K%d = 0; (void)K%d;\n", d, d, d);
-    s += buf;
-  }
-  for (int r = 0; r <= L; ++r) {
-    snprintf(buf, sizeof(buf), "  double F%d[4]; int FK%d = 0; (void)FK%d;\n", r, r, r);
-    s += buf;
-  }
-  s += "  switch (frag_base + (int)blockIdx.y) {\n";
-  std::vector<JitEvent> ev;
+// Per fragment (tier order): its events, with TIP events renumbered to fragment-local
+// tip indices; tips[f] lists the fragment's tips (local index -> tip).
+inline void jit_fragments(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts,
+                          std::vector<std::vector<JitEvent> >& events, std::vector<std::vector<int> >& tips) {
+  events.assign(starts.size(), {});
+  tips.assign(starts.size(), {});
   for (size_t f = 0; f < starts.size(); ++f) {
-    ev.clear();
     int d = 0;
     for (size_t i = (size_t)starts[f];; ++i) {
       const TInstr& w = prog[i];
-      if (w.op == T_TIP || w.op == T_LOAD) {
-        ev.push_back({w.op, d, w.a, w.b});
+      if (w.op == T_TIP) {
+        events[f].push_back({T_TIP, d, (int)tips[f].size(), w.b});
+        tips[f].push_back(w.a);
+      } else if (w.op == T_LOAD) {
+        events[f].push_back({T_LOAD, d, w.a, w.b});
       } else if (w.op == T_DESCEND) {
         ++d;
-        ev.push_back({T_DESCEND, d, 0, 0});
+        events[f].push_back({T_DESCEND, d, 0, 0});
       } else if (w.op == T_ASCEND) {
         if (d == 0) continue;  // fragment root: finished by ROOT
-        ev.push_back({T_ASCEND, d, w.a, w.b});
+        events[f].push_back({T_ASCEND, d, w.a, w.b});
         --d;
       } else if (w.op == T_ROOT) {
-        ev.push_back({T_ROOT, 0, w.a, w.b});
+        events[f].push_back({T_ROOT, 0, w.a, w.b});
         break;
       }
     }
-    // fetching events (TIP / LOAD) get ring slots in order
+  }
+}
+
+// Most tips of any fragment (LDS table slots the kernel needs).
+inline int jit_max_fragment_tips(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts) {
+  int best = 0;
+  for (size_t f = 0; f < starts.size(); ++f) {
+    int n = 0;
+    for (size_t i = (size_t)starts[f]; prog[i].op != T_ROOT; ++i) n += prog[i].op == T_TIP;
+    best = std::max(best, n);
+  }
+  return best;
+}
+
+// Emit the kernel for a tree program (`prog` / `starts`: build_tree4_program's words
+// and fragment start offsets in tier order; fragment id = frag_base + blockIdx.y).
+inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts,
+                                    const JitShape& sh) {
+  std::vector<std::vector<JitEvent> > events;
+  std::vector<std::vector<int> > tips;
+  jit_fragments(prog, starts, events, tips);
+  const int C = sh.C, L = std::max(sh.L, 1);
+  std::string s;
+  s.reserve(100 * prog.size() + 8192);
+  s += kJitPrelude;
+  char buf[400];
+  // fragment tip lists (CSR) as constant data of the module; entry 0 of kFragTips is
+  // padding: tip k of fragment f is kFragTips[1 + kFragTipStart[f] + k]
+  s += "\n__device__ const int kFragTipStart[] = {0";
+  {
+    int acc = 0;
+    for (const auto& t : tips) {
+      acc += (int)t.size();
+      snprintf(buf, sizeof(buf), ",%d", acc);
+      s += buf;
+    }
+  }
+  s += "};\n__device__ const int kFragTips[] = {0";
+  for (const auto& t : tips)
+    for (int x : t) {
+      snprintf(buf, sizeof(buf), ",%d", x);
+      s += buf;
+    }
+  s += "};\n";
+  snprintf(buf, sizeof(buf),
+           "#define C_ %d\n#define G_ %d\n#define U_ %d\n#define NT_ %d\n#define SC_ %s\n"
+           "extern \"C\" __global__ __launch_bounds__(%d) void plk_jit_tree4(JArgs a, const double* __restrict__ "
+           "pmats, int frag_base) {\n",
+           C, sh.G, sh.U, std::max(sh.NT, 1), sh.scale ? "true" : "false", 64 * C * sh.G);
+  s += buf;
+  s += R"PLKJIT(  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* tab = lds;                                          // [NT_][C_][U_][4]
+  double* xch = tab + NT_ * C_ * U_ * 4;                      // [G_ * C_][64]
+  u8* code_lds = reinterpret_cast<u8*>(xch + G_ * C_ * 64);   // [G_][NT_][64]
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = w % C_, g = w / C_;
+  const int frag = frag_base + (int)blockIdx.y;
+  const int t0 = 1 + kFragTipStart[frag], nt = kFragTipStart[frag + 1] - kFragTipStart[frag];
+  for (int i = threadIdx.x; i < nt * (C_ * U_ * 4); i += blockDim.x) {
+    const int k = i / (C_ * U_ * 4), r = i - k * (C_ * U_ * 4);
+    tab[i] = a.tipP[(i64)kFragTips[t0 + k] * (C_ * U_ * 4) + r];
+  }
+  const CPd pm = (CPd)(pmats + c0 * 16);
+  const double* trow = tab + c0 * (U_ * 4);
+  const u8* crow = code_lds + g * (NT_ * 64) + lane;
+  (void)xch; (void)trow; (void)crow;
+#define TIPF(F, k) { const double2* r_ = reinterpret_cast<const double2*>(trow + ((k) * (C_ * U_) + crow[(k) * 64]) * 4); \
+    const double2 x_ = r_[0], y_ = r_[1]; F[0] = x_.x; F[1] = x_.y; F[2] = y_.x; F[3] = y_.y; }
+#define LOADF(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
+    F[0] = L_[0]; F[1] = L_[kTile]; F[2] = L_[2 * kTile]; F[3] = L_[3 * kTile]; \
+    if (SC_) FK = a.scale[(i64)(slot) * a.n_pad + p]; }
+#define SB __builtin_amdgcn_sched_barrier(0);
+  for (int sb = blockIdx.x; sb < a.n_sblocks; sb += gridDim.x) {
+    const i64 q0 = (i64)sb * (64 * G_);
+    const i64 p0 = q0 + g * 64, p = p0 + lane;
+    const i64 toff = (p >> 7) * (C_ * 4 * kTile) + (i64)c0 * 4 * kTile + (p & (kTile - 1));
+    (void)toff;
+    __syncthreads();  // the previous super-block is done with code_lds / xch (and tab is staged)
+    for (int i = threadIdx.x; i < G_ * nt * 4; i += blockDim.x) {
+      const int gg = i / (nt * 4), r = i - gg * (nt * 4), k = r >> 2, j = r & 3;
+      reinterpret_cast<uint4*>(code_lds)[(gg * NT_ + k) * 4 + j] =
+          *reinterpret_cast<const uint4*>(a.codes + (i64)kFragTips[t0 + k] * a.n_pad + q0 + gg * 64 + 16 * j);
+    }
+    __syncthreads();
+)PLKJIT";
+  int max_level = 0;
+  for (const auto& ev : events)
+    for (const JitEvent& e : ev) max_level = std::max(max_level, e.level);
+  for (int d = 0; d <= max_level; ++d) {
+    snprintf(buf, sizeof(buf), "    double A%d[4]; int K%d = 0; (void)K%d;\n", d, d, d);
+    s += buf;
+  }
+  for (int r = 0; r <= L; ++r) {
+    snprintf(buf, sizeof(buf), "    double F%d[4]; int FK%d = 0; (void)FK%d;\n", r, r, r);
+    s += buf;
+  }
+  s += "    switch (frag) {\n";
+  for (size_t f = 0; f < events.size(); ++f) {
+    const std::vector<JitEvent>& ev = events[f];
     std::vector<int> slot(ev.size(), -1), fetchers;
     for (size_t i = 0; i < ev.size(); ++i)
       if (ev[i].op == T_TIP || ev[i].op == T_LOAD) {
@@ -253,65 +320,72 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
     auto emit_fetch = [&](int i) {
       const JitEvent& e = ev[(size_t)i];
       if (e.op == T_TIP)
-        snprintf(buf, sizeof(buf), "    TIPF(F%d, %d)\n", slot[(size_t)i], e.a);
+        snprintf(buf, sizeof(buf), "      TIPF(F%d, %d)\n", slot[(size_t)i], e.a);
       else
-        snprintf(buf, sizeof(buf), "    LOADF(F%d, FK%d, %d)\n", slot[(size_t)i], slot[(size_t)i], e.a);
+        snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %d)\n", slot[(size_t)i], slot[(size_t)i], e.a);
       s += buf;
     };
-    snprintf(buf, sizeof(buf), "  case %zu: {\n    one(A0); K0 = 0;\n", f);
+    snprintf(buf, sizeof(buf), "    case %zu: {\n      K0 = 0;\n", f);
     s += buf;
-    size_t nf = 0;  // fetches emitted
+    std::vector<char> fresh((size_t)max_level + 1, 0);
+    fresh[0] = 1;
+    size_t nf = 0;
     for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
-    s += "    SB\n";
-    size_t done_fetchers = 0;
+    s += "      SB\n";
     for (size_t i = 0; i < ev.size(); ++i) {
       const JitEvent& e = ev[i];
       const long long off = (long long)e.b * C * 16;
       if (e.op == T_TIP || e.op == T_LOAD) {
-        // keep L fetches in flight: issue the one L events ahead of this fetcher
         if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
-        snprintf(buf, sizeof(buf), "    contrib(A%d, F%d, pm + %lld);\n", e.level, slot[i], off);
+        const char* set = fresh[(size_t)e.level] ? "true" : "false";
+        if (e.op == T_TIP)
+          snprintf(buf, sizeof(buf), "      tipmul<%s>(A%d, F%d);\n", set, e.level, slot[i]);
+        else
+          snprintf(buf, sizeof(buf), "      contrib<%s>(A%d, F%d, pm + %lld);\n", set, e.level, slot[i], off);
         s += buf;
-        if (e.op == T_LOAD && scale) {
-          snprintf(buf, sizeof(buf), "    K%d += FK%d;\n", e.level, slot[i]);
+        fresh[(size_t)e.level] = 0;
+        if (e.op == T_LOAD && sh.scale) {
+          snprintf(buf, sizeof(buf), "      K%d += FK%d;\n", e.level, slot[i]);
           s += buf;
         }
-        ++done_fetchers;
-        s += "    SB\n";
+        s += "      SB\n";
       } else if (e.op == T_DESCEND) {
-        snprintf(buf, sizeof(buf), "    one(A%d); K%d = 0;\n", e.level, e.level);
+        fresh[(size_t)e.level] = 1;
+        snprintf(buf, sizeof(buf), "      K%d = 0;\n", e.level);
         s += buf;
       } else if (e.op == T_ASCEND) {
         const int dd = e.level;
         if (e.b >= 0) {
-          if (scale) {
-            snprintf(buf, sizeof(buf), "    rescale(A%d, K%d, xch, nw);\n", dd, dd);
+          if (sh.scale) {
+            snprintf(buf, sizeof(buf), "      rescale<C_>(A%d, K%d, xch, w, g);\n", dd, dd);
             s += buf;
           }
           if (e.a >= 0) {
-            snprintf(buf, sizeof(buf), "    store<C_, SC_>(a, %d, p, c0, A%d, K%d);\n", e.a, dd, dd);
+            snprintf(buf, sizeof(buf), "      store<SC_>(a, %d, toff, p, c0, A%d, K%d);\n", e.a, dd, dd);
             s += buf;
           }
         }
-        snprintf(buf, sizeof(buf), "    contrib(A%d, A%d, pm + %lld);\n", dd - 1, dd, off);
+        snprintf(buf, sizeof(buf), "      contrib<%s>(A%d, A%d, pm + %lld);\n",
+                 fresh[(size_t)dd - 1] ? "true" : "false", dd - 1, dd, off);
         s += buf;
-        if (scale) {
-          snprintf(buf, sizeof(buf), "    K%d += K%d;\n", dd - 1, dd);
+        fresh[(size_t)dd - 1] = 0;
+        if (sh.scale) {
+          snprintf(buf, sizeof(buf), "      K%d += K%d;\n", dd - 1, dd);
           s += buf;
         }
-        s += "    SB\n";
+        s += "      SB\n";
       } else {  // T_ROOT
-        if (scale) s += "    rescale(A0, K0, xch, nw);\n";
+        if (sh.scale) s += "      rescale<C_>(A0, K0, xch, w, g);\n";
         if (e.a >= 0) {
-          snprintf(buf, sizeof(buf), "    store<C_, SC_>(a, %d, p, c0, A0, K0);\n", e.a);
+          snprintf(buf, sizeof(buf), "      store<SC_>(a, %d, toff, p, c0, A0, K0);\n", e.a);
           s += buf;
         }
-        if (e.b) s += "    reduce_root<C_, SC_>(a, A0, K0, xch, c0, p0, p);\n";
+        if (e.b) s += "      reduce_root<C_, SC_>(a, A0, K0, xch, w, g, c0, p0, p);\n";
       }
     }
-    s += "  } break;\n";
+    s += "    } break;\n";
   }
-  s += "  default: break;\n  }\n#undef C_\n#undef SC_\n#undef STG_\n}\n";
+  s += "    default: break;\n    }\n  }\n}\n";
   return s;
 }
 
