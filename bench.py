@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=None, help="patterns in the CPU-baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true", help="A/B: time the steps without per-kernel HIP events")
     ap.add_argument("--mode", default="lnl", choices=["lnl", "materialize", "levelwise"],
                     help="lnl: fused traversal, interior partials kept in registers (recomputed on demand); "
                          "materialize: fused traversal writing every partial; levelwise: one launch per level")
@@ -182,7 +183,8 @@ def main():
     for _ in range(args.warmup):
         lnl = one_step()
     ev.eng.reset_timing()
-    ev.eng.set_timing(True)
+    # HIP events around the partials launches only (each timed launch adds an event pair)
+    ev.eng.set_timing(0 if args.no_events else plk.PLK_TIME_PARTIALS)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -209,7 +211,7 @@ def main():
         launches = max(tm["launches"], 1)
         traffic, traffic_src = measured_traffic(args.config, args.mode, P, launches / args.steps)
         roof = roofline(wl, args.mode, P, args.steps, part_s, launches, bytes_pattern, flops_pattern, traffic)
-        if traffic_src:
+        if traffic_src and roof:
             roof["traffic_source"] = traffic_src
         rec = {
             "metric": "site-pattern x node partial updates/s",

@@ -80,15 +80,20 @@ struct plk_handle_s {
   size_t d_ops_cap = 0;
   void* d_req = nullptr;
   size_t d_req_cap = 0;
+  // pinned host staging: P(t) requests (reused once req_done has passed) and block sums
+  char* h_req = nullptr;
+  size_t h_req_cap = 0;
+  hipEvent_t req_done = nullptr;
+  double* h_blocks = nullptr;
   int64_t slot_stride = 0;
   // state
   bool rates_set = false, pi_set = false, table_set = false;
   std::vector<char> pmat_valid;   // per node
   std::vector<char> eigen_set;    // per model
-  bool tip_tables_dirty = true;
+  std::vector<char> tip_table_valid;  // per tip: tipP row matches its P(t) and the code table
   std::vector<char> tip_set;
   // instrumentation
-  bool timing = false;
+  unsigned timing = 0;  // PLK_TIME_* mask
   std::vector<EventPair> events;
   std::vector<EventPair> event_pool;
   int64_t n_launches = 0;
@@ -131,6 +136,7 @@ struct plk_handle_s {
   std::vector<int32_t> frag_starts_host;  // fragment start offsets, tier order
   hipFunction_t jit_fn = nullptr;
   JitShape jit_shape;
+  int jit_resident = 0;  // workgroups of jit_fn resident at once on the device
   std::string kernel_path;                // what served the last plk_update_partials
 };
 
@@ -330,7 +336,8 @@ int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs
 }
 
 int refresh_tip_tables(plk_handle h) {
-  if (!h->tip_tables_dirty) return PLK_OK;
+  if (std::all_of(h->tip_table_valid.begin(), h->tip_table_valid.end(), [](char v) { return v != 0; }))
+    return PLK_OK;
   if (!h->table_set) return fail(h, PLK_ERR_STATE, "code table not set (plk_set_code_table)");
   for (int t = 0; t < h->n_tips; ++t)
     if (!h->pmat_valid[t]) return fail(h, PLK_ERR_STATE, "transition matrix of tip branch %d not set", t);
@@ -340,7 +347,7 @@ int refresh_tip_tables(plk_handle h) {
                                                   h->n_codes);
     HIPCHK(h, hipGetLastError());
   }
-  h->tip_tables_dirty = false;
+  std::fill(h->tip_table_valid.begin(), h->tip_table_valid.end(), 1);
   return PLK_OK;
 }
 
@@ -357,7 +364,7 @@ int upload_compact_table(plk_handle h) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hipMemcpy(h->code_table, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
   h->n_codes = U;
-  h->tip_tables_dirty = true;
+  h->tip_table_valid.assign(h->n_tips, 0);
   return PLK_OK;
 }
 
@@ -420,6 +427,7 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   h->pmat_valid.assign(h->n_nodes, 0);
   h->eigen_set.assign(n_models, 0);
   h->tip_set.assign(n_tips, 0);
+  h->tip_table_valid.assign(n_tips, 0);
   int rc = PLK_OK;
   auto bail = [&](int code) {
     plk_destroy(h);
@@ -468,6 +476,9 @@ int plk_destroy(plk_handle h) {
                   h->d2_sums, h->d_dprog, h->pmatsT};
   for (void* p : bufs)
     if (p) hipFree(p);
+  if (h->h_req) hipHostFree(h->h_req);
+  if (h->h_blocks) hipHostFree(h->h_blocks);
+  if (h->req_done) hipEventDestroy(h->req_done);
   for (auto& e : h->events) {
     hipEventDestroy(e.a);
     hipEventDestroy(e.b);
@@ -603,14 +614,24 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   const size_t bytes = (size_t)n * (2 * sizeof(int32_t) + sizeof(double)) + 64;
   int rc = ensure_cap(h, &h->d_req, &h->d_req_cap, bytes);
   if (rc) return rc;
-  std::vector<char> staging(bytes, 0);
+  // pinned staging, stream-ordered copy: the host does not wait for the GPU here (only
+  // for the previous request's copy, before it reuses the staging buffer)
+  if (!h->req_done) HIPCHK(h, hipEventCreateWithFlags(&h->req_done, hipEventDisableTiming));
+  HIPCHK(h, hipEventSynchronize(h->req_done));
+  if (h->h_req_cap < bytes) {
+    if (h->h_req) HIPCHK(h, hipHostFree(h->h_req));
+    h->h_req = nullptr;
+    h->h_req_cap = 0;
+    HIPCHK(h, hipHostMalloc((void**)&h->h_req, bytes, hipHostMallocDefault));
+    h->h_req_cap = bytes;
+  }
+  char* staging = h->h_req;
   const size_t off_t = 0, off_b = (size_t)n * sizeof(double), off_m = off_b + (size_t)n * sizeof(int32_t);
-  std::memcpy(staging.data() + off_t, t, n * sizeof(double));
-  std::memcpy(staging.data() + off_b, branch, n * sizeof(int32_t));
-  if (model) std::memcpy(staging.data() + off_m, model, n * sizeof(int32_t));
-  // synchronous copy keeps the pageable staging buffer safe; it is tiny
-  HIPCHK(h, hipMemcpyAsync(h->d_req, staging.data(), bytes, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  std::memcpy(staging + off_t, t, n * sizeof(double));
+  std::memcpy(staging + off_b, branch, n * sizeof(int32_t));
+  if (model) std::memcpy(staging + off_m, model, n * sizeof(int32_t));
+  HIPCHK(h, hipMemcpyAsync(h->d_req, staging, bytes, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipEventRecord(h->req_done, h->stream));
   PmatArgs a;
   a.t = reinterpret_cast<const double*>((char*)h->d_req + off_t);
   a.branch = reinterpret_cast<const int32_t*>((char*)h->d_req + off_b);
@@ -625,15 +646,22 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   a.S = h->S;
   a.C = h->C;
   a.mask = deriv_mask;
+  // tip tables ride along for S <= 20 (P of the block staged in LDS; S = 64 keeps the
+  // separate tip_table_kernel)
+  const bool tips_fused = h->table_set && h->S <= 20;
+  a.init = tips_fused ? h->code_table : nullptr;
+  a.tipP = h->tipP;
+  a.n_tips = h->n_tips;
+  a.n_codes = h->n_codes;
   EventPair ev;
-  if (h->timing) {
+  if (h->timing & PLK_TIME_PMAT) {
     ev = get_events(h, 1);
     hipEventRecord(ev.a, h->stream);
   }
-  const size_t lds = (size_t)(h->S + S2) * sizeof(double);
+  const size_t lds = (size_t)(h->S + (tips_fused ? 2 : 1) * S2) * sizeof(double);
   pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a);
   HIPCHK(h, hipGetLastError());
-  if (h->timing) {
+  if (h->timing & PLK_TIME_PMAT) {
     hipEventRecord(ev.b, h->stream);
     h->events.push_back(ev);
   }
@@ -641,7 +669,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     for (int i = 0; i < n; ++i) {
       h->pmat_valid[branch[i]] = 1;
       h->pmatsT_dirty = true;
-      if (branch[i] < h->n_tips) h->tip_tables_dirty = true;
+      if (branch[i] < h->n_tips) h->tip_table_valid[branch[i]] = tips_fused ? 1 : 0;  // row written by pmat_kernel
     }
   }
   if (h->deriv_valid.empty()) h->deriv_valid.assign(h->n_nodes, 0);
@@ -661,7 +689,7 @@ int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
   h->pmat_valid[branch] = 1;
   h->pmatsT_dirty = true;
   if (!h->deriv_valid.empty()) h->deriv_valid[branch] = 0;
-  if (branch < h->n_tips) h->tip_tables_dirty = true;
+  if (branch < h->n_tips) h->tip_table_valid[branch] = 0;
   return PLK_OK;
 }
 
@@ -1079,13 +1107,18 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.NT = jit_max_fragment_tips(h->prog_host, h->frag_starts_host);
     sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     sh.L = env_int("PLK_JIT_L", 1, 1, 8);
+    sh.LP = env_int("PLK_JIT_LP", 0, 0, 4);  // measured: SGPR ring spills, 6x slower at 1
+    sh.minw = env_int("PLK_JIT_MINW", 0, 0, 8);
+    sh.same_p = env_is("PLK_DEBUG_SAMEP", '1');
     if (sh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
     if (!h->jit_fn || sh.C != h->jit_shape.C || sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
-        sh.NT != h->jit_shape.NT || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L) {
+        sh.NT != h->jit_shape.NT || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
+        sh.LP != h->jit_shape.LP || sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p) {
       int rc = jit_function(h, jit_tree4_source(h->prog_host, h->frag_starts_host, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
+      h->jit_resident = 0;
     }
     ja.partials = a.partials;
     ja.scale = a.scale;
@@ -1108,7 +1141,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     a.frag_start = h->d_frag + first;
     dim3 grid((unsigned)(h->n_pad / 64), (unsigned)t.size());
     EventPair ev;
-    if (h->timing) {
+    if (h->timing & PLK_TIME_PARTIALS) {
       ev = get_events(h, 0);
       hipEventRecord(ev.a, h->stream);
     }
@@ -1116,7 +1149,20 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       const double* pm = h->pmats;
       int base = first;
       void* args[] = {&ja, &pm, &base};
-      const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, env_int("PLK_JIT_WGS", 2048, 1, 1 << 20));
+      // persistent grid: as many workgroups as are resident at once (occupancy query), so
+      // every workgroup stages its tables once and there is no second dispatch round
+      int wgs = env_int("PLK_JIT_WGS", 0, 0, 1 << 20);
+      if (wgs == 0) {
+        if (h->jit_resident <= 0) {
+          int per_cu = 0, n_cu = 0;
+          HIPCHK(h, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, h->jit_fn, 64 * h->C * sh.G,
+                                                                       sh.lds_bytes()));
+          HIPCHK(h, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, h->device));
+          h->jit_resident = std::max(1, per_cu) * std::max(1, n_cu);
+        }
+        wgs = h->jit_resident;
+      }
+      const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, wgs);
       HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * h->C * sh.G, 1, 1, (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
     } else if (kind == FK_TREEM) {
@@ -1131,7 +1177,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       }
     }
     HIPCHK(h, hipGetLastError());
-    if (h->timing) {
+    if (h->timing & PLK_TIME_PARTIALS) {
       hipEventRecord(ev.b, h->stream);
       h->events.push_back(ev);
     }
@@ -1220,7 +1266,7 @@ int update_levelwise(plk_handle h, const plk_op* ops, int n_ops) {
     if (cnt == 0) continue;
     const KOp* d = h->d_ops + level_start[l];
     EventPair ev;
-    if (h->timing) {
+    if (h->timing & PLK_TIME_PARTIALS) {
       ev = get_events(h, 0);
       hipEventRecord(ev.a, h->stream);
     }
@@ -1234,7 +1280,7 @@ int update_levelwise(plk_handle h, const plk_op* ops, int n_ops) {
       if (rc) return rc;
     }
     HIPCHK(h, hipGetLastError());
-    if (h->timing) {
+    if (h->timing & PLK_TIME_PARTIALS) {
       hipEventRecord(ev.b, h->stream);
       h->events.push_back(ev);
     }
@@ -1325,7 +1371,7 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
   if (h->fused_lnl_valid && h->fused_lnl_root == root) {
     // the fused traversal already reduced the root: only the block sums remain
     const int n_waves = (int)((h->n_patterns + 63) / 64);
-    wave_sums_to_blocks<<<(h->n_blocks + 255) / 256, 256, 0, h->stream>>>(h->wave_sums, h->block_sums, n_waves,
+    wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, h->block_sums, n_waves,
                                                                           h->n_blocks);
     HIPCHK(h, hipGetLastError());
   } else {
@@ -1333,16 +1379,18 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
     int rc = launch_root(h, root);
     if (rc) return rc;
   }
-  std::vector<double> bs(h->n_blocks);
-  HIPCHK(h, hipMemcpyAsync(bs.data(), h->block_sums, bs.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  if (!h->h_blocks) HIPCHK(h, hipHostMalloc((void**)&h->h_blocks, (size_t)h->n_blocks * sizeof(double),
+                                            hipHostMallocDefault));
+  HIPCHK(h, hipMemcpyAsync(h->h_blocks, h->block_sums, (size_t)h->n_blocks * sizeof(double), hipMemcpyDeviceToHost,
+                           h->stream));
   if (site_lnl)
     HIPCHK(h, hipMemcpyAsync(site_lnl, h->site_lnl, (size_t)h->n_patterns * sizeof(double), hipMemcpyDeviceToHost,
                              h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   double s = 0.0;
-  for (double v : bs) s += v;  // fixed order: block 0, 1, 2, ...
+  for (int b = 0; b < h->n_blocks; ++b) s += h->h_blocks[b];  // fixed order: block 0, 1, 2, ...
   if (lnl) *lnl = s;
-  if (block_sums) std::memcpy(block_sums, bs.data(), bs.size() * sizeof(double));
+  if (block_sums) std::memcpy(block_sums, h->h_blocks, (size_t)h->n_blocks * sizeof(double));
   return PLK_OK;
 }
 
@@ -1360,17 +1408,17 @@ static int launch_root(plk_handle h, int root) {
   a.C = h->C;
   a.guard = (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0;
   EventPair ev;
-  if (h->timing) {
+  if (h->timing & PLK_TIME_ROOT) {
     ev = get_events(h, 2);
     hipEventRecord(ev.a, h->stream);
   }
   root_kernel<<<(unsigned)(h->n_pad / 64), 64, 0, h->stream>>>(a);
   HIPCHK(h, hipGetLastError());
   const int n_waves = (int)((h->n_patterns + 63) / 64);
-  wave_sums_to_blocks<<<(h->n_blocks + 255) / 256, 256, 0, h->stream>>>(h->wave_sums, h->block_sums, n_waves,
+  wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, h->block_sums, n_waves,
                                                                         h->n_blocks);
   HIPCHK(h, hipGetLastError());
-  if (h->timing) {
+  if (h->timing & PLK_TIME_ROOT) {
     hipEventRecord(ev.b, h->stream);
     h->events.push_back(ev);
   }
@@ -1477,7 +1525,7 @@ int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
 
 int plk_set_timing(plk_handle h, int enable) {
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
-  h->timing = enable != 0;
+  h->timing = (unsigned)enable;
   return PLK_OK;
 }
 

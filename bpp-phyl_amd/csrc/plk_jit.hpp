@@ -68,6 +68,19 @@ __device__ __forceinline__ void contrib(double (&dst)[4], const double (&src)[4]
   }
 }
 
+// the same with P already in registers (prefetched ring slot)
+template <bool SET>
+__device__ __forceinline__ void contribr(double (&dst)[4], const double (&src)[4], const double (&P)[16]) {
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    double s = P[4 * x + 0] * src[0];
+    s = __builtin_fma(P[4 * x + 1], src[1], s);
+    s = __builtin_fma(P[4 * x + 2], src[2], s);
+    s = __builtin_fma(P[4 * x + 3], src[3], s);
+    if (SET) dst[x] = s; else dst[x] *= s;
+  }
+}
+
 template <bool SET>
 __device__ __forceinline__ void tipmul(double (&dst)[4], const double (&row)[4]) {
 #pragma unroll
@@ -172,6 +185,9 @@ struct JitShape {
   int NT = 0;       // most tips of any fragment (LDS table slots)
   bool scale = false;
   int L = 1;        // operand fetch lookahead (events)
+  int LP = 0;       // P(t) prefetch lookahead (P-consuming events; 0: load at use)
+  int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
+  bool same_p = false;  // timing experiments only: every internal branch reads P(t) of node 0
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     return nt * C * U * 4 * sizeof(double) + (size_t)G * C * 64 * sizeof(double) + (size_t)G * nt * 64;
@@ -237,6 +253,7 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
   s.reserve(100 * prog.size() + 8192);
   s += kJitPrelude;
   char buf[400];
+  const std::string minw_s = sh.minw > 0 ? ", " + std::to_string(sh.minw) : std::string();
   // fragment tip lists (CSR) as constant data of the module; entry 0 of kFragTips is
   // padding: tip k of fragment f is kFragTips[1 + kFragTipStart[f] + k]
   s += "\n__device__ const int kFragTipStart[] = {0";
@@ -257,9 +274,9 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
   s += "};\n";
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define G_ %d\n#define U_ %d\n#define NT_ %d\n#define SC_ %s\n"
-           "extern \"C\" __global__ __launch_bounds__(%d) void plk_jit_tree4(JArgs a, const double* __restrict__ "
+           "extern \"C\" __global__ __launch_bounds__(%d%s) void plk_jit_tree4(JArgs a, const double* __restrict__ "
            "pmats, int frag_base) {\n",
-           C, sh.G, sh.U, std::max(sh.NT, 1), sh.scale ? "true" : "false", 64 * C * sh.G);
+           C, sh.G, sh.U, std::max(sh.NT, 1), sh.scale ? "true" : "false", 64 * C * sh.G, minw_s.c_str());
   s += buf;
   s += R"PLKJIT(  extern __shared__ __attribute__((aligned(16))) double lds[];
   double* tab = lds;                                          // [NT_][C_][U_][4]
@@ -283,6 +300,7 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
 #define LOADF(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
     F[0] = L_[0]; F[1] = L_[kTile]; F[2] = L_[2 * kTile]; F[3] = L_[3 * kTile]; \
     if (SC_) FK = a.scale[(i64)(slot) * a.n_pad + p]; }
+#define PF(Q, off) { const CPd P_ = pm + (off); _Pragma("unroll") for (int i_ = 0; i_ < 16; ++i_) Q[i_] = P_[i_]; }
 #define SB __builtin_amdgcn_sched_barrier(0);
   for (int sb = blockIdx.x; sb < a.n_sblocks; sb += gridDim.x) {
     const i64 q0 = (i64)sb * (64 * G_);
@@ -308,6 +326,11 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
     snprintf(buf, sizeof(buf), "    double F%d[4]; int FK%d = 0; (void)FK%d;\n", r, r, r);
     s += buf;
   }
+  const int LP = std::max(sh.LP, 0);
+  for (int r = 0; LP > 0 && r <= LP; ++r) {
+    snprintf(buf, sizeof(buf), "    double Q%d[16];\n", r);
+    s += buf;
+  }
   s += "    switch (frag) {\n";
   for (size_t f = 0; f < events.size(); ++f) {
     const std::vector<JitEvent>& ev = events[f];
@@ -317,6 +340,27 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
         slot[i] = (int)(fetchers.size() % (size_t)(L + 1));
         fetchers.push_back((int)i);
       }
+    // P-consuming events (LOAD, ASCEND) and their P ring slots
+    std::vector<int> pslot(ev.size(), -1), pevents;
+    for (size_t i = 0; i < ev.size(); ++i)
+      if (ev[i].op == T_LOAD || ev[i].op == T_ASCEND) {
+        pslot[i] = LP > 0 ? (int)(pevents.size() % (size_t)(LP + 1)) : -1;
+        pevents.push_back((int)i);
+      }
+    size_t np = 0;  // P prefetches emitted
+    auto emit_pf = [&](int i) {
+      snprintf(buf, sizeof(buf), "      PF(Q%d, %lld)\n", pslot[(size_t)i],
+               sh.same_p ? 0LL : (long long)ev[(size_t)i].b * C * 16);
+      s += buf;
+    };
+    auto pref = [&](size_t i) -> std::string {  // P operand of event i
+      if (LP > 0) {
+        snprintf(buf, sizeof(buf), "Q%d", pslot[i]);
+      } else {
+        snprintf(buf, sizeof(buf), "pm + %lld", sh.same_p ? 0LL : (long long)ev[i].b * C * 16);
+      }
+      return buf;
+    };
     auto emit_fetch = [&](int i) {
       const JitEvent& e = ev[(size_t)i];
       if (e.op == T_TIP)
@@ -331,6 +375,7 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
     fresh[0] = 1;
     size_t nf = 0;
     for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
+    for (; LP > 0 && np < pevents.size() && np < (size_t)LP; ++np) emit_pf(pevents[np]);
     s += "      SB\n";
     for (size_t i = 0; i < ev.size(); ++i) {
       const JitEvent& e = ev[i];
@@ -338,11 +383,16 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
       if (e.op == T_TIP || e.op == T_LOAD) {
         if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
         const char* set = fresh[(size_t)e.level] ? "true" : "false";
-        if (e.op == T_TIP)
+        if (e.op == T_TIP) {
           snprintf(buf, sizeof(buf), "      tipmul<%s>(A%d, F%d);\n", set, e.level, slot[i]);
-        else
-          snprintf(buf, sizeof(buf), "      contrib<%s>(A%d, F%d, pm + %lld);\n", set, e.level, slot[i], off);
-        s += buf;
+          s += buf;
+        } else {
+          if (LP > 0 && np < pevents.size()) emit_pf(pevents[np++]);
+          const std::string pr = pref(i);
+          snprintf(buf, sizeof(buf), "      %s<%s>(A%d, F%d, %s);\n", LP > 0 ? "contribr" : "contrib", set, e.level,
+                   slot[i], pr.c_str());
+          s += buf;
+        }
         fresh[(size_t)e.level] = 0;
         if (e.op == T_LOAD && sh.scale) {
           snprintf(buf, sizeof(buf), "      K%d += FK%d;\n", e.level, slot[i]);
@@ -365,8 +415,10 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
             s += buf;
           }
         }
-        snprintf(buf, sizeof(buf), "      contrib<%s>(A%d, A%d, pm + %lld);\n",
-                 fresh[(size_t)dd - 1] ? "true" : "false", dd - 1, dd, off);
+        if (LP > 0 && np < pevents.size()) emit_pf(pevents[np++]);
+        const std::string pr = pref(i);
+        snprintf(buf, sizeof(buf), "      %s<%s>(A%d, A%d, %s);\n", LP > 0 ? "contribr" : "contrib",
+                 fresh[(size_t)dd - 1] ? "true" : "false", dd - 1, dd, pr.c_str());
         s += buf;
         fresh[(size_t)dd - 1] = 0;
         if (sh.scale) {

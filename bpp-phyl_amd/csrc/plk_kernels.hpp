@@ -361,6 +361,9 @@ struct PmatArgs {
   double* P;               // [n_nodes][C][S][S]
   double* dP;
   double* d2P;
+  const double* init;      // [n_codes][S] code table (null: no tip tables)
+  double* tipP;            // [n_tips][C][n_codes][S]
+  int n_tips, n_codes;
   int S, C;
   unsigned mask;
 };
@@ -398,6 +401,20 @@ __global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a) {
     if (a.mask & 1u) a.P[off + idx] = p;
     if (a.mask & 2u) a.dP[off + idx] = rc * dp;
     if (a.mask & 4u) a.d2P[off + idx] = rc * rc * d2p;
+    if (a.init && b < a.n_tips) Vm[S * S + idx] = p;
+  }
+  // tip branch: its table row tipP[b][c][code][x] = sum_y P[x][y] init[code][y], with
+  // tip_table_kernel's arithmetic (the fused kernels read tips through it)
+  if (a.init && b < a.n_tips && (a.mask & 1u)) {
+    __syncthreads();
+    const double* Pl = Vm + S * S;
+    double* out = a.tipP + ((size_t)b * a.C + c) * a.n_codes * S;
+    for (int idx = threadIdx.x; idx < a.n_codes * S; idx += blockDim.x) {
+      const int code = idx / S, x = idx % S;
+      double t = 0.0;
+      for (int y = 0; y < S; ++y) t = __builtin_fma(Pl[x * S + y], a.init[code * S + y], t);
+      out[idx] = t;
+    }
   }
 }
 

@@ -284,15 +284,24 @@ __global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a, const TInstr* __
   }
 }
 
-// block_sums[b] = sum of the 64 wave sums of patterns [b*4096, (b+1)*4096), in order.
-__global__ void wave_sums_to_blocks(const double* __restrict__ wave_sums, double* __restrict__ block_sums,
-                                    int n_waves, int n_blocks) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+// block_sums[b] = sum of the 64 wave sums of patterns [b*4096, (b+1)*4096), added in
+// wave order.  One wave per block: the 64 loads are issued together (one per lane),
+// then lane 0 adds them in order through shuffles, so the result is the plain
+// sequential sum without 64 dependent memory round trips.
+__global__ __launch_bounds__(256) void wave_sums_to_blocks(const double* __restrict__ wave_sums,
+                                                           double* __restrict__ block_sums, int n_waves,
+                                                           int n_blocks) {
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (b >= n_blocks) return;
+  const int w = b * (kRootBlock / 64) + lane;
+  const double v = w < n_waves ? wave_sums[w] : 0.0;
   double s = 0.0;
-  const int w0 = b * (kRootBlock / 64);
-  for (int w = w0; w < w0 + kRootBlock / 64 && w < n_waves; ++w) s += wave_sums[w];
-  block_sums[b] = s;
+  for (int k = 0; k < kRootBlock / 64; ++k) {
+    const double x = __shfl(v, k, 64);
+    if (b * (kRootBlock / 64) + k < n_waves) s += x;
+  }
+  if (lane == 0) block_sums[b] = s;
 }
 
 }  // namespace plk

@@ -23,6 +23,7 @@ PLK_FLAG_LNL_ONLY = 4
 PLK_FLAG_LEVELWISE = 8
 PLK_DERIV_P, PLK_DERIV_DP, PLK_DERIV_D2P = 1, 2, 4
 PLK_OP_ACCUMULATE = 1
+PLK_TIME_PARTIALS, PLK_TIME_PMAT, PLK_TIME_ROOT = 1, 2, 4
 
 # every symbol include/plk.h declares
 EXPORTS = [
@@ -194,9 +195,12 @@ class Engine:
         return out
 
     def update_partials(self, ops: Sequence[Tuple[int, Sequence[int], int]]):
-        key = tuple((p, tuple(c), f) for p, c, f in ops)
-        if self._ops_cache is None or self._ops_cache[0] != key:
-            self._ops_cache = (key, make_ops(ops))
+        if self._ops_cache is None or self._ops_cache[2] is not ops:  # same list object: reuse its ctypes array
+            key = tuple((p, tuple(c), f) for p, c, f in ops)
+            if self._ops_cache is None or self._ops_cache[0] != key:
+                self._ops_cache = (key, make_ops(ops), ops)
+            else:
+                self._ops_cache = (key, self._ops_cache[1], ops)
         arr = self._ops_cache[1]
         self._chk(self.lib.plk_update_partials(self.h, arr, len(arr)))
 
@@ -221,7 +225,8 @@ class Engine:
         return d1.value, d2.value
 
     def set_timing(self, on: bool):
-        self._chk(self.lib.plk_set_timing(self.h, 1 if on else 0))
+        self._chk(self.lib.plk_set_timing(self.h, (PLK_TIME_PARTIALS | PLK_TIME_PMAT | PLK_TIME_ROOT) if on is True
+                                          else int(on)))
 
     def get_timing(self):
         n = ct.c_int64(0)

@@ -27,10 +27,10 @@ def shard_range(rank: int, world: int, n_patterns: int, align: int = BLOCK) -> T
 
 
 def fixed_order_sum(blocks: np.ndarray) -> float:
-    s = 0.0
-    for v in blocks:
-        s += float(v)
-    return s
+    """Sequential left-to-right sum (np.add.accumulate is strictly sequential, unlike
+    np.sum's pairwise summation), i.e. the same order plk_root_loglik uses."""
+    b = np.asarray(blocks, dtype=np.float64)
+    return float(np.add.accumulate(b)[-1]) if b.size else 0.0
 
 
 def allgather_lnl(blocks: np.ndarray, dist=None, device=None) -> float:

@@ -151,9 +151,11 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
 int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2);
 int plk_block_size(void);
 
-/* Instrumentation: HIP-event timing of the partial-update kernels on the
- * handle's stream (enabled by plk_set_timing(h, 1)). */
-int plk_set_timing(plk_handle h, int enable);
+/* Instrumentation: HIP-event timing on the handle's stream of the kernels selected
+ * by the mask given to plk_set_timing (0 = off).  Each timed launch adds an event
+ * pair to the stream, so time only what is needed. */
+enum { PLK_TIME_PARTIALS = 1u, PLK_TIME_PMAT = 2u, PLK_TIME_ROOT = 4u };
+int plk_set_timing(plk_handle h, int mask);
 int plk_get_timing(plk_handle h, int64_t* n_launches, double* partials_ms, double* pmat_ms, double* root_ms);
 int plk_reset_timing(plk_handle h);
 int plk_synchronize(plk_handle h);
