@@ -105,6 +105,7 @@ struct plk_handle_s {
   std::vector<int> last_level_start;
   // fused 4-state traversal (plk_tree4.hpp)
   double* wave_sums = nullptr;
+  bool blocks_fused = false;              // the last traversal already formed block_sums
   TInstr* d_prog = nullptr;
   size_t d_prog_cap = 0;
   int32_t* d_frag = nullptr;
@@ -1102,19 +1103,24 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   JitShape sh;
   if (jit) {
     sh.C = h->C;
-    sh.G = (h->n_pad % 128 == 0) ? env_int("PLK_JIT_G", 2, 1, 2) : 1;
+    // two pattern groups per workgroup share the staged tables; with rescaling every
+    // node has two workgroup barriers, whose cost grows with the waves that meet there
+    // (cfg5: 1.93 ms at G = 2, 1.16 ms at G = 1), so scaling runs use one group
+    sh.G = (h->n_pad % 128 == 0) ? env_int("PLK_JIT_G", (h->flags & PLK_FLAG_SCALING) ? 1 : 2, 1, 2) : 1;
     sh.U = h->n_codes;
     sh.NT = jit_max_fragment_tips(h->prog_host, h->frag_starts_host);
     sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     sh.L = env_int("PLK_JIT_L", 1, 1, 8);
-    sh.LP = env_int("PLK_JIT_LP", 0, 0, 4);  // measured: SGPR ring spills, 6x slower at 1
     sh.minw = env_int("PLK_JIT_MINW", 0, 0, 8);
     sh.same_p = env_is("PLK_DEBUG_SAMEP", '1');
+    // speculative no-rescale pass (plk_jit.hpp): a win only where rescaling never
+    // fires; on cfg5 it fires in almost every super-block (1.27 vs 1.14 ms), so opt-in
+    sh.exact_only = !env_is("PLK_JIT_SPECULATE", '1');
     if (sh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
     if (!h->jit_fn || sh.C != h->jit_shape.C || sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
-        sh.LP != h->jit_shape.LP || sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p) {
+        sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.exact_only != h->jit_shape.exact_only) {
       int rc = jit_function(h, jit_tree4_source(h->prog_host, h->frag_starts_host, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
@@ -1186,6 +1192,9 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   }
   h->fused_lnl_valid = h->prog_root >= 0;
   h->fused_lnl_root = h->prog_root;
+  // (forming the block sums in the kernel's last workgroup was measured slower: the
+  // agent-scope release fence each workgroup needs costs 0.27 -> 0.42 ms on cfg2)
+  h->blocks_fused = false;
   return PLK_OK;
 }
 
@@ -1288,6 +1297,7 @@ int update_levelwise(plk_handle h, const plk_op* ops, int n_ops) {
   }
   for (int i = 0; i < n_ops; ++i) h->materialized[ops[i].parent - h->n_tips] = 1;
   h->fused_lnl_valid = false;
+  h->blocks_fused = false;
   return PLK_OK;
 }
 
@@ -1368,7 +1378,9 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
   if (!h || root < h->n_tips || root >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad root node %d", root);
   if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
   hipSetDevice(h->device);
-  if (h->fused_lnl_valid && h->fused_lnl_root == root) {
+  if (h->fused_lnl_valid && h->fused_lnl_root == root && h->blocks_fused) {
+    // the tree-specialised kernel reduced the root and formed the block sums
+  } else if (h->fused_lnl_valid && h->fused_lnl_root == root) {
     // the fused traversal already reduced the root: only the block sums remain
     const int n_waves = (int)((h->n_patterns + 63) / 64);
     wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, h->block_sums, n_waves,
@@ -1555,6 +1567,15 @@ int plk_synchronize(plk_handle h) {
   hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PLK_OK;
+}
+
+int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* model, const double* t,
+                 const plk_op* ops, int n_ops, int root, double* lnl, double* block_sums) {
+  int rc = plk_update_pmatrices(h, n, branch, model, t, PLK_DERIV_P);
+  if (rc) return rc;
+  rc = plk_update_partials(h, ops, n_ops);
+  if (rc) return rc;
+  return plk_root_loglik(h, root, lnl, nullptr, block_sums);
 }
 
 const char* plk_kernel_path(plk_handle h) { return h ? h->kernel_path.c_str() : ""; }

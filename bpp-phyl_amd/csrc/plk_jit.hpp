@@ -68,25 +68,31 @@ __device__ __forceinline__ void contrib(double (&dst)[4], const double (&src)[4]
   }
 }
 
-// the same with P already in registers (prefetched ring slot)
-template <bool SET>
-__device__ __forceinline__ void contribr(double (&dst)[4], const double (&src)[4], const double (&P)[16]) {
-#pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    double s = P[4 * x + 0] * src[0];
-    s = __builtin_fma(P[4 * x + 1], src[1], s);
-    s = __builtin_fma(P[4 * x + 2], src[2], s);
-    s = __builtin_fma(P[4 * x + 3], src[3], s);
-    if (SET) dst[x] = s; else dst[x] *= s;
-  }
-}
-
 template <bool SET>
 __device__ __forceinline__ void tipmul(double (&dst)[4], const double (&row)[4]) {
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
     if (SET) dst[x] = row[x]; else dst[x] *= row[x];
   }
+}
+
+// opaque copies (no code): values the optimiser cannot prove equal to their source
+__device__ __forceinline__ unsigned long long launder_s(unsigned long long x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+__device__ __forceinline__ unsigned long long launder_v(unsigned long long x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// own-class max below the rescale threshold (or zero / NaN): the joint check of the
+// exact pass could fire here
+// (the flag is pinned with an empty asm right away: otherwise the compares sink to the
+// vote at the end of the fragment and keep every node's accumulator alive until then)
+__device__ __forceinline__ void flag_risky(int& dng, const double (&v)[4]) {
+  dng |= !(fmax(fmax(v[0], v[1]), fmax(v[2], v[3])) >= kScaleThr);
+  asm volatile("" : "+v"(dng));
 }
 
 template <int C>
@@ -158,6 +164,7 @@ __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[
     if (lane == 0) a.wave_sums[p0 >> 6] = wr;
   }
 }
+
 )PLKJIT";
 
 // Host mirror of JArgs (field order and types must match the prelude).
@@ -185,9 +192,9 @@ struct JitShape {
   int NT = 0;       // most tips of any fragment (LDS table slots)
   bool scale = false;
   int L = 1;        // operand fetch lookahead (events)
-  int LP = 0;       // P(t) prefetch lookahead (P-consuming events; 0: load at use)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool same_p = false;  // timing experiments only: every internal branch reads P(t) of node 0
+  bool exact_only = true;   // scaling: no speculative no-rescale pass (PLK_JIT_SPECULATE=1 enables it)
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     return nt * C * U * 4 * sizeof(double) + (size_t)G * C * 64 * sizeof(double) + (size_t)G * nt * 64;
@@ -300,7 +307,6 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
 #define LOADF(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
     F[0] = L_[0]; F[1] = L_[kTile]; F[2] = L_[2 * kTile]; F[3] = L_[3 * kTile]; \
     if (SC_) FK = a.scale[(i64)(slot) * a.n_pad + p]; }
-#define PF(Q, off) { const CPd P_ = pm + (off); _Pragma("unroll") for (int i_ = 0; i_ < 16; ++i_) Q[i_] = P_[i_]; }
 #define SB __builtin_amdgcn_sched_barrier(0);
   for (int sb = blockIdx.x; sb < a.n_sblocks; sb += gridDim.x) {
     const i64 q0 = (i64)sb * (64 * G_);
@@ -326,11 +332,6 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
     snprintf(buf, sizeof(buf), "    double F%d[4]; int FK%d = 0; (void)FK%d;\n", r, r, r);
     s += buf;
   }
-  const int LP = std::max(sh.LP, 0);
-  for (int r = 0; LP > 0 && r <= LP; ++r) {
-    snprintf(buf, sizeof(buf), "    double Q%d[16];\n", r);
-    s += buf;
-  }
   s += "    switch (frag) {\n";
   for (size_t f = 0; f < events.size(); ++f) {
     const std::vector<JitEvent>& ev = events[f];
@@ -340,25 +341,8 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
         slot[i] = (int)(fetchers.size() % (size_t)(L + 1));
         fetchers.push_back((int)i);
       }
-    // P-consuming events (LOAD, ASCEND) and their P ring slots
-    std::vector<int> pslot(ev.size(), -1), pevents;
-    for (size_t i = 0; i < ev.size(); ++i)
-      if (ev[i].op == T_LOAD || ev[i].op == T_ASCEND) {
-        pslot[i] = LP > 0 ? (int)(pevents.size() % (size_t)(LP + 1)) : -1;
-        pevents.push_back((int)i);
-      }
-    size_t np = 0;  // P prefetches emitted
-    auto emit_pf = [&](int i) {
-      snprintf(buf, sizeof(buf), "      PF(Q%d, %lld)\n", pslot[(size_t)i],
-               sh.same_p ? 0LL : (long long)ev[(size_t)i].b * C * 16);
-      s += buf;
-    };
     auto pref = [&](size_t i) -> std::string {  // P operand of event i
-      if (LP > 0) {
-        snprintf(buf, sizeof(buf), "Q%d", pslot[i]);
-      } else {
-        snprintf(buf, sizeof(buf), "pm + %lld", sh.same_p ? 0LL : (long long)ev[i].b * C * 16);
-      }
+      snprintf(buf, sizeof(buf), "pm + %lld", sh.same_p ? 0LL : (long long)ev[i].b * C * 16);
       return buf;
     };
     auto emit_fetch = [&](int i) {
@@ -369,71 +353,94 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
         snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %d)\n", slot[(size_t)i], slot[(size_t)i], e.a);
       s += buf;
     };
-    snprintf(buf, sizeof(buf), "    case %zu: {\n      K0 = 0;\n", f);
-    s += buf;
-    std::vector<char> fresh((size_t)max_level + 1, 0);
-    fresh[0] = 1;
-    size_t nf = 0;
-    for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
-    for (; LP > 0 && np < pevents.size() && np < (size_t)LP; ++np) emit_pf(pevents[np]);
-    s += "      SB\n";
-    for (size_t i = 0; i < ev.size(); ++i) {
-      const JitEvent& e = ev[i];
-      const long long off = (long long)e.b * C * 16;
-      if (e.op == T_TIP || e.op == T_LOAD) {
-        if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
-        const char* set = fresh[(size_t)e.level] ? "true" : "false";
-        if (e.op == T_TIP) {
-          snprintf(buf, sizeof(buf), "      tipmul<%s>(A%d, F%d);\n", set, e.level, slot[i]);
+    // One pass over the fragment.  exact: the per-node joint rescale of the other
+    // kernels.  !exact (scaling only): no rescale, but every node the exact pass would
+    // check raises `dng` when its own-class max is below the threshold -- the joint
+    // max can then be below it too; otherwise the joint max is >= the threshold at
+    // every check, no rescale would happen, and this pass IS the exact result.
+    auto emit_body = [&](bool exact) {
+      s += "      K0 = 0;\n";
+      std::vector<char> fresh((size_t)max_level + 1, 0);
+      fresh[0] = 1;
+      size_t nf = 0;
+      for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
+      s += "      SB\n";
+      const char* check = exact ? "      rescale<C_>(A%d, K%d, xch, w, g);\n" : "      flag_risky(dng, A%d);\n";
+      for (size_t i = 0; i < ev.size(); ++i) {
+        const JitEvent& e = ev[i];
+        if (e.op == T_TIP || e.op == T_LOAD) {
+          if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
+          const char* set = fresh[(size_t)e.level] ? "true" : "false";
+          if (e.op == T_TIP) {
+            snprintf(buf, sizeof(buf), "      tipmul<%s>(A%d, F%d);\n", set, e.level, slot[i]);
+          } else {
+            const std::string pr = pref(i);
+            snprintf(buf, sizeof(buf), "      contrib<%s>(A%d, F%d, %s);\n", set, e.level, slot[i], pr.c_str());
+          }
           s += buf;
-        } else {
-          if (LP > 0 && np < pevents.size()) emit_pf(pevents[np++]);
+          fresh[(size_t)e.level] = 0;
+          if (e.op == T_LOAD && sh.scale) {
+            snprintf(buf, sizeof(buf), "      K%d += FK%d;\n", e.level, slot[i]);
+            s += buf;
+          }
+          s += "      SB\n";
+        } else if (e.op == T_DESCEND) {
+          fresh[(size_t)e.level] = 1;
+          snprintf(buf, sizeof(buf), "      K%d = 0;\n", e.level);
+          s += buf;
+        } else if (e.op == T_ASCEND) {
+          const int dd = e.level;
+          if (e.b >= 0) {
+            if (sh.scale) {
+              snprintf(buf, sizeof(buf), check, dd, dd);
+              s += buf;
+            }
+            if (e.a >= 0) {
+              snprintf(buf, sizeof(buf), "      store<SC_>(a, %d, toff, p, c0, A%d, K%d);\n", e.a, dd, dd);
+              s += buf;
+            }
+          }
           const std::string pr = pref(i);
-          snprintf(buf, sizeof(buf), "      %s<%s>(A%d, F%d, %s);\n", LP > 0 ? "contribr" : "contrib", set, e.level,
-                   slot[i], pr.c_str());
+          snprintf(buf, sizeof(buf), "      contrib<%s>(A%d, A%d, %s);\n", fresh[(size_t)dd - 1] ? "true" : "false",
+                   dd - 1, dd, pr.c_str());
           s += buf;
-        }
-        fresh[(size_t)e.level] = 0;
-        if (e.op == T_LOAD && sh.scale) {
-          snprintf(buf, sizeof(buf), "      K%d += FK%d;\n", e.level, slot[i]);
-          s += buf;
-        }
-        s += "      SB\n";
-      } else if (e.op == T_DESCEND) {
-        fresh[(size_t)e.level] = 1;
-        snprintf(buf, sizeof(buf), "      K%d = 0;\n", e.level);
-        s += buf;
-      } else if (e.op == T_ASCEND) {
-        const int dd = e.level;
-        if (e.b >= 0) {
+          fresh[(size_t)dd - 1] = 0;
           if (sh.scale) {
-            snprintf(buf, sizeof(buf), "      rescale<C_>(A%d, K%d, xch, w, g);\n", dd, dd);
+            snprintf(buf, sizeof(buf), "      K%d += K%d;\n", dd - 1, dd);
+            s += buf;
+          }
+          s += "      SB\n";
+        } else {  // T_ROOT
+          if (sh.scale) {
+            snprintf(buf, sizeof(buf), check, 0, 0);
             s += buf;
           }
           if (e.a >= 0) {
-            snprintf(buf, sizeof(buf), "      store<SC_>(a, %d, toff, p, c0, A%d, K%d);\n", e.a, dd, dd);
+            snprintf(buf, sizeof(buf), "      store<SC_>(a, %d, toff, p, c0, A0, K0);\n", e.a);
             s += buf;
           }
+          if (e.b) s += "      reduce_root<C_, SC_>(a, A0, K0, xch, w, g, c0, p0, p);\n";
         }
-        if (LP > 0 && np < pevents.size()) emit_pf(pevents[np++]);
-        const std::string pr = pref(i);
-        snprintf(buf, sizeof(buf), "      %s<%s>(A%d, A%d, %s);\n", LP > 0 ? "contribr" : "contrib",
-                 fresh[(size_t)dd - 1] ? "true" : "false", dd - 1, dd, pr.c_str());
-        s += buf;
-        fresh[(size_t)dd - 1] = 0;
-        if (sh.scale) {
-          snprintf(buf, sizeof(buf), "      K%d += K%d;\n", dd - 1, dd);
-          s += buf;
-        }
-        s += "      SB\n";
-      } else {  // T_ROOT
-        if (sh.scale) s += "      rescale<C_>(A0, K0, xch, w, g);\n";
-        if (e.a >= 0) {
-          snprintf(buf, sizeof(buf), "      store<SC_>(a, %d, toff, p, c0, A0, K0);\n", e.a);
-          s += buf;
-        }
-        if (e.b) s += "      reduce_root<C_, SC_>(a, A0, K0, xch, w, g, c0, p0, p);\n";
       }
+    };
+    snprintf(buf, sizeof(buf), "    case %zu: {\n", f);
+    s += buf;
+    if (sh.scale && !sh.exact_only) {
+      s += "      int dng = 0;\n";
+      emit_body(false);
+      // the exact pass reads its operands through laundered copies of the base pointers,
+      // so the compiler cannot reuse (and keep live across the vote) the fast pass's loads
+      s += "      if (__syncthreads_or(dng)) {  // a check could have rescaled: redo it exactly\n"
+           "      const CPd pmo_ = pm; const double* trowo_ = trow; const u8* crowo_ = crow; const i64 toffo_ = toff;\n"
+           "      {\n"
+           "      const CPd pm = (CPd)launder_s((unsigned long long)pmo_);\n"
+           "      const double* trow = (const double*)launder_s((unsigned long long)trowo_);\n"
+           "      const u8* crow = (const u8*)launder_v((unsigned long long)crowo_);\n"
+           "      const i64 toff = (i64)launder_v((unsigned long long)toffo_);\n";
+      emit_body(true);
+      s += "      }\n      }\n";
+    } else {
+      emit_body(true);
     }
     s += "    } break;\n";
   }

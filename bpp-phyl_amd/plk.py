@@ -32,7 +32,7 @@ EXPORTS = [
     "plk_set_root_frequencies", "plk_set_eigen", "plk_update_pmatrices", "plk_set_pmatrix",
     "plk_get_pmatrix", "plk_update_partials", "plk_get_partials", "plk_root_loglik", "plk_block_size",
     "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
-    "plk_kernel_path",
+    "plk_kernel_path", "plk_evaluate",
 ]
 
 
@@ -85,6 +85,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_synchronize": ([ct.c_void_p], ct.c_int),
         "plk_branch_derivatives": ([ct.c_void_p, ct.c_int, dp, dp], ct.c_int),
         "plk_kernel_path": ([ct.c_void_p], ct.c_char_p),
+        "plk_evaluate": ([ct.c_void_p, ct.c_int, ip, ip, dp, P(plk_op), ct.c_int, ct.c_int, dp, dp], ct.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -194,15 +195,35 @@ class Engine:
         self._chk(self.lib.plk_get_pmatrix(self.h, branch, _d(out)))
         return out
 
-    def update_partials(self, ops: Sequence[Tuple[int, Sequence[int], int]]):
+    def _op_array(self, ops):
         if self._ops_cache is None or self._ops_cache[2] is not ops:  # same list object: reuse its ctypes array
             key = tuple((p, tuple(c), f) for p, c, f in ops)
             if self._ops_cache is None or self._ops_cache[0] != key:
                 self._ops_cache = (key, make_ops(ops), ops)
             else:
                 self._ops_cache = (key, self._ops_cache[1], ops)
-        arr = self._ops_cache[1]
+        return self._ops_cache[1]
+
+    def update_partials(self, ops: Sequence[Tuple[int, Sequence[int], int]]):
+        arr = self._op_array(ops)
         self._chk(self.lib.plk_update_partials(self.h, arr, len(arr)))
+
+    def evaluate(self, branches: np.ndarray, t: np.ndarray, ops, root: int, models: Optional[np.ndarray] = None):
+        """plk_evaluate: P(t) of `branches`, the traversal `ops`, the root reduction in one
+        call.  Returns (lnL, block_sums)."""
+        b = np.ascontiguousarray(branches, dtype=np.int32)
+        tt = np.ascontiguousarray(t, dtype=np.float64)
+        mp = None
+        if models is not None:
+            m = np.ascontiguousarray(models, dtype=np.int32)
+            mp = m.ctypes.data_as(ct.POINTER(ct.c_int32))
+        arr = self._op_array(ops)
+        nb = (self.P + self.lib.plk_block_size() - 1) // self.lib.plk_block_size()
+        blocks = np.empty(nb)
+        lnl = ct.c_double(0.0)
+        self._chk(self.lib.plk_evaluate(self.h, len(b), b.ctypes.data_as(ct.POINTER(ct.c_int32)), mp, _d(tt), arr,
+                                        len(arr), root, ct.byref(lnl), _d(blocks)))
+        return lnl.value, blocks
 
     def get_partials(self, node: int) -> np.ndarray:
         out = np.empty((self.P, self.C, self.S))

@@ -171,6 +171,5 @@ class Evaluator:
     def step(self, brlen: Optional[np.ndarray] = None):
         et = self.wl.et
         t = (et.brlen if brlen is None else brlen)[self.branches]
-        self.eng.update_pmatrices(self.branches, t, self.model_idx)
-        self.eng.update_partials(self.ops)
-        return self.eng.root_loglik(et.root, want_blocks=True)
+        lnl, blocks = self.eng.evaluate(self.branches, t, self.ops, et.root, self.model_idx)
+        return lnl, None, blocks

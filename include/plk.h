@@ -141,6 +141,13 @@ int plk_get_partials(plk_handle h, int node, double* out /* n_patterns x C x S, 
  * gives a result independent of how patterns are sharded across devices. */
 int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums);
 
+/* One likelihood evaluation as RHomogeneousTreeLikelihood::fireParameterChanged does it
+ * (Likelihood/RHomogeneousTreeLikelihood.cpp:255-283): P(t) of the listed branches
+ * (plk_update_pmatrices, P only), the postorder traversal (plk_update_partials) and the
+ * root reduction (plk_root_loglik without per-site output), in one call. */
+int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* model, const double* t,
+                 const plk_op* ops, int n_ops, int root, double* lnl, double* block_sums);
+
 /* First and second derivatives of lnL with respect to the length of `branch` (a child
  * node index) for the tree of the last plk_update_partials call:
  *   d1 = d lnL / dt,  d2 = d2 lnL / dt2   (the reference's getFirstOrderDerivative

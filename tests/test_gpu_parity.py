@@ -301,6 +301,28 @@ def test_repeat_evaluation_bitwise():
     assert a[0] == b[0] and np.array_equal(a[1], b[1])
 
 
+@pytest.mark.parametrize("S,C,flags", [(4, 4, plk.PLK_FLAG_LNL_ONLY), (4, 2, 0), (4, 4, plk.PLK_FLAG_LEVELWISE),
+                                         (20, 4, plk.PLK_FLAG_LNL_ONLY)])
+def test_evaluate_equals_three_calls(S, C, flags):
+    """plk_evaluate (one call) == plk_update_pmatrices + plk_update_partials +
+    plk_root_loglik, bitwise, including the block sums the JIT kernel forms itself."""
+    et, m, alph, rates, probs, states = _random_problem(S, C, 40, 9000, seed=12)
+    eng = engine_for(et, S, C, 9000, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | flags)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    ops = phylo.split_ops(et.ops)
+    for scale in (1.0, 1.3):   # a second evaluation at other branch lengths
+        t = et.brlen[br] * scale
+        lnl_e, blocks_e = eng.evaluate(br, t, ops, et.root)
+        eng.update_pmatrices(br, t)
+        eng.update_partials(ops)
+        lnl_3, _, blocks_3 = eng.root_loglik(et.root, want_blocks=True)
+        assert lnl_e == lnl_3 and np.array_equal(blocks_e, blocks_3)
+        lo, so = oracle_for(et, states, alph.init_table, rates, probs, m.pi, [m],
+                            pmats=engine_pmats(eng, et))
+        assert abs(lnl_e - lo) <= REL * abs(lo)
+
+
 def test_get_partials_matches_recomputation():
     et, m, alph, rates, probs, states = _random_problem(4, 4, 6, 300, seed=8)
     eng = engine_for(et, 4, 4, 300, states, alph.init_table, rates, probs, m.pi, [m])
@@ -363,12 +385,12 @@ def test_config2_full_size_properties():
 MODES = {"materialize": 0, "lnl_only": plk.PLK_FLAG_LNL_ONLY, "levelwise": plk.PLK_FLAG_LEVELWISE}
 
 
-def _caterpillar(n, seed=3):
+def _caterpillar(n, seed=3, lo=0.02, hi=0.2):
     rng = np.random.default_rng(seed)
-    s = "t0:%.4f" % rng.uniform(0.02, 0.2)
+    s = "t0:%.4f" % rng.uniform(lo, hi)
     for i in range(1, n - 1):
-        s = "(%s,t%d:%.4f):%.4f" % (s, i, rng.uniform(0.02, 0.2), rng.uniform(0.02, 0.2))
-    return phylo.Tree.from_newick("(%s,t%d:%.4f);" % (s, n - 1, rng.uniform(0.02, 0.2)))
+        s = "(%s,t%d:%.4f):%.4f" % (s, i, rng.uniform(lo, hi), rng.uniform(lo, hi))
+    return phylo.Tree.from_newick("(%s,t%d:%.4f);" % (s, n - 1, rng.uniform(lo, hi)))
 
 
 @pytest.mark.parametrize("mode", sorted(MODES))
@@ -443,13 +465,22 @@ def test_s20_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling, dm, monkey
 @pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode", [
     (4, "balanced64", 3000, False, "lnl_only"), (4, "balanced64", 1000, False, "materialize"),
     (2, "balanced64", 700, True, "lnl_only"), (1, "caterpillar40", 300, True, "materialize"),
-    (4, "caterpillar40", 900, False, "lnl_only"), (4, "balanced300", 513, True, "lnl_only")])
+    (4, "caterpillar40", 900, False, "lnl_only"), (4, "balanced300", 513, True, "lnl_only"),
+    (4, "caterpillar200long", 600, True, "lnl_only"), (2, "caterpillar200long", 300, True, "materialize"),
+    (4, "caterpillar200longspec", 600, True, "lnl_only"), (4, "balanced64spec", 500, True, "materialize")])
 def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling, mode, monkeypatch):
     """The tree-specialised kernel (plk_jit.hpp, hiprtc) against the interpreter
     (tree4_kernel) on the same program: lnL, per-pattern lnL, block sums and every
-    interior partial bitwise; and the oracle at 1e-12."""
+    interior partial bitwise; and the oracle at 1e-12.  The long-branch caterpillar
+    drives partials below 2^-256, so the speculative no-rescale pass must detect it
+    and fall back to the exact pass."""
+    if tree_kind.endswith("spec"):   # the speculative no-rescale pass with its exact fallback
+        monkeypatch.setenv("PLK_JIT_SPECULATE", "1")
+        tree_kind = tree_kind[:-4]
     if tree_kind.startswith("balanced"):
         tree = phylo.balanced_tree(int(tree_kind[8:]), seed=23, lo=0.05, hi=0.4)
+    elif tree_kind.endswith("long"):
+        tree = _caterpillar(int(tree_kind[11:-4]), seed=5, lo=0.5, hi=1.5)
     else:
         tree = _caterpillar(int(tree_kind[11:]), seed=5)
     et = phylo.engine_tree(tree)
@@ -472,6 +503,8 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
         del eng
     (l0, s0, b0, p0), (l1, s1, b1, p1) = res["0"], res["1"]
     assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1) and np.array_equal(p0, p1)
+    if tree_kind.endswith("long"):
+        assert s1.min() < -256 * np.log(2)   # partials did go through rescaling
     lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m], scaling=scaling)
     check(l1, s1, lo, so)
 
