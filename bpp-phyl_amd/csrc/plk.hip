@@ -115,6 +115,7 @@ struct plk_handle_s {
   bool prog_reduce = false;
   int prog_dm = 0;                        // register levels the program was cut for
   bool prog_jit = false;                  // program cut for the tree-specialised kernel
+  bool prog_ciw = false;                  // ... with every class of a pattern in one wave
   int prog_tmax = 0;                      // tips per fragment the program was cut for
   int prog_nf = 0;                        // fragments of the cached program
   std::vector<std::vector<int> > prog_tiers;  // fragment ids per tier
@@ -754,6 +755,17 @@ int env_int(const char* name, int def, int lo, int hi) {
 // fused traversal; PLK_JIT=0 keeps the interpreter (tree4_kernel), e.g. for A/B runs.
 bool jit_tree4(plk_handle h) { return fused_kind(h) == FK_TREE4 && tree4_cw(h) == 1 && !env_is("PLK_JIT", '0'); }
 
+// Classes in one wave (plk_jit.hpp, CW = C): the joint rescale needs no cross-wave
+// exchange (the per-node barrier of the one-class-per-wave layout costs ~2x on cfg5),
+// at the price of C x the registers per level (so a lower fragment height).  Default
+// for scaling runs; PLK_JIT_CIW=0/1 overrides.
+bool jit_ciw(plk_handle h) {
+  if (!jit_tree4(h) || h->C == 1) return false;
+  const char* e = std::getenv("PLK_JIT_CIW");
+  if (e) return e[0] == '1';
+  return (h->flags & PLK_FLAG_SCALING) != 0;
+}
+
 // tips whose tables (C x codes-in-use x 4 doubles each) fit one fragment's LDS budget
 int jit_tip_cap(plk_handle h) {
   const int kb = env_int("PLK_JIT_TAB_KB", 48, 4, 120);
@@ -763,7 +775,9 @@ int jit_tip_cap(plk_handle h) {
 // register levels (fragment height) of the fused program
 int tree_levels(plk_handle h) {
   switch (fused_kind(h)) {
-    case FK_TREE4: return jit_tree4(h) ? env_int("PLK_JIT_DM", 10, 2, 32) : kTree4Levels(tree4_cw(h));
+    case FK_TREE4:
+      if (!jit_tree4(h)) return kTree4Levels(tree4_cw(h));
+      return jit_ciw(h) ? env_int("PLK_JIT_CIW_DM", 5, 2, 16) : env_int("PLK_JIT_DM", 10, 2, 32);
     case FK_TREES: return env_int("PLK_TREES_DM", 2, 2, 4);
     case FK_TREEM: return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 2, 2, 3);
     default: return 1;
@@ -965,6 +979,7 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   h->prog_reduce = reduce;
   h->prog_dm = DM;
   h->prog_jit = jit_tree4(h);
+  h->prog_ciw = jit_ciw(h);
   h->prog_tmax = TMAX;
   h->prog_root = root_reduce;
   // bookkeeping: which partials will be in HBM after the launch (-1: untouched)
@@ -1036,7 +1051,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const bool materialize = !(h->flags & PLK_FLAG_LNL_ONLY);
   const bool reduce = h->pi_set && h->rates_set;
   const bool same = h->prog_ops.size() == (size_t)n_ops && h->prog_materialize == materialize &&
-                    h->prog_reduce == reduce && h->prog_dm == tree_levels(h) && h->prog_jit == jit_tree4(h) &&
+                    h->prog_reduce == reduce && h->prog_dm == tree_levels(h) && h->prog_jit == jit_tree4(h) && h->prog_ciw == jit_ciw(h) &&
                     (!h->prog_jit || h->prog_tmax == jit_tip_cap(h)) &&
                     std::memcmp(h->prog_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
   if (!same) {
@@ -1103,10 +1118,13 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   JitShape sh;
   if (jit) {
     sh.C = h->C;
+    sh.CW = h->prog_ciw ? h->C : 1;
     // two pattern groups per workgroup share the staged tables; with rescaling every
     // node has two workgroup barriers, whose cost grows with the waves that meet there
     // (cfg5: 1.93 ms at G = 2, 1.16 ms at G = 1), so scaling runs use one group
-    sh.G = (h->n_pad % 128 == 0) ? env_int("PLK_JIT_G", (h->flags & PLK_FLAG_SCALING) ? 1 : 2, 1, 2) : 1;
+    sh.G = (h->n_pad % 128 == 0)
+               ? env_int("PLK_JIT_G", ((h->flags & PLK_FLAG_SCALING) && !h->prog_ciw) ? 1 : 2, 1, 2)
+               : 1;
     sh.U = h->n_codes;
     sh.NT = jit_max_fragment_tips(h->prog_host, h->frag_starts_host);
     sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
@@ -1118,7 +1136,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.exact_only = !env_is("PLK_JIT_SPECULATE", '1');
     if (sh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
-    if (!h->jit_fn || sh.C != h->jit_shape.C || sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
+    if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW || sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
         sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.exact_only != h->jit_shape.exact_only) {
       int rc = jit_function(h, jit_tree4_source(h->prog_host, h->frag_starts_host, sh), "plk_jit_tree4", &h->jit_fn);
@@ -1161,7 +1179,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       if (wgs == 0) {
         if (h->jit_resident <= 0) {
           int per_cu = 0, n_cu = 0;
-          HIPCHK(h, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, h->jit_fn, 64 * h->C * sh.G,
+          HIPCHK(h, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, h->jit_fn, 64 * (h->C / sh.CW) * sh.G,
                                                                        sh.lds_bytes()));
           HIPCHK(h, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, h->device));
           h->jit_resident = std::max(1, per_cu) * std::max(1, n_cu);
@@ -1169,7 +1187,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         wgs = h->jit_resident;
       }
       const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, wgs);
-      HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * h->C * sh.G, 1, 1, (unsigned)sh.lds_bytes(),
+      HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
+                                      (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
     } else if (kind == FK_TREEM) {
       launch_treeM(h, a, grid, lds_m);

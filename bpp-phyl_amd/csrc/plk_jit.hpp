@@ -55,24 +55,27 @@ struct JArgs {
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
 };
 
-// dst[x] (*)= sum_y P[x][y] src[y]   (P row-major, this wave's class); SET: dst was 1
-template <bool SET>
-__device__ __forceinline__ void contrib(double (&dst)[4], const double (&src)[4], CPd P) {
+// dst[cw][x] (*)= sum_y P_cw[x][y] src[cw][y] for the CW classes of the wave (P_cw at
+// P + 16 cw, row-major); SET: dst was 1
+template <int CW, bool SET>
+__device__ __forceinline__ void contrib(double (&dst)[4 * CW], const double (&src)[4 * CW], CPd P) {
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    double s = P[4 * x + 0] * src[0];
-    s = __builtin_fma(P[4 * x + 1], src[1], s);
-    s = __builtin_fma(P[4 * x + 2], src[2], s);
-    s = __builtin_fma(P[4 * x + 3], src[3], s);
-    if (SET) dst[x] = s; else dst[x] *= s;
-  }
+  for (int cw = 0; cw < CW; ++cw)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      double s = P[16 * cw + 4 * x + 0] * src[4 * cw + 0];
+      s = __builtin_fma(P[16 * cw + 4 * x + 1], src[4 * cw + 1], s);
+      s = __builtin_fma(P[16 * cw + 4 * x + 2], src[4 * cw + 2], s);
+      s = __builtin_fma(P[16 * cw + 4 * x + 3], src[4 * cw + 3], s);
+      if (SET) dst[4 * cw + x] = s; else dst[4 * cw + x] *= s;
+    }
 }
 
-template <bool SET>
-__device__ __forceinline__ void tipmul(double (&dst)[4], const double (&row)[4]) {
+template <int CW, bool SET>
+__device__ __forceinline__ void tipmul(double (&dst)[4 * CW], const double (&row)[4 * CW]) {
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    if (SET) dst[x] = row[x]; else dst[x] *= row[x];
+  for (int i = 0; i < 4 * CW; ++i) {
+    if (SET) dst[i] = row[i]; else dst[i] *= row[i];
   }
 }
 
@@ -90,61 +93,78 @@ __device__ __forceinline__ unsigned long long launder_v(unsigned long long x) {
 // exact pass could fire here
 // (the flag is pinned with an empty asm right away: otherwise the compares sink to the
 // vote at the end of the fragment and keep every node's accumulator alive until then)
-__device__ __forceinline__ void flag_risky(int& dng, const double (&v)[4]) {
-  dng |= !(fmax(fmax(v[0], v[1]), fmax(v[2], v[3])) >= kScaleThr);
+template <int N>
+__device__ __forceinline__ void flag_risky(int& dng, const double (&v)[N]) {
+  double m = v[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) m = fmax(m, v[i]);
+  dng |= !(m >= kScaleThr);
   asm volatile("" : "+v"(dng));
 }
 
-template <int C>
-__device__ __forceinline__ void rescale(double (&v)[4], int& cnt, double* xch, int w, int g) {
+// Joint (all-class) exact power-of-two rescale.  NW = C / CW waves hold the classes
+// of one pattern group; with NW = 1 the joint max is all in registers.
+template <int C, int CW>
+__device__ __forceinline__ void rescale(double (&v)[4 * CW], int& cnt, double* xch, int w, int g) {
+  constexpr int NW = C / CW;
   double m = 0.0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) m = fmax(m, v[i]);
-  if (C > 1) {
+  for (int i = 0; i < 4 * CW; ++i) m = fmax(m, v[i]);
+  if (NW > 1) {
+    // one barrier: consecutive rescales alternate between two exchange buffers, so a
+    // wave can only overwrite this buffer after every wave has passed the next
+    // rescale's barrier, i.e. after every wave has read it here
     const int lane = threadIdx.x & 63;
     xch[w * 64 + lane] = m;
     __syncthreads();
     m = 0.0;
-    for (int k = 0; k < C; ++k) m = fmax(m, xch[(g * C + k) * 64 + lane]);
-    __syncthreads();
+    for (int k = 0; k < NW; ++k) m = fmax(m, xch[(g * NW + k) * 64 + lane]);
   }
   if (m > 0.0 && m < kScaleThr) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] *= kScaleUp;
+    for (int i = 0; i < 4 * CW; ++i) v[i] *= kScaleUp;
     cnt += 1;
   }
 }
 
-template <bool SCALE>
-__device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0, const double (&v)[4], int cnt) {
+template <int CW, bool SCALE>
+__device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0, const double (&v)[4 * CW],
+                                      int cnt) {
   double* dst = a.partials + (i64)slot * a.slot_stride + off;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(v[i], dst + (i64)i * kTile);
+  for (int i = 0; i < 4 * CW; ++i) __builtin_nontemporal_store(v[i], dst + (i64)i * kTile);
   if (SCALE && c0 == 0) a.scale[(i64)slot * a.n_pad + p] = cnt;
 }
 
-template <int C, bool SCALE>
-__device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[4], int cnt, double* xch, int w,
+template <int C, int CW, bool SCALE>
+__device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[4 * CW], int cnt, double* xch, int w,
                                             int g, int c0, i64 p0, i64 p) {
+  constexpr int NW = C / CW;
   const int lane = threadIdx.x & 63;
-  double lc = 0.0;
+  double t[CW];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const double li = acc[s] * a.pi[s];
-    if (a.guard) {
-      if (li > 0.0) lc += li;
-    } else {
-      lc += li;
+  for (int cw = 0; cw < CW; ++cw) {
+    double lc = 0.0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const double li = acc[4 * cw + s] * a.pi[s];
+      if (a.guard) {
+        if (li > 0.0) lc += li;
+      } else {
+        lc += li;
+      }
     }
+    t[cw] = lc * a.probs[c0 + cw];
   }
-  const double t = lc * a.probs[c0];
-  __syncthreads();
-  xch[w * 64 + lane] = t;
-  __syncthreads();
+  if (NW > 1) {
+    __syncthreads();
+    xch[w * 64 + lane] = t[0];
+    __syncthreads();
+  }
   if (c0 == 0) {
     double l = 0.0;
     for (int c = 0; c < C; ++c) {
-      const double li = xch[(g * C + c) * 64 + lane];
+      const double li = NW > 1 ? xch[(g * NW + c) * 64 + lane] : t[c < CW ? c : 0];
       if (a.guard) {
         if (li > 0.0) l += li;
       } else {
@@ -164,7 +184,6 @@ __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[
     if (lane == 0) a.wave_sums[p0 >> 6] = wr;
   }
 }
-
 )PLKJIT";
 
 // Host mirror of JArgs (field order and types must match the prelude).
@@ -186,7 +205,8 @@ struct JArgs {
 };
 
 struct JitShape {
-  int C = 1;        // rate classes = waves per pattern group
+  int C = 1;        // rate classes
+  int CW = 1;       // classes per wave (1, or C: a wave holds every class of its patterns)
   int G = 1;        // 64-pattern groups per workgroup
   int U = 1;        // codes in use (rows of a tip table)
   int NT = 0;       // most tips of any fragment (LDS table slots)
@@ -197,7 +217,7 @@ struct JitShape {
   bool exact_only = true;   // scaling: no speculative no-rescale pass (PLK_JIT_SPECULATE=1 enables it)
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
-    return nt * C * U * 4 * sizeof(double) + (size_t)G * C * 64 * sizeof(double) + (size_t)G * nt * 64;
+    return nt * C * U * 4 * sizeof(double) + 2 * (size_t)G * (C / CW) * 64 * sizeof(double) + (size_t)G * nt * 64;
   }
 };
 
@@ -279,19 +299,22 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
       s += buf;
     }
   s += "};\n";
+  const int CW = sh.CW, NW = C / CW;
   snprintf(buf, sizeof(buf),
-           "#define C_ %d\n#define G_ %d\n#define U_ %d\n#define NT_ %d\n#define SC_ %s\n"
+           "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define G_ %d\n#define U_ %d\n#define NT_ %d\n"
+           "#define SC_ %s\n"
            "extern \"C\" __global__ __launch_bounds__(%d%s) void plk_jit_tree4(JArgs a, const double* __restrict__ "
            "pmats, int frag_base) {\n",
-           C, sh.G, sh.U, std::max(sh.NT, 1), sh.scale ? "true" : "false", 64 * C * sh.G, minw_s.c_str());
+           C, CW, NW, sh.G, sh.U, std::max(sh.NT, 1), sh.scale ? "true" : "false", 64 * NW * sh.G, minw_s.c_str());
   s += buf;
   s += R"PLKJIT(  extern __shared__ __attribute__((aligned(16))) double lds[];
   double* tab = lds;                                          // [NT_][C_][U_][4]
-  double* xch = tab + NT_ * C_ * U_ * 4;                      // [G_ * C_][64]
-  u8* code_lds = reinterpret_cast<u8*>(xch + G_ * C_ * 64);   // [G_][NT_][64]
+  double* xch = tab + NT_ * C_ * U_ * 4;                      // [2][G_ * NW_][64] (rescale alternates)
+  double* xch2 = xch + G_ * NW_ * 64;
+  u8* code_lds = reinterpret_cast<u8*>(xch2 + G_ * NW_ * 64); // [G_][NT_][64]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c0 = w % C_, g = w / C_;
+  const int c0 = (w % NW_) * CW_, g = w / NW_;
   const int frag = frag_base + (int)blockIdx.y;
   const int t0 = 1 + kFragTipStart[frag], nt = kFragTipStart[frag + 1] - kFragTipStart[frag];
   for (int i = threadIdx.x; i < nt * (C_ * U_ * 4); i += blockDim.x) {
@@ -301,11 +324,14 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
   const CPd pm = (CPd)(pmats + c0 * 16);
   const double* trow = tab + c0 * (U_ * 4);
   const u8* crow = code_lds + g * (NT_ * 64) + lane;
-  (void)xch; (void)trow; (void)crow;
-#define TIPF(F, k) { const double2* r_ = reinterpret_cast<const double2*>(trow + ((k) * (C_ * U_) + crow[(k) * 64]) * 4); \
-    const double2 x_ = r_[0], y_ = r_[1]; F[0] = x_.x; F[1] = x_.y; F[2] = y_.x; F[3] = y_.y; }
+  (void)xch; (void)xch2; (void)trow; (void)crow;
+#define TIPF(F, k) { const double* r0_ = trow + ((k) * (C_ * U_) + crow[(k) * 64]) * 4; \
+    _Pragma("unroll") for (int cw_ = 0; cw_ < CW_; ++cw_) { \
+      const double2* r_ = reinterpret_cast<const double2*>(r0_ + cw_ * (U_ * 4)); \
+      const double2 x_ = r_[0], y_ = r_[1]; \
+      F[4 * cw_] = x_.x; F[4 * cw_ + 1] = x_.y; F[4 * cw_ + 2] = y_.x; F[4 * cw_ + 3] = y_.y; } }
 #define LOADF(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
-    F[0] = L_[0]; F[1] = L_[kTile]; F[2] = L_[2 * kTile]; F[3] = L_[3 * kTile]; \
+    _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[i_] = L_[(i64)i_ * kTile]; \
     if (SC_) FK = a.scale[(i64)(slot) * a.n_pad + p]; }
 #define SB __builtin_amdgcn_sched_barrier(0);
   for (int sb = blockIdx.x; sb < a.n_sblocks; sb += gridDim.x) {
@@ -325,11 +351,11 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
   for (const auto& ev : events)
     for (const JitEvent& e : ev) max_level = std::max(max_level, e.level);
   for (int d = 0; d <= max_level; ++d) {
-    snprintf(buf, sizeof(buf), "    double A%d[4]; int K%d = 0; (void)K%d;\n", d, d, d);
+    snprintf(buf, sizeof(buf), "    double A%d[4 * CW_]; int K%d = 0; (void)K%d;\n", d, d, d);
     s += buf;
   }
   for (int r = 0; r <= L; ++r) {
-    snprintf(buf, sizeof(buf), "    double F%d[4]; int FK%d = 0; (void)FK%d;\n", r, r, r);
+    snprintf(buf, sizeof(buf), "    double F%d[4 * CW_]; int FK%d = 0; (void)FK%d;\n", r, r, r);
     s += buf;
   }
   s += "    switch (frag) {\n";
@@ -365,17 +391,25 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
       size_t nf = 0;
       for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
       s += "      SB\n";
-      const char* check = exact ? "      rescale<C_>(A%d, K%d, xch, w, g);\n" : "      flag_risky(dng, A%d);\n";
+      int n_rescale = 0;  // rescales alternate exchange buffers (the superblock barrier resets)
+      auto check_line = [&](int d) {
+        if (exact)
+          snprintf(buf, sizeof(buf), "      rescale<C_, CW_>(A%d, K%d, %s, w, g);\n", d, d,
+                   (n_rescale++ & 1) ? "xch2" : "xch");
+        else
+          snprintf(buf, sizeof(buf), "      flag_risky(dng, A%d);\n", d);
+        s += buf;
+      };
       for (size_t i = 0; i < ev.size(); ++i) {
         const JitEvent& e = ev[i];
         if (e.op == T_TIP || e.op == T_LOAD) {
           if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
           const char* set = fresh[(size_t)e.level] ? "true" : "false";
           if (e.op == T_TIP) {
-            snprintf(buf, sizeof(buf), "      tipmul<%s>(A%d, F%d);\n", set, e.level, slot[i]);
+            snprintf(buf, sizeof(buf), "      tipmul<CW_, %s>(A%d, F%d);\n", set, e.level, slot[i]);
           } else {
             const std::string pr = pref(i);
-            snprintf(buf, sizeof(buf), "      contrib<%s>(A%d, F%d, %s);\n", set, e.level, slot[i], pr.c_str());
+            snprintf(buf, sizeof(buf), "      contrib<CW_, %s>(A%d, F%d, %s);\n", set, e.level, slot[i], pr.c_str());
           }
           s += buf;
           fresh[(size_t)e.level] = 0;
@@ -391,17 +425,14 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
         } else if (e.op == T_ASCEND) {
           const int dd = e.level;
           if (e.b >= 0) {
-            if (sh.scale) {
-              snprintf(buf, sizeof(buf), check, dd, dd);
-              s += buf;
-            }
+            if (sh.scale) check_line(dd);
             if (e.a >= 0) {
-              snprintf(buf, sizeof(buf), "      store<SC_>(a, %d, toff, p, c0, A%d, K%d);\n", e.a, dd, dd);
+              snprintf(buf, sizeof(buf), "      store<CW_, SC_>(a, %d, toff, p, c0, A%d, K%d);\n", e.a, dd, dd);
               s += buf;
             }
           }
           const std::string pr = pref(i);
-          snprintf(buf, sizeof(buf), "      contrib<%s>(A%d, A%d, %s);\n", fresh[(size_t)dd - 1] ? "true" : "false",
+          snprintf(buf, sizeof(buf), "      contrib<CW_, %s>(A%d, A%d, %s);\n", fresh[(size_t)dd - 1] ? "true" : "false",
                    dd - 1, dd, pr.c_str());
           s += buf;
           fresh[(size_t)dd - 1] = 0;
@@ -411,15 +442,12 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
           }
           s += "      SB\n";
         } else {  // T_ROOT
-          if (sh.scale) {
-            snprintf(buf, sizeof(buf), check, 0, 0);
-            s += buf;
-          }
+          if (sh.scale) check_line(0);
           if (e.a >= 0) {
-            snprintf(buf, sizeof(buf), "      store<SC_>(a, %d, toff, p, c0, A0, K0);\n", e.a);
+            snprintf(buf, sizeof(buf), "      store<CW_, SC_>(a, %d, toff, p, c0, A0, K0);\n", e.a);
             s += buf;
           }
-          if (e.b) s += "      reduce_root<C_, SC_>(a, A0, K0, xch, w, g, c0, p0, p);\n";
+          if (e.b) s += "      reduce_root<C_, CW_, SC_>(a, A0, K0, xch, w, g, c0, p0, p);\n";
         }
       }
     };

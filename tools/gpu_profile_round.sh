@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round profile set: quick GPU tests, then for each config/mode the bench line,
+# rocprofv3 kernel-trace stats and PMC passes (tools/gpu_prof.sh).
+#   tools/gpu_profile_round.sh <prefix>
+set -o pipefail
+P=${1:-r}
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${P}_pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/${P}_pytest.log; exit 1; }
+tail -1 gpurun_out/${P}_pytest.log
+bash tools/gpu_prof.sh ${P}_cfg2_lnl gtr_g4_dna_1M_64 lnl 20 || exit 1
+bash tools/gpu_prof.sh ${P}_cfg2_mat gtr_g4_dna_1M_64 materialize 10 || exit 1
+bash tools/gpu_prof.sh ${P}_cfg3_lnl lg08_g4_protein_200k_256 lnl 5 || exit 1
+bash tools/gpu_prof.sh ${P}_cfg4_lnl yn98_codon_50k_128 lnl 10 || exit 1
+bash tools/gpu_prof.sh ${P}_cfg5_lnl nh_gtr_g4_dna_2M_512 lnl 10 || exit 1
+timeout -k 10 300 python bench.py > gpurun_out/${P}_bench_default.json 2> gpurun_out/${P}_bench_default.err || { tail -5 gpurun_out/${P}_bench_default.err; exit 1; }
+cat gpurun_out/${P}_bench_default.json
