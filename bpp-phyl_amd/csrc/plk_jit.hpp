@@ -325,6 +325,12 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
   const double* trow = tab + c0 * (U_ * 4);
   const u8* crow = code_lds + g * (NT_ * 64) + lane;
   (void)xch; (void)xch2; (void)trow; (void)crow;
+#define CODEF(Q, k) Q = crow[(k) * 64];
+#define ROWF(F, k, Q) { const double* r0_ = trow + ((k) * (C_ * U_) + (Q)) * 4; \
+    _Pragma("unroll") for (int cw_ = 0; cw_ < CW_; ++cw_) { \
+      const double2* r_ = reinterpret_cast<const double2*>(r0_ + cw_ * (U_ * 4)); \
+      const double2 x_ = r_[0], y_ = r_[1]; \
+      F[4 * cw_] = x_.x; F[4 * cw_ + 1] = x_.y; F[4 * cw_ + 2] = y_.x; F[4 * cw_ + 3] = y_.y; } }
 #define TIPF(F, k) { const double* r0_ = trow + ((k) * (C_ * U_) + crow[(k) * 64]) * 4; \
     _Pragma("unroll") for (int cw_ = 0; cw_ < CW_; ++cw_) { \
       const double2* r_ = reinterpret_cast<const double2*>(r0_ + cw_ * (U_ * 4)); \
@@ -355,7 +361,8 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
     s += buf;
   }
   for (int r = 0; r <= L; ++r) {
-    snprintf(buf, sizeof(buf), "    double F%d[4 * CW_]; int FK%d = 0; (void)FK%d;\n", r, r, r);
+    snprintf(buf, sizeof(buf), "    double F%d[4 * CW_]; int FK%d = 0; (void)FK%d; int Q%d = 0; (void)Q%d;\n", r, r, r,
+             r, r);
     s += buf;
   }
   s += "    switch (frag) {\n";
@@ -370,6 +377,23 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
     auto pref = [&](size_t i) -> std::string {  // P operand of event i
       snprintf(buf, sizeof(buf), "pm + %lld", sh.same_p ? 0LL : (long long)ev[i].b * C * 16);
       return buf;
+    };
+    // Two-stage operand pipeline (L >= 2): a tip's code is read L fetchers ahead (and a
+    // materialised child partial is loaded from HBM L ahead), its table row one ahead, so
+    // neither the code -> row dependency nor HBM latency sits in front of the FMAs.
+    auto emit_stage1 = [&](int i) {
+      const JitEvent& e = ev[(size_t)i];
+      if (e.op == T_TIP)
+        snprintf(buf, sizeof(buf), "      CODEF(Q%d, %d)\n", slot[(size_t)i], e.a);
+      else
+        snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %d)\n", slot[(size_t)i], slot[(size_t)i], e.a);
+      s += buf;
+    };
+    auto emit_stage2 = [&](int i) {
+      const JitEvent& e = ev[(size_t)i];
+      if (e.op != T_TIP) return;
+      snprintf(buf, sizeof(buf), "      ROWF(F%d, %d, Q%d)\n", slot[(size_t)i], e.a, slot[(size_t)i]);
+      s += buf;
     };
     auto emit_fetch = [&](int i) {
       const JitEvent& e = ev[(size_t)i];
@@ -389,7 +413,13 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
       std::vector<char> fresh((size_t)max_level + 1, 0);
       fresh[0] = 1;
       size_t nf = 0;
-      for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
+      size_t n1 = 0, n2 = 0;  // two-stage pipeline: stage-1 / stage-2 fetches emitted
+      if (L >= 2) {
+        for (; n1 < fetchers.size() && n1 < (size_t)L; ++n1) emit_stage1(fetchers[n1]);
+        if (n2 < fetchers.size()) emit_stage2(fetchers[n2++]);
+      } else {
+        for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
+      }
       s += "      SB\n";
       int n_rescale = 0;  // rescales alternate exchange buffers (the superblock barrier resets)
       auto check_line = [&](int d) {
@@ -403,7 +433,12 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
       for (size_t i = 0; i < ev.size(); ++i) {
         const JitEvent& e = ev[i];
         if (e.op == T_TIP || e.op == T_LOAD) {
-          if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
+          if (L >= 2) {
+            if (n1 < fetchers.size()) emit_stage1(fetchers[n1++]);
+            if (n2 < fetchers.size()) emit_stage2(fetchers[n2++]);
+          } else if (nf < fetchers.size()) {
+            emit_fetch(fetchers[nf++]);
+          }
           const char* set = fresh[(size_t)e.level] ? "true" : "false";
           if (e.op == T_TIP) {
             snprintf(buf, sizeof(buf), "      tipmul<CW_, %s>(A%d, F%d);\n", set, e.level, slot[i]);
