@@ -50,9 +50,11 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="A/B: time the steps without per-kernel HIP events")
-    ap.add_argument("--mode", default="lnl", choices=["lnl", "materialize", "levelwise"],
+    ap.add_argument("--mode", default="lnl", choices=["lnl", "materialize", "levelwise", "subtree"],
                     help="lnl: fused traversal, interior partials kept in registers (recomputed on demand); "
-                         "materialize: fused traversal writing every partial; levelwise: one launch per level")
+                         "materialize: fused traversal writing every partial; levelwise: one launch per level; "
+                         "subtree: per-subtree pattern compression (reference usePatterns=true) -- value is then "
+                         "an EFFECTIVE rate (SURVEY 8d), reported beside the computed updates")
     return ap.parse_args()
 
 
@@ -170,7 +172,8 @@ def main():
     wl.n_patterns = P
     start, end = rank * P, (rank + 1) * P
     t_setup = time.time()
-    extra = {"lnl": plk.PLK_FLAG_LNL_ONLY, "materialize": 0, "levelwise": plk.PLK_FLAG_LEVELWISE}[args.mode]
+    extra = {"lnl": plk.PLK_FLAG_LNL_ONLY, "materialize": 0, "levelwise": plk.PLK_FLAG_LEVELWISE,
+             "subtree": plk.PLK_FLAG_SUBTREE_PATTERNS}[args.mode]
     ev = workload.Evaluator(wl, device, start, end, extra_flags=extra)
     t_setup = time.time() - t_setup
     units_step = P * wl.et.n_internal
@@ -213,8 +216,20 @@ def main():
         roof = roofline(wl, args.mode, P, args.steps, part_s, launches, bytes_pattern, flops_pattern, traffic)
         if traffic_src and roof:
             roof["traffic_source"] = traffic_src
+        computed = None
+        if args.mode == "subtree":
+            # per-subtree compression computes fewer node updates than it is credited with;
+            # the roofline is then priced on the updates actually computed
+            computed = ev.eng.compressed_work()
+            if roof:
+                f = computed / units_step
+                roof["achieved"] *= f
+                roof["frac"] *= f
+                roof["basis"] += f"; scaled to the {computed} node updates actually computed per traversal"
+                roof.pop("other_ceiling", None)
         rec = {
-            "metric": "site-pattern x node partial updates/s",
+            "metric": ("site-pattern x node partial updates/s" if args.mode != "subtree" else
+                       "site-pattern x node partial updates/s (EFFECTIVE: per-subtree pattern compression)"),
             "value": value,
             "unit": "updates/s",
             "n_gpus": world,
@@ -246,6 +261,9 @@ def main():
             "roofline": roof,
             "setup_s": t_setup,
         }
+        if computed is not None:
+            rec["computed_updates_per_step"] = computed
+            rec["computed_updates_per_s"] = computed * world * args.steps / elapsed
         if world == 1 and not args.no_cpu_baseline:
             ns = args.cpu_sample or workload.CONFIGS[args.config]["cpu_sample"]
             rec["cpu_baseline"] = cpu_baseline(wl, min(ns, P), args.cpu_reps)

@@ -140,6 +140,18 @@ struct plk_handle_s {
   JitShape jit_shape;
   int jit_resident = 0;  // workgroups of jit_fn resident at once on the device
   std::string kernel_path;                // what served the last plk_update_partials
+  // per-subtree pattern compression (PLK_FLAG_SUBTREE_PATTERNS)
+  std::vector<std::vector<uint8_t> > tip_codes_host;  // compact codes per tip
+  bool cmp_valid = false;
+  std::vector<plk_op> cmp_ops;                        // op list the links were built for
+  std::vector<std::vector<int32_t> > cmp_ids;         // per internal slot: distinct id per pattern (empty: identity)
+  std::vector<int64_t> cmp_D;                         // per internal slot: distinct patterns
+  std::vector<int> cmp_level_start, cmp_level_maxD;
+  uint32_t* d_links = nullptr;
+  size_t d_links_cap = 0;
+  KOpL* d_opsl = nullptr;
+  size_t d_opsl_cap = 0;
+  int64_t cmp_work = 0;                               // sum over nodes of distinct patterns
 };
 
 namespace {
@@ -398,6 +410,8 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   *out = nullptr;
   if (n_states < 2 || n_states > 64) return fail(nullptr, PLK_ERR_UNSUPPORTED, "n_states %d not in [2, 64]", n_states);
   if (n_classes < 1 || n_classes > 16) return fail(nullptr, PLK_ERR_UNSUPPORTED, "n_classes %d not in [1, 16]", n_classes);
+  if ((flags & PLK_FLAG_SUBTREE_PATTERNS) && !(n_states == 4 && s4_supported(n_classes)))
+    return fail(nullptr, PLK_ERR_UNSUPPORTED, "per-subtree pattern compression needs 4 states and C in {1, 2, 4, 8}");
   if (n_patterns < 1 || n_tips < 0 || n_internal < 1 || n_models < 1)
     return fail(nullptr, PLK_ERR_ARG, "bad sizes (patterns %lld tips %d internal %d models %d)",
                 (long long)n_patterns, n_tips, n_internal, n_models);
@@ -474,7 +488,7 @@ int plk_destroy(plk_handle h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
-                  h->block_sums, h->d_ops, h->d_req, h->wave_sums, h->d_prog, h->d_frag, h->d1_sums,
+                  h->block_sums, h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -543,6 +557,11 @@ int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes) {
   }
   std::vector<uint8_t> cc((size_t)h->n_patterns);
   for (int64_t i = 0; i < h->n_patterns; ++i) cc[(size_t)i] = (uint8_t)h->code_map[codes[i]];
+  if (h->flags & PLK_FLAG_SUBTREE_PATTERNS) {
+    if (h->tip_codes_host.empty()) h->tip_codes_host.resize(h->n_tips);
+    h->tip_codes_host[tip] = cc;
+    h->cmp_valid = false;
+  }
   hipSetDevice(h->device);
   HIPCHK(h, hipMemcpy(h->codes + (size_t)tip * h->n_pad, cc.data(), (size_t)h->n_patterns, hipMemcpyHostToDevice));
   h->tip_set[tip] = 1;
@@ -1320,6 +1339,277 @@ int update_levelwise(plk_handle h, const plk_op* ops, int n_ops) {
   return PLK_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Per-subtree site-pattern compression (reference usePatterns = true,
+// DRASRTreeLikelihoodData.cpp:218-332, SitePatterns P/SitePatterns.cpp:51-100).
+// Bottom-up over the op list: a node's distinct patterns are the distinct tuples of its
+// children's distinct-pattern ids (tips: compact codes), numbered in order of first
+// appearance; its links give, per distinct pattern, each child's id.  The top node of
+// the traversal stays uncompressed (every root pattern), so the root reduction and
+// the per-site output are unchanged.
+// ---------------------------------------------------------------------------
+namespace {
+
+// id of (a, b) pairs in order of first appearance; key space a * nb + b
+struct PairIds {
+  std::vector<uint64_t> keys;
+  std::vector<int32_t> vals;
+  uint64_t mask = 0;
+  void reset(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    keys.assign(cap, ~0ull);
+    vals.assign(cap, -1);
+    mask = cap - 1;
+  }
+  int32_t get(uint64_t key, int32_t next) {
+    uint64_t i = (key * 0x9E3779B97F4A7C15ull) >> 20 & mask;
+    for (;;) {
+      if (keys[i] == key) return vals[i];
+      if (keys[i] == ~0ull) {
+        keys[i] = key;
+        vals[i] = next;
+        return next;
+      }
+      i = (i + 1) & mask;
+    }
+  }
+};
+
+// ids[p] = distinct id of (a[p], b[p]); returns the number of distinct pairs
+int64_t pair_ids(const int32_t* a, const int32_t* b, int64_t nb, int64_t P, std::vector<int32_t>& ids,
+                 int64_t na) {
+  ids.resize((size_t)P);
+  int64_t D = 0;
+  if ((uint64_t)na * (uint64_t)nb <= (uint64_t)4 * (uint64_t)P + 4096) {
+    std::vector<int32_t> direct((size_t)(na * nb), -1);  // small key space: direct table
+    for (int64_t p = 0; p < P; ++p) {
+      int32_t& v = direct[(size_t)(a[p] * nb + b[p])];
+      if (v < 0) v = (int32_t)D++;
+      ids[(size_t)p] = v;
+    }
+    return D;
+  }
+  PairIds h;
+  h.reset((size_t)P);
+  for (int64_t p = 0; p < P; ++p) {
+    const int32_t v = h.get((uint64_t)a[p] * (uint64_t)nb + (uint64_t)b[p], (int32_t)D);
+    if (v == (int32_t)D) ++D;
+    ids[(size_t)p] = v;
+  }
+  return D;
+}
+
+}  // namespace
+
+int build_compression(plk_handle h, const plk_op* ops, int n_ops) {
+  const int nt = h->n_tips;
+  const int64_t P = h->n_patterns;
+  if ((int)h->tip_codes_host.size() != nt) return fail(h, PLK_ERR_STATE, "tip codes not set");
+  // logical nodes: an ACCUMULATE op continues the previous op's node
+  struct LNode {
+    int node;
+    std::vector<int> kids;
+  };
+  std::vector<LNode> nodes;
+  for (int i = 0; i < n_ops; ++i) {
+    if ((ops[i].flags & PLK_OP_ACCUMULATE) && !nodes.empty() && nodes.back().node == ops[i].parent) {
+      for (int k = 0; k < ops[i].n_children; ++k) nodes.back().kids.push_back(ops[i].child[k]);
+      continue;
+    }
+    if (ops[i].flags & PLK_OP_ACCUMULATE)
+      return fail(h, PLK_ERR_UNSUPPORTED, "pattern compression: op %d accumulates into a node of an earlier call", i);
+    nodes.push_back({ops[i].parent, std::vector<int>(ops[i].child, ops[i].child + ops[i].n_children)});
+  }
+  std::vector<char> produced(h->n_nodes, 0), is_child(h->n_nodes, 0);
+  for (const auto& n : nodes) {
+    if (n.kids.size() > 3) return fail(h, PLK_ERR_UNSUPPORTED, "pattern compression: node %d has > 3 children", n.node);
+    for (int c : n.kids) {
+      if (c >= nt && !produced[c])
+        return fail(h, PLK_ERR_STATE, "pattern compression: child %d of node %d not produced by this call", c, n.node);
+      is_child[c] = 1;
+    }
+    produced[n.node] = 1;
+  }
+  h->cmp_ids.assign(h->n_internal, {});
+  h->cmp_D.assign(h->n_internal, P);
+  std::vector<int32_t> code32((size_t)P), tmp, tmp2;
+  std::vector<std::vector<uint32_t> > node_links;  // per logical node: [k][D] concatenated
+  std::vector<int64_t> nodeD(nodes.size());
+  h->cmp_work = 0;
+  for (size_t ni = 0; ni < nodes.size(); ++ni) {
+    const LNode& n = nodes[ni];
+    const int slot = n.node - nt;
+    // children id arrays and counts
+    std::vector<std::vector<int32_t> > kid_ids(n.kids.size());
+    std::vector<const int32_t*> kid_ptr(n.kids.size());
+    std::vector<int64_t> kid_D(n.kids.size());
+    for (size_t k = 0; k < n.kids.size(); ++k) {
+      const int c = n.kids[k];
+      if (c < nt) {
+        kid_ids[k].resize((size_t)P);
+        const std::vector<uint8_t>& cc = h->tip_codes_host[c];
+        for (int64_t p = 0; p < P; ++p) kid_ids[k][(size_t)p] = cc[(size_t)p];
+        kid_ptr[k] = kid_ids[k].data();
+        kid_D[k] = h->n_codes;
+      } else if (h->cmp_ids[c - nt].empty()) {  // identity child (cannot happen below the top)
+        kid_ids[k].resize((size_t)P);
+        for (int64_t p = 0; p < P; ++p) kid_ids[k][(size_t)p] = (int32_t)p;
+        kid_ptr[k] = kid_ids[k].data();
+        kid_D[k] = P;
+      } else {
+        kid_ptr[k] = h->cmp_ids[c - nt].data();
+        kid_D[k] = h->cmp_D[c - nt];
+      }
+    }
+    int64_t D;
+    std::vector<int64_t> rep;  // first pattern of each distinct id
+    if (!is_child[n.node]) {
+      D = P;  // top of the traversal: every root pattern
+      h->cmp_ids[slot].clear();
+    } else {
+      std::vector<int32_t> cur(kid_ptr[0], kid_ptr[0] + P);
+      int64_t Dc = kid_D[0];
+      for (size_t k = 1; k < n.kids.size(); ++k) {
+        Dc = pair_ids(cur.data(), kid_ptr[k], kid_D[k], P, tmp, Dc);
+        cur.swap(tmp);
+      }
+      if (n.kids.size() == 1) {  // one child: renumber in first-appearance order
+        tmp2.assign((size_t)P, 0);
+        Dc = pair_ids(cur.data(), tmp2.data(), 1, P, tmp, Dc);
+        cur.swap(tmp);
+      }
+      D = Dc;
+      h->cmp_ids[slot].swap(cur);
+    }
+    h->cmp_D[slot] = D;
+    h->cmp_work += D;
+    rep.assign((size_t)D, -1);
+    if (h->cmp_ids[slot].empty()) {
+      for (int64_t j = 0; j < D; ++j) rep[(size_t)j] = j;
+    } else {
+      const std::vector<int32_t>& ids = h->cmp_ids[slot];
+      for (int64_t p = 0; p < P; ++p)
+        if (rep[(size_t)ids[(size_t)p]] < 0) rep[(size_t)ids[(size_t)p]] = p;
+    }
+    std::vector<uint32_t> lk(n.kids.size() * (size_t)D);
+    for (size_t k = 0; k < n.kids.size(); ++k)
+      for (int64_t j = 0; j < D; ++j) lk[k * (size_t)D + (size_t)j] = (uint32_t)kid_ptr[k][(size_t)rep[(size_t)j]];
+    node_links.push_back(std::move(lk));
+    nodeD[ni] = D;
+  }
+  // level the logical nodes and build the device op list
+  std::vector<int> lev(h->n_nodes, -1), nlev(nodes.size());
+  int max_level = 0;
+  for (size_t ni = 0; ni < nodes.size(); ++ni) {
+    int l = 0;
+    for (int c : nodes[ni].kids)
+      if (c >= nt) l = std::max(l, lev[c] + 1);
+    lev[nodes[ni].node] = l;
+    nlev[ni] = l;
+    max_level = std::max(max_level, l);
+  }
+  std::vector<int> start(max_level + 2, 0);
+  for (size_t ni = 0; ni < nodes.size(); ++ni) start[nlev[ni] + 1]++;
+  for (int l = 0; l <= max_level; ++l) start[l + 1] += start[l];
+  std::vector<int> fill(start.begin(), start.end() - 1);
+  std::vector<KOpL> kops(nodes.size());
+  std::vector<int64_t> link_off(nodes.size());
+  int64_t total = 0;
+  for (size_t ni = 0; ni < nodes.size(); ++ni) {
+    link_off[ni] = total;
+    total += (int64_t)node_links[ni].size();
+  }
+  h->cmp_level_maxD.assign(max_level + 1, 0);
+  for (size_t ni = 0; ni < nodes.size(); ++ni) {
+    KOpL k;
+    std::memset(&k, 0, sizeof(k));
+    k.parent = nodes[ni].node - nt;
+    k.n = (int32_t)nodes[ni].kids.size();
+    k.D = (int32_t)nodeD[ni];
+    for (int j = 0; j < k.n; ++j) {
+      const int c = nodes[ni].kids[(size_t)j];
+      k.branch[j] = c;
+      k.is_tip[j] = c < nt;
+      k.child[j] = c < nt ? c : c - nt;
+      k.link[j] = link_off[ni] + (int64_t)j * nodeD[ni];
+    }
+    kops[(size_t)fill[nlev[ni]]++] = k;
+    h->cmp_level_maxD[nlev[ni]] = std::max<int>(h->cmp_level_maxD[nlev[ni]], k.D);
+  }
+  int rc = ensure_cap(h, (void**)&h->d_links, &h->d_links_cap, (size_t)std::max<int64_t>(total, 1) * sizeof(uint32_t));
+  if (rc) return rc;
+  rc = ensure_cap(h, (void**)&h->d_opsl, &h->d_opsl_cap, kops.size() * sizeof(KOpL));
+  if (rc) return rc;
+  for (size_t ni = 0; ni < nodes.size(); ++ni)
+    HIPCHK(h, hipMemcpy(h->d_links + link_off[ni], node_links[ni].data(), node_links[ni].size() * sizeof(uint32_t),
+                        hipMemcpyHostToDevice));
+  HIPCHK(h, hipMemcpy(h->d_opsl, kops.data(), kops.size() * sizeof(KOpL), hipMemcpyHostToDevice));
+  h->cmp_level_start = start;
+  h->cmp_ops.assign(ops, ops + n_ops);
+  h->cmp_valid = true;
+  return PLK_OK;
+}
+
+template <int C>
+void launch_links(plk_handle h, const KOpL* d, int cnt, int maxD, const PartialsArgs& a) {
+  const dim3 grid((unsigned)((maxD + 255) / 256), (unsigned)cnt), block(256);
+  if (h->flags & PLK_FLAG_SCALING)
+    partials_links_s4_kernel<C, true><<<grid, block, 0, h->stream>>>(d, a, h->d_links);
+  else
+    partials_links_s4_kernel<C, false><<<grid, block, 0, h->stream>>>(d, a, h->d_links);
+}
+
+int update_compressed(plk_handle h, const plk_op* ops, int n_ops) {
+  h->kernel_path = "subtree_patterns";
+  const bool same = h->cmp_valid && h->cmp_ops.size() == (size_t)n_ops &&
+                    std::memcmp(h->cmp_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
+  if (!same) {
+    int rc = build_compression(h, ops, n_ops);
+    if (rc) return rc;
+  }
+  int rc = refresh_tip_tables(h);
+  if (rc) return rc;
+  PartialsArgs a;
+  a.partials = h->partials;
+  a.scale = h->scale;
+  a.codes = h->codes;
+  a.tipP = h->tipP;
+  a.pmats = h->pmats;
+  a.slot_stride = h->slot_stride;
+  a.n_pad = h->n_pad;
+  a.n_tiles = h->n_tiles;
+  a.n_codes = h->n_codes;
+  const int L = (int)h->cmp_level_start.size() - 1;
+  for (int l = 0; l < L; ++l) {
+    const int cnt = h->cmp_level_start[l + 1] - h->cmp_level_start[l];
+    if (cnt == 0) continue;
+    const KOpL* d = h->d_opsl + h->cmp_level_start[l];
+    EventPair ev;
+    if (h->timing & PLK_TIME_PARTIALS) {
+      ev = get_events(h, 0);
+      hipEventRecord(ev.a, h->stream);
+    }
+    const int maxD = h->cmp_level_maxD[l];
+    switch (h->C) {
+      case 1: launch_links<1>(h, d, cnt, maxD, a); break;
+      case 2: launch_links<2>(h, d, cnt, maxD, a); break;
+      case 4: launch_links<4>(h, d, cnt, maxD, a); break;
+      case 8: launch_links<8>(h, d, cnt, maxD, a); break;
+    }
+    HIPCHK(h, hipGetLastError());
+    if (h->timing & PLK_TIME_PARTIALS) {
+      hipEventRecord(ev.b, h->stream);
+      h->events.push_back(ev);
+    }
+    h->n_launches++;
+  }
+  for (int i = 0; i < n_ops; ++i) h->materialized[ops[i].parent - h->n_tips] = 1;
+  h->fused_lnl_valid = false;
+  h->blocks_fused = false;
+  return PLK_OK;
+}
+
 int validate_ops(plk_handle h, const plk_op* ops, int n_ops) {
   std::vector<char> done(h->n_nodes, 0);
   for (int i = 0; i < n_ops; ++i) {
@@ -1360,6 +1650,7 @@ int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
   int rc = validate_ops(h, ops, n_ops);
   if (rc) return rc;
   h->trav_ops.assign(ops, ops + n_ops);
+  if (h->flags & PLK_FLAG_SUBTREE_PATTERNS) return update_compressed(h, ops, n_ops);
   if (tree4_supported(h) && fusable(ops, n_ops)) return update_tree4(h, ops, n_ops);
   return update_levelwise(h, ops, n_ops);
 }
@@ -1384,8 +1675,13 @@ int plk_get_partials(plk_handle h, int node, double* out) {
   HIPCHK(h, hipMemcpy(buf.data(), h->partials + (size_t)(node - h->n_tips) * h->slot_stride,
                       buf.size() * sizeof(double), hipMemcpyDeviceToHost));
   const int CS = h->C * h->S;
+  // compressed node: its slot holds one entry per distinct subtree pattern
+  const std::vector<int32_t>* ids = nullptr;
+  if ((h->flags & PLK_FLAG_SUBTREE_PATTERNS) && h->cmp_valid && !h->cmp_ids[node - h->n_tips].empty())
+    ids = &h->cmp_ids[node - h->n_tips];
   for (int64_t p = 0; p < h->n_patterns; ++p) {
-    const int64_t tile = p / kTile, q = p % kTile;
+    const int64_t j = ids ? (*ids)[(size_t)p] : p;
+    const int64_t tile = j / kTile, q = j % kTile;
     for (int cs = 0; cs < CS; ++cs) out[p * CS + cs] = buf[(tile * CS + cs) * kTile + q];
   }
   return PLK_OK;
@@ -1598,5 +1894,13 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
 }
 
 const char* plk_kernel_path(plk_handle h) { return h ? h->kernel_path.c_str() : ""; }
+
+int plk_compressed_work(plk_handle h, int64_t* updates) {
+  if (!h || !updates) return fail(h, PLK_ERR_ARG, "null argument");
+  if (!(h->flags & PLK_FLAG_SUBTREE_PATTERNS) || !h->cmp_valid)
+    return fail(h, PLK_ERR_STATE, "no compressed traversal yet");
+  *updates = h->cmp_work;
+  return PLK_OK;
+}
 
 }  // extern "C"

@@ -172,6 +172,104 @@ __global__ __launch_bounds__(256) void partials_s4_kernel(const KOp* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// Per-subtree site-pattern compression (reference usePatterns = true,
+// Likelihood/DRASRTreeLikelihoodData.cpp:218-332): a node's partial is computed once
+// per DISTINCT pattern of its subtree's tips (D of them, D <= n_patterns; the first D
+// entries of its slot, same tile layout) and each child is read through a pattern
+// link -- the child's distinct pattern (or, for a tip, its compact code) of parent
+// pattern j, the reference's patternLinks_[node][son].  One lane = one parent
+// pattern; the arithmetic per pattern is partials_s4_kernel's, so the values are
+// bitwise those of the uncompressed traversal.
+// ---------------------------------------------------------------------------
+struct KOpL {
+  int32_t parent;    // internal slot
+  int32_t n;         // children (1..3)
+  int32_t D;         // distinct patterns of the parent's subtree
+  int32_t pad_;
+  int32_t child[3];  // tip index or internal slot
+  int32_t branch[3]; // node index of the child = transition-matrix index
+  int32_t is_tip[3];
+  int32_t pad2_;
+  int64_t link[3];   // offset of the child's link array (D uint32) in the link pool
+};
+
+template <int C, bool SCALE>
+__global__ __launch_bounds__(256) void partials_links_s4_kernel(const KOpL* __restrict__ ops, PartialsArgs a,
+                                                                const uint32_t* __restrict__ links) {
+  constexpr int S = 4;
+  constexpr int CS = C * S;
+  __shared__ double tipT[3][C * kMaxCodes4 * S];
+  const KOpL& op = ops[blockIdx.y];
+  const int n = op.n;
+  const int nc = a.n_codes;
+  if ((int)(blockIdx.x * blockDim.x) >= op.D) return;  // whole workgroup past this op's patterns
+  for (int k = 0; k < n; ++k)
+    if (op.is_tip[k]) {
+      const double* src = a.tipP + (size_t)op.child[k] * (C * nc * S);
+      for (int i = threadIdx.x; i < C * nc * S; i += blockDim.x) tipT[k][i] = src[i];
+    }
+  __syncthreads();
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= op.D) return;
+  double acc[C][S];
+  int cnt = 0;
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int x = 0; x < S; ++x) acc[c][x] = 1.0;
+  for (int k = 0; k < n; ++k) {
+    const uint32_t l = links[op.link[k] + j];
+    if (op.is_tip[k]) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const double* t = &tipT[k][(c * nc + (int)l) * S];
+#pragma unroll
+        for (int x = 0; x < S; ++x) acc[c][x] *= t[x];
+      }
+    } else {
+      const double* __restrict__ P = a.pmats + (size_t)op.branch[k] * (C * S * S);
+      const double* L = a.partials + (size_t)op.child[k] * a.slot_stride + (size_t)(l >> 7) * (CS * kTile) + (l & 127);
+      double v[C][S];
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int y = 0; y < S; ++y) v[c][y] = L[(c * S + y) * kTile];
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+          const double* Px = P + (c * S + x) * S;
+          double s = Px[0] * v[c][0];
+#pragma unroll
+          for (int y = 1; y < S; ++y) s = __builtin_fma(Px[y], v[c][y], s);
+          acc[c][x] *= s;
+        }
+      if (SCALE) cnt += a.scale[(size_t)op.child[k] * a.n_pad + l];
+    }
+  }
+  if (SCALE) {
+    double m = 0.0;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int x = 0; x < S; ++x) m = fmax(m, acc[c][x]);
+    if (m > 0.0 && m < kScaleThr) {
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int x = 0; x < S; ++x) acc[c][x] *= kScaleUp;
+      cnt += 1;
+    }
+    a.scale[(size_t)op.parent * a.n_pad + j] = cnt;
+  }
+  double* out = a.partials + (size_t)op.parent * a.slot_stride + (size_t)(j >> 7) * (CS * kTile) + (j & 127);
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int x = 0; x < S; ++x) out[(c * S + x) * kTile] = acc[c][x];
+}
+
+// ---------------------------------------------------------------------------
 // Generic-S kernel (S up to 64): one lane = one pattern, 2 tiles per 256-thread
 // workgroup.  The children's P(t) (C x S x S each) and tip tables are staged in
 // LDS once per workgroup; inner products read P by wave-uniform LDS address

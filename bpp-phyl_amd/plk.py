@@ -21,6 +21,7 @@ PLK_FLAG_SCALING = 1
 PLK_FLAG_NONNEG_GUARD = 2
 PLK_FLAG_LNL_ONLY = 4
 PLK_FLAG_LEVELWISE = 8
+PLK_FLAG_SUBTREE_PATTERNS = 16
 PLK_DERIV_P, PLK_DERIV_DP, PLK_DERIV_D2P = 1, 2, 4
 PLK_OP_ACCUMULATE = 1
 PLK_TIME_PARTIALS, PLK_TIME_PMAT, PLK_TIME_ROOT = 1, 2, 4
@@ -32,7 +33,7 @@ EXPORTS = [
     "plk_set_root_frequencies", "plk_set_eigen", "plk_update_pmatrices", "plk_set_pmatrix",
     "plk_get_pmatrix", "plk_update_partials", "plk_get_partials", "plk_root_loglik", "plk_block_size",
     "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
-    "plk_kernel_path", "plk_evaluate",
+    "plk_kernel_path", "plk_evaluate", "plk_compressed_work",
 ]
 
 
@@ -85,6 +86,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_synchronize": ([ct.c_void_p], ct.c_int),
         "plk_branch_derivatives": ([ct.c_void_p, ct.c_int, dp, dp], ct.c_int),
         "plk_kernel_path": ([ct.c_void_p], ct.c_char_p),
+        "plk_compressed_work": ([ct.c_void_p, P(ct.c_int64)], ct.c_int),
         "plk_evaluate": ([ct.c_void_p, ct.c_int, ip, ip, dp, P(plk_op), ct.c_int, ct.c_int, dp, dp], ct.c_int),
     }
     for name, (args, res) in sig.items():
@@ -260,6 +262,12 @@ class Engine:
 
     def synchronize(self):
         self._chk(self.lib.plk_synchronize(self.h))
+
+    def compressed_work(self) -> int:
+        """Node updates the last compressed traversal computed (sum of distinct subtree patterns)."""
+        n = ct.c_int64(0)
+        self._chk(self.lib.plk_compressed_work(self.h, ct.byref(n)))
+        return n.value
 
     def kernel_path(self) -> str:
         """Kernel that served the last update_partials ("jit_tree4", "tree4", "treeS", "treeM", "levelwise")."""

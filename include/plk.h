@@ -78,8 +78,15 @@ enum {
   PLK_FLAG_LNL_ONLY = 1u << 2,   /* 4-state fused traversal keeps interior partials in
                                     registers and materialises only fragment roots; other
                                     partials are recomputed on demand by plk_get_partials */
-  PLK_FLAG_LEVELWISE = 1u << 3   /* force one launch per tree level (every child partial
+  PLK_FLAG_LEVELWISE = 1u << 3,  /* force one launch per tree level (every child partial
                                     re-read from HBM); for A/B measurements */
+  PLK_FLAG_SUBTREE_PATTERNS = 1u << 4 /* per-subtree site-pattern compression, the reference's
+                                    usePatterns = true (DRASRTreeLikelihoodData.cpp:218-332):
+                                    each internal node is computed once per distinct pattern of
+                                    its subtree and read through pattern links.  Links are
+                                    built on the host from the tip codes and the op list (all
+                                    internal children must be produced by the same call);
+                                    4-state models only */
 };
 
 /* plk_update_pmatrices deriv_mask */
@@ -170,6 +177,11 @@ int plk_synchronize(plk_handle h);
 /* Name of the kernel that served the last plk_update_partials call ("jit_tree4",
  * "tree4", "treeS", "treeM" or "levelwise"); "" before the first call. */
 const char* plk_kernel_path(plk_handle h);
+
+/* With PLK_FLAG_SUBTREE_PATTERNS: the node updates the last traversal actually computed,
+ * i.e. the sum over its internal nodes of their distinct subtree patterns (the
+ * uncompressed traversal computes n_patterns per node). */
+int plk_compressed_work(plk_handle h, int64_t* updates);
 
 #ifdef __cplusplus
 }

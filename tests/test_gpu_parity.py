@@ -568,3 +568,79 @@ def test_branch_derivatives_require_dp():
     with pytest.raises(plk.PlkError) as ei:
         eng.branch_derivatives(0)
     assert ei.value.code == -5
+
+
+# ---------------------------------------------------------------- per-subtree pattern compression (row f3)
+
+@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,amb", [
+    (4, "balanced64", 5000, False, False), (4, "balanced64", 3000, False, True), (1, "caterpillar40", 700, True, True),
+    (2, "balanced300", 900, True, False), (4, "caterpillar200long", 400, True, False)])
+def test_subtree_patterns_bitwise_vs_uncompressed(C, tree_kind, n_patterns, scaling, amb):
+    """PLK_FLAG_SUBTREE_PATTERNS (the reference's usePatterns=true, links built from the
+    data) gives bitwise the uncompressed traversal's lnL, per-site lnL, block sums and every
+    node's partial (expanded through the links), computes fewer node updates, and matches
+    the oracle's own usePatterns=true path at 1e-12."""
+    if tree_kind.startswith("balanced"):
+        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=29, lo=0.05, hi=0.4)
+    elif tree_kind.endswith("long"):
+        tree = _caterpillar(int(tree_kind[11:-4]), seed=7, lo=0.5, hi=1.5)
+    else:
+        tree = _caterpillar(int(tree_kind[11:]), seed=7)
+    et = phylo.engine_tree(tree)
+    rng = np.random.default_rng(C * 13 + n_patterns)
+    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
+    rates, probs = phylo.gamma_rates(C, 0.5) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, scaling, True, 9)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    if amb:
+        mask = rng.random(states.shape) < 0.05
+        states[mask] = rng.integers(4, 15, size=mask.sum())
+    sc = plk.PLK_FLAG_SCALING if scaling else 0
+    ref = engine_for(et, 4, C, n_patterns, states, phylo.DNA.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | sc)
+    l0, s0, b0 = run_engine(ref, et)
+    p0 = np.stack([ref.get_partials(p) for p, _ in et.ops])
+    del ref
+    eng = engine_for(et, 4, C, n_patterns, states, phylo.DNA.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | sc | plk.PLK_FLAG_SUBTREE_PATTERNS)
+    l1, s1, b1 = run_engine(eng, et)
+    assert eng.kernel_path() == "subtree_patterns"
+    p1 = np.stack([eng.get_partials(p) for p, _ in et.ops])
+    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1) and np.array_equal(p0, p1)
+    assert eng.compressed_work() < n_patterns * et.n_internal
+    # a second evaluation at other branch lengths reuses the links
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    l2, _ = eng.evaluate(br, et.brlen[br] * 1.2, phylo.split_ops(et.ops), et.root)
+    assert np.isfinite(l2) and l2 != l1
+    ss, sons, lr = et.son_arrays()
+    lo, so, _, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, phylo.DNA.init_table, engine_pmats(eng, et), probs,
+                                      m.pi, use_patterns=True, scaling=scaling, want_sites=True)
+    check(l2, eng.root_loglik(et.root, want_sites=True)[1], lo, so)
+
+
+def test_subtree_patterns_follow_new_tip_codes():
+    """New tip codes invalidate the links: the compressed engine then agrees with a fresh
+    uncompressed engine on the new data."""
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 24, 2000, seed=41)
+    eng = engine_for(et, 4, 4, 2000, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_SUBTREE_PATTERNS)
+    run_engine(eng, et)
+    states2 = states.copy()
+    states2[3] = np.random.default_rng(1).integers(0, 4, size=states.shape[1])
+    eng.set_tip_codes(3, states2[3].astype(np.uint8))
+    l1, s1, _ = run_engine(eng, et)
+    ref = engine_for(et, 4, 4, 2000, states2, alph.init_table, rates, probs, m.pi, [m])
+    l0, s0, _ = run_engine(ref, et)
+    assert l0 == l1 and np.array_equal(s0, s1)
+
+
+def test_subtree_patterns_errors():
+    et, m, alph, rates, probs, states = _random_problem(4, 2, 12, 300, seed=43)
+    with pytest.raises(plk.PlkError):   # 20 states: not supported with compression
+        plk.Engine(0, 20, 2, 300, et.n_tips, et.n_internal, 1, plk.PLK_FLAG_SUBTREE_PATTERNS)
+    eng = engine_for(et, 4, 2, 300, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_SUBTREE_PATTERNS)
+    run_engine(eng, et)
+    ops = phylo.split_ops(et.ops)
+    with pytest.raises(plk.PlkError):   # a child produced by an earlier call: links need the whole subtree
+        eng.update_partials(ops[-1:])
