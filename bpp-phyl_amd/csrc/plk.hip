@@ -267,6 +267,8 @@ int jit_function(plk_handle h, const std::string& src, const char* name, hipFunc
 
 bool s4_supported(int C) { return C == 1 || C == 2 || C == 4 || C == 8; }
 
+constexpr int kDerivScratch = 4;  // partial slots: dL ping-pong, d2L ping-pong
+
 template <bool SCALE>
 void launch_s4(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
   dim3 grid((a.n_tiles + 3) / 4, n_ops), block(256);
@@ -291,12 +293,12 @@ void launch_generic_S(plk_handle h, const KOp* d_ops, int n_ops, const PartialsA
 // refreshed lazily after any P(t) change.
 int ensure_pmatsT(plk_handle h) {
   if (!h->pmatsT) {
-    int rc = dalloc(h, (void**)&h->pmatsT, (size_t)h->n_nodes * h->C * h->S * h->S * sizeof(double));
+    int rc = dalloc(h, (void**)&h->pmatsT, (size_t)(h->n_nodes + 2) * h->C * h->S * h->S * sizeof(double));
     if (rc) return rc;
     h->pmatsT_dirty = true;
   }
   if (h->pmatsT_dirty) {
-    const dim3 grid(h->n_nodes, h->C);
+    const dim3 grid(h->n_nodes + 2, h->C);  // + the derivative scratch matrices
     if (h->S == 64)
       transpose_pmats<64><<<grid, 256, 0, h->stream>>>(h->pmats, h->pmatsT, h->C);
     else if (h->S == 20)
@@ -452,12 +454,16 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(nullptr, PLK_ERR_DEVICE, "hipStreamCreate failed"));
   const size_t S2 = (size_t)n_states * n_states;
-  if ((rc = dalloc(h, (void**)&h->partials, (size_t)n_internal * h->slot_stride * sizeof(double)))) return bail(rc);
+  // kDerivScratch extra slots / scale rows, 2 extra tip rows and 2 extra transition
+  // matrices: scratch for the path derivatives of plk_branch_derivatives (S != 4 path)
+  if ((rc = dalloc(h, (void**)&h->partials, (size_t)(n_internal + kDerivScratch) * h->slot_stride * sizeof(double))))
+    return bail(rc);
   if (flags & PLK_FLAG_SCALING) {
-    if ((rc = dalloc(h, (void**)&h->scale, (size_t)n_internal * h->n_pad * sizeof(int32_t)))) return bail(rc);
+    if ((rc = dalloc(h, (void**)&h->scale, (size_t)(n_internal + kDerivScratch) * h->n_pad * sizeof(int32_t))))
+      return bail(rc);
   }
-  if ((rc = dalloc(h, (void**)&h->codes, (size_t)std::max(n_tips, 1) * h->n_pad))) return bail(rc);
-  if ((rc = dalloc(h, (void**)&h->pmats, (size_t)h->n_nodes * n_classes * S2 * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->codes, (size_t)(n_tips + 2) * h->n_pad))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->pmats, (size_t)(h->n_nodes + 2) * n_classes * S2 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->V, (size_t)n_models * S2 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->Vinv, (size_t)n_models * S2 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->lambda, (size_t)n_models * n_states * sizeof(double)))) return bail(rc);
@@ -523,7 +529,7 @@ int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec) {
   h->tipP = nullptr;
   int rc;
   if ((rc = dalloc(h, (void**)&h->code_table, (size_t)n_codes * h->S * sizeof(double)))) return rc;
-  if ((rc = dalloc(h, (void**)&h->tipP, (size_t)std::max(h->n_tips, 1) * h->C * n_codes * h->S * sizeof(double))))
+  if ((rc = dalloc(h, (void**)&h->tipP, (size_t)(h->n_tips + 2) * h->C * n_codes * h->S * sizeof(double))))
     return rc;
   h->code_table_host.assign(code_to_vec, code_to_vec + (size_t)n_codes * h->S);
   h->n_codes_table = n_codes;
@@ -1610,6 +1616,173 @@ int update_compressed(plk_handle h, const plk_op* ops, int n_ops) {
   return PLK_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Branch derivatives for any S and C (row f1; the 4-state fast path is deriv_kernel):
+// the reference's computeDownSubtreeDLikelihood / D2 twins
+// (Likelihood/RHomogeneousTreeLikelihood.cpp:365-541, 615-791) as levelwise partial
+// updates.  lnL is linear in the P(t) of one branch, so dL at the root is the
+// traversal with P_b replaced by dP_b (d2L: d2P_b), recomputed only along the path
+// from the branch to the root with every sibling read from its materialised partial.
+// dP_b / d2P_b go to two scratch transition matrices (and, for a tip branch, a scratch
+// tip row with its codes and table); the path vectors ping-pong between scratch slots.
+// ---------------------------------------------------------------------------
+int launch_partials_ops(plk_handle h, const KOp* d_ops, int n_ops) {
+  PartialsArgs a;
+  a.partials = h->partials;
+  a.scale = h->scale;
+  a.codes = h->codes;
+  a.tipP = h->tipP;
+  a.pmats = h->pmats;
+  a.slot_stride = h->slot_stride;
+  a.n_pad = h->n_pad;
+  a.n_tiles = h->n_tiles;
+  a.n_codes = h->n_codes;
+  if (h->S == 4 && s4_supported(h->C) && h->n_codes <= kMaxCodes4) {
+    if (h->flags & PLK_FLAG_SCALING)
+      launch_s4<true>(h, d_ops, n_ops, a);
+    else
+      launch_s4<false>(h, d_ops, n_ops, a);
+  } else {
+    int rc = launch_generic(h, d_ops, n_ops, a);
+    if (rc) return rc;
+  }
+  HIPCHK(h, hipGetLastError());
+  return PLK_OK;
+}
+
+int materialize_last_traversal(plk_handle h);
+
+int path_derivatives(plk_handle h, int branch, double* d1, double* d2) {
+  if (h->deriv_valid.empty() || !h->deriv_valid[branch])
+    return fail(h, PLK_ERR_STATE, "dP/d2P of branch %d not computed (PLK_DERIV_DP | PLK_DERIV_D2P)", branch);
+  if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
+  if (h->flags & PLK_FLAG_SUBTREE_PATTERNS)
+    return fail(h, PLK_ERR_UNSUPPORTED, "path derivatives read full-length partials (no pattern compression)");
+  hipSetDevice(h->device);
+  const int nt = h->n_tips;
+  std::vector<std::vector<int> > kids(h->n_nodes);
+  std::vector<int> parent(h->n_nodes, -1);
+  for (const plk_op& o : h->trav_ops)
+    for (int k = 0; k < o.n_children; ++k) {
+      kids[o.parent].push_back(o.child[k]);
+      parent[o.child[k]] = o.parent;
+    }
+  if (parent[branch] < 0) return fail(h, PLK_ERR_ARG, "branch %d is not below any node of the last traversal", branch);
+  int root = parent[branch];
+  while (parent[root] >= 0) root = parent[root];
+  bool need = !h->materialized[root - nt];
+  for (int n = parent[branch]; n >= 0; n = parent[n])
+    for (int c : kids[n])
+      if (c >= nt && !h->materialized[c - nt]) need = true;
+  if (need) {
+    int rc = materialize_last_traversal(h);
+    if (rc) return rc;
+  }
+  int rc = refresh_tip_tables(h);
+  if (rc) return rc;
+  const int C = h->C, S = h->S, nc = h->n_codes;
+  const size_t PS = (size_t)C * S * S;
+  const int sb[2] = {h->n_nodes, h->n_nodes + 1};     // scratch transition matrices (dP_b, d2P_b)
+  const int st[2] = {nt, nt + 1};                     // scratch tip rows
+  const int slot0 = h->n_internal;                    // scratch slots: pass x uses slot0 + 2x, +1
+  const double* src[2] = {h->dpmats, h->d2pmats};
+  for (int x = 0; x < 2; ++x) {
+    HIPCHK(h, hipMemcpyAsync(h->pmats + (size_t)sb[x] * PS, src[x] + (size_t)branch * PS, PS * sizeof(double),
+                             hipMemcpyDeviceToDevice, h->stream));
+    if (branch < nt) {
+      HIPCHK(h, hipMemcpyAsync(h->codes + (size_t)st[x] * h->n_pad, h->codes + (size_t)branch * h->n_pad,
+                               (size_t)h->n_pad, hipMemcpyDeviceToDevice, h->stream));
+      tip_table_kernel<<<dim3(1, C), 256, 0, h->stream>>>(h->pmats + (size_t)sb[x] * PS, h->code_table,
+                                                          h->tipP + (size_t)st[x] * C * nc * S, 1, C, S, nc);
+      HIPCHK(h, hipGetLastError());
+    }
+  }
+  h->pmatsT_dirty = true;  // S = 64 kernels read the transposed copy, scratch included
+  // one launch per (path node, child chunk): both passes side by side
+  std::vector<std::vector<KOp> > launches;
+  int path = branch, cur = 0;
+  for (int n = parent[branch]; n >= 0; path = n, n = parent[n]) {
+    std::vector<KOp> chunk[2];
+    for (int x = 0; x < 2; ++x) {
+      const int out = slot0 + 2 * x + (cur & 1), in = slot0 + 2 * x + ((cur + 1) & 1);
+      const std::vector<int>& ks = kids[n];
+      for (size_t k0 = 0; k0 < ks.size(); k0 += 3) {
+        KOp op;
+        std::memset(&op, 0, sizeof(op));
+        op.parent = out;
+        op.flags = k0 == 0 ? 0 : PLK_OP_ACCUMULATE;
+        for (size_t k = k0; k < ks.size() && k < k0 + 3; ++k) {
+          const int c = ks[k], j = op.n++;
+          if (c == path && path == branch) {        // the differentiated branch
+            op.is_tip[j] = c < nt;
+            op.child[j] = c < nt ? st[x] : c - nt;
+            op.branch[j] = sb[x];
+          } else if (c == path) {                   // the path vector from the step below
+            op.is_tip[j] = 0;
+            op.child[j] = in;
+            op.branch[j] = c;
+          } else {
+            op.is_tip[j] = c < nt;
+            op.child[j] = c < nt ? c : c - nt;
+            op.branch[j] = c;
+          }
+        }
+        chunk[x].push_back(op);
+      }
+    }
+    for (size_t j = 0; j < chunk[0].size(); ++j) launches.push_back({chunk[0][j], chunk[1][j]});
+    ++cur;
+  }
+  std::vector<KOp> flat;
+  for (auto& l : launches) flat.insert(flat.end(), l.begin(), l.end());
+  rc = ensure_cap(h, (void**)&h->d_ops, &h->d_ops_cap, flat.size() * sizeof(KOp));
+  if (rc) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->d_ops, flat.data(), flat.size() * sizeof(KOp), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->last_ops.clear();  // d_ops now holds these ops, not the levelwise traversal's
+  for (size_t l = 0; l < launches.size(); ++l) {
+    rc = launch_partials_ops(h, h->d_ops + 2 * l, 2);
+    if (rc) return rc;
+  }
+  const int last = (cur - 1) & 1;
+  if (!h->d1_sums) {
+    if ((rc = dalloc(h, (void**)&h->d1_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return rc;
+    if ((rc = dalloc(h, (void**)&h->d2_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return rc;
+  }
+  DRArgs a;
+  a.L = h->partials + (size_t)(root - nt) * h->slot_stride;
+  a.dL = h->partials + (size_t)(slot0 + last) * h->slot_stride;
+  a.d2L = h->partials + (size_t)(slot0 + 2 + last) * h->slot_stride;
+  const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
+  a.k0 = sc ? h->scale + (size_t)(root - nt) * h->n_pad : nullptr;
+  a.k1 = sc ? h->scale + (size_t)(slot0 + last) * h->n_pad : nullptr;
+  a.k2 = sc ? h->scale + (size_t)(slot0 + 2 + last) * h->n_pad : nullptr;
+  a.pi = h->pi;
+  a.probs = h->probs;
+  a.weights = h->weights;
+  a.d1_sums = h->d1_sums;
+  a.d2_sums = h->d2_sums;
+  a.n_patterns = h->n_patterns;
+  a.S = S;
+  a.C = C;
+  a.guard = (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0;
+  deriv_reduce_kernel<<<(unsigned)(h->n_pad / 256), 256, 0, h->stream>>>(a);
+  HIPCHK(h, hipGetLastError());
+  const int n_waves = (int)((h->n_patterns + 63) / 64);
+  std::vector<double> w1(n_waves), w2(n_waves);
+  HIPCHK(h, hipMemcpyAsync(w1.data(), h->d1_sums, n_waves * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(w2.data(), h->d2_sums, n_waves * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = 0; i < n_waves; ++i) {
+    s1 += w1[i];
+    s2 += w2[i];
+  }
+  if (d1) *d1 = s1;
+  if (d2) *d2 = s2;
+  return PLK_OK;
+}
+
 int validate_ops(plk_handle h, const plk_op* ops, int n_ops) {
   std::vector<char> done(h->n_nodes, 0);
   for (int i = 0; i < n_ops; ++i) {
@@ -1637,6 +1810,18 @@ bool fusable(const plk_op* ops, int n_ops) {
   for (int i = 0; i < n_ops; ++i)
     if ((ops[i].flags & PLK_OP_ACCUMULATE) && (i == 0 || ops[i - 1].parent != ops[i].parent)) return false;
   return true;
+}
+
+// Re-run the last traversal writing every partial (same arithmetic, identical values).
+int materialize_last_traversal(plk_handle h) {
+  const unsigned saved = h->flags;
+  const std::vector<plk_op> ops = h->trav_ops;
+  h->flags &= ~(unsigned)PLK_FLAG_LNL_ONLY;
+  const int rc = tree4_supported(h) && fusable(ops.data(), (int)ops.size())
+                     ? update_tree4(h, ops.data(), (int)ops.size())
+                     : update_levelwise(h, ops.data(), (int)ops.size());
+  h->flags = saved;
+  return rc;
 }
 
 }  // namespace
@@ -1754,9 +1939,9 @@ static int launch_root(plk_handle h, int root) {
 
 int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   if (!h || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
-  if (h->S != 4 || !(h->C == 1 || h->C == 2 || h->C == 4))
-    return fail(h, PLK_ERR_UNSUPPORTED, "branch derivatives need S = 4 and C in {1, 2, 4}");
   if (h->trav_ops.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet (plk_update_partials)");
+  if (h->S != 4 || !(h->C == 1 || h->C == 2 || h->C == 4) || env_is("PLK_DERIV_PATH", '1'))
+    return path_derivatives(h, branch, d1, d2);
   if (h->deriv_valid.empty() || !h->deriv_valid[branch])
     return fail(h, PLK_ERR_STATE, "dP/d2P of branch %d not computed (PLK_DERIV_DP | PLK_DERIV_D2P)", branch);
   if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");

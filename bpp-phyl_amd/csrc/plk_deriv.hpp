@@ -174,4 +174,68 @@ __global__ __launch_bounds__(256) void deriv_kernel(DerivArgs a, const DInstr* _
   }
 }
 
+// ---------------------------------------------------------------------------
+// Any S, C: derivatives from the path partials of plk_branch_derivatives' levelwise
+// path (dL and d2L of the root computed by the partials kernels with the branch's P
+// replaced by r_c dP/dt and r_c^2 d2P/dt2 -- lnL is linear in P of one branch).  Each
+// root vector carries its own power-of-two scale count, so per pattern
+//   dl / l = (dl' / l') 2^(256 (k - k1)),   d2l / l = (d2l'' / l') 2^(256 (k - k2))
+// with the same guards as deriv_kernel (per-term <= 0 dropped in l only).
+// ---------------------------------------------------------------------------
+struct DRArgs {
+  const double* L;    // root slot
+  const double* dL;   // root dL (scratch slot)
+  const double* d2L;  // root d2L (scratch slot)
+  const int32_t* k0;  // scale rows (null without scaling)
+  const int32_t* k1;
+  const int32_t* k2;
+  const double* pi;
+  const double* probs;
+  const double* weights;
+  double* d1_sums;
+  double* d2_sums;
+  int64_t n_patterns;
+  int S, C, guard;
+};
+
+__global__ __launch_bounds__(256) void deriv_reduce_kernel(DRArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tile = p >> 7, q = p & (kTile - 1);
+  const int CS = a.C * a.S;
+  double r1 = 0.0, r2 = 0.0;
+  if (p < a.n_patterns) {
+    const size_t off = (size_t)tile * CS * kTile + q;
+    double l = 0.0, dl = 0.0, d2l = 0.0;
+    for (int c = 0; c < a.C; ++c) {
+      double lc = 0.0, dlc = 0.0, d2lc = 0.0;
+      for (int x = 0; x < a.S; ++x) {
+        const size_t i = off + (size_t)(c * a.S + x) * kTile;
+        const double li = a.L[i] * a.pi[x];
+        if (!a.guard || li > 0.0) lc += li;
+        dlc += a.dL[i] * a.pi[x];
+        d2lc += a.d2L[i] * a.pi[x];
+      }
+      l += lc * a.probs[c];
+      dl += dlc * a.probs[c];
+      d2l += d2lc * a.probs[c];
+    }
+    double g = dl / l, hh = d2l / l;
+    if (a.k0) {
+      g = ldexp(g, 256 * (a.k0[p] - a.k1[p]));
+      hh = ldexp(hh, 256 * (a.k0[p] - a.k2[p]));
+    }
+    r1 = a.weights[p] * g;
+    r2 = a.weights[p] * (hh - g * g);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    r1 += __shfl_xor(r1, off, 64);
+    r2 += __shfl_xor(r2, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    a.d1_sums[p >> 6] = r1;
+    a.d2_sums[p >> 6] = r2;
+  }
+}
+
 }  // namespace plk

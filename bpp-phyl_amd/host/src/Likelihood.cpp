@@ -302,9 +302,9 @@ VVVdouble AbstractPlkTreeLikelihood::getLikelihoodArray(int nodeId) const {
 }
 
 // Branch-length derivatives: analytic on the device (plk_branch_derivatives, the
-// dL / d2L propagation of Likelihood/RHomogeneousTreeLikelihood.cpp:346-541, 596-791);
-// central differences of the device log-likelihood where the engine has no
-// derivative kernel (state counts other than 4).
+// dL / d2L propagation of Likelihood/RHomogeneousTreeLikelihood.cpp:346-541, 596-791)
+// for every model; central differences of the device log-likelihood only if the
+// engine reports PLK_ERR_UNSUPPORTED (per-subtree pattern compression).
 bool AbstractPlkTreeLikelihood::analyticDerivatives(const std::string& variable, double* d1, double* d2) const {
   if (!(derivFirst_ || derivSecond_)) return false;
   const Node* n = nodes_.at(TextTools::to<size_t>(variable.substr(5)));

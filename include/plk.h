@@ -161,7 +161,10 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
  *   returns -d1, RHomogeneousTreeLikelihood.cpp:346-360, 596-610).
  * Requires dP and d2P of the branch (plk_update_pmatrices with PLK_DERIV_DP | PLK_DERIV_D2P).
  * Replaces computeTreeDLikelihood / computeTreeD2Likelihood (:365-541, :615-791).
- * Supported for 4-state models with 1, 2 or 4 classes (PLK_ERR_UNSUPPORTED otherwise). */
+ * Any state and class count: 4 states with 1, 2 or 4 classes propagate L, dL, d2L up the
+ * path in registers; other shapes recompute the path with dP / d2P substituted on the
+ * branch (lnL is linear in one branch's P).  PLK_ERR_UNSUPPORTED with
+ * PLK_FLAG_SUBTREE_PATTERNS. */
 int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2);
 int plk_block_size(void);
 

@@ -561,6 +561,53 @@ def test_branch_derivatives_vs_oracle_finite_differences(C, mode):
         assert abs(d2 - fd2) <= 2e-4 * max(1.0, abs(fd2)), (b, d2, fd2)
 
 
+@pytest.mark.parametrize("S,C,mode,scaling", [(20, 4, "lnl_only", False), (20, 2, "levelwise", True),
+                                              (64, 1, "lnl_only", False), (4, 8, "materialize", False)])
+def test_branch_derivatives_any_state_count(S, C, mode, scaling):
+    """Row f1 beyond DNA: the levelwise path derivatives (dP / d2P substituted on the
+    branch, the path to the root recomputed) against central differences of the oracle."""
+    n_pat = 300 if S == 64 else 500
+    et, m, alph, rates, probs, states = _random_problem(S, C, 10, n_pat, seed=50 + S + C)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, S, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    pm = engine_pmats(eng, et)
+    for b in (0, et.n_tips, br[-1]):
+        d1, d2 = eng.branch_derivatives(int(b))
+
+        def lnl_at(t):
+            bl = et.brlen.copy()
+            bl[b] = t
+            e2 = phylo.EngineTree(et.n_tips, et.n_internal, et.root, et.tip_names, et.ops, bl, {}, [], [])
+            return oracle_for(e2, states, alph.init_table, rates, probs, m.pi, [m], scaling=scaling)[0]
+
+        t = et.brlen[b]
+        h = 1e-5
+        fd1 = (lnl_at(t + h) - lnl_at(t - h)) / (2 * h)
+        h2 = 1e-4
+        fd2 = (lnl_at(t + h2) - 2 * lnl_at(t) + lnl_at(t - h2)) / h2 ** 2
+        assert abs(d1 - fd1) <= 1e-6 * max(1.0, abs(fd1)), (b, d1, fd1)
+        assert abs(d2 - fd2) <= 2e-4 * max(1.0, abs(fd2)), (b, d2, fd2)
+    del pm
+
+
+def test_branch_derivatives_path_equals_kernel(monkeypatch):
+    """4 states: the levelwise path derivatives equal the register-resident deriv_kernel."""
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 24, 3000, seed=61)
+    eng = engine_for(et, 4, 4, 3000, states, alph.init_table, rates, probs, m.pi, [m])
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    for b in (0, 5, et.n_tips + 2, br[-1]):
+        k1, k2 = eng.branch_derivatives(int(b))
+        monkeypatch.setenv("PLK_DERIV_PATH", "1")
+        p1, p2 = eng.branch_derivatives(int(b))
+        monkeypatch.delenv("PLK_DERIV_PATH")
+        assert abs(k1 - p1) <= 1e-11 * max(1.0, abs(k1)) and abs(k2 - p2) <= 1e-10 * max(1.0, abs(k2)), (b, k1, p1, k2, p2)
+
+
 def test_branch_derivatives_require_dp():
     et, m, alph, rates, probs, states = _random_problem(4, 4, 6, 100, seed=3)
     eng = engine_for(et, 4, 4, 100, states, alph.init_table, rates, probs, m.pi, [m])
