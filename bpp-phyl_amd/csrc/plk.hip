@@ -1153,7 +1153,10 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.U = h->n_codes;
     sh.NT = jit_max_fragment_tips(h->prog_host, h->frag_starts_host);
     sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
-    sh.L = env_int("PLK_JIT_L", 3, 1, 8);  // two-stage pipeline: codes / HBM loads 3 ahead (cfg2 0.274 -> 0.259 ms)
+    // two-stage pipeline, codes / HBM loads 3 ahead (cfg2 0.274 -> 0.259 ms); with every
+    // class in the wave a ring slot is C x larger, so there one event ahead (cfg5 1.04 ms
+    // at L = 1, 1.48 ms at L = 3)
+    sh.L = env_int("PLK_JIT_L", h->prog_ciw ? 1 : 3, 1, 8);
     sh.minw = env_int("PLK_JIT_MINW", 0, 0, 8);
     sh.same_p = env_is("PLK_DEBUG_SAMEP", '1');
     // speculative no-rescale pass (plk_jit.hpp): a win only where rescaling never
