@@ -1150,6 +1150,11 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.G = (h->n_pad % 128 == 0)
                ? env_int("PLK_JIT_G", ((h->flags & PLK_FLAG_SCALING) && !h->prog_ciw) ? 1 : 2, 1, 2)
                : 1;
+    // two patterns per lane halve the P(t) reads per FMA but double the registers:
+    // measured slower (cfg2 0.255-0.301 vs 0.241 ms), so opt-in; not with speculation
+    sh.PW = env_int("PLK_JIT_PW", 1, 1, 2);
+    sh.pin = env_int("PLK_JIT_PIN", 1, 0, 1) != 0;  // cfg2 0.244 -> 0.241, cfg5 1.04 -> 0.93 ms
+    if (sh.G * sh.PW > 4 || h->n_pad % (64 * sh.G * sh.PW) != 0 || env_is("PLK_JIT_SPECULATE", '1')) sh.PW = 1;
     sh.U = h->n_codes;
     sh.NT = jit_max_fragment_tips(h->prog_host, h->frag_starts_host);
     sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
@@ -1164,7 +1169,9 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.exact_only = !env_is("PLK_JIT_SPECULATE", '1');
     if (sh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
-    if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW || sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
+    if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW || sh.PW != h->jit_shape.PW ||
+        sh.pin != h->jit_shape.pin ||
+        sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
         sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.exact_only != h->jit_shape.exact_only) {
       int rc = jit_function(h, jit_tree4_source(h->prog_host, h->frag_starts_host, sh), "plk_jit_tree4", &h->jit_fn);
@@ -1184,7 +1191,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.slot_stride = a.slot_stride;
     ja.n_pad = a.n_pad;
     ja.n_patterns = a.n_patterns;
-    ja.n_sblocks = (int32_t)(h->n_pad / (64 * sh.G));
+    ja.n_sblocks = (int32_t)(h->n_pad / (64 * sh.G * sh.PW));
     ja.guard = a.guard;
   }
   h->kernel_path = jit ? "jit_tree4" : kind == FK_TREEM ? "treeM" : kind == FK_TREES ? "treeS" : "tree4";

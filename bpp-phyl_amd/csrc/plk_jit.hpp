@@ -55,28 +55,54 @@ struct JArgs {
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
 };
 
-// dst[cw][x] (*)= sum_y P_cw[x][y] src[cw][y] for the CW classes of the wave (P_cw at
-// P + 16 cw, row-major); SET: dst was 1
-template <int CW, bool SET>
-__device__ __forceinline__ void contrib(double (&dst)[4 * CW], const double (&src)[4 * CW], CPd P) {
+// Register vectors hold 4 * CW * PW doubles: vector v = pw * CW + cw is class c0 + cw of
+// the lane's pattern pw (patterns p and p + 64 of a 128-pattern tile when PW = 2).
+
+// dst[v][x] (*)= sum_y P_cw[x][y] src[v][y] (P_cw at P + 16 cw, row-major; one P read
+// serves every pattern of the lane); SET: dst was 1
+template <int CW, int PW, bool SET>
+__device__ __forceinline__ void contrib(double (&dst)[4 * CW * PW], const double (&src)[4 * CW * PW], CPd P) {
 #pragma unroll
   for (int cw = 0; cw < CW; ++cw)
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      double s = P[16 * cw + 4 * x + 0] * src[4 * cw + 0];
-      s = __builtin_fma(P[16 * cw + 4 * x + 1], src[4 * cw + 1], s);
-      s = __builtin_fma(P[16 * cw + 4 * x + 2], src[4 * cw + 2], s);
-      s = __builtin_fma(P[16 * cw + 4 * x + 3], src[4 * cw + 3], s);
-      if (SET) dst[4 * cw + x] = s; else dst[4 * cw + x] *= s;
-    }
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int pw = 0; pw < PW; ++pw) {
+        const int v = 4 * (pw * CW + cw);
+        double s = P[16 * cw + 4 * x + 0] * src[v + 0];
+        s = __builtin_fma(P[16 * cw + 4 * x + 1], src[v + 1], s);
+        s = __builtin_fma(P[16 * cw + 4 * x + 2], src[v + 2], s);
+        s = __builtin_fma(P[16 * cw + 4 * x + 3], src[v + 3], s);
+        if (SET) dst[v + x] = s; else dst[v + x] *= s;
+      }
 }
 
-template <int CW, bool SET>
-__device__ __forceinline__ void tipmul(double (&dst)[4 * CW], const double (&row)[4 * CW]) {
+template <int N, bool SET>
+__device__ __forceinline__ void tipmul(double (&dst)[N], const double (&row)[N]) {
 #pragma unroll
-  for (int i = 0; i < 4 * CW; ++i) {
+  for (int i = 0; i < N; ++i) {
     if (SET) dst[i] = row[i]; else dst[i] *= row[i];
   }
+}
+
+// Keep a freshly computed accumulator where the program put it: sched_barrier only binds
+// the machine scheduler, and IR-level sinking would otherwise delay multiplies of one
+// pattern to their next use (their operands then stay live and spill).  No code.
+template <int N>
+__device__ __forceinline__ void pin(double (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
+template <int PW>
+__device__ __forceinline__ void kzero(int (&k)[PW]) {
+#pragma unroll
+  for (int i = 0; i < PW; ++i) k[i] = 0;
+}
+template <int PW>
+__device__ __forceinline__ void kadd(int (&k)[PW], const int (&d)[PW]) {
+#pragma unroll
+  for (int i = 0; i < PW; ++i) k[i] += d[i];
 }
 
 // opaque copies (no code): values the optimiser cannot prove equal to their source
@@ -102,86 +128,113 @@ __device__ __forceinline__ void flag_risky(int& dng, const double (&v)[N]) {
   asm volatile("" : "+v"(dng));
 }
 
-// Joint (all-class) exact power-of-two rescale.  NW = C / CW waves hold the classes
-// of one pattern group; with NW = 1 the joint max is all in registers.
-template <int C, int CW>
-__device__ __forceinline__ void rescale(double (&v)[4 * CW], int& cnt, double* xch, int w, int g) {
+// Joint (all-class) exact power-of-two rescale of each of the lane's patterns.  NW =
+// C / CW waves hold the classes of one pattern group (NWT waves in the workgroup);
+// with NW = 1 the joint max is all in registers.
+template <int C, int CW, int PW, int NWT>
+__device__ __forceinline__ void rescale(double (&v)[4 * CW * PW], int (&cnt)[PW], double* xch, int w, int g) {
   constexpr int NW = C / CW;
-  double m = 0.0;
+  double m[PW];
 #pragma unroll
-  for (int i = 0; i < 4 * CW; ++i) m = fmax(m, v[i]);
+  for (int pw = 0; pw < PW; ++pw) {
+    m[pw] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4 * CW; ++i) m[pw] = fmax(m[pw], v[4 * CW * pw + i]);
+  }
   if (NW > 1) {
     // one barrier: consecutive rescales alternate between two exchange buffers, so a
     // wave can only overwrite this buffer after every wave has passed the next
     // rescale's barrier, i.e. after every wave has read it here
     const int lane = threadIdx.x & 63;
-    xch[w * 64 + lane] = m;
-    __syncthreads();
-    m = 0.0;
-    for (int k = 0; k < NW; ++k) m = fmax(m, xch[(g * NW + k) * 64 + lane]);
-  }
-  if (m > 0.0 && m < kScaleThr) {
 #pragma unroll
-    for (int i = 0; i < 4 * CW; ++i) v[i] *= kScaleUp;
-    cnt += 1;
+    for (int pw = 0; pw < PW; ++pw) xch[(pw * NWT + w) * 64 + lane] = m[pw];
+    __syncthreads();
+#pragma unroll
+    for (int pw = 0; pw < PW; ++pw) {
+      m[pw] = 0.0;
+      for (int k = 0; k < NW; ++k) m[pw] = fmax(m[pw], xch[(pw * NWT + g * NW + k) * 64 + lane]);
+    }
   }
+#pragma unroll
+  for (int pw = 0; pw < PW; ++pw)
+    if (m[pw] > 0.0 && m[pw] < kScaleThr) {
+#pragma unroll
+      for (int i = 0; i < 4 * CW; ++i) v[4 * CW * pw + i] *= kScaleUp;
+      cnt[pw] += 1;
+    }
 }
 
-template <int CW, bool SCALE>
-__device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0, const double (&v)[4 * CW],
-                                      int cnt) {
+// off: the lane's first pattern in the slot (tile layout); pattern pw is 64 further
+template <int CW, int PW, bool SCALE>
+__device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0,
+                                      const double (&v)[4 * CW * PW], const int (&cnt)[PW]) {
   double* dst = a.partials + (i64)slot * a.slot_stride + off;
 #pragma unroll
-  for (int i = 0; i < 4 * CW; ++i) __builtin_nontemporal_store(v[i], dst + (i64)i * kTile);
-  if (SCALE && c0 == 0) a.scale[(i64)slot * a.n_pad + p] = cnt;
+  for (int pw = 0; pw < PW; ++pw)
+#pragma unroll
+    for (int i = 0; i < 4 * CW; ++i) __builtin_nontemporal_store(v[4 * CW * pw + i], dst + 64 * pw + (i64)i * kTile);
+  if (SCALE && c0 == 0)
+#pragma unroll
+    for (int pw = 0; pw < PW; ++pw) a.scale[(i64)slot * a.n_pad + p + 64 * pw] = cnt[pw];
 }
 
-template <int C, int CW, bool SCALE>
-__device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[4 * CW], int cnt, double* xch, int w,
-                                            int g, int c0, i64 p0, i64 p) {
+// log() out of line: inlined into the persistent loop, its polynomial constants are
+// hoisted out of the loop into registers (and spilled with two patterns per lane)
+__device__ __attribute__((noinline)) double jit_log(double x) { return log(x); }
+
+template <int C, int CW, int PW, int NWT, bool SCALE>
+__device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[4 * CW * PW], const int (&cnt)[PW],
+                                            double* xch, int w, int g, int c0, i64 p0, i64 p) {
   constexpr int NW = C / CW;
   const int lane = threadIdx.x & 63;
-  double t[CW];
+  double t[PW][CW];
 #pragma unroll
-  for (int cw = 0; cw < CW; ++cw) {
-    double lc = 0.0;
+  for (int pw = 0; pw < PW; ++pw)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const double li = acc[4 * cw + s] * a.pi[s];
-      if (a.guard) {
-        if (li > 0.0) lc += li;
-      } else {
-        lc += li;
+    for (int cw = 0; cw < CW; ++cw) {
+      double lc = 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double li = acc[4 * (pw * CW + cw) + s] * a.pi[s];
+        if (a.guard) {
+          if (li > 0.0) lc += li;
+        } else {
+          lc += li;
+        }
       }
+      t[pw][cw] = lc * a.probs[c0 + cw];
     }
-    t[cw] = lc * a.probs[c0 + cw];
-  }
   if (NW > 1) {
     __syncthreads();
-    xch[w * 64 + lane] = t[0];
+#pragma unroll
+    for (int pw = 0; pw < PW; ++pw) xch[(pw * NWT + w) * 64 + lane] = t[pw][0];
     __syncthreads();
   }
   if (c0 == 0) {
-    double l = 0.0;
-    for (int c = 0; c < C; ++c) {
-      const double li = NW > 1 ? xch[(g * NW + c) * 64 + lane] : t[c < CW ? c : 0];
-      if (a.guard) {
-        if (li > 0.0) l += li;
-      } else {
-        l += li;
-      }
-    }
-    if (!a.guard && l < 0.0) l = 0.0;
-    double r = log(l);
-    if (SCALE) r -= (double)cnt * kLn2x256;
-    double wr = 0.0;
-    if (p < a.n_patterns) {
-      a.site_lnl[p] = r;
-      wr = a.weights[p] * r;
-    }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
-    if (lane == 0) a.wave_sums[p0 >> 6] = wr;
+    for (int pw = 0; pw < PW; ++pw) {
+      double l = 0.0;
+      for (int c = 0; c < C; ++c) {
+        const double li = NW > 1 ? xch[(pw * NWT + g * NW + c) * 64 + lane] : t[pw][c < CW ? c : 0];
+        if (a.guard) {
+          if (li > 0.0) l += li;
+        } else {
+          l += li;
+        }
+      }
+      if (!a.guard && l < 0.0) l = 0.0;
+      double r = jit_log(l);
+      if (SCALE) r -= (double)cnt[pw] * kLn2x256;
+      double wr = 0.0;
+      const i64 pp = p + 64 * pw;
+      if (pp < a.n_patterns) {
+        a.site_lnl[pp] = r;
+        wr = a.weights[pp] * r;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+      if (lane == 0) a.wave_sums[(p0 + 64 * pw) >> 6] = wr;
+    }
   }
 }
 )PLKJIT";
@@ -207,6 +260,8 @@ struct JArgs {
 struct JitShape {
   int C = 1;        // rate classes
   int CW = 1;       // classes per wave (1, or C: a wave holds every class of its patterns)
+  int PW = 1;       // patterns per lane (1 or 2: p and p + 64 share every P(t) read)
+  bool pin = false; // pin accumulators after every event (see pin())
   int G = 1;        // 64-pattern groups per workgroup
   int U = 1;        // codes in use (rows of a tip table)
   int NT = 0;       // most tips of any fragment (LDS table slots)
@@ -217,7 +272,8 @@ struct JitShape {
   bool exact_only = true;   // scaling: no speculative no-rescale pass (PLK_JIT_SPECULATE=1 enables it)
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
-    return nt * C * U * 4 * sizeof(double) + 2 * (size_t)G * (C / CW) * 64 * sizeof(double) + (size_t)G * nt * 64;
+    return nt * C * U * 4 * sizeof(double) + 2 * (size_t)PW * G * (C / CW) * 64 * sizeof(double) +
+           (size_t)G * nt * 64 * PW;
   }
 };
 
@@ -299,19 +355,20 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
       s += buf;
     }
   s += "};\n";
-  const int CW = sh.CW, NW = C / CW;
+  const int CW = sh.CW, NW = C / CW, PW = sh.PW;
   snprintf(buf, sizeof(buf),
-           "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define G_ %d\n#define U_ %d\n#define NT_ %d\n"
-           "#define SC_ %s\n"
+           "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
+           "#define U_ %d\n#define NT_ %d\n#define SC_ %s\n#define V_ (4 * CW_ * PW_)\n"
            "extern \"C\" __global__ __launch_bounds__(%d%s) void plk_jit_tree4(JArgs a, const double* __restrict__ "
            "pmats, int frag_base) {\n",
-           C, CW, NW, sh.G, sh.U, std::max(sh.NT, 1), sh.scale ? "true" : "false", 64 * NW * sh.G, minw_s.c_str());
+           C, CW, NW, PW, sh.G, NW * sh.G, sh.U, std::max(sh.NT, 1), sh.scale ? "true" : "false", 64 * NW * sh.G,
+           minw_s.c_str());
   s += buf;
   s += R"PLKJIT(  extern __shared__ __attribute__((aligned(16))) double lds[];
   double* tab = lds;                                          // [NT_][C_][U_][4]
-  double* xch = tab + NT_ * C_ * U_ * 4;                      // [2][G_ * NW_][64] (rescale alternates)
-  double* xch2 = xch + G_ * NW_ * 64;
-  u8* code_lds = reinterpret_cast<u8*>(xch2 + G_ * NW_ * 64); // [G_][NT_][64]
+  double* xch = tab + NT_ * C_ * U_ * 4;                      // [2][PW_][NWT_][64] (rescale alternates)
+  double* xch2 = xch + PW_ * NWT_ * 64;
+  u8* code_lds = reinterpret_cast<u8*>(xch2 + PW_ * NWT_ * 64); // [G_][NT_][64 * PW_]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c0 = (w % NW_) * CW_, g = w / NW_;
@@ -323,33 +380,33 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
   }
   const CPd pm = (CPd)(pmats + c0 * 16);
   const double* trow = tab + c0 * (U_ * 4);
-  const u8* crow = code_lds + g * (NT_ * 64) + lane;
+  const u8* crow = code_lds + g * (NT_ * 64 * PW_) + lane;
   (void)xch; (void)xch2; (void)trow; (void)crow;
-#define CODEF(Q, k) Q = crow[(k) * 64];
-#define ROWF(F, k, Q) { const double* r0_ = trow + ((k) * (C_ * U_) + (Q)) * 4; \
+// tip k: codes of the lane's patterns (4 per int), then their table rows
+#define CODEF(Q, k) { Q = 0; _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) \
+    Q |= (int)crow[(k) * (64 * PW_) + 64 * pw_] << (8 * pw_); }
+#define ROWF(F, k, Q) { _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
+    const double* r0_ = trow + ((k) * (C_ * U_) + (((Q) >> (8 * pw_)) & 255)) * 4; \
     _Pragma("unroll") for (int cw_ = 0; cw_ < CW_; ++cw_) { \
       const double2* r_ = reinterpret_cast<const double2*>(r0_ + cw_ * (U_ * 4)); \
-      const double2 x_ = r_[0], y_ = r_[1]; \
-      F[4 * cw_] = x_.x; F[4 * cw_ + 1] = x_.y; F[4 * cw_ + 2] = y_.x; F[4 * cw_ + 3] = y_.y; } }
-#define TIPF(F, k) { const double* r0_ = trow + ((k) * (C_ * U_) + crow[(k) * 64]) * 4; \
-    _Pragma("unroll") for (int cw_ = 0; cw_ < CW_; ++cw_) { \
-      const double2* r_ = reinterpret_cast<const double2*>(r0_ + cw_ * (U_ * 4)); \
-      const double2 x_ = r_[0], y_ = r_[1]; \
-      F[4 * cw_] = x_.x; F[4 * cw_ + 1] = x_.y; F[4 * cw_ + 2] = y_.x; F[4 * cw_ + 3] = y_.y; } }
+      const double2 x_ = r_[0], y_ = r_[1]; const int v_ = 4 * (pw_ * CW_ + cw_); \
+      F[v_] = x_.x; F[v_ + 1] = x_.y; F[v_ + 2] = y_.x; F[v_ + 3] = y_.y; } } }
+#define TIPF(F, k) { int q_; CODEF(q_, k) ROWF(F, k, q_) }
 #define LOADF(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
-    _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[i_] = L_[(i64)i_ * kTile]; \
-    if (SC_) FK = a.scale[(i64)(slot) * a.n_pad + p]; }
+    _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
+      _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[4 * CW_ * pw_ + i_] = L_[64 * pw_ + (i64)i_ * kTile]; \
+      if (SC_) FK[pw_] = a.scale[(i64)(slot) * a.n_pad + p + 64 * pw_]; } }
 #define SB __builtin_amdgcn_sched_barrier(0);
   for (int sb = blockIdx.x; sb < a.n_sblocks; sb += gridDim.x) {
-    const i64 q0 = (i64)sb * (64 * G_);
-    const i64 p0 = q0 + g * 64, p = p0 + lane;
+    const i64 q0 = (i64)sb * (64 * PW_ * G_);
+    const i64 p0 = q0 + g * (64 * PW_), p = p0 + lane;
     const i64 toff = (p >> 7) * (C_ * 4 * kTile) + (i64)c0 * 4 * kTile + (p & (kTile - 1));
     (void)toff;
     __syncthreads();  // the previous super-block is done with code_lds / xch (and tab is staged)
-    for (int i = threadIdx.x; i < G_ * nt * 4; i += blockDim.x) {
-      const int gg = i / (nt * 4), r = i - gg * (nt * 4), k = r >> 2, j = r & 3;
-      reinterpret_cast<uint4*>(code_lds)[(gg * NT_ + k) * 4 + j] =
-          *reinterpret_cast<const uint4*>(a.codes + (i64)kFragTips[t0 + k] * a.n_pad + q0 + gg * 64 + 16 * j);
+    for (int i = threadIdx.x; i < G_ * nt * 4 * PW_; i += blockDim.x) {
+      const int gg = i / (nt * 4 * PW_), r = i - gg * (nt * 4 * PW_), k = r / (4 * PW_), j = r - k * (4 * PW_);
+      reinterpret_cast<uint4*>(code_lds)[(gg * NT_ + k) * 4 * PW_ + j] =
+          *reinterpret_cast<const uint4*>(a.codes + (i64)kFragTips[t0 + k] * a.n_pad + q0 + gg * (64 * PW_) + 16 * j);
     }
     __syncthreads();
 )PLKJIT";
@@ -357,12 +414,12 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
   for (const auto& ev : events)
     for (const JitEvent& e : ev) max_level = std::max(max_level, e.level);
   for (int d = 0; d <= max_level; ++d) {
-    snprintf(buf, sizeof(buf), "    double A%d[4 * CW_]; int K%d = 0; (void)K%d;\n", d, d, d);
+    snprintf(buf, sizeof(buf), "    double A%d[V_]; int K%d[PW_] = {}; (void)K%d;\n", d, d, d);
     s += buf;
   }
   for (int r = 0; r <= L; ++r) {
-    snprintf(buf, sizeof(buf), "    double F%d[4 * CW_]; int FK%d = 0; (void)FK%d; int Q%d = 0; (void)Q%d;\n", r, r, r,
-             r, r);
+    snprintf(buf, sizeof(buf), "    double F%d[V_]; int FK%d[PW_] = {}; (void)FK%d; int Q%d = 0; (void)Q%d;\n", r, r,
+             r, r, r);
     s += buf;
   }
   s += "    switch (frag) {\n";
@@ -409,7 +466,7 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
     // max can then be below it too; otherwise the joint max is >= the threshold at
     // every check, no rescale would happen, and this pass IS the exact result.
     auto emit_body = [&](bool exact) {
-      s += "      K0 = 0;\n";
+      s += "      kzero(K0);\n";
       std::vector<char> fresh((size_t)max_level + 1, 0);
       fresh[0] = 1;
       size_t nf = 0;
@@ -424,7 +481,7 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
       int n_rescale = 0;  // rescales alternate exchange buffers (the superblock barrier resets)
       auto check_line = [&](int d) {
         if (exact)
-          snprintf(buf, sizeof(buf), "      rescale<C_, CW_>(A%d, K%d, %s, w, g);\n", d, d,
+          snprintf(buf, sizeof(buf), "      rescale<C_, CW_, PW_, NWT_>(A%d, K%d, %s, w, g);\n", d, d,
                    (n_rescale++ & 1) ? "xch2" : "xch");
         else
           snprintf(buf, sizeof(buf), "      flag_risky(dng, A%d);\n", d);
@@ -441,48 +498,57 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
           }
           const char* set = fresh[(size_t)e.level] ? "true" : "false";
           if (e.op == T_TIP) {
-            snprintf(buf, sizeof(buf), "      tipmul<CW_, %s>(A%d, F%d);\n", set, e.level, slot[i]);
+            snprintf(buf, sizeof(buf), "      tipmul<V_, %s>(A%d, F%d);\n", set, e.level, slot[i]);
           } else {
             const std::string pr = pref(i);
-            snprintf(buf, sizeof(buf), "      contrib<CW_, %s>(A%d, F%d, %s);\n", set, e.level, slot[i], pr.c_str());
+            snprintf(buf, sizeof(buf), "      contrib<CW_, PW_, %s>(A%d, F%d, %s);\n", set, e.level, slot[i],
+                     pr.c_str());
           }
           s += buf;
+          if (sh.pin) {
+            snprintf(buf, sizeof(buf), "      pin(A%d);\n", e.level);
+            s += buf;
+          }
           fresh[(size_t)e.level] = 0;
           if (e.op == T_LOAD && sh.scale) {
-            snprintf(buf, sizeof(buf), "      K%d += FK%d;\n", e.level, slot[i]);
+            snprintf(buf, sizeof(buf), "      kadd(K%d, FK%d);\n", e.level, slot[i]);
             s += buf;
           }
           s += "      SB\n";
         } else if (e.op == T_DESCEND) {
           fresh[(size_t)e.level] = 1;
-          snprintf(buf, sizeof(buf), "      K%d = 0;\n", e.level);
+          snprintf(buf, sizeof(buf), "      kzero(K%d);\n", e.level);
           s += buf;
         } else if (e.op == T_ASCEND) {
           const int dd = e.level;
           if (e.b >= 0) {
             if (sh.scale) check_line(dd);
             if (e.a >= 0) {
-              snprintf(buf, sizeof(buf), "      store<CW_, SC_>(a, %d, toff, p, c0, A%d, K%d);\n", e.a, dd, dd);
+              snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %d, toff, p, c0, A%d, K%d);\n", e.a, dd, dd);
               s += buf;
             }
           }
           const std::string pr = pref(i);
-          snprintf(buf, sizeof(buf), "      contrib<CW_, %s>(A%d, A%d, %s);\n", fresh[(size_t)dd - 1] ? "true" : "false",
+          snprintf(buf, sizeof(buf), "      contrib<CW_, PW_, %s>(A%d, A%d, %s);\n", fresh[(size_t)dd - 1] ? "true" : "false",
                    dd - 1, dd, pr.c_str());
           s += buf;
+          if (sh.pin) {
+            snprintf(buf, sizeof(buf), "      pin(A%d);\n", dd - 1);
+            s += buf;
+          }
           fresh[(size_t)dd - 1] = 0;
           if (sh.scale) {
-            snprintf(buf, sizeof(buf), "      K%d += K%d;\n", dd - 1, dd);
+            snprintf(buf, sizeof(buf), "      kadd(K%d, K%d);\n", dd - 1, dd);
             s += buf;
           }
           s += "      SB\n";
         } else {  // T_ROOT
           if (sh.scale) check_line(0);
           if (e.a >= 0) {
-            snprintf(buf, sizeof(buf), "      store<CW_, SC_>(a, %d, toff, p, c0, A0, K0);\n", e.a);
+            snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %d, toff, p, c0, A0, K0);\n", e.a);
             s += buf;
           }
-          if (e.b) s += "      reduce_root<C_, CW_, SC_>(a, A0, K0, xch, w, g, c0, p0, p);\n";
+          if (e.b) s += "      reduce_root<C_, CW_, PW_, NWT_, SC_>(a, A0, K0, xch, w, g, c0, p0, p);\n";
         }
       }
     };
