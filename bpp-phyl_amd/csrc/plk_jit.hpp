@@ -272,7 +272,8 @@ struct JitShape {
   bool exact_only = true;   // scaling: no speculative no-rescale pass (PLK_JIT_SPECULATE=1 enables it)
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
-    return nt * C * U * 4 * sizeof(double) + 2 * (size_t)PW * G * (C / CW) * 64 * sizeof(double) +
+    // the second exchange buffer only serves the per-node rescale
+    return nt * C * U * 4 * sizeof(double) + (scale ? 2 : 1) * (size_t)PW * G * (C / CW) * 64 * sizeof(double) +
            (size_t)G * nt * 64 * PW;
   }
 };
@@ -368,7 +369,7 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
   double* tab = lds;                                          // [NT_][C_][U_][4]
   double* xch = tab + NT_ * C_ * U_ * 4;                      // [2][PW_][NWT_][64] (rescale alternates)
   double* xch2 = xch + PW_ * NWT_ * 64;
-  u8* code_lds = reinterpret_cast<u8*>(xch2 + PW_ * NWT_ * 64); // [G_][NT_][64 * PW_]
+  u8* code_lds = reinterpret_cast<u8*>(xch + (SC_ ? 2 : 1) * PW_ * NWT_ * 64); // [G_][NT_][64 * PW_]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c0 = (w % NW_) * CW_, g = w / NW_;
