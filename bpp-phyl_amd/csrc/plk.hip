@@ -472,7 +472,11 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   if ((rc = dalloc(h, (void**)&h->probs, 16 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->pi, 64 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->site_lnl, (size_t)h->n_pad * sizeof(double)))) return bail(rc);
-  if ((rc = dalloc(h, (void**)&h->block_sums, (size_t)h->n_blocks * sizeof(double)))) return bail(rc);
+  // block sums go straight to pinned host memory (the kernel writes them through the
+  // mapped device address), so the evaluation needs no separate device-to-host copy
+  if (hipHostMalloc((void**)&h->h_blocks, (size_t)h->n_blocks * sizeof(double), hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&h->block_sums, h->h_blocks, 0) != hipSuccess)
+    return bail(fail(h, PLK_ERR_OOM, "pinned block-sum buffer"));
   if ((rc = dalloc(h, (void**)&h->wave_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return bail(rc);
   h->materialized.assign(n_internal, 0);
   // default weights 1 for real patterns, 0 for padding
@@ -494,7 +498,7 @@ int plk_destroy(plk_handle h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
-                  h->block_sums, h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
+                  h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -637,28 +641,40 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     int rc = dalloc(h, (void**)&h->d2pmats, (size_t)h->n_nodes * h->C * S2 * sizeof(double));
     if (rc) return rc;
   }
-  // request buffer: branch[n] | model[n] | t[n]
-  const size_t bytes = (size_t)n * (2 * sizeof(int32_t) + sizeof(double)) + 64;
-  int rc = ensure_cap(h, &h->d_req, &h->d_req_cap, bytes);
-  if (rc) return rc;
-  // pinned staging, stream-ordered copy: the host does not wait for the GPU here (only
-  // for the previous request's copy, before it reuses the staging buffer)
-  if (!h->req_done) HIPCHK(h, hipEventCreateWithFlags(&h->req_done, hipEventDisableTiming));
-  HIPCHK(h, hipEventSynchronize(h->req_done));
-  if (h->h_req_cap < bytes) {
-    if (h->h_req) HIPCHK(h, hipHostFree(h->h_req));
-    h->h_req = nullptr;
-    h->h_req_cap = 0;
-    HIPCHK(h, hipHostMalloc((void**)&h->h_req, bytes, hipHostMallocDefault));
-    h->h_req_cap = bytes;
-  }
-  char* staging = h->h_req;
+  // small requests ride in the kernel arguments; larger ones go through pinned staging
+  // and a stream-ordered copy (the host only waits for the previous request's copy)
+  static_assert(sizeof(PmatInline) + sizeof(PmatArgs) <= 4096, "kernel argument block");
+  PmatInline inl;
+  inl.n = 0;
   const size_t off_t = 0, off_b = (size_t)n * sizeof(double), off_m = off_b + (size_t)n * sizeof(int32_t);
-  std::memcpy(staging + off_t, t, n * sizeof(double));
-  std::memcpy(staging + off_b, branch, n * sizeof(int32_t));
-  if (model) std::memcpy(staging + off_m, model, n * sizeof(int32_t));
-  HIPCHK(h, hipMemcpyAsync(h->d_req, staging, bytes, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipEventRecord(h->req_done, h->stream));
+  const char* staged_env = std::getenv("PLK_PMAT_STAGED");
+  if (n <= kPmatInline && !(staged_env && staged_env[0] == '1')) {
+    inl.n = n;
+    for (int i = 0; i < n; ++i) {
+      inl.t[i] = t[i];
+      inl.branch[i] = branch[i];
+      inl.model[i] = model ? model[i] : 0;
+    }
+  } else {
+    const size_t bytes = (size_t)n * (2 * sizeof(int32_t) + sizeof(double)) + 64;
+    int rc = ensure_cap(h, &h->d_req, &h->d_req_cap, bytes);
+    if (rc) return rc;
+    if (!h->req_done) HIPCHK(h, hipEventCreateWithFlags(&h->req_done, hipEventDisableTiming));
+    HIPCHK(h, hipEventSynchronize(h->req_done));
+    if (h->h_req_cap < bytes) {
+      if (h->h_req) HIPCHK(h, hipHostFree(h->h_req));
+      h->h_req = nullptr;
+      h->h_req_cap = 0;
+      HIPCHK(h, hipHostMalloc((void**)&h->h_req, bytes, hipHostMallocDefault));
+      h->h_req_cap = bytes;
+    }
+    char* staging = h->h_req;
+    std::memcpy(staging + off_t, t, n * sizeof(double));
+    std::memcpy(staging + off_b, branch, n * sizeof(int32_t));
+    if (model) std::memcpy(staging + off_m, model, n * sizeof(int32_t));
+    HIPCHK(h, hipMemcpyAsync(h->d_req, staging, bytes, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipEventRecord(h->req_done, h->stream));
+  }
   PmatArgs a;
   a.t = reinterpret_cast<const double*>((char*)h->d_req + off_t);
   a.branch = reinterpret_cast<const int32_t*>((char*)h->d_req + off_b);
@@ -686,7 +702,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     hipEventRecord(ev.a, h->stream);
   }
   const size_t lds = (size_t)(h->S + (tips_fused ? 2 : 1) * S2) * sizeof(double);
-  pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a);
+  pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a, inl);
   HIPCHK(h, hipGetLastError());
   if (h->timing & PLK_TIME_PMAT) {
     hipEventRecord(ev.b, h->stream);
@@ -1901,10 +1917,6 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
     int rc = launch_root(h, root);
     if (rc) return rc;
   }
-  if (!h->h_blocks) HIPCHK(h, hipHostMalloc((void**)&h->h_blocks, (size_t)h->n_blocks * sizeof(double),
-                                            hipHostMallocDefault));
-  HIPCHK(h, hipMemcpyAsync(h->h_blocks, h->block_sums, (size_t)h->n_blocks * sizeof(double), hipMemcpyDeviceToHost,
-                           h->stream));
   if (site_lnl)
     HIPCHK(h, hipMemcpyAsync(site_lnl, h->site_lnl, (size_t)h->n_patterns * sizeof(double), hipMemcpyDeviceToHost,
                              h->stream));

@@ -466,13 +466,23 @@ struct PmatArgs {
   unsigned mask;
 };
 
-__global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a) {
+// Requests of up to kPmatInline branches travel in the kernel arguments (no staging
+// copy, no dependent launch in front of the kernel).
+constexpr int kPmatInline = 160;
+struct PmatInline {
+  double t[kPmatInline];
+  int32_t branch[kPmatInline];
+  int32_t model[kPmatInline];
+  int32_t n;  // 0: use PmatArgs' device arrays
+};
+
+__global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a, const PmatInline inl) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int i = blockIdx.x, c = blockIdx.y, S = a.S;
-  const int b = a.branch[i];
-  const int m = a.model ? a.model[i] : 0;
+  const int b = inl.n ? inl.branch[i] : a.branch[i];
+  const int m = inl.n ? inl.model[i] : (a.model ? a.model[i] : 0);
   const double rc = a.rates[c];
-  const double tt = a.t[i] * rc;
+  const double tt = (inl.n ? inl.t[i] : a.t[i]) * rc;
   double* e = sm;           // exp(lambda t)
   double* Vm = sm + S;      // V
   const double* V = a.V + (size_t)m * S * S;
