@@ -129,6 +129,7 @@ class Engine:
         self.S, self.C, self.P = n_states, n_classes, n_patterns
         self.n_tips, self.n_internal = n_tips, n_internal
         self._ops_cache = None
+        self._eval_cache = None
         rc = self.lib.plk_create(device, n_states, n_classes, n_patterns, n_tips, n_internal, n_models, flags,
                                  ct.byref(self.h))
         if rc != PLK_OK:
@@ -212,20 +213,22 @@ class Engine:
 
     def evaluate(self, branches: np.ndarray, t: np.ndarray, ops, root: int, models: Optional[np.ndarray] = None):
         """plk_evaluate: P(t) of `branches`, the traversal `ops`, the root reduction in one
-        call.  Returns (lnL, block_sums)."""
-        b = np.ascontiguousarray(branches, dtype=np.int32)
-        tt = np.ascontiguousarray(t, dtype=np.float64)
-        mp = None
-        if models is not None:
-            m = np.ascontiguousarray(models, dtype=np.int32)
-            mp = m.ctypes.data_as(ct.POINTER(ct.c_int32))
+        call.  Returns (lnL, block_sums).  The branch / model index arrays are converted
+        once per array object (an optimiser loop passes the same ones every time)."""
+        key = (id(branches), id(models))
+        if self._eval_cache is None or self._eval_cache[0] != key or self._eval_cache[1] is not branches:
+            b = np.ascontiguousarray(branches, dtype=np.int32)
+            m = None if models is None else np.ascontiguousarray(models, dtype=np.int32)
+            nb = (self.P + self.lib.plk_block_size() - 1) // self.lib.plk_block_size()
+            self._eval_cache = (key, branches, b, m, b.ctypes.data_as(ct.POINTER(ct.c_int32)),
+                                None if m is None else m.ctypes.data_as(ct.POINTER(ct.c_int32)), np.empty(nb))
+        _, _, b, _, bp, mp, blocks_buf = self._eval_cache
+        tt = t if (t.dtype == np.float64 and t.flags.c_contiguous) else np.ascontiguousarray(t, dtype=np.float64)
         arr = self._op_array(ops)
-        nb = (self.P + self.lib.plk_block_size() - 1) // self.lib.plk_block_size()
-        blocks = np.empty(nb)
         lnl = ct.c_double(0.0)
-        self._chk(self.lib.plk_evaluate(self.h, len(b), b.ctypes.data_as(ct.POINTER(ct.c_int32)), mp, _d(tt), arr,
-                                        len(arr), root, ct.byref(lnl), _d(blocks)))
-        return lnl.value, blocks
+        self._chk(self.lib.plk_evaluate(self.h, len(b), bp, mp, _d(tt), arr, len(arr), root, ct.byref(lnl),
+                                        _d(blocks_buf)))
+        return lnl.value, blocks_buf.copy()
 
     def get_partials(self, node: int) -> np.ndarray:
         out = np.empty((self.P, self.C, self.S))
