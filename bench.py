@@ -58,7 +58,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(wl, n_sample: int, reps: int):
+def cpu_baseline(wl, n_sample: int, reps: int, eng_sites=None):
     """The oracle (faithful C++11 -O2 -g restatement of computeSubtreeLikelihood with the
     reference's nested-vector layout, usePatterns=true -- the reference default) timed on
     one host core over a bounded sample of the same workload."""
@@ -79,11 +79,21 @@ def cpu_baseline(wl, n_sample: int, reps: int):
             for c in range(C):
                 pm[n, c] = m.pij(et.brlen[n] * wl.rates[c])
     ss, sons, lr = et.son_arrays()
-    res = {}
+    res, sites = {}, None
     for up in (True, False):
-        _, _, t_trav, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, wl.alphabet.init_table, pm, wl.probs,
-                                             wl.root_freqs, use_patterns=up, scaling=wl.scaling, n_rep=reps)
+        _, site, t_trav, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, wl.alphabet.init_table, pm, wl.probs,
+                                                wl.root_freqs, use_patterns=up, scaling=wl.scaling, n_rep=reps,
+                                                want_sites=up)
         res[up] = n_sample * et.n_internal / t_trav
+        if up:
+            sites = site
+    parity = None
+    if eng_sites is not None:
+        # SURVEY 8(d)'s third figure, on the sample: the GPU's per-pattern lnL vs the oracle's
+        e = np.asarray(eng_sites[:n_sample], dtype=np.float64)
+        lo, le = float(np.add.accumulate(sites)[-1]), float(np.add.accumulate(e)[-1])
+        parity = {"patterns": n_sample, "rel_err_lnl": abs(le - lo) / abs(lo),
+                  "max_rel_err_site": float(np.max(np.abs(e - sites) / np.abs(sites)))}
     return {
         "value": res[True],
         "unit": "site-pattern x node partial updates/s",
@@ -94,6 +104,7 @@ def cpu_baseline(wl, n_sample: int, reps: int):
                    f"(reference default), median-free mean of {reps} traversals on 1 pinned core of "
                    f"{platform.processor() or platform.machine()}"),
         "value_use_patterns_false": res[False],
+        "parity_vs_oracle": parity,
     }
 
 
@@ -266,7 +277,8 @@ def main():
             rec["computed_updates_per_s"] = computed * world * args.steps / elapsed
         if world == 1 and not args.no_cpu_baseline:
             ns = args.cpu_sample or workload.CONFIGS[args.config]["cpu_sample"]
-            rec["cpu_baseline"] = cpu_baseline(wl, min(ns, P), args.cpu_reps)
+            _, eng_sites, _ = ev.eng.root_loglik(wl.et.root, want_sites=True)
+            rec["cpu_baseline"] = cpu_baseline(wl, min(ns, P), args.cpu_reps, eng_sites)
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.destroy_process_group()
