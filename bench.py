@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="A/B: time the steps without per-kernel HIP events")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N>1 path on ONE GPU (every rank on cuda:0, collectives on the host); "
+                         "never a measurement")
     ap.add_argument("--mode", default="lnl", choices=["lnl", "materialize", "levelwise", "subtree"],
                     help="lnl: fused traversal, interior partials kept in registers (recomputed on demand); "
                          "materialize: fused traversal writing every partial; levelwise: one launch per level; "
@@ -170,13 +173,19 @@ def main():
     import torch
 
     dist = None
+    rehearse = world > 1 and args.dist_backend == "gloo"
     if world > 1:
         import torch.distributed as dist  # noqa: F811
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    device = local if world > 1 else 0
+    device = local if world > 1 and not rehearse else 0
+    coll_dev = "cpu" if rehearse else "cuda"
 
     wl = workload.make_workload(args.config)
     P = args.patterns or wl.n_patterns
@@ -192,7 +201,7 @@ def main():
     def one_step():
         _, _, blocks = ev.step()
         # the one cross-GPU exchange: RCCL all-gather of fixed-order block sums
-        return shard.allgather_lnl(blocks, dist, device="cuda" if dist is not None else None)
+        return shard.allgather_lnl(blocks, dist, device=coll_dev if dist is not None else None)
 
     for _ in range(args.warmup):
         lnl = one_step()
@@ -212,7 +221,7 @@ def main():
     tm = ev.eng.get_timing()
     ev.eng.set_timing(False)
     if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        e = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
