@@ -1,0 +1,62 @@
+// fp64 VALU / MFMA peak microbenchmark (gfx950): achievable fp64 FMA rate, to put the
+// fused kernels' fraction of the 78.6 TF/s spec into context.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+__global__ __launch_bounds__(256) void fma_kernel(double* out, int iters, double a, double b) {
+  double x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      x0 = __builtin_fma(x0, a, b); x1 = __builtin_fma(x1, a, b); x2 = __builtin_fma(x2, a, b);
+      x3 = __builtin_fma(x3, a, b); x4 = __builtin_fma(x4, a, b); x5 = __builtin_fma(x5, a, b);
+      x6 = __builtin_fma(x6, a, b); x7 = __builtin_fma(x7, a, b);
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x0 + x1 + x2 + x3 + x4 + x5 + x6 + x7;
+}
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void mfma_kernel(double* out, int iters, double a, double b) {
+  f64x4 d0 = {0, 0, 0, 0}, d1 = d0, d2 = d0, d3 = d0;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d1, 0, 0, 0);
+      d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d2, 0, 0, 0);
+      d3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, d3, 0, 0, 0);
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = d0[0] + d1[1] + d2[2] + d3[3];
+}
+
+int main() {
+  const int blocks = 256 * 8, threads = 256, iters = 4096;
+  double* out;
+  hipMalloc(&out, (size_t)blocks * threads * sizeof(double));
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (int rep = 0; rep < 3; ++rep) {
+    hipEventRecord(e0);
+    fma_kernel<<<blocks, threads>>>(out, iters, 0.999999, 1e-7);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double flops = 2.0 * 8 * 8 * (double)iters * blocks * threads;
+    printf("VALU v_fma_f64: %.1f TF/s (%.3f ms)\n", flops / ms / 1e9, ms);
+  }
+  for (int rep = 0; rep < 3; ++rep) {
+    hipEventRecord(e0);
+    mfma_kernel<<<blocks, threads>>>(out, iters / 4, 0.999999, 1e-7);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double flops = 2.0 * 16 * 16 * 4 * 8 * 4 * (double)(iters / 4) * blocks * (threads / 64);
+    printf("MFMA v_mfma_f64_16x16x4: %.1f TF/s (%.3f ms)\n", flops / ms / 1e9, ms);
+  }
+  return 0;
+}
