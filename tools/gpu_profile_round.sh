@@ -11,5 +11,6 @@ bash tools/gpu_prof.sh ${P}_cfg2_mat gtr_g4_dna_1M_64 materialize 10 || exit 1
 bash tools/gpu_prof.sh ${P}_cfg3_lnl lg08_g4_protein_200k_256 lnl 5 || exit 1
 bash tools/gpu_prof.sh ${P}_cfg4_lnl yn98_codon_50k_128 lnl 10 || exit 1
 bash tools/gpu_prof.sh ${P}_cfg5_lnl nh_gtr_g4_dna_2M_512 lnl 10 || exit 1
+bash tools/gpu_prof.sh ${P}_cfg2_sub gtr_g4_dna_1M_64 subtree 10 || exit 1
 timeout -k 10 300 python bench.py > gpurun_out/${P}_bench_default.json 2> gpurun_out/${P}_bench_default.err || { tail -5 gpurun_out/${P}_bench_default.err; exit 1; }
 cat gpurun_out/${P}_bench_default.json
