@@ -199,9 +199,11 @@ def main():
     units_step = P * wl.et.n_internal
 
     def one_step():
-        _, _, blocks = ev.step()
+        lnl, _, blocks = ev.step()
+        if dist is None:
+            return lnl  # plk_evaluate already summed the block sums in the fixed global order
         # the one cross-GPU exchange: RCCL all-gather of fixed-order block sums
-        return shard.allgather_lnl(blocks, dist, device=coll_dev if dist is not None else None)
+        return shard.allgather_lnl(blocks, dist, device=coll_dev)
 
     for _ in range(args.warmup):
         lnl = one_step()
