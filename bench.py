@@ -153,6 +153,13 @@ def roofline(wl, mode, P, steps, part_s, launches, bytes_pattern, flops_pattern,
            "basis": (f"algorithmic {bytes_pattern} B/pattern/traversal = 16*C*S*I + N + 8 "
                      f"({bytes_pattern / wl.et.n_internal:.1f} B/update) x {pat_per_launch:.0f} patterns per launch "
                      f"/ mean HIP-event launch duration")}
+    if fused:
+        # the fused traversal's own bytes: tip codes (1 B per tip), weight in, site lnL out
+        fb = wl.et.n_tips + 16
+        g2 = fb * pat_per_launch / per_launch_s / 1e9
+        hbm.update(achieved=g2, frac=g2 / HBM_PEAK_GBS,
+                   basis=(f"fused traversal: {fb} B/pattern = N tip codes + 8 weight + 8 site lnL "
+                          f"x {pat_per_launch:.0f} patterns per launch / mean HIP-event launch duration"))
     mf = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / FP64_PEAK_TFS,
           "traffic": traffic,
           "basis": (f"algorithmic {flops_pattern} flop/pattern/traversal = 2*C*S^2 per internal child + (k-1)*C*S "

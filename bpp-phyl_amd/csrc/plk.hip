@@ -138,6 +138,13 @@ struct plk_handle_s {
   std::vector<int32_t> frag_starts_host;  // fragment start offsets, tier order
   hipFunction_t jit_fn = nullptr;
   JitShape jit_shape;
+  JitPlan jit_plan;            // table units / events of the current program (plk_jit.hpp)
+  bool jit_plan_valid = false;
+  int jit_plan_U = 0, jit_plan_budget = -1;
+  uint8_t* d_ucodes = nullptr;  // code row of every table unit of jit_plan (unit_codes_kernel)
+  int2* d_units = nullptr;      // (ta, tb) of every unit
+  size_t ucodes_cap = 0, units_cap = 0;
+  bool ucodes_valid = false;    // cleared by new tip codes and by a new plan
   int jit_resident = 0;  // workgroups of jit_fn resident at once on the device
   std::string kernel_path;                // what served the last plk_update_partials
   // per-subtree pattern compression (PLK_FLAG_SUBTREE_PATTERNS)
@@ -256,6 +263,19 @@ int jit_function(plk_handle h, const std::string& src, const char* name, hipFunc
   std::vector<char> code(n);
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
+  // PLK_JIT_DUMP=<dir>: keep the generated source and code object for inspection
+  // (llvm-objdump -d --mcpu=gfx950 <dir>/plk_jit_<n>.co)
+  if (const char* dir = std::getenv("PLK_JIT_DUMP")) {
+    const std::string stem = std::string(dir) + "/plk_jit_" + std::to_string(g_jit_cache.size());
+    if (FILE* f = std::fopen((stem + ".hip").c_str(), "wb")) {
+      std::fwrite(src.data(), 1, src.size(), f);
+      std::fclose(f);
+    }
+    if (FILE* f = std::fopen((stem + ".co").c_str(), "wb")) {
+      std::fwrite(code.data(), 1, code.size(), f);
+      std::fclose(f);
+    }
+  }
   hipModule_t mod;
   HIPCHK(h, hipModuleLoadData(&mod, code.data()));
   hipFunction_t fn;
@@ -499,7 +519,7 @@ int plk_destroy(plk_handle h) {
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
-                  h->d2_sums, h->d_dprog, h->pmatsT};
+                  h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) hipHostFree(h->h_req);
@@ -575,6 +595,7 @@ int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes) {
   hipSetDevice(h->device);
   HIPCHK(h, hipMemcpy(h->codes + (size_t)tip * h->n_pad, cc.data(), (size_t)h->n_patterns, hipMemcpyHostToDevice));
   h->tip_set[tip] = 1;
+  h->ucodes_valid = false;
   return PLK_OK;
 }
 
@@ -1014,6 +1035,7 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   h->prog_host = prog;
   h->frag_starts_host.assign(start_sorted.begin(), start_sorted.begin() + nf);
   h->jit_fn = nullptr;  // specialised kernel of the new program: compiled on first use
+  h->jit_plan_valid = false;
   HIPCHK(h, hipStreamSynchronize(h->stream));  // host staging vectors go out of scope
   h->prog_ops.assign(ops, ops + n_ops);
   h->prog_materialize = materialize;
@@ -1160,20 +1182,51 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   if (jit) {
     sh.C = h->C;
     sh.CW = h->prog_ciw ? h->C : 1;
-    // two pattern groups per workgroup share the staged tables; with rescaling every
-    // node has two workgroup barriers, whose cost grows with the waves that meet there
-    // (cfg5: 1.93 ms at G = 2, 1.16 ms at G = 1), so scaling runs use one group
-    sh.G = (h->n_pad % 128 == 0)
-               ? env_int("PLK_JIT_G", ((h->flags & PLK_FLAG_SCALING) && !h->prog_ciw) ? 1 : 2, 1, 2)
-               : 1;
+    sh.pin = env_int("PLK_JIT_PIN", 1, 0, 1) != 0;  // cfg2 0.244 -> 0.241, cfg5 1.04 -> 0.93 ms
+    sh.U = h->n_codes;
+    // cherries read one product table (plk_jit.hpp: JitUnit) while a fragment's tables stay
+    // within PLK_JIT_PAIR_KB (0: no pairs)
+    const int budget = env_int("PLK_JIT_PAIR_KB", 64, 0, 150) * 1024 / (int)sizeof(double);
+    if (!h->jit_plan_valid || h->jit_plan_U != sh.U || h->jit_plan_budget != budget) {
+      h->jit_plan = jit_plan(h->prog_host, h->frag_starts_host, sh.C, sh.U, budget);
+      h->jit_plan_valid = true;
+      h->jit_plan_U = sh.U;
+      h->jit_plan_budget = budget;
+      h->jit_fn = nullptr;
+      h->ucodes_valid = false;
+    }
+    if (!h->ucodes_valid) {
+      std::vector<int2> units;
+      for (const auto& un : h->jit_plan.units)
+        for (const JitUnit& u : un) units.push_back(make_int2(u.ta, u.tb));
+      int rc = ensure_cap(h, (void**)&h->d_ucodes, &h->ucodes_cap, std::max<size_t>(units.size(), 1) * h->n_pad);
+      if (!rc) rc = ensure_cap(h, (void**)&h->d_units, &h->units_cap, std::max<size_t>(units.size(), 1) * sizeof(int2));
+      if (rc) return rc;
+      if (!units.empty()) {
+        HIPCHK(h, hipMemcpyAsync(h->d_units, units.data(), units.size() * sizeof(int2), hipMemcpyHostToDevice,
+                                 h->stream));
+        const dim3 ug((unsigned)((h->n_pad / 16 + 255) / 256), (unsigned)units.size());
+        hipLaunchKernelGGL(unit_codes_kernel, ug, dim3(256), 0, h->stream, h->codes, h->n_pad, h->d_units, sh.U,
+                           h->d_ucodes);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipStreamSynchronize(h->stream));  // `units` goes out of scope
+      }
+      h->ucodes_valid = true;
+    }
+    sh.NT = h->jit_plan.NU;
+    sh.TD = h->jit_plan.tab_doubles;
+    sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
+    // pattern groups per workgroup (they share the staged tables): with per-node rescaling
+    // and one class per wave every node has two workgroup barriers, whose cost grows with
+    // the waves that meet there (cfg5: 1.93 ms at G = 2, 1.16 ms at G = 1), so one group;
+    // otherwise the G with the most resident waves (jit_auto_groups; cfg2 with cherry
+    // tables: G = 3, 0.207 ms, G = 2 0.222 ms)
+    sh.G = env_int("PLK_JIT_G", 0, 0, 4);
+    if (sh.G == 0) sh.G = (sh.scale && !h->prog_ciw) ? 1 : jit_auto_groups(sh);
     // two patterns per lane halve the P(t) reads per FMA but double the registers:
     // measured slower (cfg2 0.255-0.301 vs 0.241 ms), so opt-in; not with speculation
     sh.PW = env_int("PLK_JIT_PW", 1, 1, 2);
-    sh.pin = env_int("PLK_JIT_PIN", 1, 0, 1) != 0;  // cfg2 0.244 -> 0.241, cfg5 1.04 -> 0.93 ms
     if (sh.G * sh.PW > 4 || h->n_pad % (64 * sh.G * sh.PW) != 0 || env_is("PLK_JIT_SPECULATE", '1')) sh.PW = 1;
-    sh.U = h->n_codes;
-    sh.NT = jit_max_fragment_tips(h->prog_host, h->frag_starts_host);
-    sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     // two-stage pipeline, codes / HBM loads 3 ahead (cfg2 0.274 -> 0.259 ms); with every
     // class in the wave a ring slot is C x larger, so there one event ahead (cfg5 1.04 ms
     // at L = 1, 1.48 ms at L = 3)
@@ -1188,16 +1241,16 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW || sh.PW != h->jit_shape.PW ||
         sh.pin != h->jit_shape.pin ||
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
-        sh.NT != h->jit_shape.NT || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
+        sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
         sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.exact_only != h->jit_shape.exact_only) {
-      int rc = jit_function(h, jit_tree4_source(h->prog_host, h->frag_starts_host, sh), "plk_jit_tree4", &h->jit_fn);
+      int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
       h->jit_resident = 0;
     }
     ja.partials = a.partials;
     ja.scale = a.scale;
-    ja.codes = a.codes;
+    ja.codes = h->d_ucodes;
     ja.tipP = h->tipP;
     ja.weights = a.weights;
     ja.pi = a.pi;
@@ -1207,7 +1260,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.slot_stride = a.slot_stride;
     ja.n_pad = a.n_pad;
     ja.n_patterns = a.n_patterns;
-    ja.n_sblocks = (int32_t)(h->n_pad / (64 * sh.G * sh.PW));
+    ja.n_sblocks = (int32_t)((h->n_pad + 64 * sh.G * sh.PW - 1) / (64 * sh.G * sh.PW));  // last may be ragged
     ja.guard = a.guard;
   }
   h->kernel_path = jit ? "jit_tree4" : kind == FK_TREEM ? "treeM" : kind == FK_TREES ? "treeS" : "tree4";

@@ -49,7 +49,7 @@ typedef __attribute__((address_space(4))) const double* CPd;
 #define kScaleUp 115792089237316195423570985008687907853269984665640564039457584007913129639936.0
 #define kScaleThr (1.0 / kScaleUp)
 
-struct JArgs {
+struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
   double* partials; i32* scale; const u8* codes; const double* tipP; const double* weights;
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
@@ -167,7 +167,8 @@ __device__ __forceinline__ void rescale(double (&v)[4 * CW * PW], int (&cnt)[PW]
 // off: the lane's first pattern in the slot (tile layout); pattern pw is 64 further
 template <int CW, int PW, bool SCALE>
 __device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0,
-                                      const double (&v)[4 * CW * PW], const int (&cnt)[PW]) {
+                                      const double (&v)[4 * CW * PW], const int (&cnt)[PW], bool gv) {
+  if (!gv) return;  // a group past the last pattern (ragged last super-block) recomputes group 0
   double* dst = a.partials + (i64)slot * a.slot_stride + off;
 #pragma unroll
   for (int pw = 0; pw < PW; ++pw)
@@ -184,7 +185,7 @@ __device__ __attribute__((noinline)) double jit_log(double x) { return log(x); }
 
 template <int C, int CW, int PW, int NWT, bool SCALE>
 __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[4 * CW * PW], const int (&cnt)[PW],
-                                            double* xch, int w, int g, int c0, i64 p0, i64 p) {
+                                            double* xch, int w, int g, int c0, i64 p0, i64 p, bool gv) {
   constexpr int NW = C / CW;
   const int lane = threadIdx.x & 63;
   double t[PW][CW];
@@ -227,13 +228,13 @@ __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[
       if (SCALE) r -= (double)cnt[pw] * kLn2x256;
       double wr = 0.0;
       const i64 pp = p + 64 * pw;
-      if (pp < a.n_patterns) {
+      if (gv && pp < a.n_patterns) {
         a.site_lnl[pp] = r;
         wr = a.weights[pp] * r;
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
-      if (lane == 0) a.wave_sums[(p0 + 64 * pw) >> 6] = wr;
+      if (gv && lane == 0) a.wave_sums[(p0 + 64 * pw) >> 6] = wr;
     }
   }
 }
@@ -264,7 +265,8 @@ struct JitShape {
   bool pin = false; // pin accumulators after every event (see pin())
   int G = 1;        // 64-pattern groups per workgroup
   int U = 1;        // codes in use (rows of a tip table)
-  int NT = 0;       // most tips of any fragment (LDS table slots)
+  int NT = 0;       // most table units (tips or tip pairs) of any fragment: code rows in LDS
+  int TD = 0;       // most table doubles of any fragment (JitPlan::tab_doubles)
   bool scale = false;
   int L = 1;        // operand fetch lookahead (events)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
@@ -273,143 +275,233 @@ struct JitShape {
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     // the second exchange buffer only serves the per-node rescale
-    return nt * C * U * 4 * sizeof(double) + (scale ? 2 : 1) * (size_t)PW * G * (C / CW) * 64 * sizeof(double) +
+    return (size_t)std::max(TD, 4) * sizeof(double) + (scale ? 2 : 1) * (size_t)PW * G * (C / CW) * 64 * sizeof(double) +
            (size_t)G * nt * 64 * PW;
   }
 };
 
+// Pattern groups per workgroup with the most waves resident per CU: LDS (160 KiB per CU)
+// against the tables every workgroup stages once, and VGPRs at the ~72 registers these
+// kernels take (7 waves per SIMD); ties go to fewer groups.
+inline int jit_auto_groups(const JitShape& base) {
+  int best_g = 1, best_w = 0;
+  for (int g = 1; g <= 4; ++g) {
+    JitShape t = base;
+    t.G = g;
+    const int waves_wg = (t.C / t.CW) * g;
+    const int by_lds = (int)((160 * 1024) / std::max<size_t>(t.lds_bytes(), 1));
+    const int by_vgpr = (4 * 7) / waves_wg;
+    const int waves = std::min(by_lds, by_vgpr) * waves_wg;
+    if (waves > best_w) {
+      best_w = waves;
+      best_g = g;
+    }
+  }
+  return best_g;
+}
+
 struct JitEvent {
-  int op;     // T_TIP (a = local tip index), T_LOAD, T_DESCEND, T_ASCEND (level >= 1), T_ROOT
+  int op;     // T_TIP (a = fragment-local table unit), T_LOAD, T_DESCEND, T_ASCEND (level >= 1), T_ROOT
   int level;  // accumulator level the event works on
   int a, b;   // program word fields
 };
 
-// Per fragment (tier order): its events, with TIP events renumbered to fragment-local
-// tip indices; tips[f] lists the fragment's tips (local index -> tip).
-inline void jit_fragments(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts,
-                          std::vector<std::vector<JitEvent> >& events, std::vector<std::vector<int> >& tips) {
-  events.assign(starts.size(), {});
-  tips.assign(starts.size(), {});
+// One LDS table of a fragment: a tip's rows tipP[tip][c][code][x] (tb < 0), or -- for two
+// tips that are the first two contributions of one node (a cherry) -- their product
+// rows pair[c][ca * U + cb][x] = tipP[ta][c][ca][x] * tipP[tb][c][cb][x], read with one
+// combined code (ca * U + cb, formed while staging the codes).  The interpreter forms the
+// same product (A = row_a, then A *= row_b), so the results stay bitwise identical while
+// a cherry costs one table read instead of two and no multiply.  Layout in LDS at `off`
+// (doubles): [C][rows][4].
+struct JitUnit {
+  int ta, tb;
+  int off;
+};
+
+struct JitPlan {
+  std::vector<std::vector<JitEvent> > events;  // per fragment (tier order)
+  std::vector<std::vector<JitUnit> > units;    // per fragment: its tables, in event order
+  int NU = 0;           // most units of any fragment
+  int tab_doubles = 0;  // most table doubles of any fragment
+};
+
+// Per fragment: its events with TIP events renumbered to fragment-local table units.
+// Cherries become pair units while the fragment's tables stay within pair_budget
+// doubles (0: no pairs; pairs need U * U <= 256 so that a combined code is one byte).
+inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts, int C, int U,
+                        int pair_budget) {
+  JitPlan plan;
+  plan.events.assign(starts.size(), {});
+  plan.units.assign(starts.size(), {});
+  const bool pairs = pair_budget > 0 && U * U <= 256;
+  const int single = C * U * 4, grow = C * U * 4 * (U - 1);
   for (size_t f = 0; f < starts.size(); ++f) {
-    int d = 0;
+    std::vector<JitEvent>& ev = plan.events[f];
+    std::vector<JitUnit>& un = plan.units[f];
+    int d = 0, total = 0;
     for (size_t i = (size_t)starts[f];; ++i) {
       const TInstr& w = prog[i];
       if (w.op == T_TIP) {
-        events[f].push_back({T_TIP, d, (int)tips[f].size(), w.b});
-        tips[f].push_back(w.a);
+        // the previous event is this node's first contribution, a tip not yet paired
+        const size_t n = ev.size();
+        const bool first_tip = n >= 1 && ev[n - 1].op == T_TIP && ev[n - 1].level == d &&
+                               un[(size_t)ev[n - 1].a].tb < 0 &&
+                               (n == 1 ? d == 0 : ev[n - 2].op == T_DESCEND && ev[n - 2].level == d);
+        if (pairs && first_tip && total + grow <= pair_budget) {
+          un[(size_t)ev[n - 1].a].tb = w.a;
+          total += grow;
+        } else {
+          ev.push_back({T_TIP, d, (int)un.size(), w.b});
+          un.push_back({w.a, -1, 0});
+          total += single;
+        }
       } else if (w.op == T_LOAD) {
-        events[f].push_back({T_LOAD, d, w.a, w.b});
+        ev.push_back({T_LOAD, d, w.a, w.b});
       } else if (w.op == T_DESCEND) {
         ++d;
-        events[f].push_back({T_DESCEND, d, 0, 0});
+        ev.push_back({T_DESCEND, d, 0, 0});
       } else if (w.op == T_ASCEND) {
         if (d == 0) continue;  // fragment root: finished by ROOT
-        events[f].push_back({T_ASCEND, d, w.a, w.b});
+        ev.push_back({T_ASCEND, d, w.a, w.b});
         --d;
       } else if (w.op == T_ROOT) {
-        events[f].push_back({T_ROOT, 0, w.a, w.b});
+        ev.push_back({T_ROOT, 0, w.a, w.b});
         break;
       }
     }
+    int off = 0;
+    for (JitUnit& u : un) {
+      u.off = off;
+      off += u.tb < 0 ? single : C * U * U * 4;
+    }
+    plan.NU = std::max(plan.NU, (int)un.size());
+    plan.tab_doubles = std::max(plan.tab_doubles, off);
   }
+  return plan;
 }
 
-// Most tips of any fragment (LDS table slots the kernel needs).
-inline int jit_max_fragment_tips(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts) {
-  int best = 0;
-  for (size_t f = 0; f < starts.size(); ++f) {
-    int n = 0;
-    for (size_t i = (size_t)starts[f]; prog[i].op != T_ROOT; ++i) n += prog[i].op == T_TIP;
-    best = std::max(best, n);
-  }
-  return best;
-}
-
-// Emit the kernel for a tree program (`prog` / `starts`: build_tree4_program's words
-// and fragment start offsets in tier order; fragment id = frag_base + blockIdx.y).
-inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts,
-                                    const JitShape& sh) {
-  std::vector<std::vector<JitEvent> > events;
-  std::vector<std::vector<int> > tips;
-  jit_fragments(prog, starts, events, tips);
-  const int C = sh.C, L = std::max(sh.L, 1);
+// Emit the kernel for a fragment plan (jit_plan over build_tree4_program's words and
+// fragment start offsets in tier order; fragment id = frag_base + blockIdx.y).
+inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
+  const std::vector<std::vector<JitEvent> >& events = plan.events;
+  const int C = sh.C, L = std::max(sh.L, 1), U = sh.U;
   std::string s;
-  s.reserve(100 * prog.size() + 8192);
+  s.reserve(4096 * events.size() + 16384);
   s += kJitPrelude;
   char buf[400];
   const std::string minw_s = sh.minw > 0 ? ", " + std::to_string(sh.minw) : std::string();
-  // fragment tip lists (CSR) as constant data of the module; entry 0 of kFragTips is
-  // padding: tip k of fragment f is kFragTips[1 + kFragTipStart[f] + k]
-  s += "\n__device__ const int kFragTipStart[] = {0";
+  // fragment table units (CSR) as constant data of the module: unit k of fragment f is
+  // entry kFragUnitStart[f] + k of kUnitTA / kUnitTB (-1: single tip) / kUnitOff
+  std::string ua = "};\n__device__ const int kUnitTA[] = {0", ub = "};\n__device__ const int kUnitTB[] = {0",
+              uo = "};\n__device__ const int kUnitOff[] = {0";
+  s += "\n__device__ const int kFragUnitStart[] = {0";
   {
     int acc = 0;
-    for (const auto& t : tips) {
-      acc += (int)t.size();
+    for (const auto& un : plan.units) {
+      acc += (int)un.size();
       snprintf(buf, sizeof(buf), ",%d", acc);
       s += buf;
+      for (const JitUnit& u : un) {
+        snprintf(buf, sizeof(buf), ",%d", u.ta);
+        ua += buf;
+        snprintf(buf, sizeof(buf), ",%d", u.tb);
+        ub += buf;
+        snprintf(buf, sizeof(buf), ",%d", u.off);
+        uo += buf;
+      }
     }
   }
-  s += "};\n__device__ const int kFragTips[] = {0";
-  for (const auto& t : tips)
-    for (int x : t) {
-      snprintf(buf, sizeof(buf), ",%d", x);
-      s += buf;
-    }
-  s += "};\n";
+  s += ua + ub + uo + "};\n";
   const int CW = sh.CW, NW = C / CW, PW = sh.PW;
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
-           "#define U_ %d\n#define NT_ %d\n#define SC_ %s\n#define V_ (4 * CW_ * PW_)\n"
+           "#define U_ %d\n#define NT_ %d\n#define TD_ %d\n#define SC_ %s\n#define V_ (4 * CW_ * PW_)\n"
            "extern \"C\" __global__ __launch_bounds__(%d%s) void plk_jit_tree4(JArgs a, const double* __restrict__ "
            "pmats, int frag_base) {\n",
-           C, CW, NW, PW, sh.G, NW * sh.G, sh.U, std::max(sh.NT, 1), sh.scale ? "true" : "false", 64 * NW * sh.G,
-           minw_s.c_str());
+           C, CW, NW, PW, sh.G, NW * sh.G, U, std::max(sh.NT, 1), std::max(sh.TD, 4), sh.scale ? "true" : "false",
+           64 * NW * sh.G, minw_s.c_str());
   s += buf;
   s += R"PLKJIT(  extern __shared__ __attribute__((aligned(16))) double lds[];
-  double* tab = lds;                                          // [NT_][C_][U_][4]
-  double* xch = tab + NT_ * C_ * U_ * 4;                      // [2][PW_][NWT_][64] (rescale alternates)
+  double* tab = lds;                                          // units: [C_][U_ or U_ * U_][4] each
+  double* xch = tab + TD_;                                    // [2][PW_][NWT_][64] (rescale alternates)
   double* xch2 = xch + PW_ * NWT_ * 64;
   u8* code_lds = reinterpret_cast<u8*>(xch + (SC_ ? 2 : 1) * PW_ * NWT_ * 64); // [G_][NT_][64 * PW_]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c0 = (w % NW_) * CW_, g = w / NW_;
   const int frag = frag_base + (int)blockIdx.y;
-  const int t0 = 1 + kFragTipStart[frag], nt = kFragTipStart[frag + 1] - kFragTipStart[frag];
-  for (int i = threadIdx.x; i < nt * (C_ * U_ * 4); i += blockDim.x) {
-    const int k = i / (C_ * U_ * 4), r = i - k * (C_ * U_ * 4);
-    tab[i] = a.tipP[(i64)kFragTips[t0 + k] * (C_ * U_ * 4) + r];
+  const int u0 = 1 + kFragUnitStart[frag], nu = kFragUnitStart[frag + 1] - kFragUnitStart[frag];
+  // tables: wave w stages units w, w + NWT_, ... (one dependent chain per unit and wave,
+  // the waves' chains overlap)
+  for (int k = w; k < nu; k += NWT_) {
+    const int ta = kUnitTA[u0 + k], tb = kUnitTB[u0 + k];
+    double* dst = tab + kUnitOff[u0 + k];
+    const double* ra = a.tipP + (i64)ta * (C_ * U_ * 4);
+    if (tb < 0) {
+      for (int i = lane; i < C_ * U_ * 4; i += 64) dst[i] = ra[i];
+    } else {
+      const double* rb = a.tipP + (i64)tb * (C_ * U_ * 4);
+      for (int i = lane; i < C_ * U_ * U_ * 4; i += 64) {
+        const int c = i / (U_ * U_ * 4), r = i - c * (U_ * U_ * 4), ca = r / (U_ * 4), cb = (r >> 2) % U_, x = i & 3;
+        dst[i] = ra[(c * U_ + ca) * 4 + x] * rb[(c * U_ + cb) * 4 + x];
+      }
+    }
   }
   const CPd pm = (CPd)(pmats + c0 * 16);
-  const double* trow = tab + c0 * (U_ * 4);
-  const u8* crow = code_lds + g * (NT_ * 64 * PW_) + lane;
-  (void)xch; (void)xch2; (void)trow; (void)crow;
-// tip k: codes of the lane's patterns (4 per int), then their table rows
+  const double* trow = tab + c0 * (U_ * 4);         // single-tip units
+  const double* trow2 = tab + c0 * (U_ * U_ * 4);   // pair units
+  (void)xch; (void)xch2; (void)trow; (void)trow2;
+// unit k: codes of the lane's patterns (4 per int), then their table rows (R rows per
+// class at OFF doubles from the class base TB)
 #define CODEF(Q, k) { Q = 0; _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) \
     Q |= (int)crow[(k) * (64 * PW_) + 64 * pw_] << (8 * pw_); }
-#define ROWF(F, k, Q) { _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
-    const double* r0_ = trow + ((k) * (C_ * U_) + (((Q) >> (8 * pw_)) & 255)) * 4; \
+#define ROWF(F, TB, OFF, R, Q) { _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
+    const double* r0_ = TB + (OFF) + (((Q) >> (8 * pw_)) & 255) * 4; \
     _Pragma("unroll") for (int cw_ = 0; cw_ < CW_; ++cw_) { \
-      const double2* r_ = reinterpret_cast<const double2*>(r0_ + cw_ * (U_ * 4)); \
+      const double2* r_ = reinterpret_cast<const double2*>(r0_ + cw_ * ((R) * 4)); \
       const double2 x_ = r_[0], y_ = r_[1]; const int v_ = 4 * (pw_ * CW_ + cw_); \
       F[v_] = x_.x; F[v_ + 1] = x_.y; F[v_ + 2] = y_.x; F[v_ + 3] = y_.y; } } }
-#define TIPF(F, k) { int q_; CODEF(q_, k) ROWF(F, k, q_) }
+#define TIPF(F, k, TB, OFF, R) { int q_; CODEF(q_, k) ROWF(F, TB, OFF, R, q_) }
 #define LOADF(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
     _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
       _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[4 * CW_ * pw_ + i_] = L_[64 * pw_ + (i64)i_ * kTile]; \
       if (SC_) FK[pw_] = a.scale[(i64)(slot) * a.n_pad + p + 64 * pw_]; } }
 #define SB __builtin_amdgcn_sched_barrier(0);
+  // code staging: this thread's items (uint4 column j of group gg in unit k's code row;
+  // JArgs::codes holds one row per unit, unit_codes_kernel), fixed over the super-blocks.
+  // The codes of the next super-block are loaded into registers while this one computes.
+  constexpr int NI_ = (G_ * NT_ * 4 * PW_ + 64 * NWT_ - 1) / (64 * NWT_);
+  const uint4* ucodes = reinterpret_cast<const uint4*>(a.codes);
+  const i64 row16 = a.n_pad / 16;
+  i64 iu_[NI_]; int ic_[NI_], il_[NI_]; uint4 va_[NI_];
+  _Pragma("unroll") for (int m = 0; m < NI_; ++m) {
+    const int i = threadIdx.x + m * (64 * NWT_);
+    const int gg = i / (nu * 4 * PW_), r = i - gg * (nu * 4 * PW_), k = r / (4 * PW_), j = r - k * (4 * PW_);
+    const bool ok = i < G_ * nu * 4 * PW_;
+    ic_[m] = ok ? gg * (64 * PW_) + 16 * j : 0x7fffffff;  // column in the super-block (none: past n_pad)
+    iu_[m] = (i64)(u0 - 1 + k) * row16 + (ic_[m] >> 4);
+    il_[m] = (gg * NT_ + k) * 4 * PW_ + j;
+  }
+  auto fetch_codes = [&](int sb_) {
+    const i64 q0_ = (i64)sb_ * (64 * PW_ * G_);
+    _Pragma("unroll") for (int m = 0; m < NI_; ++m)
+      if (q0_ + ic_[m] < a.n_pad) va_[m] = ucodes[iu_[m] + (q0_ >> 4)];
+  };
+  fetch_codes(blockIdx.x);
   for (int sb = blockIdx.x; sb < a.n_sblocks; sb += gridDim.x) {
     const i64 q0 = (i64)sb * (64 * PW_ * G_);
-    const i64 p0 = q0 + g * (64 * PW_), p = p0 + lane;
+    // super-blocks of G_ groups; in a ragged last one, groups past n_pad recompute group 0
+    // (in bounds everywhere) and store nothing
+    const bool gv = q0 + g * (64 * PW_) < a.n_pad;
+    const i64 p0 = gv ? q0 + g * (64 * PW_) : q0, p = p0 + lane;
+    const u8* crow = code_lds + (gv ? g : 0) * (NT_ * 64 * PW_) + lane;
     const i64 toff = (p >> 7) * (C_ * 4 * kTile) + (i64)c0 * 4 * kTile + (p & (kTile - 1));
     (void)toff;
     __syncthreads();  // the previous super-block is done with code_lds / xch (and tab is staged)
-    for (int i = threadIdx.x; i < G_ * nt * 4 * PW_; i += blockDim.x) {
-      const int gg = i / (nt * 4 * PW_), r = i - gg * (nt * 4 * PW_), k = r / (4 * PW_), j = r - k * (4 * PW_);
-      reinterpret_cast<uint4*>(code_lds)[(gg * NT_ + k) * 4 * PW_ + j] =
-          *reinterpret_cast<const uint4*>(a.codes + (i64)kFragTips[t0 + k] * a.n_pad + q0 + gg * (64 * PW_) + 16 * j);
-    }
+    _Pragma("unroll") for (int m = 0; m < NI_; ++m)
+      if (q0 + ic_[m] < a.n_pad) reinterpret_cast<uint4*>(code_lds)[il_[m]] = va_[m];
     __syncthreads();
+    fetch_codes(sb + gridDim.x);
 )PLKJIT";
   int max_level = 0;
   for (const auto& ev : events)
@@ -447,16 +539,22 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
         snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %d)\n", slot[(size_t)i], slot[(size_t)i], e.a);
       s += buf;
     };
+    auto unit_args = [&](const JitEvent& e) -> std::string {  // TB, OFF, R of a unit
+      const JitUnit& u = plan.units[f][(size_t)e.a];
+      char ubuf[96];
+      snprintf(ubuf, sizeof(ubuf), "%s, %d, %d", u.tb < 0 ? "trow" : "trow2", u.off, u.tb < 0 ? U : U * U);
+      return ubuf;
+    };
     auto emit_stage2 = [&](int i) {
       const JitEvent& e = ev[(size_t)i];
       if (e.op != T_TIP) return;
-      snprintf(buf, sizeof(buf), "      ROWF(F%d, %d, Q%d)\n", slot[(size_t)i], e.a, slot[(size_t)i]);
+      snprintf(buf, sizeof(buf), "      ROWF(F%d, %s, Q%d)\n", slot[(size_t)i], unit_args(e).c_str(), slot[(size_t)i]);
       s += buf;
     };
     auto emit_fetch = [&](int i) {
       const JitEvent& e = ev[(size_t)i];
       if (e.op == T_TIP)
-        snprintf(buf, sizeof(buf), "      TIPF(F%d, %d)\n", slot[(size_t)i], e.a);
+        snprintf(buf, sizeof(buf), "      TIPF(F%d, %d, %s)\n", slot[(size_t)i], e.a, unit_args(e).c_str());
       else
         snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %d)\n", slot[(size_t)i], slot[(size_t)i], e.a);
       s += buf;
@@ -525,7 +623,7 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
           if (e.b >= 0) {
             if (sh.scale) check_line(dd);
             if (e.a >= 0) {
-              snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %d, toff, p, c0, A%d, K%d);\n", e.a, dd, dd);
+              snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %d, toff, p, c0, A%d, K%d, gv);\n", e.a, dd, dd);
               s += buf;
             }
           }
@@ -546,10 +644,10 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
         } else {  // T_ROOT
           if (sh.scale) check_line(0);
           if (e.a >= 0) {
-            snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %d, toff, p, c0, A0, K0);\n", e.a);
+            snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %d, toff, p, c0, A0, K0, gv);\n", e.a);
             s += buf;
           }
-          if (e.b) s += "      reduce_root<C_, CW_, PW_, NWT_, SC_>(a, A0, K0, xch, w, g, c0, p0, p);\n";
+          if (e.b) s += "      reduce_root<C_, CW_, PW_, NWT_, SC_>(a, A0, K0, xch, w, g, c0, p0, p, gv);\n";
         }
       }
     };
@@ -561,10 +659,11 @@ inline std::string jit_tree4_source(const std::vector<TInstr>& prog, const std::
       // the exact pass reads its operands through laundered copies of the base pointers,
       // so the compiler cannot reuse (and keep live across the vote) the fast pass's loads
       s += "      if (__syncthreads_or(dng)) {  // a check could have rescaled: redo it exactly\n"
-           "      const CPd pmo_ = pm; const double* trowo_ = trow; const u8* crowo_ = crow; const i64 toffo_ = toff;\n"
+           "      const CPd pmo_ = pm; const double* trowo_ = trow; const double* trow2o_ = trow2; const u8* crowo_ = crow; const i64 toffo_ = toff;\n"
            "      {\n"
            "      const CPd pm = (CPd)launder_s((unsigned long long)pmo_);\n"
            "      const double* trow = (const double*)launder_s((unsigned long long)trowo_);\n"
+           "      const double* trow2 = (const double*)launder_s((unsigned long long)trow2o_);\n"
            "      const u8* crow = (const u8*)launder_v((unsigned long long)crowo_);\n"
            "      const i64 toff = (i64)launder_v((unsigned long long)toffo_);\n";
       emit_body(true);

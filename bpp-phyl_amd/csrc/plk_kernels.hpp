@@ -542,6 +542,27 @@ __global__ __launch_bounds__(256) void tip_table_kernel(const double* __restrict
   }
 }
 
+// Code rows of the tree-specialised kernel's table units (plk_jit.hpp: JitUnit): unit u
+// reads codes[ta] (tb < 0) or the combined code codes[ta] * U + codes[tb] of a cherry's
+// product table.  Rebuilt when tip codes or the unit list change, not per evaluation.
+// Bytes are combined four to a word: a byte times U plus a byte < U stays below 256.
+__global__ __launch_bounds__(256) void unit_codes_kernel(const uint8_t* __restrict__ codes, int64_t n_pad,
+                                                         const int2* __restrict__ units, int U,
+                                                         uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // uint4 index in the row
+  if (i * 16 >= n_pad) return;
+  const int2 u = units[blockIdx.y];
+  uint4 v = reinterpret_cast<const uint4*>(codes + (int64_t)u.x * n_pad)[i];
+  if (u.y >= 0) {
+    const uint4 b = reinterpret_cast<const uint4*>(codes + (int64_t)u.y * n_pad)[i];
+    v.x = v.x * U + b.x;
+    v.y = v.y * U + b.y;
+    v.z = v.z * U + b.z;
+    v.w = v.w * U + b.w;
+  }
+  reinterpret_cast<uint4*>(out + (int64_t)blockIdx.y * n_pad)[i] = v;
+}
+
 // ---------------------------------------------------------------------------
 // K5: root reduction.  Per pattern p: l_c = sum_s L[c][s] pi_s, l = sum_c l_c w_c
 // with the reference's "<= 0 terms dropped" guards (HOMOG) or NH clamp;

@@ -14,7 +14,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libplk.so")
+LIB_PATH = os.environ.get("PLK_LIB") or os.path.join(_HERE, "libplk.so")  # PLK_LIB: A/B builds
 
 PLK_OK = 0
 PLK_FLAG_SCALING = 1

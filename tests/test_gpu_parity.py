@@ -462,18 +462,28 @@ def test_s20_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling, dm, monkey
     assert lnl2 == lnl and np.array_equal(site2, site)
 
 
-@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode", [
+@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode,extra", [(*c, "")[:6] for c in [
     (4, "balanced64", 3000, False, "lnl_only"), (4, "balanced64", 1000, False, "materialize"),
     (2, "balanced64", 700, True, "lnl_only"), (1, "caterpillar40", 300, True, "materialize"),
     (4, "caterpillar40", 900, False, "lnl_only"), (4, "balanced300", 513, True, "lnl_only"),
     (4, "caterpillar200long", 600, True, "lnl_only"), (2, "caterpillar200long", 300, True, "materialize"),
-    (4, "caterpillar200longspec", 600, True, "lnl_only"), (4, "balanced64spec", 500, True, "materialize")])
-def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling, mode, monkeypatch):
+    (4, "caterpillar200longspec", 600, True, "lnl_only"), (4, "balanced64spec", 500, True, "materialize"),
+    # cherry pair tables (every cherry with 4 codes; within a small budget) and G groups per
+    # workgroup with a ragged last super-block
+    (4, "balanced64", 3000, False, "lnl_only", "acgt"), (4, "balanced64", 1000, False, "materialize", "acgt G=3"),
+    (4, "balanced64", 2000, False, "lnl_only", "acgt G=4 PAIR_KB=20"), (2, "balanced300", 513, True, "lnl_only", "G=3"),
+    (4, "balanced300", 700, True, "materialize", "acgt G=4"), (4, "balanced64", 700, False, "lnl_only", "PAIR_KB=0"),
+    (1, "caterpillar40", 300, True, "materialize", "acgt G=3")]])
+def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling, mode, extra, monkeypatch):
     """The tree-specialised kernel (plk_jit.hpp, hiprtc) against the interpreter
     (tree4_kernel) on the same program: lnL, per-pattern lnL, block sums and every
     interior partial bitwise; and the oracle at 1e-12.  The long-branch caterpillar
     drives partials below 2^-256, so the speculative no-rescale pass must detect it
     and fall back to the exact pass."""
+    for kv in extra.split():
+        if "=" in kv:
+            k, v = kv.split("=")
+            monkeypatch.setenv("PLK_JIT_" + k, v)
     if tree_kind.endswith("spec"):   # the speculative no-rescale pass with its exact fallback
         monkeypatch.setenv("PLK_JIT_SPECULATE", "1")
         tree_kind = tree_kind[:-4]
@@ -489,8 +499,9 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     rates, probs = phylo.gamma_rates(C, 0.5) if C > 1 else (np.ones(1), np.ones(1))
     wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, scaling, True, 5)
     states = wl.simulate(0, n_patterns).astype(np.int32)
-    mask = rng.random(states.shape) < 0.05
-    states[mask] = rng.integers(4, 15, size=mask.sum())
+    if "acgt" not in extra.split():
+        mask = rng.random(states.shape) < 0.05
+        states[mask] = rng.integers(4, 15, size=mask.sum())
     flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
     res = {}
     for kernel in ("0", "1"):
