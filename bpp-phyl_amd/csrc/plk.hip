@@ -1184,11 +1184,12 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.CW = h->prog_ciw ? h->C : 1;
     sh.pin = env_int("PLK_JIT_PIN", 1, 0, 1) != 0;  // cfg2 0.244 -> 0.241, cfg5 1.04 -> 0.93 ms
     sh.U = h->n_codes;
+    sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     // cherries read one product table (plk_jit.hpp: JitUnit) while a fragment's tables stay
     // within PLK_JIT_PAIR_KB (0: no pairs)
     const int budget = env_int("PLK_JIT_PAIR_KB", 64, 0, 150) * 1024 / (int)sizeof(double);
     if (!h->jit_plan_valid || h->jit_plan_U != sh.U || h->jit_plan_budget != budget) {
-      h->jit_plan = jit_plan(h->prog_host, h->frag_starts_host, sh.C, sh.U, budget);
+      h->jit_plan = jit_plan(h->prog_host, h->frag_starts_host, sh.C, sh.U, budget, sh.scale);
       h->jit_plan_valid = true;
       h->jit_plan_U = sh.U;
       h->jit_plan_budget = budget;
@@ -1215,7 +1216,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     }
     sh.NT = h->jit_plan.NU;
     sh.TD = h->jit_plan.tab_doubles;
-    sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     // pattern groups per workgroup (they share the staged tables): with per-node rescaling
     // and one class per wave every node has two workgroup barriers, whose cost grows with
     // the waves that meet there (cfg5: 1.93 ms at G = 2, 1.16 ms at G = 1), so one group;

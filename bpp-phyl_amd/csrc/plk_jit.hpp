@@ -313,9 +313,14 @@ struct JitEvent {
 // same product (A = row_a, then A *= row_b), so the results stay bitwise identical while
 // a cherry costs one table read instead of two and no multiply.  Layout in LDS at `off`
 // (doubles): [C][rows][4].
+// Without rescaling, a cherry whose partial is not stored goes one step further: its unit
+// holds the cherry's contribution to its parent, cont[c][ca * U + cb][x] =
+// sum_y P_br[c][x][y] pair[c][ca * U + cb][y] (br = the cherry node), formed in the
+// interpreter's operation order (contrib), and the cherry's branch costs no FMA either.
 struct JitUnit {
   int ta, tb;
   int off;
+  int br = -1;  // >= 0: contribution unit through P of node br
 };
 
 struct JitPlan {
@@ -329,7 +334,7 @@ struct JitPlan {
 // Cherries become pair units while the fragment's tables stay within pair_budget
 // doubles (0: no pairs; pairs need U * U <= 256 so that a combined code is one byte).
 inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts, int C, int U,
-                        int pair_budget) {
+                        int pair_budget, bool scale) {
   JitPlan plan;
   plan.events.assign(starts.size(), {});
   plan.units.assign(starts.size(), {});
@@ -362,6 +367,18 @@ inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32
         ev.push_back({T_DESCEND, d, 0, 0});
       } else if (w.op == T_ASCEND) {
         if (d == 0) continue;  // fragment root: finished by ROOT
+        const size_t n = ev.size();
+        if (!scale && w.a < 0 && w.b >= 0 && n >= 2 && ev[n - 1].op == T_TIP && ev[n - 1].level == d &&
+            un[(size_t)ev[n - 1].a].tb >= 0 && ev[n - 2].op == T_DESCEND && ev[n - 2].level == d) {
+          // a cherry (two tips, nothing else) that is not stored: its contribution unit is
+          // a tip-like operand of the parent
+          const int k = ev[n - 1].a;
+          un[(size_t)k].br = w.b;
+          ev.resize(n - 2);
+          --d;
+          ev.push_back({T_TIP, d, k, w.b});
+          continue;
+        }
         ev.push_back({T_ASCEND, d, w.a, w.b});
         --d;
       } else if (w.op == T_ROOT) {
@@ -393,7 +410,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // fragment table units (CSR) as constant data of the module: unit k of fragment f is
   // entry kFragUnitStart[f] + k of kUnitTA / kUnitTB (-1: single tip) / kUnitOff
   std::string ua = "};\n__device__ const int kUnitTA[] = {0", ub = "};\n__device__ const int kUnitTB[] = {0",
-              uo = "};\n__device__ const int kUnitOff[] = {0";
+              uo = "};\n__device__ const int kUnitOff[] = {0", ur = "};\n__device__ const int kUnitBr[] = {0";
   s += "\n__device__ const int kFragUnitStart[] = {0";
   {
     int acc = 0;
@@ -408,10 +425,12 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         ub += buf;
         snprintf(buf, sizeof(buf), ",%d", u.off);
         uo += buf;
+        snprintf(buf, sizeof(buf), ",%d", u.br);
+        ur += buf;
       }
     }
   }
-  s += ua + ub + uo + "};\n";
+  s += ua + ub + uo + ur + "};\n";
   const int CW = sh.CW, NW = C / CW, PW = sh.PW;
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
@@ -441,9 +460,21 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       for (int i = lane; i < C_ * U_ * 4; i += 64) dst[i] = ra[i];
     } else {
       const double* rb = a.tipP + (i64)tb * (C_ * U_ * 4);
+      const int br = kUnitBr[u0 + k];
       for (int i = lane; i < C_ * U_ * U_ * 4; i += 64) {
         const int c = i / (U_ * U_ * 4), r = i - c * (U_ * U_ * 4), ca = r / (U_ * 4), cb = (r >> 2) % U_, x = i & 3;
-        dst[i] = ra[(c * U_ + ca) * 4 + x] * rb[(c * U_ + cb) * 4 + x];
+        if (br < 0) {
+          dst[i] = ra[(c * U_ + ca) * 4 + x] * rb[(c * U_ + cb) * 4 + x];
+        } else {  // contrib<.., true>: the same operations in the same order
+          const double* P = pmats + ((i64)br * C_ + c) * 16 + 4 * x;
+          double v[4];
+          for (int y = 0; y < 4; ++y) v[y] = ra[(c * U_ + ca) * 4 + y] * rb[(c * U_ + cb) * 4 + y];
+          double t = P[0] * v[0];
+          t = __builtin_fma(P[1], v[1], t);
+          t = __builtin_fma(P[2], v[2], t);
+          t = __builtin_fma(P[3], v[3], t);
+          dst[i] = t;
+        }
       }
     }
   }
