@@ -313,14 +313,18 @@ struct JitEvent {
 // same product (A = row_a, then A *= row_b), so the results stay bitwise identical while
 // a cherry costs one table read instead of two and no multiply.  Layout in LDS at `off`
 // (doubles): [C][rows][4].
-// Without rescaling, a cherry whose partial is not stored goes one step further: its unit
-// holds the cherry's contribution to its parent, cont[c][ca * U + cb][x] =
+// A cherry whose partial is not stored goes one step further: its unit holds the
+// cherry's contribution to its parent, cont[c][ca * U + cb][x] =
 // sum_y P_br[c][x][y] pair[c][ca * U + cb][y] (br = the cherry node), formed in the
 // interpreter's operation order (contrib), and the cherry's branch costs no FMA either.
+// With rescaling, the cherry's joint check depends on its row alone: the row is rescaled
+// before the product exactly as the kernel would, and its count (0 / 1) is kept in U * U
+// bytes at koff, added to the parent's count with the contribution.
 struct JitUnit {
   int ta, tb;
   int off;
-  int br = -1;  // >= 0: contribution unit through P of node br
+  int br = -1;    // >= 0: contribution unit through P of node br
+  int koff = -1;  // rescaling contribution unit: doubles offset of its count bytes
 };
 
 struct JitPlan {
@@ -374,6 +378,7 @@ inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32
           // a tip-like operand of the parent
           const int k = ev[n - 1].a;
           un[(size_t)k].br = w.b;
+          if (scale) un[(size_t)k].koff = 0;  // placed below
           ev.resize(n - 2);
           --d;
           ev.push_back({T_TIP, d, k, w.b});
@@ -390,6 +395,10 @@ inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32
     for (JitUnit& u : un) {
       u.off = off;
       off += u.tb < 0 ? single : C * U * U * 4;
+      if (u.koff >= 0) {
+        u.koff = off;
+        off += (U * U + 31) / 32 * 4;  // count bytes, whole 32-byte rows
+      }
     }
     plan.NU = std::max(plan.NU, (int)un.size());
     plan.tab_doubles = std::max(plan.tab_doubles, off);
@@ -410,7 +419,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // fragment table units (CSR) as constant data of the module: unit k of fragment f is
   // entry kFragUnitStart[f] + k of kUnitTA / kUnitTB (-1: single tip) / kUnitOff
   std::string ua = "};\n__device__ const int kUnitTA[] = {0", ub = "};\n__device__ const int kUnitTB[] = {0",
-              uo = "};\n__device__ const int kUnitOff[] = {0", ur = "};\n__device__ const int kUnitBr[] = {0";
+              uo = "};\n__device__ const int kUnitOff[] = {0", ur = "};\n__device__ const int kUnitBr[] = {0",
+              uk = "};\n__device__ const int kUnitKOff[] = {0";
   s += "\n__device__ const int kFragUnitStart[] = {0";
   {
     int acc = 0;
@@ -427,10 +437,12 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         uo += buf;
         snprintf(buf, sizeof(buf), ",%d", u.br);
         ur += buf;
+        snprintf(buf, sizeof(buf), ",%d", u.koff);
+        uk += buf;
       }
     }
   }
-  s += ua + ub + uo + ur + "};\n";
+  s += ua + ub + uo + ur + uk + "};\n";
   const int CW = sh.CW, NW = C / CW, PW = sh.PW;
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
@@ -460,7 +472,35 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       for (int i = lane; i < C_ * U_ * 4; i += 64) dst[i] = ra[i];
     } else {
       const double* rb = a.tipP + (i64)tb * (C_ * U_ * 4);
-      const int br = kUnitBr[u0 + k];
+      const int br = kUnitBr[u0 + k], koff = kUnitKOff[u0 + k];
+      if (SC_ && koff >= 0) {
+        // rescaling contribution unit: one row (all classes) per lane, the cherry's joint
+        // check as rescale() makes it, then contrib<.., true>
+        for (int r = lane; r < U_ * U_; r += 64) {
+          const int ca = r / U_, cb = r - ca * U_;
+          double v[C_][4], m = 0.0;
+          for (int c = 0; c < C_; ++c)
+            for (int y = 0; y < 4; ++y) {
+              v[c][y] = ra[(c * U_ + ca) * 4 + y] * rb[(c * U_ + cb) * 4 + y];
+              m = fmax(m, v[c][y]);
+            }
+          const bool up = m > 0.0 && m < kScaleThr;
+          for (int c = 0; c < C_; ++c) {
+            if (up)
+              for (int y = 0; y < 4; ++y) v[c][y] *= kScaleUp;
+            for (int x = 0; x < 4; ++x) {
+              const double* P = pmats + ((i64)br * C_ + c) * 16 + 4 * x;
+              double t = P[0] * v[c][0];
+              t = __builtin_fma(P[1], v[c][1], t);
+              t = __builtin_fma(P[2], v[c][2], t);
+              t = __builtin_fma(P[3], v[c][3], t);
+              dst[(c * U_ * U_ + r) * 4 + x] = t;
+            }
+          }
+          reinterpret_cast<u8*>(tab + koff)[r] = up ? 1 : 0;
+        }
+        continue;
+      }
       for (int i = lane; i < C_ * U_ * U_ * 4; i += 64) {
         const int c = i / (U_ * U_ * 4), r = i - c * (U_ * U_ * 4), ca = r / (U_ * 4), cb = (r >> 2) % U_, x = i & 3;
         if (br < 0) {
@@ -492,7 +532,10 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       const double2* r_ = reinterpret_cast<const double2*>(r0_ + cw_ * ((R) * 4)); \
       const double2 x_ = r_[0], y_ = r_[1]; const int v_ = 4 * (pw_ * CW_ + cw_); \
       F[v_] = x_.x; F[v_ + 1] = x_.y; F[v_ + 2] = y_.x; F[v_ + 3] = y_.y; } } }
-#define TIPF(F, k, TB, OFF, R) { int q_; CODEF(q_, k) ROWF(F, TB, OFF, R, q_) }
+#define TIPF(F, Q, k, TB, OFF, R) { CODEF(Q, k) ROWF(F, TB, OFF, R, Q) }
+// count bytes of a rescaling contribution unit
+#define KTF(K, KOFF, Q) { _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) \
+    K[pw_] += (int)reinterpret_cast<const u8*>(tab + (KOFF))[((Q) >> (8 * pw_)) & 255]; }
 #define LOADF(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
     _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
       _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[4 * CW_ * pw_ + i_] = L_[64 * pw_ + (i64)i_ * kTile]; \
@@ -585,7 +628,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     auto emit_fetch = [&](int i) {
       const JitEvent& e = ev[(size_t)i];
       if (e.op == T_TIP)
-        snprintf(buf, sizeof(buf), "      TIPF(F%d, %d, %s)\n", slot[(size_t)i], e.a, unit_args(e).c_str());
+        snprintf(buf, sizeof(buf), "      TIPF(F%d, Q%d, %d, %s)\n", slot[(size_t)i], slot[(size_t)i], e.a,
+                 unit_args(e).c_str());
       else
         snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %d)\n", slot[(size_t)i], slot[(size_t)i], e.a);
       s += buf;
@@ -629,6 +673,11 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
           const char* set = fresh[(size_t)e.level] ? "true" : "false";
           if (e.op == T_TIP) {
             snprintf(buf, sizeof(buf), "      tipmul<V_, %s>(A%d, F%d);\n", set, e.level, slot[i]);
+            const JitUnit& u = plan.units[f][(size_t)e.a];
+            if (u.koff >= 0) {
+              s += buf;
+              snprintf(buf, sizeof(buf), "      KTF(K%d, %d, Q%d)\n", e.level, u.koff, slot[i]);
+            }
           } else {
             const std::string pr = pref(i);
             snprintf(buf, sizeof(buf), "      contrib<CW_, PW_, %s>(A%d, F%d, %s);\n", set, e.level, slot[i],

@@ -473,7 +473,11 @@ def test_s20_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling, dm, monkey
     (4, "balanced64", 3000, False, "lnl_only", "acgt"), (4, "balanced64", 1000, False, "materialize", "acgt G=3"),
     (4, "balanced64", 2000, False, "lnl_only", "acgt G=4 PAIR_KB=20"), (2, "balanced300", 513, True, "lnl_only", "G=3"),
     (4, "balanced300", 700, True, "materialize", "acgt G=4"), (4, "balanced64", 700, False, "lnl_only", "PAIR_KB=0"),
-    (1, "caterpillar40", 300, True, "materialize", "acgt G=3")]])
+    (1, "caterpillar40", 300, True, "materialize", "acgt G=3"),
+    # rescaling cherry contribution units: a code whose vector is 1e-80 drives cherry
+    # partials below 2^-256, so the tables' precomputed joint checks must fire
+    (4, "balanced64", 1500, True, "lnl_only", "tiny"), (2, "balanced300", 900, True, "lnl_only", "tiny G=3"),
+    (4, "balanced64", 700, True, "lnl_only", "tiny CIW=0")]])
 def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling, mode, extra, monkeypatch):
     """The tree-specialised kernel (plk_jit.hpp, hiprtc) against the interpreter
     (tree4_kernel) on the same program: lnL, per-pattern lnL, block sums and every
@@ -499,14 +503,20 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     rates, probs = phylo.gamma_rates(C, 0.5) if C > 1 else (np.ones(1), np.ones(1))
     wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, scaling, True, 5)
     states = wl.simulate(0, n_patterns).astype(np.int32)
-    if "acgt" not in extra.split():
+    init = phylo.DNA.init_table
+    if "tiny" in extra.split():
+        init = np.array(init, dtype=np.float64, copy=True)
+        init[4] = 1e-80
+        mask = rng.random(states.shape) < 0.3
+        states[mask] = 4
+    elif "acgt" not in extra.split():
         mask = rng.random(states.shape) < 0.05
         states[mask] = rng.integers(4, 15, size=mask.sum())
     flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
     res = {}
     for kernel in ("0", "1"):
         monkeypatch.setenv("PLK_JIT", kernel)
-        eng = engine_for(et, 4, C, n_patterns, states, phylo.DNA.init_table, rates, probs, m.pi, [m], flags=flags)
+        eng = engine_for(et, 4, C, n_patterns, states, init, rates, probs, m.pi, [m], flags=flags)
         lnl, site, blocks = run_engine(eng, et)
         assert eng.kernel_path() == ("jit_tree4" if kernel == "1" else "tree4")
         parts = np.stack([eng.get_partials(p) for p, _ in et.ops])
@@ -514,9 +524,9 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
         del eng
     (l0, s0, b0, p0), (l1, s1, b1, p1) = res["0"], res["1"]
     assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1) and np.array_equal(p0, p1)
-    if tree_kind.endswith("long"):
+    if tree_kind.endswith("long") or "tiny" in extra.split():
         assert s1.min() < -256 * np.log(2)   # partials did go through rescaling
-    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m], scaling=scaling)
+    lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=scaling)
     check(l1, s1, lo, so)
 
 
