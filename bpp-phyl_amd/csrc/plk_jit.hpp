@@ -372,7 +372,7 @@ inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32
       } else if (w.op == T_ASCEND) {
         if (d == 0) continue;  // fragment root: finished by ROOT
         const size_t n = ev.size();
-        if (!scale && w.a < 0 && w.b >= 0 && n >= 2 && ev[n - 1].op == T_TIP && ev[n - 1].level == d &&
+        if (w.a < 0 && w.b >= 0 && n >= 2 && ev[n - 1].op == T_TIP && ev[n - 1].level == d &&
             un[(size_t)ev[n - 1].a].tb >= 0 && ev[n - 2].op == T_DESCEND && ev[n - 2].level == d) {
           // a cherry (two tips, nothing else) that is not stored: its contribution unit is
           // a tip-like operand of the parent
