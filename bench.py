@@ -153,6 +153,15 @@ def roofline(wl, mode, P, steps, part_s, launches, bytes_pattern, flops_pattern,
            "basis": (f"algorithmic {bytes_pattern} B/pattern/traversal = 16*C*S*I + N + 8 "
                      f"({bytes_pattern / wl.et.n_internal:.1f} B/update) x {pat_per_launch:.0f} patterns per launch "
                      f"/ mean HIP-event launch duration")}
+    if mode == "materialize" and wl.S == 4 and wl.C in (1, 2, 4):
+        # the fused traversal writing every partial: children come from registers, so the
+        # bytes are the writes (8*C*S per internal node) plus codes, weight and site lnL
+        mb = 8 * wl.C * wl.S * wl.et.n_internal + wl.et.n_tips + 16
+        g2 = mb * pat_per_launch / per_launch_s / 1e9
+        hbm.update(achieved=g2, frac=g2 / HBM_PEAK_GBS,
+                   basis=(f"fused traversal writing every partial: {mb} B/pattern = 8*C*S*I writes + N tip codes "
+                          f"+ 8 weight + 8 site lnL x {pat_per_launch:.0f} patterns per launch / mean HIP-event "
+                          f"launch duration"))
     if fused:
         # the fused traversal's own bytes: tip codes (1 B per tip), weight in, site lnL out
         fb = wl.et.n_tips + 16

@@ -30,6 +30,10 @@
 using namespace plk;
 
 namespace {
+bool env_is(const char* name, char v) {
+  const char* e = std::getenv(name);
+  return e && e[0] == v;
+}
 
 std::string g_last_error;
 
@@ -135,6 +139,14 @@ struct plk_handle_s {
   int fused_lnl_root = -1;
   // tree-specialised kernel of the cached program (plk_jit.hpp); null: interpreter
   std::vector<TInstr> prog_host;
+  // treeM cherry contribution tables (plk_treeM.hpp: CherryLayout): (tip a, tip b, node)
+  // per T_CHERRY of the program, the device copy, and the [table | counts | codes] buffer
+  std::vector<int32_t> cherry3;
+  int32_t* d_cherry3 = nullptr;
+  int32_t* d_cherry_tips = nullptr;
+  uint8_t* d_cherry = nullptr;
+  size_t cherry3_cap = 0, cherry_tips_cap = 0, cherry_cap = 0;
+  bool cherry_codes_valid = false;
   std::vector<int32_t> frag_starts_host;  // fragment start offsets, tier order
   hipFunction_t jit_fn = nullptr;
   JitShape jit_shape;
@@ -379,8 +391,12 @@ int refresh_tip_tables(plk_handle h) {
     if (!h->pmat_valid[t]) return fail(h, PLK_ERR_STATE, "transition matrix of tip branch %d not set", t);
   if (h->n_tips > 0) {
     dim3 grid(h->n_tips, h->C);
-    tip_table_kernel<<<grid, 256, 0, h->stream>>>(h->pmats, h->code_table, h->tipP, h->n_tips, h->C, h->S,
-                                                  h->n_codes);
+    if (h->S == 64 && !env_is("PLK_PMAT64", '0'))
+      tip_table64_kernel<<<grid, 256, (size_t)(64 * 64 + h->n_codes * 64) * sizeof(double), h->stream>>>(
+          h->pmats, h->code_table, h->tipP, h->n_tips, h->C, h->n_codes);
+    else
+      tip_table_kernel<<<grid, 256, 0, h->stream>>>(h->pmats, h->code_table, h->tipP, h->n_tips, h->C, h->S,
+                                                    h->n_codes);
     HIPCHK(h, hipGetLastError());
   }
   std::fill(h->tip_table_valid.begin(), h->tip_table_valid.end(), 1);
@@ -519,7 +535,8 @@ int plk_destroy(plk_handle h) {
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
-                  h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units};
+                  h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
+                  h->d_cherry_tips, h->d_cherry};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) hipHostFree(h->h_req);
@@ -596,6 +613,7 @@ int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes) {
   HIPCHK(h, hipMemcpy(h->codes + (size_t)tip * h->n_pad, cc.data(), (size_t)h->n_patterns, hipMemcpyHostToDevice));
   h->tip_set[tip] = 1;
   h->ucodes_valid = false;
+  h->cherry_codes_valid = false;
   return PLK_OK;
 }
 
@@ -723,7 +741,10 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     hipEventRecord(ev.a, h->stream);
   }
   const size_t lds = (size_t)(h->S + (tips_fused ? 2 : 1) * S2) * sizeof(double);
-  pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a, inl);
+  if (h->S == 64 && deriv_mask == PLK_DERIV_P && !env_is("PLK_PMAT64", '0'))
+    pmat64_kernel<<<dim3(n, h->C), dim3(256), (size_t)(64 + 2 * S2) * sizeof(double), h->stream>>>(a, inl);
+  else
+    pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a, inl);
   HIPCHK(h, hipGetLastError());
   if (h->timing & PLK_TIME_PMAT) {
     hipEventRecord(ev.b, h->stream);
@@ -790,11 +811,6 @@ int tree4_cw(plk_handle h) {
 // counts on the levelwise kernels (K2 / K3).
 enum FusedKind { FK_NONE = 0, FK_TREE4, FK_TREES, FK_TREEM };
 
-bool env_is(const char* name, char v) {
-  const char* e = std::getenv(name);
-  return e && e[0] == v;
-}
-
 FusedKind fused_kind(plk_handle h) {
   if (h->flags & PLK_FLAG_LEVELWISE) return FK_NONE;
   if (h->S == 4) return (h->C == 1 || h->C == 2 || h->C == 4) ? FK_TREE4 : FK_NONE;
@@ -834,6 +850,56 @@ int jit_tip_cap(plk_handle h) {
   return std::max(2, (kb * 1024) / (h->C * std::max(h->n_codes, 1) * 4 * (int)sizeof(double)));
 }
 
+// treeM programs replace unstored cherries by T_CHERRY rows (PLK_TREEM_CHERRY=0: off);
+// combined codes are 16-bit
+bool treeM_cherries(plk_handle h) {
+  return fused_kind(h) == FK_TREEM && h->n_codes * h->n_codes <= 65535 && !env_is("PLK_TREEM_CHERRY", '0');
+}
+
+// Cherry contribution tables of the current treeM program (plk_treeM.hpp), rebuilt on
+// every traversal (P(t) and the tip tables may have changed); combined codes only when
+// the tip codes or the program changed.
+int build_cherry_tables(plk_handle h) {
+  const int nch = (int)h->cherry3.size() / 3;
+  if (nch == 0) return PLK_OK;
+  const int U = h->n_codes, S = h->S, C = h->C;
+  const CherryLayout lay(C, U, S, h->n_pad);
+  int rc = ensure_cap(h, (void**)&h->d_cherry, &h->cherry_cap, (size_t)nch * lay.stride);
+  if (rc) return rc;
+  if (!h->cherry_codes_valid) {
+    std::vector<int32_t> tips(2 * (size_t)nch);
+    for (int k = 0; k < nch; ++k) {
+      tips[2 * (size_t)k] = h->cherry3[3 * (size_t)k];
+      tips[2 * (size_t)k + 1] = h->cherry3[3 * (size_t)k + 1];
+    }
+    rc = ensure_cap(h, (void**)&h->d_cherry3, &h->cherry3_cap, h->cherry3.size() * sizeof(int32_t));
+    if (!rc) rc = ensure_cap(h, (void**)&h->d_cherry_tips, &h->cherry_tips_cap, tips.size() * sizeof(int32_t));
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(h->d_cherry3, h->cherry3.data(), h->cherry3.size() * sizeof(int32_t),
+                             hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->d_cherry_tips, tips.data(), tips.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                             h->stream));
+    cherry_codes_kernel<<<dim3((unsigned)((h->n_pad + 255) / 256), (unsigned)nch), 256, 0, h->stream>>>(
+        h->codes, h->n_pad, h->d_cherry_tips, U, lay, h->d_cherry);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));  // `tips` goes out of scope
+    h->cherry_codes_valid = true;
+  }
+  const dim3 grid((unsigned)((U * U + 15) / 16), (unsigned)(nch * C));
+  const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
+  if (S == 20) {
+    if (sc) cherry_table_kernel<20, true><<<grid, 64, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+    else cherry_table_kernel<20, false><<<grid, 64, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+  } else if (S == 64) {
+    if (sc) cherry_table_kernel<64, true><<<grid, 64, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+    else cherry_table_kernel<64, false><<<grid, 64, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+  } else {
+    return fail(h, PLK_ERR_UNSUPPORTED, "cherry tables for %d states", S);
+  }
+  HIPCHK(h, hipGetLastError());
+  return PLK_OK;
+}
+
 // register levels (fragment height) of the fused program
 int tree_levels(plk_handle h) {
   switch (fused_kind(h)) {
@@ -841,6 +907,8 @@ int tree_levels(plk_handle h) {
       if (!jit_tree4(h)) return kTree4Levels(tree4_cw(h));
       return jit_ciw(h) ? env_int("PLK_JIT_CIW_DM", 5, 2, 16) : env_int("PLK_JIT_DM", 10, 2, 32);
     case FK_TREES: return env_int("PLK_TREES_DM", 2, 2, 4);
+    // S = 20: 3 levels (with cherry tables 7.8 ms on cfg3, 2 levels 8.7 ms although DM = 3
+    // spills a few registers at 128 VGPRs)
     case FK_TREEM: return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 2, 2, 3);
     default: return 1;
   }
@@ -889,6 +957,12 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   const int EMAX = jit_tree4(h) ? env_int("PLK_JIT_EDGES", 160, 8, 1 << 20) : (1 << 30);
   // ... and its tips' tables must fit the LDS budget (PLK_JIT_TAB_KB, default 48 KiB)
   const int TMAX = jit_tree4(h) ? jit_tip_cap(h) : (1 << 30);
+  // treeM: an unstored cherry (two tip children) is a leaf operand (T_CHERRY)
+  std::vector<char> is_cherry(h->n_nodes, 0);
+  if (!materialize && treeM_cherries(h))
+    for (int n = nt; n < h->n_nodes; ++n)
+      is_cherry[n] = produced[n] && is_child[n] && kids[n].size() == 2 && kids[n][0] < nt && kids[n][1] < nt;
+  std::vector<int32_t> cherry3;
   std::vector<int> rh(h->n_nodes, 0), ne(h->n_nodes, 0), ntp(h->n_nodes, 0);
   std::vector<char> cut_node(h->n_nodes, 0);
   for (int i = 0; i < n_ops; ++i) {
@@ -896,7 +970,7 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
     if (i + 1 < n_ops && ops[i + 1].parent == n) continue;  // polytomy: handle the node at its last op
     std::vector<int> in;
     for (int c : kids[n])
-      if (c >= nt && produced[c]) in.push_back(c);
+      if (c >= nt && produced[c] && !is_cherry[c]) in.push_back(c);
     std::sort(in.begin(), in.end(), [&](int x, int y) { return rh[x] > rh[y]; });
     size_t first = 0;
     while (first < in.size() && 1 + rh[in[first]] > DM) cut_node[in[first++]] = 1;
@@ -967,6 +1041,9 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
     for (int c : kids[n]) {
       if (c < nt) {
         prog.push_back({T_TIP, d, c, c});
+      } else if (is_cherry[c] && frag_of[c] == frag_of[n]) {
+        prog.push_back({T_CHERRY, d, (int32_t)(cherry3.size() / 3), c});
+        cherry3.insert(cherry3.end(), {kids[c][0], kids[c][1], c});
       } else if (produced[c] && frag_of[c] == frag_of[n]) {
         prog.push_back({T_DESCEND, d, 0, 0});
         emit(c, d + 1, false);
@@ -1045,6 +1122,8 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   h->prog_ciw = jit_ciw(h);
   h->prog_tmax = TMAX;
   h->prog_root = root_reduce;
+  h->cherry3.swap(cherry3);
+  h->cherry_codes_valid = false;
   // bookkeeping: which partials will be in HBM after the launch (-1: untouched)
   h->prog_mat_after.assign(h->n_internal, -1);
   for (int n = nt; n < h->n_nodes; ++n)
@@ -1132,9 +1211,11 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   }
   if (kind == FK_TREEM) {
     int rc = ensure_pmatsT(h);
+    if (!rc) rc = build_cherry_tables(h);
     if (rc) return rc;
   }
   TreeArgs a;
+  a.cherry = h->d_cherry;
   a.prog = h->d_prog;
   a.partials = h->partials;
   a.scale = h->scale;

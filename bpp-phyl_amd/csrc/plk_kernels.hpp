@@ -526,6 +526,99 @@ __global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a, const PmatInline 
   }
 }
 
+// K4 for 64 states (codon models), P only: the same sums as pmat_kernel in the same order
+// (k ascending, w = V[x][k] Vinv[k][y], fma(w, e_k, p)), so bitwise its results, but with
+// V, Vinv and e staged in LDS and a 4 x 4 register block of outputs per thread (16
+// independent FMA chains over 8 LDS reads per k instead of one chain over two reads, one
+// of them from L2).  256 threads = the 64 x 64 outputs.
+__global__ __launch_bounds__(256) void pmat64_kernel(PmatArgs a, const PmatInline inl) {
+  constexpr int S = 64;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int i = blockIdx.x, c = blockIdx.y;
+  const int b = inl.n ? inl.branch[i] : a.branch[i];
+  const int m = inl.n ? inl.model[i] : (a.model ? a.model[i] : 0);
+  const double tt = (inl.n ? inl.t[i] : a.t[i]) * a.rates[c];
+  double* e = sm;
+  double* Vm = sm + S;
+  double* Vi = Vm + S * S;
+  const double* V = a.V + (size_t)m * S * S;
+  const double* VI = a.Vinv + (size_t)m * S * S;
+  const double* lam = a.lambda + (size_t)m * S;
+  for (int k = threadIdx.x; k < S; k += blockDim.x) e[k] = exp(lam[k] * tt);
+  for (int k = threadIdx.x; k < S * S; k += blockDim.x) {
+    Vm[k] = V[k];
+    Vi[k] = VI[k];
+  }
+  __syncthreads();
+  const int xb = 4 * (threadIdx.x >> 4), yb = threadIdx.x & 15;
+  double p[4][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) p[u][v] = 0.0;
+  for (int k = 0; k < S; ++k) {
+    const double ek = e[k];
+    double vx[4], vy[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) vx[u] = Vm[(xb + u) * S + k];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) vy[v] = Vi[k * S + yb + 16 * v];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) p[u][v] = __builtin_fma(vx[u] * vy[v], ek, p[u][v]);
+  }
+  double* out = a.P + ((size_t)b * a.C + c) * S * S;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int x = xb + u, y = yb + 16 * v;
+      out[x * S + y] = tt == 0.0 ? (x == y ? 1.0 : 0.0) : p[u][v];  // getPij_t: t == 0 -> identity
+    }
+}
+
+// tip tables for 64 states: tip_table_kernel's sums (y ascending) with P and the code
+// table staged in LDS and 4 codes x 4 states per thread
+__global__ __launch_bounds__(256) void tip_table64_kernel(const double* __restrict__ P, const double* __restrict__ init,
+                                                          double* __restrict__ tipP, int n_tips, int C,
+                                                          int n_codes) {
+  constexpr int S = 64;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int tip = blockIdx.x, c = blockIdx.y;
+  double* Pl = sm;           // [x][y]
+  double* In = sm + S * S;   // [code][y]
+  const double* Pc = P + ((size_t)tip * C + c) * S * S;
+  for (int k = threadIdx.x; k < S * S; k += blockDim.x) Pl[k] = Pc[k];
+  for (int k = threadIdx.x; k < n_codes * S; k += blockDim.x) In[k] = init[k];
+  __syncthreads();
+  double* out = tipP + ((size_t)tip * C + c) * n_codes * S;
+  const int xb = 4 * (threadIdx.x & 15);
+  for (int cb = 4 * (threadIdx.x >> 4); cb < n_codes; cb += 64) {
+    double t[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) t[u][v] = 0.0;
+    for (int y = 0; y < S; ++y) {
+      double px[4], iv[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) px[v] = Pl[(xb + v) * S + y];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) iv[u] = cb + u < n_codes ? In[(cb + u) * S + y] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) t[u][v] = __builtin_fma(px[v], iv[u], t[u][v]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (cb + u < n_codes)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) out[(cb + u) * S + xb + v] = t[u][v];
+  }
+}
+
 // tipP[tip][c][code][x] = sum_y P[tip][c][x][y] * init[code][y]
 __global__ __launch_bounds__(256) void tip_table_kernel(const double* __restrict__ P, const double* __restrict__ init,
                                                         double* __restrict__ tipP, int n_tips, int C, int S,

@@ -27,7 +27,7 @@
 
 namespace plk {
 
-enum TreeOp : int32_t { T_TIP = 1, T_LOAD = 2, T_DESCEND = 3, T_ASCEND = 4, T_ROOT = 5 };
+enum TreeOp : int32_t { T_TIP = 1, T_LOAD = 2, T_DESCEND = 3, T_ASCEND = 4, T_ROOT = 5, T_CHERRY = 6 };
 
 // 16-byte program word: wave-uniform, fetched with s_load_dwordx4.
 // Per node: its child events in son order -- TIP / LOAD / DESCEND (followed by the
@@ -35,9 +35,11 @@ enum TreeOp : int32_t { T_TIP = 1, T_LOAD = 2, T_DESCEND = 3, T_ASCEND = 4, T_RO
 struct TInstr {
   int32_t op;
   int32_t d;  // register level (informational)
-  int32_t a;  // TIP: tip index; LOAD: internal slot; ASCEND/ROOT: store slot or -1
-  int32_t b;  // TIP/LOAD/ASCEND: branch (node index of the child; -1 for a fragment root); ROOT: 1 = reduce lnL
+  int32_t a;  // TIP: tip index; LOAD: internal slot; ASCEND/ROOT: store slot or -1; CHERRY: cherry index
+  int32_t b;  // TIP/LOAD/ASCEND/CHERRY: branch (node index of the child; -1 for a fragment root); ROOT: 1 = reduce lnL
 };
+// T_CHERRY (treeM only): an unstored cherry contributes one row of its precomputed
+// contribution table (plk_treeM.hpp: cherry_table_kernel), selected by its tips' codes.
 
 struct TreeArgs {
   const TInstr* prog;
@@ -64,6 +66,7 @@ struct TreeArgs {
   int32_t n_frags;            // fragments of the program (frag_start[n_frags + f] = first table, treeM)
   int32_t buf_doubles;        // treeM: doubles per LDS table buffer
   int32_t bmask;              // -1 (timing experiments: 0 = every branch reads P of node 0)
+  const uint8_t* cherry;      // treeM: per cherry [table | counts | codes] (plk_treeM.hpp: CherryLayout)
 };
 
 constexpr int kTreeMaxWaves = 4;

@@ -45,12 +45,17 @@ typedef double f64x4m __attribute__((ext_vector_type(4)));
 template <int S>
 using MAcc = f64x4m[MShape<S>::XT];
 
-// acc[x] *= sum_y P[x][y] src[y]  for the lane's 16-pattern column; PT = P^T of the
-// child's branch and this wave's class in LDS ([y][x], row stride S)
 template <int S>
-__device__ __forceinline__ void contribute_m(MAcc<S>& acc, const MAcc<S>& src, const double* PT, int lr, int lc) {
+__device__ __forceinline__ bool m_valid(int xt, int r, int lr) {
+  return S % 16 == 0 || 16 * xt + lr + 4 * r < S;
+}
+
+// d[x] = sum_y P[x][y] src[y]  for the lane's 16-pattern column; PT = P^T of the child's
+// branch and this wave's class ([y][x], row stride S; LDS or global)
+template <int S>
+__device__ __forceinline__ void matvec_m(f64x4m (&d)[MShape<S>::XT], const MAcc<S>& src, const double* PT, int lr,
+                                         int lc) {
   constexpr int XT = MShape<S>::XT, KS = MShape<S>::KS;
-  f64x4m d[XT];
 #pragma unroll
   for (int xt = 0; xt < XT; ++xt) d[xt] = (f64x4m){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -63,13 +68,99 @@ __device__ __forceinline__ void contribute_m(MAcc<S>& acc, const MAcc<S>& src, c
       d[xt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b, d[xt], 0, 0, 0);
     }
   }
+}
+
+// acc[x] *= sum_y P[x][y] src[y]
+template <int S>
+__device__ __forceinline__ void contribute_m(MAcc<S>& acc, const MAcc<S>& src, const double* PT, int lr, int lc) {
+  constexpr int XT = MShape<S>::XT;
+  f64x4m d[XT];
+  matvec_m<S>(d, src, PT, lr, lc);
 #pragma unroll
   for (int xt = 0; xt < XT; ++xt) acc[xt] *= d[xt];
 }
 
-template <int S>
-__device__ __forceinline__ bool m_valid(int xt, int r, int lr) {
-  return S % 16 == 0 || 16 * xt + lr + 4 * r < S;
+// Cherry contribution tables.  A cherry (a node whose only children are two tips) that
+// is not stored contributes to its parent  D = P_cherry . (row_a (*) row_b)  -- a function
+// of its tips' two codes only.  cherry_table_kernel forms D for every code pair (U^2
+// rows) with the same operations as the traversal (tip products from 1, the joint
+// rescale of rescale_m, matvec_m), so a T_CHERRY event is one row gather, bitwise equal to
+// the DESCEND / TIP / TIP / ASCEND it replaces, with no table staging and no barrier.
+// Per cherry, at a.cherry + k * stride: table [C][U^2][S] fp64 | counts [U^2] u8 (padded
+// to 8) | combined codes ca * U + cb [n_pad] u16.
+struct CherryLayout {
+  size_t table_bytes, count_bytes, stride;
+  __host__ __device__ CherryLayout(int C, int U, int S, int64_t n_pad) {
+    table_bytes = (size_t)C * U * U * S * sizeof(double);
+    count_bytes = ((size_t)U * U + 7) & ~(size_t)7;
+    stride = table_bytes + count_bytes + (size_t)n_pad * sizeof(uint16_t);
+  }
+};
+
+// codes of cherry k = blockIdx.y (tips cherry_tips[2k], [2k+1])
+__global__ __launch_bounds__(256) void cherry_codes_kernel(const uint8_t* __restrict__ codes, int64_t n_pad,
+                                                           const int32_t* __restrict__ cherry_tips, int U,
+                                                           CherryLayout lay, uint8_t* __restrict__ cherry) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pad) return;
+  const int k = blockIdx.y;
+  const int ca = codes[(int64_t)cherry_tips[2 * k] * n_pad + i], cb = codes[(int64_t)cherry_tips[2 * k + 1] * n_pad + i];
+  uint16_t* out = reinterpret_cast<uint16_t*>(cherry + (size_t)k * lay.stride + lay.table_bytes + lay.count_bytes);
+  out[i] = (uint16_t)(ca * U + cb);
+}
+
+// One wave per 16 code pairs (rows) of one cherry and class: blockIdx.x = row block,
+// blockIdx.y = cherry * C + class.  cherry_tips[3k .. 3k+2] = tip a, tip b, cherry node.
+template <int S, bool SCALE>
+__global__ __launch_bounds__(64) void cherry_table_kernel(const double* __restrict__ tipP,
+                                                          const double* __restrict__ pmatsT,
+                                                          const int32_t* __restrict__ cherry3, int C, int U,
+                                                          CherryLayout lay, uint8_t* __restrict__ cherry) {
+  constexpr int XT = MShape<S>::XT;
+  const int lane = threadIdx.x, lr = lane >> 4, lc = lane & 15;
+  const int k = blockIdx.y / C, c = blockIdx.y % C, U2 = U * U;
+  const int r = blockIdx.x * 16 + lc;  // this lane's row (code pair)
+  const bool rv = r < U2;
+  const int ca = rv ? r / U : 0, cb = rv ? r % U : 0;
+  const int ta = cherry3[3 * k], tb = cherry3[3 * k + 1], node = cherry3[3 * k + 2];
+  // the cherry's partial for every class (the joint check needs all of them), own class kept
+  MAcc<S> acc;
+  double m = 0.0;
+  for (int cc = 0; cc < C; ++cc) {
+    const double* rowa = tipP + (((size_t)ta * C + cc) * U + ca) * S;
+    const double* rowb = tipP + (((size_t)tb * C + cc) * U + cb) * S;
+#pragma unroll
+    for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int x = 16 * xt + lr + 4 * q;
+        double v = 1.0;
+        v *= m_valid<S>(xt, q, lr) ? rowa[x] : 0.0;
+        v *= m_valid<S>(xt, q, lr) ? rowb[x] : 0.0;
+        if (m_valid<S>(xt, q, lr)) m = fmax(m, v);
+        if (cc == c) acc[xt][q] = v;
+      }
+  }
+  m = fmax(m, __shfl_xor(m, 16, 64));
+  m = fmax(m, __shfl_xor(m, 32, 64));
+  int cnt = 0;
+  if (SCALE && m > 0.0 && m < kScaleThr) {
+#pragma unroll
+    for (int xt = 0; xt < XT; ++xt) acc[xt] *= kScaleUp;
+    cnt = 1;
+  }
+  f64x4m d[XT];
+  matvec_m<S>(d, acc, pmatsT + ((size_t)node * C + c) * S * S, lr, lc);
+  uint8_t* base = cherry + (size_t)k * lay.stride;
+  if (rv) {
+    double* row = reinterpret_cast<double*>(base) + ((size_t)c * U2 + r) * S;
+#pragma unroll
+    for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (m_valid<S>(xt, q, lr)) row[16 * xt + lr + 4 * q] = d[xt][q];
+    if (c == 0 && lr == 0) base[lay.table_bytes + r] = (uint8_t)cnt;
+  }
 }
 
 template <int S>
@@ -181,6 +272,17 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[xt][r] *= m_valid<S>(xt, r, lr) ? t[16 * xt + lr + 4 * r] : 0.0;
       handover<S, PF>(a, m, in.d, pf);
+    } else if (in.op == T_CHERRY) {
+      // one row of the cherry's contribution table; no table staging, no barrier
+      const CherryLayout lay(a.C, a.n_codes, S, a.n_pad);
+      const uint8_t* base = a.cherry + (size_t)in.a * lay.stride;
+      const int code = reinterpret_cast<const uint16_t*>(base + lay.table_bytes + lay.count_bytes)[p];
+      const double* t = reinterpret_cast<const double*>(base) + ((size_t)c * a.n_codes * a.n_codes + code) * S;
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[xt][r] *= m_valid<S>(xt, r, lr) ? t[16 * xt + lr + 4 * r] : 0.0;
+      if (SCALE) cnt += base[lay.table_bytes + code];
     } else if (in.op == T_LOAD) {
       const int64_t tile = p >> 7, q = p & (kTile - 1);
       const double* L = a.partials + (size_t)in.a * a.slot_stride + tile * ((int64_t)a.C * S * kTile) +

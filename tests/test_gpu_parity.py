@@ -712,3 +712,54 @@ def test_subtree_patterns_errors():
     ops = phylo.split_ops(et.ops)
     with pytest.raises(plk.PlkError):   # a child produced by an earlier call: links need the whole subtree
         eng.update_partials(ops[-1:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,C,scaling,variant", [
+    (20, 4, True, ""), (20, 2, False, "amb"), (20, 4, True, "tiny"), (64, 1, False, ""), (64, 1, True, "tiny")])
+def test_treeM_cherry_tables_bitwise(S, C, scaling, variant, monkeypatch):
+    """treeM with cherry contribution tables (T_CHERRY rows, plk_treeM.hpp) against the same
+    traversal without them (PLK_TREEM_CHERRY=0): lnL, per-pattern lnL and block sums
+    bitwise, and the oracle.  "tiny": one code's vector is 1e-80, so cherry partials fall
+    below 2^-256 and the tables' precomputed joint rescale must fire."""
+    et, m, alph, rates, probs, states = _random_problem(S, C, 48 if S == 20 else 24, 700, seed=S + C,
+                                                        amb=variant == "amb")
+    init = alph.init_table
+    if variant == "tiny":
+        init = np.array(init, dtype=np.float64, copy=True)
+        code = alph.n_codes - 1
+        init[code] = 1e-80
+        rng = np.random.default_rng(7)
+        states[rng.random(states.shape) < 0.3] = code
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | (plk.PLK_FLAG_SCALING if scaling else 0)
+    res = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("PLK_TREEM_CHERRY", on)
+        eng = engine_for(et, S, C, 700, states, init, rates, probs, m.pi, [m], flags=flags)
+        res[on] = run_engine(eng, et)
+        assert eng.kernel_path() == "treeM"
+        del eng
+    (l0, s0, b0), (l1, s1, b1) = res["0"], res["1"]
+    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1)
+    if variant == "tiny":
+        assert s1.min() < -256 * np.log(2)
+    lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=scaling)
+    check(l1, s1, lo, so, rel=1e-10)
+
+
+@pytest.mark.gpu
+def test_pmat64_kernels_bitwise(monkeypatch):
+    """The 64-state K4 and tip-table kernels (register-blocked, LDS-staged) give the generic
+    kernels' results bitwise: every P(t) and the traversal's lnL."""
+    et, m, alph, rates, probs, states = _random_problem(64, 1, 24, 500, seed=64, amb=True)
+    out = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("PLK_PMAT64", on)
+        eng = engine_for(et, 64, 1, 500, states, alph.init_table, rates, probs, m.pi, [m],
+                         flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY)
+        lnl, site, _ = run_engine(eng, et)
+        P = np.stack([eng.get_pmatrix(c) for _, ch in et.ops for c in ch])
+        out[on] = (lnl, site, P)
+        del eng
+    assert out["0"][0] == out["1"][0] and np.array_equal(out["0"][1], out["1"][1])
+    assert np.array_equal(out["0"][2], out["1"][2])
