@@ -730,7 +730,8 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   a.mask = deriv_mask;
   // tip tables ride along for S <= 20 (P of the block staged in LDS; S = 64 keeps the
   // separate tip_table_kernel)
-  const bool tips_fused = h->table_set && h->S <= 20;
+  const bool k64 = h->S == 64 && deriv_mask == PLK_DERIV_P && !env_is("PLK_PMAT64", '0');
+  const bool tips_fused = h->table_set && (h->S <= 20 || (k64 && h->n_codes <= 64));
   a.init = tips_fused ? h->code_table : nullptr;
   a.tipP = h->tipP;
   a.n_tips = h->n_tips;
@@ -741,7 +742,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     hipEventRecord(ev.a, h->stream);
   }
   const size_t lds = (size_t)(h->S + (tips_fused ? 2 : 1) * S2) * sizeof(double);
-  if (h->S == 64 && deriv_mask == PLK_DERIV_P && !env_is("PLK_PMAT64", '0'))
+  if (k64)
     pmat64_kernel<<<dim3(n, h->C), dim3(256), (size_t)(64 + 2 * S2) * sizeof(double), h->stream>>>(a, inl);
   else
     pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a, inl);
@@ -885,14 +886,14 @@ int build_cherry_tables(plk_handle h) {
     HIPCHK(h, hipStreamSynchronize(h->stream));  // `tips` goes out of scope
     h->cherry_codes_valid = true;
   }
-  const dim3 grid((unsigned)((U * U + 15) / 16), (unsigned)(nch * C));
+  const dim3 grid((unsigned)((U * U + 63) / 64), (unsigned)(nch * C));
   const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   if (S == 20) {
-    if (sc) cherry_table_kernel<20, true><<<grid, 64, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
-    else cherry_table_kernel<20, false><<<grid, 64, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+    if (sc) cherry_table_kernel<20, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+    else cherry_table_kernel<20, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
   } else if (S == 64) {
-    if (sc) cherry_table_kernel<64, true><<<grid, 64, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
-    else cherry_table_kernel<64, false><<<grid, 64, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+    if (sc) cherry_table_kernel<64, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+    else cherry_table_kernel<64, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
   } else {
     return fail(h, PLK_ERR_UNSUPPORTED, "cherry tables for %d states", S);
   }

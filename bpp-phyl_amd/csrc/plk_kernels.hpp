@@ -574,8 +574,44 @@ __global__ __launch_bounds__(256) void pmat64_kernel(PmatArgs a, const PmatInlin
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int x = xb + u, y = yb + 16 * v;
-      out[x * S + y] = tt == 0.0 ? (x == y ? 1.0 : 0.0) : p[u][v];  // getPij_t: t == 0 -> identity
+      p[u][v] = tt == 0.0 ? (x == y ? 1.0 : 0.0) : p[u][v];  // getPij_t: t == 0 -> identity
+      out[x * S + y] = p[u][v];
     }
+  // tip branch: its tip table (tip_table64_kernel's arithmetic) from the P just formed
+  if (a.init && b < a.n_tips) {
+    __syncthreads();  // done with Vm / Vi
+    double* Pl = Vm;  // [x][y]
+    double* In = Vi;  // [code][y], n_codes <= 64 (launch guarantees)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) Pl[(xb + u) * S + yb + 16 * v] = p[u][v];
+    for (int k = threadIdx.x; k < a.n_codes * S; k += blockDim.x) In[k] = a.init[k];
+    __syncthreads();
+    double* tout = a.tipP + ((size_t)b * a.C + c) * a.n_codes * S;
+    const int xq = 4 * (threadIdx.x & 15), cb = 4 * (threadIdx.x >> 4);
+    double t[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) t[u][v] = 0.0;
+    for (int y = 0; y < S; ++y) {
+      double px[4], iv[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) px[v] = Pl[(xq + v) * S + y];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) iv[u] = cb + u < a.n_codes ? In[(cb + u) * S + y] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) t[u][v] = __builtin_fma(px[v], iv[u], t[u][v]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (cb + u < a.n_codes)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) tout[(cb + u) * S + xq + v] = t[u][v];
+  }
 }
 
 // tip tables for 64 states: tip_table_kernel's sums (y ascending) with P and the code

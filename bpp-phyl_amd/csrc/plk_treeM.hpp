@@ -109,17 +109,24 @@ __global__ __launch_bounds__(256) void cherry_codes_kernel(const uint8_t* __rest
   out[i] = (uint16_t)(ca * U + cb);
 }
 
-// One wave per 16 code pairs (rows) of one cherry and class: blockIdx.x = row block,
-// blockIdx.y = cherry * C + class.  cherry_tips[3k .. 3k+2] = tip a, tip b, cherry node.
+// Four waves per block, one per 16 code pairs (rows) of one cherry and class: blockIdx.x =
+// 64-row block, blockIdx.y = cherry * C + class; P^T of the cherry branch is staged in LDS.
+// cherry3[3k .. 3k+2] = tip a, tip b, cherry node.
 template <int S, bool SCALE>
-__global__ __launch_bounds__(64) void cherry_table_kernel(const double* __restrict__ tipP,
-                                                          const double* __restrict__ pmatsT,
-                                                          const int32_t* __restrict__ cherry3, int C, int U,
-                                                          CherryLayout lay, uint8_t* __restrict__ cherry) {
+__global__ __launch_bounds__(256) void cherry_table_kernel(const double* __restrict__ tipP,
+                                                           const double* __restrict__ pmatsT,
+                                                           const int32_t* __restrict__ cherry3, int C, int U,
+                                                           CherryLayout lay, uint8_t* __restrict__ cherry) {
   constexpr int XT = MShape<S>::XT;
-  const int lane = threadIdx.x, lr = lane >> 4, lc = lane & 15;
+  __shared__ double PTl[S * S];
+  const int lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
   const int k = blockIdx.y / C, c = blockIdx.y % C, U2 = U * U;
-  const int r = blockIdx.x * 16 + lc;  // this lane's row (code pair)
+  {
+    const double* PT = pmatsT + ((size_t)cherry3[3 * k + 2] * C + c) * S * S;
+    for (int i = threadIdx.x; i < S * S; i += blockDim.x) PTl[i] = PT[i];
+    __syncthreads();
+  }
+  const int r = blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + lc;  // this lane's row (code pair)
   const bool rv = r < U2;
   const int ca = rv ? r / U : 0, cb = rv ? r % U : 0;
   const int ta = cherry3[3 * k], tb = cherry3[3 * k + 1], node = cherry3[3 * k + 2];
@@ -150,7 +157,8 @@ __global__ __launch_bounds__(64) void cherry_table_kernel(const double* __restri
     cnt = 1;
   }
   f64x4m d[XT];
-  matvec_m<S>(d, acc, pmatsT + ((size_t)node * C + c) * S * S, lr, lc);
+  (void)node;
+  matvec_m<S>(d, acc, PTl, lr, lc);
   uint8_t* base = cherry + (size_t)k * lay.stride;
   if (rv) {
     double* row = reinterpret_cast<double*>(base) + ((size_t)c * U2 + r) * S;
