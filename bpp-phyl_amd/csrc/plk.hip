@@ -12,6 +12,7 @@
 #include "plk_treeS.hpp"
 #include "plk_treeM.hpp"
 #include "plk_jit.hpp"
+#include "plk_dr.hpp"
 
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
@@ -171,6 +172,19 @@ struct plk_handle_s {
   KOpL* d_opsl = nullptr;
   size_t d_opsl_cap = 0;
   int64_t cmp_work = 0;                               // sum over nodes of distinct patterns
+  // tree of the traversals so far: sons per node, merged over plk_update_partials calls
+  // (an incremental call lists only the ancestors of changed branches)
+  std::vector<std::vector<int> > topo_kids;
+  // double-recursive derivatives (PLK_FLAG_DOUBLE_RECURSIVE, plk_dr.hpp)
+  int n_mats = 0;        // transition-matrix slots: nodes, 2 derivative scratch, DR M_f per node
+  int dr_slot0 = 0;      // partial slot of U_v = dr_slot0 + v
+  DrBranch* d_drb = nullptr;
+  size_t d_drb_cap = 0;
+  int2* d_drm = nullptr;
+  size_t d_drm_cap = 0;
+  double* dr_blk = nullptr;
+  size_t dr_blk_cap = 0;
+  double* dr_out = nullptr;
 };
 
 namespace {
@@ -325,7 +339,7 @@ void launch_generic_S(plk_handle h, const KOp* d_ops, int n_ops, const PartialsA
 // refreshed lazily after any P(t) change.
 int ensure_pmatsT(plk_handle h) {
   if (!h->pmatsT) {
-    int rc = dalloc(h, (void**)&h->pmatsT, (size_t)(h->n_nodes + 2) * h->C * h->S * h->S * sizeof(double));
+    int rc = dalloc(h, (void**)&h->pmatsT, (size_t)h->n_mats * h->C * h->S * h->S * sizeof(double));
     if (rc) return rc;
     h->pmatsT_dirty = true;
   }
@@ -448,6 +462,8 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   *out = nullptr;
   if (n_states < 2 || n_states > 64) return fail(nullptr, PLK_ERR_UNSUPPORTED, "n_states %d not in [2, 64]", n_states);
   if (n_classes < 1 || n_classes > 16) return fail(nullptr, PLK_ERR_UNSUPPORTED, "n_classes %d not in [1, 16]", n_classes);
+  if ((flags & PLK_FLAG_SUBTREE_PATTERNS) && (flags & PLK_FLAG_DOUBLE_RECURSIVE))
+    return fail(nullptr, PLK_ERR_UNSUPPORTED, "double-recursive derivatives read full-length partials (no pattern compression)");
   if ((flags & PLK_FLAG_SUBTREE_PATTERNS) && !(n_states == 4 && s4_supported(n_classes)))
     return fail(nullptr, PLK_ERR_UNSUPPORTED, "per-subtree pattern compression needs 4 states and C in {1, 2, 4, 8}");
   if (n_patterns < 1 || n_tips < 0 || n_internal < 1 || n_models < 1)
@@ -478,6 +494,11 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   h->n_pad = (int64_t)h->n_tiles * kTile;
   h->n_blocks = (int)((n_patterns + kRootBlock - 1) / kRootBlock);
   h->slot_stride = (int64_t)h->n_tiles * n_classes * n_states * kTile;
+  const bool dr = (flags & PLK_FLAG_DOUBLE_RECURSIVE) != 0;
+  h->n_mats = h->n_nodes + 2 + (dr ? h->n_nodes : 0);
+  h->dr_slot0 = n_internal + kDerivScratch;
+  const int n_slots = n_internal + kDerivScratch + (dr ? h->n_nodes : 0);
+  h->topo_kids.assign(h->n_nodes, std::vector<int>());
   h->pmat_valid.assign(h->n_nodes, 0);
   h->eigen_set.assign(n_models, 0);
   h->tip_set.assign(n_tips, 0);
@@ -491,15 +512,14 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
     return bail(fail(nullptr, PLK_ERR_DEVICE, "hipStreamCreate failed"));
   const size_t S2 = (size_t)n_states * n_states;
   // kDerivScratch extra slots / scale rows, 2 extra tip rows and 2 extra transition
-  // matrices: scratch for the path derivatives of plk_branch_derivatives (S != 4 path)
-  if ((rc = dalloc(h, (void**)&h->partials, (size_t)(n_internal + kDerivScratch) * h->slot_stride * sizeof(double))))
-    return bail(rc);
+  // matrices: scratch for the path derivatives of plk_branch_derivatives (S != 4 path);
+  // with PLK_FLAG_DOUBLE_RECURSIVE one more slot and matrix per node (U_v, M_f)
+  if ((rc = dalloc(h, (void**)&h->partials, (size_t)n_slots * h->slot_stride * sizeof(double)))) return bail(rc);
   if (flags & PLK_FLAG_SCALING) {
-    if ((rc = dalloc(h, (void**)&h->scale, (size_t)(n_internal + kDerivScratch) * h->n_pad * sizeof(int32_t))))
-      return bail(rc);
+    if ((rc = dalloc(h, (void**)&h->scale, (size_t)n_slots * h->n_pad * sizeof(int32_t)))) return bail(rc);
   }
   if ((rc = dalloc(h, (void**)&h->codes, (size_t)(n_tips + 2) * h->n_pad))) return bail(rc);
-  if ((rc = dalloc(h, (void**)&h->pmats, (size_t)(h->n_nodes + 2) * n_classes * S2 * sizeof(double)))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->pmats, (size_t)h->n_mats * n_classes * S2 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->V, (size_t)n_models * S2 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->Vinv, (size_t)n_models * S2 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->lambda, (size_t)n_models * n_states * sizeof(double)))) return bail(rc);
@@ -536,7 +556,7 @@ int plk_destroy(plk_handle h) {
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
-                  h->d_cherry_tips, h->d_cherry};
+                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) hipHostFree(h->h_req);
@@ -1986,6 +2006,202 @@ int materialize_last_traversal(plk_handle h) {
   return rc;
 }
 
+// Postorder op list of the merged topology below `root` (<= 3 children per op; a
+// polytomy continues with ACCUMULATE ops), as the host would hand it over.
+void topo_postorder(plk_handle h, int root, std::vector<plk_op>& ops) {
+  std::vector<std::pair<int, size_t> > st(1, std::make_pair(root, (size_t)0));
+  while (!st.empty()) {
+    const int n = st.back().first;
+    const std::vector<int>& ks = h->topo_kids[n];
+    if (st.back().second < ks.size()) {
+      const int c = ks[st.back().second++];
+      if (c >= h->n_tips) st.push_back(std::make_pair(c, (size_t)0));
+      continue;
+    }
+    for (size_t k0 = 0; k0 < ks.size(); k0 += 3) {
+      plk_op o;
+      std::memset(&o, 0, sizeof(o));
+      o.parent = n;
+      o.flags = k0 == 0 ? 0 : PLK_OP_ACCUMULATE;
+      for (size_t k = k0; k < ks.size() && k < k0 + 3; ++k) o.child[o.n_children++] = ks[k];
+      ops.push_back(o);
+    }
+    st.pop_back();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Double-recursive derivatives of every branch (plk_dr.hpp; row f4):
+// DRHomogeneousTreeLikelihood::computeSubtreeLikelihoodPrefix (:543-651) as a
+// levelwise preorder pass of ordinary partial updates into the U slots, then one
+// reduction launch over all branches (computeTreeDLikelihoods / D2 twins :287-423).
+// ---------------------------------------------------------------------------
+int dr_derivatives(plk_handle h, double* d1, double* d2) {
+  if (!(h->flags & PLK_FLAG_DOUBLE_RECURSIVE))
+    return fail(h, PLK_ERR_STATE, "handle was not created with PLK_FLAG_DOUBLE_RECURSIVE");
+  if (h->trav_ops.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet (plk_update_partials)");
+  if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
+  const int S = h->S, C = h->C, nt = h->n_tips, nn = h->n_nodes;
+  if (!(S == 2 || S == 3 || S == 4 || S == 20 || S == 64))
+    return fail(h, PLK_ERR_UNSUPPORTED, "state count %d has no kernel instance", S);
+  hipSetDevice(h->device);
+  std::vector<int> parent(nn, -1);
+  for (int n = 0; n < nn; ++n)
+    for (int c : h->topo_kids[n]) parent[c] = n;
+  int root = h->trav_ops.back().parent;
+  while (parent[root] >= 0) root = parent[root];
+  if (h->topo_kids[root].size() < 2) return fail(h, PLK_ERR_UNSUPPORTED, "root %d has fewer than two sons", root);
+  // preorder levels (depth 1 = sons of the root)
+  std::vector<std::vector<int> > depth(1, std::vector<int>(1, root));
+  while (true) {
+    std::vector<int> next;
+    for (int n : depth.back())
+      for (int c : h->topo_kids[n]) next.push_back(c);
+    if (next.empty()) break;
+    depth.push_back(next);
+  }
+  bool need = false;
+  for (size_t d = 0; d < depth.size(); ++d)
+    for (int v : depth[d]) {
+      if (d > 0 && (h->deriv_valid.empty() || !h->deriv_valid[v]))
+        return fail(h, PLK_ERR_STATE, "dP/d2P of branch %d not computed (PLK_DERIV_DP | PLK_DERIV_D2P)", v);
+      if (v >= nt && !h->materialized[v - nt]) need = true;
+    }
+  int rc;
+  if (need) {  // every L_v is read from HBM: materialise the whole tree once
+    std::vector<plk_op> ops;
+    topo_postorder(h, root, ops);
+    const unsigned saved = h->flags;
+    h->flags &= ~(unsigned)PLK_FLAG_LNL_ONLY;
+    rc = tree4_supported(h) && fusable(ops.data(), (int)ops.size()) ? update_tree4(h, ops.data(), (int)ops.size())
+                                                                    : update_levelwise(h, ops.data(), (int)ops.size());
+    h->flags = saved;
+    if (rc) return rc;
+  }
+  if ((rc = refresh_tip_tables(h))) return rc;
+  if ((S == 20 || S == 64) && (rc = ensure_pmatsT(h))) return rc;
+  // M_f for every internal father below the root
+  std::vector<int2> mlist;
+  for (size_t d = 1; d < depth.size(); ++d)
+    for (int f : depth[d])
+      if (f >= nt && !h->topo_kids[f].empty()) mlist.push_back(make_int2(f, parent[f] == root ? 1 : 0));
+  const int mat_base = nn + 2;
+  if (!mlist.empty()) {
+    if ((rc = ensure_cap(h, (void**)&h->d_drm, &h->d_drm_cap, mlist.size() * sizeof(int2)))) return rc;
+    HIPCHK(h, hipMemcpyAsync(h->d_drm, mlist.data(), mlist.size() * sizeof(int2), hipMemcpyHostToDevice, h->stream));
+    dr_matrix_kernel<<<dim3((unsigned)mlist.size(), C), 256, 0, h->stream>>>(
+        h->pmats, h->pmats, (S == 20 || S == 64) ? h->pmatsT : nullptr, h->pi, h->d_drm, mat_base, C, S);
+    HIPCHK(h, hipGetLastError());
+  }
+  // U_v for every non-root node, one launch per (depth, child chunk)
+  std::vector<KOp> flat;
+  std::vector<std::pair<size_t, int> > launches;
+  for (size_t d = 1; d < depth.size(); ++d) {
+    std::vector<std::vector<KOp> > chunks;
+    for (int v : depth[d]) {
+      const int f = parent[v];
+      std::vector<int> ck_tip, ck_child, ck_branch;
+      if (f != root) {
+        ck_tip.push_back(0);
+        ck_child.push_back(h->dr_slot0 + f);
+        ck_branch.push_back(mat_base + f);
+      }
+      for (int s : h->topo_kids[f])
+        if (s != v) {
+          ck_tip.push_back(s < nt);
+          ck_child.push_back(s < nt ? s : s - nt);
+          ck_branch.push_back(s);
+        }
+      for (size_t k0 = 0, j = 0; k0 < ck_tip.size(); k0 += 3, ++j) {
+        KOp op;
+        std::memset(&op, 0, sizeof(op));
+        op.parent = h->dr_slot0 + v;
+        op.flags = k0 == 0 ? 0 : PLK_OP_ACCUMULATE;
+        for (size_t k = k0; k < ck_tip.size() && k < k0 + 3; ++k) {
+          const int i = op.n++;
+          op.is_tip[i] = ck_tip[k];
+          op.child[i] = ck_child[k];
+          op.branch[i] = ck_branch[k];
+        }
+        if (chunks.size() <= j) chunks.resize(j + 1);
+        chunks[j].push_back(op);
+      }
+    }
+    for (auto& ch : chunks) {
+      launches.push_back(std::make_pair(flat.size(), (int)ch.size()));
+      flat.insert(flat.end(), ch.begin(), ch.end());
+    }
+  }
+  if ((rc = ensure_cap(h, (void**)&h->d_ops, &h->d_ops_cap, flat.size() * sizeof(KOp)))) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->d_ops, flat.data(), flat.size() * sizeof(KOp), hipMemcpyHostToDevice, h->stream));
+  h->last_ops.clear();  // d_ops now holds the preorder ops
+  for (auto& l : launches)
+    if ((rc = launch_partials_ops(h, h->d_ops + l.first, l.second))) return rc;
+  // all branches in one reduction launch
+  std::vector<DrBranch> br;
+  for (size_t d = 1; d < depth.size(); ++d)
+    for (int v : depth[d]) {
+      DrBranch b;
+      std::memset(&b, 0, sizeof(b));
+      b.node = v;
+      b.is_tip = v < nt;
+      b.child = v < nt ? v : v - nt;
+      b.uslot = h->dr_slot0 + v;
+      b.use_pi = parent[v] == root;
+      br.push_back(b);
+    }
+  const int n_blk = (int)(h->n_pad / kDrThreads);
+  if ((rc = ensure_cap(h, (void**)&h->d_drb, &h->d_drb_cap, br.size() * sizeof(DrBranch)))) return rc;
+  if ((rc = ensure_cap(h, (void**)&h->dr_blk, &h->dr_blk_cap, 2 * br.size() * n_blk * sizeof(double)))) return rc;
+  if (!h->dr_out && (rc = dalloc(h, (void**)&h->dr_out, 2 * (size_t)nn * sizeof(double)))) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->d_drb, br.data(), br.size() * sizeof(DrBranch), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->dr_out, 0, 2 * (size_t)nn * sizeof(double), h->stream));
+  DrArgs a;
+  a.partials = h->partials;
+  a.codes = h->codes;
+  a.code_table = h->code_table;
+  a.pmats = h->pmats;
+  a.dpmats = h->dpmats;
+  a.d2pmats = h->d2pmats;
+  a.pi = h->pi;
+  a.probs = h->probs;
+  a.weights = h->weights;
+  a.blk1 = h->dr_blk;
+  a.blk2 = h->dr_blk + br.size() * n_blk;
+  a.slot_stride = h->slot_stride;
+  a.n_pad = h->n_pad;
+  a.n_patterns = h->n_patterns;
+  a.C = C;
+  a.n_blk = n_blk;
+  const dim3 grid((unsigned)n_blk, (unsigned)br.size());
+  const size_t lds = 3 * (size_t)S * S * sizeof(double);
+  EventPair ev;
+  if (h->timing & PLK_TIME_PARTIALS) {
+    ev = get_events(h, 0);
+    hipEventRecord(ev.a, h->stream);
+  }
+  switch (S) {
+    case 2: dr_branch_kernel<2><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+    case 3: dr_branch_kernel<3><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+    case 4: dr_branch_kernel<4><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+    case 20: dr_branch_kernel<20><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+    case 64: dr_branch_kernel<64><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+  }
+  HIPCHK(h, hipGetLastError());
+  if (h->timing & PLK_TIME_PARTIALS) {
+    hipEventRecord(ev.b, h->stream);
+    h->events.push_back(ev);
+  }
+  dr_sum_kernel<<<(unsigned)br.size(), 256, 0, h->stream>>>(h->d_drb, a.blk1, a.blk2, n_blk, h->dr_out, h->dr_out + nn);
+  HIPCHK(h, hipGetLastError());
+  std::vector<double> out(2 * (size_t)nn);
+  HIPCHK(h, hipMemcpyAsync(out.data(), h->dr_out, out.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (d1) std::copy(out.begin(), out.begin() + nn, d1);
+  if (d2) std::copy(out.begin() + nn, out.end(), d2);
+  return PLK_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1997,6 +2213,11 @@ int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
   int rc = validate_ops(h, ops, n_ops);
   if (rc) return rc;
   h->trav_ops.assign(ops, ops + n_ops);
+  for (int i = 0; i < n_ops; ++i) {
+    std::vector<int>& k = h->topo_kids[ops[i].parent];
+    if (!(ops[i].flags & PLK_OP_ACCUMULATE)) k.clear();
+    k.insert(k.end(), ops[i].child, ops[i].child + ops[i].n_children);
+  }
   if (h->flags & PLK_FLAG_SUBTREE_PATTERNS) return update_compressed(h, ops, n_ops);
   if (tree4_supported(h) && fusable(ops, n_ops)) return update_tree4(h, ops, n_ops);
   return update_levelwise(h, ops, n_ops);
@@ -2234,6 +2455,11 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
   rc = plk_update_partials(h, ops, n_ops);
   if (rc) return rc;
   return plk_root_loglik(h, root, lnl, nullptr, block_sums);
+}
+
+int plk_all_branch_derivatives(plk_handle h, double* d1, double* d2) {
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  return dr_derivatives(h, d1, d2);
 }
 
 const char* plk_kernel_path(plk_handle h) { return h ? h->kernel_path.c_str() : ""; }

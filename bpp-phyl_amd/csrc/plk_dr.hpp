@@ -1,0 +1,189 @@
+// plk_dr.hpp -- double-recursive (DR) branch derivatives: every branch of the tree
+// from one preorder pass (row f4 of SURVEY 8(f)).
+//
+// The reference's DRHomogeneousTreeLikelihood keeps, for every node, the likelihood
+// arrays of each neighbour direction (computeSubtreeLikelihoodPostfix / Prefix,
+// Likelihood/DRHomogeneousTreeLikelihood.cpp:483-651) and forms the derivative of a
+// branch from the two arrays on either side of it (computeTreeDLikelihoodAtNode
+// :287-328, computeTreeD2LikelihoodAtNode :373-413).  Here the father-side array of
+// branch v is the "upper" vector
+//     U_v[c][y] = (M_f U_f)[c][y] * prod_{siblings s of v} (P_s L_s)[c][y]
+// at v's father f (y = state at f), with M_f = P_f^T for an ordinary father and
+// M_f = P_f^T diag(pi) for a child of the root (whose own upper vector leaves pi out;
+// pi enters the branch reduction instead).  U_v is produced by the ordinary partial
+// kernels (plk_kernels.hpp et al.): it is a product of children, U_f being a child
+// whose "transition matrix" is M_f -- so the preorder pass reuses the levelwise S=4,
+// S=20 (SGPR) and S=64 (MFMA) paths as they are, rescaling included.
+//
+// Per branch and pattern the reduction below forms
+//     l = sum_c p_c sum_y u[c][y] (P_v L_v)[c][y],   u = U_v (x pi at the root's children)
+// and l', l'' with r_c dP_v and r_c^2 d2P_v in place of P_v (lnL is linear in P_v), then
+// d1 += w l'/l and d2 += w (l''/l - (l'/l)^2).  Power-of-two scale counts of U_v and
+// L_v multiply l, l', l'' alike, so the ratios need no scale bookkeeping.
+#pragma once
+
+#include "plk_kernels.hpp"
+
+namespace plk {
+
+// M_f of one father f and class c: dst[f][c][y][w] = P_f[c][w][y] * (use_pi ? pi_w : 1),
+// and its transpose (the P^T copy the MFMA kernels read) when dstT is given.
+__global__ __launch_bounds__(256) void dr_matrix_kernel(const double* __restrict__ pmats, double* __restrict__ dst,
+                                                        double* __restrict__ dstT, const double* __restrict__ pi,
+                                                        const int2* __restrict__ list, int dst_base, int C, int S) {
+  const int2 e = list[blockIdx.x];
+  const int c = blockIdx.y;
+  const int SS = S * S;
+  const double* P = pmats + ((size_t)e.x * C + c) * SS;
+  const size_t o = ((size_t)(dst_base + e.x) * C + c) * SS;
+  for (int i = threadIdx.x; i < SS; i += blockDim.x) {
+    const int y = i / S, w = i - y * S;
+    const double v = e.y ? P[w * S + y] * pi[w] : P[w * S + y];
+    dst[o + i] = v;
+    if (dstT) dstT[o + (size_t)w * S + y] = v;
+  }
+}
+
+struct DrBranch {
+  int32_t node;    // branch = child node index (P, dP, d2P index)
+  int32_t is_tip;  // L_v from the tip's codes
+  int32_t child;   // tip index or internal slot of v
+  int32_t uslot;   // slot of U_v
+  int32_t use_pi;  // v is a child of the root
+  int32_t pad_[3];
+};
+
+struct DrArgs {
+  const double* partials;
+  const uint8_t* codes;       // compact codes [tip][n_pad]
+  const double* code_table;   // compact table [n_codes][S]
+  const double* pmats;
+  const double* dpmats;
+  const double* d2pmats;
+  const double* pi;
+  const double* probs;
+  const double* weights;
+  double* blk1;               // [branch][n_blk] block sums of w l'/l
+  double* blk2;               // [branch][n_blk] block sums of w (l''/l - (l'/l)^2)
+  int64_t slot_stride;
+  int64_t n_pad;
+  int64_t n_patterns;
+  int32_t C;
+  int32_t n_blk;
+};
+
+constexpr int kDrThreads = 256;
+
+// One workgroup = 256 patterns of one branch.  P_v, dP_v, d2P_v of the current class
+// are staged in LDS (3 S^2 doubles, read as wave-wide broadcasts); L_v of the lane's
+// pattern sits in registers; U_v is read once per (class, state), coalesced.
+template <int S>
+__global__ __launch_bounds__(kDrThreads) void dr_branch_kernel(const DrBranch* __restrict__ branches, DrArgs a) {
+  extern __shared__ double lds[];
+  double* sP = lds;
+  double* sD = lds + S * S;
+  double* sD2 = lds + 2 * S * S;
+  __shared__ double red[2][kDrThreads / 64];
+  const DrBranch b = branches[blockIdx.y];
+  const int64_t p = (int64_t)blockIdx.x * kDrThreads + threadIdx.x;
+  const bool live = p < a.n_patterns;
+  const int64_t tile = p >> 7, q = p & (kTile - 1);
+  const int CS = a.C * S;
+  double l0 = 0.0, l1 = 0.0, l2 = 0.0;
+  for (int c = 0; c < a.C; ++c) {
+    __syncthreads();
+    const size_t mo = ((size_t)b.node * a.C + c) * S * S;
+    for (int i = threadIdx.x; i < S * S; i += kDrThreads) {
+      sP[i] = a.pmats[mo + i];
+      sD[i] = a.dpmats[mo + i];
+      sD2[i] = a.d2pmats[mo + i];
+    }
+    __syncthreads();
+    if (live) {
+      double L[S];
+      if (b.is_tip) {
+        const double* row = a.code_table + (size_t)a.codes[(size_t)b.child * a.n_pad + p] * S;
+#pragma unroll
+        for (int z = 0; z < S; ++z) L[z] = row[z];
+      } else {
+        const double* src = a.partials + (size_t)b.child * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
+#pragma unroll
+        for (int z = 0; z < S; ++z) L[z] = src[(size_t)z * kTile];
+      }
+      const double* U = a.partials + (size_t)b.uslot * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+      for (int y = 0; y < S; ++y) {
+        double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+#pragma unroll
+        for (int z = 0; z < S; ++z) {
+          t0 = fma(sP[y * S + z], L[z], t0);
+          t1 = fma(sD[y * S + z], L[z], t1);
+          t2 = fma(sD2[y * S + z], L[z], t2);
+        }
+        const double u = b.use_pi ? U[(size_t)y * kTile] * a.pi[y] : U[(size_t)y * kTile];
+        s0 = fma(u, t0, s0);
+        s1 = fma(u, t1, s1);
+        s2 = fma(u, t2, s2);
+      }
+      l0 = fma(a.probs[c], s0, l0);
+      l1 = fma(a.probs[c], s1, l1);
+      l2 = fma(a.probs[c], s2, l2);
+    }
+  }
+  double r1 = 0.0, r2 = 0.0;
+  if (live) {
+    const double g = l1 / l0, hh = l2 / l0;
+    r1 = a.weights[p] * g;
+    r2 = a.weights[p] * (hh - g * g);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    r1 += __shfl_xor(r1, off, 64);
+    r2 += __shfl_xor(r2, off, 64);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wv] = r1;
+    red[1][wv] = r2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < kDrThreads / 64; ++k) {  // fixed order
+      t1 += red[0][k];
+      t2 += red[1][k];
+    }
+    a.blk1[(size_t)blockIdx.y * a.n_blk + blockIdx.x] = t1;
+    a.blk2[(size_t)blockIdx.y * a.n_blk + blockIdx.x] = t2;
+  }
+}
+
+// Per branch: the fixed-order sum of its block sums (strided partial sums, then a
+// fixed LDS tree), written to out1/out2[node].
+__global__ __launch_bounds__(256) void dr_sum_kernel(const DrBranch* __restrict__ branches, const double* __restrict__ blk1,
+                                                     const double* __restrict__ blk2, int n_blk, double* __restrict__ out1,
+                                                     double* __restrict__ out2) {
+  __shared__ double s1[256], s2[256];
+  const size_t o = (size_t)blockIdx.x * n_blk;
+  double t1 = 0.0, t2 = 0.0;
+  for (int i = threadIdx.x; i < n_blk; i += 256) {
+    t1 += blk1[o + i];
+    t2 += blk2[o + i];
+  }
+  s1[threadIdx.x] = t1;
+  s2[threadIdx.x] = t2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      s1[threadIdx.x] += s1[threadIdx.x + w];
+      s2[threadIdx.x] += s2[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out1[branches[blockIdx.x].node] = s1[0];
+    out2[branches[blockIdx.x].node] = s2[0];
+  }
+}
+
+}  // namespace plk

@@ -75,6 +75,11 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   bool scaling_ = true;
   bool incremental_ = true;
   bool derivFirst_ = true, derivSecond_ = true;
+  unsigned extraFlags_ = 0;                  // plk_create flags of the subclass (PLK_FLAG_DOUBLE_RECURSIVE)
+  // double-recursive derivative cache: every branch from one plk_all_branch_derivatives call,
+  // valid until the next traversal (indexed by engine node)
+  mutable std::vector<double> drD1_, drD2_;
+  mutable bool drValid_ = false;
   double minimumBrLen_ = 0.000001, maximumBrLen_ = 10000.;
   std::shared_ptr<IntervalConstraint> brLenConstraint_;
   ParameterList brLenParameters_;
@@ -158,6 +163,19 @@ class RHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
   const SubstitutionModel* getModel() const { return model_; }
   SubstitutionModel* getModel() { return model_; }
   void computeAllTransitionProbabilities();
+};
+
+// Likelihood/DRHomogeneousTreeLikelihood.h: same likelihood, derivatives of all branches
+// from one double-recursive pass on the device (plk_all_branch_derivatives) instead of one
+// path traversal per branch; getFirstOrderDerivative / getSecondOrderDerivative then read
+// the per-branch values computed after the last parameter change
+// (DRHomogeneousTreeLikelihood.cpp:287-456).
+class DRHomogeneousTreeLikelihood : public RHomogeneousTreeLikelihood {
+ public:
+  DRHomogeneousTreeLikelihood(const Tree& tree, SubstitutionModel* model, DiscreteDistribution* rDist,
+                              bool checkRooted = true, bool verbose = true);
+  DRHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data, SubstitutionModel* model,
+                              DiscreteDistribution* rDist, bool checkRooted = true, bool verbose = true);
 };
 
 class RNonHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {

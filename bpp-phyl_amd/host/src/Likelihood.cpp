@@ -133,7 +133,8 @@ void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
     plk_destroy(engine_);
     engine_ = nullptr;
   }
-  unsigned flags = (scaling_ ? (unsigned)PLK_FLAG_SCALING : 0u) | (nonNegGuard ? (unsigned)PLK_FLAG_NONNEG_GUARD : 0u);
+  unsigned flags = (scaling_ ? (unsigned)PLK_FLAG_SCALING : 0u) | (nonNegGuard ? (unsigned)PLK_FLAG_NONNEG_GUARD : 0u) |
+                   extraFlags_;
   plk_handle h = nullptr;
   int rc = plk_create(deviceFromEnv(), (int)nbStates_, (int)nbClasses_, (int64_t)nbDistinctSites_, nTips_, nInternal_,
                       (int)nModels, flags, &h);
@@ -230,6 +231,7 @@ void AbstractPlkTreeLikelihood::computeTreeLikelihood(const std::vector<const No
     for (size_t k = 0; k < 3; k++) o.child[k] = k < opChildren_[i].size() ? opChildren_[i][k] : -1;
     o.flags = opFlags_[i];
   }
+  drValid_ = false;
   if (ops.empty()) {
     siteLnlValid_ = false;
     return;
@@ -308,6 +310,18 @@ VVVdouble AbstractPlkTreeLikelihood::getLikelihoodArray(int nodeId) const {
 bool AbstractPlkTreeLikelihood::analyticDerivatives(const std::string& variable, double* d1, double* d2) const {
   if (!(derivFirst_ || derivSecond_)) return false;
   const Node* n = nodes_.at(TextTools::to<size_t>(variable.substr(5)));
+  if (extraFlags_ & PLK_FLAG_DOUBLE_RECURSIVE) {
+    if (!drValid_) {
+      const size_t nn = (size_t)(nTips_ + nInternal_);
+      drD1_.assign(nn, 0.);
+      drD2_.assign(nn, 0.);
+      check(plk_all_branch_derivatives(engine_, drD1_.data(), drD2_.data()), "plk_all_branch_derivatives");
+      drValid_ = true;
+    }
+    *d1 = drD1_[(size_t)engineIndex_.at(n)];
+    *d2 = drD2_[(size_t)engineIndex_.at(n)];
+    return true;
+  }
   const int rc = plk_branch_derivatives(engine_, engineIndex_.at(n), d1, d2);
   if (rc == PLK_ERR_UNSUPPORTED) return false;
   check(rc, "plk_branch_derivatives");
@@ -449,6 +463,24 @@ void RHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList& param
   }
   computeTreeLikelihood();
   minusLogLik_ = -reduceRoot();
+}
+
+// ---------------------------------------------------------------------------
+// DRHomogeneousTreeLikelihood (Likelihood/DRHomogeneousTreeLikelihood.h): the engine keeps
+// an upper vector per branch (PLK_FLAG_DOUBLE_RECURSIVE)
+// ---------------------------------------------------------------------------
+
+DRHomogeneousTreeLikelihood::DRHomogeneousTreeLikelihood(const Tree& tree, SubstitutionModel* model,
+                                                         DiscreteDistribution* rDist, bool checkRooted, bool verbose)
+    : RHomogeneousTreeLikelihood(tree, model, rDist, checkRooted, verbose, true) {
+  extraFlags_ = PLK_FLAG_DOUBLE_RECURSIVE;
+}
+
+DRHomogeneousTreeLikelihood::DRHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data,
+                                                         SubstitutionModel* model, DiscreteDistribution* rDist,
+                                                         bool checkRooted, bool verbose)
+    : DRHomogeneousTreeLikelihood(tree, model, rDist, checkRooted, verbose) {
+  setData(data);
 }
 
 // ---------------------------------------------------------------------------

@@ -22,6 +22,7 @@ PLK_FLAG_NONNEG_GUARD = 2
 PLK_FLAG_LNL_ONLY = 4
 PLK_FLAG_LEVELWISE = 8
 PLK_FLAG_SUBTREE_PATTERNS = 16
+PLK_FLAG_DOUBLE_RECURSIVE = 32
 PLK_DERIV_P, PLK_DERIV_DP, PLK_DERIV_D2P = 1, 2, 4
 PLK_OP_ACCUMULATE = 1
 PLK_TIME_PARTIALS, PLK_TIME_PMAT, PLK_TIME_ROOT = 1, 2, 4
@@ -33,7 +34,7 @@ EXPORTS = [
     "plk_set_root_frequencies", "plk_set_eigen", "plk_update_pmatrices", "plk_set_pmatrix",
     "plk_get_pmatrix", "plk_update_partials", "plk_get_partials", "plk_root_loglik", "plk_block_size",
     "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
-    "plk_kernel_path", "plk_evaluate", "plk_compressed_work",
+    "plk_kernel_path", "plk_evaluate", "plk_compressed_work", "plk_all_branch_derivatives",
 ]
 
 
@@ -85,6 +86,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_reset_timing": ([ct.c_void_p], ct.c_int),
         "plk_synchronize": ([ct.c_void_p], ct.c_int),
         "plk_branch_derivatives": ([ct.c_void_p, ct.c_int, dp, dp], ct.c_int),
+        "plk_all_branch_derivatives": ([ct.c_void_p, dp, dp], ct.c_int),
         "plk_kernel_path": ([ct.c_void_p], ct.c_char_p),
         "plk_compressed_work": ([ct.c_void_p, P(ct.c_int64)], ct.c_int),
         "plk_evaluate": ([ct.c_void_p, ct.c_int, ip, ip, dp, P(plk_op), ct.c_int, ct.c_int, dp, dp], ct.c_int),
@@ -249,6 +251,14 @@ class Engine:
         d1, d2 = ct.c_double(0), ct.c_double(0)
         self._chk(self.lib.plk_branch_derivatives(self.h, branch, ct.byref(d1), ct.byref(d2)))
         return d1.value, d2.value
+
+    def all_branch_derivatives(self):
+        """Double-recursive pass (PLK_FLAG_DOUBLE_RECURSIVE): (d1, d2) arrays indexed by
+        node, d lnL/dt and d2 lnL/dt2 of every branch of the last traversal (0 at the root)."""
+        n = self.n_tips + self.n_internal
+        d1, d2 = np.zeros(n), np.zeros(n)
+        self._chk(self.lib.plk_all_branch_derivatives(self.h, _d(d1), _d(d2)))
+        return d1, d2
 
     def set_timing(self, on: bool):
         self._chk(self.lib.plk_set_timing(self.h, (PLK_TIME_PARTIALS | PLK_TIME_PMAT | PLK_TIME_ROOT) if on is True

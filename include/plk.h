@@ -86,7 +86,12 @@ enum {
                                     its subtree and read through pattern links.  Links are
                                     built on the host from the tip codes and the op list (all
                                     internal children must be produced by the same call);
-                                    4-state models only */
+                                    4-state models only */,
+  PLK_FLAG_DOUBLE_RECURSIVE = 1u << 5 /* DRHomogeneousTreeLikelihood: keep one "upper" conditional
+                                    likelihood per branch (the reference's father-side arrays,
+                                    DRHomogeneousTreeLikelihood.cpp:543-651) so that
+                                    plk_all_branch_derivatives serves every branch from one
+                                    preorder pass; n_nodes extra partial slots in HBM */
 };
 
 /* plk_update_pmatrices deriv_mask */
@@ -167,6 +172,19 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
  * PLK_FLAG_SUBTREE_PATTERNS. */
 int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2);
 int plk_block_size(void);
+
+/* Double-recursive derivatives (handle created with PLK_FLAG_DOUBLE_RECURSIVE): d lnL/dt and
+ * d2 lnL/dt2 for EVERY branch of the last plk_update_partials tree, written to d1[node] and
+ * d2[node] (n_nodes entries each, 0 at the root).  One preorder pass computes each branch's
+ * upper vector U_v (everything outside v's subtree, conditional on the state at v's father,
+ * root frequencies folded in), then per branch and pattern
+ *   l = sum_c p_c sum_y U_v[c][y] (P_v L_v)[c][y],  l' and l'' with r_c dP_v and r_c^2 d2P_v,
+ *   d1 += w l'/l,  d2 += w (l''/l - (l'/l)^2).
+ * Replaces DRHomogeneousTreeLikelihood::computeSubtreeLikelihoodPrefix (:543-651),
+ * computeTreeDLikelihoodAtNode / computeTreeDLikelihoods (:287-338) and the D2 twins
+ * (:373-423).  Requires dP and d2P of every branch.  Any state count the partial kernels
+ * support; not with PLK_FLAG_SUBTREE_PATTERNS. */
+int plk_all_branch_derivatives(plk_handle h, double* d1, double* d2);
 
 /* Instrumentation: HIP-event timing on the handle's stream of the kernels selected
  * by the mask given to plk_set_timing (0 = off).  Each timed launch adds an event

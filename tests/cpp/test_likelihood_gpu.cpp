@@ -4,6 +4,7 @@
 // initialize / getValue, optimizeTreeScale + optimizeNumericalParameters2), checked
 // against the goldens those tests hold.  Exit code 0 = pass (reference convention).
 #include <Bpp/Numeric/Prob/GammaDiscreteDistribution.h>
+#include <Bpp/Phyl/Likelihood/DRHomogeneousTreeLikelihood.h>
 #include <Bpp/Phyl/Likelihood/RHomogeneousTreeLikelihood.h>
 #include <Bpp/Phyl/Model/Nucleotide/T92.h>
 #include <Bpp/Phyl/Model/RateDistribution/GammaDiscreteRateDistribution.h>
@@ -111,6 +112,40 @@ static void rootedConstantCase() {
   expectNear("T92 rooted clock-optimised -lnL", tl.getValue(), 71.2657, 1e-3);
 }
 
+// test/test_likelihood.cpp:111-135: fitModelHDR with the double-recursive class (same
+// goldens), then the R-vs-DR first-derivative comparison at 1e-6 on every branch
+static void doubleRecursiveCase() {
+  std::unique_ptr<TreeTemplate<Node> > tree(
+      TreeTemplateTools::parenthesisToTree("((A:0.01, B:0.02):0.03,C:0.01,D:0.1);"));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  const char* names[] = {"A", "B", "C", "D"};
+  const char* seqs[] = {"AAATGGCTGTGCACGTC", "GACTGGATCTGCACGTC", "CTCTGGATGTGCACGTG", "AAATGGCGGTGCGCCTA"};
+  for (int i = 0; i < 4; i++) aln.addSequence(BasicSequence(names[i], seqs[i], dna));
+  {
+    T92 model(dna, 3.);
+    GammaDiscreteRateDistribution rdist(4, 1.0);
+    DRHomogeneousTreeLikelihood tl(*tree, aln, &model, &rdist, true, false);
+    tl.initialize();
+    expectNear("DR T92+G4 initial -lnL", tl.getValue(), 85.030942031997312824, 1e-9);
+    OptimizationTools::optimizeTreeScale(&tl);
+    OptimizationTools::optimizeNumericalParameters2(&tl, tl.getParameters(), 0, 0.000001, 10000, 0, 0);
+    expectNear("DR T92+G4 optimised -lnL", tl.getValue(), 65.72293577214308868406, 1e-3);
+  }
+  T92 model(dna, 3.);
+  GammaDiscreteRateDistribution rdist(4, 1.0);
+  RHomogeneousTreeLikelihood tlsr(*tree, aln, &model, &rdist, true, false);
+  tlsr.initialize();
+  DRHomogeneousTreeLikelihood tldr(*tree, aln, &model, &rdist, true, false);
+  tldr.initialize();
+  for (const std::string& name : tlsr.getBranchLengthsParameters().getParameterNames()) {
+    expectNear((std::string("R vs DR d1 ") + name).c_str(), tldr.getFirstOrderDerivative(name),
+               tlsr.getFirstOrderDerivative(name), 1e-6);
+    expectNear((std::string("R vs DR d2 ") + name).c_str(), tldr.getSecondOrderDerivative(name),
+               tlsr.getSecondOrderDerivative(name), 1e-6);
+  }
+}
+
 // gaps are not allowed by the model: BadIntException like getInitValue
 static void gapCase() {
   std::unique_ptr<TreeTemplate<Node> > tree(TreeTemplateTools::parenthesisToTree("((A:0.1,B:0.2):0.1,C:0.3);"));
@@ -135,6 +170,7 @@ int main() {
   try {
     unrootedGammaCase();
     rootedConstantCase();
+    doubleRecursiveCase();
     gapCase();
   } catch (Exception& e) {
     std::cerr << e.what() << std::endl;

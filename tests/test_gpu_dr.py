@@ -1,0 +1,170 @@
+"""Row f4: double-recursive derivatives of every branch (plk_all_branch_derivatives,
+PLK_FLAG_DOUBLE_RECURSIVE) -- the reference's DRHomogeneousTreeLikelihood
+(Likelihood/DRHomogeneousTreeLikelihood.cpp:287-423, 543-651).
+
+Checked against
+  - the single-traversal path derivatives of the same engine (plk_branch_derivatives,
+    themselves checked against central differences of the oracle in test_gpu_parity.py):
+    relative 1e-10 on d1 and d2 (the reference's own R-vs-DR check is 1e-6 absolute,
+    test/test_likelihood.cpp:122-135);
+  - central differences of the CPU oracle for a few branches.
+"""
+import numpy as np
+import pytest
+
+import phylo
+import plk
+import workload
+from test_gpu_parity import MODES, _caterpillar, _random_problem, engine_for, oracle_for, run_engine
+
+pytestmark = pytest.mark.gpu
+
+DR = plk.PLK_FLAG_DOUBLE_RECURSIVE
+
+
+def _close(a, b, rel):
+    return abs(a - b) <= rel * max(1.0, abs(a), abs(b))
+
+
+def _dr_vs_path(eng, et, rel=1e-10):
+    d1, d2 = eng.all_branch_derivatives()
+    assert d1[et.root] == 0.0 and d2[et.root] == 0.0
+    for b in range(et.n_nodes):
+        if b == et.root:
+            continue
+        p1, p2 = eng.branch_derivatives(b)
+        assert _close(d1[b], p1, rel), (b, d1[b], p1)
+        assert _close(d2[b], p2, rel), (b, d2[b], p2)
+    return d1, d2
+
+
+@pytest.mark.parametrize("S,C,mode,scaling,n_taxa,n_pat", [
+    (4, 4, "materialize", False, 16, 3000), (4, 1, "lnl_only", False, 9, 700), (4, 2, "levelwise", True, 12, 777),
+    (4, 8, "materialize", False, 10, 300), (20, 4, "lnl_only", False, 10, 500), (20, 2, "levelwise", True, 12, 400),
+    (64, 1, "lnl_only", False, 8, 300), (64, 2, "materialize", False, 6, 130), (4, 4, "lnl_only", False, 3, 1)])
+def test_dr_equals_path_derivatives(S, C, mode, scaling, n_taxa, n_pat):
+    et, m, alph, rates, probs, states = _random_problem(S, C, n_taxa, n_pat, seed=70 + S + C + n_taxa)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | DR | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, S, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    _dr_vs_path(eng, et)
+
+
+def test_dr_vs_oracle_finite_differences():
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 14, 900, seed=81)
+    eng = engine_for(et, 4, 4, 900, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | DR)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    d1, d2 = eng.all_branch_derivatives()
+    for b in (0, 3, et.n_tips, et.ops[0][0], br[-1]):
+        def lnl_at(t):
+            bl = et.brlen.copy()
+            bl[b] = t
+            e2 = phylo.EngineTree(et.n_tips, et.n_internal, et.root, et.tip_names, et.ops, bl, {}, [], [])
+            return oracle_for(e2, states, alph.init_table, rates, probs, m.pi, [m])[0]
+
+        t = et.brlen[b]
+        fd1 = (lnl_at(t + 1e-5) - lnl_at(t - 1e-5)) / 2e-5
+        fd2 = (lnl_at(t + 1e-4) - 2 * lnl_at(t) + lnl_at(t - 1e-4)) / 1e-8
+        assert abs(d1[b] - fd1) <= 1e-6 * max(1.0, abs(fd1)), (b, d1[b], fd1)
+        assert abs(d2[b] - fd2) <= 2e-4 * max(1.0, abs(fd2)), (b, d2[b], fd2)
+
+
+def test_dr_polytomy_and_deep_caterpillar():
+    # polytomies: U_v of a son of a 5-way node has 4 siblings + the father's U (ACCUMULATE chunks)
+    t = phylo.Tree.from_newick("((a:0.1,b:0.2,c:0.05,d:0.3,e:0.12):0.1,(f:0.2,g:0.1):0.05,h:0.3,i:0.2);")
+    et = phylo.engine_tree(t)
+    m = phylo.gtr(1.2, 0.4, 0.6, 0.8, 0.5, 0.3, 0.2, 0.25, 0.25)
+    rates, probs = phylo.gamma_rates(4, 0.5)
+    wl = workload.Workload("p", et, [m], None, rates, probs, m.pi, phylo.DNA, 1000, False, True, 9)
+    states = wl.simulate(0, 1000).astype(np.int32)
+    eng = engine_for(et, 4, 4, 1000, states, phylo.DNA.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | DR)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    _dr_vs_path(eng, et)
+    # a 300-taxon caterpillar drives the upper vectors through rescaling
+    tree = _caterpillar(300, lo=0.1, hi=0.4)
+    et = phylo.engine_tree(tree)
+    wl = workload.Workload("c", et, [m], None, rates, probs, m.pi, phylo.DNA, 600, False, True, 5)
+    states = wl.simulate(0, 600).astype(np.int32)
+    eng = engine_for(et, 4, 4, 600, states, phylo.DNA.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_SCALING | DR)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    lnl, _, _ = run_engine(eng, et)
+    assert lnl < -745 * 4
+    d1, d2 = _dr_vs_path(eng, et, rel=1e-9)
+    assert np.all(np.isfinite(d1)) and np.all(np.isfinite(d2))
+
+
+def test_dr_nonhomogeneous_rooted():
+    """NH trees stay rooted (2-son root); per-branch models."""
+    wl = workload.make_workload("nh_gtr_g4_dna_2M_512", n_patterns=1500)
+    et = wl.et
+    states = wl.simulate(0, 1500).astype(np.int32)
+    eng = engine_for(et, 4, 4, 1500, states, phylo.DNA.init_table, wl.rates, wl.probs, wl.root_freqs, wl.models,
+                     model_of_node=wl.model_of_node, flags=plk.PLK_FLAG_SCALING | DR)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], np.asarray(wl.model_of_node)[br].astype(np.int32), deriv_mask=7)
+    run_engine(eng, et)
+    d1, d2 = eng.all_branch_derivatives()
+    for b in (0, 1, et.n_tips, et.n_nodes - 2, int(br[len(br) // 2])):
+        p1, p2 = eng.branch_derivatives(b)
+        assert _close(d1[b], p1, 1e-9) and _close(d2[b], p2, 1e-9), (b, d1[b], p1, d2[b], p2)
+
+
+def test_dr_after_incremental_traversal():
+    """An incremental call lists only the ancestors of a changed branch; the engine keeps
+    the tree of earlier calls, so every branch is still served."""
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 16, 800, seed=91)
+    eng = engine_for(et, 4, 4, 800, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | DR)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    b = 2
+    bl = et.brlen.copy()
+    bl[b] *= 1.7
+    eng.update_pmatrices(np.array([b], dtype=np.int32), bl[[b]], deriv_mask=7)
+    parents = {c: p for p, ch in et.ops for c in ch}
+    anc = set()
+    n = b
+    while n in parents:
+        n = parents[n]
+        anc.add(n)
+    eng.update_partials(phylo.split_ops([(p, ch) for p, ch in et.ops if p in anc]))
+    d1, _ = eng.all_branch_derivatives()
+    # fresh engine on the changed lengths, full traversal
+    et2 = phylo.EngineTree(et.n_tips, et.n_internal, et.root, et.tip_names, et.ops, bl, {}, [], [])
+    eng2 = engine_for(et2, 4, 4, 800, states, alph.init_table, rates, probs, m.pi, [m],
+                      flags=plk.PLK_FLAG_NONNEG_GUARD | DR)
+    eng2.update_pmatrices(br, bl[br], deriv_mask=7)
+    run_engine(eng2, et2)
+    e1, _ = eng2.all_branch_derivatives()
+    assert np.allclose(d1, e1, rtol=1e-12, atol=0)
+
+
+def test_dr_errors():
+    et, m, alph, rates, probs, states = _random_problem(4, 4, 6, 100, seed=3)
+    eng = engine_for(et, 4, 4, 100, states, alph.init_table, rates, probs, m.pi, [m])
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    with pytest.raises(plk.PlkError) as ei:
+        eng.all_branch_derivatives()  # no PLK_FLAG_DOUBLE_RECURSIVE
+    assert ei.value.code == -5
+    eng = engine_for(et, 4, 4, 100, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | DR)
+    run_engine(eng, et)
+    with pytest.raises(plk.PlkError) as ei:
+        eng.all_branch_derivatives()  # dP / d2P missing
+    assert ei.value.code == -5
+    with pytest.raises(plk.PlkError) as ei:
+        plk.Engine(0, 4, 4, 100, 6, 4, 1, DR | plk.PLK_FLAG_SUBTREE_PATTERNS)
+    assert ei.value.code == -4
