@@ -1184,13 +1184,31 @@ void launch_treeS(plk_handle h, const TreeArgs& a, dim3 grid) {
   }
 }
 
+// treeM tables: staged in LDS behind one barrier per event, or read by every wave straight
+// from L1/L2 (no staging, no barrier).  Measured (profiles/r01/tm1_*): S = 20 (16 waves per
+// workgroup) 7.70 -> 7.48 ms direct; S = 64 (4 waves, 64x64 tables) 0.95 -> 1.35 ms, so
+// direct is the default for 20 states only.  PLK_TREEM_DIRECT=0/1 overrides.
+bool treeM_direct(plk_handle h) {
+  if (env_is("PLK_TREEM_DIRECT", '0')) return false;
+  if (env_is("PLK_TREEM_DIRECT", '1')) return true;
+  return h->S == 20;
+}
+
 template <int S, int DM>
 void launch_treeM_dm(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
   const dim3 block(64 * kTreeMGroups * h->C);
-  if (h->flags & PLK_FLAG_SCALING)
-    treeM_kernel<S, DM, true><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
-  else
-    treeM_kernel<S, DM, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+  const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
+  if (treeM_direct(h)) {
+    if (sc)
+      treeM_kernel<S, DM, true, true><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+    else
+      treeM_kernel<S, DM, false, true><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+  } else {
+    if (sc)
+      treeM_kernel<S, DM, true, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+    else
+      treeM_kernel<S, DM, false, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+  }
 }
 
 void launch_treeM(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
@@ -1271,6 +1289,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       return fail(h, PLK_ERR_UNSUPPORTED, "fused MFMA tables (%d doubles) exceed the staging registers",
                   a.buf_doubles);
     a.buf_doubles = std::max(a.buf_doubles, (pf - 1) * threads);  // unconditional stores stay inside
+    if (treeM_direct(h)) a.buf_doubles = 0;  // tables read from L1/L2: LDS holds the codes only
     lds_m = 2 * (size_t)a.buf_doubles * sizeof(double);
     a.stage_codes = (lds_m + (size_t)h->n_tips * 64 <= 76 * 1024) ? 1 : 0;  // two workgroups per CU
     if (a.stage_codes) lds_m += (size_t)h->n_tips * 64;
@@ -2173,8 +2192,10 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   a.n_patterns = h->n_patterns;
   a.C = C;
   a.n_blk = n_blk;
+  a.G = 3 * (size_t)C * S * S * sizeof(double) <= 96 * 1024 ? C : 1;
+  a.pad_ = 0;
   const dim3 grid((unsigned)n_blk, (unsigned)br.size());
-  const size_t lds = 3 * (size_t)S * S * sizeof(double);
+  const size_t lds = 3 * (size_t)a.G * S * S * sizeof(double);
   EventPair ev;
   if (h->timing & PLK_TIME_PARTIALS) {
     ev = get_events(h, 0);

@@ -70,19 +70,18 @@ struct DrArgs {
   int64_t n_patterns;
   int32_t C;
   int32_t n_blk;
+  int32_t G;                  // classes staged in LDS at a time
+  int32_t pad_;
 };
 
 constexpr int kDrThreads = 256;
 
-// One workgroup = 256 patterns of one branch.  P_v, dP_v, d2P_v of the current class
-// are staged in LDS (3 S^2 doubles, read as wave-wide broadcasts); L_v of the lane's
+// One workgroup = 256 patterns of one branch.  P_v, dP_v, d2P_v of G classes are
+// staged in LDS (3 G S^2 doubles, read as wave-wide broadcasts); L_v of the lane's
 // pattern sits in registers; U_v is read once per (class, state), coalesced.
 template <int S>
 __global__ __launch_bounds__(kDrThreads) void dr_branch_kernel(const DrBranch* __restrict__ branches, DrArgs a) {
   extern __shared__ double lds[];
-  double* sP = lds;
-  double* sD = lds + S * S;
-  double* sD2 = lds + 2 * S * S;
   __shared__ double red[2][kDrThreads / 64];
   const DrBranch b = branches[blockIdx.y];
   const int64_t p = (int64_t)blockIdx.x * kDrThreads + threadIdx.x;
@@ -90,44 +89,54 @@ __global__ __launch_bounds__(kDrThreads) void dr_branch_kernel(const DrBranch* _
   const int64_t tile = p >> 7, q = p & (kTile - 1);
   const int CS = a.C * S;
   double l0 = 0.0, l1 = 0.0, l2 = 0.0;
-  for (int c = 0; c < a.C; ++c) {
+  // classes staged G at a time (G = C when 3 C S^2 doubles fit the LDS budget of the
+  // launch, else 1): no barrier inside a group
+  for (int c0 = 0; c0 < a.C; c0 += a.G) {
+    const int g = min(a.G, a.C - c0);
+    const int SS = S * S;
     __syncthreads();
-    const size_t mo = ((size_t)b.node * a.C + c) * S * S;
-    for (int i = threadIdx.x; i < S * S; i += kDrThreads) {
-      sP[i] = a.pmats[mo + i];
-      sD[i] = a.dpmats[mo + i];
-      sD2[i] = a.d2pmats[mo + i];
+    for (int i = threadIdx.x; i < g * SS; i += kDrThreads) {
+      const size_t mo = ((size_t)b.node * a.C + c0) * SS + i;
+      lds[i] = a.pmats[mo];
+      lds[g * SS + i] = a.dpmats[mo];
+      lds[2 * g * SS + i] = a.d2pmats[mo];
     }
     __syncthreads();
     if (live) {
-      double L[S];
-      if (b.is_tip) {
-        const double* row = a.code_table + (size_t)a.codes[(size_t)b.child * a.n_pad + p] * S;
+      for (int cc = 0; cc < g; ++cc) {
+        const int c = c0 + cc;
+        const double* sP = lds + cc * SS;
+        const double* sD = lds + (g + cc) * SS;
+        const double* sD2 = lds + (2 * g + cc) * SS;
+        double L[S];
+        if (b.is_tip) {
+          const double* row = a.code_table + (size_t)a.codes[(size_t)b.child * a.n_pad + p] * S;
 #pragma unroll
-        for (int z = 0; z < S; ++z) L[z] = row[z];
-      } else {
-        const double* src = a.partials + (size_t)b.child * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
+          for (int z = 0; z < S; ++z) L[z] = row[z];
+        } else {
+          const double* src = a.partials + (size_t)b.child * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
 #pragma unroll
-        for (int z = 0; z < S; ++z) L[z] = src[(size_t)z * kTile];
-      }
-      const double* U = a.partials + (size_t)b.uslot * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
-      double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-      for (int y = 0; y < S; ++y) {
-        double t0 = 0.0, t1 = 0.0, t2 = 0.0;
-#pragma unroll
-        for (int z = 0; z < S; ++z) {
-          t0 = fma(sP[y * S + z], L[z], t0);
-          t1 = fma(sD[y * S + z], L[z], t1);
-          t2 = fma(sD2[y * S + z], L[z], t2);
+          for (int z = 0; z < S; ++z) L[z] = src[(size_t)z * kTile];
         }
-        const double u = b.use_pi ? U[(size_t)y * kTile] * a.pi[y] : U[(size_t)y * kTile];
-        s0 = fma(u, t0, s0);
-        s1 = fma(u, t1, s1);
-        s2 = fma(u, t2, s2);
+        const double* U = a.partials + (size_t)b.uslot * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        for (int y = 0; y < S; ++y) {
+          double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+#pragma unroll
+          for (int z = 0; z < S; ++z) {
+            t0 = fma(sP[y * S + z], L[z], t0);
+            t1 = fma(sD[y * S + z], L[z], t1);
+            t2 = fma(sD2[y * S + z], L[z], t2);
+          }
+          const double u = b.use_pi ? U[(size_t)y * kTile] * a.pi[y] : U[(size_t)y * kTile];
+          s0 = fma(u, t0, s0);
+          s1 = fma(u, t1, s1);
+          s2 = fma(u, t2, s2);
+        }
+        l0 = fma(a.probs[c], s0, l0);
+        l1 = fma(a.probs[c], s1, l1);
+        l2 = fma(a.probs[c], s2, l2);
       }
-      l0 = fma(a.probs[c], s0, l0);
-      l1 = fma(a.probs[c], s1, l1);
-      l2 = fma(a.probs[c], s2, l2);
     }
   }
   double r1 = 0.0, r2 = 0.0;

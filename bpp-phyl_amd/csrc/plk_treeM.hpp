@@ -253,7 +253,7 @@ __device__ __forceinline__ void handover(const TreeArgs& a, MCtx& m, int next, c
   m.cur ^= 1;
 }
 
-template <int S, int PF, int D, int DM, bool SCALE>
+template <int S, int PF, int D, int DM, bool SCALE, bool DIRECT>
 __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __restrict__& pc,
                                             const double* __restrict__ pmatsT, MCtx& m, int c, int g, int lr,
                                             int lc, int64_t p, MAcc<S>& acc, int& cnt) {
@@ -271,15 +271,24 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
       return;
     }
     if (in.op == T_TIP) {
-      double pf[PF];
-      stage_load<S, PF>(a, pmatsT, in.d, pf);
       const int code = m.codes ? m.codes[in.a * 64 + 16 * g + lc] : a.codes[(size_t)in.a * a.n_pad + p];
-      const double* t = m.buf + m.cur * a.buf_doubles + (c * a.n_codes + code) * S;
+      if constexpr (DIRECT) {
+        // the tip table row straight from L2 (a per-lane gather by code)
+        const double* t = a.tipP + ((size_t)in.a * a.C * a.n_codes + (size_t)c * a.n_codes + code) * S;
 #pragma unroll
-      for (int xt = 0; xt < XT; ++xt)
+        for (int xt = 0; xt < XT; ++xt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[xt][r] *= m_valid<S>(xt, r, lr) ? t[16 * xt + lr + 4 * r] : 0.0;
-      handover<S, PF>(a, m, in.d, pf);
+          for (int r = 0; r < 4; ++r) acc[xt][r] *= m_valid<S>(xt, r, lr) ? t[16 * xt + lr + 4 * r] : 0.0;
+      } else {
+        double pf[PF];
+        stage_load<S, PF>(a, pmatsT, in.d, pf);
+        const double* t = m.buf + m.cur * a.buf_doubles + (c * a.n_codes + code) * S;
+#pragma unroll
+        for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[xt][r] *= m_valid<S>(xt, r, lr) ? t[16 * xt + lr + 4 * r] : 0.0;
+        handover<S, PF>(a, m, in.d, pf);
+      }
     } else if (in.op == T_CHERRY) {
       // one row of the cherry's contribution table; no table staging, no barrier
       const CherryLayout lay(a.C, a.n_codes, S, a.n_pad);
@@ -302,20 +311,28 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
         for (int r = 0; r < 4; ++r)
           src[xt][r] = m_valid<S>(xt, r, lr) ? L[(size_t)(16 * xt + lr + 4 * r) * kTile] : 0.0;
       if (SCALE) cnt += a.scale[(size_t)in.a * a.n_pad + p];
-      double pf[PF];
-      stage_load<S, PF>(a, pmatsT, in.d, pf);
-      contribute_m<S>(acc, src, m.buf + m.cur * a.buf_doubles + c * S * S, lr, lc);
-      handover<S, PF>(a, m, in.d, pf);
+      if constexpr (DIRECT) {
+        contribute_m<S>(acc, src, pmatsT + ((size_t)in.b * a.C + c) * S * S, lr, lc);
+      } else {
+        double pf[PF];
+        stage_load<S, PF>(a, pmatsT, in.d, pf);
+        contribute_m<S>(acc, src, m.buf + m.cur * a.buf_doubles + c * S * S, lr, lc);
+        handover<S, PF>(a, m, in.d, pf);
+      }
     } else {  // T_DESCEND
       if constexpr (D + 1 < DM) {
         MAcc<S> child;
         int ccnt;
-        eval_node_m<S, PF, D + 1, DM, SCALE>(a, pc, pmatsT, m, c, g, lr, lc, p, child, ccnt);
+        eval_node_m<S, PF, D + 1, DM, SCALE, DIRECT>(a, pc, pmatsT, m, c, g, lr, lc, p, child, ccnt);
         const TInstr up = fetch_instr(pc - 1);
-        double pf[PF];
-        stage_load<S, PF>(a, pmatsT, up.d, pf);
-        contribute_m<S>(acc, child, m.buf + m.cur * a.buf_doubles + c * S * S, lr, lc);
-        handover<S, PF>(a, m, up.d, pf);
+        if constexpr (DIRECT) {
+          contribute_m<S>(acc, child, pmatsT + ((size_t)up.b * a.C + c) * S * S, lr, lc);
+        } else {
+          double pf[PF];
+          stage_load<S, PF>(a, pmatsT, up.d, pf);
+          contribute_m<S>(acc, child, m.buf + m.cur * a.buf_doubles + c * S * S, lr, lc);
+          handover<S, PF>(a, m, up.d, pf);
+        }
         if (SCALE) cnt += ccnt;
       }
     }
@@ -330,7 +347,9 @@ constexpr int treeM_threads() { return S == 64 ? 64 * kTreeMGroups : 64 * kTreeM
 template <int S>
 constexpr int treeM_pf() { return S == 64 ? 17 : 3; }
 
-template <int S, int DM, bool SCALE>
+// DIRECT: no LDS staging and no per-event barrier -- MFMA A operands (P^T) and tip
+// table rows are read by each wave straight from L1/L2 (same values, same order).
+template <int S, int DM, bool SCALE, bool DIRECT>
 __global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, const TInstr* __restrict__ prog,
                                                                    const int32_t* __restrict__ frag_start,
                                                                    const double* __restrict__ pmatsT) {
@@ -358,17 +377,19 @@ __global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, c
     }
     m.codes = cl;
   }
-  {
+  if constexpr (!DIRECT) {
     const int first = frag_start[a.n_frags + blockIdx.y];
     double pf[PF];
     stage_load<S, PF>(a, pmatsT, first, pf);
     stage_store<S, PF>(a, first, pf, m.buf);
     __syncthreads();
+  } else if (a.stage_codes) {
+    __syncthreads();
   }
   const TInstr* __restrict__ pc = prog + frag_start[blockIdx.y];
   MAcc<S> acc;
   int cnt;
-  eval_node_m<S, PF, 0, DM, SCALE>(a, pc, pmatsT, m, c, g, lr, lc, p, acc, cnt);
+  eval_node_m<S, PF, 0, DM, SCALE, DIRECT>(a, pc, pmatsT, m, c, g, lr, lc, p, acc, cnt);
   const TInstr in = fetch_instr(pc);  // T_ROOT
   if (SCALE) rescale_m<S>(acc, cnt, xch, a.C, c, g, lr, lc);
   if (in.a >= 0) store_partial_m<S, SCALE>(a, in.a, p, c, acc, cnt, lr);

@@ -763,3 +763,25 @@ def test_pmat64_kernels_bitwise(monkeypatch):
         del eng
     assert out["0"][0] == out["1"][0] and np.array_equal(out["0"][1], out["1"][1])
     assert np.array_equal(out["0"][2], out["1"][2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,C,scaling,mode", [(20, 4, True, "lnl_only"), (20, 2, False, "materialize"),
+                                              (64, 1, False, "lnl_only"), (64, 1, True, "materialize")])
+def test_treeM_direct_tables_bitwise(S, C, scaling, mode, monkeypatch):
+    """treeM reading P^T and tip-table rows straight from L1/L2 (PLK_TREEM_DIRECT=1) equals the
+    LDS-staged kernel (=0) bitwise: lnL, per-pattern lnL, block sums and stored partials."""
+    et, m, alph, rates, probs, states = _random_problem(S, C, 40 if S == 20 else 20, 600, seed=S + 3 * C,
+                                                        amb=S == 20)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    res = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("PLK_TREEM_DIRECT", on)
+        eng = engine_for(et, S, C, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+        lnl, site, blocks = run_engine(eng, et)
+        assert eng.kernel_path() == "treeM"
+        parts = np.stack([eng.get_partials(p) for p, _ in et.ops[-3:]])
+        res[on] = (lnl, site, blocks, parts)
+        del eng
+    a, b = res["0"], res["1"]
+    assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
