@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="A/B: time the steps without per-kernel HIP events")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="HIP events bracket the partials launches of every K-th timed step (an event pair costs "
+                         "~6 us of stream time per step on the box; 1 = every step)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path on ONE GPU (every rank on cuda:0, collectives on the host); "
                          "never a measurement")
@@ -224,13 +227,22 @@ def main():
     for _ in range(args.warmup):
         lnl = one_step()
     ev.eng.reset_timing()
-    # HIP events around the partials launches only (each timed launch adds an event pair)
-    ev.eng.set_timing(0 if args.no_events else plk.PLK_TIME_PARTIALS)
+    # HIP events around the partials launches only (each timed launch adds an event pair),
+    # on every K-th timed step: the kernel's mean launch duration is sampled inside the
+    # timed region without charging every step the events' own stream time
+    k_ev = max(1, args.event_every)
+    mask = 0 if args.no_events else plk.PLK_TIME_PARTIALS
+    ev_steps = 0
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if i % k_ev == 0:
+            ev.eng.set_timing(mask)
+            ev_steps += 1
+        elif k_ev > 1 and i % k_ev == 1:
+            ev.eng.set_timing(0)
         lnl = one_step()
     if dist is not None:
         dist.barrier()
@@ -250,8 +262,10 @@ def main():
         flops_pattern = wl.algorithmic_flops_per_pattern()
         part_s = tm["partials_ms"] * 1e-3
         launches = max(tm["launches"], 1)
-        traffic, traffic_src = measured_traffic(args.config, args.mode, P, launches / args.steps)
-        roof = roofline(wl, args.mode, P, args.steps, part_s, launches, bytes_pattern, flops_pattern, traffic)
+        traffic, traffic_src = measured_traffic(args.config, args.mode, P, launches / ev_steps)
+        roof = roofline(wl, args.mode, P, ev_steps, part_s, launches, bytes_pattern, flops_pattern, traffic)
+        if roof:
+            roof["event_sample"] = f"HIP events on {ev_steps} of {args.steps} timed steps (every {k_ev})"
         if traffic_src and roof:
             roof["traffic_source"] = traffic_src
         computed = None
@@ -292,10 +306,10 @@ def main():
                 "parallelism": f"pattern-shard x{world}",
             },
             "lnl": lnl,
-            "partials_only_updates_per_s": units_step * args.steps / part_s if part_s > 0 else None,
-            "kernel_ms_per_step": {"partials": tm["partials_ms"] / args.steps, "pmatrix": tm["pmat_ms"] / args.steps,
-                                   "root": tm["root_ms"] / args.steps},
-            "partials_launches_per_step": launches / args.steps,
+            "partials_only_updates_per_s": units_step * ev_steps / part_s if part_s > 0 else None,
+            "kernel_ms_per_step": {"partials": tm["partials_ms"] / ev_steps, "pmatrix": tm["pmat_ms"] / ev_steps,
+                                   "root": tm["root_ms"] / ev_steps},
+            "partials_launches_per_step": launches / ev_steps,
             "roofline": roof,
             "setup_s": t_setup,
         }

@@ -231,6 +231,20 @@ int ensure_cap(plk_handle h, void** p, size_t* cap, size_t bytes) {
   return PLK_OK;
 }
 
+// Completion wait of an evaluation.  PLK_SPIN=1 polls hipStreamQuery instead of
+// hipStreamSynchronize (A/B of the host wake-up latency).
+int stream_wait(plk_handle h) {
+  if (env_is("PLK_SPIN", '1')) {
+    hipError_t e;
+    while ((e = hipStreamQuery(h->stream)) == hipErrorNotReady) {
+    }
+    if (e != hipSuccess) return fail(h, PLK_ERR_DEVICE, "hipStreamQuery: %s", hipGetErrorString(e));
+    return PLK_OK;
+  }
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PLK_OK;
+}
+
 EventPair get_events(plk_handle h, int kind) {
   EventPair e;
   if (!h->event_pool.empty()) {
@@ -1432,7 +1446,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       hipEventRecord(ev.b, h->stream);
       h->events.push_back(ev);
     }
-    h->n_launches++;
+    if (h->timing & PLK_TIME_PARTIALS) h->n_launches++;  // launches timed by the events
     first += (int)t.size();
   }
   h->fused_lnl_valid = h->prog_root >= 0;
@@ -1538,7 +1552,7 @@ int update_levelwise(plk_handle h, const plk_op* ops, int n_ops) {
       hipEventRecord(ev.b, h->stream);
       h->events.push_back(ev);
     }
-    h->n_launches++;
+    if (h->timing & PLK_TIME_PARTIALS) h->n_launches++;  // launches timed by the events
   }
   for (int i = 0; i < n_ops; ++i) h->materialized[ops[i].parent - h->n_tips] = 1;
   h->fused_lnl_valid = false;
@@ -1809,7 +1823,7 @@ int update_compressed(plk_handle h, const plk_op* ops, int n_ops) {
       hipEventRecord(ev.b, h->stream);
       h->events.push_back(ev);
     }
-    h->n_launches++;
+    if (h->timing & PLK_TIME_PARTIALS) h->n_launches++;  // launches timed by the events
   }
   for (int i = 0; i < n_ops; ++i) h->materialized[ops[i].parent - h->n_tips] = 1;
   h->fused_lnl_valid = false;
@@ -2298,7 +2312,7 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
   if (site_lnl)
     HIPCHK(h, hipMemcpyAsync(site_lnl, h->site_lnl, (size_t)h->n_patterns * sizeof(double), hipMemcpyDeviceToHost,
                              h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (int rc = stream_wait(h)) return rc;
   double s = 0.0;
   for (int b = 0; b < h->n_blocks; ++b) s += h->h_blocks[b];  // fixed order: block 0, 1, 2, ...
   if (lnl) *lnl = s;

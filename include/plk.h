@@ -191,6 +191,7 @@ int plk_all_branch_derivatives(plk_handle h, double* d1, double* d2);
  * pair to the stream, so time only what is needed. */
 enum { PLK_TIME_PARTIALS = 1u, PLK_TIME_PMAT = 2u, PLK_TIME_ROOT = 4u };
 int plk_set_timing(plk_handle h, int mask);
+/* n_launches: partials launches issued while PLK_TIME_PARTIALS was set (the timed ones) */
 int plk_get_timing(plk_handle h, int64_t* n_launches, double* partials_ms, double* pmat_ms, double* root_ms);
 int plk_reset_timing(plk_handle h);
 int plk_synchronize(plk_handle h);

@@ -14,3 +14,8 @@ bash tools/gpu_prof.sh ${P}_cfg5_lnl nh_gtr_g4_dna_2M_512 lnl 10 || exit 1
 bash tools/gpu_prof.sh ${P}_cfg2_sub gtr_g4_dna_1M_64 subtree 10 || exit 1
 timeout -k 10 300 python bench.py > gpurun_out/${P}_bench_default.json 2> gpurun_out/${P}_bench_default.err || { tail -5 gpurun_out/${P}_bench_default.err; exit 1; }
 cat gpurun_out/${P}_bench_default.json
+# row f4: the double-recursive all-branch derivative pass (kernel-trace stats)
+mkdir -p gpurun_out/prof/${P}_cfg2_dr
+( export TMPDIR=/tmp; cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof/${P}_cfg2_dr/trace -o run -- \
+  python3 $GRAFT_REPO_ROOT/tools/bench_dr.py --config gtr_g4_dna_1M_64 --path-branches 16 > $GRAFT_REPO_ROOT/gpurun_out/prof/${P}_cfg2_dr/bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/prof/${P}_cfg2_dr/trace.err ) || { echo "dr profile failed"; exit 1; }
+cat gpurun_out/prof/${P}_cfg2_dr/bench.json
