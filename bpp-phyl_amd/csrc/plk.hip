@@ -1866,6 +1866,7 @@ int launch_partials_ops(plk_handle h, const KOp* d_ops, int n_ops) {
 }
 
 int materialize_last_traversal(plk_handle h);
+void topo_postorder(plk_handle h, int root, std::vector<plk_op>& ops);
 
 int path_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   if (h->deriv_valid.empty() || !h->deriv_valid[branch])
@@ -1877,10 +1878,12 @@ int path_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   const int nt = h->n_tips;
   std::vector<std::vector<int> > kids(h->n_nodes);
   std::vector<int> parent(h->n_nodes, -1);
-  for (const plk_op& o : h->trav_ops)
-    for (int k = 0; k < o.n_children; ++k) {
-      kids[o.parent].push_back(o.child[k]);
-      parent[o.child[k]] = o.parent;
+  // the merged tree of every traversal so far (an incremental call lists only the
+  // ancestors of the changed branches)
+  for (int n = 0; n < h->n_nodes; ++n)
+    for (int c : h->topo_kids[n]) {
+      kids[n].push_back(c);
+      parent[c] = n;
     }
   if (parent[branch] < 0) return fail(h, PLK_ERR_ARG, "branch %d is not below any node of the last traversal", branch);
   int root = parent[branch];
@@ -2027,10 +2030,17 @@ bool fusable(const plk_op* ops, int n_ops) {
   return true;
 }
 
-// Re-run the last traversal writing every partial (same arithmetic, identical values).
+// Re-run the traversal of the whole (merged) tree writing every partial (same arithmetic,
+// identical values).
 int materialize_last_traversal(plk_handle h) {
+  std::vector<int> parent(h->n_nodes, -1);
+  for (int n = 0; n < h->n_nodes; ++n)
+    for (int c : h->topo_kids[n]) parent[c] = n;
+  int root = h->trav_ops.back().parent;
+  while (parent[root] >= 0) root = parent[root];
+  std::vector<plk_op> ops;
+  topo_postorder(h, root, ops);
   const unsigned saved = h->flags;
-  const std::vector<plk_op> ops = h->trav_ops;
   h->flags &= ~(unsigned)PLK_FLAG_LNL_ONLY;
   const int rc = tree4_supported(h) && fusable(ops.data(), (int)ops.size())
                      ? update_tree4(h, ops.data(), (int)ops.size())
@@ -2183,7 +2193,9 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
       b.use_pi = parent[v] == root;
       br.push_back(b);
     }
-  const int n_blk = (int)(h->n_pad / kDrThreads);
+  // S = 20 / 64 reduce on fp64 MFMA (64-pattern blocks) unless PLK_DR_MFMA=0
+  const bool dr_mfma = (S == 20 || S == 64) && !env_is("PLK_DR_MFMA", '0');
+  const int n_blk = (int)(h->n_pad / (dr_mfma ? 64 : kDrThreads));
   if ((rc = ensure_cap(h, (void**)&h->d_drb, &h->d_drb_cap, br.size() * sizeof(DrBranch)))) return rc;
   if ((rc = ensure_cap(h, (void**)&h->dr_blk, &h->dr_blk_cap, 2 * br.size() * n_blk * sizeof(double)))) return rc;
   if (!h->dr_out && (rc = dalloc(h, (void**)&h->dr_out, 2 * (size_t)nn * sizeof(double)))) return rc;
@@ -2215,12 +2227,20 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
     ev = get_events(h, 0);
     hipEventRecord(ev.a, h->stream);
   }
-  switch (S) {
-    case 2: dr_branch_kernel<2><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
-    case 3: dr_branch_kernel<3><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
-    case 4: dr_branch_kernel<4><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
-    case 20: dr_branch_kernel<20><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
-    case 64: dr_branch_kernel<64><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+  if (dr_mfma) {
+    const size_t lds_m = 3 * (size_t)S * S * sizeof(double);
+    if (S == 20)
+      dr_branch_mfma_kernel<20><<<grid, kDrmThreads, lds_m, h->stream>>>(h->d_drb, a);
+    else
+      dr_branch_mfma_kernel<64><<<grid, kDrmThreads, lds_m, h->stream>>>(h->d_drb, a);
+  } else {
+    switch (S) {
+      case 2: dr_branch_kernel<2><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+      case 3: dr_branch_kernel<3><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+      case 4: dr_branch_kernel<4><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+      case 20: dr_branch_kernel<20><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+      case 64: dr_branch_kernel<64><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
+    }
   }
   HIPCHK(h, hipGetLastError());
   if (h->timing & PLK_TIME_PARTIALS) {
@@ -2364,10 +2384,12 @@ int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   // tree of the last traversal: sons per node (ops merged), parent map
   std::vector<std::vector<int> > kids(h->n_nodes);
   std::vector<int> parent(h->n_nodes, -1);
-  for (const plk_op& o : h->trav_ops)
-    for (int k = 0; k < o.n_children; ++k) {
-      kids[o.parent].push_back(o.child[k]);
-      parent[o.child[k]] = o.parent;
+  // the merged tree of every traversal so far (an incremental call lists only the
+  // ancestors of the changed branches)
+  for (int n = 0; n < h->n_nodes; ++n)
+    for (int c : h->topo_kids[n]) {
+      kids[n].push_back(c);
+      parent[c] = n;
     }
   if (parent[branch] < 0) return fail(h, PLK_ERR_ARG, "branch %d is not below any node of the last traversal", branch);
   // every partial read along the path must be in HBM: re-materialise if needed
@@ -2376,13 +2398,7 @@ int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
     for (int c : kids[n])
       if (c >= nt && !h->materialized[c - nt]) need = true;
   if (need) {
-    const unsigned saved = h->flags;
-    const std::vector<plk_op> ops = h->trav_ops;
-    h->flags &= ~(unsigned)PLK_FLAG_LNL_ONLY;
-    int rc = tree4_supported(h) && fusable(ops.data(), (int)ops.size())
-                 ? update_tree4(h, ops.data(), (int)ops.size())
-                 : update_levelwise(h, ops.data(), (int)ops.size());
-    h->flags = saved;
+    int rc = materialize_last_traversal(h);
     if (rc) return rc;
   }
   // path program: father of the branch first, then every ancestor up to the root

@@ -23,6 +23,7 @@
 #pragma once
 
 #include "plk_kernels.hpp"
+#include "plk_treeM.hpp"
 
 namespace plk {
 
@@ -159,6 +160,109 @@ __global__ __launch_bounds__(kDrThreads) void dr_branch_kernel(const DrBranch* _
   if (threadIdx.x == 0) {
     double t1 = 0.0, t2 = 0.0;
     for (int k = 0; k < kDrThreads / 64; ++k) {  // fixed order
+      t1 += red[0][k];
+      t2 += red[1][k];
+    }
+    a.blk1[(size_t)blockIdx.y * a.n_blk + blockIdx.x] = t1;
+    a.blk2[(size_t)blockIdx.y * a.n_blk + blockIdx.x] = t2;
+  }
+}
+
+// S = 20 / 64: the same reduction on fp64 matrix cores.  A wave owns 16 patterns; L_v of
+// the wave's patterns is the B operand of v_mfma_f64_16x16x4f64 in treeM's C/D layout
+// (plk_treeM.hpp: lane l holds states 16 xt + (l >> 4) + 4 r of pattern l & 15), and
+// (P_v L_v), (dP_v L_v), (d2P_v L_v) come out of matvec_m in that same layout, so the
+// dot with U_v is lane-local plus two cross-lane adds.  P^T, dP^T, d2P^T of one class are
+// staged transposed in LDS (3 S^2 doubles).  Block sums cover 64 patterns.
+constexpr int kDrmThreads = 256;
+
+template <int S>
+__global__ __launch_bounds__(kDrmThreads) void dr_branch_mfma_kernel(const DrBranch* __restrict__ branches, DrArgs a) {
+  constexpr int XT = MShape<S>::XT;
+  extern __shared__ double lds[];
+  __shared__ double red[2][kDrmThreads / 64];
+  const DrBranch b = branches[blockIdx.y];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int lr = lane >> 4, lc = lane & 15;
+  const int64_t p = (int64_t)blockIdx.x * 64 + 16 * g + lc;
+  const bool live = p < a.n_patterns;
+  const int64_t tile = p >> 7, q = p & (kTile - 1);
+  const int CS = a.C * S;
+  double* sP = lds;
+  double* sD = lds + S * S;
+  double* sD2 = lds + 2 * S * S;
+  double l0 = 0.0, l1 = 0.0, l2 = 0.0;
+  for (int c = 0; c < a.C; ++c) {
+    __syncthreads();
+    const size_t mo = ((size_t)b.node * a.C + c) * S * S;
+    for (int i = threadIdx.x; i < S * S; i += kDrmThreads) {
+      const int x = i / S, y = i - x * S;  // source [x][y] -> LDS [y][x]
+      sP[y * S + x] = a.pmats[mo + i];
+      sD[y * S + x] = a.dpmats[mo + i];
+      sD2[y * S + x] = a.d2pmats[mo + i];
+    }
+    __syncthreads();
+    MAcc<S> src;
+    if (b.is_tip) {
+      const double* row = a.code_table + (size_t)a.codes[(size_t)b.child * a.n_pad + p] * S;
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) src[xt][r] = m_valid<S>(xt, r, lr) ? row[16 * xt + lr + 4 * r] : 0.0;
+    } else {
+      const double* L = a.partials + (size_t)b.child * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          src[xt][r] = m_valid<S>(xt, r, lr) ? L[(size_t)(16 * xt + lr + 4 * r) * kTile] : 0.0;
+    }
+    f64x4m d0[XT], d1[XT], d2[XT];
+    matvec_m<S>(d0, src, sP, lr, lc);
+    matvec_m<S>(d1, src, sD, lr, lc);
+    matvec_m<S>(d2, src, sD2, lr, lc);
+    const double* U = a.partials + (size_t)b.uslot * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (m_valid<S>(xt, r, lr)) {
+          const int x = 16 * xt + lr + 4 * r;
+          const double u = b.use_pi ? U[(size_t)x * kTile] * a.pi[x] : U[(size_t)x * kTile];
+          s0 = fma(u, d0[xt][r], s0);
+          s1 = fma(u, d1[xt][r], s1);
+          s2 = fma(u, d2[xt][r], s2);
+        }
+    s0 += __shfl_xor(s0, 16, 64);
+    s1 += __shfl_xor(s1, 16, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s0 += __shfl_xor(s0, 32, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    l0 = fma(a.probs[c], s0, l0);
+    l1 = fma(a.probs[c], s1, l1);
+    l2 = fma(a.probs[c], s2, l2);
+  }
+  double r1 = 0.0, r2 = 0.0;
+  if (live && lr == 0) {
+    const double gg = l1 / l0, hh = l2 / l0;
+    r1 = a.weights[p] * gg;
+    r2 = a.weights[p] * (hh - gg * gg);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    r1 += __shfl_xor(r1, off, 64);
+    r2 += __shfl_xor(r2, off, 64);
+  }
+  if (lane == 0) {
+    red[0][g] = r1;
+    red[1][g] = r2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < kDrmThreads / 64; ++k) {  // fixed order
       t1 += red[0][k];
       t2 += red[1][k];
     }

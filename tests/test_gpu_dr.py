@@ -168,3 +168,34 @@ def test_dr_errors():
     with pytest.raises(plk.PlkError) as ei:
         plk.Engine(0, 4, 4, 100, 6, 4, 1, DR | plk.PLK_FLAG_SUBTREE_PATTERNS)
     assert ei.value.code == -4
+
+
+@pytest.mark.parametrize("S,C", [(4, 4), (20, 2)])
+def test_path_derivatives_after_incremental_traversal(S, C):
+    """plk_branch_derivatives on a branch outside the last (incremental) op list: the engine
+    answers from the merged tree, equal to a fresh engine's full traversal."""
+    et, m, alph, rates, probs, states = _random_problem(S, C, 16, 500, seed=93 + S)
+    eng = engine_for(et, S, C, 500, states, alph.init_table, rates, probs, m.pi, [m])
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    b = 0
+    bl = et.brlen.copy()
+    bl[b] *= 1.5
+    eng.update_pmatrices(np.array([b], dtype=np.int32), bl[[b]], deriv_mask=7)
+    parents = {c: p for p, ch in et.ops for c in ch}
+    anc, n = set(), b
+    while n in parents:
+        n = parents[n]
+        anc.add(n)
+    eng.update_partials(phylo.split_ops([(p, ch) for p, ch in et.ops if p in anc]))
+    far = [v for v in range(et.n_nodes) if v != et.root and parents.get(v) not in anc]
+    assert far
+    et2 = phylo.EngineTree(et.n_tips, et.n_internal, et.root, et.tip_names, et.ops, bl, {}, [], [])
+    eng2 = engine_for(et2, S, C, 500, states, alph.init_table, rates, probs, m.pi, [m])
+    eng2.update_pmatrices(br, bl[br], deriv_mask=7)
+    run_engine(eng2, et2)
+    for v in far[:4] + [b]:
+        a1, a2 = eng.branch_derivatives(v)
+        e1, e2 = eng2.branch_derivatives(v)
+        assert _close(a1, e1, 1e-12) and _close(a2, e2, 1e-12), (v, a1, e1, a2, e2)
