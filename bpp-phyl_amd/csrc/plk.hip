@@ -1293,6 +1293,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
                      (a.stage_codes ? (size_t)h->n_tips * 64 : 0);
   a.n_frags = h->prog_nf;
   a.bmask = env_is("PLK_DEBUG_SAMEP", '1') ? 0 : -1;
+  a.cherry_pairs = env_is("PLK_TREEM_PAIRS", '0') ? 0 : 1;
+  a.n_cherry_staged = 0;
   size_t lds_m = 0;
   if (kind == FK_TREEM) {
     a.buf_doubles = std::max(h->C * h->S * h->S, h->C * h->n_codes * h->S);
@@ -1307,6 +1309,15 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     lds_m = 2 * (size_t)a.buf_doubles * sizeof(double);
     a.stage_codes = (lds_m + (size_t)h->n_tips * 64 <= 76 * 1024) ? 1 : 0;  // two workgroups per CU
     if (a.stage_codes) lds_m += (size_t)h->n_tips * 64;
+    // direct tables: the cherries' combined codes of the workgroup staged beside the tip codes
+    // (opt-in PLK_TREEM_CCODES=1: every workgroup stages all cherries but runs one fragment,
+    // cfg3 7.64 -> 7.86 ms)
+    const int nch = (int)h->cherry3.size() / 3;
+    if (treeM_direct(h) && nch > 0 && h->d_cherry && env_is("PLK_TREEM_CCODES", '1') &&
+        lds_m + (size_t)nch * 128 <= 76 * 1024) {
+      a.n_cherry_staged = nch;
+      lds_m += (size_t)nch * 128;
+    }
   }
   const int cw = tree4_cw(h);
   // 4 states, one class per wave: the tree-specialised kernel (PLK_JIT=0 keeps the

@@ -67,6 +67,8 @@ struct TreeArgs {
   int32_t buf_doubles;        // treeM: doubles per LDS table buffer
   int32_t bmask;              // -1 (timing experiments: 0 = every branch reads P of node 0)
   const uint8_t* cherry;      // treeM: per cherry [table | counts | codes] (plk_treeM.hpp: CherryLayout)
+  int32_t cherry_pairs;       // treeM: two consecutive T_CHERRY rows gathered together
+  int32_t n_cherry_staged;    // treeM: cherries whose combined codes are staged in LDS (0: none)
 };
 
 constexpr int kTreeMaxWaves = 4;

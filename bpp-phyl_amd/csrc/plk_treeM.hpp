@@ -242,6 +242,7 @@ __device__ __forceinline__ void stage_store(const TreeArgs& a, int res, const do
 struct MCtx {
   double* buf;            // two table buffers of a.buf_doubles each
   const uint8_t* codes;   // staged codes [n_tips][64] or null
+  const uint16_t* ccodes; // staged cherry codes [n_cherry_staged][64] or null
   double* xch;
   int cur;
 };
@@ -293,8 +294,43 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
       // one row of the cherry's contribution table; no table staging, no barrier
       const CherryLayout lay(a.C, a.n_codes, S, a.n_pad);
       const uint8_t* base = a.cherry + (size_t)in.a * lay.stride;
-      const int code = reinterpret_cast<const uint16_t*>(base + lay.table_bytes + lay.count_bytes)[p];
+      const int code = m.ccodes ? m.ccodes[in.a * 64 + 16 * g + lc]
+                                : reinterpret_cast<const uint16_t*>(base + lay.table_bytes + lay.count_bytes)[p];
       const double* t = reinterpret_cast<const double*>(base) + ((size_t)c * a.n_codes * a.n_codes + code) * S;
+      if (a.cherry_pairs) {
+        const TInstr nx = fetch_instr(pc);
+        if (nx.op == T_CHERRY) {
+          // a sibling cherry follows: both rows' gathers in flight at once (their L2 / MALL
+          // latencies overlap); multiplied in event order, so bitwise the same
+          const uint8_t* base2 = a.cherry + (size_t)nx.a * lay.stride;
+          const int code2 = m.ccodes ? m.ccodes[nx.a * 64 + 16 * g + lc]
+                                     : reinterpret_cast<const uint16_t*>(base2 + lay.table_bytes + lay.count_bytes)[p];
+          const double* t2 =
+              reinterpret_cast<const double*>(base2) + ((size_t)c * a.n_codes * a.n_codes + code2) * S;
+          double r1[XT][4], r2[XT][4];
+#pragma unroll
+          for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              r1[xt][r] = m_valid<S>(xt, r, lr) ? t[16 * xt + lr + 4 * r] : 0.0;
+              r2[xt][r] = m_valid<S>(xt, r, lr) ? t2[16 * xt + lr + 4 * r] : 0.0;
+            }
+#pragma unroll
+          for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[xt][r] *= r1[xt][r];
+#pragma unroll
+          for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[xt][r] *= r2[xt][r];
+          if (SCALE) {
+            cnt += base[lay.table_bytes + code];
+            cnt += base2[lay.table_bytes + code2];
+          }
+          ++pc;
+          continue;
+        }
+      }
 #pragma unroll
       for (int xt = 0; xt < XT; ++xt)
 #pragma unroll
@@ -377,13 +413,29 @@ __global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, c
     }
     m.codes = cl;
   }
+  m.ccodes = nullptr;
+  if constexpr (DIRECT) {
+    if (a.n_cherry_staged) {
+      // the cherries' combined codes of the workgroup's 64 patterns (read by every T_CHERRY
+      // of every wave; one latency here instead of one per event)
+      uint16_t* cc = reinterpret_cast<uint16_t*>(lds + 2 * a.buf_doubles) + (a.stage_codes ? a.n_tips * 32 : 0);
+      const CherryLayout lay(a.C, a.n_codes, S, a.n_pad);
+      for (int i = threadIdx.x; i < a.n_cherry_staged * 16; i += blockDim.x) {
+        const int k = i >> 4, j = i & 15;
+        const uint16_t* src = reinterpret_cast<const uint16_t*>(a.cherry + (size_t)k * lay.stride + lay.table_bytes +
+                                                                lay.count_bytes) + p0 + 4 * j;
+        reinterpret_cast<uint2*>(cc)[i] = *reinterpret_cast<const uint2*>(src);
+      }
+      m.ccodes = cc;
+    }
+  }
   if constexpr (!DIRECT) {
     const int first = frag_start[a.n_frags + blockIdx.y];
     double pf[PF];
     stage_load<S, PF>(a, pmatsT, first, pf);
     stage_store<S, PF>(a, first, pf, m.buf);
     __syncthreads();
-  } else if (a.stage_codes) {
+  } else if (a.stage_codes || a.n_cherry_staged) {
     __syncthreads();
   }
   const TInstr* __restrict__ pc = prog + frag_start[blockIdx.y];
