@@ -1308,6 +1308,11 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     if (treeM_direct(h)) a.buf_doubles = 0;  // tables read from L1/L2: LDS holds the codes only
     lds_m = 2 * (size_t)a.buf_doubles * sizeof(double);
     a.stage_codes = (lds_m + (size_t)h->n_tips * 64 <= 76 * 1024) ? 1 : 0;  // two workgroups per CU
+    // a program whose tips all sit in cherry tables (balanced trees) has no T_TIP event:
+    // staging every tip's codes would only cost each workgroup a load of n_tips x 64 B
+    if (!env_is("PLK_TREEM_STAGE_CODES", '1') &&
+        std::none_of(h->prog_host.begin(), h->prog_host.end(), [](const TInstr& w) { return w.op == T_TIP; }))
+      a.stage_codes = 0;
     if (a.stage_codes) lds_m += (size_t)h->n_tips * 64;
     // direct tables: the cherries' combined codes of the workgroup staged beside the tip codes
     // (opt-in PLK_TREEM_CCODES=1: every workgroup stages all cherries but runs one fragment,
