@@ -184,6 +184,12 @@ class RNonHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
 
   int modelIndexForNode(const Node* n) const override;
 
+ protected:
+  // engine flags of a subclass (DRNonHomogeneousTreeLikelihood) must be known before setData
+  RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data, SubstitutionModelSet* modelSet,
+                                DiscreteDistribution* rDist, bool verbose, bool usePatterns, bool reparametrizeRoot,
+                                unsigned extraFlags);
+
  public:
   RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data, SubstitutionModelSet* modelSet,
                                 DiscreteDistribution* rDist, bool verbose = true, bool usePatterns = true,
@@ -193,6 +199,14 @@ class RNonHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
   void fireParameterChanged(const ParameterList& params) override;
   ParameterList getSubstitutionModelParameters() const override;
   void computeAllTransitionProbabilities();
+};
+
+// Likelihood/DRNonHomogeneousTreeLikelihood.h:114-120: the NH likelihood with every branch's
+// derivatives from one double-recursive pass (plk_all_branch_derivatives)
+class DRNonHomogeneousTreeLikelihood : public RNonHomogeneousTreeLikelihood {
+ public:
+  DRNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data, SubstitutionModelSet* modelSet,
+                                 DiscreteDistribution* rDist, bool verbose = true, bool reparametrizeRoot = false);
 };
 
 }  // namespace bpp

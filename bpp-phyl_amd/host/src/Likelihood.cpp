@@ -490,9 +490,23 @@ DRHomogeneousTreeLikelihood::DRHomogeneousTreeLikelihood(const Tree& tree, const
 RNonHomogeneousTreeLikelihood::RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data,
                                                              SubstitutionModelSet* modelSet,
                                                              DiscreteDistribution* rDist, bool verbose,
-                                                             bool usePatterns, bool)
+                                                             bool usePatterns, bool reparametrizeRoot)
+    : RNonHomogeneousTreeLikelihood(tree, data, modelSet, rDist, verbose, usePatterns, reparametrizeRoot, 0u) {}
+
+DRNonHomogeneousTreeLikelihood::DRNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data,
+                                                               SubstitutionModelSet* modelSet,
+                                                               DiscreteDistribution* rDist, bool verbose,
+                                                               bool reparametrizeRoot)
+    : RNonHomogeneousTreeLikelihood(tree, data, modelSet, rDist, verbose, true, reparametrizeRoot,
+                                    PLK_FLAG_DOUBLE_RECURSIVE) {}
+
+RNonHomogeneousTreeLikelihood::RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data,
+                                                             SubstitutionModelSet* modelSet,
+                                                             DiscreteDistribution* rDist, bool verbose,
+                                                             bool usePatterns, bool, unsigned extraFlags)
     : AbstractPlkTreeLikelihood(tree, rDist, false, verbose, usePatterns), modelSet_(modelSet) {
   if (!modelSet) throw NullPointerException("RNonHomogeneousTreeLikelihood: null model set");
+  extraFlags_ = extraFlags;
   nbStates_ = modelSet->getNumberOfStates();
   for (const Node* n : nodes_) modelOfNodeId_[n->getId()] = (int)modelSet_->getModelIndexForNode(n->getId());
   setData(data);

@@ -5,6 +5,10 @@
 // against the goldens those tests hold.  Exit code 0 = pass (reference convention).
 #include <Bpp/Numeric/Prob/GammaDiscreteDistribution.h>
 #include <Bpp/Phyl/Likelihood/DRHomogeneousTreeLikelihood.h>
+#include <Bpp/Phyl/Likelihood/DRNonHomogeneousTreeLikelihood.h>
+#include <Bpp/Phyl/Likelihood/RNonHomogeneousTreeLikelihood.h>
+#include <Bpp/Phyl/Model/FrequencySet/NucleotideFrequencySet.h>
+#include <Bpp/Phyl/Model/SubstitutionModelSetTools.h>
 #include <Bpp/Phyl/Likelihood/RHomogeneousTreeLikelihood.h>
 #include <Bpp/Phyl/Model/Nucleotide/T92.h>
 #include <Bpp/Phyl/Model/RateDistribution/GammaDiscreteRateDistribution.h>
@@ -146,6 +150,38 @@ static void doubleRecursiveCase() {
   }
 }
 
+// Non-homogeneous (test_likelihood_nh.cpp model set: T92 per branch with its own GC
+// content): the R and DR classes give the same -lnL and the same branch derivatives
+static void nonHomogeneousDrCase() {
+  std::unique_ptr<TreeTemplate<Node> > tree(
+      TreeTemplateTools::parenthesisToTree("(((A:0.01, B:0.02):0.03,C:0.05):0.01,(D:0.1,E:0.04):0.02);"));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  const char* names[] = {"A", "B", "C", "D", "E"};
+  const char* seqs[] = {"AAATGGCTGTGCACGTC", "GACTGGATCTGCACGTC", "CTCTGGATGTGCACGTG", "AAATGGCGGTGCGCCTA",
+                        "AACTGGATGTGCGCGTA"};
+  for (int i = 0; i < 5; i++) aln.addSequence(BasicSequence(names[i], seqs[i], dna));
+  std::map<std::string, std::vector<Vint> > globals;
+  globals["T92.kappa"] = {};
+  std::map<std::string, std::string> alias;
+  std::unique_ptr<SubstitutionModelSet> set(SubstitutionModelSetTools::createNonHomogeneousModelSet(
+      new T92(dna, 3.), new GCFrequencySet(dna), tree.get(), alias, globals));
+  for (size_t k = 0; k < set->getNumberOfModels(); k++)
+    set->setParameterValue("T92.theta_" + std::to_string(k + 1), 0.3 + 0.05 * (double)k);
+  GammaDiscreteRateDistribution rdist(4, 0.8);
+  RNonHomogeneousTreeLikelihood r(*tree, aln, set.get(), &rdist, false);
+  r.initialize();
+  DRNonHomogeneousTreeLikelihood dr(*tree, aln, set.get(), &rdist, false);
+  dr.initialize();
+  expectNear("NH R vs DR -lnL", dr.getValue(), r.getValue(), 1e-12);
+  for (const std::string& name : r.getBranchLengthsParameters().getParameterNames()) {
+    expectNear((std::string("NH R vs DR d1 ") + name).c_str(), dr.getFirstOrderDerivative(name),
+               r.getFirstOrderDerivative(name), 1e-6);
+    expectNear((std::string("NH R vs DR d2 ") + name).c_str(), dr.getSecondOrderDerivative(name),
+               r.getSecondOrderDerivative(name), 1e-6);
+  }
+}
+
 // gaps are not allowed by the model: BadIntException like getInitValue
 static void gapCase() {
   std::unique_ptr<TreeTemplate<Node> > tree(TreeTemplateTools::parenthesisToTree("((A:0.1,B:0.2):0.1,C:0.3);"));
@@ -171,6 +207,7 @@ int main() {
     unrootedGammaCase();
     rootedConstantCase();
     doubleRecursiveCase();
+    nonHomogeneousDrCase();
     gapCase();
   } catch (Exception& e) {
     std::cerr << e.what() << std::endl;
