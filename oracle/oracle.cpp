@@ -652,6 +652,122 @@ int orc_tree_loglik(int n_nodes, int root, const int* son_start, const int* sons
   return 0;
 }
 
+// Double-recursive branch derivatives, restating DRHomogeneousTreeLikelihood
+// (Likelihood/DRHomogeneousTreeLikelihood.cpp): the son-side arrays of every node by the
+// postorder recursion (computeSubtreeLikelihoodPostfix :483-541), the father-side array
+// of every branch at its father excluding the branch (computeLikelihoodAtNode_ :723-816,
+// root frequencies folded in at the root; the father's own father-side array enters
+// through pxy of the father, computeLikelihoodFromArrays :868-940), and per branch and
+// site dL = sum_c p_c sum_x larray[x] sum_y dpxy[x][y] L_node[y] (computeTreeDLikelihoodAtNode
+// :287-328; D2 twin :373-413) divided by the site likelihood.  Flat sites (every column,
+// weight 1), no rescaling.  d1[v] = sum_i dL_i / L_i, d2[v] = sum_i (d2L_i / L_i - (dL_i / L_i)^2)
+// (getFirstOrderDerivative / getSecondOrderDerivative return the negatives, :340-371, 425-456).
+int orc_dr_derivatives(int n_nodes, int root, const int* son_start, const int* sons, const int* leaf_row,
+                       int n_sites, const int* states, int S, int C, int n_codes, const double* init_values,
+                       const double* pmats, const double* dpmats, const double* d2pmats, const double* class_probs,
+                       const double* root_freqs, double* d1, double* d2) {
+  std::vector<std::vector<int> > kids(n_nodes);
+  std::vector<int> father(n_nodes, -1);
+  for (int i = 0; i < n_nodes; i++) {
+    kids[i].assign(sons + son_start[i], sons + son_start[i + 1]);
+    for (int k : kids[i]) father[k] = i;
+  }
+  auto P = [&](const double* m, int n, int c, int x, int y) { return m[(((size_t)n * C + c) * S + x) * S + y]; };
+  // son-side arrays (postfix), postorder by explicit stack
+  std::vector<VVVdouble> down(n_nodes);
+  std::vector<int> order;
+  {
+    std::vector<std::pair<int, size_t> > st(1, std::make_pair(root, (size_t)0));
+    while (!st.empty()) {
+      const int n = st.back().first;
+      if (st.back().second < kids[n].size()) {
+        st.push_back(std::make_pair(kids[n][st.back().second++], (size_t)0));
+        continue;
+      }
+      order.push_back(n);
+      st.pop_back();
+    }
+  }
+  for (int n : order) {
+    VVVdouble& a = down[n];
+    a.assign(n_sites, VVdouble(C, Vdouble(S, 1.)));
+    if (kids[n].empty()) {
+      for (int i = 0; i < n_sites; i++) {
+        const int code = states[(size_t)leaf_row[n] * n_sites + i];
+        if (code < 0 || code >= n_codes) return -2;
+        for (int c = 0; c < C; c++)
+          for (int x = 0; x < S; x++) a[i][c][x] = init_values[(size_t)code * S + x];
+      }
+      continue;
+    }
+    for (int k : kids[n])
+      for (int i = 0; i < n_sites; i++)
+        for (int c = 0; c < C; c++)
+          for (int x = 0; x < S; x++) {
+            double t = 0.;
+            for (int y = 0; y < S; y++) t += P(pmats, k, c, x, y) * down[k][i][c][y];
+            a[i][c][x] *= t;
+          }
+  }
+  // father-side arrays in preorder: up[v] = array at father(v) excluding v
+  std::vector<VVVdouble> up(n_nodes);
+  for (auto it = order.rbegin(); it != order.rend(); ++it) {
+    const int v = *it;
+    if (v == root) continue;
+    const int f = father[v];
+    VVVdouble& a = up[v];
+    a.assign(n_sites, VVdouble(C, Vdouble(S, 1.)));
+    for (int s2 : kids[f]) {
+      if (s2 == v) continue;
+      for (int i = 0; i < n_sites; i++)
+        for (int c = 0; c < C; c++)
+          for (int x = 0; x < S; x++) {
+            double t = 0.;
+            for (int y = 0; y < S; y++) t += P(pmats, s2, c, x, y) * down[s2][i][c][y];
+            a[i][c][x] *= t;
+          }
+    }
+    for (int i = 0; i < n_sites; i++)
+      for (int c = 0; c < C; c++)
+        for (int x = 0; x < S; x++) {
+          if (f == root) {
+            a[i][c][x] *= root_freqs[x];
+          } else {
+            double t = 0.;
+            for (int w = 0; w < S; w++) t += up[f][i][c][w] * P(pmats, f, c, w, x);
+            a[i][c][x] *= t;
+          }
+        }
+  }
+  for (int v = 0; v < n_nodes; v++) {
+    d1[v] = d2[v] = 0.;
+    if (v == root) continue;
+    for (int i = 0; i < n_sites; i++) {
+      double l = 0., dl = 0., d2l = 0.;
+      for (int c = 0; c < C; c++) {
+        double lc = 0., dlc = 0., d2lc = 0.;
+        for (int x = 0; x < S; x++) {
+          double t0 = 0., t1 = 0., t2 = 0.;
+          for (int y = 0; y < S; y++) {
+            t0 += P(pmats, v, c, x, y) * down[v][i][c][y];
+            t1 += P(dpmats, v, c, x, y) * down[v][i][c][y];
+            t2 += P(d2pmats, v, c, x, y) * down[v][i][c][y];
+          }
+          lc += t0 * up[v][i][c][x];
+          dlc += t1 * up[v][i][c][x];
+          d2lc += t2 * up[v][i][c][x];
+        }
+        l += class_probs[c] * lc;
+        dl += class_probs[c] * dlc;
+        d2l += class_probs[c] * d2lc;
+      }
+      d1[v] += dl / l;
+      d2[v] += d2l / l - (dl / l) * (dl / l);
+    }
+  }
+  return 0;
+}
+
 // Number of distinct root patterns (SitePatterns over all leaves).
 int orc_count_patterns(int n_rows, int n_sites, const int* states) {
   std::vector<std::string> cols(n_sites);

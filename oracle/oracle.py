@@ -38,6 +38,8 @@ def load() -> ct.CDLL:
     lib.orc_tree_loglik.argtypes = [ct.c_int, ct.c_int, ip, ip, ip, ct.c_int, ip, ct.c_int, ct.c_int, ct.c_int, dp,
                                     dp, dp, dp, ct.c_int, ct.c_int, ct.c_int, dp, dp, dp, dp]
     lib.orc_count_patterns.argtypes = [ct.c_int, ct.c_int, ip]
+    lib.orc_dr_derivatives.argtypes = [ct.c_int, ct.c_int, ip, ip, ip, ct.c_int, ip, ct.c_int, ct.c_int, ct.c_int,
+                                       dp, dp, dp, dp, dp, dp, dp, dp]
     _lib = lib
     return lib
 
@@ -118,6 +120,29 @@ def tree_loglik(son_start, sons, leaf_row, root, states, init_table, pmats, clas
     if rc != 0:
         raise ValueError(f"oracle error {rc} (state code not allowed by the model?)")
     return lnl.value, sites, tt.value, tr.value
+
+
+def dr_derivatives(son_start, sons, leaf_row, root, states, init_table, pmats, dpmats, d2pmats, class_probs,
+                   root_freqs):
+    """DRHomogeneousTreeLikelihood restatement (orc_dr_derivatives): (d1, d2) per node, d lnL/dt
+    and d2 lnL/dt2 of the branch above each node over all sites (flat, unscaled)."""
+    lib = load()
+    n_nodes = len(leaf_row)
+    states = np.ascontiguousarray(states, dtype=np.int32)
+    S = init_table.shape[1]
+    C = pmats.shape[1]
+    args = [np.ascontiguousarray(x, dtype=np.int32) for x in (son_start, sons, leaf_row)]
+    it = np.ascontiguousarray(init_table, dtype=np.float64)
+    mats = [np.ascontiguousarray(m, dtype=np.float64) for m in (pmats, dpmats, d2pmats)]
+    cp = np.ascontiguousarray(class_probs, dtype=np.float64)
+    rf = np.ascontiguousarray(root_freqs, dtype=np.float64)
+    d1, d2 = np.zeros(n_nodes), np.zeros(n_nodes)
+    rc = lib.orc_dr_derivatives(n_nodes, root, _i(args[0]), _i(args[1]), _i(args[2]), states.shape[1], _i(states), S,
+                                C, it.shape[0], _d(it), _d(mats[0]), _d(mats[1]), _d(mats[2]), _d(cp), _d(rf),
+                                _d(d1), _d(d2))
+    if rc != 0:
+        raise ValueError(f"oracle error {rc} (state code not allowed by the model?)")
+    return d1, d2
 
 
 def count_patterns(states: np.ndarray) -> int:

@@ -199,3 +199,32 @@ def test_path_derivatives_after_incremental_traversal(S, C):
         a1, a2 = eng.branch_derivatives(v)
         e1, e2 = eng2.branch_derivatives(v)
         assert _close(a1, e1, 1e-12) and _close(a2, e2, 1e-12), (v, a1, e1, a2, e2)
+
+
+@pytest.mark.parametrize("S,C,n_taxa,n_pat", [(4, 4, 12, 400), (20, 2, 8, 150), (4, 1, 5, 64)])
+def test_dr_vs_oracle_restatement(S, C, n_taxa, n_pat):
+    """Engine DR pass against the oracle's DRHomogeneousTreeLikelihood restatement
+    (oracle.dr_derivatives, itself pinned by central differences in test_oracle_golden.py)
+    on the same alignment; P, dP, d2P on the oracle side from scipy-free expm of Q
+    (oracle.reversible_pij): relative 1e-10 per branch."""
+    import oracle
+    et, m, alph, rates, probs, states = _random_problem(S, C, n_taxa, n_pat, seed=100 + S + C)
+    eng = engine_for(et, S, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | DR)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    d1, d2 = eng.all_branch_derivatives()
+    P = np.zeros((et.n_nodes, C, S, S))
+    dP, d2P = np.zeros_like(P), np.zeros_like(P)
+    for n in range(et.n_nodes):
+        if n == et.root:
+            continue
+        for c in range(C):
+            p = oracle.reversible_pij(m.Q, m.pi, et.brlen[n] * rates[c])
+            P[n, c], dP[n, c], d2P[n, c] = p, rates[c] * m.Q @ p, rates[c] ** 2 * m.Q @ m.Q @ p
+    ss, sons, lr = et.son_arrays()
+    o1, o2 = oracle.dr_derivatives(ss, sons, lr, et.root, states, alph.init_table, P, dP, d2P, probs, m.pi)
+    for b in br:
+        assert _close(d1[b], o1[b], 1e-10), (b, d1[b], o1[b])
+        assert _close(d2[b], o2[b], 1e-10), (b, d2[b], o2[b])

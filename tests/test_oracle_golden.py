@@ -171,3 +171,55 @@ def test_oracle_scaling_rescues_underflow():
     ok = np.isfinite(s0) & (s0 > -700)   # sites the unscaled arithmetic still resolves
     assert np.allclose(s0[ok], s1[ok], rtol=1e-12)
     assert (~np.isfinite(s0)).any() or (s0 < -700).any()
+
+
+def _dr_problem(seed, n_taxa=9, n_sites=60, C=3):
+    rng = np.random.default_rng(seed)
+    tree = phylo.balanced_tree(n_taxa, seed=seed, lo=0.02, hi=0.4)
+    et = phylo.engine_tree(tree)
+    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
+    rates, probs = phylo.gamma_rates(C, 0.7)
+    states = rng.integers(0, 4, size=(et.n_tips, n_sites)).astype(np.int32)
+    return et, m, rates, probs, states
+
+
+def _pmats(et, m, rates, brlen):
+    C = len(rates)
+    P = np.zeros((et.n_nodes, C, 4, 4))
+    dP, d2P = np.zeros_like(P), np.zeros_like(P)
+    for n in range(et.n_nodes):
+        if n == et.root:
+            continue
+        for c in range(C):
+            p = oracle.reversible_pij(m.Q, m.pi, brlen[n] * rates[c])
+            P[n, c] = p
+            dP[n, c] = rates[c] * m.Q @ p
+            d2P[n, c] = rates[c] ** 2 * m.Q @ m.Q @ p
+    return P, dP, d2P
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_oracle_dr_derivatives_vs_central_differences(seed):
+    """Pins the oracle's DRHomogeneousTreeLikelihood restatement (orc_dr_derivatives) with
+    central differences of its own pruning (orc_tree_loglik), every branch."""
+    et, m, rates, probs, states = _dr_problem(seed)
+    ss, sons, lr = et.son_arrays()
+    P, dP, d2P = _pmats(et, m, rates, et.brlen)
+    d1, d2 = oracle.dr_derivatives(ss, sons, lr, et.root, states, phylo.DNA.init_table, P, dP, d2P, probs, m.pi)
+    assert d1[et.root] == 0.0
+    for v in range(et.n_nodes):
+        if v == et.root:
+            continue
+
+        def lnl_at(t):
+            bl = et.brlen.copy()
+            bl[v] = t
+            pm, _, _ = _pmats(et, m, rates, bl)
+            return oracle.tree_loglik(ss, sons, lr, et.root, states, phylo.DNA.init_table, pm, probs, m.pi,
+                                      use_patterns=False)[0]
+
+        t = et.brlen[v]
+        fd1 = (lnl_at(t + 1e-5) - lnl_at(t - 1e-5)) / 2e-5
+        fd2 = (lnl_at(t + 1e-4) - 2 * lnl_at(t) + lnl_at(t - 1e-4)) / 1e-8
+        assert abs(d1[v] - fd1) <= 1e-6 * max(1.0, abs(fd1)), (v, d1[v], fd1)
+        assert abs(d2[v] - fd2) <= 1e-4 * max(1.0, abs(fd2)), (v, d2[v], fd2)
