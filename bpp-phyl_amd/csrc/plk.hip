@@ -1208,21 +1208,47 @@ bool treeM_direct(plk_handle h) {
   return h->S == 20;
 }
 
-template <int S, int DM>
-void launch_treeM_dm(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
-  const dim3 block(64 * kTreeMGroups * h->C);
+// 16-pattern groups per treeM workgroup.  20 states with direct tables: 1 (16 patterns x C
+// classes, four workgroups per CU, so one workgroup's rescale barriers overlap the others'
+// MFMA chains): cfg3 G = 4 / 2 / 1 = 7.40 / 6.87 / 6.43 ms (profiles/r01/g1_*).
+// PLK_TREEM_G overrides; staged tables and 64 states keep 4.
+int treeM_groups(plk_handle h) {
+  if (h->S != 20 || !treeM_direct(h)) return 4;  // staged tables need 64-pattern workgroups
+  const int g = env_int("PLK_TREEM_G", 1, 1, 4);
+  return g == 3 ? 4 : g;
+}
+
+template <int S, int DM, int G>
+void launch_treeM_g(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
+  const dim3 block(64 * G * h->C);
   const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   if (treeM_direct(h)) {
     if (sc)
-      treeM_kernel<S, DM, true, true><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+      treeM_kernel<S, DM, true, true, G><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
     else
-      treeM_kernel<S, DM, false, true><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+      treeM_kernel<S, DM, false, true, G><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
   } else {
     if (sc)
-      treeM_kernel<S, DM, true, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+      treeM_kernel<S, DM, true, false, G><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
     else
-      treeM_kernel<S, DM, false, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+      treeM_kernel<S, DM, false, false, G><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
   }
+}
+
+template <int S, int DM>
+void launch_treeM_dm(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
+  if constexpr (S == 20) {
+    const int g = treeM_groups(h);
+    if (g == 2 || g == 1) {
+      grid.x = (unsigned)(h->n_pad / (16 * g));
+      if (g == 2)
+        launch_treeM_g<S, DM, 2>(h, a, grid, lds);
+      else
+        launch_treeM_g<S, DM, 1>(h, a, grid, lds);
+      return;
+    }
+  }
+  launch_treeM_g<S, DM, 4>(h, a, grid, lds);
 }
 
 void launch_treeM(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
@@ -1299,9 +1325,9 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   if (kind == FK_TREEM) {
     a.buf_doubles = std::max(h->C * h->S * h->S, h->C * h->n_codes * h->S);
     a.buf_doubles = (a.buf_doubles + 1) & ~1;
-    const int threads = 64 * kTreeMGroups * (h->S == 64 ? 1 : h->C);
+    const int threads = 64 * treeM_groups(h) * (h->S == 64 ? 1 : h->C);
     const int pf = h->S == 64 ? treeM_pf<64>() : treeM_pf<20>();
-    if (a.buf_doubles > pf * threads)
+    if (!treeM_direct(h) && a.buf_doubles > pf * threads)
       return fail(h, PLK_ERR_UNSUPPORTED, "fused MFMA tables (%d doubles) exceed the staging registers",
                   a.buf_doubles);
     a.buf_doubles = std::max(a.buf_doubles, (pf - 1) * threads);  // unconditional stores stay inside
@@ -1318,7 +1344,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // (opt-in PLK_TREEM_CCODES=1: every workgroup stages all cherries but runs one fragment,
     // cfg3 7.64 -> 7.86 ms)
     const int nch = (int)h->cherry3.size() / 3;
-    if (treeM_direct(h) && nch > 0 && h->d_cherry && env_is("PLK_TREEM_CCODES", '1') &&
+    if (treeM_direct(h) && nch > 0 && h->d_cherry && env_is("PLK_TREEM_CCODES", '1') && treeM_groups(h) == 4 &&
         lds_m + (size_t)nch * 128 <= 76 * 1024) {
       a.n_cherry_staged = nch;
       lds_m += (size_t)nch * 128;
@@ -1448,6 +1474,11 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
                                       h->stream, args, nullptr));
     } else if (kind == FK_TREEM) {
       launch_treeM(h, a, grid, lds_m);
+      if (treeM_groups(h) != kTreeMGroups && h->prog_root >= 0 && first + (int)t.size() == h->prog_nf) {
+        // 32-pattern workgroups: the root's 64-pattern wave sums from site_lnl
+        site_wave_sums_kernel<<<(unsigned)(h->n_pad / 256), 256, 0, h->stream>>>(a.site_lnl, a.weights,
+                                                                                 a.wave_sums, a.n_patterns, a.n_pad);
+      }
     } else if (kind == FK_TREES) {
       launch_treeS<20>(h, a, grid);
     } else {

@@ -378,15 +378,18 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
 // Workgroup = C x kTreeMGroups waves; wave w: class c = w / 4, pattern group g = w % 4.
 // S = 64 runs with one class (4 waves, up to 256 VGPRs); S = 20 with up to 4 classes
 // (16 waves, 128 VGPRs = 4 waves per SIMD).  PF = table doubles per thread.
-template <int S>
-constexpr int treeM_threads() { return S == 64 ? 64 * kTreeMGroups : 64 * kTreeMGroups * kTreeMaxWaves; }
+template <int S, int G>
+constexpr int treeM_threads() { return S == 64 ? 64 * G : 64 * G * kTreeMaxWaves; }
 template <int S>
 constexpr int treeM_pf() { return S == 64 ? 17 : 3; }
 
 // DIRECT: no LDS staging and no per-event barrier -- MFMA A operands (P^T) and tip
 // table rows are read by each wave straight from L1/L2 (same values, same order).
-template <int S, int DM, bool SCALE, bool DIRECT>
-__global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, const TInstr* __restrict__ prog,
+// G = 16-pattern groups per workgroup (4: 64 patterns; 2: 32 patterns, two workgroups per
+// CU for S = 20 -- the root's fixed-order 64-pattern wave sums are then formed from
+// site_lnl by site_wave_sums_kernel, same butterfly, same bits).
+template <int S, int DM, bool SCALE, bool DIRECT, int G>
+__global__ __launch_bounds__((treeM_threads<S, G>()), (S == 64 ? 1 : 4)) void treeM_kernel(TreeArgs a, const TInstr* __restrict__ prog,
                                                                    const int32_t* __restrict__ frag_start,
                                                                    const double* __restrict__ pmatsT) {
   constexpr int XT = MShape<S>::XT;
@@ -396,9 +399,9 @@ __global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, c
   __shared__ double red[64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = w / kTreeMGroups, g = w % kTreeMGroups;
+  const int c = w / G, g = w % G;
   const int lr = lane >> 4, lc = lane & 15;
-  const int64_t p0 = (int64_t)blockIdx.x * 64;
+  const int64_t p0 = (int64_t)blockIdx.x * (16 * G);
   const int64_t p = p0 + 16 * g + lc;
   MCtx m;
   m.buf = lds;
@@ -487,7 +490,7 @@ __global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, c
       red[16 * g + lc] = wr;
     }
     __syncthreads();
-    if (w == 0) {
+    if (G == kTreeMGroups && w == 0) {
       // the 64 patterns of the workgroup in root_kernel's butterfly order
       double wr = red[lane];
 #pragma unroll
@@ -495,6 +498,19 @@ __global__ __launch_bounds__(treeM_threads<S>()) void treeM_kernel(TreeArgs a, c
       if (lane == 0) a.wave_sums[p0 >> 6] = wr;
     }
   }
+}
+
+// wave_sums[k] = fixed butterfly over patterns 64k .. 64k + 63 of weights[p] * site_lnl[p]
+// (0 beyond n_patterns): what treeM_kernel<.., 4> forms in its root fragment.
+__global__ __launch_bounds__(256) void site_wave_sums_kernel(const double* __restrict__ site_lnl,
+                                                             const double* __restrict__ weights, double* __restrict__ wave_sums,
+                                                             int64_t n_patterns, int64_t n_pad) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pad) return;  // n_pad is a multiple of 256: whole waves only
+  double wr = p < n_patterns ? weights[p] * site_lnl[p] : 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+  if ((threadIdx.x & 63) == 0) wave_sums[p >> 6] = wr;
 }
 
 // P^T copy: PT[b][c][y][x] = P[b][c][x][y]  (grid: nodes x classes)

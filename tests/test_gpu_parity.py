@@ -785,3 +785,26 @@ def test_treeM_direct_tables_bitwise(S, C, scaling, mode, monkeypatch):
         del eng
     a, b = res["0"], res["1"]
     assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,scaling,mode,n_pat", [(4, True, "lnl_only", 700), (2, False, "materialize", 333),
+                                                  (4, False, "lnl_only", 64)])
+def test_treeM_32_pattern_workgroups_bitwise(C, scaling, mode, n_pat, monkeypatch):
+    """20 states with 32- and 16-pattern workgroups (PLK_TREEM_G=2, 1; root wave sums formed from
+    site_lnl by site_wave_sums_kernel) equal the 64-pattern kernel bitwise."""
+    et, m, alph, rates, probs, states = _random_problem(20, C, 40, n_pat, seed=7 * C + n_pat)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    res = {}
+    for g in ("4", "2", "1"):
+        monkeypatch.setenv("PLK_TREEM_G", g)
+        eng = engine_for(et, 20, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+        lnl, site, blocks = run_engine(eng, et)
+        assert eng.kernel_path() == "treeM"
+        parts = np.stack([eng.get_partials(p) for p, _ in et.ops[-3:]])
+        res[g] = (lnl, site, blocks, parts)
+        del eng
+    a = res["4"]
+    for g in ("2", "1"):
+        b = res[g]
+        assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
