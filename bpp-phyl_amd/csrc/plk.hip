@@ -87,6 +87,7 @@ struct plk_handle_s {
   size_t d_req_cap = 0;
   // pinned host staging: P(t) requests (reused once req_done has passed) and block sums
   char* h_req = nullptr;
+  char* h_req_dev = nullptr;   // device address of the mapped staging (PLK_PMAT_MAPPED)
   size_t h_req_cap = 0;
   hipEvent_t req_done = nullptr;
   double* h_blocks = nullptr;
@@ -728,30 +729,46 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
       inl.branch[i] = branch[i];
       inl.model[i] = model ? model[i] : 0;
     }
-  } else {
+  }
+  // larger requests: pinned staging and a stream-ordered copy into device memory, or with
+  // PLK_PMAT_MAPPED=1 the kernel reads the mapped staging over PCIe (no copy; measured
+  // neutral on cfg3 / cfg5, profiles/r01/mp*_*).  The host rewrites the staging only after
+  // the previous request's reader (req_done) finished.
+  const bool mapped = env_is("PLK_PMAT_MAPPED", '1');
+  const char* req = nullptr;
+  if (inl.n == 0) {
     const size_t bytes = (size_t)n * (2 * sizeof(int32_t) + sizeof(double)) + 64;
-    int rc = ensure_cap(h, &h->d_req, &h->d_req_cap, bytes);
-    if (rc) return rc;
+    if (!mapped) {
+      int rc = ensure_cap(h, &h->d_req, &h->d_req_cap, bytes);
+      if (rc) return rc;
+    }
     if (!h->req_done) HIPCHK(h, hipEventCreateWithFlags(&h->req_done, hipEventDisableTiming));
     HIPCHK(h, hipEventSynchronize(h->req_done));
     if (h->h_req_cap < bytes) {
       if (h->h_req) HIPCHK(h, hipHostFree(h->h_req));
       h->h_req = nullptr;
+      h->h_req_dev = nullptr;
       h->h_req_cap = 0;
-      HIPCHK(h, hipHostMalloc((void**)&h->h_req, bytes, hipHostMallocDefault));
+      HIPCHK(h, hipHostMalloc((void**)&h->h_req, bytes, hipHostMallocMapped));
+      HIPCHK(h, hipHostGetDevicePointer((void**)&h->h_req_dev, h->h_req, 0));
       h->h_req_cap = bytes;
     }
     char* staging = h->h_req;
     std::memcpy(staging + off_t, t, n * sizeof(double));
     std::memcpy(staging + off_b, branch, n * sizeof(int32_t));
     if (model) std::memcpy(staging + off_m, model, n * sizeof(int32_t));
-    HIPCHK(h, hipMemcpyAsync(h->d_req, staging, bytes, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipEventRecord(h->req_done, h->stream));
+    if (mapped) {
+      req = h->h_req_dev;
+    } else {
+      HIPCHK(h, hipMemcpyAsync(h->d_req, staging, bytes, hipMemcpyHostToDevice, h->stream));
+      HIPCHK(h, hipEventRecord(h->req_done, h->stream));
+      req = (const char*)h->d_req;
+    }
   }
   PmatArgs a;
-  a.t = reinterpret_cast<const double*>((char*)h->d_req + off_t);
-  a.branch = reinterpret_cast<const int32_t*>((char*)h->d_req + off_b);
-  a.model = model ? reinterpret_cast<const int32_t*>((char*)h->d_req + off_m) : nullptr;
+  a.t = inl.n ? nullptr : reinterpret_cast<const double*>(req + off_t);
+  a.branch = inl.n ? nullptr : reinterpret_cast<const int32_t*>(req + off_b);
+  a.model = (model && !inl.n) ? reinterpret_cast<const int32_t*>(req + off_m) : nullptr;
   a.rates = h->rates;
   a.V = h->V;
   a.Vinv = h->Vinv;
@@ -781,6 +798,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   else
     pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a, inl);
   HIPCHK(h, hipGetLastError());
+  if (inl.n == 0 && mapped) HIPCHK(h, hipEventRecord(h->req_done, h->stream));  // the kernel read the staging
   if (h->timing & PLK_TIME_PMAT) {
     hipEventRecord(ev.b, h->stream);
     h->events.push_back(ev);
@@ -2314,11 +2332,15 @@ int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
   hipSetDevice(h->device);
   int rc = validate_ops(h, ops, n_ops);
   if (rc) return rc;
-  h->trav_ops.assign(ops, ops + n_ops);
-  for (int i = 0; i < n_ops; ++i) {
-    std::vector<int>& k = h->topo_kids[ops[i].parent];
-    if (!(ops[i].flags & PLK_OP_ACCUMULATE)) k.clear();
-    k.insert(k.end(), ops[i].child, ops[i].child + ops[i].n_children);
+  // merge the op list into the tree (skipped when it repeats the last call's list, the
+  // common case of an optimiser's evaluations)
+  if (h->trav_ops.size() != (size_t)n_ops || std::memcmp(h->trav_ops.data(), ops, n_ops * sizeof(plk_op)) != 0) {
+    h->trav_ops.assign(ops, ops + n_ops);
+    for (int i = 0; i < n_ops; ++i) {
+      std::vector<int>& k = h->topo_kids[ops[i].parent];
+      if (!(ops[i].flags & PLK_OP_ACCUMULATE)) k.clear();
+      k.insert(k.end(), ops[i].child, ops[i].child + ops[i].n_children);
+    }
   }
   if (h->flags & PLK_FLAG_SUBTREE_PATTERNS) return update_compressed(h, ops, n_ops);
   if (tree4_supported(h) && fusable(ops, n_ops)) return update_tree4(h, ops, n_ops);
