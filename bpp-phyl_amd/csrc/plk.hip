@@ -938,14 +938,16 @@ int build_cherry_tables(plk_handle h) {
     HIPCHK(h, hipStreamSynchronize(h->stream));  // `tips` goes out of scope
     h->cherry_codes_valid = true;
   }
-  const dim3 grid((unsigned)((U * U + 63) / 64), (unsigned)(nch * C));
+  // rows per workgroup: 64-row passes sharing one P^T staging (PLK_CHERRY_ROWS, default 256)
+  const int rows = 64 * std::max(1, env_int("PLK_CHERRY_ROWS", 256, 64, 4096) / 64);
+  const dim3 grid((unsigned)((U * U + rows - 1) / rows), (unsigned)(nch * C));
   const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   if (S == 20) {
-    if (sc) cherry_table_kernel<20, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
-    else cherry_table_kernel<20, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+    if (sc) cherry_table_kernel<20, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
+    else cherry_table_kernel<20, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
   } else if (S == 64) {
-    if (sc) cherry_table_kernel<64, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
-    else cherry_table_kernel<64, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry);
+    if (sc) cherry_table_kernel<64, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
+    else cherry_table_kernel<64, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
   } else {
     return fail(h, PLK_ERR_UNSUPPORTED, "cherry tables for %d states", S);
   }

@@ -116,7 +116,8 @@ template <int S, bool SCALE>
 __global__ __launch_bounds__(256) void cherry_table_kernel(const double* __restrict__ tipP,
                                                            const double* __restrict__ pmatsT,
                                                            const int32_t* __restrict__ cherry3, int C, int U,
-                                                           CherryLayout lay, uint8_t* __restrict__ cherry) {
+                                                           CherryLayout lay, uint8_t* __restrict__ cherry,
+                                                           int rows_per_wg) {
   constexpr int XT = MShape<S>::XT;
   __shared__ double PTl[S * S];
   const int lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
@@ -126,7 +127,9 @@ __global__ __launch_bounds__(256) void cherry_table_kernel(const double* __restr
     for (int i = threadIdx.x; i < S * S; i += blockDim.x) PTl[i] = PT[i];
     __syncthreads();
   }
-  const int r = blockIdx.x * 64 + (threadIdx.x >> 6) * 16 + lc;  // this lane's row (code pair)
+  // each workgroup stages P^T once and covers rows_per_wg code pairs, 64 per pass
+  for (int r0 = blockIdx.x * rows_per_wg; r0 < min(U2, (int)(blockIdx.x + 1) * rows_per_wg); r0 += 64) {
+  const int r = r0 + (threadIdx.x >> 6) * 16 + lc;  // this lane's row (code pair)
   const bool rv = r < U2;
   const int ca = rv ? r / U : 0, cb = rv ? r % U : 0;
   const int ta = cherry3[3 * k], tb = cherry3[3 * k + 1], node = cherry3[3 * k + 2];
@@ -169,6 +172,7 @@ __global__ __launch_bounds__(256) void cherry_table_kernel(const double* __restr
         if (m_valid<S>(xt, q, lr)) row[16 * xt + lr + 4 * q] = d[xt][q];
     if (c == 0 && lr == 0) base[lay.table_bytes + r] = (uint8_t)cnt;
   }
+  }  // row passes
 }
 
 template <int S>
