@@ -793,7 +793,9 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     hipEventRecord(ev.a, h->stream);
   }
   const size_t lds = (size_t)(h->S + (tips_fused ? 2 : 1) * S2) * sizeof(double);
-  if (k64)
+  if (k64 && !env_is("PLK_PMAT64_SPLIT", '0'))
+    pmat64s_kernel<<<dim3(n, h->C, 4), dim3(256), (size_t)(64 + 16 * 64 + S2) * sizeof(double), h->stream>>>(a, inl);
+  else if (k64)
     pmat64_kernel<<<dim3(n, h->C), dim3(256), (size_t)(64 + 2 * S2) * sizeof(double), h->stream>>>(a, inl);
   else
     pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a, inl);

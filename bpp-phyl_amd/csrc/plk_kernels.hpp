@@ -614,6 +614,67 @@ __global__ __launch_bounds__(256) void pmat64_kernel(PmatArgs a, const PmatInlin
   }
 }
 
+// pmat64_kernel split over four 16-row slabs of P (blockIdx.z): 4x the workgroups, so a
+// tree's few hundred branches fill the device several deep instead of one workgroup per CU.
+// Every element is the same sum in the same order as in pmat64_kernel (bitwise).
+__global__ __launch_bounds__(256) void pmat64s_kernel(PmatArgs a, const PmatInline inl) {
+  constexpr int S = 64, R = 16;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int i = blockIdx.x, c = blockIdx.y, x0 = R * blockIdx.z;
+  const int b = inl.n ? inl.branch[i] : a.branch[i];
+  const int m = inl.n ? inl.model[i] : (a.model ? a.model[i] : 0);
+  const double tt = (inl.n ? inl.t[i] : a.t[i]) * a.rates[c];
+  double* e = sm;
+  double* Vm = sm + S;      // rows x0 .. x0 + R - 1 of V
+  double* Vi = Vm + R * S;  // all of Vinv
+  const double* V = a.V + (size_t)m * S * S;
+  const double* VI = a.Vinv + (size_t)m * S * S;
+  const double* lam = a.lambda + (size_t)m * S;
+  for (int k = threadIdx.x; k < S; k += blockDim.x) e[k] = exp(lam[k] * tt);
+  for (int k = threadIdx.x; k < R * S; k += blockDim.x) Vm[k] = V[x0 * S + k];
+  for (int k = threadIdx.x; k < S * S; k += blockDim.x) Vi[k] = VI[k];
+  __syncthreads();
+  const int xr = threadIdx.x >> 4, yb = threadIdx.x & 15;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k < S; ++k) {
+    const double ek = e[k];
+    const double vx = Vm[xr * S + k];
+    double vy[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) vy[v] = Vi[k * S + yb + 16 * v];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) p[v] = __builtin_fma(vx * vy[v], ek, p[v]);
+  }
+  double* out = a.P + ((size_t)b * a.C + c) * S * S;
+  const int x = x0 + xr;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int y = yb + 16 * v;
+    p[v] = tt == 0.0 ? (x == y ? 1.0 : 0.0) : p[v];  // getPij_t: t == 0 -> identity
+    out[x * S + y] = p[v];
+  }
+  if (a.init && b < a.n_tips) {
+    __syncthreads();  // done with Vm / Vi
+    double* Pl = Vm;  // [R][y]
+    double* In = Vi;  // [code][y], n_codes <= 64 (launch guarantees)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) Pl[xr * S + yb + 16 * v] = p[v];
+    for (int k = threadIdx.x; k < a.n_codes * S; k += blockDim.x) In[k] = a.init[k];
+    __syncthreads();
+    double* tout = a.tipP + ((size_t)b * a.C + c) * a.n_codes * S;
+    const int xl = threadIdx.x & 15, cb = 4 * (threadIdx.x >> 4);
+    double t[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int y = 0; y < S; ++y) {
+      const double px = Pl[xl * S + y];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = __builtin_fma(px, cb + u < a.n_codes ? In[(cb + u) * S + y] : 0.0, t[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (cb + u < a.n_codes) tout[(cb + u) * S + x0 + xl] = t[u];
+  }
+}
+
 // tip tables for 64 states: tip_table_kernel's sums (y ascending) with P and the code
 // table staged in LDS and 4 codes x 4 states per thread
 __global__ __launch_bounds__(256) void tip_table64_kernel(const double* __restrict__ P, const double* __restrict__ init,

@@ -753,16 +753,18 @@ def test_pmat64_kernels_bitwise(monkeypatch):
     kernels' results bitwise: every P(t) and the traversal's lnL."""
     et, m, alph, rates, probs, states = _random_problem(64, 1, 24, 500, seed=64, amb=True)
     out = {}
-    for on in ("0", "1"):
+    for on, split in (("0", "1"), ("1", "0"), ("1", "1")):  # generic, pmat64_kernel, pmat64s_kernel
         monkeypatch.setenv("PLK_PMAT64", on)
+        monkeypatch.setenv("PLK_PMAT64_SPLIT", split)
         eng = engine_for(et, 64, 1, 500, states, alph.init_table, rates, probs, m.pi, [m],
                          flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY)
         lnl, site, _ = run_engine(eng, et)
         P = np.stack([eng.get_pmatrix(c) for _, ch in et.ops for c in ch])
-        out[on] = (lnl, site, P)
+        out[on + split] = (lnl, site, P)
         del eng
-    assert out["0"][0] == out["1"][0] and np.array_equal(out["0"][1], out["1"][1])
-    assert np.array_equal(out["0"][2], out["1"][2])
+    for k in ("10", "11"):
+        assert out["01"][0] == out[k][0] and np.array_equal(out["01"][1], out[k][1])
+        assert np.array_equal(out["01"][2], out[k][2])
 
 
 @pytest.mark.gpu
