@@ -2205,12 +2205,21 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
         h->pmats, h->pmats, (S == 20 || S == 64) ? h->pmatsT : nullptr, h->pi, h->d_drm, mat_base, C, S);
     HIPCHK(h, hipGetLastError());
   }
+  // S = 20 / 64 reduce on fp64 MFMA (64-pattern blocks) unless PLK_DR_MFMA=0
+  const bool dr_mfma = (S == 20 || S == 64) && !env_is("PLK_DR_MFMA", '0');
+  // tips whose father has one other son and a father of its own: U_v formed inside the
+  // reduction (S <= 4 kernel), never stored (PLK_DR_FUSE=0 stores every U_v)
+  std::vector<char> fused(nn, 0);
+  if (!dr_mfma && S <= 4 && !env_is("PLK_DR_FUSE", '0'))
+    for (int v = 0; v < nt; ++v)
+      if (parent[v] >= 0 && parent[v] != root && h->topo_kids[parent[v]].size() == 2) fused[v] = 1;
   // U_v for every non-root node, one launch per (depth, child chunk)
   std::vector<KOp> flat;
   std::vector<std::pair<size_t, int> > launches;
   for (size_t d = 1; d < depth.size(); ++d) {
     std::vector<std::vector<KOp> > chunks;
     for (int v : depth[d]) {
+      if (fused[v]) continue;
       const int f = parent[v];
       std::vector<int> ck_tip, ck_child, ck_branch;
       if (f != root) {
@@ -2260,10 +2269,18 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
       b.child = v < nt ? v : v - nt;
       b.uslot = h->dr_slot0 + v;
       b.use_pi = parent[v] == root;
+      if (fused[v]) {
+        const int f = parent[v];
+        const int sb = h->topo_kids[f][0] == v ? h->topo_kids[f][1] : h->topo_kids[f][0];
+        b.fuse = 1;
+        b.uf_slot = h->dr_slot0 + f;
+        b.mf = mat_base + f;
+        b.sib_tip = sb < nt;
+        b.sib = sb < nt ? sb : sb - nt;
+        b.sib_branch = sb;
+      }
       br.push_back(b);
     }
-  // S = 20 / 64 reduce on fp64 MFMA (64-pattern blocks) unless PLK_DR_MFMA=0
-  const bool dr_mfma = (S == 20 || S == 64) && !env_is("PLK_DR_MFMA", '0');
   const int n_blk = (int)(h->n_pad / (dr_mfma ? 64 : kDrThreads));
   if ((rc = ensure_cap(h, (void**)&h->d_drb, &h->d_drb_cap, br.size() * sizeof(DrBranch)))) return rc;
   if ((rc = ensure_cap(h, (void**)&h->dr_blk, &h->dr_blk_cap, 2 * br.size() * n_blk * sizeof(double)))) return rc;
@@ -2280,6 +2297,8 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   a.pi = h->pi;
   a.probs = h->probs;
   a.weights = h->weights;
+  a.tipP = h->tipP;
+  a.n_codes = h->n_codes;
   a.blk1 = h->dr_blk;
   a.blk2 = h->dr_blk + br.size() * n_blk;
   a.slot_stride = h->slot_stride;
@@ -2288,7 +2307,6 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   a.C = C;
   a.n_blk = n_blk;
   a.G = 3 * (size_t)C * S * S * sizeof(double) <= 96 * 1024 ? C : 1;
-  a.pad_ = 0;
   const dim3 grid((unsigned)n_blk, (unsigned)br.size());
   const size_t lds = 3 * (size_t)a.G * S * S * sizeof(double);
   EventPair ev;

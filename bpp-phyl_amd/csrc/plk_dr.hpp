@@ -51,7 +51,16 @@ struct DrBranch {
   int32_t child;   // tip index or internal slot of v
   int32_t uslot;   // slot of U_v
   int32_t use_pi;  // v is a child of the root
-  int32_t pad_[3];
+  // fuse = 1 (a tip whose father f has exactly one other son s and a father of its own):
+  // U_v = (M_f U_f) (*) (P_s L_s) is formed here instead of being written by the preorder
+  // pass and read back -- the upper vectors of such tips are never stored
+  int32_t fuse;
+  int32_t uf_slot;     // slot of U_f
+  int32_t mf;          // matrix index of M_f
+  int32_t sib_tip;     // s is a tip (row of its tip table) or internal (P_s L_s)
+  int32_t sib;         // tip index or internal slot of s
+  int32_t sib_branch;  // node index of s (its P)
+  int32_t pad_;
 };
 
 struct DrArgs {
@@ -64,6 +73,7 @@ struct DrArgs {
   const double* pi;
   const double* probs;
   const double* weights;
+  const double* tipP;         // [n_tips][C][n_codes][S] (fused tips' siblings)
   double* blk1;               // [branch][n_blk] block sums of w l'/l
   double* blk2;               // [branch][n_blk] block sums of w (l''/l - (l'/l)^2)
   int64_t slot_stride;
@@ -72,7 +82,7 @@ struct DrArgs {
   int32_t C;
   int32_t n_blk;
   int32_t G;                  // classes staged in LDS at a time
-  int32_t pad_;
+  int32_t n_codes;
 };
 
 constexpr int kDrThreads = 256;
@@ -119,8 +129,63 @@ __global__ __launch_bounds__(kDrThreads) void dr_branch_kernel(const DrBranch* _
 #pragma unroll
           for (int z = 0; z < S; ++z) L[z] = src[(size_t)z * kTile];
         }
-        const double* U = a.partials + (size_t)b.uslot * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
         double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        if constexpr (S <= 4) {
+        double uu[S];
+        if (b.fuse) {
+          const size_t co = ((size_t)tile * CS + c * S) * kTile + q;
+          const double* Uf = a.partials + (size_t)b.uf_slot * a.slot_stride + co;
+          const double* Mf = a.pmats + ((size_t)b.mf * a.C + c) * S * S;
+          double uf[S], sv[S];
+#pragma unroll
+          for (int w = 0; w < S; ++w) uf[w] = Uf[(size_t)w * kTile];
+          if (b.sib_tip) {
+            const double* row =
+                a.tipP + (((size_t)b.sib * a.C + c) * a.n_codes + a.codes[(size_t)b.sib * a.n_pad + p]) * S;
+#pragma unroll
+            for (int y = 0; y < S; ++y) sv[y] = row[y];
+          } else {
+            const double* Ls = a.partials + (size_t)b.sib * a.slot_stride + co;
+            const double* Ps = a.pmats + ((size_t)b.sib_branch * a.C + c) * S * S;
+            double ls[S];
+#pragma unroll
+            for (int z = 0; z < S; ++z) ls[z] = Ls[(size_t)z * kTile];
+#pragma unroll
+            for (int y = 0; y < S; ++y) {
+              double t = 0.0;
+#pragma unroll
+              for (int z = 0; z < S; ++z) t = fma(Ps[y * S + z], ls[z], t);
+              sv[y] = t;
+            }
+          }
+#pragma unroll
+          for (int y = 0; y < S; ++y) {
+            double t = 0.0;
+#pragma unroll
+            for (int w = 0; w < S; ++w) t = fma(Mf[y * S + w], uf[w], t);
+            uu[y] = t * sv[y];
+          }
+        } else {
+          const double* U = a.partials + (size_t)b.uslot * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
+#pragma unroll
+          for (int y = 0; y < S; ++y) uu[y] = b.use_pi ? U[(size_t)y * kTile] * a.pi[y] : U[(size_t)y * kTile];
+        }
+#pragma unroll
+        for (int y = 0; y < S; ++y) {
+          double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+#pragma unroll
+          for (int z = 0; z < S; ++z) {
+            t0 = fma(sP[y * S + z], L[z], t0);
+            t1 = fma(sD[y * S + z], L[z], t1);
+            t2 = fma(sD2[y * S + z], L[z], t2);
+          }
+          const double u = uu[y];
+          s0 = fma(u, t0, s0);
+          s1 = fma(u, t1, s1);
+          s2 = fma(u, t2, s2);
+        }
+        } else {
+        const double* U = a.partials + (size_t)b.uslot * a.slot_stride + ((size_t)tile * CS + c * S) * kTile + q;
         for (int y = 0; y < S; ++y) {
           double t0 = 0.0, t1 = 0.0, t2 = 0.0;
 #pragma unroll
@@ -133,6 +198,7 @@ __global__ __launch_bounds__(kDrThreads) void dr_branch_kernel(const DrBranch* _
           s0 = fma(u, t0, s0);
           s1 = fma(u, t1, s1);
           s2 = fma(u, t2, s2);
+        }
         }
         l0 = fma(a.probs[c], s0, l0);
         l1 = fma(a.probs[c], s1, l1);
