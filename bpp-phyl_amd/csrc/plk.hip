@@ -966,7 +966,7 @@ int tree_levels(plk_handle h) {
     case FK_TREES: return env_int("PLK_TREES_DM", 2, 2, 4);
     // S = 20: 3 levels (with cherry tables 7.8 ms on cfg3, 2 levels 8.7 ms although DM = 3
     // spills a few registers at 128 VGPRs)
-    case FK_TREEM: return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 2, 2, 3);
+    case FK_TREEM: return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 3, 2, 3);
     default: return 1;
   }
 }
