@@ -2307,7 +2307,7 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   a.C = C;
   a.n_blk = n_blk;
   a.G = 3 * (size_t)C * S * S * sizeof(double) <= 96 * 1024 ? C : 1;
-  const dim3 grid((unsigned)n_blk, (unsigned)br.size());
+  dim3 grid((unsigned)n_blk, (unsigned)br.size());
   const size_t lds = 3 * (size_t)a.G * S * S * sizeof(double);
   EventPair ev;
   if (h->timing & PLK_TIME_PARTIALS) {
@@ -2315,11 +2315,16 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
     hipEventRecord(ev.a, h->stream);
   }
   if (dr_mfma) {
-    const size_t lds_m = 3 * (size_t)S * S * sizeof(double);
+    DrArgs am = a;
+    am.G = 3 * (size_t)C * S * S * sizeof(double) <= 64 * 1024 ? C : 1;
+    const size_t lds_m = 3 * (size_t)am.G * S * S * sizeof(double);
+    // a few workgroups per branch, each looping over pattern blocks (PLK_DR_WGS total)
+    const int want = env_int("PLK_DR_WGS", 4096, 1, 1 << 20);
+    grid.x = (unsigned)std::min<int64_t>(n_blk, std::max<int64_t>(1, (want + (int)br.size() - 1) / (int)br.size()));
     if (S == 20)
-      dr_branch_mfma_kernel<20><<<grid, kDrmThreads, lds_m, h->stream>>>(h->d_drb, a);
+      dr_branch_mfma_kernel<20><<<grid, kDrmThreads, lds_m, h->stream>>>(h->d_drb, am);
     else
-      dr_branch_mfma_kernel<64><<<grid, kDrmThreads, lds_m, h->stream>>>(h->d_drb, a);
+      dr_branch_mfma_kernel<64><<<grid, kDrmThreads, lds_m, h->stream>>>(h->d_drb, am);
   } else {
     switch (S) {
       case 2: dr_branch_kernel<2><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;

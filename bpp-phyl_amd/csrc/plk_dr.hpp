@@ -250,24 +250,35 @@ __global__ __launch_bounds__(kDrmThreads) void dr_branch_mfma_kernel(const DrBra
   const DrBranch b = branches[blockIdx.y];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int lr = lane >> 4, lc = lane & 15;
-  const int64_t p = (int64_t)blockIdx.x * 64 + 16 * g + lc;
+  // persistent over the branch's 64-pattern blocks: the matrices are staged once per
+  // workgroup (not once per block) when all classes fit
+  bool staged = false;
+  for (int64_t blk = blockIdx.x; blk < a.n_blk; blk += gridDim.x) {
+  const int64_t p = blk * 64 + 16 * g + lc;
   const bool live = p < a.n_patterns;
   const int64_t tile = p >> 7, q = p & (kTile - 1);
   const int CS = a.C * S;
-  double* sP = lds;
-  double* sD = lds + S * S;
-  double* sD2 = lds + 2 * S * S;
   double l0 = 0.0, l1 = 0.0, l2 = 0.0;
+  // classes staged G at a time (all of them when 3 C S^2 doubles fit the launch's LDS)
   for (int c = 0; c < a.C; ++c) {
-    __syncthreads();
-    const size_t mo = ((size_t)b.node * a.C + c) * S * S;
-    for (int i = threadIdx.x; i < S * S; i += kDrmThreads) {
-      const int x = i / S, y = i - x * S;  // source [x][y] -> LDS [y][x]
-      sP[y * S + x] = a.pmats[mo + i];
-      sD[y * S + x] = a.dpmats[mo + i];
-      sD2[y * S + x] = a.d2pmats[mo + i];
+    const int cc = c % a.G;
+    if (cc == 0 && !(staged && a.G == a.C)) {
+      const int g = min(a.G, a.C - c);
+      staged = true;
+      __syncthreads();
+      for (int i = threadIdx.x; i < g * S * S; i += kDrmThreads) {
+        const int k = i / (S * S), e = i - k * S * S;
+        const int x = e / S, y = e - x * S;  // source [x][y] -> LDS [y][x]
+        const size_t mo = ((size_t)b.node * a.C + c + k) * S * S + e;
+        lds[(3 * k) * S * S + y * S + x] = a.pmats[mo];
+        lds[(3 * k + 1) * S * S + y * S + x] = a.dpmats[mo];
+        lds[(3 * k + 2) * S * S + y * S + x] = a.d2pmats[mo];
+      }
+      __syncthreads();
     }
-    __syncthreads();
+    const double* sP = lds + (3 * cc) * S * S;
+    const double* sD = lds + (3 * cc + 1) * S * S;
+    const double* sD2 = lds + (3 * cc + 2) * S * S;
     MAcc<S> src;
     if (b.is_tip) {
       const double* row = a.code_table + (size_t)a.codes[(size_t)b.child * a.n_pad + p] * S;
@@ -332,9 +343,11 @@ __global__ __launch_bounds__(kDrmThreads) void dr_branch_mfma_kernel(const DrBra
       t1 += red[0][k];
       t2 += red[1][k];
     }
-    a.blk1[(size_t)blockIdx.y * a.n_blk + blockIdx.x] = t1;
-    a.blk2[(size_t)blockIdx.y * a.n_blk + blockIdx.x] = t2;
+    a.blk1[(size_t)blockIdx.y * a.n_blk + blk] = t1;
+    a.blk2[(size_t)blockIdx.y * a.n_blk + blk] = t2;
   }
+  __syncthreads();  // red[] and (G < C) the staged matrices are reused by the next block
+  }  // blocks
 }
 
 // Per branch: the fixed-order sum of its block sums (strided partial sums, then a
