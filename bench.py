@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--config", default="gtr_g4_dna_1M_64", choices=sorted(workload.CONFIGS))
     ap.add_argument("--patterns", type=int, default=None, help="override patterns per rank")
     ap.add_argument("--cpu-sample", type=int, default=None, help="patterns in the CPU-baseline sample")
-    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-reps", type=int, default=10, help="traversals per CPU-baseline variant (~10-15 s of CPU work for cfg2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="A/B: time the steps without per-kernel HIP events")
     ap.add_argument("--event-every", type=int, default=4,
