@@ -455,6 +455,11 @@ extern "C" {
 
 int plk_abi_version(void) { return PLK_ABI_VERSION; }
 
+#ifndef PLK_SOURCE_HASH
+#define PLK_SOURCE_HASH "unknown"
+#endif
+const char* plk_build_id(void) { return PLK_SOURCE_HASH; }
+
 int plk_block_size(void) { return kRootBlock; }
 
 int plk_device_count(int* count) {

@@ -29,7 +29,7 @@ PLK_TIME_PARTIALS, PLK_TIME_PMAT, PLK_TIME_ROOT = 1, 2, 4
 
 # every symbol include/plk.h declares
 EXPORTS = [
-    "plk_abi_version", "plk_device_count", "plk_last_error", "plk_create", "plk_destroy",
+    "plk_abi_version", "plk_build_id", "plk_device_count", "plk_last_error", "plk_create", "plk_destroy",
     "plk_set_code_table", "plk_set_tip_codes", "plk_set_pattern_weights", "plk_set_category_rates",
     "plk_set_root_frequencies", "plk_set_eigen", "plk_update_pmatrices", "plk_set_pmatrix",
     "plk_get_pmatrix", "plk_update_partials", "plk_get_partials", "plk_root_loglik", "plk_block_size",
@@ -63,6 +63,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
     dp, ip = P(ct.c_double), P(ct.c_int32)
     sig = {
         "plk_abi_version": ([], ct.c_int),
+        "plk_build_id": ([], ct.c_char_p),
         "plk_device_count": ([P(ct.c_int)], ct.c_int),
         "plk_last_error": ([ct.c_void_p], ct.c_char_p),
         "plk_create": ([ct.c_int, ct.c_int, ct.c_int, ct.c_int64, ct.c_int, ct.c_int, ct.c_int, ct.c_uint,
@@ -97,6 +98,27 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         f.restype = res
     _lib = lib
     return lib
+
+
+def source_hash() -> str:
+    """The build id libplk.so should report when built from the sources beside it
+    (same recipe as bpp-phyl_amd/Makefile: SHA-256 over csrc/*.hip, csrc/*.hpp in sorted
+    order, then include/plk.h; first 16 hex digits)."""
+    import glob
+    import hashlib
+
+    csrc = os.path.join(_HERE, "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp")))
+    files.append(os.path.join(os.path.dirname(_HERE), "include", "plk.h"))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> str:
+    return load().plk_build_id().decode()
 
 
 def _d(a: np.ndarray):
@@ -216,13 +238,16 @@ class Engine:
     def evaluate(self, branches: np.ndarray, t: np.ndarray, ops, root: int, models: Optional[np.ndarray] = None):
         """plk_evaluate: P(t) of `branches`, the traversal `ops`, the root reduction in one
         call.  Returns (lnL, block_sums).  The branch / model index arrays are converted
-        once per array object (an optimiser loop passes the same ones every time)."""
-        key = (id(branches), id(models))
-        if self._eval_cache is None or self._eval_cache[0] != key or self._eval_cache[1] is not branches:
+        once per array object (an optimiser loop passes the same ones every time): the
+        cache holds strong references to the caller's objects and matches them by
+        identity, so a freed array's id can never alias a new one.  Index arrays must not
+        be mutated in place between calls (they are treated as immutable)."""
+        c = self._eval_cache
+        if c is None or c[0] is not branches or c[1] is not models:
             b = np.ascontiguousarray(branches, dtype=np.int32)
             m = None if models is None else np.ascontiguousarray(models, dtype=np.int32)
             nb = (self.P + self.lib.plk_block_size() - 1) // self.lib.plk_block_size()
-            self._eval_cache = (key, branches, b, m, b.ctypes.data_as(ct.POINTER(ct.c_int32)),
+            self._eval_cache = (branches, models, b, m, b.ctypes.data_as(ct.POINTER(ct.c_int32)),
                                 None if m is None else m.ctypes.data_as(ct.POINTER(ct.c_int32)), np.empty(nb))
         _, _, b, _, bp, mp, blocks_buf = self._eval_cache
         tt = t if (t.dtype == np.float64 and t.flags.c_contiguous) else np.ascontiguousarray(t, dtype=np.float64)

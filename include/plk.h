@@ -114,6 +114,10 @@ typedef struct plk_handle_s* plk_handle;
 
 /* Library / device */
 int plk_abi_version(void);
+/* First 16 hex digits of the SHA-256 of the library's sources (csrc/*.hip, csrc/*.hpp in
+ * sorted order, then this header), fixed at compile time: lets a caller check that the
+ * loaded binary was built from the sources it ships with. */
+const char* plk_build_id(void);
 int plk_device_count(int* count);
 const char* plk_last_error(plk_handle h); /* h may be NULL: last global error */
 

@@ -5,8 +5,11 @@ Three kinds of vectors:
                      (test/test_likelihood.cpp:108, test/test_likelihood_clock.cpp:115)
                      plus the inputs those tests use (trees, alignments, model params).
   pmatrix.npz     -- P(t) = expm(Q t) via scipy.linalg.expm (Pade, independent of every
-                     eigen-decomposition in this repo) for T92, GTR and LG08 generators
-                     built from the reference's parameterisations.
+                     eigen-decomposition in this repo) for T92, GTR, LG08 and YN98
+                     generators built from the reference's parameterisations.  The YN98
+                     generator is restated here from the reference chain on its own
+                     (yn98_Q below), not taken from phylo.yn98, so the fixture also pins
+                     the product's codon generator.
   pruning.npz     -- per-site log-likelihoods of small seeded trees/alignments computed
                      here by a straightforward numpy pruning (per-site, no pattern
                      compression) on the expm matrices above, for T92, GTR and LG08 with
@@ -70,6 +73,44 @@ def t92_Q(kappa, theta):
     return phylo.t92(kappa, theta).Q
 
 
+# Standard genetic code in the reference's codon numbering 16*n1 + 4*n2 + n3 over ACGT
+# (bpp-seq StandardGeneticCode; '*' = stop: TAA = 48, TAG = 50, TGA = 56).
+STD_CODE = "KNKNTTTTRSRSIIMIQHQHPPPPRRRRLLLLEDEDAAAAGGGGVVVV*Y*YSSSS*CWCLFLF"
+
+
+def yn98_Q(kappa, omega):
+    """YN98 generator on 64 codon states, restated from the reference chain:
+    YN98 (Model/Codon/YN98.cpp:51-78) = CodonDistanceFrequenciesSubstitutionModel over
+    K80(kappa) on every codon position; AbstractWordSubstitutionModel::fillBasicGenerator
+    (Model/AbstractWordSubstitutionModel.cpp:355-390) puts the nucleotide rate on codons that
+    differ at exactly one position; AbstractCodonSubstitutionModel::completeMatrices
+    (Model/Codon/AbstractCodonSubstitutionModel.cpp:174-190) zeroes stop rows/columns and
+    multiplies by getCodonsMulRate = (omega if non-synonymous,
+    AbstractCodonDistanceSubstitutionModel.cpp:80-88) x pi_j
+    (AbstractCodonFrequenciesSubstitutionModel.cpp:82-85); F3X4 with equal nucleotide
+    frequencies gives pi = 1/61 on sense codons.  Normalised to -sum pi_i Q_ii = 1
+    (Model/AbstractSubstitutionModel.cpp:645-690); K80's own scale cancels there."""
+    sense = np.array([a != "*" for a in STD_CODE])
+    pi = sense / sense.sum()
+    Q = np.zeros((64, 64))
+    transition = {(0, 2), (2, 0), (1, 3), (3, 1)}   # A<->G, C<->T
+    for i in range(64):
+        for j in range(64):
+            if i == j or not (sense[i] and sense[j]):
+                continue
+            di = [(i >> s) & 3 for s in (4, 2, 0)]
+            dj = [(j >> s) & 3 for s in (4, 2, 0)]
+            pos = [k for k in range(3) if di[k] != dj[k]]
+            if len(pos) != 1:
+                continue
+            r = kappa if (di[pos[0]], dj[pos[0]]) in transition else 1.0
+            if STD_CODE[i] != STD_CODE[j]:
+                r *= omega
+            Q[i, j] = r * pi[j]
+    Q[np.diag_indices(64)] = -Q.sum(axis=1)
+    return Q / -(np.diag(Q) @ pi), pi
+
+
 def np_pruning(et, states, init_table, Pfun, C, probs, pi):
     """Per-site pruning, straightforward numpy: partial[node] = prod_son P_son @ L_son."""
     n_sites = states.shape[1]
@@ -101,6 +142,11 @@ def main():
         out[f"{name}_pi"] = m.pi
         out[f"{name}_t"] = ts
         out[f"{name}_P"] = np.stack([expm(m.Q * t) for t in ts])
+    # YN98(kappa=2, omega=0.3), config 4's model: expm on the full 64 x 64 generator (stop
+    # rows and columns are zero, so their rows of P(t) are unit rows)
+    Qy, piy = yn98_Q(2.0, 0.3)
+    out["YN98_Q"], out["YN98_pi"], out["YN98_t"] = Qy, piy, ts
+    out["YN98_P"] = np.stack([expm(Qy * t) for t in ts])
     np.savez_compressed(os.path.join(HERE, "pmatrix.npz"), **out)
 
     # ---- pruning fixtures on small seeded problems
@@ -108,12 +154,14 @@ def main():
     cases = [("T92", mods["T92"], 6, 40, 4, 1.0, phylo.DNA),
              ("GTR", mods["GTR"], 9, 60, 4, 0.5, phylo.DNA),
              ("GTRamb", mods["GTR"], 7, 50, 4, 0.7, phylo.DNA),
-             ("LG08", mods["LG08"], 8, 30, 4, 0.5, phylo.PROTEIN)]
+             ("LG08", mods["LG08"], 8, 30, 4, 0.5, phylo.PROTEIN),
+             ("YN98", phylo.Model("YN98", 64, Qy, piy, None, None, None), 7, 40, 1, None, phylo.CODON)]
     for name, m, ntaxa, nsites, C, alpha, alph in cases:
         tree = phylo.balanced_tree(ntaxa, seed=int(rng.integers(1 << 30)), lo=0.02, hi=0.3)
         et = phylo.engine_tree(tree)
-        rates, probs = phylo.gamma_rates(C, alpha)
-        states = phylo.simulate(et, [m], None, rates, nsites, seed=int(rng.integers(1 << 30)))
+        rates, probs = phylo.gamma_rates(C, alpha) if C > 1 else (np.ones(1), np.ones(1))
+        sim = m if m.V is not None else phylo.Model(name, m.S, m.Q, m.pi, *phylo.reversible_eigen(m.Q, m.pi))
+        states = phylo.simulate(et, [sim], None, rates, nsites, seed=int(rng.integers(1 << 30)))
         if name == "GTRamb":   # sprinkle ambiguity codes (4..14)
             mask = rng.random(states.shape) < 0.1
             states[mask] = rng.integers(4, 15, size=mask.sum())

@@ -42,6 +42,14 @@ def test_library_loads_and_reports_version():
     assert lib.plk_block_size() == 4096
 
 
+def test_library_built_from_these_sources():
+    """The loaded libplk.so carries the hash of the sources beside it (Makefile recipe), so
+    a stale binary cannot pass for HEAD's code -- here and, through the gpu twin in
+    tests/test_gpu_configs.py, on the GPU box that receives the prebuilt library."""
+    _ensure_built()
+    assert plk.build_id() == plk.source_hash()
+
+
 def test_code_object_is_gfx950():
     _ensure_built()
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", plk.LIB_PATH], capture_output=True,

@@ -86,11 +86,14 @@ def check(lnl_g, site_g, lnl_o, site_o, rel=REL):
 
 # ---------------------------------------------------------------- transition matrices (K4)
 
-@pytest.mark.parametrize("name", ["T92", "GTR", "LG08"])
+@pytest.mark.parametrize("name", ["T92", "GTR", "LG08", "YN98"])
 def test_pmatrix_kernel_vs_expm(name):
+    """K4 against the scipy expm fixtures; YN98 runs the 64-state pmat64s_kernel that
+    config 4's bench line times (C = 1, stop states as null rows)."""
     f = np.load(os.path.join(GOLD, "pmatrix.npz"))
     m = {"T92": phylo.t92(3.0, 0.5), "GTR": phylo.gtr(a=1.2, b=0.4, c=0.6, d=0.8, e=0.5, piA=0.30, piC=0.20,
-                                                          piG=0.25, piT=0.25), "LG08": phylo.lg08()}[name]
+                                                          piG=0.25, piT=0.25), "LG08": phylo.lg08(),
+         "YN98": phylo.yn98(2.0, 0.3)}[name]
     ts = f[f"{name}_t"]
     et = phylo.engine_tree(phylo.balanced_tree(8))
     eng = plk.Engine(0, m.S, 1, 256, et.n_tips, et.n_internal, 1)
@@ -166,8 +169,9 @@ def test_closed_form_pmatrix_path():
 # ---------------------------------------------------------------- committed pruning fixtures
 
 @pytest.mark.parametrize("name,alph", [("T92", phylo.DNA), ("GTR", phylo.DNA), ("GTRamb", phylo.DNA),
-                                        ("LG08", phylo.PROTEIN)])
-def test_pruning_fixtures(name, alph):
+                                        ("LG08", phylo.PROTEIN), ("YN98", phylo.CODON)])
+@pytest.mark.parametrize("extra", [0, plk.PLK_FLAG_LNL_ONLY])
+def test_pruning_fixtures(name, alph, extra):
     f = np.load(os.path.join(GOLD, "pruning.npz"))
     g = {k[len(name) + 1:]: f[k] for k in f.files if k.startswith(name + "_")}
     # rebuild the engine tree from the fixture arrays
@@ -180,7 +184,7 @@ def test_pruning_fixtures(name, alph):
     V, Vinv, lam = phylo.reversible_eigen(Q, pi)
     m = phylo.Model(name, Q.shape[0], Q, pi, V, Vinv, lam)
     eng = engine_for(et, m.S, len(g["rates"]), g["states"].shape[1], g["states"], alph.init_table, g["rates"],
-                     g["probs"], pi, [m])
+                     g["probs"], pi, [m], flags=plk.PLK_FLAG_NONNEG_GUARD | extra)
     lnl, site, _ = run_engine(eng, et)
     assert np.allclose(site, g["site_lnl"], rtol=REL, atol=0)
     assert abs(lnl - float(g["lnl"])) <= REL * abs(lnl)

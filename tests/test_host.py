@@ -69,6 +69,19 @@ def test_host_yn98_properties(host_records):
         assert np.allclose(P, oracle.reversible_pij(Q, pi, t), atol=1e-12)
 
 
+def test_host_yn98_vs_expm_fixture(host_records):
+    """The C++ mirror's YN98 (config 4's model) against the fixture built from the
+    independent restatement in tests/golden/make_golden.py: generator, frequencies, and
+    P(t) through both getPij_t and the eigen-system."""
+    f = np.load(os.path.join(GOLD, "pmatrix.npz"))
+    r = _models(host_records)["YN98"]
+    assert np.allclose(np.array(r["Q"]).reshape(64, 64), f["YN98_Q"], atol=1e-14)
+    assert np.allclose(r["pi"], f["YN98_pi"], atol=1e-16)
+    for P, Pe, Pf in zip(r["P"], r["P_eigen"], f["YN98_P"]):
+        assert np.allclose(np.array(P).reshape(64, 64), Pf, atol=1e-13)
+        assert np.allclose(np.array(Pe).reshape(64, 64), Pf, atol=1e-13)
+
+
 def test_host_trees(host_records):
     trees = [r for r in host_records if r["kind"] == "tree"]
     assert trees[0]["leaves"] == ["A", "B", "C", "D"] and not trees[0]["rooted"]
@@ -108,11 +121,13 @@ def test_engine_tree_unroots_and_clamps():
     assert et2.n_internal == 62 and len(et.ops) == et.n_internal
 
 
-@pytest.mark.parametrize("name", ["T92", "GTR", "LG08"])
+@pytest.mark.parametrize("name", ["T92", "GTR", "LG08", "YN98"])
 def test_python_models_vs_expm(name):
     f = np.load(os.path.join(GOLD, "pmatrix.npz"))
     m = {"T92": phylo.t92(3.0, 0.5), "GTR": phylo.gtr(1.2, 0.4, 0.6, 0.8, 0.5, 0.30, 0.20, 0.25, 0.25),
-         "LG08": phylo.lg08()}[name]
+         "LG08": phylo.lg08(), "YN98": phylo.yn98(2.0, 0.3)}[name]
+    if name == "YN98":
+        assert np.allclose(m.Q, f["YN98_Q"], atol=1e-14) and np.allclose(m.pi, f["YN98_pi"], atol=1e-16)
     for t, P in zip(f[f"{name}_t"], f[f"{name}_P"]):
         assert np.allclose(m.pij(t), P, atol=1e-13)
 

@@ -92,7 +92,7 @@ def test_t92_closed_form_vs_expm():
         assert np.allclose(oracle.t92_pij(2.0, 0.3, t), P, atol=1e-14)
 
 
-@pytest.mark.parametrize("name", ["GTR", "LG08", "T92"])
+@pytest.mark.parametrize("name", ["GTR", "LG08", "T92", "YN98"])
 def test_reversible_pij_vs_expm(name):
     f = np.load(os.path.join(GOLD, "pmatrix.npz"))
     Q, pi = f[f"{name}_Q"], f[f"{name}_pi"]
@@ -131,7 +131,7 @@ def _oracle_fixture(g, alph, use_patterns=True, scaling=False):
 
 
 @pytest.mark.parametrize("name,alph", [("T92", phylo.DNA), ("GTR", phylo.DNA), ("GTRamb", phylo.DNA),
-                                        ("LG08", phylo.PROTEIN)])
+                                        ("LG08", phylo.PROTEIN), ("YN98", phylo.CODON)])
 @pytest.mark.parametrize("use_patterns", [True, False])
 def test_oracle_vs_numpy_pruning(name, alph, use_patterns):
     g = _fixture_case(name)
