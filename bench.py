@@ -11,11 +11,16 @@ nodes).  Weak scaling: every rank evaluates its own 1M-pattern slice of one glob
 synthetic alignment (patterns are independent), so per-GPU work is fixed as N grows.
 
 One step = one likelihood evaluation as RHomogeneousTreeLikelihood::fireParameterChanged
-does it: all branch transition matrices (K4), the full postorder traversal (partials
-kernel, one launch per tree level), the root reduction (K5) whose fixed-order
-4096-pattern block sums are all-gathered over RCCL and summed in global order (the
-only cross-GPU exchange).  value = (P x I x K x N) / max-over-ranks wall time of the
-K timed steps, inputs already resident in HBM.
+does it (plk_evaluate): all branch transition matrices (K4), the full postorder
+traversal -- by default (--mode lnl) the fused, tree-specialised kernel that keeps
+interior partials in registers and reads cherries from code-pair tables -- and the root
+reduction, whose fixed-order 4096-pattern block sums are all-gathered across ranks and
+summed in global order (the only cross-GPU exchange).  value = (P x I x K x N) /
+max-over-ranks wall time of the K timed steps, inputs already resident in HBM; this is
+the reference-equivalent rate (the reference computes every one of those node
+updates).  computed_updates_* report the updates actually computed per pattern
+(cherry-table nodes are lookups, SURVEY 8(d) "effective"), and roofline.executed the
+fp64 work the kernels really issue (plk_traversal_work, counted from the program).
 """
 from __future__ import annotations
 
@@ -47,7 +52,7 @@ def parse():
     ap.add_argument("--config", default="gtr_g4_dna_1M_64", choices=sorted(workload.CONFIGS))
     ap.add_argument("--patterns", type=int, default=None, help="override patterns per rank")
     ap.add_argument("--cpu-sample", type=int, default=None, help="patterns in the CPU-baseline sample")
-    ap.add_argument("--cpu-reps", type=int, default=10, help="traversals per CPU-baseline variant (~10-15 s of CPU work for cfg2)")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU-baseline traversals per variant (median, after 1 warm-up)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="A/B: time the steps without per-kernel HIP events")
     ap.add_argument("--event-every", type=int, default=4,
@@ -64,13 +69,34 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(wl, n_sample: int, reps: int, eng_sites=None):
+def host_cpu() -> dict:
+    """CPU model and core counts of this host (state them)."""
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except Exception:
+        usable = os.cpu_count()
+    return {"model": model, "nproc": os.cpu_count(), "usable_cores": usable}
+
+
+def cpu_baseline(wl, n_sample: int, runs: int, eng_sites=None):
     """The oracle (faithful C++11 -O2 -g restatement of computeSubtreeLikelihood with the
-    reference's nested-vector layout, usePatterns=true -- the reference default) timed on
-    one host core over a bounded sample of the same workload."""
+    reference's nested-vector layout) timed on ONE pinned host core over a bounded sample
+    of the same workload: median of `runs` traversals after 1 warm-up, for
+    usePatterns = true (the reference default, per-subtree pattern compression) and
+    false.  The reference itself cannot be built here."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test/bench infrastructure only
 
+    cpu = host_cpu()
     try:
         os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
     except Exception:
@@ -87,12 +113,17 @@ def cpu_baseline(wl, n_sample: int, reps: int, eng_sites=None):
     ss, sons, lr = et.son_arrays()
     res, sites = {}, None
     for up in (True, False):
-        _, site, t_trav, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, wl.alphabet.init_table, pm, wl.probs,
-                                                wl.root_freqs, use_patterns=up, scaling=wl.scaling, n_rep=reps,
-                                                want_sites=up)
-        res[up] = n_sample * et.n_internal / t_trav
-        if up:
-            sites = site
+        times = []
+        for r in range(runs + 1):   # the first run is the warm-up
+            _, site, t_trav, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, wl.alphabet.init_table, pm,
+                                                    wl.probs, wl.root_freqs, use_patterns=up, scaling=wl.scaling,
+                                                    n_rep=1, want_sites=up and r == 0)
+            if r == 0:
+                if up:
+                    sites = site
+                continue
+            times.append(t_trav)
+        res[up] = n_sample * et.n_internal / float(np.median(times))
     parity = None
     if eng_sites is not None:
         # SURVEY 8(d)'s third figure, on the sample: the GPU's per-pattern lnL vs the oracle's
@@ -105,10 +136,10 @@ def cpu_baseline(wl, n_sample: int, reps: int, eng_sites=None):
         "unit": "site-pattern x node partial updates/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"{n_sample} patterns of the same workload ({et.n_tips} taxa, I={et.n_internal}), "
+        "sample": (f"{n_sample} patterns of the same workload ({et.n_tips} taxa, I={et.n_internal}); "
                    f"oracle/oracle.cpp computeSubtreeLikelihood restatement, g++ -O2 -g, usePatterns=true "
-                   f"(reference default), median-free mean of {reps} traversals on 1 pinned core of "
-                   f"{platform.processor() or platform.machine()}"),
+                   f"(reference default); median of {runs} traversals after 1 warm-up on 1 pinned core"),
+        "host_cpu": cpu,
         "value_use_patterns_false": res[False],
         "parity_vs_oracle": parity,
     }
@@ -116,71 +147,89 @@ def cpu_baseline(wl, n_sample: int, reps: int, eng_sites=None):
 
 FP64_PEAK_TFS = 78.6   # MI355X fp64 peak, vector and matrix alike (AMD spec sheet; the guide lists no fp64 row)
 RIDGE = FP64_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop/B
+TRAFFIC_FILES = ("profiles/r02/traffic.json", "profiles/traffic.json")
 
 
-def measured_traffic(config, mode, P, launches_per_step):
-    """HBM bytes per partials launch from the committed PMC passes (profiles/traffic.json,
-    keyed config/mode), rescaled to this run's pattern count."""
-    prof = os.path.join(ROOT, "profiles", "traffic.json")
-    try:
-        tr = json.load(open(prof)).get(f"{config}/{mode}")
-    except Exception:
-        return None, None
-    if not tr:
-        return None, None
-    per_traversal = tr["hbm_bytes_per_traversal"] * P / tr["patterns"]
-    return per_traversal / launches_per_step, tr["source"]
+def measured_traffic(config, mode, P):
+    """HBM bytes per traversal (traversal + table launches) from the committed PMC passes
+    (keyed config/mode), rescaled to this run's pattern count."""
+    for rel in TRAFFIC_FILES:
+        try:
+            tr = json.load(open(os.path.join(ROOT, rel))).get(f"{config}/{mode}")
+        except Exception:
+            tr = None
+        if tr:
+            return tr["hbm_bytes_per_traversal"] * P / tr["patterns"], tr["source"]
+    return None, None
 
 
-def roofline(wl, mode, P, steps, part_s, launches, bytes_pattern, flops_pattern, traffic):
-    """Roofline of the partials kernel.  achieved = algorithmic bytes (or flops) per launch
-    (SURVEY 8(d) per-pattern figures x patterns) / mean launch duration (HIP events).
-    The binding ceiling follows the bytes the design actually moves: the fused traversal
-    (mode lnl, 4 states) keeps interior partials in registers, so it moves ~N+8 B/pattern
-    and is fp64-compute bound; the materialising paths stream every partial through HBM
-    (intensity <= 7.6 flop/B < the 9.8 flop/B ridge) and are HBM bound."""
-    if part_s <= 0:
+def roofline(wl, mode, P, ev_steps, tm, work, traffic):
+    """Roofline of one traversal: the traversal launches plus the table builds that feed
+    them (cherry_table_kernel), timed with HIP events on the handle's stream.
+
+    achieved: SURVEY 8(d)'s algorithmic work per traversal (flops for the fused lnL-only
+    traversal, which keeps interior partials in registers and is fp64 bound; bytes for
+    the materialising paths, which stream every partial through HBM) / traversal time.
+    executed: the fp64 flops the kernels actually issue, counted from the program that
+    ran (plk_traversal_work) -- lower than algorithmic where cherries are table lookups,
+    higher where MFMA tiles carry padding rows (20 states in 32-row tiles).
+    hbm: the bytes the kernels really move (PMC FETCH/WRITE, profiles/) / traversal time.
+    algorithmic_bytes_equiv: SURVEY 8(d)'s materialised-partials byte basis as a rate --
+    an equivalence, not a hardware rate, for the fused traversal (it never moves them)."""
+    part_ms, tab_ms = tm["partials_ms"], tm.get("tables_ms", 0.0)
+    if part_ms <= 0:
         return None
-    per_launch_s = part_s / launches
-    pat_per_launch = P * steps / launches
-    gbs = bytes_pattern * pat_per_launch / per_launch_s / 1e9
-    tfs = flops_pattern * pat_per_launch / per_launch_s / 1e12
-    fused = mode == "lnl" and wl.S == 4 and wl.C in (1, 2, 4)  # tree4_supported() in plk.hip
-    if traffic:
-        intensity = flops_pattern * pat_per_launch / traffic
-        compute_bound = intensity > RIDGE
-    else:
-        compute_bound = fused
-    hbm = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-           "traffic": traffic,
-           "basis": (f"algorithmic {bytes_pattern} B/pattern/traversal = 16*C*S*I + N + 8 "
-                     f"({bytes_pattern / wl.et.n_internal:.1f} B/update) x {pat_per_launch:.0f} patterns per launch "
-                     f"/ mean HIP-event launch duration")}
+    t_s = (part_ms + tab_ms) * 1e-3 / ev_steps
+    launches = tm["launches"] / ev_steps
+    bytes_pattern = wl.algorithmic_bytes_per_pattern()
+    flops_pattern = wl.algorithmic_flops_per_pattern()
+    alg_flops = flops_pattern * P
+    alg_bytes = bytes_pattern * P
+    fused = mode == "lnl"
     if mode == "materialize" and wl.S == 4 and wl.C in (1, 2, 4):
         # the fused traversal writing every partial: children come from registers, so the
         # bytes are the writes (8*C*S per internal node) plus codes, weight and site lnL
-        mb = 8 * wl.C * wl.S * wl.et.n_internal + wl.et.n_tips + 16
-        g2 = mb * pat_per_launch / per_launch_s / 1e9
-        hbm.update(achieved=g2, frac=g2 / HBM_PEAK_GBS,
-                   basis=(f"fused traversal writing every partial: {mb} B/pattern = 8*C*S*I writes + N tip codes "
-                          f"+ 8 weight + 8 site lnL x {pat_per_launch:.0f} patterns per launch / mean HIP-event "
-                          f"launch duration"))
-    if fused:
-        # the fused traversal's own bytes: tip codes (1 B per tip), weight in, site lnL out
-        fb = wl.et.n_tips + 16
-        g2 = fb * pat_per_launch / per_launch_s / 1e9
-        hbm.update(achieved=g2, frac=g2 / HBM_PEAK_GBS,
-                   basis=(f"fused traversal: {fb} B/pattern = N tip codes + 8 weight + 8 site lnL "
-                          f"x {pat_per_launch:.0f} patterns per launch / mean HIP-event launch duration"))
-    mf = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / FP64_PEAK_TFS,
-          "traffic": traffic,
-          "basis": (f"algorithmic {flops_pattern} flop/pattern/traversal = 2*C*S^2 per internal child + (k-1)*C*S "
-                    f"per combine ({flops_pattern / wl.et.n_internal:.1f} flop/update) x {pat_per_launch:.0f} "
-                    f"patterns per launch / mean HIP-event launch duration; peak = fp64 (vector = matrix) spec")}
-    main, alt = (mf, hbm) if compute_bound else (hbm, mf)
-    main = dict(main)
-    main["other_ceiling"] = {k: alt[k] for k in ("bound", "achieved", "peak", "unit", "frac")}
-    main["launch_ms"] = per_launch_s * 1e3
+        alg_bytes = (8 * wl.C * wl.S * wl.et.n_internal + wl.et.n_tips + 16) * P
+    if traffic:
+        compute_bound = alg_flops / traffic > RIDGE
+    else:
+        compute_bound = fused
+    ex = None
+    if work:
+        issued = work["issued_flops"] + work["table_flops"]
+        ex = {"useful_flops_per_traversal": work["useful_flops"], "issued_flops_per_traversal": work["issued_flops"],
+              "table_flops_per_traversal": work["table_flops"],
+              "achieved": issued / t_s / 1e12, "unit": "TFLOP/s", "frac": issued / t_s / 1e12 / FP64_PEAK_TFS,
+              "useful_frac": (work["useful_flops"] + work["table_flops"]) / t_s / 1e12 / FP64_PEAK_TFS,
+              "counted_from_program": bool(work["exact"])}
+    hbm = None
+    if traffic:
+        g = traffic / t_s / 1e9
+        hbm = {"achieved": g, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g / HBM_PEAK_GBS,
+               "bytes_per_traversal": traffic}
+    if compute_bound:
+        main = {"bound": "mfma", "achieved": alg_flops / t_s / 1e12, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                "basis": (f"algorithmic {flops_pattern} flop/pattern/traversal = 2*C*S^2 per internal child + "
+                          f"(k-1)*C*S per combine ({flops_pattern / wl.et.n_internal:.1f} flop/update) x {P} "
+                          f"patterns / traversal time ({launches:.0f} traversal launch(es) + table builds, HIP "
+                          f"events); peak = fp64 spec (vector = matrix on MI355X)")}
+    else:
+        main = {"bound": "hbm", "achieved": alg_bytes / t_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "basis": (f"algorithmic {alg_bytes / P:.0f} B/pattern/traversal x {P} patterns / traversal time "
+                          f"({launches:.0f} launch(es), HIP events)")}
+    main["frac"] = main["achieved"] / main["peak"]
+    main["traffic"] = traffic
+    main["traversal_ms"] = t_s * 1e3
+    main["launch_ms"] = part_ms / tm["launches"]
+    main["table_ms_per_traversal"] = tab_ms / ev_steps
+    main["executed"] = ex
+    main["hbm"] = hbm
+    if compute_bound:
+        main["algorithmic_bytes_equiv"] = {
+            "GB/s": bytes_pattern * P / t_s / 1e9,
+            "note": (f"SURVEY 8(d) byte basis {bytes_pattern} B/pattern (every partial written and read once) "
+                     f"as a rate; the fused traversal does not move these bytes (see hbm), so this is an "
+                     f"equivalence, not a fraction of the HBM peak")}
     return main
 
 
@@ -214,24 +263,25 @@ def main():
     extra = {"lnl": plk.PLK_FLAG_LNL_ONLY, "materialize": 0, "levelwise": plk.PLK_FLAG_LEVELWISE,
              "subtree": plk.PLK_FLAG_SUBTREE_PATTERNS}[args.mode]
     ev = workload.Evaluator(wl, device, start, end, extra_flags=extra)
+    xchg = shard.BlockExchange(dist, ev.n_blocks, device=coll_dev) if dist is not None else None
     t_setup = time.time() - t_setup
     units_step = P * wl.et.n_internal
 
     def one_step():
         lnl, _, blocks = ev.step()
-        if dist is None:
+        if xchg is None:
             return lnl  # plk_evaluate already summed the block sums in the fixed global order
-        # the one cross-GPU exchange: RCCL all-gather of fixed-order block sums
-        return shard.allgather_lnl(blocks, dist, device=coll_dev)
+        # the one cross-GPU exchange: all-gather of fixed-order block sums
+        return xchg.lnl(blocks)
 
     for _ in range(args.warmup):
         lnl = one_step()
     ev.eng.reset_timing()
-    # HIP events around the partials launches only (each timed launch adds an event pair),
-    # on every K-th timed step: the kernel's mean launch duration is sampled inside the
-    # timed region without charging every step the events' own stream time
+    # HIP events around the traversal launches and their table builds only (each timed
+    # launch adds an event pair), on every K-th timed step: the kernels' mean durations are
+    # sampled inside the timed region without charging every step the events' stream time
     k_ev = max(1, args.event_every)
-    mask = 0 if args.no_events else plk.PLK_TIME_PARTIALS
+    mask = 0 if args.no_events else (plk.PLK_TIME_PARTIALS | plk.PLK_TIME_TABLES)
     ev_steps = 0
     if dist is not None:
         dist.barrier()
@@ -258,30 +308,16 @@ def main():
     if rank == 0:
         ms_step = elapsed * 1e3 / args.steps
         value = units_step * world * args.steps / elapsed
-        bytes_pattern = wl.algorithmic_bytes_per_pattern()
-        flops_pattern = wl.algorithmic_flops_per_pattern()
-        part_s = tm["partials_ms"] * 1e-3
-        launches = max(tm["launches"], 1)
-        traffic, traffic_src = measured_traffic(args.config, args.mode, P, launches / ev_steps)
-        roof = roofline(wl, args.mode, P, ev_steps, part_s, launches, bytes_pattern, flops_pattern, traffic)
+        work = ev.eng.traversal_work()
+        traffic, traffic_src = measured_traffic(args.config, args.mode, P)
+        roof = roofline(wl, args.mode, P, ev_steps, tm, work, traffic) if not args.no_events else None
         if roof:
             roof["event_sample"] = f"HIP events on {ev_steps} of {args.steps} timed steps (every {k_ev})"
-        if traffic_src and roof:
-            roof["traffic_source"] = traffic_src
-        computed = None
-        if args.mode == "subtree":
-            # per-subtree compression computes fewer node updates than it is credited with;
-            # the roofline is then priced on the updates actually computed
-            computed = ev.eng.compressed_work()
-            if roof:
-                f = computed / units_step
-                roof["achieved"] *= f
-                roof["frac"] *= f
-                roof["basis"] += f"; scaled to the {computed} node updates actually computed per traversal"
-                roof.pop("other_ceiling", None)
+            if traffic_src:
+                roof["traffic_source"] = traffic_src
+        computed = work["node_updates"]
         rec = {
-            "metric": ("site-pattern x node partial updates/s" if args.mode != "subtree" else
-                       "site-pattern x node partial updates/s (EFFECTIVE: per-subtree pattern compression)"),
+            "metric": "site-pattern x node partial updates/s",
             "value": value,
             "unit": "updates/s",
             "n_gpus": world,
@@ -306,20 +342,30 @@ def main():
                 "parallelism": f"pattern-shard x{world}",
             },
             "lnl": lnl,
-            "partials_only_updates_per_s": units_step * ev_steps / part_s if part_s > 0 else None,
-            "kernel_ms_per_step": {"partials": tm["partials_ms"] / ev_steps, "pmatrix": tm["pmat_ms"] / ev_steps,
-                                   "root": tm["root_ms"] / ev_steps},
-            "partials_launches_per_step": launches / ev_steps,
+            "kernel_path": ev.eng.kernel_path(),
+            # node updates the kernels compute per pattern (cherry-table nodes and
+            # per-subtree compression are lookups / skipped) -- value above is the
+            # reference-equivalent ("effective") rate
+            "computed_updates_per_step": computed * world,
+            "computed_updates_per_s": computed * world * args.steps / elapsed,
+            "table_nodes": work["table_nodes"],
+            "partials_only_updates_per_s": (units_step * ev_steps / (tm["partials_ms"] * 1e-3)
+                                            if tm["partials_ms"] > 0 else None),
+            "kernel_ms_per_step": {"partials": tm["partials_ms"] / max(ev_steps, 1),
+                                   "tables": tm["tables_ms"] / max(ev_steps, 1),
+                                   "pmatrix": tm["pmat_ms"] / max(ev_steps, 1),
+                                   "root": tm["root_ms"] / max(ev_steps, 1)},
+            "partials_launches_per_step": tm["launches"] / max(ev_steps, 1),
+            "table_launches_per_step": tm["table_launches"] / max(ev_steps, 1),
             "roofline": roof,
             "setup_s": t_setup,
         }
-        if computed is not None:
-            rec["computed_updates_per_step"] = computed
-            rec["computed_updates_per_s"] = computed * world * args.steps / elapsed
+        if args.mode == "subtree":
+            rec["metric"] += " (EFFECTIVE: per-subtree pattern compression)"
         if world == 1 and not args.no_cpu_baseline:
             ns = args.cpu_sample or workload.CONFIGS[args.config]["cpu_sample"]
             _, eng_sites, _ = ev.eng.root_loglik(wl.et.root, want_sites=True)
-            rec["cpu_baseline"] = cpu_baseline(wl, min(ns, P), args.cpu_reps, eng_sites)
+            rec["cpu_baseline"] = cpu_baseline(wl, min(ns, P), args.cpu_runs, eng_sites)
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -40,7 +40,7 @@ std::string g_last_error;
 
 struct EventPair {
   hipEvent_t a, b;
-  int kind;  // 0 partials, 1 pmat, 2 root
+  int kind;  // 0 partials, 1 pmat, 2 root, 3 tables
 };
 
 }  // namespace
@@ -102,8 +102,9 @@ struct plk_handle_s {
   unsigned timing = 0;  // PLK_TIME_* mask
   std::vector<EventPair> events;
   std::vector<EventPair> event_pool;
-  int64_t n_launches = 0;
-  double acc_ms[3] = {0, 0, 0};
+  int64_t n_launches = 0, n_table_launches = 0;
+  double acc_ms[4] = {0, 0, 0, 0};
+  int jit_last_gx = 0;                    // workgroups per fragment of the last JIT launch
   std::string last_error;
   // host copy of the op list last uploaded to d_ops (re-used when identical)
   std::vector<KOp> h_ops;
@@ -1317,8 +1318,20 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   }
   if (kind == FK_TREEM) {
     int rc = ensure_pmatsT(h);
-    if (!rc) rc = build_cherry_tables(h);
     if (rc) return rc;
+    EventPair tev;
+    const bool timed = (h->timing & PLK_TIME_TABLES) && !h->cherry3.empty();
+    if (timed) {
+      tev = get_events(h, 3);
+      hipEventRecord(tev.a, h->stream);
+    }
+    rc = build_cherry_tables(h);
+    if (rc) return rc;
+    if (timed) {
+      hipEventRecord(tev.b, h->stream);
+      h->events.push_back(tev);
+      h->n_table_launches++;
+    }
   }
   TreeArgs a;
   a.cherry = h->d_cherry;
@@ -1496,6 +1509,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         wgs = h->jit_resident;
       }
       const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, wgs);
+      h->jit_last_gx = (int)gx;
       HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
                                       (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
@@ -1941,6 +1955,107 @@ int launch_partials_ops(plk_handle h, const KOp* d_ops, int n_ops) {
 
 int materialize_last_traversal(plk_handle h);
 void topo_postorder(plk_handle h, int root, std::vector<plk_op>& ops);
+
+// plk_traversal_work: the program that served the last traversal, walked on the host.
+void traversal_work(plk_handle h, plk_work* w) {
+  const int S = h->S, C = h->C, nt = h->n_tips;
+  const double P = (double)h->n_pad;
+  std::memset(w, 0, sizeof(*w));
+  w->patterns = h->n_patterns;
+  // internal nodes of the last traversal and the algorithmic count
+  double alg = 0.0;
+  {
+    std::vector<int> nk(h->n_nodes, 0), ni(h->n_nodes, 0);
+    for (const plk_op& o : h->trav_ops)
+      for (int k = 0; k < o.n_children; ++k) {
+        nk[o.parent]++;
+        if (o.child[k] >= nt) ni[o.parent]++;
+      }
+    for (int n = 0; n < h->n_nodes; ++n)
+      if (nk[n]) {
+        w->internal_nodes++;
+        alg += (double)C * (2.0 * S * S * ni[n] + (double)(nk[n] - 1) * S);
+      }
+  }
+  w->node_updates = h->n_patterns * (int64_t)w->internal_nodes;
+  w->useful_flops = w->issued_flops = alg * P;
+  if (h->kernel_path == "subtree_patterns") {
+    w->node_updates = h->cmp_work;
+    const double f = w->internal_nodes ? (double)h->cmp_work / ((double)h->n_patterns * w->internal_nodes) : 0.0;
+    w->useful_flops = w->issued_flops = alg * P * f;
+    return;
+  }
+  if (h->kernel_path == "jit_tree4" && h->jit_plan_valid) {
+    // contrib: per class and state 1 mul + (S - 1) FMA, then a multiply unless it is the
+    // node's first contribution (an assignment); a table row: S multiplies unless first
+    double per = 0.0, tab = 0.0;
+    int64_t tnodes = 0, rows = 0;
+    const int U = h->n_codes;
+    for (size_t f = 0; f < h->jit_plan.events.size(); ++f) {
+      std::vector<char> fresh(256, 0);
+      fresh[0] = 1;
+      for (const JitEvent& e : h->jit_plan.events[f]) {
+        const int d = e.level;
+        if (e.op == T_TIP) {
+          if (!fresh[d]) per += S;
+          fresh[d] = 0;
+        } else if (e.op == T_LOAD) {
+          per += (double)S * (2 * S - 1) + (fresh[d] ? 0 : S);
+          fresh[d] = 0;
+        } else if (e.op == T_DESCEND) {
+          fresh[d] = 1;
+        } else if (e.op == T_ASCEND) {
+          per += (double)S * (2 * S - 1) + (fresh[d - 1] ? 0 : S);
+          fresh[d - 1] = 0;
+        }
+      }
+      for (const JitUnit& u : h->jit_plan.units[f]) {
+        if (u.tb < 0) continue;
+        tnodes++;
+        rows += (int64_t)U * U * C;
+        tab += (double)C * U * U * (S + (u.br >= 0 ? (double)S * (2 * S - 1) : 0.0));
+      }
+    }
+    w->useful_flops = w->issued_flops = per * C * P;
+    w->table_nodes = tnodes;
+    w->table_rows = rows;
+    w->table_flops = tab * std::max(h->jit_last_gx, 1);
+    w->node_updates = h->n_patterns * (int64_t)(w->internal_nodes - tnodes);
+    w->exact = 1;
+    return;
+  }
+  if (h->kernel_path == "treeM") {
+    // acc starts at 1 and every operand multiplies it (S per class); a contribution is an
+    // MFMA chain: useful 2 S^2 per pattern and class, issued XT x KS 16x16x4 MFMAs per 16
+    // patterns (32-row tiles for S = 20) plus the multiply on the padded rows
+    const int XT = (S + 15) / 16, KS = S / 4;
+    double use = 0.0, iss = 0.0;
+    int64_t tnodes = 0;
+    for (size_t i = 0; i < h->prog_host.size(); ++i) {
+      const TInstr& in = h->prog_host[i];
+      if (in.op == T_TIP || in.op == T_CHERRY) {
+        use += S;
+        iss += 16.0 * XT;
+        tnodes += in.op == T_CHERRY;
+      } else if (in.op == T_LOAD || (in.op == T_ASCEND && in.b >= 0)) {
+        use += 2.0 * S * S + S;
+        iss += (double)XT * KS * 2.0 * 16 * 16 * 4 / 16 + 16.0 * XT;
+      }
+    }
+    const int nch = (int)h->cherry3.size() / 3;
+    const int U = h->n_codes;
+    w->useful_flops = use * C * P;
+    w->issued_flops = iss * C * P;
+    w->table_nodes = tnodes;
+    w->table_rows = (int64_t)nch * U * U * C;
+    // cherry_table_kernel: per cherry, class and code pair the two tip rows of every class
+    // and the product through P_cherry
+    w->table_flops = (double)nch * C * U * U * (2.0 * S * C + (double)XT * KS * 2.0 * 16 * 16 * 4 / 16);
+    w->node_updates = h->n_patterns * (int64_t)(w->internal_nodes - tnodes);
+    w->exact = 1;
+    return;
+  }
+}
 
 int path_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   if (h->deriv_valid.empty() || !h->deriv_valid[branch])
@@ -2588,8 +2703,29 @@ int plk_reset_timing(plk_handle h) {
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
   int rc = collect_events(h);
   if (rc) return rc;
-  h->n_launches = 0;
-  h->acc_ms[0] = h->acc_ms[1] = h->acc_ms[2] = 0.0;
+  h->n_launches = h->n_table_launches = 0;
+  h->acc_ms[0] = h->acc_ms[1] = h->acc_ms[2] = h->acc_ms[3] = 0.0;
+  return PLK_OK;
+}
+
+int plk_get_timing_ex(plk_handle h, plk_timing* out) {
+  if (!h || !out) return fail(h, PLK_ERR_ARG, "null argument");
+  hipSetDevice(h->device);
+  int rc = collect_events(h);
+  if (rc) return rc;
+  out->partials_launches = h->n_launches;
+  out->partials_ms = h->acc_ms[0];
+  out->pmat_ms = h->acc_ms[1];
+  out->root_ms = h->acc_ms[2];
+  out->tables_ms = h->acc_ms[3];
+  out->table_launches = h->n_table_launches;
+  return PLK_OK;
+}
+
+int plk_traversal_work(plk_handle h, plk_work* out) {
+  if (!h || !out) return fail(h, PLK_ERR_ARG, "null argument");
+  if (h->kernel_path.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet");
+  traversal_work(h, out);
   return PLK_OK;
 }
 

@@ -17,6 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PLK_LIB") or os.path.join(_HERE, "libplk.so")  # PLK_LIB: A/B builds
 
 PLK_OK = 0
+BLOCK = 4096  # plk_block_size(): patterns per fixed-order root block sum
 PLK_FLAG_SCALING = 1
 PLK_FLAG_NONNEG_GUARD = 2
 PLK_FLAG_LNL_ONLY = 4
@@ -25,7 +26,7 @@ PLK_FLAG_SUBTREE_PATTERNS = 16
 PLK_FLAG_DOUBLE_RECURSIVE = 32
 PLK_DERIV_P, PLK_DERIV_DP, PLK_DERIV_D2P = 1, 2, 4
 PLK_OP_ACCUMULATE = 1
-PLK_TIME_PARTIALS, PLK_TIME_PMAT, PLK_TIME_ROOT = 1, 2, 4
+PLK_TIME_PARTIALS, PLK_TIME_PMAT, PLK_TIME_ROOT, PLK_TIME_TABLES = 1, 2, 4, 8
 
 # every symbol include/plk.h declares
 EXPORTS = [
@@ -35,6 +36,7 @@ EXPORTS = [
     "plk_get_pmatrix", "plk_update_partials", "plk_get_partials", "plk_root_loglik", "plk_block_size",
     "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
     "plk_kernel_path", "plk_evaluate", "plk_compressed_work", "plk_all_branch_derivatives",
+    "plk_get_timing_ex", "plk_traversal_work",
 ]
 
 
@@ -47,6 +49,17 @@ class PlkError(RuntimeError):
 class plk_op(ct.Structure):
     _fields_ = [("parent", ct.c_int32), ("n_children", ct.c_int32), ("child", ct.c_int32 * 3),
                 ("flags", ct.c_int32)]
+
+
+class plk_timing(ct.Structure):
+    _fields_ = [("partials_launches", ct.c_int64), ("partials_ms", ct.c_double), ("pmat_ms", ct.c_double),
+                ("root_ms", ct.c_double), ("tables_ms", ct.c_double), ("table_launches", ct.c_int64)]
+
+
+class plk_work(ct.Structure):
+    _fields_ = [("patterns", ct.c_int64), ("node_updates", ct.c_int64), ("table_nodes", ct.c_int64),
+                ("table_rows", ct.c_int64), ("useful_flops", ct.c_double), ("issued_flops", ct.c_double),
+                ("table_flops", ct.c_double), ("exact", ct.c_int32), ("internal_nodes", ct.c_int32)]
 
 
 _lib = None
@@ -84,6 +97,8 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_block_size": ([], ct.c_int),
         "plk_set_timing": ([ct.c_void_p, ct.c_int], ct.c_int),
         "plk_get_timing": ([ct.c_void_p, P(ct.c_int64), dp, dp, dp], ct.c_int),
+        "plk_get_timing_ex": ([ct.c_void_p, P(plk_timing)], ct.c_int),
+        "plk_traversal_work": ([ct.c_void_p, P(plk_work)], ct.c_int),
         "plk_reset_timing": ([ct.c_void_p], ct.c_int),
         "plk_synchronize": ([ct.c_void_p], ct.c_int),
         "plk_branch_derivatives": ([ct.c_void_p, ct.c_int, dp, dp], ct.c_int),
@@ -290,10 +305,17 @@ class Engine:
                                           else int(on)))
 
     def get_timing(self):
-        n = ct.c_int64(0)
-        a, b, c = ct.c_double(0), ct.c_double(0), ct.c_double(0)
-        self._chk(self.lib.plk_get_timing(self.h, ct.byref(n), ct.byref(a), ct.byref(b), ct.byref(c)))
-        return {"launches": n.value, "partials_ms": a.value, "pmat_ms": b.value, "root_ms": c.value}
+        t = plk_timing()
+        self._chk(self.lib.plk_get_timing_ex(self.h, ct.byref(t)))
+        return {"launches": t.partials_launches, "partials_ms": t.partials_ms, "pmat_ms": t.pmat_ms,
+                "root_ms": t.root_ms, "tables_ms": t.tables_ms, "table_launches": t.table_launches}
+
+    def traversal_work(self) -> dict:
+        """plk_traversal_work: node updates computed per pattern vs served by tables, and
+        the fp64 flops of the last traversal (counted from the program that ran)."""
+        w = plk_work()
+        self._chk(self.lib.plk_traversal_work(self.h, ct.byref(w)))
+        return {k: getattr(w, k) for k, _ in plk_work._fields_}
 
     def reset_timing(self):
         self._chk(self.lib.plk_reset_timing(self.h))

@@ -50,3 +50,44 @@ def allgather_lnl(blocks: np.ndarray, dist=None, device=None) -> float:
     dist.all_gather(out, buf)
     allb = np.concatenate([o[: int(c.item())].cpu().numpy() for o, c in zip(out, counts)])
     return fixed_order_sum(allb)
+
+
+class BlockExchange:
+    """The one exchange of a sharded evaluation, sized at setup: every rank's block count
+    is all-gathered ONCE here, so each evaluation is a single fixed-size all-gather of the
+    padded block sums (no count exchange, no per-rank .item() syncs) followed by the
+    fixed-order sum on the host -- bitwise identical for any GPU count."""
+
+    def __init__(self, dist, n_blocks: int, device=None):
+        import torch
+
+        self.dist = dist
+        self.world = dist.get_world_size()
+        n = torch.tensor([n_blocks], dtype=torch.int64, device=device)
+        counts = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(counts, n)
+        self.counts = [int(c.item()) for c in counts]
+        self.cmax = max(self.counts)
+        self.n = n_blocks
+        self.buf = torch.zeros(self.cmax, dtype=torch.float64, device=device)
+        self.out = torch.empty(self.world * self.cmax, dtype=torch.float64, device=device)
+        self.host = torch.empty(self.world * self.cmax, dtype=torch.float64,
+                                pin_memory=str(device).startswith("cuda"))
+        try:
+            self._gather = dist.all_gather_into_tensor
+            self._gather(self.out, self.buf)   # probe once: gloo may not provide it
+        except (RuntimeError, AttributeError, NotImplementedError):
+            self._gather = None
+        self.views = list(self.out.view(self.world, self.cmax))
+
+    def lnl(self, blocks: np.ndarray) -> float:
+        import torch
+
+        self.buf[: self.n].copy_(torch.from_numpy(np.asarray(blocks, dtype=np.float64)))
+        if self._gather is not None:
+            self._gather(self.out, self.buf)
+        else:
+            self.dist.all_gather(self.views, self.buf)
+        self.host.copy_(self.out)
+        allb = self.host.numpy().reshape(self.world, self.cmax)
+        return fixed_order_sum(np.concatenate([allb[r, : self.counts[r]] for r in range(self.world)]))

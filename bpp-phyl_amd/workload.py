@@ -167,6 +167,7 @@ class Evaluator:
         self.branches = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
         self.model_idx = None if wl.model_of_node is None else wl.model_of_node[self.branches].astype(np.int32)
         self.ops = phylo.split_ops(et.ops)
+        self.n_blocks = (end - start + plk.BLOCK - 1) // plk.BLOCK
 
     def step(self, brlen: Optional[np.ndarray] = None):
         et = self.wl.et

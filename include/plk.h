@@ -193,16 +193,52 @@ int plk_all_branch_derivatives(plk_handle h, double* d1, double* d2);
 /* Instrumentation: HIP-event timing on the handle's stream of the kernels selected
  * by the mask given to plk_set_timing (0 = off).  Each timed launch adds an event
  * pair to the stream, so time only what is needed. */
-enum { PLK_TIME_PARTIALS = 1u, PLK_TIME_PMAT = 2u, PLK_TIME_ROOT = 4u };
+enum { PLK_TIME_PARTIALS = 1u, PLK_TIME_PMAT = 2u, PLK_TIME_ROOT = 4u, PLK_TIME_TABLES = 8u };
 int plk_set_timing(plk_handle h, int mask);
 /* n_launches: partials launches issued while PLK_TIME_PARTIALS was set (the timed ones) */
 int plk_get_timing(plk_handle h, int64_t* n_launches, double* partials_ms, double* pmat_ms, double* root_ms);
+/* All timers: PLK_TIME_TABLES times the per-traversal table builds that feed a fused
+ * traversal (the 20/64-state cherry contribution tables, cherry_table_kernel), which
+ * belong to the traversal's cost but are separate launches. */
+typedef struct plk_timing {
+  int64_t partials_launches;  /* traversal launches timed */
+  double partials_ms, pmat_ms, root_ms, tables_ms;
+  int64_t table_launches;     /* table-build launches timed */
+} plk_timing;
+int plk_get_timing_ex(plk_handle h, plk_timing* out);
 int plk_reset_timing(plk_handle h);
 int plk_synchronize(plk_handle h);
 
 /* Name of the kernel that served the last plk_update_partials call ("jit_tree4",
  * "tree4", "treeS", "treeM" or "levelwise"); "" before the first call. */
 const char* plk_kernel_path(plk_handle h);
+
+/* Work of the last traversal, counted on the host from the program that ran (no device
+ * call).  A node update is one site pattern of one internal node's partial; the
+ * reference computes n_patterns x n_internal of them per traversal
+ * (RHomogeneousTreeLikelihood.cpp:839-861).  Here some are table lookups instead:
+ *   - cherry tables: the partial of a cherry (two tip sons) -- and, for an unstored
+ *     cherry, its contribution to the parent -- is read from a row precomputed per code
+ *     pair (table_rows rows per traversal);
+ *   - per-subtree pattern compression: a node is computed once per distinct pattern of
+ *     its subtree.
+ * node_updates counts only the updates computed per pattern.  flops are fp64 operations
+ * (an FMA is 2) of the traversal kernel(s) per traversal over the padded patterns:
+ * useful = on live states, issued = including MFMA padding rows (20 states run
+ * 32-row tiles); table_flops = the table builds (every workgroup of the fused 4-state
+ * kernel forms its own tables).  exact = 1 when counted from the fused program that
+ * ran, 0 for the levelwise / interpreter paths (then the algorithmic count
+ * 2 C S^2 per internal child + (k - 1) C S per combine is reported). */
+typedef struct plk_work {
+  int64_t patterns;       /* patterns of the handle */
+  int64_t node_updates;   /* computed per pattern, summed over patterns and internal nodes */
+  int64_t table_nodes;    /* internal nodes served from cherry tables (per pattern) */
+  int64_t table_rows;     /* cherry-table rows built per traversal (code pairs x classes x cherries) */
+  double useful_flops, issued_flops, table_flops;
+  int32_t exact;
+  int32_t internal_nodes; /* internal nodes of the traversal */
+} plk_work;
+int plk_traversal_work(plk_handle h, plk_work* out);
 
 /* With PLK_FLAG_SUBTREE_PATTERNS: the node updates the last traversal actually computed,
  * i.e. the sum over its internal nodes of their distinct subtree patterns (the

@@ -1,5 +1,8 @@
-"""World-size-2 gloo tests of the multi-GPU path on CPU: shard ranges, the block-sum
-all-gather and the fixed-order total (bitwise identical to one process)."""
+"""World-size-2/3 gloo tests of the multi-GPU path on CPU: shard ranges, the block-sum
+all-gather and the fixed-order total (bitwise identical to one process).  The exchange
+under test is shard.BlockExchange, the code bench.py's N > 1 branch runs each step; the
+block sums come from the oracle's per-pattern lnL of a real workload shard (what each
+rank's plk_evaluate returns on the GPU)."""
 import os
 import socket
 
@@ -42,6 +45,57 @@ def _worker(rank, world, port, n, q):
     lnl = shard.allgather_lnl(_block_sums(site, a, b), dist)
     q.put((rank, a, b, lnl))
     dist.destroy_process_group()
+
+
+def _oracle_sites(config, start, end):
+    import oracle
+    import workload
+
+    wl = workload.make_workload(config, n_patterns=end)
+    et = wl.et
+    states = wl.simulate(start, end).astype(np.int32)
+    pm = np.zeros((et.n_nodes, wl.C, wl.S, wl.S))
+    for n in range(et.n_nodes):
+        if n != et.root:
+            m = wl.models[0] if wl.model_of_node is None else wl.models[wl.model_of_node[n]]
+            for c in range(wl.C):
+                pm[n, c] = m.pij(et.brlen[n] * wl.rates[c])
+    ss, sons, lr = et.son_arrays()
+    _, site, _, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, wl.alphabet.init_table, pm, wl.probs,
+                                       wl.root_freqs, use_patterns=False, scaling=wl.scaling, want_sites=True)
+    return site
+
+
+def _bench_worker(rank, world, port, config, n, q):
+    """bench.py's N > 1 exchange: each rank holds its shard's block sums, BlockExchange
+    (sized once at setup) all-gathers them and sums in global block order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a, b = shard.shard_range(rank, world, n)
+    site = _oracle_sites(config, a, b)
+    blocks = _block_sums(np.concatenate([np.zeros(a), site]), a, b)   # block sums of [a, b)
+    x = shard.BlockExchange(dist, len(blocks), device="cpu")
+    lnl1 = x.lnl(blocks)
+    lnl2 = x.lnl(blocks)        # a second evaluation reuses the buffers
+    q.put((rank, lnl1, lnl2))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("config,world,n", [("gtr_g4_dna_1M_64", 2, 3 * 4096 + 300),
+                                            ("nh_gtr_g4_dna_2M_512", 3, 2 * 4096 + 5),
+                                            ("gtr_g4_dna_1M_64", 3, 900)])
+def test_block_exchange_bitwise_vs_one_process(config, world, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, config, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    whole = shard.fixed_order_sum(_block_sums(_oracle_sites(config, 0, n), 0, n))
+    assert all(r[1] == whole and r[2] == whole for r in res), (res, whole)
 
 
 @pytest.mark.parametrize("world,n", [(2, 3 * 4096 + 17), (2, 100), (3, 10 * 4096)])

@@ -31,6 +31,27 @@ __global__ __launch_bounds__(256) void mfma_kernel(double* out, int iters, doubl
   out[blockIdx.x * blockDim.x + threadIdx.x] = d0[0] + d1[1] + d2[2] + d3[3];
 }
 
+// v_mfma_f64_4x4x4_4b_f64: 4 blocks of 4x4x4 per wave (512 flops per instruction, one
+// f64 result per lane).  20 states tile as 5 x 4 rows with no padding, where the 16x16x4
+// form runs 32-row tiles (37.5 % padding): worth it only if its flop rate is close.
+__global__ __launch_bounds__(256) void mfma4_kernel(double* out, int iters, double a, double b) {
+  double d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0, d5 = 0, d6 = 0, d7 = 0;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      d0 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, d1, 0, 0, 0);
+      d2 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, d2, 0, 0, 0);
+      d3 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, d3, 0, 0, 0);
+      d4 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, d4, 0, 0, 0);
+      d5 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, d5, 0, 0, 0);
+      d6 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, d6, 0, 0, 0);
+      d7 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, d7, 0, 0, 0);
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7;
+}
+
 int main() {
   const int blocks = 256 * 8, threads = 256, iters = 4096;
   double* out;
@@ -57,6 +78,16 @@ int main() {
     hipEventElapsedTime(&ms, e0, e1);
     const double flops = 2.0 * 16 * 16 * 4 * 8 * 4 * (double)(iters / 4) * blocks * (threads / 64);
     printf("MFMA v_mfma_f64_16x16x4: %.1f TF/s (%.3f ms)\n", flops / ms / 1e9, ms);
+  }
+  for (int rep = 0; rep < 3; ++rep) {
+    hipEventRecord(e0);
+    mfma4_kernel<<<blocks, threads>>>(out, iters / 4, 0.999999, 1e-7);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double flops = 2.0 * 4 * 4 * 4 * 4 * 8 * 8 * (double)(iters / 4) * blocks * (threads / 64);
+    printf("MFMA v_mfma_f64_4x4x4_4b: %.1f TF/s (%.3f ms)\n", flops / ms / 1e9, ms);
   }
   return 0;
 }

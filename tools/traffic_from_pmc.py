@@ -3,8 +3,8 @@
 FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md HBM section: KB units, and on gfx950
 FETCH_SIZE tallies half the bytes of a wide streaming read, so bytes = (2*FETCH + WRITE)*1024),
 the SQ instruction mix of the same launches, and the kernel-trace stats.  Copies the
-summaries into profiles/<round>/ and records traffic in profiles/traffic.json under
-"<config>/<mode>".
+summaries into profiles/<round>/ and records traffic in profiles/<round>/traffic.json under
+"<config>/<mode>" (bench.py reads profiles/r02/traffic.json, then the round-1 file).
 
   python tools/traffic_from_pmc.py <tag> <config> <mode> <round>
 """
@@ -17,7 +17,7 @@ import sys
 from collections import OrderedDict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PARTIALS = ("tree4_kernel", "treeS_kernel", "treeM_kernel", "partials_", "plk_jit_tree4")  # partials_links_ included
+PARTIALS = ("tree4_kernel", "treeS_kernel", "treeM_kernel", "partials_", "plk_jit_tree4", "cherry_table_kernel")  # partials_links_ included
 
 
 def rows(d):
@@ -50,7 +50,8 @@ def main():
     tag, config, mode, rnd = sys.argv[1:5]
     src = os.path.join(ROOT, "gpurun_out", "prof", tag)
     bench = json.load(open(os.path.join(src, "bench.json")))
-    n_launch = int(round(bench["partials_launches_per_step"]))
+    # the traversal's launches plus the table builds that feed it (cherry_table_kernel)
+    n_launch = int(round(bench["partials_launches_per_step"] + bench.get("table_launches_per_step", 0)))
     P = bench["config"]["patterns_per_gpu"]
     fetch = last_traversal(per_dispatch(rows(os.path.join(src, "fetch"))), n_launch)
     write = last_traversal(per_dispatch(rows(os.path.join(src, "write"))), n_launch)
@@ -71,7 +72,7 @@ def main():
     if sqs.get("SQ_WAVES"):
         w = sqs["SQ_WAVES"]
         summary["sq_per_wave"] = {k: v / w for k, v in sqs.items() if k != "SQ_WAVES"}
-    tp = os.path.join(ROOT, "profiles", "traffic.json")
+    tp = os.path.join(ROOT, "profiles", rnd, "traffic.json")
     tr = json.load(open(tp)) if os.path.exists(tp) else {}
     tr[f"{config}/{mode}"] = {
         "patterns": P, "hbm_bytes_per_traversal": hbm, "fetch_size_kb": f_kb, "write_size_kb": w_kb,
