@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path on ONE GPU (every rank on cuda:0, collectives on the host); "
                          "never a measurement")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="under torch.distributed.run with ONE rank: still take the N>1 path (process group, "
+                         "in-handle RCCL communicator, exchange check) -- a single-GPU rehearsal of it")
     ap.add_argument("--mode", default="lnl", choices=["lnl", "materialize", "levelwise", "subtree"],
                     help="lnl: fused traversal, interior partials kept in registers (recomputed on demand); "
                          "materialize: fused traversal writing every partial; levelwise: one launch per level; "
@@ -241,8 +244,9 @@ def main():
     import torch
 
     dist = None
-    rehearse = world > 1 and args.dist_backend == "gloo"
-    if world > 1:
+    use_dist = world > 1 or (args.force_dist and "WORLD_SIZE" in os.environ)
+    rehearse = use_dist and args.dist_backend == "gloo"
+    if use_dist:
         import torch.distributed as dist  # noqa: F811
         if rehearse:
             torch.cuda.set_device(0)
@@ -252,7 +256,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    device = local if world > 1 and not rehearse else 0
+    device = local if use_dist and not rehearse else 0
     coll_dev = "cpu" if rehearse else "cuda"
 
     wl = workload.make_workload(args.config)
@@ -263,17 +267,35 @@ def main():
     extra = {"lnl": plk.PLK_FLAG_LNL_ONLY, "materialize": 0, "levelwise": plk.PLK_FLAG_LEVELWISE,
              "subtree": plk.PLK_FLAG_SUBTREE_PATTERNS}[args.mode]
     ev = workload.Evaluator(wl, device, start, end, extra_flags=extra)
-    xchg = shard.BlockExchange(dist, ev.n_blocks, device=coll_dev) if dist is not None else None
+    xchg = None
+    if dist is not None and rehearse:
+        # one GPU, every rank on cuda:0: RCCL cannot put two ranks on one device, so the
+        # rehearsal exchanges the block sums through torch.distributed (gloo)
+        xchg = shard.BlockExchange(dist, ev.n_blocks, device=coll_dev)
+    elif dist is not None:
+        # the RCCL communicator inside the handle (plk_comm_init): plk_evaluate all-gathers
+        # every rank's block sums on the engine's stream and returns the global lnL
+        cid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            cid.copy_(torch.frombuffer(bytearray(plk.comm_get_id()), dtype=torch.uint8))
+        dist.broadcast(cid, 0)
+        ev.eng.comm_init(world, rank, bytes(cid.cpu().numpy()))
     t_setup = time.time() - t_setup
     units_step = P * wl.et.n_internal
 
     def one_step():
         lnl, _, blocks = ev.step()
         if xchg is None:
-            return lnl  # plk_evaluate already summed the block sums in the fixed global order
-        # the one cross-GPU exchange: all-gather of fixed-order block sums
+            return lnl  # global: plk_evaluate summed every rank's block sums in fixed global order
         return xchg.lnl(blocks)
 
+    if dist is not None and not rehearse:
+        # check the in-handle exchange once against torch.distributed's all-gather of the
+        # same per-rank block sums (bitwise), before anything is timed
+        lnl0, _, blocks0 = ev.step()
+        ref = shard.BlockExchange(dist, ev.n_blocks, device=coll_dev).lnl(blocks0)
+        if ref != lnl0:
+            raise RuntimeError(f"rank {rank}: in-handle RCCL lnL {lnl0!r} != torch all-gather {ref!r}")
     for _ in range(args.warmup):
         lnl = one_step()
     ev.eng.reset_timing()

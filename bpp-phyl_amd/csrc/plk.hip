@@ -12,10 +12,12 @@
 #include "plk_treeS.hpp"
 #include "plk_treeM.hpp"
 #include "plk_jit.hpp"
+#include "plk_jitm.hpp"
 #include "plk_dr.hpp"
 
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <functional>
@@ -153,6 +155,10 @@ struct plk_handle_s {
   std::vector<int32_t> frag_starts_host;  // fragment start offsets, tier order
   hipFunction_t jit_fn = nullptr;
   JitShape jit_shape;
+  // tree-specialised 20-state kernel on v_mfma_f64_4x4x4_4b (plk_jitm.hpp); null: not compiled yet
+  hipFunction_t jitm_fn = nullptr;
+  JitMShape jitm_shape;
+  bool prog_jitm = false;                 // program cut for jit_treeM
   JitPlan jit_plan;            // table units / events of the current program (plk_jit.hpp)
   bool jit_plan_valid = false;
   int jit_plan_U = 0, jit_plan_budget = -1;
@@ -187,6 +193,20 @@ struct plk_handle_s {
   double* dr_blk = nullptr;
   size_t dr_blk_cap = 0;
   double* dr_out = nullptr;
+  // multi-device handle (plk_create_multi): one shard handle per device over contiguous,
+  // block-aligned pattern ranges; the parent owns no device memory
+  std::vector<plk_handle> shards;
+  std::vector<int64_t> shard_start;       // first pattern of each shard (+ n_patterns at the end)
+  // RCCL communicator of a sharded multi-process run (plk_comm_init): block sums all-gathered
+  // on the handle's stream and summed in global order on the device
+  ncclComm_t comm = nullptr;
+  int comm_ranks = 0, comm_rank = 0;
+  int64_t comm_cmax = 0;                  // block sums per rank in the all-gather (max over ranks)
+  double* d_blk_local = nullptr;          // [comm_cmax] this rank's block sums (zero padded)
+  double* d_blk_all = nullptr;            // [comm_ranks][comm_cmax]
+  int64_t* d_comm_counts = nullptr;       // block sums per rank
+  double* h_total = nullptr;              // mapped pinned: the global lnL
+  double* d_total = nullptr;              // its device address
 };
 
 namespace {
@@ -450,6 +470,150 @@ int upload_compact_table(plk_handle h) {
   return PLK_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Multi-device handle (plk_create_multi): the parent forwards every call to its shards.
+// ---------------------------------------------------------------------------
+int multi_forward(plk_handle h, int rc) {
+  if (rc) {
+    h->last_error = std::string("shard: ") + g_last_error;
+    for (plk_handle s : h->shards)
+      if (!s->last_error.empty()) h->last_error = "shard: " + s->last_error;
+  }
+  return rc;
+}
+
+int multi_each(plk_handle h, const std::function<int(plk_handle)>& f) {
+  for (size_t i = 0; i < h->shards.size(); ++i) {
+    const int rc = f(h->shards[i]);
+    if (rc) return fail(h, rc, "shard %zu (device %d): %s", i, h->shards[i]->device, h->shards[i]->last_error.c_str());
+  }
+  return PLK_OK;
+}
+
+// f(shard, first pattern of the shard): per-pattern arrays are sliced at the shard starts
+int multi_slices(plk_handle h, const std::function<int(plk_handle, int64_t)>& f) {
+  for (size_t i = 0; i < h->shards.size(); ++i) {
+    const int rc = f(h->shards[i], h->shard_start[i]);
+    if (rc) return fail(h, rc, "shard %zu (device %d): %s", i, h->shards[i]->device, h->shards[i]->last_error.c_str());
+  }
+  return PLK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+int root_launch_c(plk_handle h, int root, double* site_lnl);
+int root_finish_c(plk_handle h, double* lnl, double* block_sums);
+}
+
+namespace {
+
+// every device's root reduction in flight, then one wait per device; the lnL is the sum of
+// all block sums in global block order (bitwise the single-device value)
+int multi_root_finish_all(plk_handle h, double* lnl, double* block_sums) {
+  std::vector<double> all;
+  all.reserve((size_t)h->n_blocks);
+  for (size_t i = 0; i < h->shards.size(); ++i) {
+    plk_handle x = h->shards[i];
+    std::vector<double> b((size_t)x->n_blocks);
+    const int rc = root_finish_c(x, nullptr, b.data());
+    if (rc) return fail(h, rc, "shard %zu: %s", i, x->last_error.c_str());
+    all.insert(all.end(), b.begin(), b.end());
+  }
+  double s = 0.0;
+  for (double v : all) s += v;
+  if (lnl) *lnl = s;
+  if (block_sums) std::memcpy(block_sums, all.data(), all.size() * sizeof(double));
+  return PLK_OK;
+}
+
+int multi_root_loglik_impl(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums) {
+  const int rc = multi_slices(h, [&](plk_handle x, int64_t a) { return root_launch_c(x, root, site_lnl ? site_lnl + a : nullptr); });
+  if (rc) return rc;
+  return multi_root_finish_all(h, lnl, block_sums);
+}
+
+int multi_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* model, const double* t,
+                   const plk_op* ops, int n_ops, int root, double* lnl, double* block_sums) {
+  const int rc = multi_each(h, [&](plk_handle x) {
+    int r = plk_update_pmatrices(x, n, branch, model, t, PLK_DERIV_P);
+    if (!r) r = plk_update_partials(x, ops, n_ops);
+    if (!r) r = root_launch_c(x, root, nullptr);
+    return r;
+  });
+  if (rc) return rc;
+  return multi_root_finish_all(h, lnl, block_sums);
+}
+
+int multi_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
+  double s1 = 0.0, s2 = 0.0;
+  const int rc = multi_each(h, [&](plk_handle x) {
+    double a = 0.0, b = 0.0;
+    const int r = plk_branch_derivatives(x, branch, &a, &b);
+    s1 += a;
+    s2 += b;
+    return r;
+  });
+  if (rc) return rc;
+  if (d1) *d1 = s1;
+  if (d2) *d2 = s2;
+  return PLK_OK;
+}
+
+int multi_all_branch_derivatives(plk_handle h, double* d1, double* d2) {
+  const size_t n = (size_t)h->n_nodes;
+  std::vector<double> s1(n, 0.0), s2(n, 0.0), a(n), b(n);
+  const int rc = multi_each(h, [&](plk_handle x) {
+    const int r = plk_all_branch_derivatives(x, a.data(), b.data());
+    for (size_t i = 0; i < n; ++i) {
+      s1[i] += a[i];
+      s2[i] += b[i];
+    }
+    return r;
+  });
+  if (rc) return rc;
+  if (d1) std::memcpy(d1, s1.data(), n * sizeof(double));
+  if (d2) std::memcpy(d2, s2.data(), n * sizeof(double));
+  return PLK_OK;
+}
+
+int multi_compressed_work(plk_handle h, int64_t* updates) {
+  int64_t s = 0;
+  const int rc = multi_each(h, [&](plk_handle x) {
+    int64_t u = 0;
+    const int r = plk_compressed_work(x, &u);
+    s += u;
+    return r;
+  });
+  if (rc) return rc;
+  if (updates) *updates = s;
+  return PLK_OK;
+}
+
+int multi_traversal_work(plk_handle h, plk_work* out) {
+  plk_work sum;
+  std::memset(&sum, 0, sizeof(sum));
+  sum.exact = 1;
+  const int rc = multi_each(h, [&](plk_handle x) {
+    plk_work w;
+    const int r = plk_traversal_work(x, &w);
+    if (r) return r;
+    sum.patterns += w.patterns;
+    sum.node_updates += w.node_updates;
+    sum.table_nodes = w.table_nodes;
+    sum.table_rows += w.table_rows;
+    sum.useful_flops += w.useful_flops;
+    sum.issued_flops += w.issued_flops;
+    sum.table_flops += w.table_flops;
+    sum.exact = sum.exact && w.exact;
+    sum.internal_nodes = w.internal_nodes;
+    return 0;
+  });
+  if (rc) return rc;
+  if (out) *out = sum;
+  return PLK_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -571,7 +735,19 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
 
 int plk_destroy(plk_handle h) {
   if (!h) return PLK_OK;
+  if (!h->shards.empty()) {
+    for (plk_handle s : h->shards) plk_destroy(s);
+    delete h;
+    return PLK_OK;
+  }
   hipSetDevice(h->device);
+  if (h->comm) {
+    if (h->stream) hipStreamSynchronize(h->stream);
+    ncclCommDestroy(h->comm);
+  }
+  for (void* p : {(void*)h->d_blk_local, (void*)h->d_blk_all, (void*)h->d_comm_counts})
+    if (p) hipFree(p);
+  if (h->h_total) hipHostFree(h->h_total);
   if (h->stream) hipStreamSynchronize(h->stream);
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
@@ -596,7 +772,54 @@ int plk_destroy(plk_handle h) {
   return PLK_OK;
 }
 
+int plk_comm_get_id(plk_comm_id* id) {
+  if (!id) return fail(nullptr, PLK_ERR_ARG, "null id");
+  static_assert(sizeof(plk_comm_id) == sizeof(ncclUniqueId), "plk_comm_id wraps ncclUniqueId");
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return fail(nullptr, PLK_ERR_DEVICE, "ncclGetUniqueId failed");
+  std::memcpy(id->internal, u.internal, sizeof(u.internal));
+  return PLK_OK;
+}
+
+int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id) {
+  if (!h || !id || n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(h, PLK_ERR_ARG, "bad communicator arguments");
+  if (!h->shards.empty()) return fail(h, PLK_ERR_UNSUPPORTED, "a multi-device handle exchanges in-process");
+  if (h->comm) return fail(h, PLK_ERR_STATE, "communicator already initialised");
+  hipSetDevice(h->device);
+  ncclUniqueId u;
+  std::memcpy(u.internal, id->internal, sizeof(u.internal));
+  if (ncclCommInitRank(&h->comm, n_ranks, u, rank) != ncclSuccess) {
+    h->comm = nullptr;
+    return fail(h, PLK_ERR_DEVICE, "ncclCommInitRank(%d ranks, rank %d) failed", n_ranks, rank);
+  }
+  h->comm_ranks = n_ranks;
+  h->comm_rank = rank;
+  // block counts of every rank, once: per evaluation the all-gather has a fixed size
+  int rc = dalloc(h, (void**)&h->d_comm_counts, (size_t)n_ranks * sizeof(int64_t));
+  if (rc) return rc;
+  int64_t* d_one = nullptr;
+  if ((rc = dalloc(h, (void**)&d_one, sizeof(int64_t)))) return rc;
+  const int64_t mine = h->n_blocks;
+  HIPCHK(h, hipMemcpy(d_one, &mine, sizeof(int64_t), hipMemcpyHostToDevice));
+  if (ncclAllGather(d_one, h->d_comm_counts, 1, ncclInt64, h->comm, h->stream) != ncclSuccess)
+    return fail(h, PLK_ERR_DEVICE, "ncclAllGather of the block counts failed");
+  std::vector<int64_t> counts((size_t)n_ranks);
+  HIPCHK(h, hipMemcpyAsync(counts.data(), h->d_comm_counts, counts.size() * sizeof(int64_t), hipMemcpyDeviceToHost,
+                           h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  hipFree(d_one);
+  h->comm_cmax = *std::max_element(counts.begin(), counts.end());
+  if ((rc = dalloc(h, (void**)&h->d_blk_local, (size_t)h->comm_cmax * sizeof(double)))) return rc;
+  if ((rc = dalloc(h, (void**)&h->d_blk_all, (size_t)n_ranks * h->comm_cmax * sizeof(double)))) return rc;
+  HIPCHK(h, hipMemset(h->d_blk_local, 0, (size_t)h->comm_cmax * sizeof(double)));
+  if (hipHostMalloc((void**)&h->h_total, sizeof(double), hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&h->d_total, h->h_total, 0) != hipSuccess)
+    return fail(h, PLK_ERR_OOM, "pinned total");
+  return PLK_OK;
+}
+
 int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_code_table(x, n_codes, code_to_vec); });
   if (!h || !code_to_vec || n_codes < 1 || n_codes > 256) return fail(h, PLK_ERR_ARG, "bad code table (n_codes %d)", n_codes);
   if (h->S == 4 && n_codes > kMaxCodes4 && s4_supported(h->C))
     return fail(h, PLK_ERR_UNSUPPORTED, "4-state engine supports at most %d codes", kMaxCodes4);
@@ -621,6 +844,7 @@ int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec) {
 }
 
 int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes) {
+  if (h && !h->shards.empty()) return multi_slices(h, [&](plk_handle x, int64_t a) { return plk_set_tip_codes(x, tip, codes ? codes + a : nullptr); });
   if (!h || !codes || tip < 0 || tip >= h->n_tips) return fail(h, PLK_ERR_ARG, "bad tip index %d", tip);
   if (!h->table_set) return fail(h, PLK_ERR_STATE, "plk_set_code_table must precede plk_set_tip_codes");
   bool seen[256] = {false};
@@ -659,6 +883,7 @@ int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes) {
 }
 
 int plk_set_pattern_weights(plk_handle h, const double* weights) {
+  if (h && !h->shards.empty()) return multi_slices(h, [&](plk_handle x, int64_t a) { return plk_set_pattern_weights(x, weights ? weights + a : nullptr); });
   if (!h || !weights) return fail(h, PLK_ERR_ARG, "null weights");
   hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -667,6 +892,7 @@ int plk_set_pattern_weights(plk_handle h, const double* weights) {
 }
 
 int plk_set_category_rates(plk_handle h, const double* rates, const double* probs) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_category_rates(x, rates, probs); });
   if (!h || !rates || !probs) return fail(h, PLK_ERR_ARG, "null rates/probs");
   hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -677,6 +903,7 @@ int plk_set_category_rates(plk_handle h, const double* rates, const double* prob
 }
 
 int plk_set_root_frequencies(plk_handle h, const double* pi) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_root_frequencies(x, pi); });
   if (!h || !pi) return fail(h, PLK_ERR_ARG, "null frequencies");
   hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -686,6 +913,7 @@ int plk_set_root_frequencies(plk_handle h, const double* pi) {
 }
 
 int plk_set_eigen(plk_handle h, int model, const double* V, const double* Vinv, const double* lambda) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_eigen(x, model, V, Vinv, lambda); });
   if (!h || !V || !Vinv || !lambda || model < 0 || model >= h->n_models)
     return fail(h, PLK_ERR_ARG, "bad eigen system (model %d)", model);
   hipSetDevice(h->device);
@@ -700,6 +928,7 @@ int plk_set_eigen(plk_handle h, int model, const double* V, const double* Vinv, 
 
 int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32_t* model, const double* t,
                          unsigned deriv_mask) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_update_pmatrices(x, n, branch, model, t, deriv_mask); });
   if (!h || n < 0 || (n > 0 && (!branch || !t))) return fail(h, PLK_ERR_ARG, "bad pmatrix request");
   if (n == 0) return PLK_OK;
   if (!h->rates_set) return fail(h, PLK_ERR_STATE, "plk_set_category_rates must precede plk_update_pmatrices");
@@ -827,6 +1056,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
 }
 
 int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_pmatrix(x, branch, P); });
   if (!h || !P || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
   hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -840,6 +1070,7 @@ int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
 }
 
 int plk_get_pmatrix(plk_handle h, int branch, double* P) {
+  if (h && !h->shards.empty()) return multi_forward(h, plk_get_pmatrix(h->shards[0], branch, P));
   if (!h || !P || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
   hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -893,6 +1124,10 @@ int env_int(const char* name, int def, int lo, int hi) {
 // 4 states, one class per wave: the tree-specialised kernel (plk_jit.hpp) serves the
 // fused traversal; PLK_JIT=0 keeps the interpreter (tree4_kernel), e.g. for A/B runs.
 bool jit_tree4(plk_handle h) { return fused_kind(h) == FK_TREE4 && tree4_cw(h) == 1 && !env_is("PLK_JIT", '0'); }
+
+// 20 states: the tree-specialised kernel on v_mfma_f64_4x4x4_4b (plk_jitm.hpp) serves the
+// fused traversal; PLK_JITM=0 keeps the treeM interpreter (16x16x4 MFMA), e.g. for A/B runs.
+bool jit_treeM(plk_handle h) { return fused_kind(h) == FK_TREEM && h->S == 20 && !env_is("PLK_JITM", '0'); }
 
 // Classes in one wave (plk_jit.hpp, CW = C): the joint rescale needs no cross-wave
 // exchange (the per-node barrier of the one-class-per-wave layout costs ~2x on cfg5),
@@ -972,7 +1207,9 @@ int tree_levels(plk_handle h) {
     case FK_TREES: return env_int("PLK_TREES_DM", 2, 2, 4);
     // S = 20: 3 levels (with cherry tables 7.8 ms on cfg3, 2 levels 8.7 ms although DM = 3
     // spills a few registers at 128 VGPRs)
-    case FK_TREEM: return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 3, 2, 3);
+    case FK_TREEM:
+      if (jit_treeM(h)) return env_int("PLK_JITM_DM", 3, 2, 6);
+      return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 3, 2, 3);
     default: return 1;
   }
 }
@@ -1175,6 +1412,7 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   h->prog_host = prog;
   h->frag_starts_host.assign(start_sorted.begin(), start_sorted.begin() + nf);
   h->jit_fn = nullptr;  // specialised kernel of the new program: compiled on first use
+  h->jitm_fn = nullptr;
   h->jit_plan_valid = false;
   HIPCHK(h, hipStreamSynchronize(h->stream));  // host staging vectors go out of scope
   h->prog_ops.assign(ops, ops + n_ops);
@@ -1182,6 +1420,7 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   h->prog_reduce = reduce;
   h->prog_dm = DM;
   h->prog_jit = jit_tree4(h);
+  h->prog_jitm = jit_treeM(h);
   h->prog_ciw = jit_ciw(h);
   h->prog_tmax = TMAX;
   h->prog_root = root_reduce;
@@ -1301,6 +1540,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const bool reduce = h->pi_set && h->rates_set;
   const bool same = h->prog_ops.size() == (size_t)n_ops && h->prog_materialize == materialize &&
                     h->prog_reduce == reduce && h->prog_dm == tree_levels(h) && h->prog_jit == jit_tree4(h) && h->prog_ciw == jit_ciw(h) &&
+                    h->prog_jitm == jit_treeM(h) &&
                     (!h->prog_jit || h->prog_tmax == jit_tip_cap(h)) &&
                     std::memcmp(h->prog_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
   if (!same) {
@@ -1481,7 +1721,44 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.n_sblocks = (int32_t)((h->n_pad + 64 * sh.G * sh.PW - 1) / (64 * sh.G * sh.PW));  // last may be ragged
     ja.guard = a.guard;
   }
-  h->kernel_path = jit ? "jit_tree4" : kind == FK_TREEM ? "treeM" : kind == FK_TREES ? "treeS" : "tree4";
+  const bool jitm = kind == FK_TREEM && h->prog_jitm;
+  JMArgs ma;
+  JitMShape msh;
+  if (jitm) {
+    msh.S = h->S;
+    msh.C = h->C;
+    msh.U = h->n_codes;
+    msh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
+    msh.L = env_int("PLK_JITM_L", 1, 1, 4);
+    msh.minw = env_int("PLK_JITM_MINW", 2, 1, 8);
+    if (msh.lds_bytes() > 160 * 1024)
+      return fail(h, PLK_ERR_UNSUPPORTED, "jit_treeM needs %zu B of LDS", msh.lds_bytes());
+    if (!h->jitm_fn || !(msh == h->jitm_shape)) {
+      int rc = jit_function(h, jit_treeM4_source(h->prog_host, h->frag_starts_host, msh), "plk_jit_treeM", &h->jitm_fn);
+      if (rc) return rc;
+      h->jitm_shape = msh;
+    }
+    const CherryLayout lay(h->C, h->n_codes, h->S, h->n_pad);
+    ma.partials = h->partials;
+    ma.scale = h->scale;
+    ma.codes = h->codes;
+    ma.tipP = h->tipP;
+    ma.cherry = h->d_cherry;
+    ma.pmats = h->pmats;
+    ma.weights = h->weights;
+    ma.pi = h->pi;
+    ma.probs = h->probs;
+    ma.site_lnl = h->site_lnl;
+    ma.wave_sums = h->wave_sums;
+    ma.slot_stride = h->slot_stride;
+    ma.n_pad = h->n_pad;
+    ma.n_patterns = h->n_patterns;
+    ma.cherry_stride = (int64_t)lay.stride;
+    ma.cherry_table_bytes = (int64_t)lay.table_bytes;
+    ma.cherry_count_bytes = (int64_t)lay.count_bytes;
+    ma.guard = a.guard;
+  }
+  h->kernel_path = jit ? "jit_tree4" : jitm ? "jit_treeM" : kind == FK_TREEM ? "treeM" : kind == FK_TREES ? "treeS" : "tree4";
   int first = 0;
   for (const auto& t : h->prog_tiers) {
     a.frag_start = h->d_frag + first;
@@ -1513,6 +1790,11 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
                                       (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
+    } else if (jitm) {
+      int base = first;
+      void* args[] = {&ma, &base};
+      HIPCHK(h, hipModuleLaunchKernel(h->jitm_fn, (unsigned)(h->n_pad / (16 * JitMShape::G)), grid.y, 1,
+                                      64 * JitMShape::G, 1, 1, (unsigned)msh.lds_bytes(), h->stream, args, nullptr));
     } else if (kind == FK_TREEM) {
       launch_treeM(h, a, grid, lds_m);
       if (treeM_groups(h) != kTreeMGroups && h->prog_root >= 0 && first + (int)t.size() == h->prog_nf) {
@@ -2024,6 +2306,41 @@ void traversal_work(plk_handle h, plk_work* w) {
     w->exact = 1;
     return;
   }
+  if (h->kernel_path == "jit_treeM") {
+    // v_mfma_f64_4x4x4_4b: no padding rows; the first operand of a node is an assignment
+    double per = 0.0;
+    int64_t tnodes = 0;
+    for (size_t f = 0; f < h->frag_starts_host.size(); ++f) {
+      std::vector<char> fresh(64, 0);
+      fresh[0] = 1;
+      int d = 0;
+      for (size_t i = (size_t)h->frag_starts_host[f]; h->prog_host[i].op != T_ROOT; ++i) {
+        const TInstr& in = h->prog_host[i];
+        if (in.op == T_TIP || in.op == T_CHERRY) {
+          if (!fresh[d]) per += S;
+          fresh[d] = 0;
+          tnodes += in.op == T_CHERRY;
+        } else if (in.op == T_LOAD) {
+          per += 2.0 * S * S + (fresh[d] ? 0 : S);
+          fresh[d] = 0;
+        } else if (in.op == T_DESCEND) {
+          fresh[++d] = 1;
+        } else if (in.op == T_ASCEND && in.b >= 0) {
+          per += 2.0 * S * S + (fresh[d - 1] ? 0 : S);
+          fresh[--d] = 0;
+        }
+      }
+    }
+    const int nch = (int)h->cherry3.size() / 3;
+    const int U = h->n_codes, XT = (S + 15) / 16, KS = S / 4;
+    w->useful_flops = w->issued_flops = per * C * P;
+    w->table_nodes = tnodes;
+    w->table_rows = (int64_t)nch * U * U * C;
+    w->table_flops = (double)nch * C * U * U * (2.0 * S * C + (double)XT * KS * 2.0 * 16 * 16 * 4 / 16);
+    w->node_updates = h->n_patterns * (int64_t)(w->internal_nodes - tnodes);
+    w->exact = 1;
+    return;
+  }
   if (h->kernel_path == "treeM") {
     // acc starts at 1 and every operand multiplies it (S per class); a contribution is an
     // MFMA chain: useful 2 S^2 per pattern and class, issued XT x KS 16x16x4 MFMAs per 16
@@ -2474,6 +2791,7 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
 extern "C" {
 
 int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_update_partials(x, ops, n_ops); });
   if (!h || n_ops < 0 || (n_ops > 0 && !ops)) return fail(h, PLK_ERR_ARG, "bad op list");
   if (n_ops == 0) return PLK_OK;
   hipSetDevice(h->device);
@@ -2495,6 +2813,7 @@ int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
 }
 
 int plk_get_partials(plk_handle h, int node, double* out) {
+  if (h && !h->shards.empty()) return multi_slices(h, [&](plk_handle x, int64_t a) { return plk_get_partials(x, node, out ? out + a * h->C * h->S : nullptr); });
   if (!h || !out || node < h->n_tips || node >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad internal node %d", node);
   hipSetDevice(h->device);
   if (!h->materialized[node - h->n_tips]) {
@@ -2527,17 +2846,43 @@ int plk_get_partials(plk_handle h, int node, double* out) {
 }
 
 static int launch_root(plk_handle h, int root);
+static int multi_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums);
 
-int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums) {
-  if (!h || root < h->n_tips || root >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad root node %d", root);
+}  // extern "C"
+
+namespace {
+
+// global lnL of a communicator run: every rank's block sums in rank order (ranks hold
+// consecutive pattern ranges), each rank's in block order -- the same sequence of adds as
+// one process over all patterns; this rank's own block sums are copied to the mapped host
+// buffer beside it
+__global__ void comm_sum_kernel(const double* __restrict__ all, const int64_t* __restrict__ counts, int n_ranks,
+                                int64_t cmax, const double* __restrict__ local, int64_t n_local,
+                                double* __restrict__ local_out, double* __restrict__ total_out) {
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int r = 0; r < n_ranks; ++r)
+      for (int64_t b = 0; b < counts[r]; ++b) s += all[(int64_t)r * cmax + b];
+    *total_out = s;
+  }
+  for (int64_t i = threadIdx.x; i < n_local; i += blockDim.x) local_out[i] = local[i];
+}
+
+// block sums land in mapped host memory, or in the all-gather's send buffer under a communicator
+double* block_target(plk_handle h) { return h->comm ? h->d_blk_local : h->block_sums; }
+
+// Enqueue the root reduction of `root` (fused traversals already did it), the fixed-order
+// 4096-pattern block sums, the RCCL exchange under a communicator, and the per-pattern lnL
+// copy; root_finish waits and sums.  Split so that a multi-device handle can have every
+// device's reduction in flight before it waits for the first.
+int root_launch(plk_handle h, int root, double* site_lnl) {
+  if (root < h->n_tips || root >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad root node %d", root);
   if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
   hipSetDevice(h->device);
-  if (h->fused_lnl_valid && h->fused_lnl_root == root && h->blocks_fused) {
-    // the tree-specialised kernel reduced the root and formed the block sums
-  } else if (h->fused_lnl_valid && h->fused_lnl_root == root) {
+  if (h->fused_lnl_valid && h->fused_lnl_root == root) {
     // the fused traversal already reduced the root: only the block sums remain
     const int n_waves = (int)((h->n_patterns + 63) / 64);
-    wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, h->block_sums, n_waves,
+    wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, block_target(h), n_waves,
                                                                           h->n_blocks);
     HIPCHK(h, hipGetLastError());
   } else {
@@ -2545,15 +2890,100 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
     int rc = launch_root(h, root);
     if (rc) return rc;
   }
+  if (h->comm) {
+    // the one cross-GPU exchange of an evaluation: a fixed-size all-gather of block sums
+    if (ncclAllGather(h->d_blk_local, h->d_blk_all, (size_t)h->comm_cmax, ncclFloat64, h->comm, h->stream) !=
+        ncclSuccess)
+      return fail(h, PLK_ERR_DEVICE, "ncclAllGather of the block sums failed");
+    comm_sum_kernel<<<1, 256, 0, h->stream>>>(h->d_blk_all, h->d_comm_counts, h->comm_ranks, h->comm_cmax,
+                                              h->d_blk_local, h->n_blocks, h->block_sums, h->d_total);
+    HIPCHK(h, hipGetLastError());
+  }
   if (site_lnl)
     HIPCHK(h, hipMemcpyAsync(site_lnl, h->site_lnl, (size_t)h->n_patterns * sizeof(double), hipMemcpyDeviceToHost,
                              h->stream));
+  return PLK_OK;
+}
+
+int root_finish(plk_handle h, double* lnl, double* block_sums) {
+  hipSetDevice(h->device);
   if (int rc = stream_wait(h)) return rc;
   double s = 0.0;
-  for (int b = 0; b < h->n_blocks; ++b) s += h->h_blocks[b];  // fixed order: block 0, 1, 2, ...
+  if (h->comm) {
+    s = *h->h_total;
+  } else {
+    for (int b = 0; b < h->n_blocks; ++b) s += h->h_blocks[b];  // fixed order: block 0, 1, 2, ...
+  }
   if (lnl) *lnl = s;
   if (block_sums) std::memcpy(block_sums, h->h_blocks, (size_t)h->n_blocks * sizeof(double));
   return PLK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int root_launch_c(plk_handle h, int root, double* site_lnl) { return root_launch(h, root, site_lnl); }
+int root_finish_c(plk_handle h, double* lnl, double* block_sums) { return root_finish(h, lnl, block_sums); }
+
+static int multi_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums) {
+  return multi_root_loglik_impl(h, root, lnl, site_lnl, block_sums);
+}
+
+int plk_create_multi(const int* devices, int n_devices, int n_states, int n_classes, int64_t n_patterns, int n_tips,
+                     int n_internal, int n_models, unsigned flags, plk_handle* out) {
+  if (!out || !devices || n_devices < 1) return fail(nullptr, PLK_ERR_ARG, "bad device list");
+  *out = nullptr;
+  if (n_patterns < 1) return fail(nullptr, PLK_ERR_ARG, "bad pattern count");
+  plk_handle h = new plk_handle_s();
+  h->S = n_states;
+  h->C = n_classes;
+  h->n_tips = n_tips;
+  h->n_internal = n_internal;
+  h->n_nodes = n_tips + n_internal;
+  h->n_models = n_models;
+  h->flags = flags;
+  h->n_patterns = n_patterns;
+  h->n_blocks = (int)((n_patterns + kRootBlock - 1) / kRootBlock);
+  h->device = devices[0];
+  // contiguous block-aligned ranges (the last takes the remainder); fewer shards than
+  // devices when there are fewer blocks than devices
+  const int64_t nb = h->n_blocks;
+  const int nd = (int)std::min<int64_t>(n_devices, nb);
+  const int64_t per = nb / nd, extra = nb % nd;
+  int64_t b = 0;
+  for (int i = 0; i < nd; ++i) {
+    const int64_t cnt = per + (i < extra ? 1 : 0);
+    const int64_t a = b * kRootBlock;
+    b += cnt;
+    const int64_t e = std::min<int64_t>(b * kRootBlock, n_patterns);
+    plk_handle s = nullptr;
+    const int rc = plk_create(devices[i], n_states, n_classes, e - a, n_tips, n_internal, n_models, flags, &s);
+    if (rc) {
+      const std::string msg = g_last_error;
+      plk_destroy(h);
+      return fail(nullptr, rc, "plk_create_multi: shard %d on device %d: %s", i, devices[i], msg.c_str());
+    }
+    h->shards.push_back(s);
+    h->shard_start.push_back(a);
+  }
+  h->shard_start.push_back(n_patterns);
+  *out = h;
+  return PLK_OK;
+}
+
+int plk_shard_count(plk_handle h, int* n_shards) {
+  if (!h || !n_shards) return fail(h, PLK_ERR_ARG, "null argument");
+  *n_shards = h->shards.empty() ? 1 : (int)h->shards.size();
+  return PLK_OK;
+}
+
+int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums) {
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  if (!h->shards.empty()) return multi_root_loglik(h, root, lnl, site_lnl, block_sums);
+  int rc = root_launch(h, root, site_lnl);
+  if (rc) return rc;
+  return root_finish(h, lnl, block_sums);
 }
 
 static int launch_root(plk_handle h, int root) {
@@ -2577,7 +3007,7 @@ static int launch_root(plk_handle h, int root) {
   root_kernel<<<(unsigned)(h->n_pad / 64), 64, 0, h->stream>>>(a);
   HIPCHK(h, hipGetLastError());
   const int n_waves = (int)((h->n_patterns + 63) / 64);
-  wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, h->block_sums, n_waves,
+  wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, block_target(h), n_waves,
                                                                         h->n_blocks);
   HIPCHK(h, hipGetLastError());
   if (h->timing & PLK_TIME_ROOT) {
@@ -2588,6 +3018,7 @@ static int launch_root(plk_handle h, int root) {
 }
 
 int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
+  if (h && !h->shards.empty()) return multi_branch_derivatives(h, branch, d1, d2);
   if (!h || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
   if (h->trav_ops.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet (plk_update_partials)");
   if (h->S != 4 || !(h->C == 1 || h->C == 2 || h->C == 4) || env_is("PLK_DERIV_PATH", '1'))
@@ -2682,12 +3113,14 @@ int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
 }
 
 int plk_set_timing(plk_handle h, int enable) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_timing(x, enable); });
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
   h->timing = (unsigned)enable;
   return PLK_OK;
 }
 
 int plk_get_timing(plk_handle h, int64_t* n_launches, double* partials_ms, double* pmat_ms, double* root_ms) {
+  if (h && !h->shards.empty()) return multi_forward(h, plk_get_timing(h->shards[0], n_launches, partials_ms, pmat_ms, root_ms));
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
   hipSetDevice(h->device);
   int rc = collect_events(h);
@@ -2700,6 +3133,7 @@ int plk_get_timing(plk_handle h, int64_t* n_launches, double* partials_ms, doubl
 }
 
 int plk_reset_timing(plk_handle h) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_reset_timing(x); });
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
   int rc = collect_events(h);
   if (rc) return rc;
@@ -2709,6 +3143,7 @@ int plk_reset_timing(plk_handle h) {
 }
 
 int plk_get_timing_ex(plk_handle h, plk_timing* out) {
+  if (h && !h->shards.empty()) return multi_forward(h, plk_get_timing_ex(h->shards[0], out));
   if (!h || !out) return fail(h, PLK_ERR_ARG, "null argument");
   hipSetDevice(h->device);
   int rc = collect_events(h);
@@ -2723,6 +3158,7 @@ int plk_get_timing_ex(plk_handle h, plk_timing* out) {
 }
 
 int plk_traversal_work(plk_handle h, plk_work* out) {
+  if (h && !h->shards.empty()) return multi_traversal_work(h, out);
   if (!h || !out) return fail(h, PLK_ERR_ARG, "null argument");
   if (h->kernel_path.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet");
   traversal_work(h, out);
@@ -2730,6 +3166,7 @@ int plk_traversal_work(plk_handle h, plk_work* out) {
 }
 
 int plk_synchronize(plk_handle h) {
+  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_synchronize(x); });
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
   hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2738,6 +3175,7 @@ int plk_synchronize(plk_handle h) {
 
 int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* model, const double* t,
                  const plk_op* ops, int n_ops, int root, double* lnl, double* block_sums) {
+  if (h && !h->shards.empty()) return multi_evaluate(h, n, branch, model, t, ops, n_ops, root, lnl, block_sums);
   int rc = plk_update_pmatrices(h, n, branch, model, t, PLK_DERIV_P);
   if (rc) return rc;
   rc = plk_update_partials(h, ops, n_ops);
@@ -2746,13 +3184,18 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
 }
 
 int plk_all_branch_derivatives(plk_handle h, double* d1, double* d2) {
+  if (h && !h->shards.empty()) return multi_all_branch_derivatives(h, d1, d2);
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
   return dr_derivatives(h, d1, d2);
 }
 
-const char* plk_kernel_path(plk_handle h) { return h ? h->kernel_path.c_str() : ""; }
+const char* plk_kernel_path(plk_handle h) {
+  if (h && !h->shards.empty()) return plk_kernel_path(h->shards[0]);
+  return h ? h->kernel_path.c_str() : "";
+}
 
 int plk_compressed_work(plk_handle h, int64_t* updates) {
+  if (h && !h->shards.empty()) return multi_compressed_work(h, updates);
   if (!h || !updates) return fail(h, PLK_ERR_ARG, "null argument");
   if (!(h->flags & PLK_FLAG_SUBTREE_PATTERNS) || !h->cmp_valid)
     return fail(h, PLK_ERR_STATE, "no compressed traversal yet");

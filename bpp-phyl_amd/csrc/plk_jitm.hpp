@@ -1,0 +1,351 @@
+// plk_jitm.hpp -- tree-specialised fused traversal for 20-state (protein) models on
+// v_mfma_f64_4x4x4_4b (gfx950).
+//
+// Why a second matrix-core layout.  treeM_kernel (plk_treeM.hpp) runs the contraction
+//     D[x][p] = sum_y P[x][y] L[y][p]          (RHomogeneousTreeLikelihood.cpp:839-861)
+// on v_mfma_f64_16x16x4: 20 states occupy two 16-row tiles, so 12 of every 32 rows are
+// padding (37.5 % of the issued flops), and the instruction itself peaks at 72.9 TF/s.
+// v_mfma_f64_4x4x4_4b -- four independent 4x4x4 blocks per instruction -- peaks at 77.9 TF/s
+// on this part (99 % of the fp64 spec, profiles/r02/fp64_mfma_peak.txt) and tiles 20 states
+// as 5 x 4 rows with no padding: 1.7x less matrix-pipe time per contraction.
+//
+// Layout (decoded on the device, profiles/r02/mfma_f64_4x4x4_layout.txt): lane
+// l = 16*hi + 4*b + lo holds A_b[lo][hi], B_b[hi][lo] and D_b[hi][lo].  A wave owns 16
+// site patterns -- pattern 4b + lo of its group -- and EVERY rate class; lane l keeps the
+// states x = 4X + hi (X = 0..4) of its pattern for each class, i.e. D of x-block X.  That
+// register is exactly the B operand of y-block Y = X of the parent's contraction, so a
+// child feeds its parent straight from registers.  The A operand of block (X, Y) is
+// P[4X + lo][4Y + hi] -- pattern-independent, one 16-double tile per (class, X, Y) in LDS,
+// read with ds_read_b64 at a constant offset (the 4 blocks of a lane group broadcast).
+//
+// All classes in one wave: the joint (all states, all classes) exact power-of-two
+// rescale of the other kernels is an in-register max plus two shuffles -- no LDS exchange
+// and no barrier per node (treeM_kernel's one-class-per-wave layout needs two per node).
+//
+// Per tree: the fragment programs of build_tree4_program (cherries as T_CHERRY rows of
+// the contribution tables built by cherry_table_kernel) are emitted as straight-line HIP
+// -- constant branch / cherry / slot offsets, no program decode -- and compiled once per
+// (program, shape) with hiprtc.  The P(t) of the next contributing branch is loaded into
+// registers while the current contraction runs and written to the other LDS buffer
+// behind one workgroup barrier; operands of later events (cherry rows, tip rows, child
+// partials from HBM) are fetched L events ahead.
+//
+// Results are not bitwise those of treeM_kernel (the dot products group their terms in
+// 4-term MFMA blocks instead of 16x16 tiles); the traversal is checked against the oracle
+// at 1e-12 per pattern, and lnL-only vs materialising runs of this kernel are bitwise
+// identical (same program, same operations).
+#pragma once
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "plk_tree4.hpp"
+#include "plk_treeM.hpp"
+
+namespace plk {
+
+static const char* kJitMPrelude = R"PLKJITM(
+typedef unsigned char u8;
+typedef unsigned short u16;
+typedef long long i64;
+typedef int i32;
+#define kTile 128
+#define kLn2x256 177.44567822334599921
+#define kScaleUp 115792089237316195423570985008687907853269984665640564039457584007913129639936.0
+#define kScaleThr (1.0 / kScaleUp)
+
+struct JMArgs {
+  double* partials; i32* scale; const u8* codes; const double* tipP; const u8* cherry; const double* pmats;
+  const double* weights; const double* pi; const double* probs; double* site_lnl; double* wave_sums;
+  i64 slot_stride; i64 n_pad; i64 n_patterns; i64 cherry_stride; i64 cherry_table_bytes; i64 cherry_count_bytes;
+  i32 guard;
+};
+
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __attribute__((noinline)) double jitm_log(double x) { return log(x); }
+)PLKJITM";
+
+// Host mirror of JMArgs (field order and types must match the prelude).
+struct JMArgs {
+  double* partials;
+  int32_t* scale;
+  const uint8_t* codes;
+  const double* tipP;
+  const uint8_t* cherry;
+  const double* pmats;
+  const double* weights;
+  const double* pi;
+  const double* probs;
+  double* site_lnl;
+  double* wave_sums;
+  int64_t slot_stride;
+  int64_t n_pad;
+  int64_t n_patterns;
+  int64_t cherry_stride;
+  int64_t cherry_table_bytes;
+  int64_t cherry_count_bytes;
+  int32_t guard;
+};
+
+struct JitMShape {
+  int S = 20;
+  int C = 1;
+  int U = 1;         // codes in use (rows of a tip table; cherry tables have U * U)
+  bool scale = false;
+  int L = 1;         // operand fetch lookahead (events)
+  int minw = 2;      // __launch_bounds__ min waves per SIMD
+  static constexpr int G = 4;  // waves (16-pattern groups) per workgroup: 64 patterns
+  int pb() const { return C * S * S; }  // doubles per P buffer (every class of one branch)
+  size_t lds_bytes() const { return (size_t)(2 * pb() + 64) * sizeof(double); }
+  bool operator==(const JitMShape& o) const {
+    return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw;
+  }
+};
+
+// Emit the kernel for build_tree4_program's words `prog` and fragment start offsets
+// `starts` (tier order; fragment id = frag_base + blockIdx.y).
+inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts,
+                                     const JitMShape& sh) {
+  const int S = sh.S, C = sh.C, XB = S / 4, L = std::max(sh.L, 1);
+  std::string s;
+  s.reserve(65536 * std::max<size_t>(starts.size(), 1));
+  s += kJitMPrelude;
+  char buf[512];
+  const int NTH = 64 * JitMShape::G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH;
+  snprintf(buf, sizeof(buf),
+           "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
+           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n",
+           S, C, XB, sh.U, sh.U * sh.U, JitMShape::G, NTH, PB, PF, sh.scale ? "true" : "false");
+  s += buf;
+  s += R"PLKJITM(
+// P(t) of branch b (all classes, [c][x][y]) -> registers -> the LDS tile image
+// [c][X][Y][hi][lo] with tile element (hi, lo) = P[4X + lo][4Y + hi]
+#define PSTAGE_LOAD(R, b) { const double* s_ = a.pmats + (i64)(b) * PB_; \
+  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) { const int e_ = tid + j_ * NTH_; R[j_] = s_[e_ < PB_ ? e_ : PB_ - 1]; } }
+#define PSTAGE_STORE(R, bf) { double* d_ = lds + (bf) * PB_; \
+  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) if (sidx[j_] >= 0) d_[sidx[j_]] = R[j_]; }
+// D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1)
+#define CONTRIB(D, SRC, bf, SET) { const double* P_ = PA + (bf) * PB_; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
+    double d_ = 0.0; \
+    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) d_ = mfma4(P_[((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
+    if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } }
+#define ROWMUL(D, F, SET) { _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") \
+  for (int X_ = 0; X_ < XB_; ++X_) { if (SET) D[c_][X_] = F[c_][X_]; else D[c_][X_] *= F[c_][X_]; } }
+// one row of cherry k's contribution table (combined code of the pattern's two tips)
+#define CHERRY_FETCH(F, FK, k) { const u8* base_ = a.cherry + (i64)(k) * a.cherry_stride; \
+  const int code_ = reinterpret_cast<const u16*>(base_ + a.cherry_table_bytes + a.cherry_count_bytes)[p]; \
+  const double* r_ = reinterpret_cast<const double*>(base_) + (i64)code_ * S_ + hi; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
+    F[c_][X_] = r_[(i64)c_ * (U2_ * S_) + 4 * X_]; \
+  if (SC_) FK = (int)base_[a.cherry_table_bytes + code_]; }
+#define TIP_FETCH(F, t) { const int code_ = a.codes[(i64)(t) * a.n_pad + p]; \
+  const double* r_ = a.tipP + ((i64)(t) * (C_ * U_) + code_) * S_ + hi; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
+    F[c_][X_] = r_[(i64)c_ * (U_ * S_) + 4 * X_]; }
+#define LOAD_FETCH(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
+    F[c_][X_] = L_[(i64)(c_ * S_ + 4 * X_) * kTile]; \
+  if (SC_) FK = a.scale[(i64)(slot) * a.n_pad + p]; }
+#define STORE(V, K, slot) { double* D_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
+    __builtin_nontemporal_store(V[c_][X_], D_ + (i64)(c_ * S_ + 4 * X_) * kTile); \
+  if (SC_ && hi == 0) a.scale[(i64)(slot) * a.n_pad + p] = K; }
+// joint exact power-of-two rescale of the pattern (its states sit in lanes hi = 0..3)
+#define RESCALE(V, K) { double m_ = 0.0; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) m_ = fmax(m_, V[c_][X_]); \
+  m_ = fmax(m_, __shfl_xor(m_, 16, 64)); m_ = fmax(m_, __shfl_xor(m_, 32, 64)); \
+  if (m_ > 0.0 && m_ < kScaleThr) { \
+    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) V[c_][X_] *= kScaleUp; \
+    K += 1; } }
+// root reduction (RHomogeneousTreeLikelihood.cpp:162-216 / NH :168-233) and the fixed
+// butterfly over the workgroup's 64 patterns (root_kernel's order)
+#define REDUCE_ROOT(V, K) { double l_ = 0.0; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { double s_ = 0.0; \
+    _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { const double li_ = V[c_][X_] * a.pi[4 * X_ + hi]; \
+      if (a.guard) { if (li_ > 0.0) s_ += li_; } else { s_ += li_; } } \
+    s_ += __shfl_xor(s_, 16, 64); s_ += __shfl_xor(s_, 32, 64); \
+    const double t_ = s_ * a.probs[c_]; \
+    if (a.guard) { if (t_ > 0.0) l_ += t_; } else { l_ += t_; } } \
+  if (!a.guard && l_ < 0.0) l_ = 0.0; \
+  double rr_ = jitm_log(l_); \
+  if (SC_) rr_ -= (double)K * kLn2x256; \
+  double wr_ = 0.0; \
+  if (p < a.n_patterns) { if (hi == 0) a.site_lnl[p] = rr_; wr_ = a.weights[p] * rr_; } \
+  if (hi == 0) red[16 * w + pl] = wr_; \
+  __syncthreads(); \
+  if (w == 0) { double v_ = red[lane]; \
+    _Pragma("unroll") for (int off_ = 32; off_ > 0; off_ >>= 1) v_ += __shfl_xor(v_, off_, 64); \
+    if (lane == 0) a.wave_sums[p0 >> 6] = v_; } }
+#define SB __builtin_amdgcn_sched_barrier(0);
+)PLKJITM";
+  snprintf(buf, sizeof(buf),
+           "extern \"C\" __global__ __launch_bounds__(%d, %d) void plk_jit_treeM(JMArgs a, int frag_base) {\n", NTH,
+           std::max(sh.minw, 1));
+  s += buf;
+  s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PB_] P tiles | red[64]
+  double* red = lds + 2 * PB_;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 4, pl = lane & 15;
+  const i64 p0 = (i64)blockIdx.x * (16 * G_);
+  const i64 p = p0 + 16 * w + pl;
+  const i64 toff = (p >> 7) * (i64)(C_ * S_ * kTile) + (p & (kTile - 1)) + (i64)hi * kTile;
+  const double* PA = lds + ((hi << 2) | (lane & 3));
+  int sidx[PF_];   // this thread's staging elements -> tile slots (-1: past the table)
+  _Pragma("unroll") for (int j = 0; j < PF_; ++j) {
+    const int e = tid + j * NTH_;
+    const int c = e / (S_ * S_), r = e - c * (S_ * S_), x = r / S_, y = r - x * S_;
+    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3) : -1;
+  }
+  double R[PF_];
+  (void)red; (void)PA; (void)R; (void)toff;
+  const int frag = frag_base + (int)blockIdx.y;
+)PLKJITM";
+  // accumulators per register level and the operand ring
+  int max_level = 0;
+  for (size_t f = 0; f < starts.size(); ++f) {
+    int d = 0;
+    for (size_t i = (size_t)starts[f]; prog[i].op != T_ROOT; ++i) {
+      if (prog[i].op == T_DESCEND) max_level = std::max(max_level, ++d);
+      if (prog[i].op == T_ASCEND) --d;
+    }
+  }
+  for (int d = 0; d <= max_level; ++d) {
+    snprintf(buf, sizeof(buf), "  double A%d[C_][XB_]; int K%d = 0; (void)K%d;\n", d, d, d);
+    s += buf;
+  }
+  for (int r = 0; r <= L; ++r) {
+    snprintf(buf, sizeof(buf), "  double F%d[C_][XB_]; int FK%d = 0; (void)FK%d;\n", r, r, r);
+    s += buf;
+  }
+  s += "  switch (frag) {\n";
+  for (size_t f = 0; f < starts.size(); ++f) {
+    std::vector<TInstr> ev;
+    for (size_t i = (size_t)starts[f];; ++i) {
+      ev.push_back(prog[i]);
+      if (prog[i].op == T_ROOT) break;
+    }
+    // operand fetchers (ring slots) and the P chain (events that contract through a branch)
+    std::vector<int> slot(ev.size(), -1), fetchers, pchain;
+    for (size_t i = 0; i < ev.size(); ++i) {
+      const int op = ev[i].op;
+      if (op == T_CHERRY || op == T_TIP || op == T_LOAD) {
+        slot[i] = (int)(fetchers.size() % (size_t)(L + 1));
+        fetchers.push_back((int)i);
+      }
+      if (op == T_LOAD || (op == T_ASCEND && ev[i].b >= 0)) pchain.push_back((int)i);
+    }
+    auto emit_fetch = [&](int i) {
+      const TInstr& e = ev[(size_t)i];
+      const int sl = slot[(size_t)i];
+      if (e.op == T_CHERRY)
+        snprintf(buf, sizeof(buf), "    CHERRY_FETCH(F%d, FK%d, %d)\n", sl, sl, e.a);
+      else if (e.op == T_TIP)
+        snprintf(buf, sizeof(buf), "    TIP_FETCH(F%d, %d)\n", sl, e.a);
+      else
+        snprintf(buf, sizeof(buf), "    LOAD_FETCH(F%d, FK%d, %d)\n", sl, sl, e.a);
+      s += buf;
+    };
+    snprintf(buf, sizeof(buf), "  case %zu: {\n", f);
+    s += buf;
+    size_t nf = 0;
+    for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
+    int cur = 0;
+    size_t np = 0;  // P-chain events consumed
+    if (!pchain.empty()) {
+      const TInstr& e0 = ev[(size_t)pchain[0]];
+      snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R, %d) PSTAGE_STORE(R, 0) __syncthreads();\n", e0.b);
+      s += buf;
+    }
+    s += "    SB\n";
+    std::vector<char> fresh((size_t)max_level + 2, 0);
+    fresh[0] = 1;
+    int d = 0;
+    for (size_t i = 0; i < ev.size(); ++i) {
+      const TInstr& e = ev[i];
+      if (e.op == T_CHERRY || e.op == T_TIP || e.op == T_LOAD) {
+        if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
+        const int sl = slot[i];
+        if (e.op == T_LOAD) {
+          const bool more = np + 1 < pchain.size();
+          if (more) {
+            snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R, %d)\n", ev[(size_t)pchain[np + 1]].b);
+            s += buf;
+          }
+          snprintf(buf, sizeof(buf), "    CONTRIB(A%d, F%d, %d, %s)\n", d, sl, cur, fresh[(size_t)d] ? "true" : "false");
+          s += buf;
+          if (more) {
+            snprintf(buf, sizeof(buf), "    PSTAGE_STORE(R, %d) __syncthreads();\n", cur ^ 1);
+            s += buf;
+            cur ^= 1;
+          }
+          ++np;
+          if (sh.scale) {
+            snprintf(buf, sizeof(buf), "    K%d += FK%d;\n", d, sl);
+            s += buf;
+          }
+        } else {
+          snprintf(buf, sizeof(buf), "    ROWMUL(A%d, F%d, %s)\n", d, sl, fresh[(size_t)d] ? "true" : "false");
+          s += buf;
+          if (e.op == T_CHERRY && sh.scale) {
+            snprintf(buf, sizeof(buf), "    K%d += FK%d;\n", d, sl);
+            s += buf;
+          }
+        }
+        fresh[(size_t)d] = 0;
+        s += "    SB\n";
+      } else if (e.op == T_DESCEND) {
+        ++d;
+        fresh[(size_t)d] = 1;
+        snprintf(buf, sizeof(buf), "    K%d = 0;\n", d);
+        s += buf;
+      } else if (e.op == T_ASCEND) {
+        if (e.b < 0) continue;  // the fragment root: finished by ROOT
+        if (sh.scale) {
+          snprintf(buf, sizeof(buf), "    RESCALE(A%d, K%d)\n", d, d);
+          s += buf;
+        }
+        if (e.a >= 0) {
+          snprintf(buf, sizeof(buf), "    STORE(A%d, K%d, %d)\n", d, d, e.a);
+          s += buf;
+        }
+        const bool more = np + 1 < pchain.size();
+        if (more) {
+          snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R, %d)\n", ev[(size_t)pchain[np + 1]].b);
+          s += buf;
+        }
+        snprintf(buf, sizeof(buf), "    CONTRIB(A%d, A%d, %d, %s)\n", d - 1, d, cur, fresh[(size_t)d - 1] ? "true" : "false");
+        s += buf;
+        if (more) {
+          snprintf(buf, sizeof(buf), "    PSTAGE_STORE(R, %d) __syncthreads();\n", cur ^ 1);
+          s += buf;
+          cur ^= 1;
+        }
+        ++np;
+        if (sh.scale) {
+          snprintf(buf, sizeof(buf), "    K%d += K%d;\n", d - 1, d);
+          s += buf;
+        }
+        fresh[(size_t)d - 1] = 0;
+        --d;
+        s += "    SB\n";
+      } else {  // T_ROOT
+        if (sh.scale) s += "    RESCALE(A0, K0)\n";
+        if (e.a >= 0) {
+          snprintf(buf, sizeof(buf), "    STORE(A0, K0, %d)\n", e.a);
+          s += buf;
+        }
+        if (e.b) s += "    REDUCE_ROOT(A0, K0)\n";
+      }
+    }
+    s += "  } break;\n";
+  }
+  s += "  default: break;\n  }\n}\n";
+  return s;
+}
+
+}  // namespace plk

@@ -45,6 +45,8 @@ class TreeLikelihood : public AbstractParametrizable {
   virtual double getFirstOrderDerivative(const std::string& variable) const = 0;
   virtual double getSecondOrderDerivative(const std::string& variable) const = 0;
   virtual void enableDerivatives(bool yn) = 0;
+  // both analytic branch-length derivatives enabled (PseudoNewton then uses them)
+  virtual bool derivativesEnabled() const { return false; }
   virtual void enableFirstOrderDerivatives(bool yn) = 0;
   virtual void enableSecondOrderDerivatives(bool yn) = 0;
 };
@@ -132,6 +134,7 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   double getFirstOrderDerivative(const std::string& variable) const override;
   double getSecondOrderDerivative(const std::string& variable) const override;
   void enableDerivatives(bool yn) override { derivFirst_ = derivSecond_ = yn; }
+  bool derivativesEnabled() const override { return derivFirst_ && derivSecond_; }
   void enableFirstOrderDerivatives(bool yn) override { derivFirst_ = yn; }
   void enableSecondOrderDerivatives(bool yn) override { derivSecond_ = yn; }
   const std::vector<unsigned int>& getWeights() const { return rootWeights_; }

@@ -1,9 +1,12 @@
 // Host-side optimisers driving repeated likelihood evaluations (the callers of the
 // hot path): optimizeTreeScale (OptimizationTools.cpp:119-143) and
 // optimizeNumericalParameters2 (:266-353).  Every function evaluation is one GPU
-// evaluation through fireParameterChanged.  The search is a bounded Brent line
-// search per parameter, cycled to convergence; it reaches the same optimum as the
-// reference's PseudoNewton/BFGS combination (the test goldens are optima).
+// evaluation through fireParameterChanged.  optimizeNumericalParameters2 with
+// OPTIMIZATION_NEWTON (the default) restates PseudoNewtonOptimizer::doStep
+// (Likelihood/PseudoNewtonOptimizer.cpp:96-190) with the device's analytic branch-length
+// derivatives; other methods (and BPP_AMD_OPT_BRENT=1) use a bounded Brent line search per
+// parameter, cycled to convergence.  optimizeTreeScale is Brent on the log scale factor as in
+// the reference (:119-143).
 #ifndef BPP_AMD_OPTIMIZATIONTOOLS_H
 #define BPP_AMD_OPTIMIZATIONTOOLS_H
 
@@ -39,6 +42,11 @@ struct OptimizationTools {
                                                    OutputStream* profiler = nullptr, bool reparametrization = false,
                                                    bool useClock = false, unsigned int verbose = 1,
                                                    const std::string& optMethodDeriv = OPTIMIZATION_NEWTON);
+
+  // PseudoNewton steps of the last OPTIMIZATION_NEWTON run (diagnostics)
+  static unsigned int lastSteps_;
+  static unsigned int pseudoNewtonParameters(TreeLikelihood* tl, const ParameterList& pl, double tolerance,
+                                             unsigned int tlEvalMax, bool useClock);
 
   // Bounded 1-D Brent minimisation of f on [a, b]; returns the argmin, *fmin the value.
   template <class F>

@@ -23,6 +23,23 @@ int deviceFromEnv() {
   const char* e = std::getenv("BPP_AMD_DEVICE");
   return e ? std::atoi(e) : 0;
 }
+
+// BPP_AMD_DEVICES=0,1,2,...: shard the site patterns over these devices (plk_create_multi);
+// empty: one device (BPP_AMD_DEVICE, default 0)
+std::vector<int> devicesFromEnv() {
+  std::vector<int> d;
+  const char* e = std::getenv("BPP_AMD_DEVICES");
+  if (!e) return d;
+  std::string s(e);
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t j = s.find(',', i);
+    if (j == std::string::npos) j = s.size();
+    if (j > i) d.push_back(std::atoi(s.substr(i, j - i).c_str()));
+    i = j + 1;
+  }
+  return d;
+}
 }  // namespace
 
 void AbstractPlkTreeLikelihood::check(int rc, const char* what) const {
@@ -136,8 +153,11 @@ void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
   unsigned flags = (scaling_ ? (unsigned)PLK_FLAG_SCALING : 0u) | (nonNegGuard ? (unsigned)PLK_FLAG_NONNEG_GUARD : 0u) |
                    extraFlags_;
   plk_handle h = nullptr;
-  int rc = plk_create(deviceFromEnv(), (int)nbStates_, (int)nbClasses_, (int64_t)nbDistinctSites_, nTips_, nInternal_,
-                      (int)nModels, flags, &h);
+  const std::vector<int> devs = devicesFromEnv();
+  int rc = devs.empty() ? plk_create(deviceFromEnv(), (int)nbStates_, (int)nbClasses_, (int64_t)nbDistinctSites_, nTips_,
+                                     nInternal_, (int)nModels, flags, &h)
+                        : plk_create_multi(devs.data(), (int)devs.size(), (int)nbStates_, (int)nbClasses_,
+                                           (int64_t)nbDistinctSites_, nTips_, nInternal_, (int)nModels, flags, &h);
   if (rc != PLK_OK) throw DeviceException(rc, std::string("plk_create: ") + plk_last_error(nullptr));
   engine_ = h;
 }

@@ -2,9 +2,13 @@
 #include "Bpp/Phyl/OptimizationTools.h"
 
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
 #include <limits>
 #include <map>
 #include <memory>
+#include <vector>
 
 namespace bpp {
 
@@ -50,6 +54,116 @@ void searchInterval(const Parameter& p, double* lo, double* hi, bool* logScale) 
       *hi = std::min(*hi, x + 10. * std::max(1., std::fabs(x)));
     }
   }
+}
+
+// One parameter of a PseudoNewton problem: its constraint (CONSTRAINTS_AUTO maps an
+// out-of-range value to the accepted limit, bpp-core AutoParameter) and whether the
+// likelihood supplies analytic derivatives for it.
+struct PNParam {
+  std::string name;
+  std::shared_ptr<Constraint> constraint;
+  bool analytic = false;
+  double accept(double v) const {
+    return (constraint && !constraint->isCorrect(v)) ? constraint->getAcceptedLimit(v) : v;
+  }
+  bool correct(double v) const { return !constraint || constraint->isCorrect(v); }
+};
+
+// PseudoNewtonOptimizer (Likelihood/PseudoNewtonOptimizer.cpp:96-190) as
+// optimizeNumericalParameters2 sets it up for OPTIMIZATION_NEWTON (OptimizationTools.cpp:
+// 266-353): the function is -lnL; branch lengths take the likelihood's analytic d1 / d2
+// (getFirstOrderDerivative / getSecondOrderDerivative, the device path derivatives), the
+// non-derivable parameters a ThreePointsNumericalDerivative of interval 1e-4 (:311-314,
+// 330-331).  Each step moves every parameter by d1 / |d2| at once (0 if d2 == 0 or the move
+// is NaN), clamped into its constraint; while f grows by more than the tolerance (or is NaN)
+// the Felsenstein-Churchill correction halves all moves, at most 10 times; a step that cannot
+// improve keeps the point.  Stop: |f_new - f_old| < tolerance (FunctionStopCondition) or the
+// evaluation budget.  Deviation: the reference swaps the fourth correction for a
+// conjugate-gradient search (useCG_, :151-170); here the halving continues.
+// f(x) sets every parameter and returns -lnL; evaluations are counted in *nEval.
+unsigned int pseudoNewton(const std::vector<PNParam>& par, std::vector<double>& x,
+                          const std::function<double(const std::vector<double>&)>& f,
+                          const std::function<void(size_t, double*, double*)>& analytic, double tolerance,
+                          unsigned int maxEval, unsigned int* steps_out) {
+  const size_t n = par.size();
+  unsigned int nEval = 0, steps = 0;
+  auto eval = [&](const std::vector<double>& y) {
+    nEval++;
+    return f(y);
+  };
+  double fcur = eval(x);
+  std::vector<double> d1(n), d2(n), mv(n), y(n);
+  const double kInterval = 0.0001;
+  while (nEval < maxEval) {
+    steps++;
+    // derivatives at x (the likelihood sits at x)
+    bool moved_away = false;
+    for (size_t i = 0; i < n; i++) {
+      if (par[i].analytic) {
+        if (moved_away) {
+          eval(x);
+          moved_away = false;
+        }
+        analytic(i, &d1[i], &d2[i]);
+        continue;
+      }
+      // ThreePointsNumericalDerivative: central differences, one-sided at a constraint
+      const double v = x[i], h = (1. + std::fabs(v)) * kInterval;
+      y = x;
+      double fm, fp, f2;
+      if (par[i].correct(v - h) && par[i].correct(v + h)) {
+        y[i] = v - h;
+        fm = eval(y);
+        y[i] = v + h;
+        fp = eval(y);
+        d1[i] = (fp - fm) / (2. * h);
+        d2[i] = (fp - 2. * fcur + fm) / (h * h);
+      } else if (par[i].correct(v + 2. * h)) {  // left limit: forward
+        y[i] = v + h;
+        fp = eval(y);
+        y[i] = v + 2. * h;
+        f2 = eval(y);
+        d1[i] = (fp - fcur) / h;
+        d2[i] = (f2 - 2. * fp + fcur) / (h * h);
+      } else {  // right limit: backward
+        y[i] = v - h;
+        fm = eval(y);
+        y[i] = v - 2. * h;
+        f2 = eval(y);
+        d1[i] = (fcur - fm) / h;
+        d2[i] = (fcur - 2. * fm + f2) / (h * h);
+      }
+      moved_away = true;
+    }
+    if (moved_away) eval(x);
+    // Newton moves (PseudoNewtonOptimizer.cpp:108-135)
+    for (size_t i = 0; i < n; i++) {
+      double m = d2[i] == 0. ? 0. : (d2[i] < 0. ? -d1[i] / d2[i] : d1[i] / d2[i]);
+      if (std::isnan(m)) m = 0.;
+      y[i] = par[i].accept(x[i] - m);
+      mv[i] = x[i] - y[i];
+    }
+    double fnew = eval(y);
+    // Felsenstein-Churchill correction (:140-175)
+    for (unsigned int count = 0; count < 10 && (fnew > fcur + tolerance || std::isnan(fnew)); count++) {
+      for (size_t i = 0; i < n; i++) {
+        mv[i] /= 2.;
+        y[i] = par[i].accept(x[i] - mv[i]);
+      }
+      fnew = eval(y);
+    }
+    if (fnew > fcur + tolerance || std::isnan(fnew)) {
+      eval(x);  // could not be ameliorated: stay at x
+      fnew = fcur;
+    } else {
+      x = y;
+    }
+    const bool done = std::fabs(fnew - fcur) < tolerance;
+    fcur = fnew;
+    if (done) break;
+  }
+  if (steps_out) *steps_out = steps;
+  return nEval;
 }
 
 }  // namespace
@@ -127,11 +241,91 @@ struct ClockMap {
 
 }  // namespace
 
+// optimizeNumericalParameters2 with OPTIMIZATION_NEWTON (the default): PseudoNewton over
+// the requested parameters, or with useClock over the non-branch parameters plus the clock
+// heights of GlobalClockTreeLikelihoodFunctionWrapper (TotalHeight, HeightP_v), whose
+// derivatives are numerical (OptimizationTools.cpp:277-288, 329-331).
+unsigned int OptimizationTools::pseudoNewtonParameters(TreeLikelihood* tl, const ParameterList& pl, double tolerance,
+                                                       unsigned int tlEvalMax, bool useClock) {
+  std::vector<PNParam> par;
+  std::vector<double> x;
+  std::vector<size_t> plIndex;  // parameter -> index in pl (non-clock parameters)
+  std::unique_ptr<ClockMap> clock;
+  ParameterList brl;
+  const bool deriv = tl->derivativesEnabled();
+  for (size_t i = 0; i < pl.size(); i++) {
+    const bool br = pl[i].getName().compare(0, 5, "BrLen") == 0;
+    if (useClock && br) continue;
+    PNParam p;
+    p.name = pl[i].getName();
+    if (pl[i].hasConstraint()) p.constraint.reset(pl[i].getConstraint()->clone());
+    p.analytic = br && deriv;
+    par.push_back(p);
+    x.push_back(pl[i].getValue());
+    plIndex.push_back(i);
+  }
+  const size_t nPlain = par.size();
+  if (useClock) {
+    const TreeTemplate<Node>* tree = dynamic_cast<const TreeTemplate<Node>*>(&tl->getTree());
+    clock.reset(new ClockMap(*tree));
+    brl = tl->getBranchLengthsParameters();
+    PNParam th;
+    th.name = "TotalHeight";
+    th.constraint.reset(new IntervalConstraint(0., 1e300, false, true));
+    par.push_back(th);
+    x.push_back(clock->totalHeight);
+    for (size_t k = 0; k < clock->heightP.size(); k++) {
+      PNParam hp;
+      hp.name = "HeightP" + std::to_string(k);
+      hp.constraint.reset(new IntervalConstraint(1e-6, 1. - 1e-6, true, true));
+      par.push_back(hp);
+      x.push_back(clock->heightP[k]);
+    }
+  }
+  ParameterList cur = pl;
+  auto f = [&](const std::vector<double>& y) {
+    ParameterList set;
+    for (size_t i = 0; i < nPlain; i++) {
+      Parameter q = cur[plIndex[i]];
+      q.setValue(y[i]);
+      set.addParameter(q);
+    }
+    if (clock) {
+      clock->totalHeight = y[nPlain];
+      for (size_t k = 0; k < clock->heightP.size(); k++) clock->heightP[k] = y[nPlain + 1 + k];
+      const std::vector<double> bl = clock->branchLengths();
+      for (size_t i = 0; i < brl.size(); i++) {
+        Parameter q = brl[i];
+        q.setValue(bl[i]);
+        set.addParameter(q);
+      }
+    }
+    tl->setParameters(set);
+    return tl->getValue();
+  };
+  auto an = [&](size_t i, double* d1, double* d2) {
+    *d1 = tl->getFirstOrderDerivative(par[i].name);
+    *d2 = tl->getSecondOrderDerivative(par[i].name);
+  };
+  unsigned int steps = 0;
+  const unsigned int nEval = pseudoNewton(par, x, f, an, tolerance, tlEvalMax, &steps);
+  f(x);  // leave the likelihood at the accepted point
+  lastSteps_ = steps;
+  if (std::getenv("BPP_AMD_OPT_LOG"))
+    std::fprintf(stderr, "PseudoNewton: %u steps, %u function evaluations, -lnL = %.12f\n", steps, nEval,
+                 tl->getValue());
+  return nEval;
+}
+
+unsigned int OptimizationTools::lastSteps_ = 0;
+
 unsigned int OptimizationTools::optimizeNumericalParameters2(TreeLikelihood* tl, const ParameterList& parameters,
                                                              OptimizationListener*, double tolerance,
                                                              unsigned int tlEvalMax, OutputStream*, OutputStream*,
-                                                             bool, bool useClock, unsigned int, const std::string&) {
+                                                             bool, bool useClock, unsigned int, const std::string& optMethodDeriv) {
   ParameterList pl = tl->getParameters().getCommonParametersWith(parameters);
+  if (optMethodDeriv == OPTIMIZATION_NEWTON && !std::getenv("BPP_AMD_OPT_BRENT"))
+    return pseudoNewtonParameters(tl, pl, tolerance, tlEvalMax, useClock);
   unsigned int nEval = 0;
   std::unique_ptr<ClockMap> clock;
   ParameterList brl;

@@ -36,7 +36,8 @@ EXPORTS = [
     "plk_get_pmatrix", "plk_update_partials", "plk_get_partials", "plk_root_loglik", "plk_block_size",
     "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
     "plk_kernel_path", "plk_evaluate", "plk_compressed_work", "plk_all_branch_derivatives",
-    "plk_get_timing_ex", "plk_traversal_work",
+    "plk_get_timing_ex", "plk_traversal_work", "plk_create_multi", "plk_shard_count", "plk_comm_get_id",
+    "plk_comm_init",
 ]
 
 
@@ -62,6 +63,10 @@ class plk_work(ct.Structure):
                 ("table_flops", ct.c_double), ("exact", ct.c_int32), ("internal_nodes", ct.c_int32)]
 
 
+class plk_comm_id(ct.Structure):
+    _fields_ = [("internal", ct.c_char * 128)]
+
+
 _lib = None
 
 
@@ -82,6 +87,11 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_create": ([ct.c_int, ct.c_int, ct.c_int, ct.c_int64, ct.c_int, ct.c_int, ct.c_int, ct.c_uint,
                         P(ct.c_void_p)], ct.c_int),
         "plk_destroy": ([ct.c_void_p], ct.c_int),
+        "plk_create_multi": ([P(ct.c_int), ct.c_int, ct.c_int, ct.c_int, ct.c_int64, ct.c_int, ct.c_int, ct.c_int,
+                              ct.c_uint, P(ct.c_void_p)], ct.c_int),
+        "plk_shard_count": ([ct.c_void_p, P(ct.c_int)], ct.c_int),
+        "plk_comm_get_id": ([P(plk_comm_id)], ct.c_int),
+        "plk_comm_init": ([ct.c_void_p, ct.c_int, ct.c_int, P(plk_comm_id)], ct.c_int),
         "plk_set_code_table": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
         "plk_set_tip_codes": ([ct.c_void_p, ct.c_int, P(ct.c_uint8)], ct.c_int),
         "plk_set_pattern_weights": ([ct.c_void_p, dp], ct.c_int),
@@ -132,6 +142,16 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+def comm_get_id() -> bytes:
+    """plk_comm_get_id (ncclGetUniqueId) on one rank; share the 128 bytes with the others."""
+    cid = plk_comm_id()
+    lib = load()
+    rc = lib.plk_comm_get_id(ct.byref(cid))
+    if rc != PLK_OK:
+        raise PlkError(rc, lib.plk_last_error(None).decode())
+    return bytes(cid.internal)
+
+
 def build_id() -> str:
     return load().plk_build_id().decode()
 
@@ -161,16 +181,24 @@ def make_ops(ops: Sequence[Tuple[int, Sequence[int], int]]):
 class Engine:
     """One libplk handle (one device, one pattern shard)."""
 
-    def __init__(self, device: int, n_states: int, n_classes: int, n_patterns: int, n_tips: int,
+    def __init__(self, device, n_states: int, n_classes: int, n_patterns: int, n_tips: int,
                  n_internal: int, n_models: int = 1, flags: int = PLK_FLAG_NONNEG_GUARD):
+        """device: one HIP device, or a list of devices (plk_create_multi: the patterns are
+        sharded over them in contiguous block-aligned ranges; same calls, whole-alignment
+        arguments)."""
         self.lib = load()
         self.h = ct.c_void_p()
         self.S, self.C, self.P = n_states, n_classes, n_patterns
         self.n_tips, self.n_internal = n_tips, n_internal
         self._ops_cache = None
         self._eval_cache = None
-        rc = self.lib.plk_create(device, n_states, n_classes, n_patterns, n_tips, n_internal, n_models, flags,
-                                 ct.byref(self.h))
+        if isinstance(device, (list, tuple)):
+            devs = (ct.c_int * len(device))(*device)
+            rc = self.lib.plk_create_multi(devs, len(device), n_states, n_classes, n_patterns, n_tips, n_internal,
+                                           n_models, flags, ct.byref(self.h))
+        else:
+            rc = self.lib.plk_create(device, n_states, n_classes, n_patterns, n_tips, n_internal, n_models, flags,
+                                     ct.byref(self.h))
         if rc != PLK_OK:
             raise PlkError(rc, self.lib.plk_last_error(None).decode())
 
@@ -328,6 +356,18 @@ class Engine:
         n = ct.c_int64(0)
         self._chk(self.lib.plk_compressed_work(self.h, ct.byref(n)))
         return n.value
+
+    def shard_count(self) -> int:
+        n = ct.c_int(0)
+        self._chk(self.lib.plk_shard_count(self.h, ct.byref(n)))
+        return n.value
+
+    def comm_init(self, n_ranks: int, rank: int, comm_id: bytes):
+        """plk_comm_init: RCCL communicator inside the handle; evaluations then return the
+        global lnL of all ranks (one all-gather of block sums per evaluation)."""
+        cid = plk_comm_id()
+        ct.memmove(cid.internal, comm_id, 128)
+        self._chk(self.lib.plk_comm_init(self.h, n_ranks, rank, ct.byref(cid)))
 
     def kernel_path(self) -> str:
         """Kernel that served the last update_partials ("jit_tree4", "tree4", "treeS", "treeM", "levelwise")."""

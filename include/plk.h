@@ -114,19 +114,53 @@ typedef struct plk_handle_s* plk_handle;
 
 /* Library / device */
 int plk_abi_version(void);
-/* First 16 hex digits of the SHA-256 of the library's sources (csrc/*.hip, csrc/*.hpp in
+/* First 16 hex digits of the SHA-256 of the library's sources (the .hip and .hpp files of csrc in
  * sorted order, then this header), fixed at compile time: lets a caller check that the
  * loaded binary was built from the sources it ships with. */
 const char* plk_build_id(void);
 int plk_device_count(int* count);
 const char* plk_last_error(plk_handle h); /* h may be NULL: last global error */
 
-/* Create an engine instance on HIP device `device`.
+/* Create an engine instance on HIP device `device`.  (Several devices: plk_create_multi
+ * below; several processes: plk_comm_init.)
  *   n_states: 2..64, n_classes: 1..16, n_patterns >= 1 (padded internally),
  *   n_models: number of eigen systems (1 for homogeneous; one per branch for NH). */
 int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int n_tips, int n_internal,
                int n_models, unsigned flags, plk_handle* out);
 int plk_destroy(plk_handle h);
+
+/* Multi-GPU at the boundary (SURVEY 8(b) device_mask, 8(e)).  Site patterns are
+ * independent, so a run is sharded into contiguous pattern ranges whose boundaries are
+ * multiples of plk_block_size(); each device evaluates its range with no traffic during
+ * the traversal, and the only exchange of an evaluation is the fixed-order block sums of
+ * the root reduction, summed in global block order -- the lnL is bitwise identical for any
+ * device count.
+ *
+ * One process, several devices: plk_create_multi takes the device list (a device may be
+ * listed twice: two shards on one GPU, for tests) and the TOTAL pattern count; the handle
+ * it returns accepts every call of this header with whole-alignment arguments (tip codes,
+ * weights, per-pattern outputs span all patterns) and fans them out: launches on all
+ * devices first, then one wait per device; each device's block sums arrive in mapped host
+ * memory and the host sums them in global order (the result is needed on the host, so an
+ * in-process collective would only add a hop).  Derivatives are summed over shards.  Timing
+ * and plk_kernel_path report shard 0; plk_traversal_work sums the shards. */
+int plk_create_multi(const int* devices, int n_devices, int n_states, int n_classes, int64_t n_patterns, int n_tips,
+                     int n_internal, int n_models, unsigned flags, plk_handle* out);
+int plk_shard_count(plk_handle h, int* n_shards);
+
+/* One process per GPU (torch.distributed / MPI launch): rank r creates its handle with
+ * plk_create for ITS pattern range, one rank gets an id with plk_comm_get_id and shares
+ * it (any channel), and every rank calls plk_comm_init.  From then on plk_root_loglik and
+ * plk_evaluate all-gather every rank's block sums over RCCL (xGMI) on the handle's stream
+ * -- one fixed-size ncclAllGather per evaluation -- and return the GLOBAL lnL on every
+ * rank (block_sums / site_lnl stay per rank).  Ranks must hold consecutive pattern ranges
+ * in rank order with block-aligned boundaries.  Replaces nothing in the reference (which
+ * is single-threaded); it is the single reduce north_star names. */
+typedef struct plk_comm_id {
+  char internal[128];
+} plk_comm_id;
+int plk_comm_get_id(plk_comm_id* id);
+int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id);
 
 /* Data */
 int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec /* n_codes x S */);

@@ -90,8 +90,20 @@ static void unrootedGammaCase() {
   }
   OptimizationTools::optimizeTreeScale(&tl);
   std::cout << "after tree scale: " << tl.getValue() << std::endl;
-  OptimizationTools::optimizeNumericalParameters2(&tl, tl.getParameters(), 0, 0.000001, 10000, 0, 0);
-  expectNear("T92+G4 optimised -lnL", tl.getValue(), 65.72293577214308868406, 1e-3);
+  const ParameterList scaled = tl.getParameters();
+  // the reference's default method: PseudoNewton on the device's analytic branch derivatives
+  const unsigned int nPN = OptimizationTools::optimizeNumericalParameters2(&tl, tl.getParameters(), 0, 0.000001, 10000, 0, 0);
+  std::cout << "PseudoNewton: " << OptimizationTools::lastSteps_ << " steps, " << nPN << " evaluations" << std::endl;
+  expectNear("T92+G4 optimised -lnL (PseudoNewton)", tl.getValue(), 65.72293577214308868406, 1e-3);
+  // the same optimum from the coordinate Brent search, for comparison of evaluation counts
+  RHomogeneousTreeLikelihood tlb(*tree, aln, &model, &rdist, true, false);
+  tlb.initialize();
+  tlb.setParameters(scaled);
+  const unsigned int nBrent = OptimizationTools::optimizeNumericalParameters2(
+      &tlb, tlb.getParameters(), 0, 0.000001, 10000, 0, 0, false, false, 0, OptimizationTools::OPTIMIZATION_BRENT);
+  std::cout << "Brent: " << nBrent << " evaluations" << std::endl;
+  expectNear("T92+G4 optimised -lnL (Brent)", tlb.getValue(), 65.72293577214308868406, 1e-3);
+  expectNear("PseudoNewton vs Brent optimum", tl.getValue(), tlb.getValue(), 1e-4);
 }
 
 // test/test_likelihood_clock.cpp:99-115: rooted tree kept rooted, constant rate

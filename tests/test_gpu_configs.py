@@ -30,7 +30,7 @@ REL = 1e-12
 # config -> (patterns for the oracle comparison, kernel path of the bench's mode)
 CASES = {
     "gtr_g4_dna_1M_64": (20000, "jit_tree4"),
-    "lg08_g4_protein_200k_256": (1500, "treeM"),
+    "lg08_g4_protein_200k_256": (1500, "jit_treeM"),
     "yn98_codon_50k_128": (3000, "treeM"),
     "nh_gtr_g4_dna_2M_512": (4000, "jit_tree4"),
 }

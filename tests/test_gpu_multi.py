@@ -1,0 +1,127 @@
+"""Multi-GPU at the C-ABI boundary, on the one-GPU test box.
+
+  - plk_create_multi: one process, several devices.  Listing device 0 twice gives two
+    shards on one GPU, which exercises everything the handle does for several GPUs --
+    block-aligned pattern ranges, sliced tip codes / weights / per-pattern outputs,
+    launches on every shard before the first wait, the global fixed-order block sum --
+    except the devices being different.  Results must equal one handle BITWISE (lnL,
+    block sums, per-pattern lnL, partials) for every kernel path.
+  - plk_comm_init: the RCCL communicator inside a handle (one process per GPU).  With one
+    rank the all-gather + device-side fixed-order sum must return the single-handle lnL
+    bitwise; multi-rank runs happen in bench.py --gpus N on a multi-GPU node.
+  - the Bio++ mirror sharded through BPP_AMD_DEVICES reproduces the reference goldens.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import phylo
+import plk
+import workload
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _setup(eng, wl, states):
+    eng.set_code_table(wl.alphabet.init_table)
+    for i in range(wl.et.n_tips):
+        eng.set_tip_codes(i, phylo.states_to_codes(states[i]))
+    eng.set_category_rates(wl.rates, wl.probs)
+    eng.set_root_frequencies(wl.root_freqs)
+    for k, m in enumerate(wl.models):
+        eng.set_eigen(k, m.V, m.Vinv, m.lam)
+    return eng
+
+
+@pytest.mark.parametrize("config,n,flags,devs", [
+    ("gtr_g4_dna_1M_64", 3 * 4096 + 100, plk.PLK_FLAG_LNL_ONLY, [0, 0]),
+    ("gtr_g4_dna_1M_64", 5 * 4096, 0, [0, 0, 0]),
+    ("lg08_g4_protein_200k_256", 2 * 4096 + 7, plk.PLK_FLAG_LNL_ONLY, [0, 0]),
+    ("yn98_codon_50k_128", 4096 + 50, plk.PLK_FLAG_LNL_ONLY, [0, 0]),
+    ("nh_gtr_g4_dna_2M_512", 3 * 4096, plk.PLK_FLAG_LNL_ONLY, [0, 0, 0]),
+    ("gtr_g4_dna_1M_64", 2 * 4096, plk.PLK_FLAG_LEVELWISE, [0, 0])])
+def test_multi_device_handle_bitwise(config, n, flags, devs):
+    wl = workload.make_workload(config, n_patterns=n)
+    et = wl.et
+    states = wl.simulate(0, n)
+    base = (plk.PLK_FLAG_SCALING if wl.scaling else 0) | (plk.PLK_FLAG_NONNEG_GUARD if wl.guard else 0) | flags
+    one = _setup(plk.Engine(0, wl.S, wl.C, n, et.n_tips, et.n_internal, len(wl.models), base), wl, states)
+    multi = _setup(plk.Engine(devs, wl.S, wl.C, n, et.n_tips, et.n_internal, len(wl.models), base), wl, states)
+    assert multi.shard_count() == min(len(devs), (n + 4095) // 4096)
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    mi = None if wl.model_of_node is None else wl.model_of_node[br].astype(np.int32)
+    ops = phylo.split_ops(et.ops)
+    w = np.random.default_rng(3).integers(1, 5, size=n).astype(np.float64)
+    one.set_pattern_weights(w)
+    multi.set_pattern_weights(w)
+    for scale in (1.0, 0.8):
+        t = et.brlen[br] * scale
+        l1, b1 = one.evaluate(br, t, ops, et.root, mi)
+        lm, bm = multi.evaluate(br, t, ops, et.root, mi)
+        assert l1 == lm and np.array_equal(b1, bm)
+    r1 = one.root_loglik(et.root, want_sites=True, want_blocks=True)
+    rm = multi.root_loglik(et.root, want_sites=True, want_blocks=True)
+    assert r1[0] == rm[0] and np.array_equal(r1[1], rm[1]) and np.array_equal(r1[2], rm[2])
+    node = et.ops[len(et.ops) // 2][0]
+    assert np.array_equal(one.get_partials(node), multi.get_partials(node))
+    assert multi.kernel_path() == one.kernel_path()
+    w1, wm = one.traversal_work(), multi.traversal_work()
+    assert wm["patterns"] == n and wm["node_updates"] == w1["node_updates"]
+
+
+def test_multi_device_branch_derivatives():
+    wl = workload.make_workload("gtr_g4_dna_1M_64", n_patterns=2 * 4096 + 11)
+    et, n = wl.et, wl.n_patterns
+    states = wl.simulate(0, n)
+    one = _setup(plk.Engine(0, 4, 4, n, et.n_tips, et.n_internal, 1), wl, states)
+    multi = _setup(plk.Engine([0, 0], 4, 4, n, et.n_tips, et.n_internal, 1), wl, states)
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    for e in (one, multi):
+        e.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+        e.update_partials(phylo.split_ops(et.ops))
+        e.root_loglik(et.root)
+    for b in (0, et.n_tips, br[-1]):
+        a1, a2 = one.branch_derivatives(int(b))
+        m1, m2 = multi.branch_derivatives(int(b))
+        assert abs(a1 - m1) <= 1e-12 * abs(a1) and abs(a2 - m2) <= 1e-12 * abs(a2)
+
+
+@pytest.mark.parametrize("config,flags", [("gtr_g4_dna_1M_64", plk.PLK_FLAG_LNL_ONLY),
+                                          ("lg08_g4_protein_200k_256", plk.PLK_FLAG_LNL_ONLY),
+                                          ("gtr_g4_dna_1M_64", plk.PLK_FLAG_LEVELWISE)])
+def test_comm_single_rank_bitwise(config, flags):
+    """plk_comm_init with one rank: the RCCL all-gather and the device-side fixed-order sum
+    return the handle's own host-side sum bitwise, evaluation after evaluation."""
+    n = 3 * 4096 + 21
+    wl = workload.make_workload(config, n_patterns=n)
+    et = wl.et
+    states = wl.simulate(0, n)
+    base = (plk.PLK_FLAG_SCALING if wl.scaling else 0) | plk.PLK_FLAG_NONNEG_GUARD | flags
+    ref = _setup(plk.Engine(0, wl.S, wl.C, n, et.n_tips, et.n_internal, 1, base), wl, states)
+    eng = _setup(plk.Engine(0, wl.S, wl.C, n, et.n_tips, et.n_internal, 1, base), wl, states)
+    eng.comm_init(1, 0, plk.comm_get_id())
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    ops = phylo.split_ops(et.ops)
+    for scale in (1.0, 1.2, 0.9):
+        t = et.brlen[br] * scale
+        l0, b0 = ref.evaluate(br, t, ops, et.root)
+        l1, b1 = eng.evaluate(br, t, ops, et.root)
+        assert l0 == l1 and np.array_equal(b0, b1)
+    s0 = ref.root_loglik(et.root, want_sites=True)
+    s1 = eng.root_loglik(et.root, want_sites=True)
+    assert s0[0] == s1[0] and np.array_equal(s0[1], s1[1])
+
+
+def test_cpp_drop_in_sharded_goldens():
+    """The Bio++ mirror's drop-in program with the patterns sharded over two handles on the
+    GPU (BPP_AMD_DEVICES=0,0): the reference goldens, optimisers included."""
+    host = os.path.join(ROOT, "bpp-phyl_amd", "host")
+    subprocess.run(["make", "-s", "-j8", "-C", host], check=True)
+    env = dict(os.environ, BPP_AMD_DEVICES="0,0")
+    r = subprocess.run([os.path.join(host, "bin", "test_likelihood_gpu")], capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASSED" in r.stdout

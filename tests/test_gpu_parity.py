@@ -736,6 +736,7 @@ def test_treeM_cherry_tables_bitwise(S, C, scaling, variant, monkeypatch):
         rng = np.random.default_rng(7)
         states[rng.random(states.shape) < 0.3] = code
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | (plk.PLK_FLAG_SCALING if scaling else 0)
+    monkeypatch.setenv("PLK_JITM", "0")   # the treeM interpreter (20 states default to jit_treeM)
     res = {}
     for on in ("0", "1"):
         monkeypatch.setenv("PLK_TREEM_CHERRY", on)
@@ -780,6 +781,7 @@ def test_treeM_direct_tables_bitwise(S, C, scaling, mode, monkeypatch):
     et, m, alph, rates, probs, states = _random_problem(S, C, 40 if S == 20 else 20, 600, seed=S + 3 * C,
                                                         amb=S == 20)
     flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    monkeypatch.setenv("PLK_JITM", "0")
     res = {}
     for on in ("0", "1"):
         monkeypatch.setenv("PLK_TREEM_DIRECT", on)
@@ -801,6 +803,7 @@ def test_treeM_32_pattern_workgroups_bitwise(C, scaling, mode, n_pat, monkeypatc
     site_lnl by site_wave_sums_kernel) equal the 64-pattern kernel bitwise."""
     et, m, alph, rates, probs, states = _random_problem(20, C, 40, n_pat, seed=7 * C + n_pat)
     flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    monkeypatch.setenv("PLK_JITM", "0")
     res = {}
     for g in ("4", "2", "1"):
         monkeypatch.setenv("PLK_TREEM_G", g)
@@ -814,3 +817,76 @@ def test_treeM_32_pattern_workgroups_bitwise(C, scaling, mode, n_pat, monkeypatc
     for g in ("2", "1"):
         b = res[g]
         assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+
+
+# ---------------------------------------------------------------- jit_treeM (20 states, v_mfma_f64_4x4x4_4b)
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode,variant", [
+    (4, "balanced64", 700, False, "lnl_only", ""), (4, "balanced64", 700, True, "materialize", "amb"),
+    (1, "balanced64", 333, True, "lnl_only", ""), (2, "caterpillar30", 400, True, "lnl_only", "amb"),
+    (3, "balanced100", 257, True, "materialize", ""), (4, "caterpillar30", 300, False, "materialize", ""),
+    (4, "balanced300", 513, True, "lnl_only", "amb"), (4, "balanced64", 900, True, "lnl_only", "tiny"),
+    (2, "caterpillar30", 500, True, "materialize", "tiny"), (4, "balanced64", 64, False, "lnl_only", "")])
+def test_jit_treeM_vs_oracle(C, tree_kind, n_patterns, scaling, mode, variant, monkeypatch):
+    """The tree-specialised 20-state kernel (plk_jitm.hpp) against the oracle on identical
+    P(t) (per pattern 1e-12), against the treeM interpreter (PLK_JITM=0, 1e-12), and
+    self-consistent: a second evaluation and the materialised partials bitwise.  "tiny": a
+    code whose vector is 1e-80 forces the joint rescale (cherry tables and in-kernel)."""
+    if tree_kind.startswith("balanced"):
+        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=31, lo=0.05, hi=0.4)
+    else:
+        tree = _caterpillar(int(tree_kind[11:]), seed=9)
+    et = phylo.engine_tree(tree)
+    m = phylo.lg08()
+    rates, probs = phylo.gamma_rates(C, 0.6) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.PROTEIN, n_patterns, scaling, True, 8)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    rng = np.random.default_rng(C + n_patterns)
+    init = phylo.PROTEIN.init_table
+    if variant == "amb":
+        mask = rng.random(states.shape) < 0.05
+        states[mask] = rng.integers(20, phylo.PROTEIN.n_codes, size=mask.sum())
+    elif variant == "tiny":
+        init = np.array(init, dtype=np.float64, copy=True)
+        code = phylo.PROTEIN.n_codes - 1
+        init[code] = 1e-80
+        states[rng.random(states.shape) < 0.3] = code
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, 20, C, n_patterns, states, init, rates, probs, m.pi, [m], flags=flags)
+    lnl, site, blocks = run_engine(eng, et)
+    assert eng.kernel_path() == "jit_treeM"
+    lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=scaling, pmats=engine_pmats(eng, et))
+    check(lnl, site, lo, so)
+    if variant == "tiny":
+        assert site.min() < -256 * np.log(2)
+    lnl2, site2, blocks2 = run_engine(eng, et)
+    assert lnl2 == lnl and np.array_equal(site2, site) and np.array_equal(blocks2, blocks)
+    parts = np.stack([eng.get_partials(p) for p, _ in et.ops[-4:]])
+    assert np.all(np.isfinite(parts))
+    # the treeM interpreter on the same inputs
+    monkeypatch.setenv("PLK_JITM", "0")
+    ref = engine_for(et, 20, C, n_patterns, states, init, rates, probs, m.pi, [m], flags=flags)
+    lr, sr, _ = run_engine(ref, et)
+    assert ref.kernel_path() == "treeM"
+    check(lnl, site, lr, sr)
+    pr = np.stack([ref.get_partials(p) for p, _ in et.ops[-4:]])
+    assert np.allclose(parts, pr, rtol=1e-11, atol=1e-300)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dm,L", [(2, 1), (4, 2)])
+def test_jit_treeM_register_depths(dm, L, monkeypatch):
+    """Other fragment heights and fetch lookaheads give the default kernel's results to
+    rounding (different cuts store different partials; the arithmetic per node is the same)."""
+    et, m, alph, rates, probs, states = _random_problem(20, 4, 80, 600, seed=77, amb=True)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
+    eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+    l0, s0, _ = run_engine(eng, et)
+    del eng
+    monkeypatch.setenv("PLK_JITM_DM", str(dm))
+    monkeypatch.setenv("PLK_JITM_L", str(L))
+    eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+    l1, s1, _ = run_engine(eng, et)
+    assert eng.kernel_path() == "jit_treeM"
+    assert np.array_equal(s0, s1) and l0 == l1
