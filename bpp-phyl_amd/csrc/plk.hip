@@ -171,6 +171,7 @@ struct plk_handle_s {
   // per-subtree pattern compression (PLK_FLAG_SUBTREE_PATTERNS)
   std::vector<std::vector<uint8_t> > tip_codes_host;  // compact codes per tip
   bool cmp_valid = false;
+  bool slots_expanded = false;                        // a derivative re-ran the traversal uncompressed
   std::vector<plk_op> cmp_ops;                        // op list the links were built for
   std::vector<std::vector<int32_t> > cmp_ids;         // per internal slot: distinct id per pattern (empty: identity)
   std::vector<int64_t> cmp_D;                         // per internal slot: distinct patterns
@@ -649,8 +650,6 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   if (n_classes < 1 || n_classes > 16) return fail(nullptr, PLK_ERR_UNSUPPORTED, "n_classes %d not in [1, 16]", n_classes);
   if ((flags & PLK_FLAG_SUBTREE_PATTERNS) && (flags & PLK_FLAG_DOUBLE_RECURSIVE))
     return fail(nullptr, PLK_ERR_UNSUPPORTED, "double-recursive derivatives read full-length partials (no pattern compression)");
-  if ((flags & PLK_FLAG_SUBTREE_PATTERNS) && !(n_states == 4 && s4_supported(n_classes)))
-    return fail(nullptr, PLK_ERR_UNSUPPORTED, "per-subtree pattern compression needs 4 states and C in {1, 2, 4, 8}");
   if (n_patterns < 1 || n_tips < 0 || n_internal < 1 || n_models < 1)
     return fail(nullptr, PLK_ERR_ARG, "bad sizes (patterns %lld tips %d internal %d models %d)",
                 (long long)n_patterns, n_tips, n_internal, n_models);
@@ -1927,6 +1926,7 @@ int update_levelwise(plk_handle h, const plk_op* ops, int n_ops) {
   for (int i = 0; i < n_ops; ++i) h->materialized[ops[i].parent - h->n_tips] = 1;
   h->fused_lnl_valid = false;
   h->blocks_fused = false;
+  h->slots_expanded = false;
   return PLK_OK;
 }
 
@@ -2151,6 +2151,29 @@ void launch_links(plk_handle h, const KOpL* d, int cnt, int maxD, const Partials
     partials_links_s4_kernel<C, false><<<grid, block, 0, h->stream>>>(d, a, h->d_links);
 }
 
+template <int S, int XB>
+void launch_links_generic_S(plk_handle h, const KOpL* d, int cnt, int maxD, const PartialsArgs& a, size_t lds) {
+  const dim3 grid((unsigned)((maxD + 255) / 256), (unsigned)cnt), block(256);
+  if (h->flags & PLK_FLAG_SCALING)
+    partials_links_generic_kernel<S, XB, true><<<grid, block, lds, h->stream>>>(d, a, h->d_links, h->C);
+  else
+    partials_links_generic_kernel<S, XB, false><<<grid, block, lds, h->stream>>>(d, a, h->d_links, h->C);
+}
+
+int launch_links_generic(plk_handle h, const KOpL* d, int cnt, int maxD, const PartialsArgs& a) {
+  const size_t lds = 3 * (size_t)h->C * h->S * std::max(h->S, h->n_codes) * sizeof(double);
+  if (lds > 160 * 1024) return fail(h, PLK_ERR_UNSUPPORTED, "LDS image of %zu bytes exceeds 160 KiB", lds);
+  switch (h->S) {
+    case 2: launch_links_generic_S<2, 2>(h, d, cnt, maxD, a, lds); break;
+    case 3: launch_links_generic_S<3, 3>(h, d, cnt, maxD, a, lds); break;
+    case 4: launch_links_generic_S<4, 4>(h, d, cnt, maxD, a, lds); break;
+    case 20: launch_links_generic_S<20, 20>(h, d, cnt, maxD, a, lds); break;
+    case 64: launch_links_generic_S<64, 16>(h, d, cnt, maxD, a, lds); break;
+    default: return fail(h, PLK_ERR_UNSUPPORTED, "state count %d has no kernel instance", h->S);
+  }
+  return PLK_OK;
+}
+
 int update_compressed(plk_handle h, const plk_op* ops, int n_ops) {
   h->kernel_path = "subtree_patterns";
   const bool same = h->cmp_valid && h->cmp_ops.size() == (size_t)n_ops &&
@@ -2182,11 +2205,16 @@ int update_compressed(plk_handle h, const plk_op* ops, int n_ops) {
       hipEventRecord(ev.a, h->stream);
     }
     const int maxD = h->cmp_level_maxD[l];
-    switch (h->C) {
-      case 1: launch_links<1>(h, d, cnt, maxD, a); break;
-      case 2: launch_links<2>(h, d, cnt, maxD, a); break;
-      case 4: launch_links<4>(h, d, cnt, maxD, a); break;
-      case 8: launch_links<8>(h, d, cnt, maxD, a); break;
+    if (h->S == 4 && s4_supported(h->C)) {
+      switch (h->C) {
+        case 1: launch_links<1>(h, d, cnt, maxD, a); break;
+        case 2: launch_links<2>(h, d, cnt, maxD, a); break;
+        case 4: launch_links<4>(h, d, cnt, maxD, a); break;
+        case 8: launch_links<8>(h, d, cnt, maxD, a); break;
+      }
+    } else {
+      int rc2 = launch_links_generic(h, d, cnt, maxD, a);
+      if (rc2) return rc2;
     }
     HIPCHK(h, hipGetLastError());
     if (h->timing & PLK_TIME_PARTIALS) {
@@ -2198,6 +2226,7 @@ int update_compressed(plk_handle h, const plk_op* ops, int n_ops) {
   for (int i = 0; i < n_ops; ++i) h->materialized[ops[i].parent - h->n_tips] = 1;
   h->fused_lnl_valid = false;
   h->blocks_fused = false;
+  h->slots_expanded = false;
   return PLK_OK;
 }
 
@@ -2378,8 +2407,6 @@ int path_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   if (h->deriv_valid.empty() || !h->deriv_valid[branch])
     return fail(h, PLK_ERR_STATE, "dP/d2P of branch %d not computed (PLK_DERIV_DP | PLK_DERIV_D2P)", branch);
   if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
-  if (h->flags & PLK_FLAG_SUBTREE_PATTERNS)
-    return fail(h, PLK_ERR_UNSUPPORTED, "path derivatives read full-length partials (no pattern compression)");
   hipSetDevice(h->device);
   const int nt = h->n_tips;
   std::vector<std::vector<int> > kids(h->n_nodes);
@@ -2552,6 +2579,7 @@ int materialize_last_traversal(plk_handle h) {
                      ? update_tree4(h, ops.data(), (int)ops.size())
                      : update_levelwise(h, ops.data(), (int)ops.size());
   h->flags = saved;
+  if (!rc && (h->flags & PLK_FLAG_SUBTREE_PATTERNS)) h->slots_expanded = true;
   return rc;
 }
 
@@ -2835,7 +2863,8 @@ int plk_get_partials(plk_handle h, int node, double* out) {
   const int CS = h->C * h->S;
   // compressed node: its slot holds one entry per distinct subtree pattern
   const std::vector<int32_t>* ids = nullptr;
-  if ((h->flags & PLK_FLAG_SUBTREE_PATTERNS) && h->cmp_valid && !h->cmp_ids[node - h->n_tips].empty())
+  if ((h->flags & PLK_FLAG_SUBTREE_PATTERNS) && h->cmp_valid && !h->slots_expanded &&
+      !h->cmp_ids[node - h->n_tips].empty())
     ids = &h->cmp_ids[node - h->n_tips];
   for (int64_t p = 0; p < h->n_patterns; ++p) {
     const int64_t j = ids ? (*ids)[(size_t)p] : p;
@@ -3039,8 +3068,10 @@ int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
       parent[c] = n;
     }
   if (parent[branch] < 0) return fail(h, PLK_ERR_ARG, "branch %d is not below any node of the last traversal", branch);
-  // every partial read along the path must be in HBM: re-materialise if needed
-  bool need = false;
+  // every partial read along the path must be in HBM at full length: re-materialise if
+  // needed (a compressed traversal's slots hold distinct subtree patterns: the derivative
+  // re-runs the traversal uncompressed once, until the next compressed traversal)
+  bool need = (h->flags & PLK_FLAG_SUBTREE_PATTERNS) && !h->slots_expanded;
   for (int n = parent[branch]; n >= 0; n = parent[n])
     for (int c : kids[n])
       if (c >= nt && !h->materialized[c - nt]) need = true;

@@ -269,6 +269,84 @@ __global__ __launch_bounds__(256) void partials_links_s4_kernel(const KOpL* __re
     for (int x = 0; x < S; ++x) out[(c * S + x) * kTile] = acc[c][x];
 }
 
+// Any state count: partials_generic_kernel's arithmetic (P and tip tables staged in LDS,
+// XB states per chunk, the same product and FMA order) with the children read through
+// their pattern links -- so values are bitwise those of the uncompressed generic kernel
+// (PLK_FLAG_LEVELWISE with PLK_GENERIC20 / PLK_GENERIC64).  One lane = one distinct
+// pattern j of the parent (its slot entry j).
+template <int S, int XB, bool SCALE>
+__global__ __launch_bounds__(256) void partials_links_generic_kernel(const KOpL* __restrict__ ops, PartialsArgs a,
+                                                                     const uint32_t* __restrict__ links, int C) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const KOpL& op = ops[blockIdx.y];
+  const int n = op.n;
+  const int nc = a.n_codes;
+  const int CS = C * S;
+  if ((int)(blockIdx.x * blockDim.x) >= op.D) return;  // whole workgroup past this op's patterns
+  const int per = C * S * ((S > nc) ? S : nc);
+  for (int k = 0; k < n; ++k) {
+    const double* src = op.is_tip[k] ? a.tipP + (size_t)op.child[k] * (C * nc * S)
+                                     : a.pmats + (size_t)op.branch[k] * (C * S * S);
+    const int cnt = op.is_tip[k] ? C * nc * S : C * S * S;
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) lds[k * per + i] = src[i];
+  }
+  __syncthreads();
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= op.D) return;
+  double* outp = a.partials + (size_t)op.parent * a.slot_stride + (size_t)(j >> 7) * ((size_t)CS * kTile) + (j & 127);
+  uint32_t l[3] = {0u, 0u, 0u};
+  for (int k = 0; k < n; ++k) l[k] = links[op.link[k] + j];
+  int cnt = 0;
+  if (SCALE)
+    for (int k = 0; k < n; ++k)
+      if (!op.is_tip[k]) cnt += a.scale[(size_t)op.child[k] * a.n_pad + l[k]];
+  double m = 0.0;
+  for (int c = 0; c < C; ++c) {
+    for (int x0 = 0; x0 < S; x0 += XB) {
+      double acc[XB];
+#pragma unroll
+      for (int xb = 0; xb < XB; ++xb) acc[xb] = 1.0;
+      for (int k = 0; k < n; ++k) {
+        if (op.is_tip[k]) {
+          const double* t = &lds[k * per + (c * nc + (int)l[k]) * S + x0];
+#pragma unroll
+          for (int xb = 0; xb < XB; ++xb) acc[xb] *= t[xb];
+        } else {
+          const double* L = a.partials + (size_t)op.child[k] * a.slot_stride +
+                            (size_t)(l[k] >> 7) * ((size_t)CS * kTile) + (l[k] & 127) + (size_t)c * S * kTile;
+          const double* Pc = &lds[k * per + (c * S + x0) * S];
+          double s[XB];
+          {
+            const double l0 = L[0];
+#pragma unroll
+            for (int xb = 0; xb < XB; ++xb) s[xb] = Pc[xb * S] * l0;
+          }
+#pragma unroll 4
+          for (int y = 1; y < S; ++y) {
+            const double ly = L[(size_t)y * kTile];
+#pragma unroll
+            for (int xb = 0; xb < XB; ++xb) s[xb] = __builtin_fma(Pc[xb * S + y], ly, s[xb]);
+          }
+#pragma unroll
+          for (int xb = 0; xb < XB; ++xb) acc[xb] *= s[xb];
+        }
+      }
+#pragma unroll
+      for (int xb = 0; xb < XB; ++xb) {
+        if (SCALE) m = fmax(m, acc[xb]);
+        outp[(size_t)(c * S + x0 + xb) * kTile] = acc[xb];
+      }
+    }
+  }
+  if (SCALE) {
+    if (m > 0.0 && m < kScaleThr) {
+      for (int i = 0; i < CS; ++i) outp[(size_t)i * kTile] *= kScaleUp;
+      cnt += 1;
+    }
+    a.scale[(size_t)op.parent * a.n_pad + j] = cnt;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Generic-S kernel (S up to 64): one lane = one pattern, 2 tiles per 256-thread
 // workgroup.  The children's P(t) (C x S x S each) and tip tables are staged in

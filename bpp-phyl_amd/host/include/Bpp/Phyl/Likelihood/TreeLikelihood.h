@@ -76,6 +76,8 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   bool initialized_ = false;
   bool scaling_ = true;
   bool incremental_ = true;
+  bool compressed_ = false;  // usePatterns: PLK_FLAG_SUBTREE_PATTERNS on the engine
+  size_t maxSons_ = 0;
   bool derivFirst_ = true, derivSecond_ = true;
   unsigned extraFlags_ = 0;                  // plk_create flags of the subclass (PLK_FLAG_DOUBLE_RECURSIVE)
   // double-recursive derivative cache: every branch from one plk_all_branch_derivatives call,

@@ -79,8 +79,10 @@ void AbstractPlkTreeLikelihood::buildEngineLayout() {
   opParent_.clear();
   opChildren_.clear();
   opFlags_.clear();
+  maxSons_ = 0;
   for (Node* n : all) {
     if (n->isLeaf()) continue;
+    maxSons_ = std::max(maxSons_, n->getNumberOfSons());
     for (size_t k = 0; k < n->getNumberOfSons(); k += 3) {
       std::vector<int> ch;
       for (size_t j = k; j < std::min(k + 3, n->getNumberOfSons()); j++) ch.push_back(engineIndex_[n->getSon(j)]);
@@ -152,6 +154,14 @@ void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
   }
   unsigned flags = (scaling_ ? (unsigned)PLK_FLAG_SCALING : 0u) | (nonNegGuard ? (unsigned)PLK_FLAG_NONNEG_GUARD : 0u) |
                    extraFlags_;
+  // usePatterns (the reference default): per-subtree site-pattern compression on the device
+  // (DRASRTreeLikelihoodData.cpp:218-332, PLK_FLAG_SUBTREE_PATTERNS); not for the double-
+  // recursive classes (their data class has no compression either, DRASDRTreeLikelihoodData)
+  // nor for nodes of more than 3 sons, and BPP_AMD_USE_PATTERNS=0 switches it off
+  compressed_ = usePatterns_ && !(extraFlags_ & PLK_FLAG_DOUBLE_RECURSIVE) && maxSons_ <= 3;
+  if (const char* e = std::getenv("BPP_AMD_USE_PATTERNS"))
+    if (e[0] == '0') compressed_ = false;
+  if (compressed_) flags |= PLK_FLAG_SUBTREE_PATTERNS;
   plk_handle h = nullptr;
   const std::vector<int> devs = devicesFromEnv();
   int rc = devs.empty() ? plk_create(deviceFromEnv(), (int)nbStates_, (int)nbClasses_, (int64_t)nbDistinctSites_, nTips_,
@@ -231,7 +241,8 @@ void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& 
 // the result is bit-identical to a full traversal.
 void AbstractPlkTreeLikelihood::computeTreeLikelihood(const std::vector<const Node*>* changed) {
   std::vector<char> need;
-  if (changed && incremental_) {
+  // a compressed traversal rebuilds every node from its subtree's patterns: always full
+  if (changed && incremental_ && !compressed_) {
     need.assign((size_t)(nTips_ + nInternal_), 0);
     for (const Node* n : *changed)
       for (const Node* p = n->getFather(); p; p = p->getFather()) {

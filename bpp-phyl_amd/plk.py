@@ -149,7 +149,7 @@ def comm_get_id() -> bytes:
     rc = lib.plk_comm_get_id(ct.byref(cid))
     if rc != PLK_OK:
         raise PlkError(rc, lib.plk_last_error(None).decode())
-    return bytes(cid.internal)
+    return ct.string_at(ct.addressof(cid), 128)   # all 128 bytes (a c_char field stops at NUL)
 
 
 def build_id() -> str:
@@ -365,8 +365,10 @@ class Engine:
     def comm_init(self, n_ranks: int, rank: int, comm_id: bytes):
         """plk_comm_init: RCCL communicator inside the handle; evaluations then return the
         global lnL of all ranks (one all-gather of block sums per evaluation)."""
+        if len(comm_id) != 128:
+            raise ValueError("a plk_comm_id is 128 bytes")
         cid = plk_comm_id()
-        ct.memmove(cid.internal, comm_id, 128)
+        ct.memmove(ct.addressof(cid), bytes(comm_id), 128)   # (a c_char field reads back as a copy)
         self._chk(self.lib.plk_comm_init(self.h, n_ranks, rank, ct.byref(cid)))
 
     def kernel_path(self) -> str:

@@ -708,14 +708,67 @@ def test_subtree_patterns_follow_new_tip_codes():
 
 def test_subtree_patterns_errors():
     et, m, alph, rates, probs, states = _random_problem(4, 2, 12, 300, seed=43)
-    with pytest.raises(plk.PlkError):   # 20 states: not supported with compression
-        plk.Engine(0, 20, 2, 300, et.n_tips, et.n_internal, 1, plk.PLK_FLAG_SUBTREE_PATTERNS)
+    with pytest.raises(plk.PlkError):   # no compressed double-recursive passes
+        plk.Engine(0, 4, 2, 300, et.n_tips, et.n_internal, 1,
+                   plk.PLK_FLAG_SUBTREE_PATTERNS | plk.PLK_FLAG_DOUBLE_RECURSIVE)
     eng = engine_for(et, 4, 2, 300, states, alph.init_table, rates, probs, m.pi, [m],
                      flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_SUBTREE_PATTERNS)
     run_engine(eng, et)
     ops = phylo.split_ops(et.ops)
     with pytest.raises(plk.PlkError):   # a child produced by an earlier call: links need the whole subtree
         eng.update_partials(ops[-1:])
+
+
+@pytest.mark.parametrize("S,C,n_taxa,n_patterns,scaling,amb", [
+    (20, 4, 24, 900, False, True), (20, 2, 40, 700, True, False), (20, 1, 9, 300, False, False),
+    (64, 1, 16, 600, False, True), (64, 1, 30, 400, True, False), (64, 1, 8, 300, False, False)])
+def test_subtree_patterns_any_state_count(S, C, n_taxa, n_patterns, scaling, amb, monkeypatch):
+    """Row f3 beyond DNA: per-subtree compression for 20 and 64 states
+    (partials_links_generic_kernel) against the oracle's own usePatterns = true pruning
+    at 1e-12 and, bitwise, against the uncompressed generic levelwise kernel it restates
+    (lnL, per-pattern lnL, block sums and every partial expanded through the links)."""
+    et, m, alph, rates, probs, states = _random_problem(S, C, n_taxa, n_patterns, seed=90 + S + C, amb=amb)
+    sc = plk.PLK_FLAG_SCALING if scaling else 0
+    monkeypatch.setenv("PLK_GENERIC20", "1")
+    monkeypatch.setenv("PLK_GENERIC64", "1")
+    ref = engine_for(et, S, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | sc | plk.PLK_FLAG_LEVELWISE)
+    l0, s0, b0 = run_engine(ref, et)
+    p0 = np.stack([ref.get_partials(p) for p, _ in et.ops])
+    del ref
+    eng = engine_for(et, S, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | sc | plk.PLK_FLAG_SUBTREE_PATTERNS)
+    l1, s1, b1 = run_engine(eng, et)
+    assert eng.kernel_path() == "subtree_patterns"
+    p1 = np.stack([eng.get_partials(p) for p, _ in et.ops])
+    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1) and np.array_equal(p0, p1)
+    assert eng.compressed_work() < n_patterns * et.n_internal
+    ss, sons, lr = et.son_arrays()
+    lo, so, _, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, alph.init_table, engine_pmats(eng, et), probs,
+                                      m.pi, use_patterns=True, scaling=scaling, want_sites=True)
+    check(l1, s1, lo, so)
+
+
+@pytest.mark.parametrize("S,C", [(4, 4), (20, 2), (64, 1)])
+def test_subtree_patterns_derivatives(S, C):
+    """Branch derivatives on a compressed handle: the traversal is re-run uncompressed once
+    (slots expanded) and the path derivatives equal those of an uncompressed handle; the
+    next compressed evaluation is unchanged."""
+    et, m, alph, rates, probs, states = _random_problem(S, C, 12, 500, seed=7 + S)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    res = []
+    for fl in (0, plk.PLK_FLAG_SUBTREE_PATTERNS):
+        eng = engine_for(et, S, C, 500, states, alph.init_table, rates, probs, m.pi, [m],
+                         flags=plk.PLK_FLAG_NONNEG_GUARD | fl)
+        eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+        l, _, _ = run_engine(eng, et)
+        d = [eng.branch_derivatives(int(b)) for b in (0, et.n_tips, br[-1])]
+        l2, _, _ = run_engine(eng, et)
+        res.append((l, d, l2))
+    (la, da, la2), (lb, db, lb2) = res
+    assert abs(la - lb) <= 1e-12 * abs(la) and lb == lb2
+    for (a1, a2), (b1, b2) in zip(da, db):
+        assert abs(a1 - b1) <= 1e-10 * max(1.0, abs(a1)) and abs(a2 - b2) <= 1e-9 * max(1.0, abs(a2))
 
 
 @pytest.mark.gpu
