@@ -386,6 +386,8 @@ int ensure_pmatsT(plk_handle h) {
       transpose_pmats<64><<<grid, 256, 0, h->stream>>>(h->pmats, h->pmatsT, h->C);
     else if (h->S == 20)
       transpose_pmats<20><<<grid, 256, 0, h->stream>>>(h->pmats, h->pmatsT, h->C);
+    else if (h->S == 4)
+      transpose_pmats<4><<<grid, 256, 0, h->stream>>>(h->pmats, h->pmatsT, h->C);
     else
       return fail(h, PLK_ERR_UNSUPPORTED, "no transposed-P path for %d states", h->S);
     HIPCHK(h, hipGetLastError());
@@ -1068,6 +1070,19 @@ int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
   return PLK_OK;
 }
 
+int plk_get_dpmatrix(plk_handle h, int branch, int order, double* dP) {
+  if (h && !h->shards.empty()) return multi_forward(h, plk_get_dpmatrix(h->shards[0], branch, order, dP));
+  if (!h || !dP || branch < 0 || branch >= h->n_nodes || (order != 1 && order != 2))
+    return fail(h, PLK_ERR_ARG, "bad derivative request (branch %d, order %d)", branch, order);
+  const double* src = order == 1 ? h->dpmats : h->d2pmats;
+  if (!src) return fail(h, PLK_ERR_STATE, "no derivative matrices (PLK_DERIV_DP / PLK_DERIV_D2P)");
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const size_t n = (size_t)h->C * h->S * h->S;
+  HIPCHK(h, hipMemcpy(dP, src + (size_t)branch * n, n * sizeof(double), hipMemcpyDeviceToHost));
+  return PLK_OK;
+}
+
 int plk_get_pmatrix(plk_handle h, int branch, double* P) {
   if (h && !h->shards.empty()) return multi_forward(h, plk_get_pmatrix(h->shards[0], branch, P));
   if (!h || !P || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
@@ -1104,6 +1119,9 @@ enum FusedKind { FK_NONE = 0, FK_TREE4, FK_TREES, FK_TREEM };
 
 FusedKind fused_kind(plk_handle h) {
   if (h->flags & PLK_FLAG_LEVELWISE) return FK_NONE;
+  // 4 states: the VALU tree kernel (plk_jit.hpp); PLK_S4_JITM=1 runs them on the matrix
+  // cores instead (jit_treeM with one 4x4x4 block per class and 16 patterns)
+  if (h->S == 4 && env_is("PLK_S4_JITM", '1') && !env_is("PLK_JITM", '0') && h->C <= kTreeMaxWaves) return FK_TREEM;
   if (h->S == 4) return (h->C == 1 || h->C == 2 || h->C == 4) ? FK_TREE4 : FK_NONE;
   if (h->C > kTreeMaxWaves) return FK_NONE;
   if (h->S == 20 && !env_is("PLK_FUSED20", '0')) return env_is("PLK_TREES", '1') ? FK_TREES : FK_TREEM;
@@ -1126,7 +1144,10 @@ bool jit_tree4(plk_handle h) { return fused_kind(h) == FK_TREE4 && tree4_cw(h) =
 
 // 20 states: the tree-specialised kernel on v_mfma_f64_4x4x4_4b (plk_jitm.hpp) serves the
 // fused traversal; PLK_JITM=0 keeps the treeM interpreter (16x16x4 MFMA), e.g. for A/B runs.
-bool jit_treeM(plk_handle h) { return fused_kind(h) == FK_TREEM && h->S == 20 && !env_is("PLK_JITM", '0'); }
+bool jit_treeM(plk_handle h) {
+  if (fused_kind(h) != FK_TREEM || env_is("PLK_JITM", '0')) return false;
+  return h->S == 20 || h->S == 4 || (h->S == 64 && env_is("PLK_JITM64", '1'));
+}
 
 // Classes in one wave (plk_jit.hpp, CW = C): the joint rescale needs no cross-wave
 // exchange (the per-node barrier of the one-class-per-wave layout costs ~2x on cfg5),
@@ -1187,6 +1208,9 @@ int build_cherry_tables(plk_handle h) {
   if (S == 20) {
     if (sc) cherry_table_kernel<20, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
     else cherry_table_kernel<20, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
+  } else if (S == 4) {
+    if (sc) cherry_table_kernel<4, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
+    else cherry_table_kernel<4, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
   } else if (S == 64) {
     if (sc) cherry_table_kernel<64, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
     else cherry_table_kernel<64, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
@@ -1207,7 +1231,8 @@ int tree_levels(plk_handle h) {
     // S = 20: 3 levels (with cherry tables 7.8 ms on cfg3, 2 levels 8.7 ms although DM = 3
     // spills a few registers at 128 VGPRs)
     case FK_TREEM:
-      if (jit_treeM(h)) return env_int("PLK_JITM_DM", 3, 2, 6);
+      if (jit_treeM(h))
+        return h->S == 4 ? env_int("PLK_JITM_DM", 8, 2, 16) : env_int("PLK_JITM_DM", h->S == 64 ? 3 : 4, 2, 6);
       return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 3, 2, 3);
     default: return 1;
   }
@@ -1730,6 +1755,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     msh.L = env_int("PLK_JITM_L", 1, 1, 4);
     msh.minw = env_int("PLK_JITM_MINW", 2, 1, 8);
+    msh.direct = env_is("PLK_JITM_DIRECT", '1');
     if (msh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "jit_treeM needs %zu B of LDS", msh.lds_bytes());
     if (!h->jitm_fn || !(msh == h->jitm_shape)) {
@@ -2421,7 +2447,8 @@ int path_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   if (parent[branch] < 0) return fail(h, PLK_ERR_ARG, "branch %d is not below any node of the last traversal", branch);
   int root = parent[branch];
   while (parent[root] >= 0) root = parent[root];
-  bool need = !h->materialized[root - nt];
+  // a compressed traversal's slots hold distinct subtree patterns: expand once
+  bool need = !h->materialized[root - nt] || ((h->flags & PLK_FLAG_SUBTREE_PATTERNS) && !h->slots_expanded);
   for (int n = parent[branch]; n >= 0; n = parent[n])
     for (int c : kids[n])
       if (c >= nt && !h->materialized[c - nt]) need = true;

@@ -97,11 +97,12 @@ struct JitMShape {
   bool scale = false;
   int L = 1;         // operand fetch lookahead (events)
   int minw = 2;      // __launch_bounds__ min waves per SIMD
+  bool direct = false;  // A operands straight from P(t) in L1/L2 (no LDS staging, no barriers)
   static constexpr int G = 4;  // waves (16-pattern groups) per workgroup: 64 patterns
   int pb() const { return C * S * S; }  // doubles per P buffer (every class of one branch)
-  size_t lds_bytes() const { return (size_t)(2 * pb() + 64) * sizeof(double); }
+  size_t lds_bytes() const { return (size_t)((direct ? 0 : 2 * pb()) + 64) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
-    return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw;
+    return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && direct == o.direct;
   }
 };
 
@@ -117,8 +118,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const int NTH = 64 * JitMShape::G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH;
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
-           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n",
-           S, C, XB, sh.U, sh.U * sh.U, JitMShape::G, NTH, PB, PF, sh.scale ? "true" : "false");
+           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n#define DIRECT_ %d\n",
+           S, C, XB, sh.U, sh.U * sh.U, JitMShape::G, NTH, PB, PF, sh.scale ? "true" : "false", sh.direct ? 1 : 0);
   s += buf;
   s += R"PLKJITM(
 // P(t) of branch b (all classes, [c][x][y]) -> registers -> the LDS tile image
@@ -132,6 +133,12 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
     double d_ = 0.0; \
     _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) d_ = mfma4(P_[((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
+    if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } }
+// direct: A(c, X, Y) = P[c][4X + lo][4Y + hi] read from the branch's P(t) in global memory
+#define CONTRIB_G(D, SRC, b, SET) { const double* P_ = PG + (i64)(b) * PB_; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
+    double d_ = 0.0; \
+    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) d_ = mfma4(P_[(c_ * S_ + 4 * X_) * S_ + 4 * Y_], SRC[c_][Y_], d_); \
     if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } }
 #define ROWMUL(D, F, SET) { _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") \
   for (int X_ = 0; X_ < XB_; ++X_) { if (SET) D[c_][X_] = F[c_][X_]; else D[c_][X_] *= F[c_][X_]; } }
@@ -187,7 +194,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
            std::max(sh.minw, 1));
   s += buf;
   s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PB_] P tiles | red[64]
-  double* red = lds + 2 * PB_;
+  double* red = lds + (DIRECT_ ? 0 : 2 * PB_);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 4, pl = lane & 15;
@@ -195,6 +202,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const i64 p = p0 + 16 * w + pl;
   const i64 toff = (p >> 7) * (i64)(C_ * S_ * kTile) + (p & (kTile - 1)) + (i64)hi * kTile;
   const double* PA = lds + ((hi << 2) | (lane & 3));
+  const double* PG = a.pmats + (lane & 3) * S_ + hi;   // direct A operands: P[..][4X + lo][4Y + hi]
   int sidx[PF_];   // this thread's staging elements -> tile slots (-1: past the table)
   _Pragma("unroll") for (int j = 0; j < PF_; ++j) {
     const int e = tid + j * NTH_;
@@ -202,7 +210,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3) : -1;
   }
   double R[PF_];
-  (void)red; (void)PA; (void)R; (void)toff;
+  (void)red; (void)PA; (void)PG; (void)R; (void)toff; (void)sidx;
   const int frag = frag_base + (int)blockIdx.y;
 )PLKJITM";
   // accumulators per register level and the operand ring
@@ -256,6 +264,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
     int cur = 0;
     size_t np = 0;  // P-chain events consumed
+    if (sh.direct) pchain.clear();  // no staging chain: every contraction reads P(t) directly
     if (!pchain.empty()) {
       const TInstr& e0 = ev[(size_t)pchain[0]];
       snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R, %d) PSTAGE_STORE(R, 0) __syncthreads();\n", e0.b);
@@ -270,7 +279,14 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
       if (e.op == T_CHERRY || e.op == T_TIP || e.op == T_LOAD) {
         if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
         const int sl = slot[i];
-        if (e.op == T_LOAD) {
+        if (e.op == T_LOAD && sh.direct) {
+          snprintf(buf, sizeof(buf), "    CONTRIB_G(A%d, F%d, %d, %s)\n", d, sl, e.b, fresh[(size_t)d] ? "true" : "false");
+          s += buf;
+          if (sh.scale) {
+            snprintf(buf, sizeof(buf), "    K%d += FK%d;\n", d, sl);
+            s += buf;
+          }
+        } else if (e.op == T_LOAD) {
           const bool more = np + 1 < pchain.size();
           if (more) {
             snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R, %d)\n", ev[(size_t)pchain[np + 1]].b);
@@ -318,7 +334,10 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
           snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R, %d)\n", ev[(size_t)pchain[np + 1]].b);
           s += buf;
         }
-        snprintf(buf, sizeof(buf), "    CONTRIB(A%d, A%d, %d, %s)\n", d - 1, d, cur, fresh[(size_t)d - 1] ? "true" : "false");
+        if (sh.direct)
+          snprintf(buf, sizeof(buf), "    CONTRIB_G(A%d, A%d, %d, %s)\n", d - 1, d, e.b, fresh[(size_t)d - 1] ? "true" : "false");
+        else
+          snprintf(buf, sizeof(buf), "    CONTRIB(A%d, A%d, %d, %s)\n", d - 1, d, cur, fresh[(size_t)d - 1] ? "true" : "false");
         s += buf;
         if (more) {
           snprintf(buf, sizeof(buf), "    PSTAGE_STORE(R, %d) __syncthreads();\n", cur ^ 1);

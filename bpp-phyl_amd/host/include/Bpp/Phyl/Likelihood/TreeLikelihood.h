@@ -77,6 +77,7 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   bool scaling_ = true;
   bool incremental_ = true;
   bool compressed_ = false;  // usePatterns: PLK_FLAG_SUBTREE_PATTERNS on the engine
+  bool hostP_ = false;       // some branch P(t) came from the host (Taylor branch)
   size_t maxSons_ = 0;
   bool derivFirst_ = true, derivSecond_ = true;
   unsigned extraFlags_ = 0;                  // plk_create flags of the subclass (PLK_FLAG_DOUBLE_RECURSIVE)
@@ -105,6 +106,8 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   // Upload transition matrices for the given branches (nodes) of model m(node).
   void updatePmatrices(const std::vector<const Node*>& nodes);
   virtual int modelIndexForNode(const Node*) const { return 0; }
+  // the model behind engine model index m (host P(t) for a model whose eigen-system failed)
+  virtual const SubstitutionModel* modelForIndex(int m) const = 0;
   void uploadEigen(int modelIndex, const SubstitutionModel& model);
   void uploadRates();
   void computeTreeLikelihood(const std::vector<const Node*>* changed = nullptr);
@@ -167,6 +170,7 @@ class RHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
   ParameterList getSubstitutionModelParameters() const override;
   const SubstitutionModel* getModel() const { return model_; }
   SubstitutionModel* getModel() { return model_; }
+  const SubstitutionModel* modelForIndex(int) const override { return model_; }
   void computeAllTransitionProbabilities();
 };
 
@@ -188,6 +192,7 @@ class RNonHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
   std::map<int, int> modelOfNodeId_;
 
   int modelIndexForNode(const Node* n) const override;
+  const SubstitutionModel* modelForIndex(int m) const override;
 
  protected:
   // engine flags of a subclass (DRNonHomogeneousTreeLikelihood) must be known before setData

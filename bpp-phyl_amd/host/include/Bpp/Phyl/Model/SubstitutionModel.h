@@ -36,6 +36,12 @@ class SubstitutionModel : public AbstractParametrizable {
   bool isNonSingular_ = true;
   bool isScalable_ = true;
   mutable RowMatrix<double> pijt_, dpijt_, d2pijt_;
+  // powers of the generator for the Taylor branch of getPij_t (singular eigenvectors,
+  // Model/AbstractSubstitutionModel.cpp:386-418, 470-492)
+  std::vector<RowMatrix<double> > vPowGen_;
+  // after the eigen-decomposition: V Lambda V^-1 must give Q back and V V^-1 = I
+  // (the reference's isDiagonalizable / isNonSingular checks, :277-330); else Taylor
+  void checkEigen();
 
  public:
   SubstitutionModel(const Alphabet* alpha, size_t size, const std::string& prefix)
@@ -72,6 +78,12 @@ class SubstitutionModel : public AbstractParametrizable {
   virtual const RowMatrix<double>& getPij_t(double t) const;
   virtual const RowMatrix<double>& getdPij_dt(double t) const;
   virtual const RowMatrix<double>& getd2Pij_dt2(double t) const;
+  // for tests: replace the eigen-system as a failed decomposition would leave it
+  void forceTaylorForTests() {
+    isNonSingular_ = false;
+    isDiagonalizable_ = false;
+    checkEigen();
+  }
 
   // Leaf init value: 1 if resolved state i is in the alias set of `state`
   // (Model/AbstractSubstitutionModel.cpp:98-112); throws BadIntException for gaps.

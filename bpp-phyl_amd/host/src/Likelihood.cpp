@@ -227,6 +227,34 @@ void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& 
     mod.push_back(modelIndexForNode(n));
     t.push_back(n->getDistanceToFather());
   }
+  // a model whose eigen-system failed its check (SubstitutionModel::checkEigen) has no
+  // device path: its branches get host P(t . r_c) from the Taylor branch of getPij_t
+  // (plk_set_pmatrix; derivatives of those branches are then numerical)
+  {
+    size_t k = 0;
+    const Vdouble& rates = rateDistribution_->getCategories();
+    std::vector<double> P(nbClasses_ * nbStates_ * nbStates_);
+    for (size_t i = 0; i < br.size(); i++) {
+      const SubstitutionModel* m = modelForIndex(mod[i]);
+      if (m && !m->isNonSingular()) {
+        hostP_ = true;
+        for (size_t c = 0; c < nbClasses_; c++) {
+          const RowMatrix<double>& Pc = m->getPij_t(t[i] * rates[c]);
+          std::copy(Pc.data(), Pc.data() + nbStates_ * nbStates_, P.begin() + c * nbStates_ * nbStates_);
+        }
+        check(plk_set_pmatrix(engine_, br[i], P.data()), "plk_set_pmatrix");
+      } else {
+        br[k] = br[i];
+        mod[k] = mod[i];
+        t[k] = t[i];
+        k++;
+      }
+    }
+    br.resize(k);
+    mod.resize(k);
+    t.resize(k);
+    if (br.empty()) return;
+  }
   // dP and d2P ride along when derivatives are enabled (the reference computes them
   // with every P, AbstractHomogeneousTreeLikelihood.cpp:375-413)
   const unsigned mask = (derivFirst_ || derivSecond_) ? (PLK_DERIV_P | PLK_DERIV_DP | PLK_DERIV_D2P) : PLK_DERIV_P;
@@ -339,7 +367,7 @@ VVVdouble AbstractPlkTreeLikelihood::getLikelihoodArray(int nodeId) const {
 // for every model; central differences of the device log-likelihood only if the
 // engine reports PLK_ERR_UNSUPPORTED (per-subtree pattern compression).
 bool AbstractPlkTreeLikelihood::analyticDerivatives(const std::string& variable, double* d1, double* d2) const {
-  if (!(derivFirst_ || derivSecond_)) return false;
+  if (!(derivFirst_ || derivSecond_) || hostP_) return false;
   const Node* n = nodes_.at(TextTools::to<size_t>(variable.substr(5)));
   if (extraFlags_ & PLK_FLAG_DOUBLE_RECURSIVE) {
     if (!drValid_) {
@@ -544,6 +572,9 @@ RNonHomogeneousTreeLikelihood::RNonHomogeneousTreeLikelihood(const Tree& tree, c
 }
 
 int RNonHomogeneousTreeLikelihood::modelIndexForNode(const Node* n) const { return modelOfNodeId_.at(n->getId()); }
+const SubstitutionModel* RNonHomogeneousTreeLikelihood::modelForIndex(int m) const {
+  return modelSet_->getModel((size_t)m);
+}
 
 void RNonHomogeneousTreeLikelihood::setData(const SiteContainer& sites) {
   const SubstitutionModel& m0 = *modelSet_->getModel(0);

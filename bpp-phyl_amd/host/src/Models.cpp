@@ -61,10 +61,74 @@ void eigenProduct(const RowMatrix<double>& V, const Vdouble& w, const RowMatrix<
 }
 }  // namespace
 
+namespace {
+void matMul(const RowMatrix<double>& A, const RowMatrix<double>& B, RowMatrix<double>& out) {
+  const size_t n = A.getNumberOfRows();
+  RowMatrix<double> r(n, n);
+  for (size_t i = 0; i < n; i++)
+    for (size_t j = 0; j < n; j++) {
+      double s = 0.;
+      for (size_t k = 0; k < n; k++) s += A(i, k) * B(k, j);
+      r(i, j) = s;
+    }
+  out = r;
+}
+}  // namespace
+
+// Model/AbstractSubstitutionModel.cpp:277-330 decide isDiagonalizable / isNonSingular from
+// the decomposition; the symmetric form used here is always diagonalizable in exact
+// arithmetic, so the check is numerical: the decomposition must reproduce the generator
+// and V V^-1 = I to 1e-10 (relative to |Q|).  On failure P(t) comes from the reference's
+// truncated Taylor series with scaling and squaring (:386-418, 470-492).
+void SubstitutionModel::checkEigen() {
+  if (isNonSingular_) {
+    double qmax = 0., err = 0.;
+    for (size_t i = 0; i < size_; i++)
+      for (size_t j = 0; j < size_; j++) qmax = std::max(qmax, std::fabs(generator_(i, j)));
+    for (size_t i = 0; i < size_ && std::isfinite(err); i++)
+      for (size_t j = 0; j < size_; j++) {
+        double q = 0., id = 0.;
+        for (size_t k = 0; k < size_; k++) {
+          q += rightEigenVectors_(i, k) * eigenValues_[k] * leftEigenVectors_(k, j);
+          id += rightEigenVectors_(i, k) * leftEigenVectors_(k, j);
+        }
+        err = std::max(err, std::fabs(q - generator_(i, j)) / std::max(qmax, 1e-300));
+        err = std::max(err, std::fabs(id - (i == j ? 1. : 0.)));
+        if (!std::isfinite(q) || !std::isfinite(id)) err = INFINITY;
+      }
+    if (!(err <= 1e-10)) isNonSingular_ = isDiagonalizable_ = false;
+  }
+  vPowGen_.clear();
+  if (!isNonSingular_) {
+    // vPowGen_[k] = Q^k / 1 (the factorials are applied in getPij_t), k = 0 .. 30
+    vPowGen_.resize(31, RowMatrix<double>(size_, size_));
+    for (size_t i = 0; i < size_; i++) vPowGen_[0](i, i) = 1.;
+    for (size_t k = 1; k < vPowGen_.size(); k++) matMul(vPowGen_[k - 1], generator_, vPowGen_[k]);
+  }
+}
+
 const RowMatrix<double>& SubstitutionModel::getPij_t(double t) const {
   if (t == 0.) {
     for (size_t i = 0; i < size_; i++)
       for (size_t j = 0; j < size_; j++) pijt_(i, j) = (i == j) ? 1. : 0.;
+    return pijt_;
+  }
+  if (!isNonSingular_) {
+    // exp(r t Q) = (exp(r t / 2^m Q))^(2^m), the inner exponential by 30 Taylor terms
+    for (size_t i = 0; i < size_; i++)
+      for (size_t j = 0; j < size_; j++) pijt_(i, j) = (i == j) ? 1. : 0.;
+    double s = 1., v = rate_ * t;
+    size_t m = 0;
+    while (v > 0.5) {
+      m++;
+      v /= 2;
+    }
+    for (size_t k = 1; k < vPowGen_.size(); k++) {
+      s *= v / (double)k;
+      for (size_t i = 0; i < size_; i++)
+        for (size_t j = 0; j < size_; j++) pijt_(i, j) += s * vPowGen_[k](i, j);
+    }
+    while (m-- > 0) matMul(pijt_, pijt_, pijt_);
     return pijt_;
   }
   Vdouble w(size_);
@@ -74,6 +138,13 @@ const RowMatrix<double>& SubstitutionModel::getPij_t(double t) const {
 }
 
 const RowMatrix<double>& SubstitutionModel::getdPij_dt(double t) const {
+  if (!isNonSingular_) {  // d/dt exp(r t Q) = r Q exp(r t Q)
+    const RowMatrix<double> P = getPij_t(t);
+    matMul(generator_, P, dpijt_);
+    for (size_t i = 0; i < size_; i++)
+      for (size_t j = 0; j < size_; j++) dpijt_(i, j) *= rate_;
+    return dpijt_;
+  }
   Vdouble w(size_);
   for (size_t k = 0; k < size_; k++) w[k] = rate_ * eigenValues_[k] * std::exp(eigenValues_[k] * rate_ * t);
   eigenProduct(rightEigenVectors_, w, leftEigenVectors_, dpijt_);
@@ -81,6 +152,13 @@ const RowMatrix<double>& SubstitutionModel::getdPij_dt(double t) const {
 }
 
 const RowMatrix<double>& SubstitutionModel::getd2Pij_dt2(double t) const {
+  if (!isNonSingular_) {  // r^2 Q^2 exp(r t Q)
+    const RowMatrix<double> P = getPij_t(t);
+    matMul(vPowGen_[2], P, d2pijt_);
+    for (size_t i = 0; i < size_; i++)
+      for (size_t j = 0; j < size_; j++) d2pijt_(i, j) *= rate_ * rate_;
+    return d2pijt_;
+  }
   Vdouble w(size_);
   for (size_t k = 0; k < size_; k++) {
     const double l = rate_ * eigenValues_[k];
@@ -134,6 +212,7 @@ void SubstitutionModel::computeEigen() {
   }
   isDiagonalizable_ = true;
   isNonSingular_ = true;
+  checkEigen();
 }
 
 void AbstractReversibleSubstitutionModel::updateMatrices() {

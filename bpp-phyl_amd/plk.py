@@ -37,7 +37,7 @@ EXPORTS = [
     "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
     "plk_kernel_path", "plk_evaluate", "plk_compressed_work", "plk_all_branch_derivatives",
     "plk_get_timing_ex", "plk_traversal_work", "plk_create_multi", "plk_shard_count", "plk_comm_get_id",
-    "plk_comm_init",
+    "plk_comm_init", "plk_get_dpmatrix",
 ]
 
 
@@ -101,6 +101,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_update_pmatrices": ([ct.c_void_p, ct.c_int, ip, ip, dp, ct.c_uint], ct.c_int),
         "plk_set_pmatrix": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
         "plk_get_pmatrix": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
+        "plk_get_dpmatrix": ([ct.c_void_p, ct.c_int, ct.c_int, dp], ct.c_int),
         "plk_update_partials": ([ct.c_void_p, P(plk_op), ct.c_int], ct.c_int),
         "plk_get_partials": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
         "plk_root_loglik": ([ct.c_void_p, ct.c_int, dp, dp, dp], ct.c_int),
@@ -263,6 +264,12 @@ class Engine:
     def get_pmatrix(self, branch: int) -> np.ndarray:
         out = np.empty((self.C, self.S, self.S))
         self._chk(self.lib.plk_get_pmatrix(self.h, branch, _d(out)))
+        return out
+
+    def get_dpmatrix(self, branch: int, order: int) -> np.ndarray:
+        """r_c dP/dt (order 1) or r_c^2 d2P/dt2 (order 2) of the branch, per class."""
+        out = np.empty((self.C, self.S, self.S))
+        self._chk(self.lib.plk_get_dpmatrix(self.h, branch, order, _d(out)))
         return out
 
     def _op_array(self, ops):

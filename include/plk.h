@@ -179,6 +179,11 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
                          const double* t, unsigned deriv_mask);
 int plk_set_pmatrix(plk_handle h, int branch, const double* P /* C x S x S */);
 int plk_get_pmatrix(plk_handle h, int branch, double* P /* C x S x S */);
+/* The derivative matrices plk_update_pmatrices stored with PLK_DERIV_DP (order 1: r_c dP/dt)
+ * or PLK_DERIV_D2P (order 2: r_c^2 d2P/dt2) -- the reference's getdPij_dt / getd2Pij_dt2
+ * (Model/AbstractSubstitutionModel.cpp:499-641) scaled as computeTransitionProbabilitiesForNode
+ * stores them (Likelihood/AbstractHomogeneousTreeLikelihood.cpp:375-413). */
+int plk_get_dpmatrix(plk_handle h, int branch, int order, double* dP /* C x S x S */);
 
 /* Partials */
 int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops);

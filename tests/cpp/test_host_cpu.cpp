@@ -64,6 +64,15 @@ int main() {
   printModel("T92_k2_t03", T92(dna, 2.0, 0.3), ts);
   printModel("GTR", GTR(dna, 1.2, 0.4, 0.6, 0.8, 0.5, 0.30, 0.20, 0.25, 0.25), ts);
   printModel("LG08", LG08(&AlphabetTools::PROTEIN_ALPHABET), ts);
+  {
+    // the Taylor branch of getPij_t (a failed eigen-system check): same P(t)
+    GTR g(dna, 1.2, 0.4, 0.6, 0.8, 0.5, 0.30, 0.20, 0.25, 0.25);
+    g.forceTaylorForTests();
+    printModel("GTR_taylor", g, ts);
+    LG08 l(&AlphabetTools::PROTEIN_ALPHABET);
+    l.forceTaylorForTests();
+    printModel("LG08_taylor", l, ts);
+  }
   StandardGeneticCode gc(dna);
   printModel("YN98", YN98(&gc, std::vector<double>(), 2.0, 0.3), ts);
   // trees: postorder ids, unroot

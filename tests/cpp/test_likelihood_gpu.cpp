@@ -10,6 +10,7 @@
 #include <Bpp/Phyl/Model/FrequencySet/NucleotideFrequencySet.h>
 #include <Bpp/Phyl/Model/SubstitutionModelSetTools.h>
 #include <Bpp/Phyl/Likelihood/RHomogeneousTreeLikelihood.h>
+#include <Bpp/Phyl/Model/Nucleotide/GTR.h>
 #include <Bpp/Phyl/Model/Nucleotide/T92.h>
 #include <Bpp/Phyl/Model/RateDistribution/GammaDiscreteRateDistribution.h>
 #include <Bpp/Phyl/OptimizationTools.h>
@@ -194,6 +195,31 @@ static void nonHomogeneousDrCase() {
   }
 }
 
+// a model whose eigen-system fails its check: P(t) from the host Taylor branch
+// (Model/AbstractSubstitutionModel.cpp:470-492) handed over with plk_set_pmatrix; the
+// likelihood equals the device eigen path's, and the optimiser still converges
+static void taylorModelCase() {
+  std::unique_ptr<TreeTemplate<Node> > tree(
+      TreeTemplateTools::parenthesisToTree("((A:0.01, B:0.02):0.03,C:0.01,D:0.1);"));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  const char* names[] = {"A", "B", "C", "D"};
+  const char* seqs[] = {"AAATGGCTGTGCACGTC", "GACTGGATCTGCACGTC", "CTCTGGATGTGCACGTG", "AAATGGCGGTGCGCCTA"};
+  for (int i = 0; i < 4; i++) aln.addSequence(BasicSequence(names[i], seqs[i], dna));
+  GTR eig(dna, 1.2, 0.4, 0.6, 0.8, 0.5, 0.30, 0.20, 0.25, 0.25);
+  GTR tay(dna, 1.2, 0.4, 0.6, 0.8, 0.5, 0.30, 0.20, 0.25, 0.25);
+  tay.forceTaylorForTests();
+  GammaDiscreteRateDistribution rdist(4, 0.7);
+  RHomogeneousTreeLikelihood a(*tree, aln, &eig, &rdist, true, false);
+  a.initialize();
+  RHomogeneousTreeLikelihood b(*tree, aln, &tay, &rdist, true, false);
+  b.initialize();
+  expectNear("host Taylor P(t) vs device eigen P(t): -lnL", b.getValue(), a.getValue(), 1e-10 * a.getValue());
+  ParameterList bl = b.getBranchLengthsParameters();
+  expectNear("numerical d1 (host P) vs analytic", b.getFirstOrderDerivative(bl[0].getName()),
+             a.getFirstOrderDerivative(bl[0].getName()), 1e-4);
+}
+
 // gaps are not allowed by the model: BadIntException like getInitValue
 static void gapCase() {
   std::unique_ptr<TreeTemplate<Node> > tree(TreeTemplateTools::parenthesisToTree("((A:0.1,B:0.2):0.1,C:0.3);"));
@@ -220,6 +246,7 @@ int main() {
     rootedConstantCase();
     doubleRecursiveCase();
     nonHomogeneousDrCase();
+    taylorModelCase();
     gapCase();
   } catch (Exception& e) {
     std::cerr << e.what() << std::endl;

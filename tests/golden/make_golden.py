@@ -147,6 +147,12 @@ def main():
     Qy, piy = yn98_Q(2.0, 0.3)
     out["YN98_Q"], out["YN98_pi"], out["YN98_t"] = Qy, piy, ts
     out["YN98_P"] = np.stack([expm(Qy * t) for t in ts])
+    # first and second derivatives in t: dP/dt = Q expm(Q t), d2P/dt2 = Q^2 expm(Q t)
+    # (getdPij_dt / getd2Pij_dt2, Model/AbstractSubstitutionModel.cpp:499-641)
+    for name in ("GTR", "LG08", "YN98"):
+        Q = out[f"{name}_Q"]
+        out[f"{name}_dP"] = np.stack([Q @ expm(Q * t) for t in ts])
+        out[f"{name}_d2P"] = np.stack([Q @ Q @ expm(Q * t) for t in ts])
     np.savez_compressed(os.path.join(HERE, "pmatrix.npz"), **out)
 
     # ---- pruning fixtures on small seeded problems

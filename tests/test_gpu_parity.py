@@ -105,6 +105,37 @@ def test_pmatrix_kernel_vs_expm(name):
         assert np.allclose(eng.get_pmatrix(i)[0], P, atol=1e-13)
 
 
+@pytest.mark.parametrize("name", ["GTR", "LG08", "YN98"])
+def test_dpmatrix_kernel_vs_expm(name):
+    """dP/dt and d2P/dt2 from K4 (PLK_DERIV_DP | PLK_DERIV_D2P) against Q expm(Qt) and
+    Q^2 expm(Qt) fixtures (getdPij_dt / getd2Pij_dt2, Model/AbstractSubstitutionModel.cpp:
+    499-641), one class of rate 1; and r_c / r_c^2 scaling with Gamma classes."""
+    f = np.load(os.path.join(GOLD, "pmatrix.npz"))
+    m = {"GTR": phylo.gtr(a=1.2, b=0.4, c=0.6, d=0.8, e=0.5, piA=0.30, piC=0.20, piG=0.25, piT=0.25),
+         "LG08": phylo.lg08(), "YN98": phylo.yn98(2.0, 0.3)}[name]
+    ts = f[f"{name}_t"]
+    et = phylo.engine_tree(phylo.balanced_tree(8))
+    eng = plk.Engine(0, m.S, 1, 256, et.n_tips, et.n_internal, 1)
+    eng.set_category_rates(np.ones(1), np.ones(1))
+    eng.set_eigen(0, m.V, m.Vinv, m.lam)
+    br = np.arange(len(ts), dtype=np.int32)
+    eng.update_pmatrices(br, ts, deriv_mask=plk.PLK_DERIV_P | plk.PLK_DERIV_DP | plk.PLK_DERIV_D2P)
+    scale = max(1.0, float(np.abs(f[f"{name}_Q"]).max()))
+    for i in range(len(ts)):
+        assert np.allclose(eng.get_dpmatrix(i, 1)[0], f[f"{name}_dP"][i], atol=1e-13 * scale)
+        assert np.allclose(eng.get_dpmatrix(i, 2)[0], f[f"{name}_d2P"][i], atol=1e-13 * scale ** 2)
+    rates, probs = phylo.gamma_rates(4, 0.5)
+    e4 = plk.Engine(0, m.S, 4, 256, et.n_tips, et.n_internal, 1)
+    e4.set_category_rates(rates, probs)
+    e4.set_eigen(0, m.V, m.Vinv, m.lam)
+    e4.update_pmatrices(np.array([0], dtype=np.int32), np.array([0.3]), deriv_mask=7)
+    Q = f[f"{name}_Q"]
+    for c, r in enumerate(rates):
+        E = m.pij(0.3 * r)
+        assert np.allclose(e4.get_dpmatrix(0, 1)[c], r * (Q @ E), atol=1e-12 * scale * r)
+        assert np.allclose(e4.get_dpmatrix(0, 2)[c], r * r * (Q @ Q @ E), atol=1e-12 * (scale * r) ** 2)
+
+
 def test_pmatrix_derivatives():
     m = phylo.gtr(a=1.2, b=0.4, c=0.6, d=0.8, e=0.5, piA=0.30, piC=0.20, piG=0.25, piT=0.25)
     eng = plk.Engine(0, 4, 4, 256, 4, 2, 1)
@@ -928,10 +959,11 @@ def test_jit_treeM_vs_oracle(C, tree_kind, n_patterns, scaling, mode, variant, m
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dm,L", [(2, 1), (4, 2)])
-def test_jit_treeM_register_depths(dm, L, monkeypatch):
-    """Other fragment heights and fetch lookaheads give the default kernel's results to
-    rounding (different cuts store different partials; the arithmetic per node is the same)."""
+@pytest.mark.parametrize("dm,L,direct", [(2, 1, "0"), (3, 2, "0"), (4, 1, "1"), (3, 1, "1")])
+def test_jit_treeM_register_depths(dm, L, direct, monkeypatch):
+    """Other fragment heights, fetch lookaheads and A-operand sources (LDS-staged / direct
+    from L1-L2) give the default kernel's results bitwise (different cuts store different
+    partials, but every operation per node is the same)."""
     et, m, alph, rates, probs, states = _random_problem(20, 4, 80, 600, seed=77, amb=True)
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
@@ -939,7 +971,83 @@ def test_jit_treeM_register_depths(dm, L, monkeypatch):
     del eng
     monkeypatch.setenv("PLK_JITM_DM", str(dm))
     monkeypatch.setenv("PLK_JITM_L", str(L))
+    monkeypatch.setenv("PLK_JITM_DIRECT", direct)
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
     l1, s1, _ = run_engine(eng, et)
     assert eng.kernel_path() == "jit_treeM"
     assert np.array_equal(s0, s1) and l0 == l1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode,nh", [
+    (4, "balanced64", 3000, False, "lnl_only", False), (4, "balanced64", 1000, False, "materialize", False),
+    (2, "caterpillar40", 700, True, "lnl_only", False), (4, "balanced300", 513, True, "lnl_only", True),
+    (1, "balanced64", 333, True, "materialize", False), (4, "caterpillar200long", 600, True, "lnl_only", False)])
+def test_s4_on_matrix_cores_vs_oracle(C, tree_kind, n_patterns, scaling, mode, nh, monkeypatch):
+    """4 states through jit_treeM (PLK_S4_JITM=1: one v_mfma_f64_4x4x4_4b block per class
+    and 16 patterns) against the oracle at 1e-12, homogeneous and per-branch models."""
+    monkeypatch.setenv("PLK_S4_JITM", "1")
+    if tree_kind.startswith("balanced"):
+        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=41, lo=0.05, hi=0.4)
+    elif tree_kind.endswith("long"):
+        tree = _caterpillar(int(tree_kind[11:-4]), seed=5, lo=0.5, hi=1.5)
+    else:
+        tree = _caterpillar(int(tree_kind[11:]), seed=6)
+    et = phylo.engine_tree(tree, unroot=not nh)
+    rng = np.random.default_rng(C * 17 + n_patterns)
+    rates, probs = phylo.gamma_rates(C, 0.5) if C > 1 else (np.ones(1), np.ones(1))
+    if nh:
+        models = [phylo.gtr(1.2, 0.4, 0.6, 0.8, 0.5, *rng.dirichlet(np.ones(4) * 5)) for _ in range(et.n_nodes)]
+        mon = np.arange(et.n_nodes)
+        pi = np.array([0.3, 0.2, 0.2, 0.3])
+    else:
+        models = [phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))]
+        mon = None
+        pi = models[0].pi
+    wl = workload.Workload("m", et, models, mon, rates, probs, pi, phylo.DNA, n_patterns, scaling, not nh, 5)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    mask = rng.random(states.shape) < 0.05
+    states[mask] = rng.integers(4, 15, size=mask.sum())
+    flags = (0 if nh else plk.PLK_FLAG_NONNEG_GUARD) | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, 4, C, n_patterns, states, phylo.DNA.init_table, rates, probs, pi, models,
+                     model_of_node=mon, flags=flags)
+    lnl, site, blocks = run_engine(eng, et)
+    assert eng.kernel_path() == "jit_treeM"
+    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, pi, models, model_of_node=mon,
+                        scaling=scaling, pmats=engine_pmats(eng, et))
+    check(lnl, site, lo, so)
+    lnl2, site2, _ = run_engine(eng, et)
+    assert lnl2 == lnl and np.array_equal(site2, site)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,n_taxa,n_patterns,scaling,mode,variant", [
+    (1, 24, 700, False, "lnl_only", ""), (1, 40, 500, True, "materialize", "amb"), (1, 128, 300, False, "lnl_only", "yn98"),
+    (2, 16, 400, True, "lnl_only", ""), (1, 24, 600, True, "lnl_only", "tiny")])
+def test_jit_treeM_64_states_vs_oracle(C, n_taxa, n_patterns, scaling, mode, variant, monkeypatch):
+    """64 states on jit_treeM (PLK_JITM64=1: 16 x 16 blocks of v_mfma_f64_4x4x4_4b per
+    class and contraction) against the oracle at 1e-12 on the engine's P(t), incl. the YN98
+    codon model of config 4 with its null stop states."""
+    monkeypatch.setenv("PLK_JITM64", "1")
+    et, m, alph, rates, probs, states = _random_problem(64, C, n_taxa, n_patterns, seed=640 + C + n_taxa,
+                                                        amb=variant == "amb")
+    if variant == "yn98":
+        m = phylo.yn98(2.0, 0.3)
+        wl = workload.Workload("y", et, [m], None, rates, probs, m.pi, phylo.CODON, n_patterns, scaling, True, 3)
+        states = wl.simulate(0, n_patterns).astype(np.int32)
+    init = alph.init_table
+    if variant == "tiny":
+        init = np.array(init, dtype=np.float64, copy=True)
+        code = alph.n_codes - 1
+        init[code] = 1e-80
+        states[np.random.default_rng(2).random(states.shape) < 0.3] = code
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, 64, C, n_patterns, states, init, rates, probs, m.pi, [m], flags=flags)
+    lnl, site, _ = run_engine(eng, et)
+    assert eng.kernel_path() == "jit_treeM"
+    lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=scaling, pmats=engine_pmats(eng, et))
+    check(lnl, site, lo, so)
+    if variant == "tiny":
+        assert site.min() < -256 * np.log(2)
+    lnl2, site2, _ = run_engine(eng, et)
+    assert lnl2 == lnl and np.array_equal(site2, site)

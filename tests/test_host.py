@@ -50,6 +50,17 @@ def test_host_pmatrix_vs_expm_fixture(host_records, name):
         assert np.allclose(np.array(Pe).reshape(S, S), Pf, atol=1e-13)
 
 
+@pytest.mark.parametrize("name", ["GTR", "LG08"])
+def test_host_taylor_branch_vs_expm_fixture(host_records, name):
+    """A model whose eigen-system fails the check gets P(t) from the reference's Taylor
+    series with scaling and squaring (Model/AbstractSubstitutionModel.cpp:470-492)."""
+    f = np.load(os.path.join(GOLD, "pmatrix.npz"))
+    r = _models(host_records)[name + "_taylor"]
+    S = r["S"]
+    for P, Pf in zip(r["P"], f[f"{name}_P"]):
+        assert np.allclose(np.array(P).reshape(S, S), Pf, atol=1e-12)
+
+
 def test_host_yn98_properties(host_records):
     r = _models(host_records)["YN98"]
     Q = np.array(r["Q"]).reshape(64, 64)
