@@ -1125,7 +1125,9 @@ FusedKind fused_kind(plk_handle h) {
   if (h->S == 4) return (h->C == 1 || h->C == 2 || h->C == 4) ? FK_TREE4 : FK_NONE;
   if (h->C > kTreeMaxWaves) return FK_NONE;
   if (h->S == 20 && !env_is("PLK_FUSED20", '0')) return env_is("PLK_TREES", '1') ? FK_TREES : FK_TREEM;
-  if (h->S == 64 && h->C == 1 && !env_is("PLK_FUSED64", '0')) return FK_TREEM;
+  if (h->S == 64 && !env_is("PLK_FUSED64", '0') &&
+      (h->C == 1 || (env_is("PLK_JITM64", '1') && !env_is("PLK_JITM", '0'))))
+    return FK_TREEM;  // the treeM interpreter takes one class; jit_treeM any C <= 4
   return FK_NONE;
 }
 
@@ -1631,7 +1633,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     a.buf_doubles = (a.buf_doubles + 1) & ~1;
     const int threads = 64 * treeM_groups(h) * (h->S == 64 ? 1 : h->C);
     const int pf = h->S == 64 ? treeM_pf<64>() : treeM_pf<20>();
-    if (!treeM_direct(h) && a.buf_doubles > pf * threads)
+    if (!h->prog_jitm && !treeM_direct(h) && a.buf_doubles > pf * threads)
       return fail(h, PLK_ERR_UNSUPPORTED, "fused MFMA tables (%d doubles) exceed the staging registers",
                   a.buf_doubles);
     a.buf_doubles = std::max(a.buf_doubles, (pf - 1) * threads);  // unconditional stores stay inside
@@ -1756,6 +1758,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.L = env_int("PLK_JITM_L", 1, 1, 4);
     msh.minw = env_int("PLK_JITM_MINW", 2, 1, 8);
     msh.direct = env_is("PLK_JITM_DIRECT", '1');
+    msh.pd = env_int("PLK_JITM_PD", 1, 1, 3);
+    msh.hoist = env_int("PLK_JITM_HOIST", 0, 0, 1) != 0;
     if (msh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "jit_treeM needs %zu B of LDS", msh.lds_bytes());
     if (!h->jitm_fn || !(msh == h->jitm_shape)) {

@@ -98,11 +98,14 @@ struct JitMShape {
   int L = 1;         // operand fetch lookahead (events)
   int minw = 2;      // __launch_bounds__ min waves per SIMD
   bool direct = false;  // A operands straight from P(t) in L1/L2 (no LDS staging, no barriers)
+  int pd = 1;           // P(t) staging prefetch distance (contractions ahead)
+  bool hoist = false;   // cherry codes of the whole fragment loaded at its start
   static constexpr int G = 4;  // waves (16-pattern groups) per workgroup: 64 patterns
   int pb() const { return C * S * S; }  // doubles per P buffer (every class of one branch)
   size_t lds_bytes() const { return (size_t)((direct ? 0 : 2 * pb()) + 64) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
-    return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && direct == o.direct;
+    return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && direct == o.direct &&
+           pd == o.pd && hoist == o.hoist;
   }
 };
 
@@ -149,6 +152,14 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
     F[c_][X_] = r_[(i64)c_ * (U2_ * S_) + 4 * X_]; \
   if (SC_) FK = (int)base_[a.cherry_table_bytes + code_]; }
+// the same with the combined code already in a register (hoisted to the fragment start)
+#define CHERRY_CODE(CC, k) const int CC = reinterpret_cast<const u16*>(a.cherry + (i64)(k) * a.cherry_stride + \
+  a.cherry_table_bytes + a.cherry_count_bytes)[p];
+#define CHERRY_FETCH_C(F, FK, k, CC) { const u8* base_ = a.cherry + (i64)(k) * a.cherry_stride; \
+  const double* r_ = reinterpret_cast<const double*>(base_) + (i64)(CC) * S_ + hi; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
+    F[c_][X_] = r_[(i64)c_ * (U2_ * S_) + 4 * X_]; \
+  if (SC_) FK = (int)base_[a.cherry_table_bytes + (CC)]; }
 #define TIP_FETCH(F, t) { const int code_ = a.codes[(i64)(t) * a.n_pad + p]; \
   const double* r_ = a.tipP + ((i64)(t) * (C_ * U_) + code_) * S_ + hi; \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
@@ -209,8 +220,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     const int c = e / (S_ * S_), r = e - c * (S_ * S_), x = r / S_, y = r - x * S_;
     sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3) : -1;
   }
-  double R[PF_];
-  (void)red; (void)PA; (void)PG; (void)R; (void)toff; (void)sidx;
+  double R0[PF_], R1[PF_], R2[PF_];
+  (void)red; (void)PA; (void)PG; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
   const int frag = frag_base + (int)blockIdx.y;
 )PLKJITM";
   // accumulators per register level and the operand ring
@@ -250,7 +261,9 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     auto emit_fetch = [&](int i) {
       const TInstr& e = ev[(size_t)i];
       const int sl = slot[(size_t)i];
-      if (e.op == T_CHERRY)
+      if (e.op == T_CHERRY && sh.hoist)
+        snprintf(buf, sizeof(buf), "    CHERRY_FETCH_C(F%d, FK%d, %d, CC%d)\n", sl, sl, e.a, e.a);
+      else if (e.op == T_CHERRY)
         snprintf(buf, sizeof(buf), "    CHERRY_FETCH(F%d, FK%d, %d)\n", sl, sl, e.a);
       else if (e.op == T_TIP)
         snprintf(buf, sizeof(buf), "    TIP_FETCH(F%d, %d)\n", sl, e.a);
@@ -260,16 +273,41 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     };
     snprintf(buf, sizeof(buf), "  case %zu: {\n", f);
     s += buf;
+    if (sh.hoist)
+      for (const TInstr& e : ev)
+        if (e.op == T_CHERRY) {
+          snprintf(buf, sizeof(buf), "    CHERRY_CODE(CC%d, %d)\n", e.a, e.a);
+          s += buf;
+        }
     size_t nf = 0;
     for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
     int cur = 0;
     size_t np = 0;  // P-chain events consumed
     if (sh.direct) pchain.clear();  // no staging chain: every contraction reads P(t) directly
+    const int PD = std::min(std::max(sh.pd, 1), 3);
+    // chain event j is staged from register set j % PD: loaded PD contractions ahead, stored
+    // to the other LDS buffer (and a barrier) at the end of the contraction before its own
+    auto pload = [&](size_t j) {
+      if (j < pchain.size()) {
+        snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R%zu, %d)\n", j % (size_t)PD, ev[(size_t)pchain[j]].b);
+        s += buf;
+      }
+    };
     if (!pchain.empty()) {
-      const TInstr& e0 = ev[(size_t)pchain[0]];
-      snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R, %d) PSTAGE_STORE(R, 0) __syncthreads();\n", e0.b);
-      s += buf;
+      pload(0);
+      s += "    PSTAGE_STORE(R0, 0) __syncthreads();\n";
+      for (size_t j = 1; j <= (size_t)PD; ++j) pload(j);
     }
+    // after chain event np's contraction: hand the next one's P(t) over, refill the set
+    auto pnext = [&]() {
+      if (np + 1 < pchain.size()) {
+        snprintf(buf, sizeof(buf), "    PSTAGE_STORE(R%zu, %d) __syncthreads();\n", (np + 1) % (size_t)PD, cur ^ 1);
+        s += buf;
+        cur ^= 1;
+        pload(np + 1 + (size_t)PD);
+      }
+      ++np;
+    };
     s += "    SB\n";
     std::vector<char> fresh((size_t)max_level + 2, 0);
     fresh[0] = 1;
@@ -287,19 +325,9 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
             s += buf;
           }
         } else if (e.op == T_LOAD) {
-          const bool more = np + 1 < pchain.size();
-          if (more) {
-            snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R, %d)\n", ev[(size_t)pchain[np + 1]].b);
-            s += buf;
-          }
           snprintf(buf, sizeof(buf), "    CONTRIB(A%d, F%d, %d, %s)\n", d, sl, cur, fresh[(size_t)d] ? "true" : "false");
           s += buf;
-          if (more) {
-            snprintf(buf, sizeof(buf), "    PSTAGE_STORE(R, %d) __syncthreads();\n", cur ^ 1);
-            s += buf;
-            cur ^= 1;
-          }
-          ++np;
+          pnext();
           if (sh.scale) {
             snprintf(buf, sizeof(buf), "    K%d += FK%d;\n", d, sl);
             s += buf;
@@ -329,22 +357,12 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
           snprintf(buf, sizeof(buf), "    STORE(A%d, K%d, %d)\n", d, d, e.a);
           s += buf;
         }
-        const bool more = np + 1 < pchain.size();
-        if (more) {
-          snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R, %d)\n", ev[(size_t)pchain[np + 1]].b);
-          s += buf;
-        }
         if (sh.direct)
           snprintf(buf, sizeof(buf), "    CONTRIB_G(A%d, A%d, %d, %s)\n", d - 1, d, e.b, fresh[(size_t)d - 1] ? "true" : "false");
         else
           snprintf(buf, sizeof(buf), "    CONTRIB(A%d, A%d, %d, %s)\n", d - 1, d, cur, fresh[(size_t)d - 1] ? "true" : "false");
         s += buf;
-        if (more) {
-          snprintf(buf, sizeof(buf), "    PSTAGE_STORE(R, %d) __syncthreads();\n", cur ^ 1);
-          s += buf;
-          cur ^= 1;
-        }
-        ++np;
+        if (!sh.direct) pnext();
         if (sh.scale) {
           snprintf(buf, sizeof(buf), "    K%d += K%d;\n", d - 1, d);
           s += buf;

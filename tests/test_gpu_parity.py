@@ -959,8 +959,9 @@ def test_jit_treeM_vs_oracle(C, tree_kind, n_patterns, scaling, mode, variant, m
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dm,L,direct", [(2, 1, "0"), (3, 2, "0"), (4, 1, "1"), (3, 1, "1")])
-def test_jit_treeM_register_depths(dm, L, direct, monkeypatch):
+@pytest.mark.parametrize("dm,L,direct,pd,hoist", [(2, 1, "0", 1, 0), (3, 2, "0", 2, 1), (4, 1, "1", 1, 0),
+                                                  (3, 1, "1", 1, 1), (4, 1, "0", 3, 0)])
+def test_jit_treeM_register_depths(dm, L, direct, pd, hoist, monkeypatch):
     """Other fragment heights, fetch lookaheads and A-operand sources (LDS-staged / direct
     from L1-L2) give the default kernel's results bitwise (different cuts store different
     partials, but every operation per node is the same)."""
@@ -972,6 +973,8 @@ def test_jit_treeM_register_depths(dm, L, direct, monkeypatch):
     monkeypatch.setenv("PLK_JITM_DM", str(dm))
     monkeypatch.setenv("PLK_JITM_L", str(L))
     monkeypatch.setenv("PLK_JITM_DIRECT", direct)
+    monkeypatch.setenv("PLK_JITM_PD", str(pd))
+    monkeypatch.setenv("PLK_JITM_HOIST", str(hoist))
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
     l1, s1, _ = run_engine(eng, et)
     assert eng.kernel_path() == "jit_treeM"

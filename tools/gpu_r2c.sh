@@ -2,7 +2,7 @@
 # matrix-core tree kernel A/B: 20 states staged vs direct, 4 states (PLK_S4_JITM) and
 # 64 states (PLK_JITM64) against the VALU / 16x16 kernels
 set -o pipefail
-bash tools/gpu_tests.sh t6 -k "jit_treeM or matrix_cores" || exit 1
+bash tools/gpu_tests.sh t6 -k "jit_treeM or matrix_cores" quick || exit 1
 O=gpurun_out/r2c; mkdir -p $O
 run() {  # name config envs
   env $(echo $3 | tr ',' ' ') timeout -k 10 200 python bench.py --config $2 --steps 10 --warmup 2 --no-cpu-baseline > $O/$1.json 2> $O/$1.err || { tail -5 $O/$1.err; return 1; }
