@@ -1705,7 +1705,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // every class in the wave (no barriers, ~104 VGPRs): two (cfg5 0.70 ms; G = 4 0.76,
     // G = 1 1.46); otherwise the G with the most resident waves (jit_auto_groups; cfg2
     // with cherry tables: G = 3, 0.207 ms, G = 2 0.222 ms)
-    sh.G = env_int("PLK_JIT_G", 0, 0, 4);
+    sh.G = env_int("PLK_JIT_G", 0, 0, 8);
     if (sh.G == 0) sh.G = h->prog_ciw ? 2 : sh.scale ? 1 : jit_auto_groups(sh);
     // two patterns per lane halve the P(t) reads per FMA but double the registers:
     // measured slower (cfg2 0.255-0.301 vs 0.241 ms), so opt-in; not with speculation

@@ -115,16 +115,27 @@ __device__ __forceinline__ unsigned long long launder_v(unsigned long long x) {
   return x;
 }
 
+// Rescale decisions from the high words of the doubles.  For x >= 0, x < 2^-256 iff
+// hi(x) < kThrHi (2^-256 has a zero low word), and negative values have negative (signed)
+// high words, so mh = max(0, hi(v)...) decides "0 < max(0, v...) < 2^-256" whenever
+// 0 < mh < 0x7FF00000: one 32-bit max3 per two values instead of an f64 max per value
+// plus the NaN canonicalisation of its operand.  Otherwise (every value <= 0, positive
+// values only denormals with a zero high word, an Inf or a NaN) the f64 path decides.
+#define kThrHi 0x2FF00000
+__device__ __forceinline__ int hiw(double x) { return (int)(__double_as_longlong(x) >> 32); }
+__device__ __forceinline__ bool hi_decides(int mh) { return mh > 0 && mh < 0x7FF00000; }
+
 // own-class max below the rescale threshold (or zero / NaN): the joint check of the
 // exact pass could fire here
 // (the flag is pinned with an empty asm right away: otherwise the compares sink to the
 // vote at the end of the fragment and keep every node's accumulator alive until then)
+// (hi-word max as in rescale(): not risky iff some value is finite and >= the threshold)
 template <int N>
 __device__ __forceinline__ void flag_risky(int& dng, const double (&v)[N]) {
-  double m = v[0];
+  int mh = hiw(v[0]);
 #pragma unroll
-  for (int i = 1; i < N; ++i) m = fmax(m, v[i]);
-  dng |= !(m >= kScaleThr);
+  for (int i = 1; i < N; ++i) mh = max(mh, hiw(v[i]));
+  dng |= !(mh >= kThrHi && mh < 0x7FF00000);
   asm volatile("" : "+v"(dng));
 }
 
@@ -134,6 +145,29 @@ __device__ __forceinline__ void flag_risky(int& dng, const double (&v)[N]) {
 template <int C, int CW, int PW, int NWT>
 __device__ __forceinline__ void rescale(double (&v)[4 * CW * PW], int (&cnt)[PW], double* xch, int w, int g) {
   constexpr int NW = C / CW;
+  if (NW == 1) {
+#pragma unroll
+    for (int pw = 0; pw < PW; ++pw) {
+      int mh = 0;
+#pragma unroll
+      for (int i = 0; i < 4 * CW; ++i) mh = max(mh, hiw(v[4 * CW * pw + i]));
+      bool up;
+      if (__builtin_expect(hi_decides(mh), 1)) {
+        up = mh < kThrHi;
+      } else {
+        double m = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4 * CW; ++i) m = fmax(m, v[4 * CW * pw + i]);
+        up = m > 0.0 && m < kScaleThr;
+      }
+      if (up) {
+#pragma unroll
+        for (int i = 0; i < 4 * CW; ++i) v[4 * CW * pw + i] *= kScaleUp;
+        cnt[pw] += 1;
+      }
+    }
+    return;
+  }
   double m[PW];
 #pragma unroll
   for (int pw = 0; pw < PW; ++pw) {
@@ -141,7 +175,7 @@ __device__ __forceinline__ void rescale(double (&v)[4 * CW * PW], int (&cnt)[PW]
 #pragma unroll
     for (int i = 0; i < 4 * CW; ++i) m[pw] = fmax(m[pw], v[4 * CW * pw + i]);
   }
-  if (NW > 1) {
+  {
     // one barrier: consecutive rescales alternate between two exchange buffers, so a
     // wave can only overwrite this buffer after every wave has passed the next
     // rescale's barrier, i.e. after every wave has read it here
@@ -169,6 +203,7 @@ template <int CW, int PW, bool SCALE>
 __device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0,
                                       const double (&v)[4 * CW * PW], const int (&cnt)[PW], bool gv) {
   if (!gv) return;  // a group past the last pattern (ragged last super-block) recomputes group 0
+  slot = (int)launder_s(slot);  // (as in LOADF)
   double* dst = a.partials + (i64)slot * a.slot_stride + off;
 #pragma unroll
   for (int pw = 0; pw < PW; ++pw)
@@ -536,10 +571,13 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
 // count bytes of a rescaling contribution unit
 #define KTF(K, KOFF, Q) { _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) \
     K[pw_] += (int)reinterpret_cast<const u8*>(tab + (KOFF))[((Q) >> (8 * pw_)) & 255]; }
-#define LOADF(F, FK, slot) { const double* L_ = a.partials + (i64)(slot) * a.slot_stride + toff; \
+// (slot numbers are laundered: otherwise every slot's base address is hoisted out of the
+// super-block loop into its own SGPR pair, and they spill)
+#define LOADF(F, FK, slot) { const i64 sl_ = (i64)launder_s(slot); \
+    const double* L_ = a.partials + sl_ * a.slot_stride + toff; \
     _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
       _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[4 * CW_ * pw_ + i_] = L_[64 * pw_ + (i64)i_ * kTile]; \
-      if (SC_) FK[pw_] = a.scale[(i64)(slot) * a.n_pad + p + 64 * pw_]; } }
+      if (SC_) FK[pw_] = a.scale[sl_ * a.n_pad + p + 64 * pw_]; } }
 #define SB __builtin_amdgcn_sched_barrier(0);
   // code staging: this thread's items (uint4 column j of group gg in unit k's code row;
   // JArgs::codes holds one row per unit, unit_codes_kernel), fixed over the super-blocks.

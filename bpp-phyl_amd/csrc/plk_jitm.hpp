@@ -66,6 +66,10 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 __device__ __attribute__((noinline)) double jitm_log(double x) { return log(x); }
+// rescale decision from the doubles' high words (see plk_jit.hpp hiw / hi_decides)
+#define kThrHi 0x2FF00000
+__device__ __forceinline__ int hiw(double x) { return (int)(__double_as_longlong(x) >> 32); }
+__device__ __forceinline__ bool hi_decides(int mh) { return mh > 0 && mh < 0x7FF00000; }
 )PLKJITM";
 
 // Host mirror of JMArgs (field order and types must match the prelude).
@@ -173,10 +177,16 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     __builtin_nontemporal_store(V[c_][X_], D_ + (i64)(c_ * S_ + 4 * X_) * kTile); \
   if (SC_ && hi == 0) a.scale[(i64)(slot) * a.n_pad + p] = K; }
 // joint exact power-of-two rescale of the pattern (its states sit in lanes hi = 0..3)
-#define RESCALE(V, K) { double m_ = 0.0; \
-  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) m_ = fmax(m_, V[c_][X_]); \
-  m_ = fmax(m_, __shfl_xor(m_, 16, 64)); m_ = fmax(m_, __shfl_xor(m_, 32, 64)); \
-  if (m_ > 0.0 && m_ < kScaleThr) { \
+// (the hi-word max is the same in the four lanes of a pattern, so a fallback to the f64
+// max runs with all four active)
+#define RESCALE(V, K) { int mh_ = 0; bool up_; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) mh_ = max(mh_, hiw(V[c_][X_])); \
+  mh_ = max(mh_, __shfl_xor(mh_, 16, 64)); mh_ = max(mh_, __shfl_xor(mh_, 32, 64)); \
+  if (__builtin_expect(hi_decides(mh_), 1)) { up_ = mh_ < kThrHi; } else { double m_ = 0.0; \
+    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) m_ = fmax(m_, V[c_][X_]); \
+    m_ = fmax(m_, __shfl_xor(m_, 16, 64)); m_ = fmax(m_, __shfl_xor(m_, 32, 64)); \
+    up_ = m_ > 0.0 && m_ < kScaleThr; } \
+  if (up_) { \
     _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) V[c_][X_] *= kScaleUp; \
     K += 1; } }
 // root reduction (RHomogeneousTreeLikelihood.cpp:162-216 / NH :168-233) and the fixed
