@@ -1228,7 +1228,8 @@ int tree_levels(plk_handle h) {
   switch (fused_kind(h)) {
     case FK_TREE4:
       if (!jit_tree4(h)) return kTree4Levels(tree4_cw(h));
-      return jit_ciw(h) ? env_int("PLK_JIT_CIW_DM", 5, 2, 16) : env_int("PLK_JIT_DM", 10, 2, 32);
+      // classes in the wave: cfg5 DM 5 / 6 / 7 = 0.70 / 0.55 / 0.84 ms at G = 4
+      return jit_ciw(h) ? env_int("PLK_JIT_CIW_DM", 6, 2, 16) : env_int("PLK_JIT_DM", 10, 2, 32);
     case FK_TREES: return env_int("PLK_TREES_DM", 2, 2, 4);
     // S = 20: 3 levels (with cherry tables 7.8 ms on cfg3, 2 levels 8.7 ms although DM = 3
     // spills a few registers at 128 VGPRs)
@@ -1702,11 +1703,12 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // pattern groups per workgroup (they share the staged tables): with per-node rescaling
     // and one class per wave every node has two workgroup barriers, whose cost grows with
     // the waves that meet there (cfg5: 1.93 ms at G = 2, 1.16 ms at G = 1), so one group;
-    // every class in the wave (no barriers, ~104 VGPRs): two (cfg5 0.70 ms; G = 4 0.76,
-    // G = 1 1.46); otherwise the G with the most resident waves (jit_auto_groups; cfg2
-    // with cherry tables: G = 3, 0.207 ms, G = 2 0.222 ms)
+    // every class in the wave (no barriers, ~200 VGPRs, two waves per SIMD): four, one
+    // wave per SIMD per workgroup (cfg5 at DM 6: G = 2 / 3 / 4 / 8 = 0.90 / 0.70 / 0.55 /
+    // 0.60 ms); otherwise the G with the most resident waves (jit_auto_groups; cfg2 with
+    // cherry tables: G = 3, 0.207 ms, G = 2 0.222 ms)
     sh.G = env_int("PLK_JIT_G", 0, 0, 8);
-    if (sh.G == 0) sh.G = h->prog_ciw ? 2 : sh.scale ? 1 : jit_auto_groups(sh);
+    if (sh.G == 0) sh.G = h->prog_ciw ? 4 : sh.scale ? 1 : jit_auto_groups(sh);
     // two patterns per lane halve the P(t) reads per FMA but double the registers:
     // measured slower (cfg2 0.255-0.301 vs 0.241 ms), so opt-in; not with speculation
     sh.PW = env_int("PLK_JIT_PW", 1, 1, 2);
@@ -1720,13 +1722,16 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // speculative no-rescale pass (plk_jit.hpp): a win only where rescaling never
     // fires; on cfg5 it fires in almost every super-block (1.27 vs 1.14 ms), so opt-in
     sh.exact_only = !env_is("PLK_JIT_SPECULATE", '1');
+    // classes in the wave: next class's P(t) loads overlap this class's FMAs (PLK_JIT_PPIPE=0: off)
+    sh.ppipe = !env_is("PLK_JIT_PPIPE", '0');
     if (sh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
     if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW || sh.PW != h->jit_shape.PW ||
         sh.pin != h->jit_shape.pin ||
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
-        sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.exact_only != h->jit_shape.exact_only) {
+        sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.exact_only != h->jit_shape.exact_only ||
+        sh.ppipe != h->jit_shape.ppipe) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;

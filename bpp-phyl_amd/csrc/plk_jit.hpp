@@ -60,21 +60,65 @@ struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
 
 // dst[v][x] (*)= sum_y P_cw[x][y] src[v][y] (P_cw at P + 16 cw, row-major; one P read
 // serves every pattern of the lane); SET: dst was 1
+template <int PW, bool SET, int CW>
+__device__ __forceinline__ void contrib_cls(double (&dst)[4 * CW * PW], const double (&src)[4 * CW * PW],
+                                            const double (&p)[16], int cw) {
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int pw = 0; pw < PW; ++pw) {
+      const int v = 4 * (pw * CW + cw);
+      double s = p[4 * x + 0] * src[v + 0];
+      s = __builtin_fma(p[4 * x + 1], src[v + 1], s);
+      s = __builtin_fma(p[4 * x + 2], src[v + 2], s);
+      s = __builtin_fma(p[4 * x + 3], src[v + 3], s);
+      if (SET) dst[v + x] = s; else dst[v + x] *= s;
+    }
+}
+// P(t) of one class (16 doubles, wave-uniform: scalar loads into SGPRs), and an empty use
+// of it that places the wait for those loads
+__device__ __forceinline__ void pload(double (&r)[16], CPd P) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r[i] = P[i];
+}
+__device__ __forceinline__ void ptouch(const double (&r)[16]) {
+  asm volatile("" ::"s"(r[0]), "s"(r[1]), "s"(r[2]), "s"(r[3]), "s"(r[4]), "s"(r[5]), "s"(r[6]), "s"(r[7]));
+  asm volatile("" ::"s"(r[8]), "s"(r[9]), "s"(r[10]), "s"(r[11]), "s"(r[12]), "s"(r[13]), "s"(r[14]), "s"(r[15]));
+}
 template <int CW, int PW, bool SET>
 __device__ __forceinline__ void contrib(double (&dst)[4 * CW * PW], const double (&src)[4 * CW * PW], CPd P) {
+  if (CW == 1 || !PPIPE_) {
 #pragma unroll
-  for (int cw = 0; cw < CW; ++cw)
+    for (int cw = 0; cw < CW; ++cw) {
+      double p[16];
+      pload(p, P + 16 * cw);
+      contrib_cls<PW, SET, CW>(dst, src, p, cw);
+    }
+    return;
+  }
+  // classes in the wave (PPIPE_): class cw + 1's loads are issued before class cw's
+  // arithmetic and waited for after it.  Scalar loads complete out of order, so every
+  // wait is for all of them: left to itself the compiler loads each class right before
+  // its use and exposes the whole scalar-load latency once per class (cfg5: P loads
+  // ~23 % of the kernel at two waves per SIMD)
+  double pa[16], pb[16];
+  pload(pa, P);
+  ptouch(pa);
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int pw = 0; pw < PW; ++pw) {
-        const int v = 4 * (pw * CW + cw);
-        double s = P[16 * cw + 4 * x + 0] * src[v + 0];
-        s = __builtin_fma(P[16 * cw + 4 * x + 1], src[v + 1], s);
-        s = __builtin_fma(P[16 * cw + 4 * x + 2], src[v + 2], s);
-        s = __builtin_fma(P[16 * cw + 4 * x + 3], src[v + 3], s);
-        if (SET) dst[v + x] = s; else dst[v + x] *= s;
-      }
+  for (int cw = 0; cw < CW; cw += 2) {
+    if (cw + 1 < CW) pload(pb, P + 16 * (cw + 1));
+    __builtin_amdgcn_sched_barrier(0);
+    contrib_cls<PW, SET, CW>(dst, src, pa, cw);
+    __builtin_amdgcn_sched_barrier(0);
+    if (cw + 1 < CW) {
+      ptouch(pb);
+      if (cw + 2 < CW) pload(pa, P + 16 * (cw + 2));
+      __builtin_amdgcn_sched_barrier(0);
+      contrib_cls<PW, SET, CW>(dst, src, pb, cw + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (cw + 2 < CW) ptouch(pa);
+    }
+  }
 }
 
 template <int N, bool SET>
@@ -307,6 +351,7 @@ struct JitShape {
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool same_p = false;  // timing experiments only: every internal branch reads P(t) of node 0
   bool exact_only = true;   // scaling: no speculative no-rescale pass (PLK_JIT_SPECULATE=1 enables it)
+  bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     // the second exchange buffer only serves the per-node rescale
@@ -448,6 +493,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   const int C = sh.C, L = std::max(sh.L, 1), U = sh.U;
   std::string s;
   s.reserve(4096 * events.size() + 16384);
+  s += sh.ppipe ? "#define PPIPE_ 1\n" : "#define PPIPE_ 0\n";  // read by the prelude's contrib
   s += kJitPrelude;
   char buf[400];
   const std::string minw_s = sh.minw > 0 ? ", " + std::to_string(sh.minw) : std::string();
