@@ -121,6 +121,29 @@ __device__ __forceinline__ void contrib(double (&dst)[4 * CW * PW], const double
   }
 }
 
+// Stream form of the pipelined contrib across a fragment's contributions: pbuf[B0] holds
+// this contribution's class 0 (loaded and waited); each class's arithmetic runs while the
+// next class's P(t) -- after the last class, class 0 of the next contribution (Pn, NEXT) --
+// is loading into the other buffer, waited for after the arithmetic.  One exposed wait per
+// fragment instead of one per contribution.
+template <int CW, int PW, bool SET, int B0, bool NEXT>
+__device__ __forceinline__ void contrib_s(double (&dst)[4 * CW * PW], const double (&src)[4 * CW * PW], CPd P,
+                                          CPd Pn, double (&pbuf)[2][16]) {
+#pragma unroll
+  for (int cw = 0; cw < CW; ++cw) {
+    double(&cur)[16] = pbuf[(B0 + cw) & 1];
+    double(&nxt)[16] = pbuf[(B0 + cw + 1) & 1];
+    if (cw + 1 < CW)
+      pload(nxt, P + 16 * (cw + 1));
+    else if (NEXT)
+      pload(nxt, Pn);
+    __builtin_amdgcn_sched_barrier(0);
+    contrib_cls<PW, SET, CW>(dst, src, cur, cw);
+    __builtin_amdgcn_sched_barrier(0);
+    if (cw + 1 < CW || NEXT) ptouch(nxt);
+  }
+}
+
 template <int N, bool SET>
 __device__ __forceinline__ void tipmul(double (&dst)[N], const double (&row)[N]) {
 #pragma unroll
@@ -723,8 +746,36 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     // check raises `dng` when its own-class max is below the threshold -- the joint
     // max can then be below it too; otherwise the joint max is >= the threshold at
     // every check, no rescale would happen, and this pass IS the exact result.
+    // classes in the wave with pipelined P(t): the fragment's contributions form one
+    // stream of class loads (contrib_s), the first loaded ahead of the body
+    const bool pstream = sh.ppipe && CW > 1;
+    std::vector<size_t> cev;  // events with a contribution, in order
+    for (size_t i = 0; i < ev.size(); ++i)
+      if (ev[i].op == T_LOAD || ev[i].op == T_ASCEND) cev.push_back(i);
     auto emit_body = [&](bool exact) {
       s += "      kzero(K0);\n";
+      size_t kc = 0;   // contributions emitted
+      int pbase = 0;   // buffer of the next contribution's class 0
+      if (pstream && !cev.empty()) {
+        snprintf(buf, sizeof(buf), "      double pbuf[2][16]; pload(pbuf[0], %s); ptouch(pbuf[0]);\n",
+                 pref(cev[0]).c_str());
+        s += buf;
+      }
+      auto contrib_line = [&](size_t i, const char* set, const std::string& dst, const std::string& src) {
+        const std::string pr = pref(i);
+        if (!pstream) {
+          snprintf(buf, sizeof(buf), "      contrib<CW_, PW_, %s>(%s, %s, %s);\n", set, dst.c_str(), src.c_str(),
+                   pr.c_str());
+        } else {
+          const bool next = kc + 1 < cev.size();
+          const std::string pn = next ? pref(cev[kc + 1]) : pr;
+          snprintf(buf, sizeof(buf), "      contrib_s<CW_, PW_, %s, %d, %s>(%s, %s, %s, %s, pbuf);\n", set, pbase,
+                   next ? "true" : "false", dst.c_str(), src.c_str(), pr.c_str(), pn.c_str());
+          pbase = (pbase + CW) & 1;
+        }
+        ++kc;
+        s += buf;
+      };
       std::vector<char> fresh((size_t)max_level + 1, 0);
       fresh[0] = 1;
       size_t nf = 0;
@@ -762,12 +813,10 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
               s += buf;
               snprintf(buf, sizeof(buf), "      KTF(K%d, %d, Q%d)\n", e.level, u.koff, slot[i]);
             }
+            s += buf;
           } else {
-            const std::string pr = pref(i);
-            snprintf(buf, sizeof(buf), "      contrib<CW_, PW_, %s>(A%d, F%d, %s);\n", set, e.level, slot[i],
-                     pr.c_str());
+            contrib_line(i, set, "A" + std::to_string(e.level), "F" + std::to_string(slot[i]));
           }
-          s += buf;
           if (sh.pin) {
             snprintf(buf, sizeof(buf), "      pin(A%d);\n", e.level);
             s += buf;
@@ -791,10 +840,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
               s += buf;
             }
           }
-          const std::string pr = pref(i);
-          snprintf(buf, sizeof(buf), "      contrib<CW_, PW_, %s>(A%d, A%d, %s);\n", fresh[(size_t)dd - 1] ? "true" : "false",
-                   dd - 1, dd, pr.c_str());
-          s += buf;
+          contrib_line(i, fresh[(size_t)dd - 1] ? "true" : "false", "A" + std::to_string(dd - 1),
+                       "A" + std::to_string(dd));
           if (sh.pin) {
             snprintf(buf, sizeof(buf), "      pin(A%d);\n", dd - 1);
             s += buf;
