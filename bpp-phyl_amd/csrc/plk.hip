@@ -107,6 +107,7 @@ struct plk_handle_s {
   int64_t n_launches = 0, n_table_launches = 0;
   double acc_ms[4] = {0, 0, 0, 0};
   int jit_last_gx = 0;                    // workgroups per fragment of the last JIT launch
+  std::vector<int> jit_frag_gx;           // workgroups per fragment of the last JIT traversal (per fragment)
   std::string last_error;
   // host copy of the op list last uploaded to d_ops (re-used when identical)
   std::vector<KOp> h_ops;
@@ -1703,20 +1704,21 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // pattern groups per workgroup (they share the staged tables): with per-node rescaling
     // and one class per wave every node has two workgroup barriers, whose cost grows with
     // the waves that meet there (cfg5: 1.93 ms at G = 2, 1.16 ms at G = 1), so one group;
-    // every class in the wave (no barriers, ~200 VGPRs, two waves per SIMD): four, one
-    // wave per SIMD per workgroup (cfg5 at DM 6: G = 2 / 3 / 4 / 8 = 0.90 / 0.70 / 0.55 /
-    // 0.60 ms); otherwise the G with the most resident waves (jit_auto_groups; cfg2 with
-    // cherry tables: G = 3, 0.207 ms, G = 2 0.222 ms)
+    // every class in the wave (no barriers, ~230 VGPRs, two waves per SIMD): eight, the
+    // whole CU's resident waves in one workgroup that stages the tables once (cfg5 at DM 6
+    // with the tier's fragments side by side: G = 6 / 7 / 8 = 0.48 / 0.43 / 0.39 ms);
+    // otherwise the G with the most resident waves (jit_auto_groups; cfg2 with cherry
+    // tables: G = 3, 0.140 ms, G = 2 0.150, G = 4 0.162)
     sh.G = env_int("PLK_JIT_G", 0, 0, 8);
-    if (sh.G == 0) sh.G = h->prog_ciw ? 4 : sh.scale ? 1 : jit_auto_groups(sh);
+    if (sh.G == 0) sh.G = h->prog_ciw ? 8 : sh.scale ? 1 : jit_auto_groups(sh);
     // two patterns per lane halve the P(t) reads per FMA but double the registers:
     // measured slower (cfg2 0.255-0.301 vs 0.241 ms), so opt-in; not with speculation
     sh.PW = env_int("PLK_JIT_PW", 1, 1, 2);
     if (sh.G * sh.PW > 4 || h->n_pad % (64 * sh.G * sh.PW) != 0 || env_is("PLK_JIT_SPECULATE", '1')) sh.PW = 1;
     // two-stage pipeline, codes / HBM loads 3 ahead (cfg2 0.274 -> 0.259 ms); with every
-    // class in the wave a ring slot is C x larger, so there one event ahead (cfg5 1.04 ms
-    // at L = 1, 1.48 ms at L = 3)
-    sh.L = env_int("PLK_JIT_L", h->prog_ciw ? 1 : 3, 1, 8);
+    // class in the wave a ring slot is C x larger, so there two events ahead (cfg5 0.385 ms
+    // at L = 2, 0.391 at L = 1; 1.48 vs 1.04 ms at L = 3 vs 1 before the P(t) stream)
+    sh.L = env_int("PLK_JIT_L", h->prog_ciw ? 2 : 3, 1, 8);
     sh.minw = env_int("PLK_JIT_MINW", 0, 0, 8);
     sh.same_p = env_is("PLK_DEBUG_SAMEP", '1');
     // speculative no-rescale pass (plk_jit.hpp): a win only where rescaling never
@@ -1817,10 +1819,16 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
           HIPCHK(h, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, h->device));
           h->jit_resident = std::max(1, per_cu) * std::max(1, n_cu);
         }
-        wgs = h->jit_resident;
+        // every fragment of the tier at once: the resident workgroups split over the
+        // fragments (each stages its fragment's tables once and walks many super-blocks)
+        // instead of the tier's fragments running one after another with every workgroup
+        // staging tables for a few super-blocks (PLK_JIT_SPLIT_Y=0: the latter)
+        wgs = env_is("PLK_JIT_SPLIT_Y", '0') ? h->jit_resident : std::max(1, h->jit_resident / (int)grid.y);
       }
       const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, wgs);
       h->jit_last_gx = (int)gx;
+      if ((int)h->jit_frag_gx.size() < h->prog_nf) h->jit_frag_gx.resize((size_t)h->prog_nf, 0);
+      for (int k = 0; k < (int)t.size(); ++k) h->jit_frag_gx[(size_t)(first + k)] = (int)gx;
       HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
                                       (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
@@ -2355,17 +2363,19 @@ void traversal_work(plk_handle h, plk_work* w) {
           fresh[d - 1] = 0;
         }
       }
+      // every workgroup of the fragment builds its tables
+      const int gx = f < h->jit_frag_gx.size() && h->jit_frag_gx[f] > 0 ? h->jit_frag_gx[f] : std::max(h->jit_last_gx, 1);
       for (const JitUnit& u : h->jit_plan.units[f]) {
         if (u.tb < 0) continue;
         tnodes++;
         rows += (int64_t)U * U * C;
-        tab += (double)C * U * U * (S + (u.br >= 0 ? (double)S * (2 * S - 1) : 0.0));
+        tab += (double)gx * C * U * U * (S + (u.br >= 0 ? (double)S * (2 * S - 1) : 0.0));
       }
     }
     w->useful_flops = w->issued_flops = per * C * P;
     w->table_nodes = tnodes;
     w->table_rows = rows;
-    w->table_flops = tab * std::max(h->jit_last_gx, 1);
+    w->table_flops = tab;
     w->node_updates = h->n_patterns * (int64_t)(w->internal_nodes - tnodes);
     w->exact = 1;
     return;
