@@ -193,8 +193,13 @@ def roofline(wl, mode, P, ev_steps, tm, work, traffic):
         # the fused traversal writing every partial: children come from registers, so the
         # bytes are the writes (8*C*S per internal node) plus codes, weight and site lnL
         alg_bytes = (8 * wl.C * wl.S * wl.et.n_internal + wl.et.n_tips + 16) * P
+    subtree = mode == "subtree"
+    if subtree and traffic:
+        # per-subtree compression: the work is the distinct patterns per node, which depends
+        # on the data, so the bytes the compressed traversal moves (PMC) are the basis
+        alg_bytes = traffic
     if traffic:
-        compute_bound = alg_flops / traffic > RIDGE
+        compute_bound = alg_flops / traffic > RIDGE and not subtree
     else:
         compute_bound = fused
     ex = None
@@ -220,6 +225,11 @@ def roofline(wl, mode, P, ev_steps, tm, work, traffic):
         main = {"bound": "hbm", "achieved": alg_bytes / t_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "basis": (f"algorithmic {alg_bytes / P:.0f} B/pattern/traversal x {P} patterns / traversal time "
                           f"({launches:.0f} launch(es), HIP events)")}
+        if subtree and traffic:
+            main["basis"] = (f"bytes the compressed traversal moves ({alg_bytes / P:.0f} B/pattern, PMC "
+                             f"FETCH/WRITE) / traversal time ({launches:.0f} launch(es), HIP events); the "
+                             f"uncompressed basis ({bytes_pattern} B/pattern) would exceed the HBM peak -- "
+                             f"compression skips that work, see value (effective)")
     main["frac"] = main["achieved"] / main["peak"]
     main["traffic"] = traffic
     main["traversal_ms"] = t_s * 1e3

@@ -17,7 +17,8 @@ import sys
 from collections import OrderedDict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PARTIALS = ("tree4_kernel", "treeS_kernel", "treeM_kernel", "partials_", "plk_jit_tree4", "cherry_table_kernel")  # partials_links_ included
+PARTIALS = ("tree4_kernel", "treeS_kernel", "treeM_kernel", "partials_", "plk_jit_tree4", "plk_jit_treeM",
+            "cherry_table_kernel")  # partials_links_ included
 
 
 def rows(d):
