@@ -104,12 +104,17 @@ struct JitMShape {
   bool direct = false;  // A operands straight from P(t) in L1/L2 (no LDS staging, no barriers)
   int pd = 1;           // P(t) staging prefetch distance (contractions ahead)
   bool hoist = false;   // cherry codes of the whole fragment loaded at its start
+  bool youter = false;  // contraction order: independent chains interleaved block by block
+  bool padstage = false; // P staging: padded LDS stride, unconditional stores (cfg3 3.93 vs 3.51 ms: off)
   static constexpr int G = 4;  // waves (16-pattern groups) per workgroup: 64 patterns
-  int pb() const { return C * S * S; }  // doubles per P buffer (every class of one branch)
-  size_t lds_bytes() const { return (size_t)((direct ? 0 : 2 * pb()) + 64) * sizeof(double); }
+  int pb() const { return C * S * S; }  // doubles of P(t) per branch (every class)
+  // LDS stride of a P buffer: every staging element of the workgroup has a slot (the
+  // elements past pb() land in the padding), so the staging stores need no condition
+  int pbs() const { return padstage ? (pb() + 64 * G - 1) / (64 * G) * (64 * G) : pb(); }
+  size_t lds_bytes() const { return (size_t)((direct ? 0 : 2 * pbs()) + 64) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
     return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && direct == o.direct &&
-           pd == o.pd && hoist == o.hoist;
+           pd == o.pd && hoist == o.hoist && youter == o.youter && padstage == o.padstage;
   }
 };
 
@@ -122,25 +127,35 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   s.reserve(65536 * std::max<size_t>(starts.size(), 1));
   s += kJitMPrelude;
   char buf[512];
-  const int NTH = 64 * JitMShape::G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH;
+  const int NTH = 64 * JitMShape::G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH, PBS = sh.pbs();
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
-           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n#define DIRECT_ %d\n",
-           S, C, XB, sh.U, sh.U * sh.U, JitMShape::G, NTH, PB, PF, sh.scale ? "true" : "false", sh.direct ? 1 : 0);
+           "#define NTH_ %d\n#define PB_ %d\n#define PBS_ %d\n#define PF_ %d\n#define SC_ %s\n#define DIRECT_ %d\n#define YOUTER_ %d\n",
+           S, C, XB, sh.U, sh.U * sh.U, JitMShape::G, NTH, PB, PBS, PF, sh.scale ? "true" : "false", sh.direct ? 1 : 0,
+           sh.youter ? 1 : 0);
   s += buf;
   s += R"PLKJITM(
 // P(t) of branch b (all classes, [c][x][y]) -> registers -> the LDS tile image
 // [c][X][Y][hi][lo] with tile element (hi, lo) = P[4X + lo][4Y + hi]
 #define PSTAGE_LOAD(R, b) { const double* s_ = a.pmats + (i64)(b) * PB_; \
   _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) { const int e_ = tid + j_ * NTH_; R[j_] = s_[e_ < PB_ ? e_ : PB_ - 1]; } }
-#define PSTAGE_STORE(R, bf) { double* d_ = lds + (bf) * PB_; \
-  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) if (sidx[j_] >= 0) d_[sidx[j_]] = R[j_]; }
+#define PSTAGE_STORE(R, bf) { double* d_ = lds + (bf) * PBS_; \
+  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) if (PBS_ > PB_ || sidx[j_] >= 0) d_[sidx[j_]] = R[j_]; }
 // D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1)
-#define CONTRIB(D, SRC, bf, SET) { const double* P_ = PA + (bf) * PB_; \
+// (YOUTER_: the C * XB independent chains advance one block at a time, so consecutive MFMAs
+// never depend on each other; the same sums in the same order either way)
+#define CONTRIB(D, SRC, bf, SET) { const double* P_ = PA + (bf) * PBS_; \
+  if (YOUTER_) { double d_[C_][XB_]; \
+    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) \
+      _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
+        d_[c_][X_] = mfma4(P_[((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], Y_ == 0 ? 0.0 : d_[c_][X_]); \
+    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
+      if (SET) D[c_][X_] = d_[c_][X_]; else D[c_][X_] *= d_[c_][X_]; } \
+  } else { \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
     double d_ = 0.0; \
     _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) d_ = mfma4(P_[((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
-    if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } }
+    if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } } }
 // direct: A(c, X, Y) = P[c][4X + lo][4Y + hi] read from the branch's P(t) in global memory
 #define CONTRIB_G(D, SRC, b, SET) { const double* P_ = PG + (i64)(b) * PB_; \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
@@ -214,8 +229,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
            "extern \"C\" __global__ __launch_bounds__(%d, %d) void plk_jit_treeM(JMArgs a, int frag_base) {\n", NTH,
            std::max(sh.minw, 1));
   s += buf;
-  s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PB_] P tiles | red[64]
-  double* red = lds + (DIRECT_ ? 0 : 2 * PB_);
+  s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PBS_] P tiles | red[64]
+  double* red = lds + (DIRECT_ ? 0 : 2 * PBS_);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 4, pl = lane & 15;
@@ -224,11 +239,11 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const i64 toff = (p >> 7) * (i64)(C_ * S_ * kTile) + (p & (kTile - 1)) + (i64)hi * kTile;
   const double* PA = lds + ((hi << 2) | (lane & 3));
   const double* PG = a.pmats + (lane & 3) * S_ + hi;   // direct A operands: P[..][4X + lo][4Y + hi]
-  int sidx[PF_];   // this thread's staging elements -> tile slots (-1: past the table)
+  int sidx[PF_];   // this thread's staging elements -> tile slots (past the table: padding)
   _Pragma("unroll") for (int j = 0; j < PF_; ++j) {
     const int e = tid + j * NTH_;
     const int c = e / (S_ * S_), r = e - c * (S_ * S_), x = r / S_, y = r - x * S_;
-    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3) : -1;
+    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3) : PBS_ > PB_ ? e : -1;
   }
   double R0[PF_], R1[PF_], R2[PF_];
   (void)red; (void)PA; (void)PG; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
