@@ -1721,6 +1721,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.L = env_int("PLK_JIT_L", h->prog_ciw ? 2 : 3, 1, 8);
     sh.minw = env_int("PLK_JIT_MINW", 0, 0, 8);
     sh.same_p = env_is("PLK_DEBUG_SAMEP", '1');
+    sh.stage_only = env_int("PLK_DEBUG_STAGE_ONLY", 0, 0, 2);
     // speculative no-rescale pass (plk_jit.hpp): a win only where rescaling never
     // fires; on cfg5 it fires in almost every super-block (1.27 vs 1.14 ms), so opt-in
     sh.exact_only = !env_is("PLK_JIT_SPECULATE", '1');
@@ -1732,7 +1733,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.pin != h->jit_shape.pin ||
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
-        sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.exact_only != h->jit_shape.exact_only ||
+        sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.stage_only != h->jit_shape.stage_only || sh.exact_only != h->jit_shape.exact_only ||
         sh.ppipe != h->jit_shape.ppipe) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;

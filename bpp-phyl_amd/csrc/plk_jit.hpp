@@ -373,6 +373,7 @@ struct JitShape {
   int L = 1;        // operand fetch lookahead (events)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool same_p = false;  // timing experiments only: every internal branch reads P(t) of node 0
+  int stage_only = 0;  // timing experiments only: return after staging the tables (1) / at once (2)
   bool exact_only = true;   // scaling: no speculative no-rescale pass (PLK_JIT_SPECULATE=1 enables it)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
   size_t lds_bytes() const {
@@ -517,6 +518,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   std::string s;
   s.reserve(4096 * events.size() + 16384);
   s += sh.ppipe ? "#define PPIPE_ 1\n" : "#define PPIPE_ 0\n";  // read by the prelude's contrib
+  s += "#define STAGE_ONLY_ " + std::to_string(sh.stage_only) + "\n";
   s += kJitPrelude;
   char buf[400];
   const std::string minw_s = sh.minw > 0 ? ", " + std::to_string(sh.minw) : std::string();
@@ -564,6 +566,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c0 = (w % NW_) * CW_, g = w / NW_;
+  if (STAGE_ONLY_ == 2) return;
   const int frag = frag_base + (int)blockIdx.y;
   const int u0 = 1 + kFragUnitStart[frag], nu = kFragUnitStart[frag + 1] - kFragUnitStart[frag];
   // tables: wave w stages units w, w + NWT_, ... (one dependent chain per unit and wave,
@@ -622,6 +625,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       }
     }
   }
+  if (STAGE_ONLY_) return;
   const CPd pm = (CPd)(pmats + c0 * 16);
   const double* trow = tab + c0 * (U_ * 4);         // single-tip units
   const double* trow2 = tab + c0 * (U_ * U_ * 4);   // pair units
