@@ -2933,16 +2933,31 @@ namespace {
 // global lnL of a communicator run: every rank's block sums in rank order (ranks hold
 // consecutive pattern ranges), each rank's in block order -- the same sequence of adds as
 // one process over all patterns; this rank's own block sums are copied to the mapped host
-// buffer beside it
+// buffer beside it.  The sequence is one dependent chain of adds, so the workgroup stages
+// the block sums in LDS (coalesced, in chunks) and one thread runs the chain from LDS: the
+// loads leave the chain (a thread walking global memory paid a load latency per add --
+// ~20 us per evaluation at one rank, 8x that at eight)
+constexpr int kCommChunk = 4096;
 __global__ void comm_sum_kernel(const double* __restrict__ all, const int64_t* __restrict__ counts, int n_ranks,
                                 int64_t cmax, const double* __restrict__ local, int64_t n_local,
                                 double* __restrict__ local_out, double* __restrict__ total_out) {
-  if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int r = 0; r < n_ranks; ++r)
-      for (int64_t b = 0; b < counts[r]; ++b) s += all[(int64_t)r * cmax + b];
-    *total_out = s;
+  __shared__ double buf[kCommChunk];
+  double s = 0.0;
+  for (int r = 0; r < n_ranks; ++r) {
+    const int64_t n = counts[r];
+    const double* src = all + (int64_t)r * cmax;
+    for (int64_t b0 = 0; b0 < n; b0 += kCommChunk) {
+      const int m = (int)(n - b0 < kCommChunk ? n - b0 : kCommChunk);
+      __syncthreads();  // the previous chunk is summed
+      for (int i = threadIdx.x; i < m; i += blockDim.x) buf[i] = src[b0 + i];
+      __syncthreads();
+      if (threadIdx.x == 0) {
+#pragma unroll 16
+        for (int i = 0; i < m; ++i) s += buf[i];
+      }
+    }
   }
+  if (threadIdx.x == 0) *total_out = s;
   for (int64_t i = threadIdx.x; i < n_local; i += blockDim.x) local_out[i] = local[i];
 }
 
