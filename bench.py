@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="gtr_g4_dna_1M_64", choices=sorted(workload.CONFIGS))
     ap.add_argument("--patterns", type=int, default=None, help="override patterns per rank")
+    ap.add_argument("--classes", type=int, default=None,
+                    help="A/B experiments only: the config's model with this many Gamma classes")
     ap.add_argument("--cpu-sample", type=int, default=None, help="patterns in the CPU-baseline sample")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU-baseline traversals per variant (median, after 1 warm-up)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -269,7 +271,7 @@ def main():
     device = local if use_dist and not rehearse else 0
     coll_dev = "cpu" if rehearse else "cuda"
 
-    wl = workload.make_workload(args.config)
+    wl = workload.make_workload(args.config, n_classes=args.classes)
     P = args.patterns or wl.n_patterns
     wl.n_patterns = P
     start, end = rank * P, (rank + 1) * P

@@ -1770,6 +1770,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.hoist = env_int("PLK_JITM_HOIST", 0, 0, 1) != 0;
     msh.youter = env_is("PLK_JITM_YOUTER", '1');
     msh.padstage = env_is("PLK_JITM_PADSTAGE", '1');
+    msh.hyb = env_is("PLK_JITM_HYB", '1');
     if (msh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "jit_treeM needs %zu B of LDS", msh.lds_bytes());
     if (!h->jitm_fn || !(msh == h->jitm_shape)) {

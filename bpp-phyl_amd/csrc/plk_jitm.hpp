@@ -65,6 +65,10 @@ struct JMArgs {
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f64x4 mfma16(double a, double b, f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
 __device__ __attribute__((noinline)) double jitm_log(double x) { return log(x); }
 // rescale decision from the doubles' high words (see plk_jit.hpp hiw / hi_decides)
 #define kThrHi 0x2FF00000
@@ -106,6 +110,9 @@ struct JitMShape {
   bool hoist = false;   // cherry codes of the whole fragment loaded at its start
   bool youter = false;  // contraction order: independent chains interleaved block by block
   bool padstage = false; // P staging: padded LDS stride, unconditional stores (cfg3 3.93 vs 3.51 ms: off)
+  bool hyb = false;     // 20 states: 16x16x4 for states 0..15 + 4x4x4 for 16..19 (CONTRIB, HYB_;
+                        // cfg3 4.37 vs 3.56 ms all-4x4x4, so off)
+  bool hybrid() const { return hyb && S == 20 && !direct; }
   static constexpr int G = 4;  // waves (16-pattern groups) per workgroup: 64 patterns
   int pb() const { return C * S * S; }  // doubles of P(t) per branch (every class)
   // LDS stride of a P buffer: every staging element of the workgroup has a slot (the
@@ -114,7 +121,7 @@ struct JitMShape {
   size_t lds_bytes() const { return (size_t)((direct ? 0 : 2 * pbs()) + 64) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
     return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && direct == o.direct &&
-           pd == o.pd && hoist == o.hoist && youter == o.youter && padstage == o.padstage;
+           pd == o.pd && hoist == o.hoist && youter == o.youter && padstage == o.padstage && hyb == o.hyb;
   }
 };
 
@@ -130,9 +137,10 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const int NTH = 64 * JitMShape::G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH, PBS = sh.pbs();
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
-           "#define NTH_ %d\n#define PB_ %d\n#define PBS_ %d\n#define PF_ %d\n#define SC_ %s\n#define DIRECT_ %d\n#define YOUTER_ %d\n",
+           "#define NTH_ %d\n#define PB_ %d\n#define PBS_ %d\n#define PF_ %d\n#define SC_ %s\n#define DIRECT_ %d\n#define YOUTER_ %d\n"
+           "#define HYB_ %d\n",
            S, C, XB, sh.U, sh.U * sh.U, JitMShape::G, NTH, PB, PBS, PF, sh.scale ? "true" : "false", sh.direct ? 1 : 0,
-           sh.youter ? 1 : 0);
+           sh.youter ? 1 : 0, sh.hybrid() ? 1 : 0);
   s += buf;
   s += R"PLKJITM(
 // P(t) of branch b (all classes, [c][x][y]) -> registers -> the LDS tile image
@@ -144,8 +152,21 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
 // D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1)
 // (YOUTER_: the C * XB independent chains advance one block at a time, so consecutive MFMAs
 // never depend on each other; the same sums in the same order either way)
+// HYB_ (20 states): states 0..15 of the output on v_mfma_f64_16x16x4 (A = the 16 x 4 tile
+// P[x][4Y + k], lane l holding x = l % 16, k = l / 16: 64 distinct values per 2048 flops) and
+// states 16..19 on v_mfma_f64_4x4x4_4b -- 4x fewer A operands per flop than all-4x4x4; the
+// 16x16 D registers q = 0..3 hold states 4q + hi, exactly the layout of blocks X = 0..3,
+// and the 4x4x4 D the layout of X = 4.  Image per class: 5 tiles of 64, then 5 of 16.
 #define CONTRIB(D, SRC, bf, SET) { const double* P_ = PA + (bf) * PBS_; \
-  if (YOUTER_) { double d_[C_][XB_]; \
+  if (HYB_) { const double* Q_ = PA16 + (bf) * PBS_; f64x4 h_[C_]; double l_[C_]; \
+    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { h_[c_] = (f64x4){0.0, 0.0, 0.0, 0.0}; l_[c_] = 0.0; } \
+    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { \
+      h_[c_] = mfma16(Q_[c_ * (S_ * S_) + Y_ * 64], SRC[c_][Y_], h_[c_]); \
+      l_[c_] = mfma4(P_[c_ * (S_ * S_) + 320 + Y_ * 16], SRC[c_][Y_], l_[c_]); } \
+    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { \
+      if (SET) { D[c_][0] = h_[c_][0]; D[c_][1] = h_[c_][1]; D[c_][2] = h_[c_][2]; D[c_][3] = h_[c_][3]; D[c_][4] = l_[c_]; } \
+      else { D[c_][0] *= h_[c_][0]; D[c_][1] *= h_[c_][1]; D[c_][2] *= h_[c_][2]; D[c_][3] *= h_[c_][3]; D[c_][4] *= l_[c_]; } } \
+  } else if (YOUTER_) { double d_[C_][XB_]; \
     _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) \
       _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
         d_[c_][X_] = mfma4(P_[((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], Y_ == 0 ? 0.0 : d_[c_][X_]); \
@@ -238,15 +259,18 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const i64 p = p0 + 16 * w + pl;
   const i64 toff = (p >> 7) * (i64)(C_ * S_ * kTile) + (p & (kTile - 1)) + (i64)hi * kTile;
   const double* PA = lds + ((hi << 2) | (lane & 3));
+  const double* PA16 = lds + lane;  // HYB_: 16x16x4 A tiles, one element per lane
   const double* PG = a.pmats + (lane & 3) * S_ + hi;   // direct A operands: P[..][4X + lo][4Y + hi]
   int sidx[PF_];   // this thread's staging elements -> tile slots (past the table: padding)
   _Pragma("unroll") for (int j = 0; j < PF_; ++j) {
     const int e = tid + j * NTH_;
     const int c = e / (S_ * S_), r = e - c * (S_ * S_), x = r / S_, y = r - x * S_;
-    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3) : PBS_ > PB_ ? e : -1;
+    const int t_ = HYB_ ? c * (S_ * S_) + (x < 16 ? (y >> 2) * 64 + (y & 3) * 16 + x : 320 + (y >> 2) * 16 + (y & 3) * 4 + (x - 16))
+                        : ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3);
+    sidx[j] = e < PB_ ? t_ : PBS_ > PB_ ? e : -1;
   }
   double R0[PF_], R1[PF_], R2[PF_];
-  (void)red; (void)PA; (void)PG; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
+  (void)red; (void)PA; (void)PA16; (void)PG; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
   const int frag = frag_base + (int)blockIdx.y;
 )PLKJITM";
   // accumulators per register level and the operand ring

@@ -115,8 +115,14 @@ CONFIGS = {
 }
 
 
-def make_workload(name: str, n_patterns: Optional[int] = None, seed: int = 42) -> Workload:
-    cfg = CONFIGS[name]
+def make_workload(name: str, n_patterns: Optional[int] = None, seed: int = 42,
+                  n_classes: Optional[int] = None) -> Workload:
+    """n_classes: A/B experiments only -- the config's model with another Gamma class count."""
+    cfg = dict(CONFIGS[name])
+    if n_classes is not None:
+        cfg["C"] = n_classes
+        if cfg["alpha"] is None:
+            cfg["alpha"] = 1.0
     tree = phylo.balanced_tree(cfg["n_taxa"], seed=seed)
     rates, probs = phylo.gamma_rates(cfg["C"], cfg["alpha"]) if cfg["C"] > 1 else (np.ones(1), np.ones(1))
     P = cfg["n_patterns"] if n_patterns is None else n_patterns

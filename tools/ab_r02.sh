@@ -88,5 +88,17 @@ case "$1" in
       ( export TMPDIR=/tmp; cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES \
         SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE \
         --output-format csv -d $O/a -o run -- python3 $R/bench.py --config $C3 --no-cpu-baseline --steps 2 --warmup 1 > /dev/null ) ;;
+  z)  # cfg3 register pressure: the same tree and model with 1 / 2 / 4 rate classes (fp64 fraction per class count)
+      O=gpurun_out/r2z; mkdir -p $O
+      for spec in "c1:1:" "c2:2:" "c2w3:2:PLK_JITM_MINW=3" "c2dm5:2:PLK_JITM_DM=5" "c4:4:"; do
+        IFS=: read name cls envs <<< "$spec"
+        env $(echo $envs | tr ',' ' ') timeout -k 10 200 python bench.py --config $C3 --classes $cls --steps 10 --warmup 2 \
+          --no-cpu-baseline > $O/$name.json 2> $O/$name.err || { tail -5 $O/$name.err; exit 1; }
+        python -c "import json; d=json.load(open('$O/$name.json')); r=d['roofline']; print('$name', d['kernel_path'], 'ms %.4f' % r['traversal_ms'], 'frac %.3f' % r['frac'], 'exec %.3f' % r['executed']['frac'])"
+      done ;;
+  hyb)  # 20 states: hybrid 16x16x4 + 4x4x4 contraction vs all-4x4x4
+      PLK_JITM_HYB=1 $T r2hyb -k "jit_treeM or bench_mode" quick || exit 1
+      $S r2hyb $C3 "hyb:PLK_JITM_HYB=1" "nohyb:" "hyb_dm3:PLK_JITM_HYB=1,PLK_JITM_DM=3" "hyb_dm5:PLK_JITM_HYB=1,PLK_JITM_DM=5" \
+        "hyb_l2:PLK_JITM_HYB=1,PLK_JITM_L=2" ;;
   *)  echo "usage: tools/ab_r02.sh <a..y>"; exit 2 ;;
 esac
