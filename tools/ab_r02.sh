@@ -100,5 +100,13 @@ case "$1" in
       PLK_JITM_HYB=1 $T r2hyb -k "jit_treeM or bench_mode" quick || exit 1
       $S r2hyb $C3 "hyb:PLK_JITM_HYB=1" "nohyb:" "hyb_dm3:PLK_JITM_HYB=1,PLK_JITM_DM=3" "hyb_dm5:PLK_JITM_HYB=1,PLK_JITM_DM=5" \
         "hyb_l2:PLK_JITM_HYB=1,PLK_JITM_L=2" ;;
+  pyov)  # Python-side evaluate overhead (cached ctypes pointers): step time of the default bench lines
+      $T r2pyov -k "multi or bench_mode or comm or evaluate" quick || exit 1
+      for c in $C2 $C5; do timeout -k 10 200 python bench.py --config $c --steps 40 --warmup 3 --no-cpu-baseline > gpurun_out/r2pyov_$c.json || exit 1
+        python -c "import json; d=json.load(open('gpurun_out/r2pyov_$c.json')); print('$c', '%.4e' % d['value'], 'ms/step %.4f' % d['ms_per_step'], 'kernel %.4f' % d['kernel_ms_per_step']['partials'])"; done ;;
+  hiptrace)  # host-side timeline of the evaluation loop (HIP API + kernels)
+      R=$(pwd); O=$R/gpurun_out/r2hiptrace; mkdir -p $O
+      ( export TMPDIR=/tmp; cd /tmp && timeout -k 10 200 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $O -o run -- \
+        python3 $R/bench.py --steps 12 --warmup 2 --no-cpu-baseline --no-events > $O/bench.json ) ;;
   *)  echo "usage: tools/ab_r02.sh <a..y>"; exit 2 ;;
 esac
