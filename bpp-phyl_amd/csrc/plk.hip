@@ -1771,6 +1771,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.youter = env_is("PLK_JITM_YOUTER", '1');
     msh.padstage = env_is("PLK_JITM_PADSTAGE", '1');
     msh.hyb = env_is("PLK_JITM_HYB", '1');
+    msh.debug = env_int("PLK_DEBUG_JITM", 0, 0, 7);
     if (msh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "jit_treeM needs %zu B of LDS", msh.lds_bytes());
     if (!h->jitm_fn || !(msh == h->jitm_shape)) {

@@ -110,6 +110,8 @@ struct JitMShape {
   bool hoist = false;   // cherry codes of the whole fragment loaded at its start
   bool youter = false;  // contraction order: independent chains interleaved block by block
   bool padstage = false; // P staging: padded LDS stride, unconditional stores (cfg3 3.93 vs 3.51 ms: off)
+  int debug = 0;        // timing experiments only (wrong results): bit 1 no P(t) staging barrier, bit 2 no
+                        // P(t) loads, bit 4 one A operand read per class and contraction
   bool hyb = false;     // 20 states: 16x16x4 for states 0..15 + 4x4x4 for 16..19 (CONTRIB, HYB_;
                         // cfg3 4.37 vs 3.56 ms all-4x4x4, so off)
   bool hybrid() const { return hyb && S == 20 && !direct; }
@@ -121,7 +123,8 @@ struct JitMShape {
   size_t lds_bytes() const { return (size_t)((direct ? 0 : 2 * pbs()) + 64) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
     return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && direct == o.direct &&
-           pd == o.pd && hoist == o.hoist && youter == o.youter && padstage == o.padstage && hyb == o.hyb;
+           pd == o.pd && hoist == o.hoist && youter == o.youter && padstage == o.padstage && hyb == o.hyb &&
+           debug == o.debug;
   }
 };
 
@@ -138,9 +141,9 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
            "#define NTH_ %d\n#define PB_ %d\n#define PBS_ %d\n#define PF_ %d\n#define SC_ %s\n#define DIRECT_ %d\n#define YOUTER_ %d\n"
-           "#define HYB_ %d\n",
+           "#define HYB_ %d\n#define DBGA_ %d\n",
            S, C, XB, sh.U, sh.U * sh.U, JitMShape::G, NTH, PB, PBS, PF, sh.scale ? "true" : "false", sh.direct ? 1 : 0,
-           sh.youter ? 1 : 0, sh.hybrid() ? 1 : 0);
+           sh.youter ? 1 : 0, sh.hybrid() ? 1 : 0, (sh.debug & 4) ? 1 : 0);
   s += buf;
   s += R"PLKJITM(
 // P(t) of branch b (all classes, [c][x][y]) -> registers -> the LDS tile image
@@ -175,7 +178,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   } else { \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
     double d_ = 0.0; \
-    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) d_ = mfma4(P_[((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
+    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) \
+      d_ = mfma4(P_[DBGA_ ? c_ * (XB_ * XB_ * 16) : ((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
     if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } } }
 // direct: A(c, X, Y) = P[c][4X + lo][4Y + hi] read from the branch's P(t) in global memory
 #define CONTRIB_G(D, SRC, b, SET) { const double* P_ = PG + (i64)(b) * PB_; \
@@ -269,7 +273,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
                         : ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3);
     sidx[j] = e < PB_ ? t_ : PBS_ > PB_ ? e : -1;
   }
-  double R0[PF_], R1[PF_], R2[PF_];
+  double R0[PF_] = {}, R1[PF_] = {}, R2[PF_] = {};
   (void)red; (void)PA; (void)PA16; (void)PG; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
   const int frag = frag_base + (int)blockIdx.y;
 )PLKJITM";
@@ -336,8 +340,9 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     const int PD = std::min(std::max(sh.pd, 1), 3);
     // chain event j is staged from register set j % PD: loaded PD contractions ahead, stored
     // to the other LDS buffer (and a barrier) at the end of the contraction before its own
+    const char* bar = (sh.debug & 1) ? "" : " __syncthreads();";
     auto pload = [&](size_t j) {
-      if (j < pchain.size()) {
+      if (j < pchain.size() && !(sh.debug & 2)) {
         snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R%zu, %d)\n", j % (size_t)PD, ev[(size_t)pchain[j]].b);
         s += buf;
       }
@@ -350,7 +355,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     // after chain event np's contraction: hand the next one's P(t) over, refill the set
     auto pnext = [&]() {
       if (np + 1 < pchain.size()) {
-        snprintf(buf, sizeof(buf), "    PSTAGE_STORE(R%zu, %d) __syncthreads();\n", (np + 1) % (size_t)PD, cur ^ 1);
+        snprintf(buf, sizeof(buf), "    PSTAGE_STORE(R%zu, %d)%s\n", (np + 1) % (size_t)PD, cur ^ 1, bar);
         s += buf;
         cur ^= 1;
         pload(np + 1 + (size_t)PD);

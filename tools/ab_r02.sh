@@ -108,5 +108,8 @@ case "$1" in
       R=$(pwd); O=$R/gpurun_out/r2hiptrace; mkdir -p $O
       ( export TMPDIR=/tmp; cd /tmp && timeout -k 10 200 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $O -o run -- \
         python3 $R/bench.py --steps 12 --warmup 2 --no-cpu-baseline --no-events > $O/bench.json ) ;;
+  jmdbg)  # jit_treeM timing anatomy: without the per-contraction barrier / P(t) loads (wrong results)
+      $S r2jmdbg $C3 "base:" "nobar:PLK_DEBUG_JITM=1" "noload:PLK_DEBUG_JITM=2" "neither:PLK_DEBUG_JITM=3" \
+        "onea:PLK_DEBUG_JITM=4" "onea_neither:PLK_DEBUG_JITM=7" ;;
   *)  echo "usage: tools/ab_r02.sh <a..y>"; exit 2 ;;
 esac
