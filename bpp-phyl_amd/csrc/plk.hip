@@ -1508,6 +1508,9 @@ bool treeM_direct(plk_handle h) {
 // MFMA chains): cfg3 G = 4 / 2 / 1 = 7.40 / 6.87 / 6.43 ms (profiles/r01/g1_*).
 // PLK_TREEM_G overrides; staged tables and 64 states keep 4.
 int treeM_groups(plk_handle h) {
+  // 64 states: 128-pattern workgroups (8 waves, one per CU) halve the P^T staging traffic
+  // per pattern (PLK_TREEM_G64=8; A/B)
+  if (h->S == 64 && !treeM_direct(h)) return env_int("PLK_TREEM_G64", 4, 4, 8) >= 8 ? 8 : 4;
   if (h->S != 20 || !treeM_direct(h)) return 4;  // staged tables need 64-pattern workgroups
   const int g = env_int("PLK_TREEM_G", 1, 1, 4);
   return g == 3 ? 4 : g;
@@ -1540,6 +1543,13 @@ void launch_treeM_dm(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
         launch_treeM_g<S, DM, 2>(h, a, grid, lds);
       else
         launch_treeM_g<S, DM, 1>(h, a, grid, lds);
+      return;
+    }
+  }
+  if constexpr (S == 64) {
+    if (treeM_groups(h) == 8) {
+      grid.x = (unsigned)(h->n_pad / (16 * 8));
+      launch_treeM_g<S, DM, 8>(h, a, grid, lds);
       return;
     }
   }
@@ -1634,7 +1644,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     a.buf_doubles = std::max(h->C * h->S * h->S, h->C * h->n_codes * h->S);
     a.buf_doubles = (a.buf_doubles + 1) & ~1;
     const int threads = 64 * treeM_groups(h) * (h->S == 64 ? 1 : h->C);
-    const int pf = h->S == 64 ? treeM_pf<64>() : treeM_pf<20>();
+    const int pf = h->S == 64 ? (treeM_groups(h) == 8 ? treeM_pf<64, 8>() : treeM_pf<64>()) : treeM_pf<20>();
     if (!h->prog_jitm && !treeM_direct(h) && a.buf_doubles > pf * threads)
       return fail(h, PLK_ERR_UNSUPPORTED, "fused MFMA tables (%d doubles) exceed the staging registers",
                   a.buf_doubles);
@@ -1647,6 +1657,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     if (!env_is("PLK_TREEM_STAGE_CODES", '1') &&
         std::none_of(h->prog_host.begin(), h->prog_host.end(), [](const TInstr& w) { return w.op == T_TIP; }))
       a.stage_codes = 0;
+    if (treeM_groups(h) == 8) a.stage_codes = 0;  // the staged code rows cover 64 patterns
     if (a.stage_codes) lds_m += (size_t)h->n_tips * 64;
     // direct tables: the cherries' combined codes of the workgroup staged beside the tip codes
     // (opt-in PLK_TREEM_CCODES=1: every workgroup stages all cherries but runs one fragment,

@@ -384,8 +384,8 @@ __device__ __forceinline__ void eval_node_m(const TreeArgs& a, const TInstr* __r
 // (16 waves, 128 VGPRs = 4 waves per SIMD).  PF = table doubles per thread.
 template <int S, int G>
 constexpr int treeM_threads() { return S == 64 ? 64 * G : 64 * G * kTreeMaxWaves; }
-template <int S>
-constexpr int treeM_pf() { return S == 64 ? 17 : 3; }
+template <int S, int G = 4>
+constexpr int treeM_pf() { return S == 64 ? (G == 8 ? 9 : 17) : 3; }
 
 // DIRECT: no LDS staging and no per-event barrier -- MFMA A operands (P^T) and tip
 // table rows are read by each wave straight from L1/L2 (same values, same order).
@@ -397,10 +397,10 @@ __global__ __launch_bounds__((treeM_threads<S, G>()), (S == 64 ? 1 : 4)) void tr
                                                                    const int32_t* __restrict__ frag_start,
                                                                    const double* __restrict__ pmatsT) {
   constexpr int XT = MShape<S>::XT;
-  constexpr int PF = treeM_pf<S>();
+  constexpr int PF = treeM_pf<S, G>();
   extern __shared__ __attribute__((aligned(16))) double lds[];  // 2 table buffers | codes
   __shared__ double xch[kTreeMaxWaves * kTreeMGroups * 16];
-  __shared__ double red[64];
+  __shared__ double red[16 * (G > kTreeMGroups ? G : kTreeMGroups)];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = w / G, g = w % G;

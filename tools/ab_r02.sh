@@ -111,5 +111,8 @@ case "$1" in
   jmdbg)  # jit_treeM timing anatomy: without the per-contraction barrier / P(t) loads (wrong results)
       $S r2jmdbg $C3 "base:" "nobar:PLK_DEBUG_JITM=1" "noload:PLK_DEBUG_JITM=2" "neither:PLK_DEBUG_JITM=3" \
         "onea:PLK_DEBUG_JITM=4" "onea_neither:PLK_DEBUG_JITM=7" ;;
+  g64)  # treeM<64>: 128-pattern workgroups (P^T staging shared by 8 waves)
+      PLK_TREEM_G64=8 $T r2g64 -k "yn98 or 64 or bench_mode" quick || exit 1
+      $S r2g64 $C4 "g4:" "g8:PLK_TREEM_G64=8" "g4b:" "g8b:PLK_TREEM_G64=8" ;;
   *)  echo "usage: tools/ab_r02.sh <a..y>"; exit 2 ;;
 esac
