@@ -19,7 +19,11 @@
 #include <hip/hiprtc.h>
 #include <rccl/rccl.h>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <chrono>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -296,37 +300,127 @@ int collect_events(plk_handle h) {
 }
 
 // ---------------------------------------------------------------------------
-// hiprtc compilation of the tree-specialised kernels (plk_jit.hpp), cached per
-// process by generated source.  Modules stay loaded for the life of the process.
+// hiprtc compilation of the tree-specialised kernels (plk_jit.hpp, plk_jitm.hpp), cached
+// per process by (device, generated source) -- a module is loaded into one device's
+// context, so a multi-device handle compiles once and loads once per device -- and on
+// disk by source hash (PLK_JIT_CACHE=<dir>, default $XDG_CACHE_HOME/plk_jit or
+// ~/.cache/plk_jit; PLK_JIT_CACHE=0 disables): a cached code object is used only when its
+// stored source equals the generated one.  Modules stay loaded for the life of the process.
 // ---------------------------------------------------------------------------
 std::mutex g_jit_mutex;
-std::map<std::string, hipFunction_t> g_jit_cache;
+std::map<std::pair<int, std::string>, hipFunction_t> g_jit_cache;
+std::map<std::string, std::vector<char> > g_jit_code;  // compiled code objects by source
 
-int jit_function(plk_handle h, const std::string& src, const char* name, hipFunction_t* out) {
-  std::lock_guard<std::mutex> lock(g_jit_mutex);
-  auto it = g_jit_cache.find(src);
-  if (it != g_jit_cache.end()) {
-    *out = it->second;
-    return PLK_OK;
+std::string jit_cache_dir() {
+  const char* e = std::getenv("PLK_JIT_CACHE");
+  if (e && (e[0] == '0' || e[0] == '\0')) return std::string();
+  std::string d;
+  if (e) {
+    d = e;
+  } else if (const char* x = std::getenv("XDG_CACHE_HOME")) {
+    d = std::string(x) + "/plk_jit";
+  } else if (const char* hm = std::getenv("HOME")) {
+    d = std::string(hm) + "/.cache/plk_jit";
+  } else {
+    return std::string();
   }
+  // create the directory (and a missing parent) private to the user; failure = no disk cache
+  const size_t slash = d.rfind('/');
+  if (slash != std::string::npos && slash > 0) mkdir(d.substr(0, slash).c_str(), 0700);
+  mkdir(d.c_str(), 0700);
+  struct stat st;
+  if (stat(d.c_str(), &st) != 0 || !S_ISDIR(st.st_mode)) return std::string();
+  return d;
+}
+
+bool read_file(const std::string& path, std::vector<char>* out) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  out->resize(n > 0 ? (size_t)n : 0);
+  const bool ok = n > 0 && std::fread(out->data(), 1, (size_t)n, f) == (size_t)n;
+  std::fclose(f);
+  return ok;
+}
+
+void write_file_atomic(const std::string& path, const char* data, size_t n) {
+  const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const bool ok = std::fwrite(data, 1, n, f) == n;
+  std::fclose(f);
+  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
+}
+
+uint64_t fnv1a64(const std::string& s) {
+  uint64_t x = 1469598103934665603ull;
+  for (unsigned char c : s) x = (x ^ c) * 1099511628211ull;
+  return x;
+}
+
+int jit_compile(plk_handle h, const std::string& src, std::vector<char>* code) {
+  const char* opts[] = {"--offload-arch=gfx950", "-O3"};
+  const bool log = env_is("PLK_JIT_LOG", '1');
+  std::string dir = jit_cache_dir(), stem;
+  if (!dir.empty()) {
+    char hx[17];
+    int maj = 0, mnr = 0;
+    hiprtcVersion(&maj, &mnr);  // a compiler update invalidates every entry
+    snprintf(hx, sizeof(hx), "%016llx",
+             (unsigned long long)fnv1a64(src + opts[0] + opts[1] + std::to_string(maj) + "." + std::to_string(mnr)));
+    stem = dir + "/" + hx;
+    std::vector<char> stored;
+    if (read_file(stem + ".hip", &stored) && stored.size() == src.size() &&
+        std::memcmp(stored.data(), src.data(), src.size()) == 0 && read_file(stem + ".co", code)) {
+      if (log) std::fprintf(stderr, "[plk] jit cache hit %s.co\n", stem.c_str());
+      return PLK_OK;
+    }
+  }
+  const auto t0 = std::chrono::steady_clock::now();
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "plk_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
     return fail(h, PLK_ERR_DEVICE, "hiprtcCreateProgram failed");
-  const char* opts[] = {"--offload-arch=gfx950", "-O3"};
   const hiprtcResult rc = hiprtcCompileProgram(prog, 2, opts);
   if (rc != HIPRTC_SUCCESS) {
     size_t n = 0;
     hiprtcGetProgramLogSize(prog, &n);
-    std::string log(n, '\0');
-    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    std::string msg(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &msg[0]);
     hiprtcDestroyProgram(&prog);
-    return fail(h, PLK_ERR_DEVICE, "hiprtc compile of the tree kernel failed: %s", log.substr(0, 400).c_str());
+    return fail(h, PLK_ERR_DEVICE, "hiprtc compile of the tree kernel failed: %s", msg.substr(0, 400).c_str());
   }
   size_t n = 0;
   hiprtcGetCodeSize(prog, &n);
-  std::vector<char> code(n);
-  hiprtcGetCode(prog, code.data());
+  code->resize(n);
+  hiprtcGetCode(prog, code->data());
   hiprtcDestroyProgram(&prog);
+  if (log)
+    std::fprintf(stderr, "[plk] jit compiled %zu bytes of source in %.2f s\n", src.size(),
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+  if (!stem.empty()) {
+    write_file_atomic(stem + ".co", code->data(), code->size());
+    write_file_atomic(stem + ".hip", src.data(), src.size());  // last: it validates the .co
+  }
+  return PLK_OK;
+}
+
+int jit_function(plk_handle h, const std::string& src, const char* name, hipFunction_t* out) {
+  std::lock_guard<std::mutex> lock(g_jit_mutex);
+  const auto key = std::make_pair(h->device, src);
+  auto it = g_jit_cache.find(key);
+  if (it != g_jit_cache.end()) {
+    *out = it->second;
+    return PLK_OK;
+  }
+  auto ct = g_jit_code.find(src);
+  if (ct == g_jit_code.end()) {
+    std::vector<char> code;
+    if (int rc = jit_compile(h, src, &code)) return rc;
+    ct = g_jit_code.emplace(src, std::move(code)).first;
+  }
+  const std::vector<char>& code = ct->second;
   // PLK_JIT_DUMP=<dir>: keep the generated source and code object for inspection
   // (llvm-objdump -d --mcpu=gfx950 <dir>/plk_jit_<n>.co)
   if (const char* dir = std::getenv("PLK_JIT_DUMP")) {
@@ -340,11 +434,12 @@ int jit_function(plk_handle h, const std::string& src, const char* name, hipFunc
       std::fclose(f);
     }
   }
+  hipSetDevice(h->device);
   hipModule_t mod;
   HIPCHK(h, hipModuleLoadData(&mod, code.data()));
   hipFunction_t fn;
   HIPCHK(h, hipModuleGetFunction(&fn, mod, name));
-  g_jit_cache.emplace(src, fn);
+  g_jit_cache.emplace(key, fn);
   *out = fn;
   return PLK_OK;
 }

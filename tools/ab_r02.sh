@@ -114,5 +114,13 @@ case "$1" in
   g64)  # treeM<64>: 128-pattern workgroups (P^T staging shared by 8 waves)
       PLK_TREEM_G64=8 $T r2g64 -k "yn98 or 64 or bench_mode" quick || exit 1
       $S r2g64 $C4 "g4:" "g8:PLK_TREEM_G64=8" "g4b:" "g8b:PLK_TREEM_G64=8" ;;
+  jitcache)  # hiprtc compile time per config and the on-disk code-object cache (second process hits it)
+      export PLK_JIT_LOG=1 PLK_JIT_CACHE=$(pwd)/gpurun_out/r2jitcache/cache
+      for c in $C2 $C3 $C5; do
+        timeout -k 10 200 python bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> gpurun_out/r2jitcache_$c.1.err || exit 1
+        timeout -k 10 200 python bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> gpurun_out/r2jitcache_$c.2.err || exit 1
+        grep "\[plk\]" gpurun_out/r2jitcache_$c.1.err gpurun_out/r2jitcache_$c.2.err
+      done
+      $T r2jitcache -k "multi or jit_tree4_bitwise" quick ;;
   *)  echo "usage: tools/ab_r02.sh <a..y>"; exit 2 ;;
 esac
