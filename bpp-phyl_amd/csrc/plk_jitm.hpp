@@ -112,9 +112,9 @@ struct JitMShape {
   bool padstage = false; // P staging: padded LDS stride, unconditional stores (cfg3 3.93 vs 3.51 ms: off)
   int debug = 0;        // timing experiments only (wrong results): bit 1 no P(t) staging barrier, bit 2 no
                         // P(t) loads, bit 4 one A operand read per class and contraction
-  bool hyb = false;     // 20 states: 16x16x4 for states 0..15 + 4x4x4 for 16..19 (CONTRIB, HYB_;
-                        // cfg3 4.37 vs 3.56 ms all-4x4x4, so off)
-  bool hybrid() const { return hyb && S == 20 && !direct; }
+  bool hyb = false;     // 16-state tiles on 16x16x4, the rest on 4x4x4 (CONTRIB, HYB_; 20 and 64
+                        // states; cfg3 4.37 vs 3.56 ms all-4x4x4, so off)
+  bool hybrid() const { return hyb && (S == 20 || S == 64) && !direct; }
   static constexpr int G = 4;  // waves (16-pattern groups) per workgroup: 64 patterns
   int pb() const { return C * S * S; }  // doubles of P(t) per branch (every class)
   // LDS stride of a P buffer: every staging element of the workgroup has a slot (the
@@ -155,20 +155,26 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
 // D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1)
 // (YOUTER_: the C * XB independent chains advance one block at a time, so consecutive MFMAs
 // never depend on each other; the same sums in the same order either way)
-// HYB_ (20 states): states 0..15 of the output on v_mfma_f64_16x16x4 (A = the 16 x 4 tile
-// P[x][4Y + k], lane l holding x = l % 16, k = l / 16: 64 distinct values per 2048 flops) and
-// states 16..19 on v_mfma_f64_4x4x4_4b -- 4x fewer A operands per flop than all-4x4x4; the
-// 16x16 D registers q = 0..3 hold states 4q + hi, exactly the layout of blocks X = 0..3,
-// and the 4x4x4 D the layout of X = 4.  Image per class: 5 tiles of 64, then 5 of 16.
+// HYB_: the output's 16-state tiles on v_mfma_f64_16x16x4 (A = the 16 x 4 tile
+// P[16 t + i][4Y + k], lane l holding i = l % 16, k = l / 16: 64 distinct values per 2048
+// flops) and the remaining S % 16 states (20 states: 16..19) on v_mfma_f64_4x4x4_4b -- 4x
+// fewer A operands per flop than all-4x4x4.  The 16x16 D registers q = 0..3 of tile t hold
+// states 16 t + 4q + hi, exactly the layout of blocks X = 4t + q, and the 4x4x4 D the
+// layout of the last block.  Image per class: NT16_ * XB_ tiles of 64, then XB_ of 16.
+#define NT16_ (S_ / 16)
+#define R4_ ((S_ % 16) / 4)
 #define CONTRIB(D, SRC, bf, SET) { const double* P_ = PA + (bf) * PBS_; \
-  if (HYB_) { const double* Q_ = PA16 + (bf) * PBS_; f64x4 h_[C_]; double l_[C_]; \
-    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { h_[c_] = (f64x4){0.0, 0.0, 0.0, 0.0}; l_[c_] = 0.0; } \
+  if (HYB_) { const double* Q_ = PA16 + (bf) * PBS_; f64x4 h_[C_][NT16_]; double l_[C_]; \
+    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { l_[c_] = 0.0; \
+      _Pragma("unroll") for (int t_ = 0; t_ < NT16_; ++t_) h_[c_][t_] = (f64x4){0.0, 0.0, 0.0, 0.0}; } \
     _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { \
-      h_[c_] = mfma16(Q_[c_ * (S_ * S_) + Y_ * 64], SRC[c_][Y_], h_[c_]); \
-      l_[c_] = mfma4(P_[c_ * (S_ * S_) + 320 + Y_ * 16], SRC[c_][Y_], l_[c_]); } \
+      _Pragma("unroll") for (int t_ = 0; t_ < NT16_; ++t_) \
+        h_[c_][t_] = mfma16(Q_[c_ * (S_ * S_) + (t_ * XB_ + Y_) * 64], SRC[c_][Y_], h_[c_][t_]); \
+      if (R4_) l_[c_] = mfma4(P_[c_ * (S_ * S_) + NT16_ * XB_ * 64 + Y_ * 16], SRC[c_][Y_], l_[c_]); } \
     _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { \
-      if (SET) { D[c_][0] = h_[c_][0]; D[c_][1] = h_[c_][1]; D[c_][2] = h_[c_][2]; D[c_][3] = h_[c_][3]; D[c_][4] = l_[c_]; } \
-      else { D[c_][0] *= h_[c_][0]; D[c_][1] *= h_[c_][1]; D[c_][2] *= h_[c_][2]; D[c_][3] *= h_[c_][3]; D[c_][4] *= l_[c_]; } } \
+      _Pragma("unroll") for (int t_ = 0; t_ < NT16_; ++t_) _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) { \
+        if (SET) D[c_][4 * t_ + q_] = h_[c_][t_][q_]; else D[c_][4 * t_ + q_] *= h_[c_][t_][q_]; } \
+      if (R4_) { if (SET) D[c_][4 * NT16_] = l_[c_]; else D[c_][4 * NT16_] *= l_[c_]; } } \
   } else if (YOUTER_) { double d_[C_][XB_]; \
     _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) \
       _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
@@ -269,7 +275,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   _Pragma("unroll") for (int j = 0; j < PF_; ++j) {
     const int e = tid + j * NTH_;
     const int c = e / (S_ * S_), r = e - c * (S_ * S_), x = r / S_, y = r - x * S_;
-    const int t_ = HYB_ ? c * (S_ * S_) + (x < 16 ? (y >> 2) * 64 + (y & 3) * 16 + x : 320 + (y >> 2) * 16 + (y & 3) * 4 + (x - 16))
+    const int t_ = HYB_ ? c * (S_ * S_) + (x < 16 * NT16_ ? ((x >> 4) * XB_ + (y >> 2)) * 64 + (y & 3) * 16 + (x & 15)
+                                                        : NT16_ * XB_ * 64 + (y >> 2) * 16 + (y & 3) * 4 + (x - 16 * NT16_))
                         : ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3);
     sidx[j] = e < PB_ ? t_ : PBS_ > PB_ ? e : -1;
   }

@@ -122,5 +122,12 @@ case "$1" in
         grep "\[plk\]" gpurun_out/r2jitcache_$c.1.err gpurun_out/r2jitcache_$c.2.err
       done
       $T r2jitcache -k "multi or jit_tree4_bitwise" quick ;;
+  occ5)  # cfg5: three waves per SIMD via lower fragment height (classes-in-wave register levels)
+      $S r2occ5 $C5 "base:" "dm3w3:PLK_JIT_CIW_DM=3,PLK_JIT_MINW=3,PLK_JIT_L=1" "dm4w3:PLK_JIT_CIW_DM=4,PLK_JIT_MINW=3,PLK_JIT_L=1" \
+        "dm3:PLK_JIT_CIW_DM=3,PLK_JIT_L=1" "dm4l1:PLK_JIT_CIW_DM=4,PLK_JIT_L=1" "dm5w3:PLK_JIT_CIW_DM=5,PLK_JIT_MINW=3,PLK_JIT_L=1" ;;
+  hyb64)  # 64 states: per-tree kernel on 16x16x4 (PLK_JITM64=1 PLK_JITM_HYB=1) vs treeM<64> and jitm64 on 4x4x4
+      PLK_JITM64=1 PLK_JITM_HYB=1 $T r2hyb64 -k "jit_treeM_64 or bench_mode" quick || exit 1
+      $S r2hyb64 $C4 "treeM:" "jitm64:PLK_JITM64=1" "jitm64hyb:PLK_JITM64=1,PLK_JITM_HYB=1" \
+        "jitm64hyb_dm2:PLK_JITM64=1,PLK_JITM_HYB=1,PLK_JITM_DM=2" "jitm64hyb_w1:PLK_JITM64=1,PLK_JITM_HYB=1,PLK_JITM_MINW=1" ;;
   *)  echo "usage: tools/ab_r02.sh <a..y>"; exit 2 ;;
 esac
