@@ -390,6 +390,11 @@ def main():
                                    "pmatrix": tm["pmat_ms"] / max(ev_steps, 1),
                                    "root": tm["root_ms"] / max(ev_steps, 1)},
             "partials_launches_per_step": tm["launches"] / max(ev_steps, 1),
+            # host side of plk_evaluate per evaluation (us): P(t) launch call, traversal launch
+            # call, block-sum launch call, completion wait, host sum, caller between evaluations
+            "host_us_per_eval": ({k: round(v / tm["evaluations"], 2) for k, v in
+                                  zip(("pmat_call", "traversal_call", "blocks_call", "wait", "sum", "caller"),
+                                      tm["host_us"])} if tm.get("evaluations") else None),
             "table_launches_per_step": tm["table_launches"] / max(ev_steps, 1),
             "roofline": roof,
             "setup_s": t_setup,

@@ -36,9 +36,40 @@
 
 using namespace plk;
 
+extern char** environ;
+
 namespace {
+// Environment switches (A/B and debug) are read on every call of the hot
+// path; a getenv walks the whole environment (~100 entries on the GPU box), and a
+// traversal reads dozens of switches (~4 us of host time per evaluation).  Reads go
+// through a per-thread cache keyed by the switch name's address (names are literals of
+// this file), dropped whenever the environment changed: every API entry fingerprints the
+// `environ` array (its entries' addresses -- setenv / putenv / unsetenv change them).
+struct EnvCache {
+  uint64_t fp = 0;
+  std::vector<std::pair<const char*, const char*> > kv;
+};
+thread_local EnvCache g_env;
+
+void env_refresh() {
+  uint64_t x = 1469598103934665603ull ^ (uint64_t)(uintptr_t)environ;
+  for (char** e = environ; e && *e; ++e) x = (x ^ (uint64_t)(uintptr_t)*e) * 1099511628211ull;
+  if (x != g_env.fp) {
+    g_env.fp = x;
+    g_env.kv.clear();
+  }
+}
+
+const char* env_get(const char* name) {
+  for (const auto& p : g_env.kv)
+    if (p.first == name) return p.second;
+  const char* v = std::getenv(name);
+  g_env.kv.emplace_back(name, v);
+  return v;
+}
+
 bool env_is(const char* name, char v) {
-  const char* e = std::getenv(name);
+  const char* e = env_get(name);
   return e && e[0] == v;
 }
 
@@ -110,6 +141,10 @@ struct plk_handle_s {
   std::vector<EventPair> event_pool;
   int64_t n_launches = 0, n_table_launches = 0;
   double acc_ms[4] = {0, 0, 0, 0};
+  // host side of plk_evaluate (plk_timing::host_us): segment sums, count, end of the last one
+  double host_us[6] = {0, 0, 0, 0, 0, 0};
+  int64_t n_evals = 0;
+  std::chrono::steady_clock::time_point last_eval_end{};
   int jit_last_gx = 0;                    // workgroups per fragment of the last JIT launch
   std::vector<int> jit_frag_gx;           // workgroups per fragment of the last JIT traversal (per fragment)
   std::string last_error;
@@ -209,6 +244,7 @@ struct plk_handle_s {
   int comm_ranks = 0, comm_rank = 0;
   int64_t comm_cmax = 0;                  // block sums per rank in the all-gather (max over ranks)
   double* d_blk_local = nullptr;          // [comm_cmax] this rank's block sums (zero padded)
+  unsigned* d_blk_cnt = nullptr;          // [n_blocks] arrival counters of the in-kernel block sums
   double* d_blk_all = nullptr;            // [comm_ranks][comm_cmax]
   int64_t* d_comm_counts = nullptr;       // block sums per rank
   double* h_total = nullptr;              // mapped pinned: the global lnL
@@ -312,14 +348,14 @@ std::map<std::pair<int, std::string>, hipFunction_t> g_jit_cache;
 std::map<std::string, std::vector<char> > g_jit_code;  // compiled code objects by source
 
 std::string jit_cache_dir() {
-  const char* e = std::getenv("PLK_JIT_CACHE");
+  const char* e = env_get("PLK_JIT_CACHE");
   if (e && (e[0] == '0' || e[0] == '\0')) return std::string();
   std::string d;
   if (e) {
     d = e;
-  } else if (const char* x = std::getenv("XDG_CACHE_HOME")) {
+  } else if (const char* x = env_get("XDG_CACHE_HOME")) {
     d = std::string(x) + "/plk_jit";
-  } else if (const char* hm = std::getenv("HOME")) {
+  } else if (const char* hm = env_get("HOME")) {
     d = std::string(hm) + "/.cache/plk_jit";
   } else {
     return std::string();
@@ -423,7 +459,7 @@ int jit_function(plk_handle h, const std::string& src, const char* name, hipFunc
   const std::vector<char>& code = ct->second;
   // PLK_JIT_DUMP=<dir>: keep the generated source and code object for inspection
   // (llvm-objdump -d --mcpu=gfx950 <dir>/plk_jit_<n>.co)
-  if (const char* dir = std::getenv("PLK_JIT_DUMP")) {
+  if (const char* dir = env_get("PLK_JIT_DUMP")) {
     const std::string stem = std::string(dir) + "/plk_jit_" + std::to_string(g_jit_cache.size());
     if (FILE* f = std::fopen((stem + ".hip").c_str(), "wb")) {
       std::fwrite(src.data(), 1, src.size(), f);
@@ -494,7 +530,7 @@ int ensure_pmatsT(plk_handle h) {
 
 int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
   const int S = h->S;
-  if (S == 64 && !std::getenv("PLK_GENERIC64")) {
+  if (S == 64 && !env_get("PLK_GENERIC64")) {
     // K3: fp64 MFMA, P^T staged in LDS
     int rc = ensure_pmatsT(h);
     if (rc) return rc;
@@ -506,7 +542,7 @@ int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs
       partials_mfma64_kernel<false><<<grid, block, lds, h->stream>>>(d_ops, a, h->pmatsT, h->C);
     return PLK_OK;
   }
-  if (S == 20 && !std::getenv("PLK_GENERIC20")) {
+  if (S == 20 && !env_get("PLK_GENERIC20")) {
     // K2: P rows through scalar loads, tip tables in LDS
     const size_t lds = 3 * (size_t)h->C * h->n_codes * S * sizeof(double);
     if (lds <= 160 * 1024) {
@@ -606,6 +642,7 @@ int root_finish_c(plk_handle h, double* lnl, double* block_sums);
 }
 
 namespace {
+double* block_target(plk_handle h);
 
 // every device's root reduction in flight, then one wait per device; the lnL is the sum of
 // all block sums in global block order (bitwise the single-device value)
@@ -742,6 +779,7 @@ const char* plk_last_error(plk_handle h) { return h ? h->last_error.c_str() : g_
 
 int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int n_tips, int n_internal,
                int n_models, unsigned flags, plk_handle* out) {
+  env_refresh();
   if (!out) return fail(nullptr, PLK_ERR_ARG, "null out handle");
   *out = nullptr;
   if (n_states < 2 || n_states > 64) return fail(nullptr, PLK_ERR_UNSUPPORTED, "n_states %d not in [2, 64]", n_states);
@@ -816,6 +854,10 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
       hipHostGetDevicePointer((void**)&h->block_sums, h->h_blocks, 0) != hipSuccess)
     return bail(fail(h, PLK_ERR_OOM, "pinned block-sum buffer"));
   if ((rc = dalloc(h, (void**)&h->wave_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return bail(rc);
+  // per-block arrival counters of the in-kernel block sums (the last arriver resets its own)
+  if ((rc = dalloc(h, (void**)&h->d_blk_cnt, (size_t)h->n_blocks * sizeof(unsigned)))) return bail(rc);
+  if (hipMemset(h->d_blk_cnt, 0, (size_t)h->n_blocks * sizeof(unsigned)) != hipSuccess)
+    return bail(fail(nullptr, PLK_ERR_DEVICE, "block counter memset failed"));
   h->materialized.assign(n_internal, 0);
   // default weights 1 for real patterns, 0 for padding
   std::vector<double> w(h->n_pad, 0.0);
@@ -850,7 +892,7 @@ int plk_destroy(plk_handle h) {
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
-                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out};
+                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_blk_cnt};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) hipHostFree(h->h_req);
@@ -870,6 +912,7 @@ int plk_destroy(plk_handle h) {
 }
 
 int plk_comm_get_id(plk_comm_id* id) {
+  env_refresh();
   if (!id) return fail(nullptr, PLK_ERR_ARG, "null id");
   static_assert(sizeof(plk_comm_id) == sizeof(ncclUniqueId), "plk_comm_id wraps ncclUniqueId");
   ncclUniqueId u;
@@ -879,6 +922,7 @@ int plk_comm_get_id(plk_comm_id* id) {
 }
 
 int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id) {
+  env_refresh();
   if (!h || !id || n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(h, PLK_ERR_ARG, "bad communicator arguments");
   if (!h->shards.empty()) return fail(h, PLK_ERR_UNSUPPORTED, "a multi-device handle exchanges in-process");
   if (h->comm) return fail(h, PLK_ERR_STATE, "communicator already initialised");
@@ -916,6 +960,7 @@ int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id) {
 }
 
 int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_code_table(x, n_codes, code_to_vec); });
   if (!h || !code_to_vec || n_codes < 1 || n_codes > 256) return fail(h, PLK_ERR_ARG, "bad code table (n_codes %d)", n_codes);
   if (h->S == 4 && n_codes > kMaxCodes4 && s4_supported(h->C))
@@ -941,6 +986,7 @@ int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec) {
 }
 
 int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_slices(h, [&](plk_handle x, int64_t a) { return plk_set_tip_codes(x, tip, codes ? codes + a : nullptr); });
   if (!h || !codes || tip < 0 || tip >= h->n_tips) return fail(h, PLK_ERR_ARG, "bad tip index %d", tip);
   if (!h->table_set) return fail(h, PLK_ERR_STATE, "plk_set_code_table must precede plk_set_tip_codes");
@@ -980,6 +1026,7 @@ int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes) {
 }
 
 int plk_set_pattern_weights(plk_handle h, const double* weights) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_slices(h, [&](plk_handle x, int64_t a) { return plk_set_pattern_weights(x, weights ? weights + a : nullptr); });
   if (!h || !weights) return fail(h, PLK_ERR_ARG, "null weights");
   hipSetDevice(h->device);
@@ -989,6 +1036,7 @@ int plk_set_pattern_weights(plk_handle h, const double* weights) {
 }
 
 int plk_set_category_rates(plk_handle h, const double* rates, const double* probs) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_category_rates(x, rates, probs); });
   if (!h || !rates || !probs) return fail(h, PLK_ERR_ARG, "null rates/probs");
   hipSetDevice(h->device);
@@ -1000,6 +1048,7 @@ int plk_set_category_rates(plk_handle h, const double* rates, const double* prob
 }
 
 int plk_set_root_frequencies(plk_handle h, const double* pi) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_root_frequencies(x, pi); });
   if (!h || !pi) return fail(h, PLK_ERR_ARG, "null frequencies");
   hipSetDevice(h->device);
@@ -1010,6 +1059,7 @@ int plk_set_root_frequencies(plk_handle h, const double* pi) {
 }
 
 int plk_set_eigen(plk_handle h, int model, const double* V, const double* Vinv, const double* lambda) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_eigen(x, model, V, Vinv, lambda); });
   if (!h || !V || !Vinv || !lambda || model < 0 || model >= h->n_models)
     return fail(h, PLK_ERR_ARG, "bad eigen system (model %d)", model);
@@ -1025,6 +1075,7 @@ int plk_set_eigen(plk_handle h, int model, const double* V, const double* Vinv, 
 
 int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32_t* model, const double* t,
                          unsigned deriv_mask) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_update_pmatrices(x, n, branch, model, t, deriv_mask); });
   if (!h || n < 0 || (n > 0 && (!branch || !t))) return fail(h, PLK_ERR_ARG, "bad pmatrix request");
   if (n == 0) return PLK_OK;
@@ -1053,7 +1104,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   PmatInline inl;
   inl.n = 0;
   const size_t off_t = 0, off_b = (size_t)n * sizeof(double), off_m = off_b + (size_t)n * sizeof(int32_t);
-  const char* staged_env = std::getenv("PLK_PMAT_STAGED");
+  const char* staged_env = env_get("PLK_PMAT_STAGED");
   if (n <= kPmatInline && !(staged_env && staged_env[0] == '1')) {
     inl.n = n;
     for (int i = 0; i < n; ++i) {
@@ -1111,6 +1162,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   a.S = h->S;
   a.C = h->C;
   a.mask = deriv_mask;
+  a.n_req = n;
   // tip tables ride along for S <= 20 (P of the block staged in LDS; S = 64 keeps the
   // separate tip_table_kernel)
   const bool k64 = h->S == 64 && deriv_mask == PLK_DERIV_P && !env_is("PLK_PMAT64", '0');
@@ -1129,6 +1181,8 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     pmat64s_kernel<<<dim3(n, h->C, 4), dim3(256), (size_t)(64 + 16 * 64 + S2) * sizeof(double), h->stream>>>(a, inl);
   else if (k64)
     pmat64_kernel<<<dim3(n, h->C), dim3(256), (size_t)(64 + 2 * S2) * sizeof(double), h->stream>>>(a, inl);
+  else if (h->S == 4 && !env_is("PLK_PMAT4", '0'))
+    pmat4_kernel<<<dim3((unsigned)((n * h->C * 4 + 63) / 64)), dim3(64), 0, h->stream>>>(a, inl);
   else
     pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a, inl);
   HIPCHK(h, hipGetLastError());
@@ -1153,6 +1207,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
 }
 
 int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_set_pmatrix(x, branch, P); });
   if (!h || !P || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
   hipSetDevice(h->device);
@@ -1167,6 +1222,7 @@ int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
 }
 
 int plk_get_dpmatrix(plk_handle h, int branch, int order, double* dP) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_forward(h, plk_get_dpmatrix(h->shards[0], branch, order, dP));
   if (!h || !dP || branch < 0 || branch >= h->n_nodes || (order != 1 && order != 2))
     return fail(h, PLK_ERR_ARG, "bad derivative request (branch %d, order %d)", branch, order);
@@ -1180,6 +1236,7 @@ int plk_get_dpmatrix(plk_handle h, int branch, int order, double* dP) {
 }
 
 int plk_get_pmatrix(plk_handle h, int branch, double* P) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_forward(h, plk_get_pmatrix(h->shards[0], branch, P));
   if (!h || !P || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
   hipSetDevice(h->device);
@@ -1202,7 +1259,7 @@ constexpr int kTree4Levels(int CW) { return CW >= 4 ? 6 : 8; }
 // wave per rate class, the smallest register footprint and the highest occupancy)
 int tree4_cw(plk_handle h) {
   int cw = 1;
-  if (const char* e = std::getenv("PLK_TREE4_CW")) cw = std::atoi(e);
+  if (const char* e = env_get("PLK_TREE4_CW")) cw = std::atoi(e);
   if (cw != 1 && cw != 2 && cw != 4) cw = 1;
   return std::min(cw, h->C);
 }
@@ -1230,7 +1287,7 @@ FusedKind fused_kind(plk_handle h) {
 bool tree4_supported(plk_handle h) { return fused_kind(h) != FK_NONE; }
 
 int env_int(const char* name, int def, int lo, int hi) {
-  const char* e = std::getenv(name);
+  const char* e = env_get(name);
   if (!e) return def;
   const int v = std::atoi(e);
   return (v >= lo && v <= hi) ? v : def;
@@ -1253,7 +1310,7 @@ bool jit_treeM(plk_handle h) {
 // for scaling runs; PLK_JIT_CIW=0/1 overrides.
 bool jit_ciw(plk_handle h) {
   if (!jit_tree4(h) || h->C == 1) return false;
-  const char* e = std::getenv("PLK_JIT_CIW");
+  const char* e = env_get("PLK_JIT_CIW");
   if (e) return e[0] == '1';
   return (h->flags & PLK_FLAG_SCALING) != 0;
 }
@@ -1833,6 +1890,12 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.exact_only = !env_is("PLK_JIT_SPECULATE", '1');
     // classes in the wave: next class's P(t) loads overlap this class's FMAs (PLK_JIT_PPIPE=0: off)
     sh.ppipe = !env_is("PLK_JIT_PPIPE", '0');
+    // PLK_JIT_BLOCKS=1: the root fragment forms the block sums (no wave_sums_to_blocks
+    // launch).  Measured slower (cfg2 traversal 0.125 -> 0.160 ms): the wave that stores a
+    // wave sum must wait for the store and the counter's atomic round trip (~3 us) before
+    // its workgroup's next super-block barrier, in every super-block.  Off; the formal
+    // release/acquire form (an L2 write-back per wave) was slower still (round 1)
+    sh.blocks = env_is("PLK_JIT_BLOCKS", '1');
     if (sh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
     if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW || sh.PW != h->jit_shape.PW ||
@@ -1840,7 +1903,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
         sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.stage_only != h->jit_shape.stage_only || sh.exact_only != h->jit_shape.exact_only ||
-        sh.ppipe != h->jit_shape.ppipe) {
+        sh.ppipe != h->jit_shape.ppipe || sh.blocks != h->jit_shape.blocks) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
@@ -1860,6 +1923,10 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.n_patterns = a.n_patterns;
     ja.n_sblocks = (int32_t)((h->n_pad + 64 * sh.G * sh.PW - 1) / (64 * sh.G * sh.PW));  // last may be ragged
     ja.guard = a.guard;
+    ja.blk_cnt = h->d_blk_cnt;
+    ja.block_sums = block_target(h);
+    ja.n_waves = (int32_t)((h->n_patterns + 63) / 64);
+    ja.n_wpad = (int32_t)(h->n_pad / 64);
   }
   const bool jitm = kind == FK_TREEM && h->prog_jitm;
   JMArgs ma;
@@ -1878,6 +1945,9 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.padstage = env_is("PLK_JITM_PADSTAGE", '1');
     msh.hyb = env_is("PLK_JITM_HYB", '1');
     msh.debug = env_int("PLK_DEBUG_JITM", 0, 0, 7);
+    // 16-pattern waves per workgroup: 4 (64 patterns) or 8 (128; every P(t) staging and its
+    // barrier serve twice the patterns)
+    msh.G = env_int("PLK_JITM_G", 4, 4, 8) >= 8 ? 8 : 4;
     if (msh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "jit_treeM needs %zu B of LDS", msh.lds_bytes());
     if (!h->jitm_fn || !(msh == h->jitm_shape)) {
@@ -1946,8 +2016,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     } else if (jitm) {
       int base = first;
       void* args[] = {&ma, &base};
-      HIPCHK(h, hipModuleLaunchKernel(h->jitm_fn, (unsigned)(h->n_pad / (16 * JitMShape::G)), grid.y, 1,
-                                      64 * JitMShape::G, 1, 1, (unsigned)msh.lds_bytes(), h->stream, args, nullptr));
+      HIPCHK(h, hipModuleLaunchKernel(h->jitm_fn, (unsigned)(h->n_pad / (16 * msh.G)), grid.y, 1,
+                                      64 * msh.G, 1, 1, (unsigned)msh.lds_bytes(), h->stream, args, nullptr));
     } else if (kind == FK_TREEM) {
       launch_treeM(h, a, grid, lds_m);
       if (treeM_groups(h) != kTreeMGroups && h->prog_root >= 0 && first + (int)t.size() == h->prog_nf) {
@@ -1974,9 +2044,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   }
   h->fused_lnl_valid = h->prog_root >= 0;
   h->fused_lnl_root = h->prog_root;
-  // (forming the block sums in the kernel's last workgroup was measured slower: the
-  // agent-scope release fence each workgroup needs costs 0.27 -> 0.42 ms on cfg2)
-  h->blocks_fused = false;
+  // the jit kernel's root fragment formed the block sums (JitShape::blocks)
+  h->blocks_fused = jit && h->prog_root >= 0 && h->jit_shape.blocks;
   return PLK_OK;
 }
 
@@ -2976,6 +3045,7 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
 extern "C" {
 
 int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_update_partials(x, ops, n_ops); });
   if (!h || n_ops < 0 || (n_ops > 0 && !ops)) return fail(h, PLK_ERR_ARG, "bad op list");
   if (n_ops == 0) return PLK_OK;
@@ -2998,6 +3068,7 @@ int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
 }
 
 int plk_get_partials(plk_handle h, int node, double* out) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_slices(h, [&](plk_handle x, int64_t a) { return plk_get_partials(x, node, out ? out + a * h->C * h->S : nullptr); });
   if (!h || !out || node < h->n_tips || node >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad internal node %d", node);
   hipSetDevice(h->device);
@@ -3081,15 +3152,21 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
   if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
   hipSetDevice(h->device);
   if (h->fused_lnl_valid && h->fused_lnl_root == root) {
-    // the fused traversal already reduced the root: only the block sums remain
-    const int n_waves = (int)((h->n_patterns + 63) / 64);
-    wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, block_target(h), n_waves,
-                                                                          h->n_blocks);
-    HIPCHK(h, hipGetLastError());
+    // the fused traversal already reduced the root: only the block sums remain (unless
+    // its root fragment formed them too)
+    if (!h->blocks_fused) {
+      const int n_waves = (int)((h->n_patterns + 63) / 64);
+      wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, block_target(h), n_waves,
+                                                                            h->n_blocks);
+      HIPCHK(h, hipGetLastError());
+    }
   } else {
     if (!h->materialized[root - h->n_tips]) return fail(h, PLK_ERR_STATE, "root %d has no partial", root);
     int rc = launch_root(h, root);
     if (rc) return rc;
+    // the wave sums and block sums of the fused root reduction are overwritten
+    h->fused_lnl_valid = false;
+    h->blocks_fused = false;
   }
   if (h->comm) {
     // the one cross-GPU exchange of an evaluation: a fixed-size all-gather of block sums
@@ -3106,9 +3183,10 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
   return PLK_OK;
 }
 
-int root_finish(plk_handle h, double* lnl, double* block_sums) {
+int root_finish(plk_handle h, double* lnl, double* block_sums, bool wait = true) {
   hipSetDevice(h->device);
-  if (int rc = stream_wait(h)) return rc;
+  if (wait)
+    if (int rc = stream_wait(h)) return rc;
   double s = 0.0;
   if (h->comm) {
     s = *h->h_total;
@@ -3133,6 +3211,7 @@ static int multi_root_loglik(plk_handle h, int root, double* lnl, double* site_l
 
 int plk_create_multi(const int* devices, int n_devices, int n_states, int n_classes, int64_t n_patterns, int n_tips,
                      int n_internal, int n_models, unsigned flags, plk_handle* out) {
+  env_refresh();
   if (!out || !devices || n_devices < 1) return fail(nullptr, PLK_ERR_ARG, "bad device list");
   *out = nullptr;
   if (n_patterns < 1) return fail(nullptr, PLK_ERR_ARG, "bad pattern count");
@@ -3180,6 +3259,7 @@ int plk_shard_count(plk_handle h, int* n_shards) {
 }
 
 int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums) {
+  env_refresh();
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
   if (!h->shards.empty()) return multi_root_loglik(h, root, lnl, site_lnl, block_sums);
   int rc = root_launch(h, root, site_lnl);
@@ -3219,6 +3299,7 @@ static int launch_root(plk_handle h, int root) {
 }
 
 int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_branch_derivatives(h, branch, d1, d2);
   if (!h || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
   if (h->trav_ops.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet (plk_update_partials)");
@@ -3342,6 +3423,9 @@ int plk_reset_timing(plk_handle h) {
   if (rc) return rc;
   h->n_launches = h->n_table_launches = 0;
   h->acc_ms[0] = h->acc_ms[1] = h->acc_ms[2] = h->acc_ms[3] = 0.0;
+  for (double& x : h->host_us) x = 0.0;
+  h->n_evals = 0;
+  h->last_eval_end = std::chrono::steady_clock::time_point{};
   return PLK_OK;
 }
 
@@ -3357,6 +3441,8 @@ int plk_get_timing_ex(plk_handle h, plk_timing* out) {
   out->root_ms = h->acc_ms[2];
   out->tables_ms = h->acc_ms[3];
   out->table_launches = h->n_table_launches;
+  out->evaluations = h->n_evals;
+  for (int i = 0; i < 6; ++i) out->host_us[i] = h->host_us[i];
   return PLK_OK;
 }
 
@@ -3378,15 +3464,39 @@ int plk_synchronize(plk_handle h) {
 
 int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* model, const double* t,
                  const plk_op* ops, int n_ops, int root, double* lnl, double* block_sums) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_evaluate(h, n, branch, model, t, ops, n_ops, root, lnl, block_sums);
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t0 = clk::now();
+  auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
   int rc = plk_update_pmatrices(h, n, branch, model, t, PLK_DERIV_P);
   if (rc) return rc;
+  const clk::time_point t1 = clk::now();
   rc = plk_update_partials(h, ops, n_ops);
   if (rc) return rc;
-  return plk_root_loglik(h, root, lnl, nullptr, block_sums);
+  const clk::time_point t2 = clk::now();
+  rc = root_launch(h, root, nullptr);
+  if (rc) return rc;
+  const clk::time_point t3 = clk::now();
+  if ((rc = stream_wait(h))) return rc;
+  const clk::time_point t4 = clk::now();
+  rc = root_finish(h, lnl, block_sums, false);
+  if (rc) return rc;
+  const clk::time_point t5 = clk::now();
+  h->host_us[0] += us(t0, t1);
+  h->host_us[1] += us(t1, t2);
+  h->host_us[2] += us(t2, t3);
+  h->host_us[3] += us(t3, t4);
+  h->host_us[4] += us(t4, t5);
+  if (h->n_evals > 0) h->host_us[5] += us(h->last_eval_end, t0);
+  h->n_evals++;
+  h->last_eval_end = t5;
+  return PLK_OK;
 }
 
 int plk_all_branch_derivatives(plk_handle h, double* d1, double* d2) {
+  env_refresh();
   if (h && !h->shards.empty()) return multi_all_branch_derivatives(h, d1, d2);
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
   return dr_derivatives(h, d1, d2);

@@ -53,6 +53,7 @@ struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
   double* partials; i32* scale; const u8* codes; const double* tipP; const double* weights;
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
+  unsigned* blk_cnt; double* block_sums; i32 n_waves; i32 n_wpad;  // BLK_: block sums in the kernel
 };
 
 // Register vectors hold 4 * CW * PW doubles: vector v = pw * CW + cw is class c0 + cw of
@@ -336,7 +337,38 @@ __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
-      if (gv && lane == 0) a.wave_sums[(p0 + 64 * pw) >> 6] = wr;
+      if (!BLK_) {
+        if (gv && lane == 0) a.wave_sums[(p0 + 64 * pw) >> 6] = wr;
+        continue;
+      }
+      // BLK_: the wave that completes a 4096-pattern block forms its block sum (the 64 wave
+      // sums added in wave order, as wave_sums_to_blocks does).  The wave sum is stored at
+      // agent scope and waited for before the block's counter is bumped; the last arriver
+      // reads the block's wave sums at agent scope -- no L2 write-back fence, which made the
+      // release/acquire form of this slower than the extra launch
+      const int wv = (int)((p0 + 64 * pw) >> 6), b = wv >> 6;
+      int last = 0;
+      if (gv && lane == 0) {
+        __hip_atomic_store(a.wave_sums + wv, wr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0);
+        const int need = min(64, a.n_wpad - b * 64);
+        last = __hip_atomic_fetch_add(a.blk_cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)(need - 1);
+      }
+      last = __shfl(last, 0, 64);
+      if (last) {
+        const int w = b * 64 + lane;
+        const double v = w < a.n_waves ? __hip_atomic_load(a.wave_sums + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        double sb = 0.0;
+        for (int k = 0; k < 64; ++k) {
+          const double x = __shfl(v, k, 64);
+          if (b * 64 + k < a.n_waves) sb += x;
+        }
+        if (lane == 0) {
+          a.block_sums[b] = sb;
+          __hip_atomic_store(a.blk_cnt + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+        }
+      }
     }
   }
 }
@@ -358,6 +390,10 @@ struct JArgs {
   int64_t n_patterns;
   int32_t n_sblocks;
   int32_t guard;
+  unsigned* blk_cnt;
+  double* block_sums;
+  int32_t n_waves;
+  int32_t n_wpad;
 };
 
 struct JitShape {
@@ -376,6 +412,7 @@ struct JitShape {
   int stage_only = 0;  // timing experiments only: return after staging the tables (1) / at once (2)
   bool exact_only = true;   // scaling: no speculative no-rescale pass (PLK_JIT_SPECULATE=1 enables it)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
+  bool blocks = false;      // the root fragment forms the 4096-pattern block sums (BLK_)
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     // the second exchange buffer only serves the per-node rescale
@@ -519,6 +556,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   s.reserve(4096 * events.size() + 16384);
   s += sh.ppipe ? "#define PPIPE_ 1\n" : "#define PPIPE_ 0\n";  // read by the prelude's contrib
   s += "#define STAGE_ONLY_ " + std::to_string(sh.stage_only) + "\n";
+  s += sh.blocks ? "#define BLK_ 1\n" : "#define BLK_ 0\n";
   s += kJitPrelude;
   char buf[400];
   const std::string minw_s = sh.minw > 0 ? ", " + std::to_string(sh.minw) : std::string();
@@ -608,19 +646,37 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         }
         continue;
       }
-      for (int i = lane; i < C_ * U_ * U_ * 4; i += 64) {
-        const int c = i / (U_ * U_ * 4), r = i - c * (U_ * U_ * 4), ca = r / (U_ * 4), cb = (r >> 2) % U_, x = i & 3;
+      // one row (class c, code pair ca, cb: 4 doubles) per lane, its operands loaded
+      // together (16-byte loads), so a unit costs one load latency, not one per double
+      for (int r = lane; r < C_ * U_ * U_; r += 64) {
+        const int c = r / (U_ * U_), q = r - c * (U_ * U_), ca = q / U_, cb = q - ca * U_;
+        const double2* pa = reinterpret_cast<const double2*>(ra + (c * U_ + ca) * 4);
+        const double2* pb = reinterpret_cast<const double2*>(rb + (c * U_ + cb) * 4);
+        const double2 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+        double v[4] = {a0.x * b0.x, a0.y * b0.y, a1.x * b1.x, a1.y * b1.y};
+        double2* o = reinterpret_cast<double2*>(dst + (i64)r * 4);
         if (br < 0) {
-          dst[i] = ra[(c * U_ + ca) * 4 + x] * rb[(c * U_ + cb) * 4 + x];
+          o[0] = make_double2(v[0], v[1]);
+          o[1] = make_double2(v[2], v[3]);
         } else {  // contrib<.., true>: the same operations in the same order
-          const double* P = pmats + ((i64)br * C_ + c) * 16 + 4 * x;
-          double v[4];
-          for (int y = 0; y < 4; ++y) v[y] = ra[(c * U_ + ca) * 4 + y] * rb[(c * U_ + cb) * 4 + y];
-          double t = P[0] * v[0];
-          t = __builtin_fma(P[1], v[1], t);
-          t = __builtin_fma(P[2], v[2], t);
-          t = __builtin_fma(P[3], v[3], t);
-          dst[i] = t;
+          const double2* P2 = reinterpret_cast<const double2*>(pmats + ((i64)br * C_ + c) * 16);
+          double P[16];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const double2 pj = P2[j];
+            P[2 * j] = pj.x;
+            P[2 * j + 1] = pj.y;
+          }
+          double t[4];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            t[x] = P[4 * x] * v[0];
+            t[x] = __builtin_fma(P[4 * x + 1], v[1], t[x]);
+            t[x] = __builtin_fma(P[4 * x + 2], v[2], t[x]);
+            t[x] = __builtin_fma(P[4 * x + 3], v[3], t[x]);
+          }
+          o[0] = make_double2(t[0], t[1]);
+          o[1] = make_double2(t[2], t[3]);
         }
       }
     }

@@ -115,16 +115,16 @@ struct JitMShape {
   bool hyb = false;     // 16-state tiles on 16x16x4, the rest on 4x4x4 (CONTRIB, HYB_; 20 and 64
                         // states; cfg3 4.37 vs 3.56 ms all-4x4x4, so off)
   bool hybrid() const { return hyb && (S == 20 || S == 64) && !direct; }
-  static constexpr int G = 4;  // waves (16-pattern groups) per workgroup: 64 patterns
+  int G = 4;  // waves (16-pattern groups) per workgroup: 64 patterns (4) or 128 (8)
   int pb() const { return C * S * S; }  // doubles of P(t) per branch (every class)
   // LDS stride of a P buffer: every staging element of the workgroup has a slot (the
   // elements past pb() land in the padding), so the staging stores need no condition
   int pbs() const { return padstage ? (pb() + 64 * G - 1) / (64 * G) * (64 * G) : pb(); }
-  size_t lds_bytes() const { return (size_t)((direct ? 0 : 2 * pbs()) + 64) * sizeof(double); }
+  size_t lds_bytes() const { return (size_t)((direct ? 0 : 2 * pbs()) + 16 * G) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
     return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && direct == o.direct &&
            pd == o.pd && hoist == o.hoist && youter == o.youter && padstage == o.padstage && hyb == o.hyb &&
-           debug == o.debug;
+           debug == o.debug && G == o.G;
   }
 };
 
@@ -137,12 +137,12 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   s.reserve(65536 * std::max<size_t>(starts.size(), 1));
   s += kJitMPrelude;
   char buf[512];
-  const int NTH = 64 * JitMShape::G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH, PBS = sh.pbs();
+  const int NTH = 64 * sh.G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH, PBS = sh.pbs();
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
            "#define NTH_ %d\n#define PB_ %d\n#define PBS_ %d\n#define PF_ %d\n#define SC_ %s\n#define DIRECT_ %d\n#define YOUTER_ %d\n"
            "#define HYB_ %d\n#define DBGA_ %d\n",
-           S, C, XB, sh.U, sh.U * sh.U, JitMShape::G, NTH, PB, PBS, PF, sh.scale ? "true" : "false", sh.direct ? 1 : 0,
+           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PBS, PF, sh.scale ? "true" : "false", sh.direct ? 1 : 0,
            sh.youter ? 1 : 0, sh.hybrid() ? 1 : 0, (sh.debug & 4) ? 1 : 0);
   s += buf;
   s += R"PLKJITM(
@@ -236,7 +236,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) V[c_][X_] *= kScaleUp; \
     K += 1; } }
 // root reduction (RHomogeneousTreeLikelihood.cpp:162-216 / NH :168-233) and the fixed
-// butterfly over the workgroup's 64 patterns (root_kernel's order)
+// butterfly over each 64 patterns of the workgroup (root_kernel's order)
 #define REDUCE_ROOT(V, K) { double l_ = 0.0; \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { double s_ = 0.0; \
     _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { const double li_ = V[c_][X_] * a.pi[4 * X_ + hi]; \
@@ -251,16 +251,16 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   if (p < a.n_patterns) { if (hi == 0) a.site_lnl[p] = rr_; wr_ = a.weights[p] * rr_; } \
   if (hi == 0) red[16 * w + pl] = wr_; \
   __syncthreads(); \
-  if (w == 0) { double v_ = red[lane]; \
+  if (w < G_ / 4) { double v_ = red[64 * w + lane]; \
     _Pragma("unroll") for (int off_ = 32; off_ > 0; off_ >>= 1) v_ += __shfl_xor(v_, off_, 64); \
-    if (lane == 0) a.wave_sums[p0 >> 6] = v_; } }
+    if (lane == 0) a.wave_sums[(p0 >> 6) + w] = v_; } }
 #define SB __builtin_amdgcn_sched_barrier(0);
 )PLKJITM";
   snprintf(buf, sizeof(buf),
            "extern \"C\" __global__ __launch_bounds__(%d, %d) void plk_jit_treeM(JMArgs a, int frag_base) {\n", NTH,
            std::max(sh.minw, 1));
   s += buf;
-  s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PBS_] P tiles | red[64]
+  s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PBS_] P tiles | red[16 G_]
   double* red = lds + (DIRECT_ ? 0 : 2 * PBS_);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);

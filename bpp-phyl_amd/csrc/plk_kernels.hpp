@@ -542,6 +542,7 @@ struct PmatArgs {
   int n_tips, n_codes;
   int S, C;
   unsigned mask;
+  int n_req;               // branches in the request
 };
 
 // Requests of up to kPmatInline branches travel in the kernel arguments (no staging
@@ -600,6 +601,70 @@ __global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a, const PmatInline 
       double t = 0.0;
       for (int y = 0; y < S; ++y) t = __builtin_fma(Pl[x * S + y], a.init[code * S + y], t);
       out[idx] = t;
+    }
+  }
+}
+
+// K4 for 4 states: one thread per (branch, class, row x) -- its row of P (and dP, d2P) and
+// the row's entries of the tip table -- with pmat_kernel's operations in the same order
+// (bitwise its results).  pmat_kernel's workgroup per (branch, class) ran a chain of
+// dependent loads, LDS staging and barriers for 16 outputs; here each thread issues its
+// loads at once and the launch is n * C * 4 threads.
+__global__ __launch_bounds__(64) void pmat4_kernel(PmatArgs a, const PmatInline inl) {
+  constexpr int S = 4;
+  const int gid = blockIdx.x * 64 + threadIdx.x;
+  if (gid >= a.n_req * a.C * S) return;
+  const int x = gid & 3, ic = gid >> 2, i = ic / a.C, c = ic - i * a.C;
+  const int b = inl.n ? inl.branch[i] : a.branch[i];
+  const int m = inl.n ? inl.model[i] : (a.model ? a.model[i] : 0);
+  const double rc = a.rates[c];
+  const double tt = (inl.n ? inl.t[i] : a.t[i]) * rc;
+  const double* V = a.V + (size_t)m * S * S;
+  const double* Vi = a.Vinv + (size_t)m * S * S;
+  const double* lam = a.lambda + (size_t)m * S;
+  double e[S], l[S], vx[S], vi[S * S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    l[k] = lam[k];
+    vx[k] = V[x * S + k];
+  }
+#pragma unroll
+  for (int k = 0; k < S * S; ++k) vi[k] = Vi[k];
+#pragma unroll
+  for (int k = 0; k < S; ++k) e[k] = exp(l[k] * tt);
+  double p[S], dp[S], d2p[S];
+#pragma unroll
+  for (int y = 0; y < S; ++y) {
+    p[y] = 0.0;
+    dp[y] = 0.0;
+    d2p[y] = 0.0;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const double w = vx[k] * vi[k * S + y];
+      p[y] = __builtin_fma(w, e[k], p[y]);
+      if (a.mask & 6u) {
+        const double le = l[k] * e[k];
+        dp[y] = __builtin_fma(w, le, dp[y]);
+        d2p[y] = __builtin_fma(w, l[k] * le, d2p[y]);
+      }
+    }
+    if (tt == 0.0) p[y] = (x == y) ? 1.0 : 0.0;  // getPij_t: t == 0 -> identity (:428-431)
+  }
+  const size_t off = ((size_t)b * a.C + c) * S * S + x * S;
+#pragma unroll
+  for (int y = 0; y < S; ++y) {
+    if (a.mask & 1u) a.P[off + y] = p[y];
+    if (a.mask & 2u) a.dP[off + y] = rc * dp[y];
+    if (a.mask & 4u) a.d2P[off + y] = rc * rc * d2p[y];
+  }
+  // tip branch: entries x of its table rows, tipP[b][c][code][x] = sum_y P[x][y] init[code][y]
+  if (a.init && b < a.n_tips && (a.mask & 1u)) {
+    double* out = a.tipP + ((size_t)b * a.C + c) * a.n_codes * S + x;
+    for (int code = 0; code < a.n_codes; ++code) {
+      double t = 0.0;
+#pragma unroll
+      for (int y = 0; y < S; ++y) t = __builtin_fma(p[y], a.init[code * S + y], t);
+      out[code * S] = t;
     }
   }
 }

@@ -54,7 +54,8 @@ class plk_op(ct.Structure):
 
 class plk_timing(ct.Structure):
     _fields_ = [("partials_launches", ct.c_int64), ("partials_ms", ct.c_double), ("pmat_ms", ct.c_double),
-                ("root_ms", ct.c_double), ("tables_ms", ct.c_double), ("table_launches", ct.c_int64)]
+                ("root_ms", ct.c_double), ("tables_ms", ct.c_double), ("table_launches", ct.c_int64),
+                ("evaluations", ct.c_int64), ("host_us", ct.c_double * 6)]
 
 
 class plk_work(ct.Structure):
@@ -348,7 +349,8 @@ class Engine:
         t = plk_timing()
         self._chk(self.lib.plk_get_timing_ex(self.h, ct.byref(t)))
         return {"launches": t.partials_launches, "partials_ms": t.partials_ms, "pmat_ms": t.pmat_ms,
-                "root_ms": t.root_ms, "tables_ms": t.tables_ms, "table_launches": t.table_launches}
+                "root_ms": t.root_ms, "tables_ms": t.tables_ms, "table_launches": t.table_launches,
+                "evaluations": t.evaluations, "host_us": list(t.host_us)}
 
     def traversal_work(self) -> dict:
         """plk_traversal_work: node updates computed per pattern vs served by tables, and

@@ -243,6 +243,13 @@ typedef struct plk_timing {
   int64_t partials_launches;  /* traversal launches timed */
   double partials_ms, pmat_ms, root_ms, tables_ms;
   int64_t table_launches;     /* table-build launches timed */
+  /* host side of plk_evaluate (single-device handles, always on): evaluations counted and
+   * the summed wall time in microseconds of its segments -- [0] the P(t) launch call,
+   * [1] the traversal launch call, [2] the block-sum launch call, [3] the completion wait,
+   * [4] the host sum, [5] the caller's time between the end of one plk_evaluate and the
+   * start of the next */
+  int64_t evaluations;
+  double host_us[6];
 } plk_timing;
 int plk_get_timing_ex(plk_handle h, plk_timing* out);
 int plk_reset_timing(plk_handle h);

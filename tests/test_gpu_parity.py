@@ -358,6 +358,45 @@ def test_evaluate_equals_three_calls(S, C, flags):
         assert abs(lnl_e - lo) <= REL * abs(lo)
 
 
+@pytest.mark.parametrize("C,scaling,n_patterns", [(4, False, 9000), (1, False, 4096), (4, True, 5000),
+                                                   (2, False, 130)])
+def test_pmat4_and_kernel_block_sums_bitwise(C, scaling, n_patterns, monkeypatch):
+    """The 4-state K4 (pmat4_kernel: a thread per row of P) equals pmat_kernel bitwise -- P,
+    dP, d2P and, through the traversal, the tip tables -- and the JIT kernel's in-kernel
+    block sums (the wave completing a 4096-pattern block adds its 64 wave sums) equal
+    wave_sums_to_blocks' bitwise, for one, several and ragged blocks; a second root
+    reduction without a new traversal returns the same block sums."""
+    et, m, alph, rates, probs, states = _random_problem(4, C, 40, n_patterns, seed=77, amb=True)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | (plk.PLK_FLAG_SCALING if scaling else 0)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    ops = phylo.split_ops(et.ops)
+    out = {}
+    for new in ("0", "1"):
+        monkeypatch.setenv("PLK_PMAT4", new)
+        monkeypatch.setenv("PLK_JIT_BLOCKS", new)
+        eng = engine_for(et, 4, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+        eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+        mats = [np.stack([eng.get_pmatrix(int(b)) for b in br]),
+                np.stack([eng.get_dpmatrix(int(b), 1) for b in br]),
+                np.stack([eng.get_dpmatrix(int(b), 2) for b in br])]
+        res = []
+        for scale in (1.0, 1.7):
+            lnl, blocks = eng.evaluate(br, et.brlen[br] * scale, ops, et.root)
+            lnl2, _, blocks2 = eng.root_loglik(et.root, want_blocks=True)
+            assert lnl2 == lnl and np.array_equal(blocks2, blocks)
+            res.append((lnl, blocks))
+        assert eng.kernel_path() == "jit_tree4"
+        out[new] = (mats, res)
+        del eng
+    (m0, r0), (m1, r1) = out["0"], out["1"]
+    for a, b in zip(m0, m1):
+        assert np.array_equal(a, b)
+    for (l0, b0), (l1, b1) in zip(r0, r1):
+        assert l0 == l1 and np.array_equal(b0, b1)
+    lo, _ = oracle_for(et, states, alph.init_table, rates, probs, m.pi, [m], scaling=scaling)
+    assert abs(r1[0][0] - lo) <= 1e-10 * abs(lo)
+
+
 def test_get_partials_matches_recomputation():
     et, m, alph, rates, probs, states = _random_problem(4, 4, 6, 300, seed=8)
     eng = engine_for(et, 4, 4, 300, states, alph.init_table, rates, probs, m.pi, [m])
@@ -959,12 +998,13 @@ def test_jit_treeM_vs_oracle(C, tree_kind, n_patterns, scaling, mode, variant, m
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dm,L,direct,pd,hoist", [(2, 1, "0", 1, 0), (3, 2, "0", 2, 1), (4, 1, "1", 1, 0),
-                                                  (3, 1, "1", 1, 1), (4, 1, "0", 3, 0)])
-def test_jit_treeM_register_depths(dm, L, direct, pd, hoist, monkeypatch):
-    """Other fragment heights, fetch lookaheads and A-operand sources (LDS-staged / direct
-    from L1-L2) give the default kernel's results bitwise (different cuts store different
-    partials, but every operation per node is the same)."""
+@pytest.mark.parametrize("dm,L,direct,pd,hoist,g", [(2, 1, "0", 1, 0, 4), (3, 2, "0", 2, 1, 4), (4, 1, "1", 1, 0, 4),
+                                                    (3, 1, "1", 1, 1, 4), (4, 1, "0", 3, 0, 4), (4, 1, "0", 1, 0, 8),
+                                                    (3, 2, "0", 2, 0, 8)])
+def test_jit_treeM_register_depths(dm, L, direct, pd, hoist, g, monkeypatch):
+    """Other fragment heights, fetch lookaheads, A-operand sources (LDS-staged / direct
+    from L1-L2) and workgroup sizes (PLK_JITM_G) give the default kernel's results bitwise
+    (different cuts store different partials, but every operation per node is the same)."""
     et, m, alph, rates, probs, states = _random_problem(20, 4, 80, 600, seed=77, amb=True)
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
@@ -975,6 +1015,7 @@ def test_jit_treeM_register_depths(dm, L, direct, pd, hoist, monkeypatch):
     monkeypatch.setenv("PLK_JITM_DIRECT", direct)
     monkeypatch.setenv("PLK_JITM_PD", str(pd))
     monkeypatch.setenv("PLK_JITM_HOIST", str(hoist))
+    monkeypatch.setenv("PLK_JITM_G", str(g))
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
     l1, s1, _ = run_engine(eng, et)
     assert eng.kernel_path() == "jit_treeM"
