@@ -174,9 +174,12 @@ class Evaluator:
         self.model_idx = None if wl.model_of_node is None else wl.model_of_node[self.branches].astype(np.int32)
         self.ops = phylo.split_ops(et.ops)
         self.n_blocks = (end - start + plk.BLOCK - 1) // plk.BLOCK
+        self.t_tree = et.brlen[self.branches]  # the tree's own branch lengths, per branch of the request
 
     def step(self, brlen: Optional[np.ndarray] = None):
+        """One evaluation: P(t) of every branch (the tree's lengths, or `brlen` per node),
+        the traversal and the root reduction (plk_evaluate)."""
         et = self.wl.et
-        t = (et.brlen if brlen is None else brlen)[self.branches]
+        t = self.t_tree if brlen is None else brlen[self.branches]
         lnl, blocks = self.eng.evaluate(self.branches, t, self.ops, et.root, self.model_idx)
         return lnl, None, blocks

@@ -397,6 +397,35 @@ def test_pmat4_and_kernel_block_sums_bitwise(C, scaling, n_patterns, monkeypatch
     assert abs(r1[0][0] - lo) <= 1e-10 * abs(lo)
 
 
+@pytest.mark.parametrize("S,C", [(4, 4), (20, 2)])
+def test_pmat_request_paths_bitwise(S, C, monkeypatch):
+    """A P(t) request in the kernel arguments, through mapped pinned staging (default for
+    more than 160 branches) and through a stream-ordered copy of the staging give the
+    same transition matrices and lnL bitwise (NH: a model index per branch)."""
+    et, m, alph, rates, probs, states = _random_problem(S, C, 24, 700, seed=5)
+    rng = np.random.default_rng(9)
+    models = [m] + [phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5)) for _ in range(2)] \
+        if S == 4 else [m]
+    mon = rng.integers(0, len(models), et.n_nodes).astype(np.int32)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    ops = phylo.split_ops(et.ops)
+    out = []
+    for staged, mapped in (("0", "1"), ("1", "1"), ("1", "0")):
+        monkeypatch.setenv("PLK_PMAT_STAGED", staged)
+        monkeypatch.setenv("PLK_PMAT_MAPPED", mapped)
+        eng = engine_for(et, S, C, 700, states, alph.init_table, rates, probs, m.pi, models, model_of_node=mon,
+                         flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY)
+        res = []
+        for scale in (0.7, 1.4):
+            lnl, blocks = eng.evaluate(br, et.brlen[br] * scale, ops, et.root, mon[br])
+            res.append((lnl, blocks, np.stack([eng.get_pmatrix(int(b)) for b in br])))
+        out.append(res)
+        del eng
+    for other in out[1:]:
+        for (l0, b0, p0), (l1, b1, p1) in zip(out[0], other):
+            assert l0 == l1 and np.array_equal(b0, b1) and np.array_equal(p0, p1)
+
+
 def test_get_partials_matches_recomputation():
     et, m, alph, rates, probs, states = _random_problem(4, 4, 6, 300, seed=8)
     eng = engine_for(et, 4, 4, 300, states, alph.init_table, rates, probs, m.pi, [m])
