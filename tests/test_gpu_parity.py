@@ -426,6 +426,39 @@ def test_pmat_request_paths_bitwise(S, C, monkeypatch):
             assert l0 == l1 and np.array_equal(b0, b1) and np.array_equal(p0, p1)
 
 
+@pytest.mark.parametrize("S,C,n_taxa,scaling", [(4, 4, 64, False), (4, 4, 40, True), (20, 4, 40, True),
+                                                 (64, 1, 24, False)])
+def test_zero_and_long_branches_vs_oracle(S, C, n_taxa, scaling):
+    """Branch lengths the P(t) kernels treat specially: t = 0 (getPij_t returns the identity,
+    AbstractSubstitutionModel.cpp:428-431) on internal and tip branches, and t = 60
+    (every row at the stationary distribution, P far from the identity) -- through the
+    benched lnL-only fused kernels, against the oracle on the engine's own P(t) at 1e-12
+    and on the oracle's P(t) at 1e-10."""
+    et, m, alph, rates, probs, states = _random_problem(S, C, n_taxa, 1500, seed=S + n_taxa, amb=True)
+    rng = np.random.default_rng(S)
+    # zero: a sixth of the internal branches and one tip in each of a few cherries (never
+    # both tips of a cherry, which could make a site likelihood exactly 0)
+    internal = rng.permutation([n for n in range(et.n_tips, et.n_nodes) if n != et.root])
+    zero = list(internal[: len(internal) // 6])
+    for parent, kids in et.ops[:4]:
+        if all(k < et.n_tips for k in kids):
+            zero.append(int(kids[0]))
+    long_ = [int(n) for n in internal[len(internal) // 6: len(internal) // 6 + 3]]
+    et.brlen[zero] = 0.0
+    et.brlen[long_] = 60.0
+    pick = np.array(zero)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, S, C, 1500, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+    lnl, site, _ = run_engine(eng, et)
+    for b in pick:
+        assert np.array_equal(eng.get_pmatrix(int(b)), np.broadcast_to(np.eye(S), (C, S, S)))
+    lo, so = oracle_for(et, states, alph.init_table, rates, probs, m.pi, [m], scaling=scaling,
+                        pmats=engine_pmats(eng, et))
+    check(lnl, site, lo, so)
+    lo2, _ = oracle_for(et, states, alph.init_table, rates, probs, m.pi, [m], scaling=scaling)
+    assert abs(lnl - lo2) <= 1e-10 * abs(lo2)
+
+
 def test_get_partials_matches_recomputation():
     et, m, alph, rates, probs, states = _random_problem(4, 4, 6, 300, seed=8)
     eng = engine_for(et, 4, 4, 300, states, alph.init_table, rates, probs, m.pi, [m])
