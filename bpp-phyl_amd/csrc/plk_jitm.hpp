@@ -59,7 +59,7 @@ struct JMArgs {
   double* partials; i32* scale; const u8* codes; const double* tipP; const u8* cherry; const double* pmats;
   const double* weights; const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i64 cherry_stride; i64 cherry_table_bytes; i64 cherry_count_bytes;
-  i32 guard;
+  i32 guard; i64 p_base;  // p_base: first pattern of the launch (pattern chunks)
 };
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
@@ -96,6 +96,7 @@ struct JMArgs {
   int64_t cherry_table_bytes;
   int64_t cherry_count_bytes;
   int32_t guard;
+  int64_t p_base;
 };
 
 struct JitMShape {
@@ -265,7 +266,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 4, pl = lane & 15;
-  const i64 p0 = (i64)blockIdx.x * (16 * G_);
+  const i64 p0 = a.p_base + (i64)blockIdx.x * (16 * G_);
   const i64 p = p0 + 16 * w + pl;
   const i64 toff = (p >> 7) * (i64)(C_ * S_ * kTile) + (p & (kTile - 1)) + (i64)hi * kTile;
   const double* PA = lds + ((hi << 2) | (lane & 3));

@@ -1085,6 +1085,33 @@ def test_jit_treeM_register_depths(dm, L, direct, pd, hoist, g, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("chunks", ["2", "3", "5"])
+def test_jit_treeM_chunked_tiers_bitwise(chunks, monkeypatch):
+    """Two-tier jit_treeM launched in pattern chunks pipelined over two streams
+    (PLK_JITM_CHUNKS) gives the one-launch-per-tier results bitwise: lnL, per-pattern lnL
+    and block sums, on a ragged pattern count, twice in a row (the second stream's work is
+    ordered before the next evaluation)."""
+    n = 3 * 4096 + 1000
+    et, m, alph, rates, probs, states = _random_problem(20, 4, 256, n, seed=31, amb=True)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    ops = phylo.split_ops(et.ops)
+    out = {}
+    for k in ("1", chunks):
+        monkeypatch.setenv("PLK_JITM_CHUNKS", k)
+        eng = engine_for(et, 20, 4, n, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+        res = [eng.evaluate(br, et.brlen[br] * s, ops, et.root) for s in (1.0, 1.3)]
+        _, site, _ = eng.root_loglik(et.root, want_sites=True)
+        assert eng.kernel_path() == "jit_treeM"
+        out[k] = (res, site)
+        del eng
+    (r0, s0), (r1, s1) = out["1"], out[chunks]
+    for (l0, b0), (l1, b1) in zip(r0, r1):
+        assert l0 == l1 and np.array_equal(b0, b1)
+    assert np.array_equal(s0, s1)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode,nh", [
     (4, "balanced64", 3000, False, "lnl_only", False), (4, "balanced64", 1000, False, "materialize", False),
     (2, "caterpillar40", 700, True, "lnl_only", False), (4, "balanced300", 513, True, "lnl_only", True),
