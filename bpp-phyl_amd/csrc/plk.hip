@@ -246,6 +246,8 @@ struct plk_handle_s {
   double* d_blk_local = nullptr;          // [comm_cmax] this rank's block sums (zero padded)
   unsigned* d_blk_cnt = nullptr;          // [n_blocks] arrival counters of the in-kernel block sums
   hipStream_t stream2 = nullptr;          // second stream of the chunked two-tier jit_treeM launch
+  DrPreOp* d_drpre = nullptr;             // fused DR preorder ops (dr_pre_s4_kernel)
+  size_t d_drpre_cap = 0;
   std::vector<hipEvent_t> chunk_events;
   double* d_blk_all = nullptr;            // [comm_ranks][comm_cmax]
   int64_t* d_comm_counts = nullptr;       // block sums per rank
@@ -894,7 +896,7 @@ int plk_destroy(plk_handle h) {
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
-                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_blk_cnt};
+                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_blk_cnt, h->d_drpre};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->stream2) {
@@ -2904,6 +2906,102 @@ void topo_postorder(plk_handle h, int root, std::vector<plk_op>& ops) {
 // levelwise preorder pass of ordinary partial updates into the U slots, then one
 // reduction launch over all branches (computeTreeDLikelihoods / D2 twins :287-423).
 // ---------------------------------------------------------------------------
+// Row f4 for 4 states without rescaling: dr_pre_s4_kernel level by level (fathers of
+// depth d in one launch), then the fixed-order sums of the per-block branch terms.
+int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth, const std::vector<int>& parent,
+                      int root, double* d1, double* d2) {
+  const int C = h->C, nt = h->n_tips, nn = h->n_nodes;
+  (void)parent;
+  std::vector<DrBranch> br;  // one row per branch (dr_sum_kernel's node map)
+  std::vector<int> bidx(nn, -1);
+  for (size_t d = 1; d < depth.size(); ++d)
+    for (int v : depth[d]) {
+      DrBranch b;
+      std::memset(&b, 0, sizeof(b));
+      b.node = v;
+      bidx[v] = (int)br.size();
+      br.push_back(b);
+    }
+  std::vector<DrPreOp> ops;
+  std::vector<std::pair<size_t, int> > levels;
+  for (size_t d = 0; d + 1 < depth.size(); ++d) {
+    const size_t first = ops.size();
+    for (int f : depth[d]) {
+      if (f < nt) continue;
+      DrPreOp op;
+      std::memset(&op, 0, sizeof(op));
+      op.f = f;
+      op.uf_slot = f == root ? -1 : h->dr_slot0 + f;
+      for (int v : h->topo_kids[f]) {
+        const int j = op.n++;
+        op.son[j] = v;
+        op.is_tip[j] = v < nt;
+        op.idx[j] = v < nt ? v : v - nt;
+        op.uslot[j] = v < nt ? -1 : h->dr_slot0 + v;
+        op.bidx[j] = bidx[v];
+      }
+      ops.push_back(op);
+    }
+    if (ops.size() > first) levels.push_back(std::make_pair(first, (int)(ops.size() - first)));
+  }
+  const int n_blk = (int)(h->n_pad / kDrThreads);
+  int rc;
+  if ((rc = ensure_cap(h, (void**)&h->d_drb, &h->d_drb_cap, br.size() * sizeof(DrBranch)))) return rc;
+  if ((rc = ensure_cap(h, (void**)&h->d_drpre, &h->d_drpre_cap, ops.size() * sizeof(DrPreOp)))) return rc;
+  if ((rc = ensure_cap(h, (void**)&h->dr_blk, &h->dr_blk_cap, 2 * br.size() * n_blk * sizeof(double)))) return rc;
+  if (!h->dr_out && (rc = dalloc(h, (void**)&h->dr_out, 2 * (size_t)nn * sizeof(double)))) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->d_drb, br.data(), br.size() * sizeof(DrBranch), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->d_drpre, ops.data(), ops.size() * sizeof(DrPreOp), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->dr_out, 0, 2 * (size_t)nn * sizeof(double), h->stream));
+  DrArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.partials = h->partials;
+  a.codes = h->codes;
+  a.code_table = h->code_table;
+  a.pmats = h->pmats;
+  a.dpmats = h->dpmats;
+  a.d2pmats = h->d2pmats;
+  a.pi = h->pi;
+  a.probs = h->probs;
+  a.weights = h->weights;
+  a.tipP = h->tipP;
+  a.n_codes = h->n_codes;
+  a.blk1 = h->dr_blk;
+  a.blk2 = h->dr_blk + br.size() * n_blk;
+  a.slot_stride = h->slot_stride;
+  a.n_pad = h->n_pad;
+  a.n_patterns = h->n_patterns;
+  a.C = C;
+  a.n_blk = n_blk;
+  EventPair ev;
+  if (h->timing & PLK_TIME_PARTIALS) {
+    ev = get_events(h, 0);
+    hipEventRecord(ev.a, h->stream);
+  }
+  for (const auto& l : levels) {
+    const dim3 grid((unsigned)n_blk, (unsigned)l.second);
+    const DrPreOp* o = h->d_drpre + l.first;
+    switch (C) {
+      case 1: dr_pre_s4_kernel<1><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+      case 2: dr_pre_s4_kernel<2><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+      case 4: dr_pre_s4_kernel<4><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+    }
+    HIPCHK(h, hipGetLastError());
+  }
+  if (h->timing & PLK_TIME_PARTIALS) {
+    hipEventRecord(ev.b, h->stream);
+    h->events.push_back(ev);
+  }
+  dr_sum_kernel<<<(unsigned)br.size(), 256, 0, h->stream>>>(h->d_drb, a.blk1, a.blk2, n_blk, h->dr_out, h->dr_out + nn);
+  HIPCHK(h, hipGetLastError());
+  std::vector<double> out(2 * (size_t)nn);
+  HIPCHK(h, hipMemcpyAsync(out.data(), h->dr_out, out.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (d1) std::copy(out.begin(), out.begin() + nn, d1);
+  if (d2) std::copy(out.begin() + nn, out.end(), d2);
+  return PLK_OK;
+}
+
 int dr_derivatives(plk_handle h, double* d1, double* d2) {
   if (!(h->flags & PLK_FLAG_DOUBLE_RECURSIVE))
     return fail(h, PLK_ERR_STATE, "handle was not created with PLK_FLAG_DOUBLE_RECURSIVE");
@@ -2948,6 +3046,14 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   }
   if ((rc = refresh_tip_tables(h))) return rc;
   if ((S == 20 || S == 64) && (rc = ensure_pmatsT(h))) return rc;
+  // 4 states without rescaling: the fused preorder (dr_pre_s4_kernel), one launch per
+  // level of fathers, branch terms reduced where U is formed (PLK_DR_PRE=0: the
+  // levelwise preorder + reduction below)
+  bool pre = S == 4 && !(h->flags & PLK_FLAG_SCALING) && (C == 1 || C == 2 || C == 4) && !env_is("PLK_DR_PRE", '0');
+  for (size_t d = 0; pre && d < depth.size(); ++d)
+    for (int f : depth[d])
+      if (f >= nt && (h->topo_kids[f].size() < 2 || h->topo_kids[f].size() > 3)) pre = false;
+  if (pre) return dr_fused_preorder(h, depth, parent, root, d1, d2);
   // M_f for every internal father below the root
   std::vector<int2> mlist;
   for (size_t d = 1; d < depth.size(); ++d)

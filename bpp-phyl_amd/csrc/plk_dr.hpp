@@ -15,6 +15,10 @@
 // whose "transition matrix" is M_f -- so the preorder pass reuses the levelwise S=4,
 // S=20 (SGPR) and S=64 (MFMA) paths as they are, rescaling included.
 //
+// 4 states without rescaling take the fused form instead (dr_pre_s4_kernel below): the
+// father-side vectors stay in registers within a father's op and the branch terms are
+// reduced where they are formed.
+//
 // Per branch and pattern the reduction below forms
 //     l = sum_c p_c sum_y u[c][y] (P_v L_v)[c][y],   u = U_v (x pi at the root's children)
 // and l', l'' with r_c dP_v and r_c^2 d2P_v in place of P_v (lnL is linear in P_v), then
@@ -352,6 +356,193 @@ __global__ __launch_bounds__(kDrmThreads) void dr_branch_mfma_kernel(const DrBra
 
 // Per branch: the fixed-order sum of its block sums (strided partial sums, then a
 // fixed LDS tree), written to out1/out2[node].
+// ---------------------------------------------------------------------------
+// Fused preorder for 4 states without rescaling: one launch per preorder level, one
+// workgroup = 256 patterns of one father f.  Per class the father-side vector of f's sons
+// is formed in registers,
+//     MU = pi (f the root) or P_f^T U_f,   Q_j = P_j L_j,   U_i = MU (*) prod_{j != i} Q_j,
+// U_i is stored only for an internal son (its own sons read it at the next level), and
+// son i's branch terms l, l', l'' (Q_i, dP_i L_i, d2P_i L_i against U_i) are reduced right
+// there -- the separate reduction pass, which re-read every U_v and L_v, disappears
+// (cfg2: 64.7 -> ~23.5 KB of HBM traffic per pattern).  pi sits in the root sons' U
+// instead of in M_f, so results equal dr_branch_kernel's to rounding, not bitwise.
+struct DrPreOp {      // (field order is read as 18 int32 by dr_pre_s4_kernel)
+  int32_t f;          // father node (its P for P_f^T)
+  int32_t uf_slot;    // slot of U_f; -1: f is the root
+  int32_t n;          // sons (2 or 3)
+  int32_t son[3];     // son node (P, dP, d2P index)
+  int32_t is_tip[3];
+  int32_t idx[3];     // tip index or internal slot of the son's L
+  int32_t uslot[3];   // slot receiving U_son (internal sons), -1: not stored
+  int32_t bidx[3];    // the son's branch row in blk1 / blk2
+};
+
+// (the op and the wave-uniform matrices are read through the constant address space:
+// scalar loads into SGPRs -- through plain pointers the U stores would make every later
+// matrix read a per-lane vector load, as the compiler cannot rule out aliasing)
+typedef __attribute__((address_space(4))) const double* DrCPd;
+template <int C>
+// (part / uout: the partial slots read (L, U_f) and written (U of internal sons) -- never
+// the same slot within a launch, so both are restrict and the next class's loads may be
+// scheduled above this class's stores)
+__global__ __launch_bounds__(kDrThreads) void dr_pre_s4_kernel(const DrPreOp* __restrict__ ops, DrArgs a,
+                                                               const double* __restrict__ part,
+                                                               double* __restrict__ uout) {
+  constexpr int S = 4;
+  __shared__ double red[2][3][kDrThreads / 64];
+  typedef __attribute__((address_space(4))) const int32_t* DrCI;
+  const DrCI w = (DrCI)(ops + blockIdx.y);
+  DrPreOp op;
+  op.f = w[0];
+  op.uf_slot = w[1];
+  op.n = w[2];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    op.son[j] = w[3 + j];
+    op.is_tip[j] = w[6 + j];
+    op.idx[j] = w[9 + j];
+    op.uslot[j] = w[12 + j];
+    op.bidx[j] = w[15 + j];
+  }
+  const int64_t p = (int64_t)blockIdx.x * kDrThreads + threadIdx.x;
+  const bool live = p < a.n_patterns;
+  const int64_t tile = p >> 7, q = p & (kTile - 1);
+  double l0[3] = {0.0, 0.0, 0.0}, l1[3] = {0.0, 0.0, 0.0}, l2[3] = {0.0, 0.0, 0.0};
+  // operand sources per son: a tip's code-table row (the same for every class) or the
+  // internal son's partial; a missing third son aliases son 0 (loaded, never used).  The
+  // next class's operands are loaded before this class's arithmetic and stores.
+  const int64_t tb = (int64_t)tile * C * S * kTile + q;
+  const double* sb[3];
+  int64_t sst[3], scs[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int jj = j < op.n ? j : 0;
+    if (op.is_tip[jj]) {
+      sb[j] = a.code_table + (int64_t)a.codes[(int64_t)op.idx[jj] * a.n_pad + p] * S;
+      sst[j] = 1;
+      scs[j] = 0;
+    } else {
+      sb[j] = part + (int64_t)op.idx[jj] * a.slot_stride + tb;
+      sst[j] = kTile;
+      scs[j] = S * kTile;
+    }
+  }
+  const bool root = op.uf_slot < 0;
+  const double* ub = part + (int64_t)(root ? 0 : op.uf_slot) * a.slot_stride + tb;
+  double Lb[2][3][S], Ub[2][S];
+  auto load = [&](int c, int bf) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int z = 0; z < S; ++z) Lb[bf][j][z] = sb[j][c * scs[j] + z * sst[j]];
+    if (!root)
+#pragma unroll
+      for (int y = 0; y < S; ++y) Ub[bf][y] = ub[(int64_t)c * S * kTile + (int64_t)y * kTile];
+  };
+  load(0, 0);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int bf = c & 1;
+    if (c + 1 < C) load(c + 1, bf ^ 1);
+    const int64_t co = tb + (int64_t)c * S * kTile;
+    double mu[S];
+    if (root) {
+#pragma unroll
+      for (int x = 0; x < S; ++x) mu[x] = ((DrCPd)a.pi)[x];
+    } else {
+      const DrCPd Pf = (DrCPd)(a.pmats + ((int64_t)op.f * C + c) * S * S);
+#pragma unroll
+      for (int x = 0; x < S; ++x) {
+        double t = 0.0;
+#pragma unroll
+        for (int y = 0; y < S; ++y) t = fma(Pf[y * S + x], Ub[bf][y], t);
+        mu[x] = t;
+      }
+    }
+    double Q[3][S];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j >= op.n) continue;
+      const DrCPd P = (DrCPd)(a.pmats + ((int64_t)op.son[j] * C + c) * S * S);
+#pragma unroll
+      for (int x = 0; x < S; ++x) {
+        double t = 0.0;
+#pragma unroll
+        for (int z = 0; z < S; ++z) t = fma(P[x * S + z], Lb[bf][j][z], t);
+        Q[j][x] = t;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i >= op.n) continue;
+      double u[S];
+#pragma unroll
+      for (int x = 0; x < S; ++x) {
+        double t = mu[x];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          if (j != i && j < op.n) t *= Q[j][x];
+        u[x] = t;
+      }
+      if (op.uslot[i] >= 0) {
+        double* dst = uout + (int64_t)op.uslot[i] * a.slot_stride + co;
+#pragma unroll
+        for (int x = 0; x < S; ++x) dst[(int64_t)x * kTile] = u[x];
+      }
+      const DrCPd D1 = (DrCPd)(a.dpmats + ((int64_t)op.son[i] * C + c) * S * S);
+      const DrCPd D2 = (DrCPd)(a.d2pmats + ((int64_t)op.son[i] * C + c) * S * S);
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int x = 0; x < S; ++x) {
+        double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+        for (int z = 0; z < S; ++z) {
+          t1 = fma(D1[x * S + z], Lb[bf][i][z], t1);
+          t2 = fma(D2[x * S + z], Lb[bf][i][z], t2);
+        }
+        s0 = fma(u[x], Q[i][x], s0);
+        s1 = fma(u[x], t1, s1);
+        s2 = fma(u[x], t2, s2);
+      }
+      const double pc = ((DrCPd)a.probs)[c];
+      l0[i] = fma(pc, s0, l0[i]);
+      l1[i] = fma(pc, s1, l1[i]);
+      l2[i] = fma(pc, s2, l2[i]);
+    }
+  }
+  const int wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (i >= op.n) continue;
+    double r1 = 0.0, r2 = 0.0;
+    if (live) {
+      const double g = l1[i] / l0[i], hh = l2[i] / l0[i];
+      r1 = a.weights[p] * g;
+      r2 = a.weights[p] * (hh - g * g);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      r1 += __shfl_xor(r1, off, 64);
+      r2 += __shfl_xor(r2, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      red[0][i][wv] = r1;
+      red[1][i][wv] = r2;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 && (int)threadIdx.x < op.n) {
+    const int i = threadIdx.x;
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < kDrThreads / 64; ++k) {  // fixed order
+      t1 += red[0][i][k];
+      t2 += red[1][i][k];
+    }
+    a.blk1[(size_t)op.bidx[i] * a.n_blk + blockIdx.x] = t1;
+    a.blk2[(size_t)op.bidx[i] * a.n_blk + blockIdx.x] = t2;
+  }
+}
+
 __global__ __launch_bounds__(256) void dr_sum_kernel(const DrBranch* __restrict__ branches, const double* __restrict__ blk1,
                                                      const double* __restrict__ blk2, int n_blk, double* __restrict__ out1,
                                                      double* __restrict__ out2) {

@@ -4,12 +4,16 @@ what RHomogeneousTreeLikelihood does per BrLen parameter).
 
     python tools/bench_dr.py --config gtr_g4_dna_1M_64 [--patterns N] [--reps K]
 
-One JSON line: branch x pattern derivative updates/s for both, the DR reduction kernel's
-HIP-event duration and its algorithmic HBM rate.  Algorithmic bytes of one DR pass
-(per pattern): every upper vector U_v written once (8 C S) and read by the reduction
-(8 C S); the preorder update of U_v reads U_father (8 C S, not at the root's sons) and
-every sibling (8 C S internal, 1 B tip); the reduction reads L_v (8 C S internal, 1 B
-tip) and the weight (8 B).
+One JSON line: branch x pattern derivative updates/s for both, the DR kernels' HIP-event
+duration and their algorithmic HBM rate.  Two engine paths (`dr_path`):
+  * fused (4 states without rescaling, dr_pre_s4_kernel): per father f, U_f read (8 C S,
+    not at the root), every son's L (8 C S internal, 1 B tip), the U of internal sons
+    written (8 C S), the weight (8 B);
+  * levelwise (otherwise, or PLK_DR_PRE=0): every upper vector U_v written once (8 C S)
+    and read by the reduction (8 C S); the preorder update of U_v reads U_father (8 C S,
+    not at the root's sons) and every sibling (8 C S internal, 1 B tip); the reduction
+    reads L_v (8 C S internal, 1 B tip) and the weight (8 B) -- `reduction_kernel_ms` and
+    `reduction_roofline` then time the reduction launch alone.
 """
 import argparse
 import json
@@ -35,6 +39,16 @@ def dr_bytes(wl):
         up += sum(CS8 if s >= et.n_tips else 1 for s in kids[f] if s != v)
         red += CS8 + (CS8 if v >= et.n_tips else 1) + 8
     return up, red
+
+
+def dr_fused_bytes(wl):
+    et = wl.et
+    CS8 = 8 * wl.C * wl.S
+    b = 0
+    for f, ch in et.ops:
+        b += (CS8 if f != et.root else 0) + 8
+        b += sum(2 * CS8 if s >= et.n_tips else 1 for s in ch)
+    return b
 
 
 def main():
@@ -72,6 +86,8 @@ def main():
         worst = max(worst, abs(p1 - d1[b]) / max(1.0, abs(p1)), abs(p2 - d2[b]) / max(1.0, abs(p2)))
     t_path = (time.perf_counter() - t0) / len(sel) * nb
     up, red = dr_bytes(wl)
+    fused = wl.S == 4 and not wl.scaling and os.environ.get("PLK_DR_PRE", "1") != "0"
+    fb = dr_fused_bytes(wl)
     rec = {
         "metric": "branch x site-pattern derivative updates/s (d1 and d2 of every branch)",
         "config": args.config, "patterns": P, "branches": nb, "states": wl.S, "classes": wl.C, "lnl": lnl,
@@ -80,13 +96,21 @@ def main():
         "speedup_dr_vs_path": t_path / t_dr,
         "path_branches_timed": int(len(sel)),
         "max_rel_diff_dr_vs_path": worst,
-        "reduction_kernel_ms": red_ms,
-        "reduction_roofline": {"bound": "hbm", "achieved": red * P / (red_ms * 1e-3) / 1e9, "peak": 8000.0,
-                               "unit": "GB/s", "frac": red * P / (red_ms * 1e-3) / 1e9 / 8000.0,
-                               "algorithmic_bytes_per_pattern": red},
-        "dr_pass_algorithmic_GBps": (up + red) * P / t_dr / 1e9,
-        "preorder_bytes_per_pattern": up,
+        "dr_path": "fused" if fused else "levelwise",
     }
+    if fused:
+        rec["fused_kernels_ms"] = red_ms
+        rec["fused_roofline"] = {"bound": "hbm", "achieved": fb * P / (red_ms * 1e-3) / 1e9, "peak": 8000.0,
+                                 "unit": "GB/s", "frac": fb * P / (red_ms * 1e-3) / 1e9 / 8000.0,
+                                 "algorithmic_bytes_per_pattern": fb}
+        rec["levelwise_bytes_per_pattern"] = up + red
+    else:
+        rec["reduction_kernel_ms"] = red_ms
+        rec["reduction_roofline"] = {"bound": "hbm", "achieved": red * P / (red_ms * 1e-3) / 1e9, "peak": 8000.0,
+                                     "unit": "GB/s", "frac": red * P / (red_ms * 1e-3) / 1e9 / 8000.0,
+                                     "algorithmic_bytes_per_pattern": red}
+        rec["dr_pass_algorithmic_GBps"] = (up + red) * P / t_dr / 1e9
+        rec["preorder_bytes_per_pattern"] = up
     print(json.dumps(rec), flush=True)
 
 
