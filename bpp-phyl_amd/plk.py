@@ -69,6 +69,7 @@ class plk_comm_id(ct.Structure):
 
 
 _lib = None
+ABI_VERSION = 2  # include/plk.h PLK_ABI_VERSION
 
 
 def load(path: str = LIB_PATH) -> ct.CDLL:
@@ -123,6 +124,8 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res
+    if lib.plk_abi_version() != ABI_VERSION:  # the structs above mirror this version of plk.h
+        raise RuntimeError(f"{path}: ABI version {lib.plk_abi_version()}, this binding needs {ABI_VERSION}")
     _lib = lib
     return lib
 

@@ -55,7 +55,9 @@
 extern "C" {
 #endif
 
-#define PLK_ABI_VERSION 1
+/* 2: plk_timing gained `evaluations` and `host_us` (a caller built against 1 must not pass
+ * its smaller struct to plk_get_timing_ex) */
+#define PLK_ABI_VERSION 2
 
 enum {
   PLK_OK = 0,

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_and_reports_version():
     _ensure_built()
     lib = plk.load()
-    assert lib.plk_abi_version() == 1
+    assert lib.plk_abi_version() == 2
     assert lib.plk_block_size() == 4096
 
 
