@@ -225,7 +225,7 @@ struct plk_handle_s {
   // (an incremental call lists only the ancestors of changed branches)
   std::vector<std::vector<int> > topo_kids;
   // double-recursive derivatives (PLK_FLAG_DOUBLE_RECURSIVE, plk_dr.hpp)
-  int n_mats = 0;        // transition-matrix slots: nodes, 2 derivative scratch, DR M_f per node
+  int n_mats = 0;        // transition-matrix slots: nodes, kScratchMats derivative scratch, DR M_f per node
   int dr_slot0 = 0;      // partial slot of U_v = dr_slot0 + v
   DrBranch* d_drb = nullptr;
   size_t d_drb_cap = 0;
@@ -486,7 +486,11 @@ int jit_function(plk_handle h, const std::string& src, const char* name, hipFunc
 
 bool s4_supported(int C) { return C == 1 || C == 2 || C == 4 || C == 8; }
 
-constexpr int kDerivScratch = 4;  // partial slots: dL ping-pong, d2L ping-pong
+// derivative scratch: partial slots (path derivatives: dL ping-pong, d2L ping-pong; root-pair
+// derivatives: five substituted root products), transition matrices and tip rows
+constexpr int kDerivScratch = 6;
+constexpr int kScratchMats = 4;
+constexpr int kScratchTips = 4;
 
 template <bool SCALE>
 void launch_s4(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
@@ -517,7 +521,7 @@ int ensure_pmatsT(plk_handle h) {
     h->pmatsT_dirty = true;
   }
   if (h->pmatsT_dirty) {
-    const dim3 grid(h->n_nodes + 2, h->C);  // + the derivative scratch matrices
+    const dim3 grid(h->n_nodes + kScratchMats, h->C);  // + the derivative scratch matrices
     if (h->S == 64)
       transpose_pmats<64><<<grid, 256, 0, h->stream>>>(h->pmats, h->pmatsT, h->C);
     else if (h->S == 20)
@@ -819,7 +823,7 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   h->n_blocks = (int)((n_patterns + kRootBlock - 1) / kRootBlock);
   h->slot_stride = (int64_t)h->n_tiles * n_classes * n_states * kTile;
   const bool dr = (flags & PLK_FLAG_DOUBLE_RECURSIVE) != 0;
-  h->n_mats = h->n_nodes + 2 + (dr ? h->n_nodes : 0);
+  h->n_mats = h->n_nodes + kScratchMats + (dr ? h->n_nodes : 0);
   h->dr_slot0 = n_internal + kDerivScratch;
   const int n_slots = n_internal + kDerivScratch + (dr ? h->n_nodes : 0);
   h->topo_kids.assign(h->n_nodes, std::vector<int>());
@@ -835,14 +839,15 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(nullptr, PLK_ERR_DEVICE, "hipStreamCreate failed"));
   const size_t S2 = (size_t)n_states * n_states;
-  // kDerivScratch extra slots / scale rows, 2 extra tip rows and 2 extra transition
-  // matrices: scratch for the path derivatives of plk_branch_derivatives (S != 4 path);
+  // kDerivScratch extra slots / scale rows, kScratchTips extra tip rows and kScratchMats
+  // extra transition matrices: scratch for the path derivatives of plk_branch_derivatives (S != 4 path) and
+  // plk_root_pair_derivatives;
   // with PLK_FLAG_DOUBLE_RECURSIVE one more slot and matrix per node (U_v, M_f)
   if ((rc = dalloc(h, (void**)&h->partials, (size_t)n_slots * h->slot_stride * sizeof(double)))) return bail(rc);
   if (flags & PLK_FLAG_SCALING) {
     if ((rc = dalloc(h, (void**)&h->scale, (size_t)n_slots * h->n_pad * sizeof(int32_t)))) return bail(rc);
   }
-  if ((rc = dalloc(h, (void**)&h->codes, (size_t)(n_tips + 2) * h->n_pad))) return bail(rc);
+  if ((rc = dalloc(h, (void**)&h->codes, (size_t)(n_tips + kScratchTips) * h->n_pad))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->pmats, (size_t)h->n_mats * n_classes * S2 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->V, (size_t)n_models * S2 * sizeof(double)))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->Vinv, (size_t)n_models * S2 * sizeof(double)))) return bail(rc);
@@ -985,7 +990,7 @@ int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec) {
   h->tipP = nullptr;
   int rc;
   if ((rc = dalloc(h, (void**)&h->code_table, (size_t)n_codes * h->S * sizeof(double)))) return rc;
-  if ((rc = dalloc(h, (void**)&h->tipP, (size_t)(h->n_tips + 2) * h->C * n_codes * h->S * sizeof(double))))
+  if ((rc = dalloc(h, (void**)&h->tipP, (size_t)(h->n_tips + kScratchTips) * h->C * n_codes * h->S * sizeof(double))))
     return rc;
   h->code_table_host.assign(code_to_vec, code_to_vec + (size_t)n_codes * h->S);
   h->n_codes_table = n_codes;
@@ -2827,6 +2832,116 @@ int path_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   return PLK_OK;
 }
 
+// plk_root_pair_derivatives: the five root products with dP / d2P substituted on the two
+// root sons a and b (scratch matrices and, for tip sons, scratch tip rows), formed by the
+// levelwise partial kernels into scratch slots, then pair_reduce_kernel (plk_deriv.hpp).
+int root_pair_derivatives(plk_handle h, int a, int b, double alpha, double beta, double* d1, double* d2) {
+  if (a == b || a < 0 || b < 0 || a >= h->n_nodes || b >= h->n_nodes)
+    return fail(h, PLK_ERR_ARG, "bad root sons %d, %d", a, b);
+  for (int x : {a, b})
+    if (h->deriv_valid.empty() || !h->deriv_valid[x])
+      return fail(h, PLK_ERR_STATE, "dP/d2P of branch %d not computed (PLK_DERIV_DP | PLK_DERIV_D2P)", x);
+  if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
+  if (h->trav_ops.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet (plk_update_partials)");
+  hipSetDevice(h->device);
+  const int nt = h->n_tips;
+  std::vector<int> parent(h->n_nodes, -1);
+  for (int n = 0; n < h->n_nodes; ++n)
+    for (int c : h->topo_kids[n]) parent[c] = n;
+  const int root = parent[a];
+  if (root < 0 || parent[b] != root || parent[root] >= 0)
+    return fail(h, PLK_ERR_ARG, "branches %d and %d are not both sons of the traversal's root", a, b);
+  const std::vector<int>& ks = h->topo_kids[root];
+  bool need = !h->materialized[root - nt] || ((h->flags & PLK_FLAG_SUBTREE_PATTERNS) && !h->slots_expanded);
+  for (int c : ks)
+    if (c >= nt && !h->materialized[c - nt]) need = true;
+  int rc;
+  if (need && (rc = materialize_last_traversal(h))) return rc;
+  if ((rc = refresh_tip_tables(h))) return rc;
+  const int C = h->C, S = h->S, nc = h->n_codes;
+  const size_t PS = (size_t)C * S * S;
+  // scratch matrices / tip rows: 0 dP_a, 1 d2P_a, 2 dP_b, 3 d2P_b
+  const int son[4] = {a, a, b, b};
+  const double* src[4] = {h->dpmats, h->d2pmats, h->dpmats, h->d2pmats};
+  for (int x = 0; x < 4; ++x) {
+    const int sm = h->n_nodes + x, st = nt + x;
+    HIPCHK(h, hipMemcpyAsync(h->pmats + (size_t)sm * PS, src[x] + (size_t)son[x] * PS, PS * sizeof(double),
+                             hipMemcpyDeviceToDevice, h->stream));
+    if (son[x] < nt) {
+      HIPCHK(h, hipMemcpyAsync(h->codes + (size_t)st * h->n_pad, h->codes + (size_t)son[x] * h->n_pad,
+                               (size_t)h->n_pad, hipMemcpyDeviceToDevice, h->stream));
+      tip_table_kernel<<<dim3(1, C), 256, 0, h->stream>>>(h->pmats + (size_t)sm * PS, h->code_table,
+                                                          h->tipP + (size_t)st * C * nc * S, 1, C, S, nc);
+      HIPCHK(h, hipGetLastError());
+    }
+  }
+  h->pmatsT_dirty = true;
+  // variant v: scratch index substituted on a and on b (-1 = the son's own P)
+  const int sub[5][2] = {{0, -1}, {-1, 2}, {1, -1}, {-1, 3}, {0, 2}};
+  const int slot0 = h->n_internal;
+  std::vector<KOp> flat;
+  const size_t n_chunks = (ks.size() + 2) / 3;
+  for (size_t k0 = 0; k0 < ks.size(); k0 += 3)
+    for (int v = 0; v < 5; ++v) {
+      KOp op;
+      std::memset(&op, 0, sizeof(op));
+      op.parent = slot0 + v;
+      op.flags = k0 == 0 ? 0 : PLK_OP_ACCUMULATE;
+      for (size_t k = k0; k < ks.size() && k < k0 + 3; ++k) {
+        const int c = ks[k], j = op.n++;
+        const int x = c == a ? sub[v][0] : c == b ? sub[v][1] : -1;
+        op.is_tip[j] = c < nt;
+        op.child[j] = c < nt ? (x >= 0 ? nt + x : c) : c - nt;
+        op.branch[j] = x >= 0 ? h->n_nodes + x : c;
+      }
+      flat.push_back(op);
+    }
+  if ((rc = ensure_cap(h, (void**)&h->d_ops, &h->d_ops_cap, flat.size() * sizeof(KOp)))) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->d_ops, flat.data(), flat.size() * sizeof(KOp), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->last_ops.clear();  // d_ops now holds these ops, not the levelwise traversal's
+  for (size_t l = 0; l < n_chunks; ++l)
+    if ((rc = launch_partials_ops(h, h->d_ops + 5 * l, 5))) return rc;
+  if (!h->d1_sums) {
+    if ((rc = dalloc(h, (void**)&h->d1_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return rc;
+    if ((rc = dalloc(h, (void**)&h->d2_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return rc;
+  }
+  const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
+  PairArgs pa;
+  pa.L = h->partials + (size_t)(root - nt) * h->slot_stride;
+  pa.k0 = sc ? h->scale + (size_t)(root - nt) * h->n_pad : nullptr;
+  for (int v = 0; v < 5; ++v) {
+    pa.X[v] = h->partials + (size_t)(slot0 + v) * h->slot_stride;
+    pa.kx[v] = sc ? h->scale + (size_t)(slot0 + v) * h->n_pad : nullptr;
+  }
+  pa.pi = h->pi;
+  pa.probs = h->probs;
+  pa.weights = h->weights;
+  pa.d1_sums = h->d1_sums;
+  pa.d2_sums = h->d2_sums;
+  pa.n_patterns = h->n_patterns;
+  pa.alpha = alpha;
+  pa.beta = beta;
+  pa.S = S;
+  pa.C = C;
+  pa.guard = (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0;
+  pair_reduce_kernel<<<(unsigned)(h->n_pad / 256), 256, 0, h->stream>>>(pa);
+  HIPCHK(h, hipGetLastError());
+  const int n_waves = (int)((h->n_patterns + 63) / 64);
+  std::vector<double> w1(n_waves), w2(n_waves);
+  HIPCHK(h, hipMemcpyAsync(w1.data(), h->d1_sums, n_waves * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(w2.data(), h->d2_sums, n_waves * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = 0; i < n_waves; ++i) {
+    s1 += w1[i];
+    s2 += w2[i];
+  }
+  if (d1) *d1 = s1;
+  if (d2) *d2 = s2;
+  return PLK_OK;
+}
+
 int validate_ops(plk_handle h, const plk_op* ops, int n_ops) {
   std::vector<char> done(h->n_nodes, 0);
   for (int i = 0; i < n_ops; ++i) {
@@ -3059,7 +3174,7 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   for (size_t d = 1; d < depth.size(); ++d)
     for (int f : depth[d])
       if (f >= nt && !h->topo_kids[f].empty()) mlist.push_back(make_int2(f, parent[f] == root ? 1 : 0));
-  const int mat_base = nn + 2;
+  const int mat_base = nn + kScratchMats;
   if (!mlist.empty()) {
     if ((rc = ensure_cap(h, (void**)&h->d_drm, &h->d_drm_cap, mlist.size() * sizeof(int2)))) return rc;
     HIPCHK(h, hipMemcpyAsync(h->d_drm, mlist.data(), mlist.size() * sizeof(int2), hipMemcpyHostToDevice, h->stream));
@@ -3565,6 +3680,26 @@ int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   if (d1) *d1 = s1;
   if (d2) *d2 = s2;
   return PLK_OK;
+}
+
+int plk_root_pair_derivatives(plk_handle h, int a, int b, double alpha, double beta, double* d1, double* d2) {
+  env_refresh();
+  if (h && !h->shards.empty()) {
+    double s1 = 0.0, s2 = 0.0;
+    const int rc = multi_each(h, [&](plk_handle x) {
+      double u = 0.0, v = 0.0;
+      const int r = plk_root_pair_derivatives(x, a, b, alpha, beta, &u, &v);
+      s1 += u;
+      s2 += v;
+      return r;
+    });
+    if (rc) return rc;
+    if (d1) *d1 = s1;
+    if (d2) *d2 = s2;
+    return PLK_OK;
+  }
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  return root_pair_derivatives(h, a, b, alpha, beta, d1, d2);
 }
 
 int plk_set_timing(plk_handle h, int enable) {

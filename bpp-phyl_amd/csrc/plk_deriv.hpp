@@ -238,4 +238,69 @@ __global__ __launch_bounds__(256) void deriv_reduce_kernel(DRArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Root-pair derivatives (plk_root_pair_derivatives): the lengths of two sons a, b of the
+// root move together, t_a + alpha s and t_b + beta s -- the reference's BrLenRoot
+// (alpha = RootPosition, beta = 1 - RootPosition) and RootPosition (alpha = -beta =
+// BrLenRoot), RNonHomogeneousTreeLikelihood.cpp:391-560 and 862-1100.  The root vector is
+// bilinear in (P_a, P_b), so per pattern
+//   l'  = alpha l_a + beta l_b,   l'' = alpha^2 l_aa + 2 alpha beta l_ab + beta^2 l_bb
+// with l_x the root reduction of the root product whose a / b factors carry dP / d2P
+// (X[0..4] = a, b, aa, bb, ab).  Each product has its own power-of-two scale count.
+// ---------------------------------------------------------------------------
+struct PairArgs {
+  const double* L;        // root slot
+  const double* X[5];     // substituted root products
+  const int32_t* k0;      // scale rows (null without scaling)
+  const int32_t* kx[5];
+  const double* pi;
+  const double* probs;
+  const double* weights;
+  double* d1_sums;
+  double* d2_sums;
+  int64_t n_patterns;
+  double alpha, beta;
+  int S, C, guard;
+};
+
+__global__ __launch_bounds__(256) void pair_reduce_kernel(PairArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tile = p >> 7, q = p & (kTile - 1);
+  const int CS = a.C * a.S;
+  double r1 = 0.0, r2 = 0.0;
+  if (p < a.n_patterns) {
+    const size_t off = (size_t)tile * CS * kTile + q;
+    double l = 0.0, lx[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int c = 0; c < a.C; ++c) {
+      double lc = 0.0, lxc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int x = 0; x < a.S; ++x) {
+        const size_t i = off + (size_t)(c * a.S + x) * kTile;
+        const double li = a.L[i] * a.pi[x];
+        if (!a.guard || li > 0.0) lc += li;
+#pragma unroll
+        for (int v = 0; v < 5; ++v) lxc[v] += a.X[v][i] * a.pi[x];
+      }
+      l += lc * a.probs[c];
+#pragma unroll
+      for (int v = 0; v < 5; ++v) lx[v] += lxc[v] * a.probs[c];
+    }
+    double g[5];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) g[v] = a.k0 ? ldexp(lx[v] / l, 256 * (a.k0[p] - a.kx[v][p])) : lx[v] / l;
+    const double g1 = a.alpha * g[0] + a.beta * g[1];
+    const double g2 = a.alpha * a.alpha * g[2] + a.beta * a.beta * g[3] + 2.0 * a.alpha * a.beta * g[4];
+    r1 = a.weights[p] * g1;
+    r2 = a.weights[p] * (g2 - g1 * g1);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    r1 += __shfl_xor(r1, off, 64);
+    r2 += __shfl_xor(r2, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    a.d1_sums[p >> 6] = r1;
+    a.d2_sums[p >> 6] = r2;
+  }
+}
+
 }  // namespace plk

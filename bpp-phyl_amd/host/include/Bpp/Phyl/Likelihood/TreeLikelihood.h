@@ -40,6 +40,10 @@ class TreeLikelihood : public AbstractParametrizable {
   virtual ParameterList getBranchLengthsParameters() const = 0;
   virtual ParameterList getSubstitutionModelParameters() const = 0;
   virtual ParameterList getRateDistributionParameters() const = 0;
+  // parameters with analytic derivatives (the branch lengths) and the others
+  // (Likelihood/TreeLikelihood.h:426-435)
+  virtual ParameterList getDerivableParameters() const = 0;
+  virtual ParameterList getNonDerivableParameters() const = 0;
   virtual void setParameters(const ParameterList& pl) = 0;
   virtual double f(const ParameterList& pl) = 0;
   virtual double getFirstOrderDerivative(const std::string& variable) const = 0;
@@ -77,6 +81,7 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   bool scaling_ = true;
   bool incremental_ = true;
   bool compressed_ = false;  // usePatterns: PLK_FLAG_SUBTREE_PATTERNS on the engine
+  bool allDirty_ = true;     // next fireParameterChanged recomputes every P(t) (initialize)
   bool hostP_ = false;       // some branch P(t) came from the host (Taylor branch)
   size_t maxSons_ = 0;
   bool derivFirst_ = true, derivSecond_ = true;
@@ -101,8 +106,9 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   void buildEngineLayout();
   void setDataImpl(const SiteContainer& sites, const Alphabet* alphabet, const SubstitutionModel& model);
   void createEngine(size_t nModels, bool nonNegGuard);
-  void initBranchLengthsParameters();
-  void applyBranchLengths();
+  virtual void initBranchLengthsParameters();
+  // set the nodes' lengths from the parameters; returns the nodes whose length changed
+  virtual std::vector<const Node*> applyBranchLengths();
   // Upload transition matrices for the given branches (nodes) of model m(node).
   void updatePmatrices(const std::vector<const Node*>& nodes);
   virtual int modelIndexForNode(const Node*) const { return 0; }
@@ -114,7 +120,16 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   double reduceRoot() const;
   void fetchSiteLnl() const;
   void check(int rc, const char* what) const;
-  bool analyticDerivatives(const std::string& variable, double* d1, double* d2) const;
+  virtual bool analyticDerivatives(const std::string& variable, double* d1, double* d2) const;
+  void uploadRootFrequencies(const Vdouble& pi);
+  // evaluation bookkeeping (see EvaluationStats)
+  struct EvaluationStats {
+    size_t evaluations = 0;      // fireParameterChanged calls that evaluated lnL
+    size_t eigenUploads = 0;     // eigen-systems handed to the engine
+    size_t pmatBranches = 0;     // branches whose P(t) was recomputed
+    size_t fullTraversals = 0;   // traversals over every internal node
+  };
+  EvaluationStats stats_;
 
  public:
   ~AbstractPlkTreeLikelihood() override;
@@ -131,6 +146,8 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   const Tree& getTree() const override { return *tree_; }
   ParameterList getBranchLengthsParameters() const override;
   ParameterList getRateDistributionParameters() const override;
+  ParameterList getDerivableParameters() const override { return getBranchLengthsParameters(); }
+  ParameterList getNonDerivableParameters() const override;
   void setParameters(const ParameterList& pl) override;
   double f(const ParameterList& pl) override {
     setParameters(pl);
@@ -153,6 +170,8 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   // Partial likelihoods of a node in the reference's [pattern][class][state] order.
   VVVdouble getLikelihoodArray(int nodeId) const;
   plk_handle_s* getEngine() const { return engine_; }
+  // what the evaluations since construction did on the engine (host counters, no device call)
+  const EvaluationStats& getEvaluationStats() const { return stats_; }
 };
 
 class RHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
@@ -187,9 +206,16 @@ class DRHomogeneousTreeLikelihood : public RHomogeneousTreeLikelihood {
                               DiscreteDistribution* rDist, bool checkRooted = true, bool verbose = true);
 };
 
+// Likelihood/RNonHomogeneousTreeLikelihood.h: rooted tree, one model per branch from a
+// SubstitutionModelSet.  With reparametrizeRoot the two root branches are parametrised
+// as BrLenRoot (their sum) and RootPosition (root1's share), as
+// AbstractNonHomogeneousTreeLikelihood.cpp:312-330, 377-389.
 class RNonHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
   SubstitutionModelSet* modelSet_;  // not owned
   std::map<int, int> modelOfNodeId_;
+  std::map<int, const Node*> idToNode_;
+  bool reparametrizeRoot_ = false;
+  int root1_ = -1, root2_ = -1;       // ids of the root's first two sons
 
   int modelIndexForNode(const Node* n) const override;
   const SubstitutionModel* modelForIndex(int m) const override;
@@ -199,6 +225,9 @@ class RNonHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
   RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data, SubstitutionModelSet* modelSet,
                                 DiscreteDistribution* rDist, bool verbose, bool usePatterns, bool reparametrizeRoot,
                                 unsigned extraFlags);
+  void initBranchLengthsParameters() override;
+  std::vector<const Node*> applyBranchLengths() override;
+  bool analyticDerivatives(const std::string& variable, double* d1, double* d2) const override;
 
  public:
   RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data, SubstitutionModelSet* modelSet,
@@ -208,6 +237,9 @@ class RNonHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
   void initialize() override;
   void fireParameterChanged(const ParameterList& params) override;
   ParameterList getSubstitutionModelParameters() const override;
+  const SubstitutionModelSet* getSubstitutionModelSet() const { return modelSet_; }
+  SubstitutionModelSet* getSubstitutionModelSet() { return modelSet_; }
+  bool isRootReparametrized() const { return reparametrizeRoot_; }
   void computeAllTransitionProbabilities();
 };
 

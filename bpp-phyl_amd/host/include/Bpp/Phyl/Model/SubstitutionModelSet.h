@@ -1,8 +1,13 @@
-// Non-homogeneous model sets: one model per branch, shared ("global") parameters,
-// root frequencies.  After Model/SubstitutionModelSet.h (getModelForNode :329-341,
-// getRootFrequencies :429-435) and SubstitutionModelSetTools::createNonHomogeneousModelSet
-// (Model/SubstitutionModelSetTools.cpp:81-175): per-model parameter names carry the
-// suffix "_<k>" (k = 1-based model index), global ones keep the model's name.
+// Non-homogeneous model sets: one model per branch, shared ("aliased") parameters, root
+// frequencies.  After Model/SubstitutionModelSet.h (getModelForNode :329-341,
+// getNodesWithParameter .cpp:110-130, getNodeParameters :457-466, getRootFrequencies
+// :429-435) and SubstitutionModelSetTools::createNonHomogeneousModelSet
+// (Model/SubstitutionModelSetTools.cpp:81-175).  Parameter names follow the reference: the
+// root frequencies' parameters first ("GC.theta"), then every model parameter with the
+// suffix "_<k>" (k = 1-based model index, "T92.kappa_1", "T92.theta_1", ...).  A global
+// parameter is the first model's copy with every other model's copy aliased to it
+// (aliasParameters, bpp-core AbstractParameterAliasable): the aliases follow their source
+// and are left out of getIndependentParameters().
 #ifndef BPP_AMD_SUBSTITUTIONMODELSET_H
 #define BPP_AMD_SUBSTITUTIONMODELSET_H
 
@@ -22,7 +27,13 @@ class SubstitutionModelSet : public AbstractParametrizable {
   std::vector<std::vector<int> > nodesOfModel_;
   std::map<int, size_t> modelOfNode_;
   std::shared_ptr<FrequencySet> rootFreqs_;
-  std::vector<std::string> globalNames_;  // model parameter names shared by all models
+  std::map<std::string, std::string> aliasOf_;  // alias name -> source name
+  // bookkeeping of the last fireParameterChanged (which models / root frequencies changed)
+  std::vector<size_t> lastChangedModels_;
+  bool lastRootFreqsChanged_ = false;
+
+  // the model index (0-based) a suffixed parameter name belongs to, or -1
+  long modelIndexOfParameter(const std::string& name) const;
 
  public:
   explicit SubstitutionModelSet(const Alphabet* alpha) : AbstractParametrizable(""), alphabet_(alpha) {}
@@ -42,6 +53,8 @@ class SubstitutionModelSet : public AbstractParametrizable {
   }
   const SubstitutionModel* getModelForNode(int nodeId) const { return models_[getModelIndexForNode(nodeId)].get(); }
   const std::vector<int>& getNodesWithModel(size_t i) const { return nodesOfModel_.at(i); }
+  // nodes whose model carries `name` or one of its aliases (SubstitutionModelSet.cpp:110-130)
+  std::vector<int> getNodesWithParameter(const std::string& name) const;
   Vdouble getRootFrequencies() const {
     return rootFreqs_ ? rootFreqs_->getFrequencies() : models_.at(0)->getFrequencies();
   }
@@ -49,12 +62,27 @@ class SubstitutionModelSet : public AbstractParametrizable {
   ParameterList getRootFrequenciesParameters() const {
     return rootFreqs_ ? rootFreqs_->getParameters() : ParameterList();
   }
-  ParameterList getModelParameters() const;
+  // every parameter but the root frequencies' (SubstitutionModelSet.h:457-466)
+  ParameterList getNodeParameters() const;
+  ParameterList getModelParameters() const { return getNodeParameters(); }
+  // the parameters that are not aliases of another one
+  ParameterList getIndependentParameters() const override;
+  std::vector<std::string> getAlias(const std::string& name) const;
+  // true when every non-root node of `tree` has a model
+  bool isFullySetUpFor(const Tree& tree) const;
 
   // Build-up API
   void setRootFrequencies(FrequencySet* rootFreqs);
-  void addModel(SubstitutionModel* model, const std::vector<int>& nodesId, const std::vector<std::string>& globalNames);
+  void addModel(SubstitutionModel* model, const std::vector<int>& nodesId);
+  // p2 follows p1 from now on (bpp-core AbstractParameterAliasable::aliasParameters)
+  void aliasParameters(const std::string& p1, const std::string& p2);
+  bool matchParametersValues(const ParameterList& pl) override;
+  void setParametersValues(const ParameterList& pl) override;
   void fireParameterChanged(const ParameterList& pl) override;
+  // what the last fireParameterChanged changed: model indices whose parameters moved (their
+  // eigen-systems were recomputed) and whether the root frequencies moved
+  const std::vector<size_t>& getLastChangedModels() const { return lastChangedModels_; }
+  bool getLastRootFrequenciesChanged() const { return lastRootFreqsChanged_; }
 };
 
 struct SubstitutionModelSetTools {

@@ -12,14 +12,11 @@
 
 #include <string>
 
+#include "../Io/OutputStream.h"
 #include "Likelihood/TreeLikelihood.h"
 
 namespace bpp {
 
-class OutputStream {
- public:
-  virtual ~OutputStream() {}
-};
 class OptimizationListener {
  public:
   virtual ~OptimizationListener() {}
@@ -46,7 +43,8 @@ struct OptimizationTools {
   // PseudoNewton steps of the last OPTIMIZATION_NEWTON run (diagnostics)
   static unsigned int lastSteps_;
   static unsigned int pseudoNewtonParameters(TreeLikelihood* tl, const ParameterList& pl, double tolerance,
-                                             unsigned int tlEvalMax, bool useClock);
+                                             unsigned int tlEvalMax, bool useClock, OutputStream* messenger = nullptr,
+                                             OutputStream* profiler = nullptr);
 
   // Bounded 1-D Brent minimisation of f on [a, b]; returns the argmin, *fmin the value.
   template <class F>

@@ -7,6 +7,7 @@
 // What runs on the MI355X: every branch transition matrix (plk_update_pmatrices),
 // the full postorder traversal (plk_update_partials) and the root reduction
 // (plk_root_loglik).  Only one scalar comes back per evaluation.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -196,11 +197,18 @@ void AbstractPlkTreeLikelihood::initBranchLengthsParameters() {
   }
 }
 
-void AbstractPlkTreeLikelihood::applyBranchLengths() {
+std::vector<const Node*> AbstractPlkTreeLikelihood::applyBranchLengths() {
+  std::vector<const Node*> changed;
   for (size_t i = 0; i < nodes_.size(); i++) {
     const std::string n = "BrLen" + std::to_string(i);
-    if (parameters_.hasParameter(n)) nodes_[i]->setDistanceToFather(parameters_.getParameterValue(n));
+    if (!parameters_.hasParameter(n)) continue;
+    const double v = parameters_.getParameterValue(n);
+    if (!nodes_[i]->hasDistanceToFather() || nodes_[i]->getDistanceToFather() != v) {
+      nodes_[i]->setDistanceToFather(v);
+      changed.push_back(nodes_[i]);
+    }
   }
+  return changed;
 }
 
 void AbstractPlkTreeLikelihood::uploadEigen(int m, const SubstitutionModel& model) {
@@ -210,6 +218,12 @@ void AbstractPlkTreeLikelihood::uploadEigen(int m, const SubstitutionModel& mode
   check(plk_set_eigen(engine_, m, model.getColumnRightEigenVectors().data(), model.getRowLeftEigenVectors().data(),
                       lam.data()),
         "plk_set_eigen");
+  stats_.eigenUploads++;
+}
+
+void AbstractPlkTreeLikelihood::uploadRootFrequencies(const Vdouble& pi) {
+  rootFreqs_ = pi;
+  check(plk_set_root_frequencies(engine_, rootFreqs_.data()), "plk_set_root_frequencies");
 }
 
 void AbstractPlkTreeLikelihood::uploadRates() {
@@ -220,6 +234,7 @@ void AbstractPlkTreeLikelihood::uploadRates() {
 
 void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& nodes) {
   if (nodes.empty()) return;
+  stats_.pmatBranches += nodes.size();
   std::vector<int32_t> br, mod;
   std::vector<double> t;
   for (const Node* n : nodes) {
@@ -291,6 +306,8 @@ void AbstractPlkTreeLikelihood::computeTreeLikelihood(const std::vector<const No
     o.flags = opFlags_[i];
   }
   drValid_ = false;
+  stats_.evaluations++;
+  if (need.empty()) stats_.fullTraversals++;
   if (ops.empty()) {
     siteLnlValid_ = false;
     return;
@@ -340,6 +357,12 @@ ParameterList AbstractPlkTreeLikelihood::getBranchLengthsParameters() const {
   return brLenParameters_.getCommonParametersWith(getParameters());
 }
 
+ParameterList AbstractPlkTreeLikelihood::getNonDerivableParameters() const {
+  ParameterList pl = getSubstitutionModelParameters();
+  pl.addParameters(getRateDistributionParameters());
+  return pl;
+}
+
 ParameterList AbstractPlkTreeLikelihood::getRateDistributionParameters() const {
   if (!initialized_) throw Exception("getRateDistributionParameters(). Object is not initialized.");
   return rateDistribution_->getIndependentParameters().getCommonParametersWith(getParameters());
@@ -368,6 +391,8 @@ VVVdouble AbstractPlkTreeLikelihood::getLikelihoodArray(int nodeId) const {
 // engine reports PLK_ERR_UNSUPPORTED (per-subtree pattern compression).
 bool AbstractPlkTreeLikelihood::analyticDerivatives(const std::string& variable, double* d1, double* d2) const {
   if (!(derivFirst_ || derivSecond_) || hostP_) return false;
+  if (variable.size() <= 5 || variable.find_first_not_of("0123456789", 5) != std::string::npos)
+    throw Exception("analyticDerivatives: not a branch-length parameter: " + variable);
   const Node* n = nodes_.at(TextTools::to<size_t>(variable.substr(5)));
   if (extraFlags_ & PLK_FLAG_DOUBLE_RECURSIVE) {
     if (!drValid_) {
@@ -389,7 +414,7 @@ bool AbstractPlkTreeLikelihood::analyticDerivatives(const std::string& variable,
 
 double AbstractPlkTreeLikelihood::getFirstOrderDerivative(const std::string& variable) const {
   if (!parameters_.hasParameter(variable)) throw ParameterNotFoundException("getFirstOrderDerivative().", variable);
-  if (variable.compare(0, 5, "BrLen") != 0)
+  if (!getDerivableParameters().hasParameter(variable))
     throw Exception("Derivatives are only implemented for branch length parameters.");
   double d1, d2;
   if (analyticDerivatives(variable, &d1, &d2)) return -d1;
@@ -411,7 +436,7 @@ double AbstractPlkTreeLikelihood::getFirstOrderDerivative(const std::string& var
 
 double AbstractPlkTreeLikelihood::getSecondOrderDerivative(const std::string& variable) const {
   if (!parameters_.hasParameter(variable)) throw ParameterNotFoundException("getSecondOrderDerivative().", variable);
-  if (variable.compare(0, 5, "BrLen") != 0)
+  if (!getDerivableParameters().hasParameter(variable))
     throw Exception("Derivatives are only implemented for branch length parameters.");
   double d1, d2;
   if (analyticDerivatives(variable, &d1, &d2)) return -d2;
@@ -476,6 +501,7 @@ void RHomogeneousTreeLikelihood::setData(const SiteContainer& sites) {
 
 void RHomogeneousTreeLikelihood::initialize() {
   if (initialized_) throw Exception("RHomogeneousTreeLikelihood::initialize(). Object is already initialized.");
+  allDirty_ = true;
   if (!data_) throw Exception("RHomogeneousTreeLikelihood::initialize(). Data are no set.");
   resetParameters_();
   initBranchLengthsParameters();
@@ -496,31 +522,27 @@ void RHomogeneousTreeLikelihood::computeAllTransitionProbabilities() {
   uploadRates();
   std::vector<const Node*> all(nodes_.begin(), nodes_.end());
   updatePmatrices(all);
-  rootFreqs_ = model_->getFrequencies();
-  check(plk_set_root_frequencies(engine_, rootFreqs_.data()), "plk_set_root_frequencies");
+  uploadRootFrequencies(model_->getFrequencies());
 }
 
-// Likelihood/RHomogeneousTreeLikelihood.cpp:255-283
-void RHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList& params) {
+// Likelihood/RHomogeneousTreeLikelihood.cpp:255-283: a model or rate-distribution change
+// recomputes every P(t); otherwise only the branches whose length changed get a new P(t),
+// and only their ancestors are re-traversed (the reference always re-traverses, :280).
+// Changes are detected by value, so a caller that hands over every parameter (as the
+// optimisers do) recomputes only what moved.
+void RHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList&) {
   if (!initialized_) throw Exception("RHomogeneousTreeLikelihood::fireParameterChanged(). Object not initialized.");
-  applyBranchLengths();
-  model_->matchParametersValues(getParameters());
-  rateDistribution_->matchParametersValues(getParameters());
-  if (rateDistribution_->getParameters().getCommonParametersWith(params).size() > 0 ||
-      model_->getParameters().getCommonParametersWith(params).size() > 0) {
+  const std::vector<const Node*> changed = applyBranchLengths();
+  const bool modelChanged = model_->matchParametersValues(getParameters());
+  const bool rateChanged = rateDistribution_->matchParametersValues(getParameters());
+  if (allDirty_ || modelChanged || rateChanged) {
+    allDirty_ = false;
     computeAllTransitionProbabilities();
-  } else if (params.size() > 0) {
-    std::vector<const Node*> changed;
-    for (size_t i = 0; i < params.size(); i++) {
-      const std::string& s = params[i].getName();
-      if (s.compare(0, 5, "BrLen") == 0) changed.push_back(nodes_[TextTools::to<size_t>(s.substr(5))]);
-    }
+    computeTreeLikelihood();
+  } else {
     updatePmatrices(changed);
     computeTreeLikelihood(&changed);
-    minusLogLik_ = -reduceRoot();
-    return;
   }
-  computeTreeLikelihood();
   minusLogLik_ = -reduceRoot();
 }
 
@@ -562,12 +584,22 @@ DRNonHomogeneousTreeLikelihood::DRNonHomogeneousTreeLikelihood(const Tree& tree,
 RNonHomogeneousTreeLikelihood::RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data,
                                                              SubstitutionModelSet* modelSet,
                                                              DiscreteDistribution* rDist, bool verbose,
-                                                             bool usePatterns, bool, unsigned extraFlags)
-    : AbstractPlkTreeLikelihood(tree, rDist, false, verbose, usePatterns), modelSet_(modelSet) {
+                                                             bool usePatterns, bool reparametrizeRoot,
+                                                             unsigned extraFlags)
+    : AbstractPlkTreeLikelihood(tree, rDist, false, verbose, usePatterns), modelSet_(modelSet),
+      reparametrizeRoot_(reparametrizeRoot) {
   if (!modelSet) throw NullPointerException("RNonHomogeneousTreeLikelihood: null model set");
   extraFlags_ = extraFlags;
   nbStates_ = modelSet->getNumberOfStates();
-  for (const Node* n : nodes_) modelOfNodeId_[n->getId()] = (int)modelSet_->getModelIndexForNode(n->getId());
+  // AbstractNonHomogeneousTreeLikelihood::init_ (:160-185)
+  const Node* root = tree_->getRootNode();
+  if (root->getNumberOfSons() < 2) throw Exception("RNonHomogeneousTreeLikelihood: the root must have two sons");
+  root1_ = root->getSon(0)->getId();
+  root2_ = root->getSon(1)->getId();
+  for (const Node* n : nodes_) {
+    modelOfNodeId_[n->getId()] = (int)modelSet_->getModelIndexForNode(n->getId());
+    idToNode_[n->getId()] = n;
+  }
   setData(data);
 }
 
@@ -595,12 +627,76 @@ void RNonHomogeneousTreeLikelihood::setData(const SiteContainer& sites) {
   check(plk_set_pattern_weights(engine_, w.data()), "plk_set_pattern_weights");
 }
 
+// AbstractNonHomogeneousTreeLikelihood::initBranchLengthsParameters (:343-390): the root's
+// two branches become BrLenRoot = l1 + l2 and RootPosition = l1 / (l1 + l2)
+void RNonHomogeneousTreeLikelihood::initBranchLengthsParameters() {
+  if (!reparametrizeRoot_) {
+    AbstractPlkTreeLikelihood::initBranchLengthsParameters();
+    return;
+  }
+  AbstractPlkTreeLikelihood::initBranchLengthsParameters();
+  double l1 = 0., l2 = 0.;
+  ParameterList kept;
+  for (size_t i = 0; i < nodes_.size(); i++) {
+    const int id = nodes_[i]->getId();
+    const Parameter& p = brLenParameters_[i];
+    if (id == root1_)
+      l1 = p.getValue();
+    else if (id == root2_)
+      l2 = p.getValue();
+    else
+      kept.addParameter(p);
+  }
+  brLenParameters_ = kept;
+  brLenParameters_.addParameter(Parameter("BrLenRoot", l1 + l2, brLenConstraint_));
+  brLenParameters_.addParameter(Parameter("RootPosition", l1 / (l1 + l2), Parameter::PROP_CONSTRAINT_EX));
+}
+
+// AbstractNonHomogeneousTreeLikelihood::applyParameters (:312-335)
+std::vector<const Node*> RNonHomogeneousTreeLikelihood::applyBranchLengths() {
+  std::vector<const Node*> changed = AbstractPlkTreeLikelihood::applyBranchLengths();
+  if (!reparametrizeRoot_) return changed;
+  const double len = parameters_.getParameterValue("BrLenRoot");
+  const double pos = parameters_.getParameterValue("RootPosition");
+  for (const Node* n : nodes_) {
+    const int id = n->getId();
+    if (id != root1_ && id != root2_) continue;
+    const double v = id == root1_ ? len * pos : len * (1. - pos);
+    Node* m = const_cast<Node*>(n);
+    if (!m->hasDistanceToFather() || m->getDistanceToFather() != v) {
+      m->setDistanceToFather(v);
+      changed.push_back(n);
+    }
+  }
+  return changed;
+}
+
+// BrLenRoot and RootPosition move both root branches: one directional derivative on the
+// device (plk_root_pair_derivatives), as computeTreeDLikelihood / computeTreeD2Likelihood do
+// for them (RNonHomogeneousTreeLikelihood.cpp:391-560, 862-1100)
+bool RNonHomogeneousTreeLikelihood::analyticDerivatives(const std::string& variable, double* d1, double* d2) const {
+  if (!reparametrizeRoot_ || (variable != "BrLenRoot" && variable != "RootPosition"))
+    return AbstractPlkTreeLikelihood::analyticDerivatives(variable, d1, d2);
+  if (!(derivFirst_ || derivSecond_) || hostP_) return false;
+  const double len = parameters_.getParameterValue("BrLenRoot");
+  const double pos = parameters_.getParameterValue("RootPosition");
+  const double alpha = variable == "BrLenRoot" ? pos : len;
+  const double beta = variable == "BrLenRoot" ? 1. - pos : -len;
+  const int a = engineIndex_.at(idToNode_.at(root1_)), b = engineIndex_.at(idToNode_.at(root2_));
+  const int rc = plk_root_pair_derivatives(engine_, a, b, alpha, beta, d1, d2);
+  if (rc == PLK_ERR_UNSUPPORTED) return false;
+  check(rc, "plk_root_pair_derivatives");
+  return true;
+}
+
 void RNonHomogeneousTreeLikelihood::initialize() {
   if (initialized_) throw Exception("RNonHomogeneousTreeLikelihood::initialize(). Object is already initialized.");
+  allDirty_ = true;
+  // AbstractNonHomogeneousTreeLikelihood::initParameters (:290-306)
   resetParameters_();
   initBranchLengthsParameters();
   addParameters_(brLenParameters_);
-  addParameters_(modelSet_->getParameters());
+  addParameters_(modelSet_->getIndependentParameters());
   addParameters_(rateDistribution_->getIndependentParameters());
   initialized_ = true;
   fireParameterChanged(getParameters());
@@ -616,31 +712,39 @@ void RNonHomogeneousTreeLikelihood::computeAllTransitionProbabilities() {
   uploadRates();
   std::vector<const Node*> all(nodes_.begin(), nodes_.end());
   updatePmatrices(all);
-  rootFreqs_ = modelSet_->getRootFrequencies();
-  check(plk_set_root_frequencies(engine_, rootFreqs_.data()), "plk_set_root_frequencies");
+  uploadRootFrequencies(modelSet_->getRootFrequencies());
 }
 
-// Likelihood/RNonHomogeneousTreeLikelihood.cpp:259-311
-void RNonHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList& params) {
+// Likelihood/RNonHomogeneousTreeLikelihood.cpp:259-311: a rate-distribution change
+// recomputes every P(t); otherwise the branches of the models whose parameters moved
+// (getNodesWithParameter, through the aliases) get a new eigen-system and P(t), as do
+// the branches whose length moved, and the root frequencies follow the model set.  Only
+// the ancestors of those branches are re-traversed (the reference re-traverses everything).
+void RNonHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList&) {
   if (!initialized_) throw Exception("RNonHomogeneousTreeLikelihood::fireParameterChanged(). Object not initialized.");
-  applyBranchLengths();
-  modelSet_->matchParametersValues(getParameters());
-  rateDistribution_->matchParametersValues(getParameters());
-  if (rateDistribution_->getParameters().getCommonParametersWith(params).size() > 0 ||
-      modelSet_->getParameters().getCommonParametersWith(params).size() > 0) {
+  std::vector<const Node*> changed = applyBranchLengths();
+  const bool setChanged = modelSet_->matchParametersValues(getParameters());
+  const bool rateChanged = rateDistribution_->matchParametersValues(getParameters());
+  if (allDirty_ || rateChanged) {
+    allDirty_ = false;
     computeAllTransitionProbabilities();
-  } else if (params.size() > 0) {
-    std::vector<const Node*> changed;
-    for (size_t i = 0; i < params.size(); i++) {
-      const std::string& s = params[i].getName();
-      if (s.compare(0, 5, "BrLen") == 0) changed.push_back(nodes_[TextTools::to<size_t>(s.substr(5))]);
-    }
-    updatePmatrices(changed);
-    computeTreeLikelihood(&changed);
+    computeTreeLikelihood();
     minusLogLik_ = -reduceRoot();
     return;
   }
-  computeTreeLikelihood();
+  if (setChanged) {
+    for (size_t m : modelSet_->getLastChangedModels()) {
+      uploadEigen((int)m, *modelSet_->getModel(m));
+      for (int id : modelSet_->getNodesWithModel(m)) {
+        auto it = idToNode_.find(id);
+        if (it != idToNode_.end() && std::find(changed.begin(), changed.end(), it->second) == changed.end())
+          changed.push_back(it->second);
+      }
+    }
+    if (modelSet_->getLastRootFrequenciesChanged()) uploadRootFrequencies(modelSet_->getRootFrequencies());
+  }
+  updatePmatrices(changed);
+  computeTreeLikelihood(&changed);
   minusLogLik_ = -reduceRoot();
 }
 

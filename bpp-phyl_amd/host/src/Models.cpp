@@ -1,6 +1,8 @@
 // Host mirror: substitution models (generator, frequencies, eigen-system, P(t)) and
 // non-homogeneous model sets.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "Bpp/Phyl/Model/Models.h"
 #include "Bpp/Phyl/Model/SubstitutionModelSet.h"
@@ -403,40 +405,70 @@ void GCFrequencySet::fireParameterChanged(const ParameterList&) {
 
 SubstitutionModelSet::SubstitutionModelSet(const SubstitutionModelSet& s)
     : AbstractParametrizable(s), alphabet_(s.alphabet_), nodesOfModel_(s.nodesOfModel_),
-      modelOfNode_(s.modelOfNode_), globalNames_(s.globalNames_) {
+      modelOfNode_(s.modelOfNode_), aliasOf_(s.aliasOf_) {
   for (auto& m : s.models_) models_.push_back(std::shared_ptr<SubstitutionModel>(m->clone()));
   if (s.rootFreqs_) rootFreqs_.reset(s.rootFreqs_->clone());
 }
 
-void SubstitutionModelSet::setRootFrequencies(FrequencySet* rootFreqs) {
-  rootFreqs_.reset(rootFreqs);
-  if (rootFreqs_) addParameters_(rootFreqs_->getParameters());
+long SubstitutionModelSet::modelIndexOfParameter(const std::string& name) const {
+  const size_t u = name.rfind('_');
+  if (u == std::string::npos || u + 1 >= name.size()) return -1;
+  for (size_t i = u + 1; i < name.size(); i++)
+    if (name[i] < '0' || name[i] > '9') return -1;
+  const long k = std::atol(name.c_str() + u + 1);
+  return (k >= 1 && (size_t)k <= models_.size()) ? k - 1 : -1;
 }
 
-void SubstitutionModelSet::addModel(SubstitutionModel* model, const std::vector<int>& nodesId,
-                                    const std::vector<std::string>& globalNames) {
+void SubstitutionModelSet::setRootFrequencies(FrequencySet* rootFreqs) {
+  // the root frequencies' parameters come first (SubstitutionModelSet.h:457-466)
+  ParameterList rest;
+  for (size_t i = 0; i < parameters_.size(); i++)
+    if (!rootFreqs_ || !rootFreqs_->getParameters().hasParameter(parameters_[i].getName()))
+      rest.addParameter(parameters_[i]);
+  rootFreqs_.reset(rootFreqs);
+  resetParameters_();
+  if (rootFreqs_) addParameters_(rootFreqs_->getParameters());
+  addParameters_(rest);
+}
+
+void SubstitutionModelSet::addModel(SubstitutionModel* model, const std::vector<int>& nodesId) {
   const size_t k = models_.size() + 1;
+  if (model->getAlphabet()->getAlphabetType() != alphabet_->getAlphabetType())
+    throw AlphabetMismatchException("SubstitutionModelSet::addModel: alphabets do not match");
   models_.push_back(std::shared_ptr<SubstitutionModel>(model));
   nodesOfModel_.push_back(nodesId);
   for (int id : nodesId) modelOfNode_[id] = k - 1;
-  globalNames_ = globalNames;
   const ParameterList& pl = model->getParameters();
   for (size_t i = 0; i < pl.size(); i++) {
-    const std::string& n = pl[i].getName();
-    bool global = false;
-    for (auto& g : globalNames_)
-      if (g == n) global = true;
-    if (global) {
-      if (!parameters_.hasParameter(n)) addParameter_(pl[i]);
-    } else {
-      Parameter p(pl[i]);
-      p.setName(n + "_" + std::to_string(k));
-      addParameter_(p);
-    }
+    Parameter p(pl[i]);
+    p.setName(pl[i].getName() + "_" + std::to_string(k));
+    addParameter_(p);
   }
 }
 
-ParameterList SubstitutionModelSet::getModelParameters() const {
+void SubstitutionModelSet::aliasParameters(const std::string& p1, const std::string& p2) {
+  if (!parameters_.hasParameter(p1)) throw ParameterNotFoundException("SubstitutionModelSet::aliasParameters", p1);
+  if (!parameters_.hasParameter(p2)) throw ParameterNotFoundException("SubstitutionModelSet::aliasParameters", p2);
+  if (p1 == p2) throw Exception("SubstitutionModelSet::aliasParameters: a parameter cannot alias itself: " + p1);
+  std::string root = p1;
+  while (aliasOf_.count(root)) root = aliasOf_.at(root);
+  if (root == p2) throw Exception("SubstitutionModelSet::aliasParameters: cyclic alias " + p1 + " <- " + p2);
+  aliasOf_[p2] = p1;
+  ParameterList one;
+  Parameter q = parameters_.getParameter(p2);
+  q.setValue(parameters_.getParameterValue(p1));
+  one.addParameter(q);
+  matchParametersValues(one);
+}
+
+std::vector<std::string> SubstitutionModelSet::getAlias(const std::string& name) const {
+  std::vector<std::string> out;
+  for (auto& kv : aliasOf_)
+    if (kv.second == name) out.push_back(kv.first);
+  return out;
+}
+
+ParameterList SubstitutionModelSet::getNodeParameters() const {
   ParameterList out;
   ParameterList rf = getRootFrequenciesParameters();
   for (size_t i = 0; i < parameters_.size(); i++)
@@ -444,38 +476,149 @@ ParameterList SubstitutionModelSet::getModelParameters() const {
   return out;
 }
 
+ParameterList SubstitutionModelSet::getIndependentParameters() const {
+  ParameterList out;
+  for (size_t i = 0; i < parameters_.size(); i++)
+    if (!aliasOf_.count(parameters_[i].getName())) out.addParameter(parameters_[i]);
+  return out;
+}
+
+std::vector<int> SubstitutionModelSet::getNodesWithParameter(const std::string& name) const {
+  if (!parameters_.hasParameter(name)) throw ParameterNotFoundException("SubstitutionModelSet::getNodesWithParameter.", name);
+  std::vector<int> out;
+  std::vector<std::string> names(1, name);
+  // the parameter, its aliases, their aliases, ...
+  for (size_t i = 0; i < names.size(); i++)
+    for (const std::string& a : getAlias(names[i]))
+      if (std::find(names.begin(), names.end(), a) == names.end()) names.push_back(a);
+  for (const std::string& n : names) {
+    const long m = modelIndexOfParameter(n);
+    if (m < 0) continue;
+    for (int id : nodesOfModel_[(size_t)m])
+      if (std::find(out.begin(), out.end(), id) == out.end()) out.push_back(id);
+  }
+  return out;
+}
+
+bool SubstitutionModelSet::isFullySetUpFor(const Tree& tree) const {
+  const TreeTemplate<Node>* tt = dynamic_cast<const TreeTemplate<Node>*>(&tree);
+  if (!tt) return false;
+  for (const Node* n : tt->getNodes())
+    if (n != tt->getRootNode() && !modelOfNode_.count(n->getId())) return false;
+  return rootFreqs_ ? rootFreqs_->getFrequencies().size() == getNumberOfStates() : true;
+}
+
+bool SubstitutionModelSet::matchParametersValues(const ParameterList& pl) {
+  std::vector<size_t> changed;
+  parameters_.matchParametersValues(pl, &changed);
+  // aliases follow their sources (in alias-chain order: repeat until stable)
+  for (bool moved = true; moved;) {
+    moved = false;
+    for (auto& kv : aliasOf_) {
+      const double v = parameters_.getParameterValue(kv.second);
+      const size_t i = parameters_.whichParameterHasName(kv.first);
+      if (parameters_[i].getValue() != v) {
+        parameters_[i].setValue(v);
+        if (std::find(changed.begin(), changed.end(), i) == changed.end()) changed.push_back(i);
+        moved = true;
+      }
+    }
+  }
+  if (changed.empty()) return false;
+  ParameterList ch;
+  for (size_t i : changed) ch.addParameter(parameters_[i]);
+  fireParameterChanged(ch);
+  return true;
+}
+
+void SubstitutionModelSet::setParametersValues(const ParameterList& pl) {
+  matchParametersValues(pl);
+}
+
+// Each model takes the values of its own "_<k>" parameters; only a model whose values moved
+// recomputes its generator and eigen-system (SubstitutionModel::fireParameterChanged).
 void SubstitutionModelSet::fireParameterChanged(const ParameterList&) {
+  lastChangedModels_.clear();
   for (size_t k = 0; k < models_.size(); k++) {
     ParameterList own;
     const ParameterList& pl = models_[k]->getParameters();
+    const std::string suffix = "_" + std::to_string(k + 1);
     for (size_t i = 0; i < pl.size(); i++) {
-      const std::string& n = pl[i].getName();
-      const std::string local = n + "_" + std::to_string(k + 1);
+      const std::string local = pl[i].getName() + suffix;
+      if (!parameters_.hasParameter(local)) continue;
       Parameter p(pl[i]);
-      if (parameters_.hasParameter(local))
-        p.setValue(parameters_.getParameterValue(local));
-      else if (parameters_.hasParameter(n))
-        p.setValue(parameters_.getParameterValue(n));
+      p.setValue(parameters_.getParameterValue(local));
       own.addParameter(p);
     }
-    models_[k]->matchParametersValues(own);
+    if (models_[k]->matchParametersValues(own)) lastChangedModels_.push_back(k);
   }
-  if (rootFreqs_) rootFreqs_->matchParametersValues(parameters_);
+  lastRootFreqsChanged_ = rootFreqs_ ? rootFreqs_->matchParametersValues(parameters_) : false;
 }
 
+namespace {
+// ApplicationTools::matchingParameters: a name with '*' wildcards against a list of names
+bool wildcardMatch(const std::string& pat, const std::string& s) {
+  size_t p = 0, q = 0, star = std::string::npos, mark = 0;
+  while (q < s.size()) {
+    if (p < pat.size() && pat[p] == s[q]) {
+      p++;
+      q++;
+    } else if (p < pat.size() && pat[p] == '*') {
+      star = p++;
+      mark = q;
+    } else if (star != std::string::npos) {
+      p = star + 1;
+      q = ++mark;
+    } else {
+      return false;
+    }
+  }
+  while (p < pat.size() && pat[p] == '*') p++;
+  return p == pat.size();
+}
+}  // namespace
+
+// SubstitutionModelSetTools.cpp:81-175: a clone of the model per non-root node (in
+// getNodesId order), global parameters aliased to the first model's copy (or, for a
+// parameter given with groups of node ids, to the copy of each group's first node), and
+// aliasFreqNames tying root-frequency parameters to model 1's global ones.
 SubstitutionModelSet* SubstitutionModelSetTools::createNonHomogeneousModelSet(
-    SubstitutionModel* model, FrequencySet* rootFreqs, const Tree* tree, const std::map<std::string, std::string>&,
+    SubstitutionModel* model, FrequencySet* rootFreqs, const Tree* tree,
+    const std::map<std::string, std::string>& aliasFreqNames,
     std::map<std::string, std::vector<Vint> >& globalParameterNames) {
   const TreeTemplate<Node>* tt = dynamic_cast<const TreeTemplate<Node>*>(tree);
   if (!tt) throw Exception("createNonHomogeneousModelSet: unsupported tree implementation");
-  std::vector<std::string> globals;
-  for (auto& kv : globalParameterNames) globals.push_back(kv.first);
-  SubstitutionModelSet* set = new SubstitutionModelSet(model->getAlphabet());
-  for (const Node* n : tt->getNodes()) {
-    if (n == tt->getRootNode()) continue;
-    set->addModel(model->clone(), std::vector<int>(1, n->getId()), globals);
+  if (rootFreqs && model->getAlphabet()->getAlphabetType() != rootFreqs->getAlphabet()->getAlphabetType())
+    throw AlphabetMismatchException("SubstitutionModelSetTools::createNonHomogeneousModelSet()");
+  const std::vector<std::string> modelNames = model->getParameters().getParameterNames();
+  std::map<std::string, std::vector<Vint> > globals;
+  for (auto& kv : globalParameterNames) {
+    bool any = false;
+    for (const std::string& n : modelNames)
+      if (wildcardMatch(kv.first, n)) {
+        globals[n] = kv.second;
+        any = true;
+      }
+    if (!any) throw Exception("SubstitutionModelSetTools::createNonHomogeneousModelSet. Parameter '" + kv.first + "' is not valid.");
   }
-  set->setRootFrequencies(rootFreqs);
+  SubstitutionModelSet* set = new SubstitutionModelSet(model->getAlphabet());
+  if (rootFreqs) set->setRootFrequencies(rootFreqs);
+  std::vector<int> ids = tt->getNodesId();
+  ids.erase(std::find(ids.begin(), ids.end(), tt->getRootNode()->getId()));
+  for (int id : ids) set->addModel(model->clone(), std::vector<int>(1, id));
+  for (const std::string& pname : modelNames) {
+    auto g = globals.find(pname);
+    if (g == globals.end()) continue;
+    auto suffixed = [&](int nodeId) { return pname + "_" + std::to_string(set->getModelIndexForNode(nodeId) + 1); };
+    if (g->second.empty()) {
+      for (size_t i = 1; i < ids.size(); i++) set->aliasParameters(suffixed(ids[0]), suffixed(ids[i]));
+    } else {
+      for (const Vint& group : g->second)
+        for (size_t i = 1; i < group.size(); i++) set->aliasParameters(suffixed(group[0]), suffixed(group[i]));
+    }
+  }
+  for (auto& kv : aliasFreqNames)
+    if (globals.count(kv.second)) set->aliasParameters(kv.second + "_1", kv.first);
   delete model;
   return set;
 }
@@ -485,13 +628,11 @@ SubstitutionModelSet* SubstitutionModelSetTools::createHomogeneousModelSet(Subst
                                                                            const Tree* tree) {
   const TreeTemplate<Node>* tt = dynamic_cast<const TreeTemplate<Node>*>(tree);
   if (!tt) throw Exception("createHomogeneousModelSet: unsupported tree implementation");
-  std::vector<int> ids;
-  for (const Node* n : tt->getNodes())
-    if (n != tt->getRootNode()) ids.push_back(n->getId());
+  std::vector<int> ids = tt->getNodesId();
+  ids.erase(std::find(ids.begin(), ids.end(), tt->getRootNode()->getId()));
   SubstitutionModelSet* set = new SubstitutionModelSet(model->getAlphabet());
-  std::vector<std::string> globals = model->getParameters().getParameterNames();
-  set->addModel(model, ids, globals);
-  set->setRootFrequencies(rootFreqs);
+  if (rootFreqs) set->setRootFrequencies(rootFreqs);
+  set->addModel(model, ids);
   return set;
 }
 

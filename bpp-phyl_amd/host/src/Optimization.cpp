@@ -84,7 +84,8 @@ struct PNParam {
 unsigned int pseudoNewton(const std::vector<PNParam>& par, std::vector<double>& x,
                           const std::function<double(const std::vector<double>&)>& f,
                           const std::function<void(size_t, double*, double*)>& analytic, double tolerance,
-                          unsigned int maxEval, unsigned int* steps_out) {
+                          unsigned int maxEval, unsigned int* steps_out,
+                          const std::function<void(unsigned int, const std::vector<double>&, double)>& onStep) {
   const size_t n = par.size();
   unsigned int nEval = 0, steps = 0;
   auto eval = [&](const std::vector<double>& y) {
@@ -160,6 +161,7 @@ unsigned int pseudoNewton(const std::vector<PNParam>& par, std::vector<double>& 
     }
     const bool done = std::fabs(fnew - fcur) < tolerance;
     fcur = fnew;
+    if (onStep) onStep(steps, x, fcur);
     if (done) break;
   }
   if (steps_out) *steps_out = steps;
@@ -170,7 +172,9 @@ unsigned int pseudoNewton(const std::vector<PNParam>& par, std::vector<double>& 
 
 unsigned int OptimizationTools::optimizeTreeScale(TreeLikelihood* tl, double tolerance, unsigned int tlEvalMax,
                                                   OutputStream*, OutputStream*, unsigned int) {
+  // ScaleFunction (OptimizationTools.cpp:77-115): every branch length but RootPosition
   ParameterList bl = tl->getBranchLengthsParameters();
+  if (bl.hasParameter("RootPosition")) bl.deleteParameter("RootPosition");
   std::vector<double> b0(bl.size());
   for (size_t i = 0; i < bl.size(); i++) b0[i] = bl[i].getValue();
   unsigned int nEval = 0;
@@ -246,15 +250,20 @@ struct ClockMap {
 // heights of GlobalClockTreeLikelihoodFunctionWrapper (TotalHeight, HeightP_v), whose
 // derivatives are numerical (OptimizationTools.cpp:277-288, 329-331).
 unsigned int OptimizationTools::pseudoNewtonParameters(TreeLikelihood* tl, const ParameterList& pl, double tolerance,
-                                                       unsigned int tlEvalMax, bool useClock) {
+                                                       unsigned int tlEvalMax, bool useClock, OutputStream* messenger,
+                                                       OutputStream* profiler) {
   std::vector<PNParam> par;
   std::vector<double> x;
   std::vector<size_t> plIndex;  // parameter -> index in pl (non-clock parameters)
   std::unique_ptr<ClockMap> clock;
   ParameterList brl;
   const bool deriv = tl->derivativesEnabled();
+  // analytic derivatives for the likelihood's derivable parameters (the branch lengths,
+  // BrLenRoot and RootPosition included), ThreePointsNumericalDerivative for the others
+  // (OptimizationTools.cpp:330-331 getNonDerivableParameters)
+  const ParameterList derivable = tl->getDerivableParameters();
   for (size_t i = 0; i < pl.size(); i++) {
-    const bool br = pl[i].getName().compare(0, 5, "BrLen") == 0;
+    const bool br = derivable.hasParameter(pl[i].getName());
     if (useClock && br) continue;
     PNParam p;
     p.name = pl[i].getName();
@@ -307,8 +316,28 @@ unsigned int OptimizationTools::pseudoNewtonParameters(TreeLikelihood* tl, const
     *d1 = tl->getFirstOrderDerivative(par[i].name);
     *d2 = tl->getSecondOrderDerivative(par[i].name);
   };
+  // profiler: one line per step with every parameter and the function value (the
+  // optimisers' profile format: a header of names, then tab-separated values)
+  if (profiler) {
+    *profiler << "Step";
+    for (auto& p : par) *profiler << "\t" << p.name;
+    *profiler << "\tFunction";
+    profiler->endLine();
+  }
+  auto onStep = [&](unsigned int step, const std::vector<double>& y, double fy) {
+    if (profiler) {
+      *profiler << (long)step;
+      for (double v : y) *profiler << "\t" << v;
+      *profiler << "\t" << fy;
+      profiler->endLine();
+    }
+    if (messenger) {
+      *messenger << "PseudoNewton step " << (long)step << ": f = " << fy;
+      messenger->endLine();
+    }
+  };
   unsigned int steps = 0;
-  const unsigned int nEval = pseudoNewton(par, x, f, an, tolerance, tlEvalMax, &steps);
+  const unsigned int nEval = pseudoNewton(par, x, f, an, tolerance, tlEvalMax, &steps, onStep);
   f(x);  // leave the likelihood at the accepted point
   lastSteps_ = steps;
   if (std::getenv("BPP_AMD_OPT_LOG"))
@@ -321,11 +350,12 @@ unsigned int OptimizationTools::lastSteps_ = 0;
 
 unsigned int OptimizationTools::optimizeNumericalParameters2(TreeLikelihood* tl, const ParameterList& parameters,
                                                              OptimizationListener*, double tolerance,
-                                                             unsigned int tlEvalMax, OutputStream*, OutputStream*,
-                                                             bool, bool useClock, unsigned int, const std::string& optMethodDeriv) {
+                                                             unsigned int tlEvalMax, OutputStream* messenger,
+                                                             OutputStream* profiler, bool, bool useClock, unsigned int,
+                                                             const std::string& optMethodDeriv) {
   ParameterList pl = tl->getParameters().getCommonParametersWith(parameters);
   if (optMethodDeriv == OPTIMIZATION_NEWTON && !std::getenv("BPP_AMD_OPT_BRENT"))
-    return pseudoNewtonParameters(tl, pl, tolerance, tlEvalMax, useClock);
+    return pseudoNewtonParameters(tl, pl, tolerance, tlEvalMax, useClock, messenger, profiler);
   unsigned int nEval = 0;
   std::unique_ptr<ClockMap> clock;
   ParameterList brl;

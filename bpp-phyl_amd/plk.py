@@ -37,7 +37,7 @@ EXPORTS = [
     "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
     "plk_kernel_path", "plk_evaluate", "plk_compressed_work", "plk_all_branch_derivatives",
     "plk_get_timing_ex", "plk_traversal_work", "plk_create_multi", "plk_shard_count", "plk_comm_get_id",
-    "plk_comm_init", "plk_get_dpmatrix",
+    "plk_comm_init", "plk_get_dpmatrix", "plk_root_pair_derivatives",
 ]
 
 
@@ -115,6 +115,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_reset_timing": ([ct.c_void_p], ct.c_int),
         "plk_synchronize": ([ct.c_void_p], ct.c_int),
         "plk_branch_derivatives": ([ct.c_void_p, ct.c_int, dp, dp], ct.c_int),
+        "plk_root_pair_derivatives": ([ct.c_void_p, ct.c_int, ct.c_int, ct.c_double, ct.c_double, dp, dp], ct.c_int),
         "plk_all_branch_derivatives": ([ct.c_void_p, dp, dp], ct.c_int),
         "plk_kernel_path": ([ct.c_void_p], ct.c_char_p),
         "plk_compressed_work": ([ct.c_void_p, P(ct.c_int64)], ct.c_int),
@@ -334,6 +335,13 @@ class Engine:
         """(d lnL/dt, d2 lnL/dt2) for the branch above node `branch`."""
         d1, d2 = ct.c_double(0), ct.c_double(0)
         self._chk(self.lib.plk_branch_derivatives(self.h, branch, ct.byref(d1), ct.byref(d2)))
+        return d1.value, d2.value
+
+    def root_pair_derivatives(self, a: int, b: int, alpha: float, beta: float):
+        """Directional (d lnL/ds, d2 lnL/ds2) for root sons a, b moved by t_a + alpha s,
+        t_b + beta s (the reference's BrLenRoot / RootPosition derivatives)."""
+        d1, d2 = ct.c_double(0), ct.c_double(0)
+        self._chk(self.lib.plk_root_pair_derivatives(self.h, a, b, alpha, beta, ct.byref(d1), ct.byref(d2)))
         return d1.value, d2.value
 
     def all_branch_derivatives(self):

@@ -218,6 +218,18 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
 int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2);
 int plk_block_size(void);
 
+/* Directional derivatives for two sons a, b of the traversal's root whose lengths move
+ * together, t_a + alpha s and t_b + beta s:  d1 = d lnL/ds, d2 = d2 lnL/ds2 at s = 0
+ * (d2 includes the mixed term 2 alpha beta d2 lnL/(dt_a dt_b)).  The reference's root
+ * reparametrisation of a rooted non-homogeneous tree (reparametrizeRoot = true,
+ * Likelihood/AbstractNonHomogeneousTreeLikelihood.cpp:312-330, 377-389) uses
+ *   BrLenRoot:    alpha = RootPosition, beta = 1 - RootPosition
+ *   RootPosition: alpha = BrLenRoot,    beta = -BrLenRoot
+ * and replaces computeTreeDLikelihood / computeTreeD2Likelihood for those two variables
+ * (Likelihood/RNonHomogeneousTreeLikelihood.cpp:391-560, 862-1100).  Requires dP and d2P of
+ * both branches.  Any state and class count. */
+int plk_root_pair_derivatives(plk_handle h, int a, int b, double alpha, double beta, double* d1, double* d2);
+
 /* Double-recursive derivatives (handle created with PLK_FLAG_DOUBLE_RECURSIVE): d lnL/dt and
  * d2 lnL/dt2 for EVERY branch of the last plk_update_partials tree, written to d1[node] and
  * d2[node] (n_nodes entries each, 0 at the root).  One preorder pass computes each branch's

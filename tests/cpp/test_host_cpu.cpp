@@ -5,7 +5,10 @@
 #include <Bpp/Phyl/Model/Nucleotide/T92.h>
 #include <Bpp/Phyl/Model/Protein/LG08.h>
 #include <Bpp/Phyl/Model/RateDistribution/GammaDiscreteRateDistribution.h>
+#include <Bpp/Phyl/Model/FrequencySet/NucleotideFrequencySet.h>
 #include <Bpp/Phyl/Model/SubstitutionModelSet.h>
+#include <Bpp/Phyl/Simulation/NonHomogeneousSequenceSimulator.h>
+#include <Bpp/Numeric/Prob/GammaDiscreteDistribution.h>
 #include <Bpp/Phyl/TreeTemplate.h>
 #include <Bpp/Seq/Alphabet/AlphabetTools.h>
 
@@ -104,7 +107,52 @@ int main() {
   std::printf("{\"kind\": \"modelset\", \"n\": %zu, \"names\": [", set->getNumberOfModels());
   std::vector<std::string> pn = set->getParameters().getParameterNames();
   for (size_t i = 0; i < pn.size(); i++) std::printf("%s\"%s\"", i ? ", " : "", pn[i].c_str());
+  std::printf("], \"independent\": [");
+  std::vector<std::string> in = set->getIndependentParameters().getParameterNames();
+  for (size_t i = 0; i < in.size(); i++) std::printf("%s\"%s\"", i ? ", " : "", in[i].c_str());
+  // the global kappa: changing model 1's copy moves every model; nodes with the parameter
+  ParameterList k = set->getParameters().createSubList(std::vector<std::string>(1, "T92.kappa_1"));
+  k[0].setValue(2.5);
+  set->matchParametersValues(k);
+  std::printf("], \"kappa_last\": %.17g, \"changed_models\": %zu, \"kappa_nodes\": %zu, \"theta2_nodes\": [",
+              set->getModel(set->getNumberOfModels() - 1)->getParameterValue("kappa"),
+              set->getLastChangedModels().size(), set->getNodesWithParameter("T92.kappa_1").size());
+  std::vector<int> tn = set->getNodesWithParameter("T92.theta_2");
+  for (size_t i = 0; i < tn.size(); i++) std::printf("%s%d", i ? ", " : "", tn[i]);
   std::printf("], \"theta2\": %.17g, \"theta1\": %.17g}\n", set->getModel(1)->getParameterValue("theta"),
               set->getModel(0)->getParameterValue("theta"));
+  // NonHomogeneousSequenceSimulator on a rooted cherry with per-branch GC content: the
+  // empirical joint distribution of the two leaves against sum_c p_c sum_x pi_x
+  // P_a[c][x][i] P_b[c][x][j] (tests/test_host.py)
+  {
+    std::unique_ptr<TreeTemplate<Node> > ch(TreeTemplateTools::parenthesisToTree("(a:0.15,b:0.4);"));
+    std::map<std::string, std::vector<Vint> > g;
+    g["T92.kappa"] = {};
+    std::unique_ptr<SubstitutionModelSet> ms(SubstitutionModelSetTools::createNonHomogeneousModelSet(
+        new T92(dna, 2.), new GCFrequencySet(dna, 0.35), ch.get(), std::map<std::string, std::string>(), g));
+    ms->setParameterValue("T92.theta_1", 0.3);
+    ms->setParameterValue("T92.theta_2", 0.7);
+    GammaDiscreteDistribution rd(4, 0.6, 0.6);
+    NonHomogeneousSequenceSimulator sim(ms.get(), &rd, ch.get());
+    const size_t n = 200000;
+    std::unique_ptr<SiteContainer> sites(sim.simulate(n));
+    std::vector<double> emp(16, 0.), want(16, 0.);
+    for (size_t i = 0; i < n; i++) emp[sites->getState(0, i) * 4 + sites->getState(1, i)] += 1. / n;
+    const Vdouble pi = ms->getRootFrequencies();
+    for (size_t c = 0; c < 4; c++) {
+      const double r = rd.getCategory(c), pc = rd.getProbability(c);
+      RowMatrix<double> Pa = ms->getModelForNode(ch->getRootNode()->getSon(0)->getId())->getPij_t(0.15 * r);
+      RowMatrix<double> Pb = ms->getModelForNode(ch->getRootNode()->getSon(1)->getId())->getPij_t(0.4 * r);
+      for (int x = 0; x < 4; x++)
+        for (int i = 0; i < 4; i++)
+          for (int j = 0; j < 4; j++) want[i * 4 + j] += pc * pi[x] * Pa(x, i) * Pb(x, j);
+    }
+    std::printf("{\"kind\": \"simulator\", \"n\": %zu, \"names\": [\"%s\", \"%s\"], ", n,
+                sites->getSequencesNames()[0].c_str(), sites->getSequencesNames()[1].c_str());
+    printVec("empirical", emp);
+    std::printf(", ");
+    printVec("expected", want);
+    std::printf("}\n");
+  }
   return 0;
 }

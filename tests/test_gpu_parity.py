@@ -750,6 +750,45 @@ def test_branch_derivatives_any_state_count(S, C, mode, scaling):
     del pm
 
 
+@pytest.mark.parametrize("S,C,mode,scaling,n_taxa", [(4, 4, "lnl_only", False, 12), (4, 4, "materialize", True, 3),
+                                                     (20, 2, "levelwise", True, 10), (4, 1, "subtree", False, 9)])
+def test_root_pair_derivatives_vs_oracle_finite_differences(S, C, mode, scaling, n_taxa):
+    """plk_root_pair_derivatives (the reference's BrLenRoot / RootPosition derivatives,
+    RNonHomogeneousTreeLikelihood.cpp:391-560, 862-1100): two root sons moved by
+    t_a + alpha s, t_b + beta s, against central differences of the oracle along that line.
+    n_taxa 3 puts two tips under the root (scratch tip rows)."""
+    n_pat = 600
+    et, m, alph, rates, probs, states = _random_problem(S, C, n_taxa, n_pat, seed=70 + S + C + n_taxa)
+    modes = dict(MODES, subtree=plk.PLK_FLAG_SUBTREE_PATTERNS)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | modes[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, S, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    kids = [c for p, ch in et.ops if p == et.root for c in ch]
+    a, b = kids[0], kids[1]
+    for alpha, beta in ((0.3, 0.7), (0.25, -0.25), (1.0, 0.0)):
+        d1, d2 = eng.root_pair_derivatives(int(a), int(b), alpha, beta)
+
+        def lnl_at(s):
+            bl = et.brlen.copy()
+            bl[a] += alpha * s
+            bl[b] += beta * s
+            e2 = phylo.EngineTree(et.n_tips, et.n_internal, et.root, et.tip_names, et.ops, bl, {}, [], [])
+            return oracle_for(e2, states, alph.init_table, rates, probs, m.pi, [m], scaling=scaling)[0]
+
+        h, h2 = 1e-5, 1e-4
+        fd1 = (lnl_at(h) - lnl_at(-h)) / (2 * h)
+        fd2 = (lnl_at(h2) - 2 * lnl_at(0.0) + lnl_at(-h2)) / h2 ** 2
+        assert abs(d1 - fd1) <= 1e-6 * max(1.0, abs(fd1)), (alpha, beta, d1, fd1)
+        assert abs(d2 - fd2) <= 2e-4 * max(1.0, abs(fd2)), (alpha, beta, d2, fd2)
+        if beta == 0.0:  # one branch only: the ordinary branch derivative
+            e1, e2_ = eng.branch_derivatives(int(a))
+            assert abs(d1 - e1) <= 1e-10 * max(1.0, abs(e1)) and abs(d2 - e2_) <= 1e-9 * max(1.0, abs(e2_))
+    with pytest.raises(plk.PlkError):
+        eng.root_pair_derivatives(int(a), int(a), 0.5, 0.5)
+
+
 def test_branch_derivatives_path_equals_kernel(monkeypatch):
     """4 states: the levelwise path derivatives equal the register-resident deriv_kernel."""
     et, m, alph, rates, probs, states = _random_problem(4, 4, 24, 3000, seed=61)

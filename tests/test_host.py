@@ -107,8 +107,26 @@ def test_host_trees(host_records):
 def test_host_model_set_naming(host_records):
     r = next(x for x in host_records if x["kind"] == "modelset")
     assert r["n"] == 6
-    assert r["names"][0] == "T92.kappa" and "T92.theta_6" in r["names"] and r["names"][-1] == "GC.theta"
+    # the reference's layout (SubstitutionModelSetTools.cpp:81-175): root frequencies first,
+    # every model parameter suffixed _<k>, the global kappa's copies aliased to model 1's
+    assert r["names"][0] == "GC.theta" and r["names"][1:3] == ["T92.kappa_1", "T92.theta_1"]
+    assert "T92.theta_6" in r["names"] and "T92.kappa_6" in r["names"]
+    assert r["independent"] == ["GC.theta", "T92.kappa_1"] + [f"T92.theta_{k}" for k in range(1, 7)]
+    assert r["kappa_last"] == 2.5 and r["changed_models"] == 6 and r["kappa_nodes"] == 6
+    assert len(r["theta2_nodes"]) == 1
     assert r["theta2"] == 0.7 and r["theta1"] == 0.5
+
+
+def test_host_simulator_joint_distribution(host_records):
+    """NonHomogeneousSequenceSimulator (Simulation/NonHomogeneousSequenceSimulator.cpp:306-353,
+    433-483): the leaves of a rooted cherry are drawn from sum_c p_c sum_x pi_x P_a P_b."""
+    r = next(x for x in host_records if x["kind"] == "simulator")
+    assert r["names"] == ["a", "b"]
+    emp, want = np.array(r["empirical"]), np.array(r["expected"])
+    assert abs(want.sum() - 1.0) < 1e-12 and abs(emp.sum() - 1.0) < 1e-9
+    # binomial standard error per cell at n = 200000: 5 sigma
+    se = np.sqrt(want * (1 - want) / r["n"])
+    assert np.all(np.abs(emp - want) <= 5 * se + 1e-12), np.max(np.abs(emp - want) / se)
 
 
 # ------------------------------------------------------------------ Python host helpers
