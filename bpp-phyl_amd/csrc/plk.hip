@@ -389,8 +389,8 @@ void write_file_atomic(const std::string& path, const char* data, size_t n) {
   const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
   FILE* f = std::fopen(tmp.c_str(), "wb");
   if (!f) return;
-  const bool ok = std::fwrite(data, 1, n, f) == n;
-  std::fclose(f);
+  bool ok = std::fwrite(data, 1, n, f) == n;
+  ok = std::fclose(f) == 0 && ok;  // a full disk often shows up only here
   if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
 }
 
@@ -400,7 +400,10 @@ uint64_t fnv1a64(const std::string& s) {
   return x;
 }
 
-int jit_compile(plk_handle h, const std::string& src, std::vector<char>* code) {
+// Code object of `src`: from the disk cache unless `bypass_cache`, else compiled with hiprtc
+// (and stored); *from_cache tells which.
+int jit_compile(plk_handle h, const std::string& src, std::vector<char>* code, bool bypass_cache, bool* from_cache) {
+  *from_cache = false;
   const char* opts[] = {"--offload-arch=gfx950", "-O3"};
   const bool log = env_is("PLK_JIT_LOG", '1');
   std::string dir = jit_cache_dir(), stem;
@@ -412,9 +415,10 @@ int jit_compile(plk_handle h, const std::string& src, std::vector<char>* code) {
              (unsigned long long)fnv1a64(src + opts[0] + opts[1] + std::to_string(maj) + "." + std::to_string(mnr)));
     stem = dir + "/" + hx;
     std::vector<char> stored;
-    if (read_file(stem + ".hip", &stored) && stored.size() == src.size() &&
+    if (!bypass_cache && read_file(stem + ".hip", &stored) && stored.size() == src.size() &&
         std::memcmp(stored.data(), src.data(), src.size()) == 0 && read_file(stem + ".co", code)) {
       if (log) std::fprintf(stderr, "[plk] jit cache hit %s.co\n", stem.c_str());
+      *from_cache = true;
       return PLK_OK;
     }
   }
@@ -455,12 +459,13 @@ int jit_function(plk_handle h, const std::string& src, const char* name, hipFunc
     return PLK_OK;
   }
   auto ct = g_jit_code.find(src);
+  bool from_cache = false;
   if (ct == g_jit_code.end()) {
     std::vector<char> code;
-    if (int rc = jit_compile(h, src, &code)) return rc;
+    if (int rc = jit_compile(h, src, &code, false, &from_cache)) return rc;
     ct = g_jit_code.emplace(src, std::move(code)).first;
   }
-  const std::vector<char>& code = ct->second;
+  std::vector<char>& code = ct->second;
   // PLK_JIT_DUMP=<dir>: keep the generated source and code object for inspection
   // (llvm-objdump -d --mcpu=gfx950 <dir>/plk_jit_<n>.co)
   if (const char* dir = env_get("PLK_JIT_DUMP")) {
@@ -476,7 +481,13 @@ int jit_function(plk_handle h, const std::string& src, const char* name, hipFunc
   }
   hipSetDevice(h->device);
   hipModule_t mod;
-  HIPCHK(h, hipModuleLoadData(&mod, code.data()));
+  if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+    if (!from_cache) return fail(h, PLK_ERR_DEVICE, "hipModuleLoadData of the compiled tree kernel failed");
+    // a damaged disk-cache entry: recompile and overwrite it
+    (void)hipGetLastError();
+    if (int rc = jit_compile(h, src, &code, true, &from_cache)) return rc;
+    HIPCHK(h, hipModuleLoadData(&mod, code.data()));
+  }
   hipFunction_t fn;
   HIPCHK(h, hipModuleGetFunction(&fn, mod, name));
   g_jit_cache.emplace(key, fn);
@@ -881,6 +892,8 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   return PLK_OK;
 }
 
+void comm_release(plk_handle h);
+
 int plk_destroy(plk_handle h) {
   if (!h) return PLK_OK;
   if (!h->shards.empty()) {
@@ -889,14 +902,8 @@ int plk_destroy(plk_handle h) {
     return PLK_OK;
   }
   hipSetDevice(h->device);
-  if (h->comm) {
-    if (h->stream) hipStreamSynchronize(h->stream);
-    ncclCommDestroy(h->comm);
-  }
-  for (void* p : {(void*)h->d_blk_local, (void*)h->d_blk_all, (void*)h->d_comm_counts})
-    if (p) hipFree(p);
-  if (h->h_total) hipHostFree(h->h_total);
   if (h->stream) hipStreamSynchronize(h->stream);
+  comm_release(h);
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
@@ -935,6 +942,23 @@ int plk_comm_get_id(plk_comm_id* id) {
   return PLK_OK;
 }
 
+// Tear down a communicator and its exchange buffers (a failed plk_comm_init leaves the
+// handle on the single-rank path, as before the call).
+void comm_release(plk_handle h) {
+  if (h->comm) ncclCommDestroy(h->comm);
+  h->comm = nullptr;
+  for (void* p : {(void*)h->d_blk_local, (void*)h->d_blk_all, (void*)h->d_comm_counts})
+    if (p) hipFree(p);
+  h->d_blk_local = h->d_blk_all = nullptr;
+  h->d_comm_counts = nullptr;
+  if (h->h_total) hipHostFree(h->h_total);
+  h->h_total = nullptr;
+  h->d_total = nullptr;
+  h->comm_ranks = 0;
+  h->comm_rank = 0;
+  h->comm_cmax = 0;
+}
+
 int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id) {
   env_refresh();
   if (!h || !id || n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(h, PLK_ERR_ARG, "bad communicator arguments");
@@ -947,29 +971,39 @@ int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id) {
     h->comm = nullptr;
     return fail(h, PLK_ERR_DEVICE, "ncclCommInitRank(%d ranks, rank %d) failed", n_ranks, rank);
   }
+  int64_t* d_one = nullptr;
+  // every failure after the communicator exists goes through comm_release
+  auto setup = [&]() -> int {
+    // block counts of every rank, once: per evaluation the all-gather has a fixed size
+    int rc = dalloc(h, (void**)&h->d_comm_counts, (size_t)n_ranks * sizeof(int64_t));
+    if (rc) return rc;
+    if ((rc = dalloc(h, (void**)&d_one, sizeof(int64_t)))) return rc;
+    const int64_t mine = h->n_blocks;
+    HIPCHK(h, hipMemcpy(d_one, &mine, sizeof(int64_t), hipMemcpyHostToDevice));
+    if (ncclAllGather(d_one, h->d_comm_counts, 1, ncclInt64, h->comm, h->stream) != ncclSuccess)
+      return fail(h, PLK_ERR_DEVICE, "ncclAllGather of the block counts failed");
+    std::vector<int64_t> counts((size_t)n_ranks);
+    HIPCHK(h, hipMemcpyAsync(counts.data(), h->d_comm_counts, counts.size() * sizeof(int64_t),
+                             hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const int64_t cmax = *std::max_element(counts.begin(), counts.end());
+    if ((rc = dalloc(h, (void**)&h->d_blk_local, (size_t)cmax * sizeof(double)))) return rc;
+    if ((rc = dalloc(h, (void**)&h->d_blk_all, (size_t)n_ranks * cmax * sizeof(double)))) return rc;
+    HIPCHK(h, hipMemset(h->d_blk_local, 0, (size_t)cmax * sizeof(double)));
+    if (hipHostMalloc((void**)&h->h_total, sizeof(double), hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&h->d_total, h->h_total, 0) != hipSuccess)
+      return fail(h, PLK_ERR_OOM, "pinned total");
+    h->comm_cmax = cmax;
+    return PLK_OK;
+  };
+  int rc = env_is("PLK_TEST_COMM_FAIL", '1') ? fail(h, PLK_ERR_OOM, "forced exchange-setup failure (test)") : setup();
+  if (d_one) hipFree(d_one);
+  if (rc) {
+    comm_release(h);
+    return rc;
+  }
   h->comm_ranks = n_ranks;
   h->comm_rank = rank;
-  // block counts of every rank, once: per evaluation the all-gather has a fixed size
-  int rc = dalloc(h, (void**)&h->d_comm_counts, (size_t)n_ranks * sizeof(int64_t));
-  if (rc) return rc;
-  int64_t* d_one = nullptr;
-  if ((rc = dalloc(h, (void**)&d_one, sizeof(int64_t)))) return rc;
-  const int64_t mine = h->n_blocks;
-  HIPCHK(h, hipMemcpy(d_one, &mine, sizeof(int64_t), hipMemcpyHostToDevice));
-  if (ncclAllGather(d_one, h->d_comm_counts, 1, ncclInt64, h->comm, h->stream) != ncclSuccess)
-    return fail(h, PLK_ERR_DEVICE, "ncclAllGather of the block counts failed");
-  std::vector<int64_t> counts((size_t)n_ranks);
-  HIPCHK(h, hipMemcpyAsync(counts.data(), h->d_comm_counts, counts.size() * sizeof(int64_t), hipMemcpyDeviceToHost,
-                           h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  hipFree(d_one);
-  h->comm_cmax = *std::max_element(counts.begin(), counts.end());
-  if ((rc = dalloc(h, (void**)&h->d_blk_local, (size_t)h->comm_cmax * sizeof(double)))) return rc;
-  if ((rc = dalloc(h, (void**)&h->d_blk_all, (size_t)n_ranks * h->comm_cmax * sizeof(double)))) return rc;
-  HIPCHK(h, hipMemset(h->d_blk_local, 0, (size_t)h->comm_cmax * sizeof(double)));
-  if (hipHostMalloc((void**)&h->h_total, sizeof(double), hipHostMallocMapped) != hipSuccess ||
-      hipHostGetDevicePointer((void**)&h->d_total, h->h_total, 0) != hipSuccess)
-    return fail(h, PLK_ERR_OOM, "pinned total");
   return PLK_OK;
 }
 

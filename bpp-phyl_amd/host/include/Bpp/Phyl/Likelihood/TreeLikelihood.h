@@ -82,6 +82,13 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   bool incremental_ = true;
   bool compressed_ = false;  // usePatterns: PLK_FLAG_SUBTREE_PATTERNS on the engine
   bool allDirty_ = true;     // next fireParameterChanged recomputes every P(t) (initialize)
+  // fused lnL-only traversal (PLK_FLAG_LNL_ONLY, the benched kernels): interior partials stay
+  // in registers, so every evaluation is one full traversal launch and derivatives
+  // recompute the partials on demand
+  bool lnlOnly_ = false;
+  // per engine node: dP / d2P older than P (evaluations upload P only; the derivative
+  // calls bring them up to date first)
+  mutable std::vector<char> derivStale_;
   bool hostP_ = false;       // some branch P(t) came from the host (Taylor branch)
   size_t maxSons_ = 0;
   bool derivFirst_ = true, derivSecond_ = true;
@@ -117,6 +124,13 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   void uploadEigen(int modelIndex, const SubstitutionModel& model);
   void uploadRates();
   void computeTreeLikelihood(const std::vector<const Node*>* changed = nullptr);
+  // One evaluation: P(t) of `pnodes`, the traversal (full, or the ancestors of `pnodes`
+  // when `incremental` and the engine keeps every partial), the root reduction -- one
+  // plk_evaluate call (Likelihood/RHomogeneousTreeLikelihood.cpp:255-283 as one launch
+  // sequence); sets minusLogLik_.
+  void evaluateTree(const std::vector<const Node*>& pnodes, bool incremental);
+  // dP / d2P of every branch whose P(t) changed since they were last computed
+  void refreshDerivativeMatrices() const;
   double reduceRoot() const;
   void fetchSiteLnl() const;
   void check(int rc, const char* what) const;

@@ -162,6 +162,19 @@ void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
   compressed_ = usePatterns_ && !(extraFlags_ & PLK_FLAG_DOUBLE_RECURSIVE) && maxSons_ <= 3;
   if (const char* e = std::getenv("BPP_AMD_USE_PATTERNS"))
     if (e[0] == '0') compressed_ = false;
+  // Shapes the fused tree kernels serve (4 states with 1, 2 or 4 classes: plk_jit_tree4;
+  // 20 states, up to 4 classes: plk_jit_treeM; 64 states, 1 class: treeM) run lnL-only:
+  // one launch per evaluation with the partials in registers, faster than the per-subtree
+  // compression at every size measured (cfg2: 0.14 vs 0.36 ms), so compression is kept for
+  // the other shapes.  BPP_AMD_FUSED=0 turns this off.
+  const size_t S = nbStates_, C = nbClasses_;
+  lnlOnly_ = (S == 4 && (C == 1 || C == 2 || C == 4)) || (S == 20 && C <= 4) || (S == 64 && C == 1);
+  if (const char* e = std::getenv("BPP_AMD_FUSED"))
+    if (e[0] == '0') lnlOnly_ = false;
+  if (lnlOnly_) {
+    compressed_ = false;
+    flags |= PLK_FLAG_LNL_ONLY;
+  }
   if (compressed_) flags |= PLK_FLAG_SUBTREE_PATTERNS;
   plk_handle h = nullptr;
   const std::vector<int> devs = devicesFromEnv();
@@ -171,6 +184,7 @@ void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
                                            (int64_t)nbDistinctSites_, nTips_, nInternal_, (int)nModels, flags, &h);
   if (rc != PLK_OK) throw DeviceException(rc, std::string("plk_create: ") + plk_last_error(nullptr));
   engine_ = h;
+  derivStale_.assign((size_t)(nTips_ + nInternal_), 1);
 }
 
 void AbstractPlkTreeLikelihood::initBranchLengthsParameters() {
@@ -270,11 +284,96 @@ void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& 
     t.resize(k);
     if (br.empty()) return;
   }
-  // dP and d2P ride along when derivatives are enabled (the reference computes them
-  // with every P, AbstractHomogeneousTreeLikelihood.cpp:375-413)
-  const unsigned mask = (derivFirst_ || derivSecond_) ? (PLK_DERIV_P | PLK_DERIV_DP | PLK_DERIV_D2P) : PLK_DERIV_P;
-  check(plk_update_pmatrices(engine_, (int)br.size(), br.data(), mod.data(), t.data(), mask),
+  // P only: dP and d2P (which the reference computes with every P,
+  // AbstractHomogeneousTreeLikelihood.cpp:375-413) follow when a derivative is requested
+  check(plk_update_pmatrices(engine_, (int)br.size(), br.data(), mod.data(), t.data(), PLK_DERIV_P),
         "plk_update_pmatrices");
+  for (int b : br) derivStale_[(size_t)b] = 1;
+}
+
+void AbstractPlkTreeLikelihood::refreshDerivativeMatrices() const {
+  std::vector<int32_t> br, mod;
+  std::vector<double> t;
+  for (const Node* n : nodes_) {
+    const int e = engineIndex_.at(n);
+    if (!derivStale_[(size_t)e]) continue;
+    const SubstitutionModel* m = modelForIndex(modelIndexForNode(n));
+    if (m && !m->isNonSingular()) continue;  // host P(t): numerical derivatives
+    br.push_back(e);
+    mod.push_back(modelIndexForNode(n));
+    t.push_back(n->getDistanceToFather());
+  }
+  if (br.empty()) return;
+  check(plk_update_pmatrices(engine_, (int)br.size(), br.data(), mod.data(), t.data(),
+                             PLK_DERIV_P | PLK_DERIV_DP | PLK_DERIV_D2P),
+        "plk_update_pmatrices");
+  for (int b : br) derivStale_[(size_t)b] = 0;
+}
+
+void AbstractPlkTreeLikelihood::evaluateTree(const std::vector<const Node*>& pnodes, bool incremental) {
+  stats_.pmatBranches += pnodes.size();
+  // host P(t) (a model whose eigen-system failed its check) goes up first
+  std::vector<int32_t> br, mod;
+  std::vector<double> t;
+  {
+    const Vdouble& rates = rateDistribution_->getCategories();
+    std::vector<double> P(nbClasses_ * nbStates_ * nbStates_);
+    for (const Node* n : pnodes) {
+      const int e = engineIndex_.at(n), mi = modelIndexForNode(n);
+      const SubstitutionModel* m = modelForIndex(mi);
+      if (m && !m->isNonSingular()) {
+        hostP_ = true;
+        for (size_t c = 0; c < nbClasses_; c++) {
+          const RowMatrix<double>& Pc = m->getPij_t(n->getDistanceToFather() * rates[c]);
+          std::copy(Pc.data(), Pc.data() + nbStates_ * nbStates_, P.begin() + c * nbStates_ * nbStates_);
+        }
+        check(plk_set_pmatrix(engine_, e, P.data()), "plk_set_pmatrix");
+      } else {
+        br.push_back(e);
+        mod.push_back(mi);
+        t.push_back(n->getDistanceToFather());
+      }
+    }
+  }
+  // the op list: every internal node, or the ancestors of the changed branches when the
+  // engine keeps all partials in HBM (not lnL-only, not compressed)
+  std::vector<char> need;
+  if (incremental && incremental_ && !compressed_ && !lnlOnly_) {
+    need.assign((size_t)(nTips_ + nInternal_), 0);
+    for (const Node* n : pnodes)
+      for (const Node* p = n->getFather(); p; p = p->getFather()) {
+        char& f = need[(size_t)engineIndex_.at(p)];
+        if (f) break;
+        f = 1;
+      }
+  }
+  std::vector<plk_op> ops;
+  ops.reserve(opParent_.size());
+  for (size_t i = 0; i < opParent_.size(); i++) {
+    if (!need.empty() && !need[(size_t)opParent_[i]]) continue;
+    ops.emplace_back();
+    plk_op& o = ops.back();
+    o.parent = opParent_[i];
+    o.n_children = (int)opChildren_[i].size();
+    for (size_t k = 0; k < 3; k++) o.child[k] = k < opChildren_[i].size() ? opChildren_[i][k] : -1;
+    o.flags = opFlags_[i];
+  }
+  drValid_ = false;
+  siteLnlValid_ = false;
+  stats_.evaluations++;
+  if (need.empty()) stats_.fullTraversals++;
+  for (int b : br) derivStale_[(size_t)b] = 1;
+  if (ops.empty()) {
+    check(plk_update_pmatrices(engine_, (int)br.size(), br.data(), mod.data(), t.data(), PLK_DERIV_P),
+          "plk_update_pmatrices");
+    minusLogLik_ = -reduceRoot();
+    return;
+  }
+  double lnl = 0.;
+  check(plk_evaluate(engine_, (int)br.size(), br.data(), mod.data(), t.data(), ops.data(), (int)ops.size(),
+                     rootEngine_, &lnl, nullptr),
+        "plk_evaluate");
+  minusLogLik_ = -lnl;
 }
 
 // Full postorder traversal (Likelihood/RHomogeneousTreeLikelihood.cpp:795-798), or,
@@ -284,8 +383,9 @@ void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& 
 // the result is bit-identical to a full traversal.
 void AbstractPlkTreeLikelihood::computeTreeLikelihood(const std::vector<const Node*>* changed) {
   std::vector<char> need;
-  // a compressed traversal rebuilds every node from its subtree's patterns: always full
-  if (changed && incremental_ && !compressed_) {
+  // a compressed traversal rebuilds every node from its subtree's patterns, an lnL-only
+  // one keeps no partials: both always full
+  if (changed && incremental_ && !compressed_ && !lnlOnly_) {
     need.assign((size_t)(nTips_ + nInternal_), 0);
     for (const Node* n : *changed)
       for (const Node* p = n->getFather(); p; p = p->getFather()) {
@@ -394,6 +494,7 @@ bool AbstractPlkTreeLikelihood::analyticDerivatives(const std::string& variable,
   if (variable.size() <= 5 || variable.find_first_not_of("0123456789", 5) != std::string::npos)
     throw Exception("analyticDerivatives: not a branch-length parameter: " + variable);
   const Node* n = nodes_.at(TextTools::to<size_t>(variable.substr(5)));
+  refreshDerivativeMatrices();
   if (extraFlags_ & PLK_FLAG_DOUBLE_RECURSIVE) {
     if (!drValid_) {
       const size_t nn = (size_t)(nTips_ + nInternal_);
@@ -537,13 +638,13 @@ void RHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList&) {
   const bool rateChanged = rateDistribution_->matchParametersValues(getParameters());
   if (allDirty_ || modelChanged || rateChanged) {
     allDirty_ = false;
-    computeAllTransitionProbabilities();
-    computeTreeLikelihood();
+    uploadEigen(0, *model_);
+    uploadRates();
+    uploadRootFrequencies(model_->getFrequencies());
+    evaluateTree(std::vector<const Node*>(nodes_.begin(), nodes_.end()), false);
   } else {
-    updatePmatrices(changed);
-    computeTreeLikelihood(&changed);
+    evaluateTree(changed, true);
   }
-  minusLogLik_ = -reduceRoot();
 }
 
 // ---------------------------------------------------------------------------
@@ -683,6 +784,7 @@ bool RNonHomogeneousTreeLikelihood::analyticDerivatives(const std::string& varia
   const double alpha = variable == "BrLenRoot" ? pos : len;
   const double beta = variable == "BrLenRoot" ? 1. - pos : -len;
   const int a = engineIndex_.at(idToNode_.at(root1_)), b = engineIndex_.at(idToNode_.at(root2_));
+  refreshDerivativeMatrices();
   const int rc = plk_root_pair_derivatives(engine_, a, b, alpha, beta, d1, d2);
   if (rc == PLK_ERR_UNSUPPORTED) return false;
   check(rc, "plk_root_pair_derivatives");
@@ -727,9 +829,10 @@ void RNonHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList&) {
   const bool rateChanged = rateDistribution_->matchParametersValues(getParameters());
   if (allDirty_ || rateChanged) {
     allDirty_ = false;
-    computeAllTransitionProbabilities();
-    computeTreeLikelihood();
-    minusLogLik_ = -reduceRoot();
+    for (size_t m = 0; m < modelSet_->getNumberOfModels(); m++) uploadEigen((int)m, *modelSet_->getModel(m));
+    uploadRates();
+    uploadRootFrequencies(modelSet_->getRootFrequencies());
+    evaluateTree(std::vector<const Node*>(nodes_.begin(), nodes_.end()), false);
     return;
   }
   if (setChanged) {
@@ -743,9 +846,7 @@ void RNonHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList&) {
     }
     if (modelSet_->getLastRootFrequenciesChanged()) uploadRootFrequencies(modelSet_->getRootFrequencies());
   }
-  updatePmatrices(changed);
-  computeTreeLikelihood(&changed);
-  minusLogLik_ = -reduceRoot();
+  evaluateTree(changed, true);
 }
 
 }  // namespace bpp

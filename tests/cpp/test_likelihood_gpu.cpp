@@ -19,6 +19,9 @@
 #include <Bpp/Seq/Container/VectorSiteContainer.h>
 
 #include <cmath>
+#include <string>
+
+#include "plk.h"
 #include <iomanip>
 #include <iostream>
 #include <memory>
@@ -48,6 +51,12 @@ static void unrootedGammaCase() {
   RHomogeneousTreeLikelihood tl(*tree, aln, &model, &rdist, true, false);
   tl.initialize();
   expectNear("T92+G4 initial -lnL", tl.getValue(), 85.030942031997312824, 1e-9);
+  // the drop-in evaluates through the benched kernel: the fused lnL-only traversal
+  {
+    const std::string path = plk_kernel_path(tl.getEngine());
+    std::cout << "kernel path through the mirror: " << path << (path == "jit_tree4" ? " ok" : " FAIL") << std::endl;
+    if (path != "jit_tree4") failures++;
+  }
   std::cout << "distinct sites: " << tl.getNumberOfDistinctSites() << " of " << tl.getNumberOfSites() << std::endl;
   // per-site log-likelihoods sum to the total
   double s = 0.;

@@ -115,6 +115,63 @@ def test_comm_single_rank_bitwise(config, flags):
     assert s0[0] == s1[0] and np.array_equal(s0[1], s1[1])
 
 
+def test_comm_init_failure_leaves_single_rank_path(monkeypatch):
+    """A failure after ncclCommInitRank (forced exchange-setup failure) releases the
+    communicator and its buffers: later evaluations take the single-rank path and give the
+    handle's own lnL, and plk_comm_init can be retried."""
+    n = 2 * 4096 + 5
+    wl = workload.make_workload("gtr_g4_dna_1M_64", n_patterns=n)
+    et = wl.et
+    states = wl.simulate(0, n)
+    base = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY
+    ref = _setup(plk.Engine(0, wl.S, wl.C, n, et.n_tips, et.n_internal, 1, base), wl, states)
+    eng = _setup(plk.Engine(0, wl.S, wl.C, n, et.n_tips, et.n_internal, 1, base), wl, states)
+    monkeypatch.setenv("PLK_TEST_COMM_FAIL", "1")
+    with pytest.raises(plk.PlkError):
+        eng.comm_init(1, 0, plk.comm_get_id())
+    monkeypatch.delenv("PLK_TEST_COMM_FAIL")
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    ops = phylo.split_ops(et.ops)
+    l0, b0 = ref.evaluate(br, et.brlen[br], ops, et.root)
+    l1, b1 = eng.evaluate(br, et.brlen[br], ops, et.root)
+    assert l0 == l1 and np.array_equal(b0, b1)
+    eng.comm_init(1, 0, plk.comm_get_id())
+    l2, b2 = eng.evaluate(br, et.brlen[br], ops, et.root)
+    assert l2 == l0 and np.array_equal(b2, b0)
+
+
+@pytest.mark.skipif(plk.device_count() < 2, reason="distinct-device handles need two GPUs (the test box has one)")
+@pytest.mark.parametrize("config,flags", [("gtr_g4_dna_1M_64", plk.PLK_FLAG_LNL_ONLY),
+                                          ("lg08_g4_protein_200k_256", plk.PLK_FLAG_LNL_ONLY),
+                                          ("gtr_g4_dna_1M_64", 0)])
+def test_multi_device_distinct_gpus(config, flags):
+    """plk_create_multi over two different GPUs: per-device JIT module, hipSetDevice
+    discipline and per-device mapped staging -- lnL, block sums and branch derivatives equal
+    one handle (bitwise / 1e-12)."""
+    n = 3 * 4096 + 77
+    wl = workload.make_workload(config, n_patterns=n)
+    et = wl.et
+    states = wl.simulate(0, n)
+    base = (plk.PLK_FLAG_SCALING if wl.scaling else 0) | plk.PLK_FLAG_NONNEG_GUARD | flags
+    one = _setup(plk.Engine(0, wl.S, wl.C, n, et.n_tips, et.n_internal, 1, base), wl, states)
+    multi = _setup(plk.Engine([0, 1], wl.S, wl.C, n, et.n_tips, et.n_internal, 1, base), wl, states)
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    ops = phylo.split_ops(et.ops)
+    for scale in (1.0, 0.7):
+        t = et.brlen[br] * scale
+        l1, b1 = one.evaluate(br, t, ops, et.root)
+        lm, bm = multi.evaluate(br, t, ops, et.root)
+        assert l1 == lm and np.array_equal(b1, bm)
+    for e in (one, multi):
+        e.update_pmatrices(br, et.brlen[br] * 0.7, deriv_mask=7)
+        e.update_partials(ops)
+        e.root_loglik(et.root)
+    for b in (0, et.n_tips, br[-1]):
+        a1, a2 = one.branch_derivatives(int(b))
+        m1, m2 = multi.branch_derivatives(int(b))
+        assert abs(a1 - m1) <= 1e-12 * abs(a1) and abs(a2 - m2) <= 1e-12 * abs(a2)
+
+
 def test_cpp_drop_in_sharded_goldens():
     """The Bio++ mirror's drop-in program with the patterns sharded over two handles on the
     GPU (BPP_AMD_DEVICES=0,0): the reference goldens, optimisers included."""
