@@ -7,16 +7,20 @@ Contract (driver): python bench.py --gpus N --steps K --warmup W
 
 Workload: BASELINE.json config 2 -- GTR+Gamma4, 4 states, 1M synthetic site patterns,
 64-taxon balanced tree (unrooted by the API like the reference, so I = 62 internal
-nodes).  Weak scaling: every rank evaluates its own 1M-pattern slice of one global
-synthetic alignment (patterns are independent), so per-GPU work is fixed as N grows.
+nodes).  Weak scaling (default): every rank evaluates its own 1M-pattern slice of one
+global synthetic alignment (patterns are independent), so per-GPU work is fixed as N
+grows.  --scaling strong: BASELINE config 5 as stated ("2M patterns ... site-sharded across
+8 x MI355X") -- the job's 2M patterns split into contiguous 4096-aligned ranges over the N
+ranks (N = 1: all 2M on one GPU), value counting the job's P x I per step.
 
 One step = one likelihood evaluation as RHomogeneousTreeLikelihood::fireParameterChanged
 does it (plk_evaluate): all branch transition matrices (K4), the full postorder
 traversal -- by default (--mode lnl) the fused, tree-specialised kernel that keeps
 interior partials in registers and reads cherries from code-pair tables -- and the root
 reduction, whose fixed-order 4096-pattern block sums are all-gathered across ranks and
-summed in global order (the only cross-GPU exchange).  value = (P x I x K x N) /
-max-over-ranks wall time of the K timed steps, inputs already resident in HBM; this is
+summed in global order (the only cross-GPU exchange).  value = (P x I x K) /
+max-over-ranks wall time of the K timed steps (P = the job's patterns: N x 1M weak,
+2M strong), inputs already resident in HBM; this is
 the reference-equivalent rate (the reference computes every one of those node
 updates).  computed_updates_* report the updates actually computed per pattern
 (cherry-table nodes are lookups, SURVEY 8(d) "effective"), and roofline.executed the
@@ -49,8 +53,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="gtr_g4_dna_1M_64", choices=sorted(workload.CONFIGS))
-    ap.add_argument("--patterns", type=int, default=None, help="override patterns per rank")
+    ap.add_argument("--config", default=None, choices=sorted(workload.CONFIGS),
+                    help="default: gtr_g4_dna_1M_64 (config 2); with --scaling strong nh_gtr_g4_dna_2M_512 (config 5)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: every rank evaluates its own --patterns slice (per-GPU work fixed as N grows); "
+                         "strong: --patterns (default: the config's global count, 2M for config 5) in total, split "
+                         "into contiguous 4096-aligned ranges over the ranks")
+    ap.add_argument("--patterns", type=int, default=None,
+                    help="override patterns per rank (weak) or in total (strong)")
     ap.add_argument("--classes", type=int, default=None,
                     help="A/B experiments only: the config's model with this many Gamma classes")
     ap.add_argument("--cpu-sample", type=int, default=None, help="patterns in the CPU-baseline sample")
@@ -71,7 +81,10 @@ def parse():
                          "materialize: fused traversal writing every partial; levelwise: one launch per level; "
                          "subtree: per-subtree pattern compression (reference usePatterns=true) -- value is then "
                          "an EFFECTIVE rate (SURVEY 8d), reported beside the computed updates")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.config is None:
+        args.config = "nh_gtr_g4_dna_2M_512" if args.scaling == "strong" else "gtr_g4_dna_1M_64"
+    return args
 
 
 def host_cpu() -> dict:
@@ -272,9 +285,11 @@ def main():
     coll_dev = "cpu" if rehearse else "cuda"
 
     wl = workload.make_workload(args.config, n_classes=args.classes)
-    P = args.patterns or wl.n_patterns
+    cfg = workload.CONFIGS[args.config]
+    P_arg = args.patterns or (cfg.get("global_patterns", wl.n_patterns) if args.scaling == "strong" else wl.n_patterns)
+    start, end, P_job = shard.bench_range(args.scaling, rank, world, P_arg)
+    P = end - start            # this rank's patterns
     wl.n_patterns = P
-    start, end = rank * P, (rank + 1) * P
     t_setup = time.time()
     extra = {"lnl": plk.PLK_FLAG_LNL_ONLY, "materialize": 0, "levelwise": plk.PLK_FLAG_LEVELWISE,
              "subtree": plk.PLK_FLAG_SUBTREE_PATTERNS}[args.mode]
@@ -293,7 +308,7 @@ def main():
         dist.broadcast(cid, 0)
         ev.eng.comm_init(world, rank, bytes(cid.cpu().numpy()))
     t_setup = time.time() - t_setup
-    units_step = P * wl.et.n_internal
+    units_step = P_job * wl.et.n_internal   # the whole job's node updates per step
 
     def one_step():
         lnl, _, blocks = ev.step()
@@ -341,7 +356,7 @@ def main():
 
     if rank == 0:
         ms_step = elapsed * 1e3 / args.steps
-        value = units_step * world * args.steps / elapsed
+        value = units_step * args.steps / elapsed
         work = ev.eng.traversal_work()
         traffic, traffic_src = measured_traffic(args.config, args.mode, P)
         roof = roofline(wl, args.mode, P, ev_steps, tm, work, traffic) if not args.no_events else None
@@ -359,15 +374,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded counter-based simulation under the model, 1 pattern = 1 column)",
             "config": {
                 "workload": (f"{args.config}: {wl.models[0].name}{'+G%d' % wl.C if wl.C > 1 else ''} "
-                             f"{wl.alphabet.name}, {P} patterns per GPU, {wl.et.n_tips}-taxon balanced tree "
+                             f"{wl.alphabet.name}, {P_job} patterns in total ({P} on rank 0), "
+                             f"{wl.et.n_tips}-taxon balanced tree "
                              f"({'rooted' if wl.model_of_node is not None else 'unrooted'}, I={wl.et.n_internal})"),
                 "patterns_per_gpu": P,
+                "patterns_total": P_job,
                 "taxa": wl.et.n_tips,
                 "internal_nodes": wl.et.n_internal,
                 "states": wl.S,
@@ -380,10 +397,10 @@ def main():
             # node updates the kernels compute per pattern (cherry-table nodes and
             # per-subtree compression are lookups / skipped) -- value above is the
             # reference-equivalent ("effective") rate
-            "computed_updates_per_step": computed * world,
-            "computed_updates_per_s": computed * world * args.steps / elapsed,
+            "computed_updates_per_step": computed * P_job / P,
+            "computed_updates_per_s": computed * P_job / P * args.steps / elapsed,
             "table_nodes": work["table_nodes"],
-            "partials_only_updates_per_s": (units_step * ev_steps / (tm["partials_ms"] * 1e-3)
+            "partials_only_updates_per_s": (P * wl.et.n_internal * ev_steps / (tm["partials_ms"] * 1e-3)
                                             if tm["partials_ms"] > 0 else None),
             "kernel_ms_per_step": {"partials": tm["partials_ms"] / max(ev_steps, 1),
                                    "tables": tm["tables_ms"] / max(ev_steps, 1),

@@ -245,10 +245,8 @@ struct plk_handle_s {
   int64_t comm_cmax = 0;                  // block sums per rank in the all-gather (max over ranks)
   double* d_blk_local = nullptr;          // [comm_cmax] this rank's block sums (zero padded)
   unsigned* d_blk_cnt = nullptr;          // [n_blocks] arrival counters of the in-kernel block sums
-  hipStream_t stream2 = nullptr;          // second stream of the chunked two-tier jit_treeM launch
   DrPreOp* d_drpre = nullptr;             // fused DR preorder ops (dr_pre_s4_kernel)
   size_t d_drpre_cap = 0;
-  std::vector<hipEvent_t> chunk_events;
   double* d_blk_all = nullptr;            // [comm_ranks][comm_cmax]
   int64_t* d_comm_counts = nullptr;       // block sums per rank
   double* h_total = nullptr;              // mapped pinned: the global lnL
@@ -911,11 +909,6 @@ int plk_destroy(plk_handle h) {
                   h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_blk_cnt, h->d_drpre};
   for (void* p : bufs)
     if (p) hipFree(p);
-  if (h->stream2) {
-    hipStreamSynchronize(h->stream2);
-    hipStreamDestroy(h->stream2);
-  }
-  for (hipEvent_t e : h->chunk_events) hipEventDestroy(e);
   if (h->h_req) hipHostFree(h->h_req);
   if (h->h_blocks) hipHostFree(h->h_blocks);
   if (h->req_done) hipEventDestroy(h->req_done);
@@ -1774,52 +1767,6 @@ void launch_treeM(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
   }
 }
 
-// Two-tier jit_treeM traversal in K pattern chunks (multiples of kRootBlock patterns):
-// tier 1 of every chunk on the handle's stream, tier 2 of chunk k on a second stream after
-// tier 1 of chunk k; the handle's stream then waits for the last tier-2 chunk.
-int launch_jitm_chunked(plk_handle h, JMArgs ma, const JitMShape& msh, int K) {
-  if (!h->stream2) HIPCHK(h, hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
-  while ((int)h->chunk_events.size() < K + 1) {
-    hipEvent_t e;
-    HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    h->chunk_events.push_back(e);
-  }
-  const int64_t nb = (h->n_pad + kRootBlock - 1) / kRootBlock, per = (nb + K - 1) / K;  // (last chunk ragged)
-  EventPair ev;
-  if (h->timing & PLK_TIME_PARTIALS) {
-    ev = get_events(h, 0);
-    hipEventRecord(ev.a, h->stream);
-  }
-  const int n1 = (int)h->prog_tiers[0].size(), n2 = (int)h->prog_tiers[1].size();
-  for (int tier = 0; tier < 2; ++tier) {
-    hipStream_t st = tier == 0 ? h->stream : h->stream2;
-    for (int k = 0; k < K; ++k) {
-      const int64_t b0 = (int64_t)k * per * kRootBlock;
-      const int64_t b1 = std::min<int64_t>(b0 + per * kRootBlock, h->n_pad);
-      if (b0 >= b1) continue;
-      if (tier == 1) HIPCHK(h, hipStreamWaitEvent(st, h->chunk_events[(size_t)k], 0));
-      ma.p_base = b0;
-      int base = tier == 0 ? 0 : n1;
-      void* args[] = {&ma, &base};
-      HIPCHK(h, hipModuleLaunchKernel(h->jitm_fn, (unsigned)((b1 - b0) / (16 * msh.G)), (unsigned)(tier == 0 ? n1 : n2),
-                                      1, 64 * msh.G, 1, 1, (unsigned)msh.lds_bytes(), st, args, nullptr));
-      HIPCHK(h, hipGetLastError());
-      if (tier == 0) HIPCHK(h, hipEventRecord(h->chunk_events[(size_t)k], st));
-    }
-  }
-  HIPCHK(h, hipEventRecord(h->chunk_events[(size_t)K], h->stream2));
-  HIPCHK(h, hipStreamWaitEvent(h->stream, h->chunk_events[(size_t)K], 0));
-  if (h->timing & PLK_TIME_PARTIALS) {
-    hipEventRecord(ev.b, h->stream);
-    h->events.push_back(ev);
-    h->n_launches++;
-  }
-  h->fused_lnl_valid = h->prog_root >= 0;
-  h->fused_lnl_root = h->prog_root;
-  h->blocks_fused = false;
-  return PLK_OK;
-}
-
 int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const bool materialize = !(h->flags & PLK_FLAG_LNL_ONLY);
   const bool reduce = h->pi_set && h->rates_set;
@@ -2033,13 +1980,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     msh.L = env_int("PLK_JITM_L", 1, 1, 4);
     msh.minw = env_int("PLK_JITM_MINW", 2, 1, 8);
-    msh.direct = env_is("PLK_JITM_DIRECT", '1');
     msh.pd = env_int("PLK_JITM_PD", 1, 1, 3);
-    msh.hoist = env_int("PLK_JITM_HOIST", 0, 0, 1) != 0;
-    msh.youter = env_is("PLK_JITM_YOUTER", '1');
-    msh.padstage = env_is("PLK_JITM_PADSTAGE", '1');
-    msh.hyb = env_is("PLK_JITM_HYB", '1');
-    msh.debug = env_int("PLK_DEBUG_JITM", 0, 0, 7);
     // 16-pattern waves per workgroup: 4 (64 patterns) or 8 (128; every P(t) staging and its
     // barrier serve twice the patterns)
     msh.G = env_int("PLK_JITM_G", 4, 4, 8) >= 8 ? 8 : 4;
@@ -2069,19 +2010,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ma.cherry_table_bytes = (int64_t)lay.table_bytes;
     ma.cherry_count_bytes = (int64_t)lay.count_bytes;
     ma.guard = a.guard;
-    ma.p_base = 0;
   }
   h->kernel_path = jit ? "jit_tree4" : jitm ? "jit_treeM" : kind == FK_TREEM ? "treeM" : kind == FK_TREES ? "treeS" : "tree4";
-  // jit_treeM over two tiers: pattern chunks pipelined across the tiers on two streams --
-  // tier 2 (the top of the tree, HBM-bound: it reads every tier-1 fragment root) of chunk k
-  // runs beside tier 1 of chunk k + 1 (PLK_JITM_CHUNKS=K; default 1 = one launch per tier:
-  // cfg3 3.54 ms, K = 2 / 4 / 8 3.62 / 3.73 / 3.81 ms -- the tier-2 workgroups take
-  // residency slots from tier 1, whose waves are latency-bound, so nothing is hidden)
-  if (jitm && h->prog_tiers.size() == 2) {
-    const int nb = (int)((h->n_pad + kRootBlock - 1) / kRootBlock);
-    const int K = std::min(nb, env_int("PLK_JITM_CHUNKS", 1, 1, 64));
-    if (K > 1) return launch_jitm_chunked(h, ma, msh, K);
-  }
   int first = 0;
   for (const auto& t : h->prog_tiers) {
     a.frag_start = h->d_frag + first;

@@ -17,6 +17,11 @@
 // child feeds its parent straight from registers.  The A operand of block (X, Y) is
 // P[4X + lo][4Y + hi] -- pattern-independent, one 16-double tile per (class, X, Y) in LDS,
 // read with ds_read_b64 at a constant offset (the 4 blocks of a lane group broadcast).
+// Inside a tile the element (hi, lo) sits at 4 hi + ((lo + Y) & 3): the staging stores
+// (ds_write_b64, 16-lane groups, bank (a/4) mod 32) write 16 consecutive y of one x row,
+// which the plain 4 hi + lo image put on 4 bank pairs (4-way conflicts, ~1 extra LDS
+// cycle per LDS instruction of the kernel); rotated by Y they land on 16 distinct pairs,
+// and each A read still covers 8 distinct doubles per 32-lane group (conflict-free).
 //
 // All classes in one wave: the joint (all states, all classes) exact power-of-two
 // rescale of the other kernels is an in-register max plus two shuffles -- no LDS exchange
@@ -59,7 +64,7 @@ struct JMArgs {
   double* partials; i32* scale; const u8* codes; const double* tipP; const u8* cherry; const double* pmats;
   const double* weights; const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i64 cherry_stride; i64 cherry_table_bytes; i64 cherry_count_bytes;
-  i32 guard; i64 p_base;  // p_base: first pattern of the launch (pattern chunks)
+  i32 guard;
 };
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
@@ -96,7 +101,6 @@ struct JMArgs {
   int64_t cherry_table_bytes;
   int64_t cherry_count_bytes;
   int32_t guard;
-  int64_t p_base;
 };
 
 struct JitMShape {
@@ -106,26 +110,13 @@ struct JitMShape {
   bool scale = false;
   int L = 1;         // operand fetch lookahead (events)
   int minw = 2;      // __launch_bounds__ min waves per SIMD
-  bool direct = false;  // A operands straight from P(t) in L1/L2 (no LDS staging, no barriers)
-  int pd = 1;           // P(t) staging prefetch distance (contractions ahead)
-  bool hoist = false;   // cherry codes of the whole fragment loaded at its start
-  bool youter = false;  // contraction order: independent chains interleaved block by block
-  bool padstage = false; // P staging: padded LDS stride, unconditional stores (cfg3 3.93 vs 3.51 ms: off)
-  int debug = 0;        // timing experiments only (wrong results): bit 1 no P(t) staging barrier, bit 2 no
-                        // P(t) loads, bit 4 one A operand read per class and contraction
-  bool hyb = false;     // 16-state tiles on 16x16x4, the rest on 4x4x4 (CONTRIB, HYB_; 20 and 64
-                        // states; cfg3 4.37 vs 3.56 ms all-4x4x4, so off)
-  bool hybrid() const { return hyb && (S == 20 || S == 64) && !direct; }
-  int G = 4;  // waves (16-pattern groups) per workgroup: 64 patterns (4) or 128 (8)
+  int pd = 1;        // P(t) staging prefetch distance (contractions ahead)
+  int G = 4;         // waves (16-pattern groups) per workgroup: 64 patterns (4) or 128 (8)
   int pb() const { return C * S * S; }  // doubles of P(t) per branch (every class)
-  // LDS stride of a P buffer: every staging element of the workgroup has a slot (the
-  // elements past pb() land in the padding), so the staging stores need no condition
-  int pbs() const { return padstage ? (pb() + 64 * G - 1) / (64 * G) * (64 * G) : pb(); }
-  size_t lds_bytes() const { return (size_t)((direct ? 0 : 2 * pbs()) + 16 * G) * sizeof(double); }
+  size_t lds_bytes() const { return (size_t)(2 * pb() + 16 * G) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
-    return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && direct == o.direct &&
-           pd == o.pd && hoist == o.hoist && youter == o.youter && padstage == o.padstage && hyb == o.hyb &&
-           debug == o.debug && G == o.G;
+    return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && pd == o.pd &&
+           G == o.G;
   }
 };
 
@@ -138,61 +129,26 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   s.reserve(65536 * std::max<size_t>(starts.size(), 1));
   s += kJitMPrelude;
   char buf[512];
-  const int NTH = 64 * sh.G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH, PBS = sh.pbs();
+  const int NTH = 64 * sh.G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH;
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
-           "#define NTH_ %d\n#define PB_ %d\n#define PBS_ %d\n#define PF_ %d\n#define SC_ %s\n#define DIRECT_ %d\n#define YOUTER_ %d\n"
-           "#define HYB_ %d\n#define DBGA_ %d\n",
-           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PBS, PF, sh.scale ? "true" : "false", sh.direct ? 1 : 0,
-           sh.youter ? 1 : 0, sh.hybrid() ? 1 : 0, (sh.debug & 4) ? 1 : 0);
+           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n",
+           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PF, sh.scale ? "true" : "false");
   s += buf;
   s += R"PLKJITM(
 // P(t) of branch b (all classes, [c][x][y]) -> registers -> the LDS tile image
-// [c][X][Y][hi][lo] with tile element (hi, lo) = P[4X + lo][4Y + hi]
+// [c][X][Y][16] with P[4X + lo][4Y + hi] at tile position 4 hi + ((lo + Y) & 3)
 #define PSTAGE_LOAD(R, b) { const double* s_ = a.pmats + (i64)(b) * PB_; \
   _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) { const int e_ = tid + j_ * NTH_; R[j_] = s_[e_ < PB_ ? e_ : PB_ - 1]; } }
-#define PSTAGE_STORE(R, bf) { double* d_ = lds + (bf) * PBS_; \
-  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) if (PBS_ > PB_ || sidx[j_] >= 0) d_[sidx[j_]] = R[j_]; }
-// D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1)
-// (YOUTER_: the C * XB independent chains advance one block at a time, so consecutive MFMAs
-// never depend on each other; the same sums in the same order either way)
-// HYB_: the output's 16-state tiles on v_mfma_f64_16x16x4 (A = the 16 x 4 tile
-// P[16 t + i][4Y + k], lane l holding i = l % 16, k = l / 16: 64 distinct values per 2048
-// flops) and the remaining S % 16 states (20 states: 16..19) on v_mfma_f64_4x4x4_4b -- 4x
-// fewer A operands per flop than all-4x4x4.  The 16x16 D registers q = 0..3 of tile t hold
-// states 16 t + 4q + hi, exactly the layout of blocks X = 4t + q, and the 4x4x4 D the
-// layout of the last block.  Image per class: NT16_ * XB_ tiles of 64, then XB_ of 16.
-#define NT16_ (S_ / 16)
-#define R4_ ((S_ % 16) / 4)
-#define CONTRIB(D, SRC, bf, SET) { const double* P_ = PA + (bf) * PBS_; \
-  if (HYB_) { const double* Q_ = PA16 + (bf) * PBS_; f64x4 h_[C_][NT16_]; double l_[C_]; \
-    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { l_[c_] = 0.0; \
-      _Pragma("unroll") for (int t_ = 0; t_ < NT16_; ++t_) h_[c_][t_] = (f64x4){0.0, 0.0, 0.0, 0.0}; } \
-    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { \
-      _Pragma("unroll") for (int t_ = 0; t_ < NT16_; ++t_) \
-        h_[c_][t_] = mfma16(Q_[c_ * (S_ * S_) + (t_ * XB_ + Y_) * 64], SRC[c_][Y_], h_[c_][t_]); \
-      if (R4_) l_[c_] = mfma4(P_[c_ * (S_ * S_) + NT16_ * XB_ * 64 + Y_ * 16], SRC[c_][Y_], l_[c_]); } \
-    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { \
-      _Pragma("unroll") for (int t_ = 0; t_ < NT16_; ++t_) _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) { \
-        if (SET) D[c_][4 * t_ + q_] = h_[c_][t_][q_]; else D[c_][4 * t_ + q_] *= h_[c_][t_][q_]; } \
-      if (R4_) { if (SET) D[c_][4 * NT16_] = l_[c_]; else D[c_][4 * NT16_] *= l_[c_]; } } \
-  } else if (YOUTER_) { double d_[C_][XB_]; \
-    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) \
-      _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
-        d_[c_][X_] = mfma4(P_[((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], Y_ == 0 ? 0.0 : d_[c_][X_]); \
-    _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
-      if (SET) D[c_][X_] = d_[c_][X_]; else D[c_][X_] *= d_[c_][X_]; } \
-  } else { \
+#define PSTAGE_STORE(R, bf) { double* d_ = lds + (bf) * PB_; \
+  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) if (sidx[j_] >= 0) d_[sidx[j_]] = R[j_]; }
+// D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1); the A read of tile (c, X, Y)
+// goes through the lane base of rotation Y & 3
+#define CONTRIB(D, SRC, bf, SET) { \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
     double d_ = 0.0; \
     _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) \
-      d_ = mfma4(P_[DBGA_ ? c_ * (XB_ * XB_ * 16) : ((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
-    if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } } }
-// direct: A(c, X, Y) = P[c][4X + lo][4Y + hi] read from the branch's P(t) in global memory
-#define CONTRIB_G(D, SRC, b, SET) { const double* P_ = PG + (i64)(b) * PB_; \
-  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
-    double d_ = 0.0; \
-    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) d_ = mfma4(P_[(c_ * S_ + 4 * X_) * S_ + 4 * Y_], SRC[c_][Y_], d_); \
+      d_ = mfma4(PA[Y_ & 3][(bf) * PB_ + ((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
     if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } }
 #define ROWMUL(D, F, SET) { _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") \
   for (int X_ = 0; X_ < XB_; ++X_) { if (SET) D[c_][X_] = F[c_][X_]; else D[c_][X_] *= F[c_][X_]; } }
@@ -203,14 +159,6 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
     F[c_][X_] = r_[(i64)c_ * (U2_ * S_) + 4 * X_]; \
   if (SC_) FK = (int)base_[a.cherry_table_bytes + code_]; }
-// the same with the combined code already in a register (hoisted to the fragment start)
-#define CHERRY_CODE(CC, k) const int CC = reinterpret_cast<const u16*>(a.cherry + (i64)(k) * a.cherry_stride + \
-  a.cherry_table_bytes + a.cherry_count_bytes)[p];
-#define CHERRY_FETCH_C(F, FK, k, CC) { const u8* base_ = a.cherry + (i64)(k) * a.cherry_stride; \
-  const double* r_ = reinterpret_cast<const double*>(base_) + (i64)(CC) * S_ + hi; \
-  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
-    F[c_][X_] = r_[(i64)c_ * (U2_ * S_) + 4 * X_]; \
-  if (SC_) FK = (int)base_[a.cherry_table_bytes + (CC)]; }
 #define TIP_FETCH(F, t) { const int code_ = a.codes[(i64)(t) * a.n_pad + p]; \
   const double* r_ = a.tipP + ((i64)(t) * (C_ * U_) + code_) * S_ + hi; \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
@@ -261,28 +209,26 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
            "extern \"C\" __global__ __launch_bounds__(%d, %d) void plk_jit_treeM(JMArgs a, int frag_base) {\n", NTH,
            std::max(sh.minw, 1));
   s += buf;
-  s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PBS_] P tiles | red[16 G_]
-  double* red = lds + (DIRECT_ ? 0 : 2 * PBS_);
+  s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PB_] P tiles | red[16 G_]
+  double* red = lds + 2 * PB_;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 4, pl = lane & 15;
-  const i64 p0 = a.p_base + (i64)blockIdx.x * (16 * G_);
+  const i64 p0 = (i64)blockIdx.x * (16 * G_);
   const i64 p = p0 + 16 * w + pl;
   const i64 toff = (p >> 7) * (i64)(C_ * S_ * kTile) + (p & (kTile - 1)) + (i64)hi * kTile;
-  const double* PA = lds + ((hi << 2) | (lane & 3));
-  const double* PA16 = lds + lane;  // HYB_: 16x16x4 A tiles, one element per lane
-  const double* PG = a.pmats + (lane & 3) * S_ + hi;   // direct A operands: P[..][4X + lo][4Y + hi]
-  int sidx[PF_];   // this thread's staging elements -> tile slots (past the table: padding)
+  // A-operand lane bases, one per tile rotation Y & 3 (lane 16 hi + 4 b + lo reads tile
+  // element (hi, lo))
+  const double* PA[4];
+  _Pragma("unroll") for (int k = 0; k < 4; ++k) PA[k] = lds + ((hi << 2) | (((lane & 3) + k) & 3));
+  int sidx[PF_];   // this thread's staging elements -> tile slots (-1: past the table)
   _Pragma("unroll") for (int j = 0; j < PF_; ++j) {
     const int e = tid + j * NTH_;
     const int c = e / (S_ * S_), r = e - c * (S_ * S_), x = r / S_, y = r - x * S_;
-    const int t_ = HYB_ ? c * (S_ * S_) + (x < 16 * NT16_ ? ((x >> 4) * XB_ + (y >> 2)) * 64 + (y & 3) * 16 + (x & 15)
-                                                        : NT16_ * XB_ * 64 + (y >> 2) * 16 + (y & 3) * 4 + (x - 16 * NT16_))
-                        : ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (x & 3);
-    sidx[j] = e < PB_ ? t_ : PBS_ > PB_ ? e : -1;
+    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (((x & 3) + (y >> 2)) & 3) : -1;
   }
   double R0[PF_] = {}, R1[PF_] = {}, R2[PF_] = {};
-  (void)red; (void)PA; (void)PA16; (void)PG; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
+  (void)red; (void)PA; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
   const int frag = frag_base + (int)blockIdx.y;
 )PLKJITM";
   // accumulators per register level and the operand ring
@@ -322,9 +268,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     auto emit_fetch = [&](int i) {
       const TInstr& e = ev[(size_t)i];
       const int sl = slot[(size_t)i];
-      if (e.op == T_CHERRY && sh.hoist)
-        snprintf(buf, sizeof(buf), "    CHERRY_FETCH_C(F%d, FK%d, %d, CC%d)\n", sl, sl, e.a, e.a);
-      else if (e.op == T_CHERRY)
+      if (e.op == T_CHERRY)
         snprintf(buf, sizeof(buf), "    CHERRY_FETCH(F%d, FK%d, %d)\n", sl, sl, e.a);
       else if (e.op == T_TIP)
         snprintf(buf, sizeof(buf), "    TIP_FETCH(F%d, %d)\n", sl, e.a);
@@ -334,23 +278,16 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     };
     snprintf(buf, sizeof(buf), "  case %zu: {\n", f);
     s += buf;
-    if (sh.hoist)
-      for (const TInstr& e : ev)
-        if (e.op == T_CHERRY) {
-          snprintf(buf, sizeof(buf), "    CHERRY_CODE(CC%d, %d)\n", e.a, e.a);
-          s += buf;
-        }
     size_t nf = 0;
     for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
     int cur = 0;
     size_t np = 0;  // P-chain events consumed
-    if (sh.direct) pchain.clear();  // no staging chain: every contraction reads P(t) directly
     const int PD = std::min(std::max(sh.pd, 1), 3);
     // chain event j is staged from register set j % PD: loaded PD contractions ahead, stored
     // to the other LDS buffer (and a barrier) at the end of the contraction before its own
-    const char* bar = (sh.debug & 1) ? "" : " __syncthreads();";
+    const char* bar = " __syncthreads();";
     auto pload = [&](size_t j) {
-      if (j < pchain.size() && !(sh.debug & 2)) {
+      if (j < pchain.size()) {
         snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R%zu, %d)\n", j % (size_t)PD, ev[(size_t)pchain[j]].b);
         s += buf;
       }
@@ -379,14 +316,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
       if (e.op == T_CHERRY || e.op == T_TIP || e.op == T_LOAD) {
         if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
         const int sl = slot[i];
-        if (e.op == T_LOAD && sh.direct) {
-          snprintf(buf, sizeof(buf), "    CONTRIB_G(A%d, F%d, %d, %s)\n", d, sl, e.b, fresh[(size_t)d] ? "true" : "false");
-          s += buf;
-          if (sh.scale) {
-            snprintf(buf, sizeof(buf), "    K%d += FK%d;\n", d, sl);
-            s += buf;
-          }
-        } else if (e.op == T_LOAD) {
+        if (e.op == T_LOAD) {
           snprintf(buf, sizeof(buf), "    CONTRIB(A%d, F%d, %d, %s)\n", d, sl, cur, fresh[(size_t)d] ? "true" : "false");
           s += buf;
           pnext();
@@ -419,12 +349,9 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
           snprintf(buf, sizeof(buf), "    STORE(A%d, K%d, %d)\n", d, d, e.a);
           s += buf;
         }
-        if (sh.direct)
-          snprintf(buf, sizeof(buf), "    CONTRIB_G(A%d, A%d, %d, %s)\n", d - 1, d, e.b, fresh[(size_t)d - 1] ? "true" : "false");
-        else
-          snprintf(buf, sizeof(buf), "    CONTRIB(A%d, A%d, %d, %s)\n", d - 1, d, cur, fresh[(size_t)d - 1] ? "true" : "false");
+        snprintf(buf, sizeof(buf), "    CONTRIB(A%d, A%d, %d, %s)\n", d - 1, d, cur, fresh[(size_t)d - 1] ? "true" : "false");
         s += buf;
-        if (!sh.direct) pnext();
+        pnext();
         if (sh.scale) {
           snprintf(buf, sizeof(buf), "    K%d += K%d;\n", d - 1, d);
           s += buf;

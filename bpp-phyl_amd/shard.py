@@ -26,6 +26,19 @@ def shard_range(rank: int, world: int, n_patterns: int, align: int = BLOCK) -> T
     return min(b0 * align, n_patterns), min(b1 * align, n_patterns)
 
 
+def bench_range(scaling: str, rank: int, world: int, patterns: int) -> Tuple[int, int, int]:
+    """bench.py's pattern range of a rank and the job's total: weak = `patterns` per rank
+    (rank r holds [r * patterns, (r + 1) * patterns) of one global alignment, so per-GPU work
+    is fixed as N grows); strong = `patterns` in total, split into contiguous block-aligned
+    ranges by shard_range (the lnL is then bitwise the same for every N)."""
+    if scaling == "weak":
+        return rank * patterns, (rank + 1) * patterns, patterns * world
+    if scaling == "strong":
+        a, b = shard_range(rank, world, patterns)
+        return a, b, patterns
+    raise ValueError(scaling)
+
+
 def fixed_order_sum(blocks: np.ndarray) -> float:
     """Sequential left-to-right sum (np.add.accumulate is strictly sequential, unlike
     np.sum's pairwise summation), i.e. the same order plk_root_loglik uses."""

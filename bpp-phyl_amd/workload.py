@@ -110,8 +110,10 @@ CONFIGS = {
     "lg08_g4_protein_200k_256": dict(model="LG08", alpha=0.5, C=4, n_taxa=256, n_patterns=200_000, scaling=True, cpu_sample=8_000),
     # config 4: "Codon YN98, 61 states, 50k patterns, 128 taxa" (64 stored states, 3 null stops)
     "yn98_codon_50k_128": dict(model="YN98", alpha=None, C=1, n_taxa=128, n_patterns=50_000, scaling=False, cpu_sample=2_000),
-    # config 5: per-branch GTR, 512 taxa, rooted; 2M patterns = 250k per GPU x 8 (weak-scaled per GPU)
-    "nh_gtr_g4_dna_2M_512": dict(model="NHGTR", alpha=1.0, C=4, n_taxa=512, n_patterns=250_000, scaling=True, cpu_sample=10_000),
+    # config 5: per-branch GTR, 512 taxa, rooted; 2M patterns = 250k per GPU x 8 (weak-scaled per GPU;
+    # bench.py --scaling strong keeps the 2M (global_patterns) fixed and splits it over the ranks)
+    "nh_gtr_g4_dna_2M_512": dict(model="NHGTR", alpha=1.0, C=4, n_taxa=512, n_patterns=250_000, scaling=True, cpu_sample=10_000,
+                                 global_patterns=2_000_000),
 }
 
 

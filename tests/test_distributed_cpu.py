@@ -66,12 +66,13 @@ def _oracle_sites(config, start, end):
     return site
 
 
-def _bench_worker(rank, world, port, config, n, q):
-    """bench.py's N > 1 exchange: each rank holds its shard's block sums, BlockExchange
-    (sized once at setup) all-gathers them and sums in global block order."""
+def _bench_worker(rank, world, port, config, n, q, scaling="strong"):
+    """bench.py's N > 1 exchange: each rank holds its shard's block sums (its range from
+    shard.bench_range, as bench.py computes it), BlockExchange (sized once at setup)
+    all-gathers them and sums in global block order."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    a, b = shard.shard_range(rank, world, n)
+    a, b, _ = shard.bench_range(scaling, rank, world, n)
     site = _oracle_sites(config, a, b)
     blocks = _block_sums(np.concatenate([np.zeros(a), site]), a, b)   # block sums of [a, b)
     x = shard.BlockExchange(dist, len(blocks), device="cpu")
@@ -81,21 +82,39 @@ def _bench_worker(rank, world, port, config, n, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("config,world,n", [("gtr_g4_dna_1M_64", 2, 3 * 4096 + 300),
-                                            ("nh_gtr_g4_dna_2M_512", 3, 2 * 4096 + 5),
-                                            ("gtr_g4_dna_1M_64", 3, 900)])
-def test_block_exchange_bitwise_vs_one_process(config, world, n):
+@pytest.mark.parametrize("config,world,n,scaling", [("gtr_g4_dna_1M_64", 2, 3 * 4096 + 300, "strong"),
+                                                    ("nh_gtr_g4_dna_2M_512", 3, 2 * 4096 + 5, "strong"),
+                                                    ("nh_gtr_g4_dna_2M_512", 2, 5 * 4096, "strong"),
+                                                    ("gtr_g4_dna_1M_64", 3, 900, "strong"),
+                                                    ("gtr_g4_dna_1M_64", 2, 2 * 4096, "weak")])
+def test_block_exchange_bitwise_vs_one_process(config, world, n, scaling):
+    """bench.py's N > 1 path in both scaling modes: strong (config 5's global pattern count
+    split over the ranks; the lnL is bitwise the one-process total) and weak (each rank its
+    own block-aligned slice; the total is that of the union)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, config, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, config, n, q, scaling)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=300) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
-    whole = shard.fixed_order_sum(_block_sums(_oracle_sites(config, 0, n), 0, n))
+    total = shard.bench_range(scaling, 0, world, n)[2]
+    whole = shard.fixed_order_sum(_block_sums(_oracle_sites(config, 0, total), 0, total))
     assert all(r[1] == whole and r[2] == whole for r in res), (res, whole)
+
+
+def test_bench_range_modes():
+    """Strong: contiguous block-aligned ranges tiling the job's patterns (config 5: 2M over
+    1/2/4/8 ranks); weak: one slice per rank."""
+    for world in (1, 2, 3, 4, 8):
+        rs = [shard.bench_range("strong", r, world, 2_000_000) for r in range(world)]
+        assert rs[0][0] == 0 and rs[-1][1] == 2_000_000 and all(r[2] == 2_000_000 for r in rs)
+        assert all(a[1] == b[0] and b[0] % shard.BLOCK == 0 for a, b in zip(rs, rs[1:]))
+        assert max(r[1] - r[0] for r in rs) - min(r[1] - r[0] for r in rs) <= 2 * shard.BLOCK
+        ws = [shard.bench_range("weak", r, world, 1_000_000) for r in range(world)]
+        assert ws[-1] == ((world - 1) * 1_000_000, world * 1_000_000, world * 1_000_000)
 
 
 @pytest.mark.parametrize("world,n", [(2, 3 * 4096 + 17), (2, 100), (3, 10 * 4096)])

@@ -1099,13 +1099,12 @@ def test_jit_treeM_vs_oracle(C, tree_kind, n_patterns, scaling, mode, variant, m
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dm,L,direct,pd,hoist,g", [(2, 1, "0", 1, 0, 4), (3, 2, "0", 2, 1, 4), (4, 1, "1", 1, 0, 4),
-                                                    (3, 1, "1", 1, 1, 4), (4, 1, "0", 3, 0, 4), (4, 1, "0", 1, 0, 8),
-                                                    (3, 2, "0", 2, 0, 8)])
-def test_jit_treeM_register_depths(dm, L, direct, pd, hoist, g, monkeypatch):
-    """Other fragment heights, fetch lookaheads, A-operand sources (LDS-staged / direct
-    from L1-L2) and workgroup sizes (PLK_JITM_G) give the default kernel's results bitwise
-    (different cuts store different partials, but every operation per node is the same)."""
+@pytest.mark.parametrize("dm,L,pd,g", [(2, 1, 1, 4), (3, 2, 2, 4), (4, 1, 1, 4), (4, 1, 3, 4), (4, 1, 1, 8),
+                                       (3, 2, 2, 8)])
+def test_jit_treeM_register_depths(dm, L, pd, g, monkeypatch):
+    """Other fragment heights, fetch lookaheads, P(t) staging distances and workgroup sizes
+    (PLK_JITM_G) give the default kernel's results bitwise (different cuts store different
+    partials, but every operation per node is the same)."""
     et, m, alph, rates, probs, states = _random_problem(20, 4, 80, 600, seed=77, amb=True)
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
@@ -1113,41 +1112,12 @@ def test_jit_treeM_register_depths(dm, L, direct, pd, hoist, g, monkeypatch):
     del eng
     monkeypatch.setenv("PLK_JITM_DM", str(dm))
     monkeypatch.setenv("PLK_JITM_L", str(L))
-    monkeypatch.setenv("PLK_JITM_DIRECT", direct)
     monkeypatch.setenv("PLK_JITM_PD", str(pd))
-    monkeypatch.setenv("PLK_JITM_HOIST", str(hoist))
     monkeypatch.setenv("PLK_JITM_G", str(g))
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
     l1, s1, _ = run_engine(eng, et)
     assert eng.kernel_path() == "jit_treeM"
     assert np.array_equal(s0, s1) and l0 == l1
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("chunks", ["2", "3", "5"])
-def test_jit_treeM_chunked_tiers_bitwise(chunks, monkeypatch):
-    """Two-tier jit_treeM launched in pattern chunks pipelined over two streams
-    (PLK_JITM_CHUNKS) gives the one-launch-per-tier results bitwise: lnL, per-pattern lnL
-    and block sums, on a ragged pattern count, twice in a row (the second stream's work is
-    ordered before the next evaluation)."""
-    n = 3 * 4096 + 1000
-    et, m, alph, rates, probs, states = _random_problem(20, 4, 256, n, seed=31, amb=True)
-    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
-    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
-    ops = phylo.split_ops(et.ops)
-    out = {}
-    for k in ("1", chunks):
-        monkeypatch.setenv("PLK_JITM_CHUNKS", k)
-        eng = engine_for(et, 20, 4, n, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
-        res = [eng.evaluate(br, et.brlen[br] * s, ops, et.root) for s in (1.0, 1.3)]
-        _, site, _ = eng.root_loglik(et.root, want_sites=True)
-        assert eng.kernel_path() == "jit_treeM"
-        out[k] = (res, site)
-        del eng
-    (r0, s0), (r1, s1) = out["1"], out[chunks]
-    for (l0, b0), (l1, b1) in zip(r0, r1):
-        assert l0 == l1 and np.array_equal(b0, b1)
-    assert np.array_equal(s0, s1)
 
 
 @pytest.mark.gpu

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-3 A/B runs: bench lines of one config under environment variants.
-#   tools/ab_r03.sh <tag> <config> <name>:<ENV=VAL,ENV=VAL> ...
+# A/B runs: bench lines of one config under environment variants.
+#   tools/ab_bench.sh <tag> <config> <name>:<ENV=VAL,ENV=VAL> ...
 # Each variant: gpurun_out/<tag>/<name>.json (bench line, no CPU baseline); summary printed.
 set -o pipefail
 T=$1; CFG=$2; shift 2
