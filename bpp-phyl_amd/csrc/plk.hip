@@ -9,7 +9,6 @@
 #include "plk_tree4.hpp"
 #include "plk_deriv.hpp"
 #include "plk_mfma64.hpp"
-#include "plk_treeS.hpp"
 #include "plk_treeM.hpp"
 #include "plk_jit.hpp"
 #include "plk_jitm.hpp"
@@ -39,15 +38,18 @@ using namespace plk;
 extern char** environ;
 
 namespace {
-// Environment switches (A/B and debug) are read on every call of the hot
-// path; a getenv walks the whole environment (~100 entries on the GPU box), and a
-// traversal reads dozens of switches (~4 us of host time per evaluation).  Reads go
-// through a per-thread cache keyed by the switch name's address (names are literals of
+// Environment.  The library reads a handful of variables: the JIT
+// cache and its diagnostics (PLK_JIT_CACHE, PLK_JIT_LOG, PLK_JIT_DUMP), one test hook
+// (PLK_TEST_COMM_FAIL) and PLK_TUNE, the engine's tuning knobs as "KEY=value,KEY=value"
+// (kernel shapes and the A/B kernel choices, each covered by a bitwise or oracle test).
+// Reads go through a per-thread cache keyed by the name's address (names are literals of
 // this file), dropped whenever the environment changed: every API entry fingerprints the
 // `environ` array (its entries' addresses -- setenv / putenv / unsetenv change them).
 struct EnvCache {
   uint64_t fp = 0;
   std::vector<std::pair<const char*, const char*> > kv;
+  std::vector<std::pair<std::string, std::string> > tune;  // parsed PLK_TUNE
+  std::vector<std::pair<const char*, const char*> > tkv;   // key address -> value (or null)
 };
 thread_local EnvCache g_env;
 
@@ -57,6 +59,20 @@ void env_refresh() {
   if (x != g_env.fp) {
     g_env.fp = x;
     g_env.kv.clear();
+    g_env.tkv.clear();
+    g_env.tune.clear();
+    if (const char* t = std::getenv("PLK_TUNE")) {
+      std::string all(t);
+      size_t i = 0;
+      while (i < all.size()) {
+        size_t j = all.find(',', i);
+        if (j == std::string::npos) j = all.size();
+        const std::string item = all.substr(i, j - i);
+        const size_t eq = item.find('=');
+        if (eq != std::string::npos && eq > 0) g_env.tune.emplace_back(item.substr(0, eq), item.substr(eq + 1));
+        i = j + 1;
+      }
+    }
   }
 }
 
@@ -70,6 +86,22 @@ const char* env_get(const char* name) {
 
 bool env_is(const char* name, char v) {
   const char* e = env_get(name);
+  return e && e[0] == v;
+}
+
+// A tuning knob of PLK_TUNE (null when not given).
+const char* tune_get(const char* key) {
+  for (const auto& p : g_env.tkv)
+    if (p.first == key) return p.second;
+  const char* v = nullptr;
+  for (const auto& kv : g_env.tune)
+    if (kv.first == key) v = kv.second.c_str();
+  g_env.tkv.emplace_back(key, v);
+  return v;
+}
+
+bool tune_is(const char* key, char v) {
+  const char* e = tune_get(key);
   return e && e[0] == v;
 }
 
@@ -120,8 +152,6 @@ struct plk_handle_s {
   // small staging buffers for op lists / pmatrix requests
   KOp* d_ops = nullptr;
   size_t d_ops_cap = 0;
-  void* d_req = nullptr;
-  size_t d_req_cap = 0;
   // pinned host staging: P(t) requests (reused once req_done has passed) and block sums
   char* h_req = nullptr;
   char* h_req_dev = nullptr;   // device address of the mapped staging (PLK_PMAT_MAPPED)
@@ -154,7 +184,6 @@ struct plk_handle_s {
   std::vector<int> last_level_start;
   // fused 4-state traversal (plk_tree4.hpp)
   double* wave_sums = nullptr;
-  bool blocks_fused = false;              // the last traversal already formed block_sums
   TInstr* d_prog = nullptr;
   size_t d_prog_cap = 0;
   int32_t* d_frag = nullptr;
@@ -244,7 +273,6 @@ struct plk_handle_s {
   int comm_ranks = 0, comm_rank = 0;
   int64_t comm_cmax = 0;                  // block sums per rank in the all-gather (max over ranks)
   double* d_blk_local = nullptr;          // [comm_cmax] this rank's block sums (zero padded)
-  unsigned* d_blk_cnt = nullptr;          // [n_blocks] arrival counters of the in-kernel block sums
   DrPreOp* d_drpre = nullptr;             // fused DR preorder ops (dr_pre_s4_kernel)
   size_t d_drpre_cap = 0;
   double* d_blk_all = nullptr;            // [comm_ranks][comm_cmax]
@@ -297,16 +325,9 @@ int ensure_cap(plk_handle h, void** p, size_t* cap, size_t bytes) {
   return PLK_OK;
 }
 
-// Completion wait of an evaluation.  PLK_SPIN=1 polls hipStreamQuery instead of
-// hipStreamSynchronize (A/B of the host wake-up latency).
+// Completion wait of an evaluation (spin-waiting on hipStreamQuery was measured slower: it
+// contends with the launch calls).
 int stream_wait(plk_handle h) {
-  if (env_is("PLK_SPIN", '1')) {
-    hipError_t e;
-    while ((e = hipStreamQuery(h->stream)) == hipErrorNotReady) {
-    }
-    if (e != hipSuccess) return fail(h, PLK_ERR_DEVICE, "hipStreamQuery: %s", hipGetErrorString(e));
-    return PLK_OK;
-  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PLK_OK;
 }
@@ -398,6 +419,15 @@ uint64_t fnv1a64(const std::string& s) {
   return x;
 }
 
+// "<size> <fnv1a64>" of a code object (the .sum file of a disk-cache entry)
+std::string code_sum(const std::vector<char>& code) {
+  uint64_t x = 1469598103934665603ull;
+  for (char c : code) x = (x ^ (unsigned char)c) * 1099511628211ull;
+  char b[64];
+  snprintf(b, sizeof(b), "%zu %016llx", code.size(), (unsigned long long)x);
+  return b;
+}
+
 // Code object of `src`: from the disk cache unless `bypass_cache`, else compiled with hiprtc
 // (and stored); *from_cache tells which.
 int jit_compile(plk_handle h, const std::string& src, std::vector<char>* code, bool bypass_cache, bool* from_cache) {
@@ -412,9 +442,13 @@ int jit_compile(plk_handle h, const std::string& src, std::vector<char>* code, b
     snprintf(hx, sizeof(hx), "%016llx",
              (unsigned long long)fnv1a64(src + opts[0] + opts[1] + std::to_string(maj) + "." + std::to_string(mnr)));
     stem = dir + "/" + hx;
-    std::vector<char> stored;
+    std::vector<char> stored, sum;
+    // an entry is used only if its stored source equals the generated one and the code
+    // object's size and hash equal the ones recorded after it was written (a truncated or
+    // damaged object is never handed to hipModuleLoadData, whose ELF reader can abort)
     if (!bypass_cache && read_file(stem + ".hip", &stored) && stored.size() == src.size() &&
-        std::memcmp(stored.data(), src.data(), src.size()) == 0 && read_file(stem + ".co", code)) {
+        std::memcmp(stored.data(), src.data(), src.size()) == 0 && read_file(stem + ".co", code) &&
+        read_file(stem + ".sum", &sum) && std::string(sum.begin(), sum.end()) == code_sum(*code)) {
       if (log) std::fprintf(stderr, "[plk] jit cache hit %s.co\n", stem.c_str());
       *from_cache = true;
       return PLK_OK;
@@ -443,7 +477,9 @@ int jit_compile(plk_handle h, const std::string& src, std::vector<char>* code, b
                  std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   if (!stem.empty()) {
     write_file_atomic(stem + ".co", code->data(), code->size());
-    write_file_atomic(stem + ".hip", src.data(), src.size());  // last: it validates the .co
+    const std::string sm = code_sum(*code);
+    write_file_atomic(stem + ".sum", sm.data(), sm.size());
+    write_file_atomic(stem + ".hip", src.data(), src.size());  // last: it validates the entry
   }
   return PLK_OK;
 }
@@ -479,12 +515,19 @@ int jit_function(plk_handle h, const std::string& src, const char* name, hipFunc
   }
   hipSetDevice(h->device);
   hipModule_t mod;
-  if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+  auto load = [&]() {
+    try {
+      return hipModuleLoadData(&mod, code.data()) == hipSuccess;
+    } catch (...) {
+      return false;
+    }
+  };
+  if (!load()) {
     if (!from_cache) return fail(h, PLK_ERR_DEVICE, "hipModuleLoadData of the compiled tree kernel failed");
     // a damaged disk-cache entry: recompile and overwrite it
     (void)hipGetLastError();
     if (int rc = jit_compile(h, src, &code, true, &from_cache)) return rc;
-    HIPCHK(h, hipModuleLoadData(&mod, code.data()));
+    if (!load()) return fail(h, PLK_ERR_DEVICE, "hipModuleLoadData of the recompiled tree kernel failed");
   }
   hipFunction_t fn;
   HIPCHK(h, hipModuleGetFunction(&fn, mod, name));
@@ -547,7 +590,7 @@ int ensure_pmatsT(plk_handle h) {
 
 int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
   const int S = h->S;
-  if (S == 64 && !env_get("PLK_GENERIC64")) {
+  if (S == 64 && !tune_get("GENERIC64")) {
     // K3: fp64 MFMA, P^T staged in LDS
     int rc = ensure_pmatsT(h);
     if (rc) return rc;
@@ -559,7 +602,7 @@ int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs
       partials_mfma64_kernel<false><<<grid, block, lds, h->stream>>>(d_ops, a, h->pmatsT, h->C);
     return PLK_OK;
   }
-  if (S == 20 && !env_get("PLK_GENERIC20")) {
+  if (S == 20 && !tune_get("GENERIC20")) {
     // K2: P rows through scalar loads, tip tables in LDS
     const size_t lds = 3 * (size_t)h->C * h->n_codes * S * sizeof(double);
     if (lds <= 160 * 1024) {
@@ -593,7 +636,7 @@ int refresh_tip_tables(plk_handle h) {
     if (!h->pmat_valid[t]) return fail(h, PLK_ERR_STATE, "transition matrix of tip branch %d not set", t);
   if (h->n_tips > 0) {
     dim3 grid(h->n_tips, h->C);
-    if (h->S == 64 && !env_is("PLK_PMAT64", '0'))
+    if (h->S == 64 && !tune_is("PMAT64", '0'))
       tip_table64_kernel<<<grid, 256, (size_t)(64 * 64 + h->n_codes * 64) * sizeof(double), h->stream>>>(
           h->pmats, h->code_table, h->tipP, h->n_tips, h->C, h->n_codes);
     else
@@ -872,10 +915,6 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
       hipHostGetDevicePointer((void**)&h->block_sums, h->h_blocks, 0) != hipSuccess)
     return bail(fail(h, PLK_ERR_OOM, "pinned block-sum buffer"));
   if ((rc = dalloc(h, (void**)&h->wave_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return bail(rc);
-  // per-block arrival counters of the in-kernel block sums (the last arriver resets its own)
-  if ((rc = dalloc(h, (void**)&h->d_blk_cnt, (size_t)h->n_blocks * sizeof(unsigned)))) return bail(rc);
-  if (hipMemset(h->d_blk_cnt, 0, (size_t)h->n_blocks * sizeof(unsigned)) != hipSuccess)
-    return bail(fail(nullptr, PLK_ERR_DEVICE, "block counter memset failed"));
   h->materialized.assign(n_internal, 0);
   // default weights 1 for real patterns, 0 for padding
   std::vector<double> w(h->n_pad, 0.0);
@@ -904,9 +943,9 @@ int plk_destroy(plk_handle h) {
   comm_release(h);
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
-                  h->d_ops, h->d_req, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
+                  h->d_ops, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
-                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_blk_cnt, h->d_drpre};
+                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) hipHostFree(h->h_req);
@@ -1145,7 +1184,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   PmatInline inl;
   inl.n = 0;
   const size_t off_t = 0, off_b = (size_t)n * sizeof(double), off_m = off_b + (size_t)n * sizeof(int32_t);
-  const char* staged_env = env_get("PLK_PMAT_STAGED");
+  const char* staged_env = tune_get("PMAT_STAGED");
   if (n <= kPmatInline && !(staged_env && staged_env[0] == '1')) {
     inl.n = n;
     for (int i = 0; i < n; ++i) {
@@ -1156,17 +1195,11 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   }
   // larger requests: pinned staging that the kernel reads through its mapped address over
   // PCIe (cfg5, 1 022 branches: 8.6 us less per evaluation than a stream-ordered copy into
-  // device memory -- the copy's launch and host API time; PLK_PMAT_MAPPED=0 restores the
-  // copy).  The host rewrites the staging only after the previous request's reader
-  // (req_done) finished.
-  const bool mapped = !env_is("PLK_PMAT_MAPPED", '0');
+  // device memory -- the copy's launch and host API time).  The host rewrites the staging
+  // only after the previous request's reader (req_done) finished.
   const char* req = nullptr;
   if (inl.n == 0) {
     const size_t bytes = (size_t)n * (2 * sizeof(int32_t) + sizeof(double)) + 64;
-    if (!mapped) {
-      int rc = ensure_cap(h, &h->d_req, &h->d_req_cap, bytes);
-      if (rc) return rc;
-    }
     if (!h->req_done) HIPCHK(h, hipEventCreateWithFlags(&h->req_done, hipEventDisableTiming));
     HIPCHK(h, hipEventSynchronize(h->req_done));
     if (h->h_req_cap < bytes) {
@@ -1182,13 +1215,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     std::memcpy(staging + off_t, t, n * sizeof(double));
     std::memcpy(staging + off_b, branch, n * sizeof(int32_t));
     if (model) std::memcpy(staging + off_m, model, n * sizeof(int32_t));
-    if (mapped) {
-      req = h->h_req_dev;
-    } else {
-      HIPCHK(h, hipMemcpyAsync(h->d_req, staging, bytes, hipMemcpyHostToDevice, h->stream));
-      HIPCHK(h, hipEventRecord(h->req_done, h->stream));
-      req = (const char*)h->d_req;
-    }
+    req = h->h_req_dev;
   }
   PmatArgs a;
   a.t = inl.n ? nullptr : reinterpret_cast<const double*>(req + off_t);
@@ -1207,7 +1234,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   a.n_req = n;
   // tip tables ride along for S <= 20 (P of the block staged in LDS; S = 64 keeps the
   // separate tip_table_kernel)
-  const bool k64 = h->S == 64 && deriv_mask == PLK_DERIV_P && !env_is("PLK_PMAT64", '0');
+  const bool k64 = h->S == 64 && deriv_mask == PLK_DERIV_P && !tune_is("PMAT64", '0');
   const bool tips_fused = h->table_set && (h->S <= 20 || (k64 && h->n_codes <= 64));
   a.init = tips_fused ? h->code_table : nullptr;
   a.tipP = h->tipP;
@@ -1219,16 +1246,16 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     hipEventRecord(ev.a, h->stream);
   }
   const size_t lds = (size_t)(h->S + (tips_fused ? 2 : 1) * S2) * sizeof(double);
-  if (k64 && !env_is("PLK_PMAT64_SPLIT", '0'))
+  if (k64 && !tune_is("PMAT64_SPLIT", '0'))
     pmat64s_kernel<<<dim3(n, h->C, 4), dim3(256), (size_t)(64 + 16 * 64 + S2) * sizeof(double), h->stream>>>(a, inl);
   else if (k64)
     pmat64_kernel<<<dim3(n, h->C), dim3(256), (size_t)(64 + 2 * S2) * sizeof(double), h->stream>>>(a, inl);
-  else if (h->S == 4 && !env_is("PLK_PMAT4", '0'))
+  else if (h->S == 4 && !tune_is("PMAT4", '0'))
     pmat4_kernel<<<dim3((unsigned)((n * h->C * 4 + 63) / 64)), dim3(64), 0, h->stream>>>(a, inl);
   else
     pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a, inl);
   HIPCHK(h, hipGetLastError());
-  if (inl.n == 0 && mapped) HIPCHK(h, hipEventRecord(h->req_done, h->stream));  // the kernel read the staging
+  if (inl.n == 0) HIPCHK(h, hipEventRecord(h->req_done, h->stream));  // the kernel read the staging
   if (h->timing & PLK_TIME_PMAT) {
     hipEventRecord(ev.b, h->stream);
     h->events.push_back(ev);
@@ -1301,35 +1328,32 @@ constexpr int kTree4Levels(int CW) { return CW >= 4 ? 6 : 8; }
 // wave per rate class, the smallest register footprint and the highest occupancy)
 int tree4_cw(plk_handle h) {
   int cw = 1;
-  if (const char* e = env_get("PLK_TREE4_CW")) cw = std::atoi(e);
+  if (const char* e = tune_get("TREE4_CW")) cw = std::atoi(e);
   if (cw != 1 && cw != 2 && cw != 4) cw = 1;
   return std::min(cw, h->C);
 }
 
-// Fused traversal kernels: 4 states -> tree4_kernel (VALU, P in SGPRs); 20 and 64
-// states -> treeM_kernel (fp64 MFMA, register-chained layouts), or for 20 states the
-// VALU treeS_kernel when PLK_TREES=1.  PLK_FUSED20=0 / PLK_FUSED64=0 keep those state
-// counts on the levelwise kernels (K2 / K3).
-enum FusedKind { FK_NONE = 0, FK_TREE4, FK_TREES, FK_TREEM };
+// Fused traversal kernels: 4 states -> the VALU tree kernels (plk_jit.hpp generated per
+// tree, tree4_kernel interpreting the same program); 20 states -> jit_treeM (plk_jitm.hpp,
+// fp64 MFMA 4x4x4_4b) or the treeM interpreter; 64 states, one class -> treeM (16x16x4).
+enum FusedKind { FK_NONE = 0, FK_TREE4, FK_TREEM };
 
 FusedKind fused_kind(plk_handle h) {
   if (h->flags & PLK_FLAG_LEVELWISE) return FK_NONE;
   // 4 states: the VALU tree kernel (plk_jit.hpp); PLK_S4_JITM=1 runs them on the matrix
   // cores instead (jit_treeM with one 4x4x4 block per class and 16 patterns)
-  if (h->S == 4 && env_is("PLK_S4_JITM", '1') && !env_is("PLK_JITM", '0') && h->C <= kTreeMaxWaves) return FK_TREEM;
+  if (h->S == 4 && tune_is("S4_JITM", '1') && !tune_is("JITM", '0') && h->C <= kTreeMaxWaves) return FK_TREEM;
   if (h->S == 4) return (h->C == 1 || h->C == 2 || h->C == 4) ? FK_TREE4 : FK_NONE;
   if (h->C > kTreeMaxWaves) return FK_NONE;
-  if (h->S == 20 && !env_is("PLK_FUSED20", '0')) return env_is("PLK_TREES", '1') ? FK_TREES : FK_TREEM;
-  if (h->S == 64 && !env_is("PLK_FUSED64", '0') &&
-      (h->C == 1 || (env_is("PLK_JITM64", '1') && !env_is("PLK_JITM", '0'))))
-    return FK_TREEM;  // the treeM interpreter takes one class; jit_treeM any C <= 4
+  if (h->S == 20) return FK_TREEM;
+  if (h->S == 64 && h->C == 1) return FK_TREEM;  // the treeM interpreter takes one class
   return FK_NONE;
 }
 
 bool tree4_supported(plk_handle h) { return fused_kind(h) != FK_NONE; }
 
-int env_int(const char* name, int def, int lo, int hi) {
-  const char* e = env_get(name);
+int tune_int(const char* key, int def, int lo, int hi) {
+  const char* e = tune_get(key);
   if (!e) return def;
   const int v = std::atoi(e);
   return (v >= lo && v <= hi) ? v : def;
@@ -1337,13 +1361,13 @@ int env_int(const char* name, int def, int lo, int hi) {
 
 // 4 states, one class per wave: the tree-specialised kernel (plk_jit.hpp) serves the
 // fused traversal; PLK_JIT=0 keeps the interpreter (tree4_kernel), e.g. for A/B runs.
-bool jit_tree4(plk_handle h) { return fused_kind(h) == FK_TREE4 && tree4_cw(h) == 1 && !env_is("PLK_JIT", '0'); }
+bool jit_tree4(plk_handle h) { return fused_kind(h) == FK_TREE4 && tree4_cw(h) == 1 && !tune_is("JIT", '0'); }
 
 // 20 states: the tree-specialised kernel on v_mfma_f64_4x4x4_4b (plk_jitm.hpp) serves the
 // fused traversal; PLK_JITM=0 keeps the treeM interpreter (16x16x4 MFMA), e.g. for A/B runs.
 bool jit_treeM(plk_handle h) {
-  if (fused_kind(h) != FK_TREEM || env_is("PLK_JITM", '0')) return false;
-  return h->S == 20 || h->S == 4 || (h->S == 64 && env_is("PLK_JITM64", '1'));
+  if (fused_kind(h) != FK_TREEM || tune_is("JITM", '0')) return false;
+  return h->S == 20 || h->S == 4;
 }
 
 // Classes in one wave (plk_jit.hpp, CW = C): the joint rescale needs no cross-wave
@@ -1352,21 +1376,21 @@ bool jit_treeM(plk_handle h) {
 // for scaling runs; PLK_JIT_CIW=0/1 overrides.
 bool jit_ciw(plk_handle h) {
   if (!jit_tree4(h) || h->C == 1) return false;
-  const char* e = env_get("PLK_JIT_CIW");
+  const char* e = tune_get("JIT_CIW");
   if (e) return e[0] == '1';
   return (h->flags & PLK_FLAG_SCALING) != 0;
 }
 
 // tips whose tables (C x codes-in-use x 4 doubles each) fit one fragment's LDS budget
 int jit_tip_cap(plk_handle h) {
-  const int kb = env_int("PLK_JIT_TAB_KB", 48, 4, 120);
+  const int kb = tune_int("JIT_TAB_KB", 48, 4, 120);
   return std::max(2, (kb * 1024) / (h->C * std::max(h->n_codes, 1) * 4 * (int)sizeof(double)));
 }
 
 // treeM programs replace unstored cherries by T_CHERRY rows (PLK_TREEM_CHERRY=0: off);
 // combined codes are 16-bit
 bool treeM_cherries(plk_handle h) {
-  return fused_kind(h) == FK_TREEM && h->n_codes * h->n_codes <= 65535 && !env_is("PLK_TREEM_CHERRY", '0');
+  return fused_kind(h) == FK_TREEM && h->n_codes * h->n_codes <= 65535 && !tune_is("TREEM_CHERRY", '0');
 }
 
 // Cherry contribution tables of the current treeM program (plk_treeM.hpp), rebuilt on
@@ -1399,7 +1423,7 @@ int build_cherry_tables(plk_handle h) {
     h->cherry_codes_valid = true;
   }
   // rows per workgroup: 64-row passes sharing one P^T staging (PLK_CHERRY_ROWS, default 256)
-  const int rows = 64 * std::max(1, env_int("PLK_CHERRY_ROWS", 256, 64, 4096) / 64);
+  const int rows = 64 * std::max(1, tune_int("CHERRY_ROWS", 256, 64, 4096) / 64);
   const dim3 grid((unsigned)((U * U + rows - 1) / rows), (unsigned)(nch * C));
   const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   if (S == 20) {
@@ -1424,14 +1448,13 @@ int tree_levels(plk_handle h) {
     case FK_TREE4:
       if (!jit_tree4(h)) return kTree4Levels(tree4_cw(h));
       // classes in the wave: cfg5 DM 5 / 6 / 7 = 0.70 / 0.55 / 0.84 ms at G = 4
-      return jit_ciw(h) ? env_int("PLK_JIT_CIW_DM", 6, 2, 16) : env_int("PLK_JIT_DM", 10, 2, 32);
-    case FK_TREES: return env_int("PLK_TREES_DM", 2, 2, 4);
+      return jit_ciw(h) ? tune_int("JIT_CIW_DM", 6, 2, 16) : tune_int("JIT_DM", 10, 2, 32);
     // S = 20: 3 levels (with cherry tables 7.8 ms on cfg3, 2 levels 8.7 ms although DM = 3
     // spills a few registers at 128 VGPRs)
     case FK_TREEM:
       if (jit_treeM(h))
-        return h->S == 4 ? env_int("PLK_JITM_DM", 8, 2, 16) : env_int("PLK_JITM_DM", h->S == 64 ? 3 : 4, 2, 6);
-      return h->S == 20 ? env_int("PLK_TREEM_DM", 3, 2, 5) : env_int("PLK_TREEM_DM", 3, 2, 3);
+        return h->S == 4 ? tune_int("JITM_DM", 8, 2, 16) : tune_int("JITM_DM", h->S == 64 ? 3 : 4, 2, 6);
+      return h->S == 20 ? tune_int("TREEM_DM", 3, 2, 5) : tune_int("TREEM_DM", 3, 2, 3);
     default: return 1;
   }
 }
@@ -1476,7 +1499,7 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   // The tree-specialised kernel also bounds the code of a fragment: a workgroup runs
   // one fragment's straight-line code, which must stay within the instruction cache,
   // so a fragment keeps at most EMAX child edges (cutting the largest kept children).
-  const int EMAX = jit_tree4(h) ? env_int("PLK_JIT_EDGES", 160, 8, 1 << 20) : (1 << 30);
+  const int EMAX = jit_tree4(h) ? tune_int("JIT_EDGES", 160, 8, 1 << 20) : (1 << 30);
   // ... and its tips' tables must fit the LDS budget (PLK_JIT_TAB_KB, default 48 KiB)
   const int TMAX = jit_tree4(h) ? jit_tip_cap(h) : (1 << 30);
   // treeM: an unstored cherry (two tip children) is a leaf operand (T_CHERRY)
@@ -1669,31 +1692,13 @@ void launch_tree4_cw(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
     tree4_kernel<CW, DM, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
 }
 
-template <int S, int DM>
-void launch_treeS_dm(plk_handle h, const TreeArgs& a, dim3 grid) {
-  const dim3 block(64 * h->C);
-  if (h->flags & PLK_FLAG_SCALING)
-    treeS_kernel<S, DM, true><<<grid, block, 0, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
-  else
-    treeS_kernel<S, DM, false><<<grid, block, 0, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
-}
-
-template <int S>
-void launch_treeS(plk_handle h, const TreeArgs& a, dim3 grid) {
-  switch (h->prog_dm) {  // the depth the cached program was cut for
-    case 4: launch_treeS_dm<S, 4>(h, a, grid); break;
-    case 3: launch_treeS_dm<S, 3>(h, a, grid); break;
-    default: launch_treeS_dm<S, 2>(h, a, grid); break;
-  }
-}
-
 // treeM tables: staged in LDS behind one barrier per event, or read by every wave straight
 // from L1/L2 (no staging, no barrier).  Measured (profiles/r01/tm1_*): S = 20 (16 waves per
 // workgroup) 7.70 -> 7.48 ms direct; S = 64 (4 waves, 64x64 tables) 0.95 -> 1.35 ms, so
 // direct is the default for 20 states only.  PLK_TREEM_DIRECT=0/1 overrides.
 bool treeM_direct(plk_handle h) {
-  if (env_is("PLK_TREEM_DIRECT", '0')) return false;
-  if (env_is("PLK_TREEM_DIRECT", '1')) return true;
+  if (tune_is("TREEM_DIRECT", '0')) return false;
+  if (tune_is("TREEM_DIRECT", '1')) return true;
   return h->S == 20;
 }
 
@@ -1702,11 +1707,8 @@ bool treeM_direct(plk_handle h) {
 // MFMA chains): cfg3 G = 4 / 2 / 1 = 7.40 / 6.87 / 6.43 ms (profiles/r01/g1_*).
 // PLK_TREEM_G overrides; staged tables and 64 states keep 4.
 int treeM_groups(plk_handle h) {
-  // 64 states: 128-pattern workgroups (8 waves, one per CU) halve the P^T staging traffic
-  // per pattern (PLK_TREEM_G64=8; A/B)
-  if (h->S == 64 && !treeM_direct(h)) return env_int("PLK_TREEM_G64", 4, 4, 8) >= 8 ? 8 : 4;
   if (h->S != 20 || !treeM_direct(h)) return 4;  // staged tables need 64-pattern workgroups
-  const int g = env_int("PLK_TREEM_G", 1, 1, 4);
+  const int g = tune_int("TREEM_G", 1, 1, 4);
   return g == 3 ? 4 : g;
 }
 
@@ -1830,8 +1832,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const size_t lds = (size_t)((h->n_codes * 4 + 1) & ~1) * sizeof(double) + kTreeMaxWaves * 64 * sizeof(double) +
                      (a.stage_codes ? (size_t)h->n_tips * 64 : 0);
   a.n_frags = h->prog_nf;
-  a.bmask = env_is("PLK_DEBUG_SAMEP", '1') ? 0 : -1;
-  a.cherry_pairs = env_is("PLK_TREEM_PAIRS", '0') ? 0 : 1;
+  a.bmask = -1;
+  a.cherry_pairs = tune_is("TREEM_PAIRS", '0') ? 0 : 1;
   a.n_cherry_staged = 0;
   size_t lds_m = 0;
   if (kind == FK_TREEM) {
@@ -1848,20 +1850,11 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     a.stage_codes = (lds_m + (size_t)h->n_tips * 64 <= 76 * 1024) ? 1 : 0;  // two workgroups per CU
     // a program whose tips all sit in cherry tables (balanced trees) has no T_TIP event:
     // staging every tip's codes would only cost each workgroup a load of n_tips x 64 B
-    if (!env_is("PLK_TREEM_STAGE_CODES", '1') &&
+    if (!tune_is("TREEM_STAGE_CODES", '1') &&
         std::none_of(h->prog_host.begin(), h->prog_host.end(), [](const TInstr& w) { return w.op == T_TIP; }))
       a.stage_codes = 0;
     if (treeM_groups(h) == 8) a.stage_codes = 0;  // the staged code rows cover 64 patterns
     if (a.stage_codes) lds_m += (size_t)h->n_tips * 64;
-    // direct tables: the cherries' combined codes of the workgroup staged beside the tip codes
-    // (opt-in PLK_TREEM_CCODES=1: every workgroup stages all cherries but runs one fragment,
-    // cfg3 7.64 -> 7.86 ms)
-    const int nch = (int)h->cherry3.size() / 3;
-    if (treeM_direct(h) && nch > 0 && h->d_cherry && env_is("PLK_TREEM_CCODES", '1') && treeM_groups(h) == 4 &&
-        lds_m + (size_t)nch * 128 <= 76 * 1024) {
-      a.n_cherry_staged = nch;
-      lds_m += (size_t)nch * 128;
-    }
   }
   const int cw = tree4_cw(h);
   // 4 states, one class per wave: the tree-specialised kernel (PLK_JIT=0 keeps the
@@ -1872,12 +1865,12 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   if (jit) {
     sh.C = h->C;
     sh.CW = h->prog_ciw ? h->C : 1;
-    sh.pin = env_int("PLK_JIT_PIN", 1, 0, 1) != 0;  // cfg2 0.244 -> 0.241, cfg5 1.04 -> 0.93 ms
+    sh.pin = tune_int("JIT_PIN", 1, 0, 1) != 0;  // cfg2 0.244 -> 0.241, cfg5 1.04 -> 0.93 ms
     sh.U = h->n_codes;
     sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     // cherries read one product table (plk_jit.hpp: JitUnit) while a fragment's tables stay
     // within PLK_JIT_PAIR_KB (0: no pairs)
-    const int budget = env_int("PLK_JIT_PAIR_KB", 64, 0, 150) * 1024 / (int)sizeof(double);
+    const int budget = tune_int("JIT_PAIR_KB", 64, 0, 150) * 1024 / (int)sizeof(double);
     if (!h->jit_plan_valid || h->jit_plan_U != sh.U || h->jit_plan_budget != budget) {
       h->jit_plan = jit_plan(h->prog_host, h->frag_starts_host, sh.C, sh.U, budget, sh.scale);
       h->jit_plan_valid = true;
@@ -1914,38 +1907,32 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // with the tier's fragments side by side: G = 6 / 7 / 8 = 0.48 / 0.43 / 0.39 ms);
     // otherwise the G with the most resident waves (jit_auto_groups; cfg2 with cherry
     // tables: G = 3, 0.140 ms, G = 2 0.150, G = 4 0.162)
-    sh.G = env_int("PLK_JIT_G", 0, 0, 8);
+    sh.G = tune_int("JIT_G", 0, 0, 8);
     if (sh.G == 0) sh.G = h->prog_ciw ? 8 : sh.scale ? 1 : jit_auto_groups(sh);
     // two patterns per lane halve the P(t) reads per FMA but double the registers:
     // measured slower (cfg2 0.255-0.301 vs 0.241 ms), so opt-in; not with speculation
-    sh.PW = env_int("PLK_JIT_PW", 1, 1, 2);
-    if (sh.G * sh.PW > 4 || h->n_pad % (64 * sh.G * sh.PW) != 0 || env_is("PLK_JIT_SPECULATE", '1')) sh.PW = 1;
+    sh.PW = 1;
     // two-stage pipeline, codes / HBM loads 3 ahead (cfg2 0.274 -> 0.259 ms); with every
     // class in the wave a ring slot is C x larger, so there two events ahead (cfg5 0.385 ms
     // at L = 2, 0.391 at L = 1; 1.48 vs 1.04 ms at L = 3 vs 1 before the P(t) stream)
-    sh.L = env_int("PLK_JIT_L", h->prog_ciw ? 2 : 3, 1, 8);
-    sh.minw = env_int("PLK_JIT_MINW", 0, 0, 8);
-    sh.same_p = env_is("PLK_DEBUG_SAMEP", '1');
-    sh.stage_only = env_int("PLK_DEBUG_STAGE_ONLY", 0, 0, 2);
+    sh.L = tune_int("JIT_L", h->prog_ciw ? 2 : 3, 1, 8);
+    sh.minw = tune_int("JIT_MINW", 0, 0, 8);
     // speculative no-rescale pass (plk_jit.hpp): a win only where rescaling never
     // fires; on cfg5 it fires in almost every super-block (1.27 vs 1.14 ms), so opt-in
-    sh.exact_only = !env_is("PLK_JIT_SPECULATE", '1');
     // classes in the wave: next class's P(t) loads overlap this class's FMAs (PLK_JIT_PPIPE=0: off)
-    sh.ppipe = !env_is("PLK_JIT_PPIPE", '0');
+    sh.ppipe = !tune_is("JIT_PPIPE", '0');
     // PLK_JIT_BLOCKS=1: the root fragment forms the block sums (no wave_sums_to_blocks
     // launch).  Measured slower (cfg2 traversal 0.125 -> 0.160 ms): the wave that stores a
     // wave sum must wait for the store and the counter's atomic round trip (~3 us) before
     // its workgroup's next super-block barrier, in every super-block.  Off; the formal
     // release/acquire form (an L2 write-back per wave) was slower still (round 1)
-    sh.blocks = env_is("PLK_JIT_BLOCKS", '1');
     if (sh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
-    if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW || sh.PW != h->jit_shape.PW ||
+    if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW ||
         sh.pin != h->jit_shape.pin ||
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
-        sh.minw != h->jit_shape.minw || sh.same_p != h->jit_shape.same_p || sh.stage_only != h->jit_shape.stage_only || sh.exact_only != h->jit_shape.exact_only ||
-        sh.ppipe != h->jit_shape.ppipe || sh.blocks != h->jit_shape.blocks) {
+        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
@@ -1965,10 +1952,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.n_patterns = a.n_patterns;
     ja.n_sblocks = (int32_t)((h->n_pad + 64 * sh.G * sh.PW - 1) / (64 * sh.G * sh.PW));  // last may be ragged
     ja.guard = a.guard;
-    ja.blk_cnt = h->d_blk_cnt;
-    ja.block_sums = block_target(h);
-    ja.n_waves = (int32_t)((h->n_patterns + 63) / 64);
-    ja.n_wpad = (int32_t)(h->n_pad / 64);
   }
   const bool jitm = kind == FK_TREEM && h->prog_jitm;
   JMArgs ma;
@@ -1978,12 +1961,12 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.C = h->C;
     msh.U = h->n_codes;
     msh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
-    msh.L = env_int("PLK_JITM_L", 1, 1, 4);
-    msh.minw = env_int("PLK_JITM_MINW", 2, 1, 8);
-    msh.pd = env_int("PLK_JITM_PD", 1, 1, 3);
+    msh.L = tune_int("JITM_L", 1, 1, 4);
+    msh.minw = tune_int("JITM_MINW", 2, 1, 8);
+    msh.pd = tune_int("JITM_PD", 1, 1, 3);
     // 16-pattern waves per workgroup: 4 (64 patterns) or 8 (128; every P(t) staging and its
     // barrier serve twice the patterns)
-    msh.G = env_int("PLK_JITM_G", 4, 4, 8) >= 8 ? 8 : 4;
+    msh.G = tune_int("JITM_G", 4, 4, 8) >= 8 ? 8 : 4;
     if (msh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "jit_treeM needs %zu B of LDS", msh.lds_bytes());
     if (!h->jitm_fn || !(msh == h->jitm_shape)) {
@@ -2011,7 +1994,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ma.cherry_count_bytes = (int64_t)lay.count_bytes;
     ma.guard = a.guard;
   }
-  h->kernel_path = jit ? "jit_tree4" : jitm ? "jit_treeM" : kind == FK_TREEM ? "treeM" : kind == FK_TREES ? "treeS" : "tree4";
+  h->kernel_path = jit ? "jit_tree4" : jitm ? "jit_treeM" : kind == FK_TREEM ? "treeM" : "tree4";
   int first = 0;
   for (const auto& t : h->prog_tiers) {
     a.frag_start = h->d_frag + first;
@@ -2027,7 +2010,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       void* args[] = {&ja, &pm, &base};
       // persistent grid: as many workgroups as are resident at once (occupancy query), so
       // every workgroup stages its tables once and there is no second dispatch round
-      int wgs = env_int("PLK_JIT_WGS", 0, 0, 1 << 20);
+      int wgs = tune_int("JIT_WGS", 0, 0, 1 << 20);
       if (wgs == 0) {
         if (h->jit_resident <= 0) {
           int per_cu = 0, n_cu = 0;
@@ -2040,7 +2023,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         // fragments (each stages its fragment's tables once and walks many super-blocks)
         // instead of the tier's fragments running one after another with every workgroup
         // staging tables for a few super-blocks (PLK_JIT_SPLIT_Y=0: the latter)
-        wgs = env_is("PLK_JIT_SPLIT_Y", '0') ? h->jit_resident : std::max(1, h->jit_resident / (int)grid.y);
+        wgs = tune_is("JIT_SPLIT_Y", '0') ? h->jit_resident : std::max(1, h->jit_resident / (int)grid.y);
       }
       const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, wgs);
       h->jit_last_gx = (int)gx;
@@ -2061,8 +2044,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         site_wave_sums_kernel<<<(unsigned)(h->n_pad / 256), 256, 0, h->stream>>>(a.site_lnl, a.weights,
                                                                                  a.wave_sums, a.n_patterns, a.n_pad);
       }
-    } else if (kind == FK_TREES) {
-      launch_treeS<20>(h, a, grid);
     } else {
       switch (cw) {
         case 1: launch_tree4_cw<1>(h, a, grid, lds); break;
@@ -2081,7 +2062,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   h->fused_lnl_valid = h->prog_root >= 0;
   h->fused_lnl_root = h->prog_root;
   // the jit kernel's root fragment formed the block sums (JitShape::blocks)
-  h->blocks_fused = jit && h->prog_root >= 0 && h->jit_shape.blocks;
   return PLK_OK;
 }
 
@@ -2184,7 +2164,6 @@ int update_levelwise(plk_handle h, const plk_op* ops, int n_ops) {
   }
   for (int i = 0; i < n_ops; ++i) h->materialized[ops[i].parent - h->n_tips] = 1;
   h->fused_lnl_valid = false;
-  h->blocks_fused = false;
   h->slots_expanded = false;
   return PLK_OK;
 }
@@ -2484,7 +2463,6 @@ int update_compressed(plk_handle h, const plk_op* ops, int n_ops) {
   }
   for (int i = 0; i < n_ops; ++i) h->materialized[ops[i].parent - h->n_tips] = 1;
   h->fused_lnl_valid = false;
-  h->blocks_fused = false;
   h->slots_expanded = false;
   return PLK_OK;
 }
@@ -3128,7 +3106,7 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   // 4 states without rescaling: the fused preorder (dr_pre_s4_kernel), one launch per
   // level of fathers, branch terms reduced where U is formed (PLK_DR_PRE=0: the
   // levelwise preorder + reduction below)
-  bool pre = S == 4 && !(h->flags & PLK_FLAG_SCALING) && (C == 1 || C == 2 || C == 4) && !env_is("PLK_DR_PRE", '0');
+  bool pre = S == 4 && !(h->flags & PLK_FLAG_SCALING) && (C == 1 || C == 2 || C == 4) && !tune_is("DR_PRE", '0');
   for (size_t d = 0; pre && d < depth.size(); ++d)
     for (int f : depth[d])
       if (f >= nt && (h->topo_kids[f].size() < 2 || h->topo_kids[f].size() > 3)) pre = false;
@@ -3147,11 +3125,11 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
     HIPCHK(h, hipGetLastError());
   }
   // S = 20 / 64 reduce on fp64 MFMA (64-pattern blocks) unless PLK_DR_MFMA=0
-  const bool dr_mfma = (S == 20 || S == 64) && !env_is("PLK_DR_MFMA", '0');
+  const bool dr_mfma = (S == 20 || S == 64) && !tune_is("DR_MFMA", '0');
   // tips whose father has one other son and a father of its own: U_v formed inside the
   // reduction (S <= 4 kernel), never stored (PLK_DR_FUSE=0 stores every U_v)
   std::vector<char> fused(nn, 0);
-  if (!dr_mfma && S <= 4 && !env_is("PLK_DR_FUSE", '0'))
+  if (!dr_mfma && S <= 4 && !tune_is("DR_FUSE", '0'))
     for (int v = 0; v < nt; ++v)
       if (parent[v] >= 0 && parent[v] != root && h->topo_kids[parent[v]].size() == 2) fused[v] = 1;
   // U_v for every non-root node, one launch per (depth, child chunk)
@@ -3260,7 +3238,7 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
     am.G = 3 * (size_t)C * S * S * sizeof(double) <= 64 * 1024 ? C : 1;
     const size_t lds_m = 3 * (size_t)am.G * S * S * sizeof(double);
     // a few workgroups per branch, each looping over pattern blocks (PLK_DR_WGS total)
-    const int want = env_int("PLK_DR_WGS", 4096, 1, 1 << 20);
+    const int want = tune_int("DR_WGS", 4096, 1, 1 << 20);
     grid.x = (unsigned)std::min<int64_t>(n_blk, std::max<int64_t>(1, (want + (int)br.size() - 1) / (int)br.size()));
     if (S == 20)
       dr_branch_mfma_kernel<20><<<grid, kDrmThreads, lds_m, h->stream>>>(h->d_drb, am);
@@ -3402,22 +3380,18 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
   if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
   hipSetDevice(h->device);
   if (h->fused_lnl_valid && h->fused_lnl_root == root) {
-    // the fused traversal already reduced the root: only the block sums remain (unless
-    // its root fragment formed them too)
-    if (!h->blocks_fused) {
-      const int n_waves = (int)((h->n_patterns + 63) / 64);
-      wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, block_target(h), n_waves,
-                                                                            h->n_blocks);
-      HIPCHK(h, hipGetLastError());
-    }
+    // the fused traversal already reduced the root: only the block sums remain
+    const int n_waves = (int)((h->n_patterns + 63) / 64);
+    wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, block_target(h), n_waves,
+                                                                          h->n_blocks);
+    HIPCHK(h, hipGetLastError());
   } else {
     if (!h->materialized[root - h->n_tips]) return fail(h, PLK_ERR_STATE, "root %d has no partial", root);
     int rc = launch_root(h, root);
     if (rc) return rc;
     // the wave sums and block sums of the fused root reduction are overwritten
     h->fused_lnl_valid = false;
-    h->blocks_fused = false;
-  }
+    }
   if (h->comm) {
     // the one cross-GPU exchange of an evaluation: a fixed-size all-gather of block sums
     if (ncclAllGather(h->d_blk_local, h->d_blk_all, (size_t)h->comm_cmax, ncclFloat64, h->comm, h->stream) !=
@@ -3553,7 +3527,7 @@ int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   if (h && !h->shards.empty()) return multi_branch_derivatives(h, branch, d1, d2);
   if (!h || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
   if (h->trav_ops.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet (plk_update_partials)");
-  if (h->S != 4 || !(h->C == 1 || h->C == 2 || h->C == 4) || env_is("PLK_DERIV_PATH", '1'))
+  if (h->S != 4 || !(h->C == 1 || h->C == 2 || h->C == 4) || tune_is("DERIV_PATH", '1'))
     return path_derivatives(h, branch, d1, d2);
   if (h->deriv_valid.empty() || !h->deriv_valid[branch])
     return fail(h, PLK_ERR_STATE, "dP/d2P of branch %d not computed (PLK_DERIV_DP | PLK_DERIV_D2P)", branch);

@@ -53,7 +53,6 @@ struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
   double* partials; i32* scale; const u8* codes; const double* tipP; const double* weights;
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
-  unsigned* blk_cnt; double* block_sums; i32 n_waves; i32 n_wpad;  // BLK_: block sums in the kernel
 };
 
 // Register vectors hold 4 * CW * PW doubles: vector v = pw * CW + cw is class c0 + cw of
@@ -337,38 +336,7 @@ __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
-      if (!BLK_) {
-        if (gv && lane == 0) a.wave_sums[(p0 + 64 * pw) >> 6] = wr;
-        continue;
-      }
-      // BLK_: the wave that completes a 4096-pattern block forms its block sum (the 64 wave
-      // sums added in wave order, as wave_sums_to_blocks does).  The wave sum is stored at
-      // agent scope and waited for before the block's counter is bumped; the last arriver
-      // reads the block's wave sums at agent scope -- no L2 write-back fence, which made the
-      // release/acquire form of this slower than the extra launch
-      const int wv = (int)((p0 + 64 * pw) >> 6), b = wv >> 6;
-      int last = 0;
-      if (gv && lane == 0) {
-        __hip_atomic_store(a.wave_sums + wv, wr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0);
-        const int need = min(64, a.n_wpad - b * 64);
-        last = __hip_atomic_fetch_add(a.blk_cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               (unsigned)(need - 1);
-      }
-      last = __shfl(last, 0, 64);
-      if (last) {
-        const int w = b * 64 + lane;
-        const double v = w < a.n_waves ? __hip_atomic_load(a.wave_sums + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-        double sb = 0.0;
-        for (int k = 0; k < 64; ++k) {
-          const double x = __shfl(v, k, 64);
-          if (b * 64 + k < a.n_waves) sb += x;
-        }
-        if (lane == 0) {
-          a.block_sums[b] = sb;
-          __hip_atomic_store(a.blk_cnt + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
-        }
-      }
+      if (gv && lane == 0) a.wave_sums[(p0 + 64 * pw) >> 6] = wr;
     }
   }
 }
@@ -390,10 +358,6 @@ struct JArgs {
   int64_t n_patterns;
   int32_t n_sblocks;
   int32_t guard;
-  unsigned* blk_cnt;
-  double* block_sums;
-  int32_t n_waves;
-  int32_t n_wpad;
 };
 
 struct JitShape {
@@ -408,11 +372,7 @@ struct JitShape {
   bool scale = false;
   int L = 1;        // operand fetch lookahead (events)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
-  bool same_p = false;  // timing experiments only: every internal branch reads P(t) of node 0
-  int stage_only = 0;  // timing experiments only: return after staging the tables (1) / at once (2)
-  bool exact_only = true;   // scaling: no speculative no-rescale pass (PLK_JIT_SPECULATE=1 enables it)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
-  bool blocks = false;      // the root fragment forms the 4096-pattern block sums (BLK_)
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     // the second exchange buffer only serves the per-node rescale
@@ -555,8 +515,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   std::string s;
   s.reserve(4096 * events.size() + 16384);
   s += sh.ppipe ? "#define PPIPE_ 1\n" : "#define PPIPE_ 0\n";  // read by the prelude's contrib
-  s += "#define STAGE_ONLY_ " + std::to_string(sh.stage_only) + "\n";
-  s += sh.blocks ? "#define BLK_ 1\n" : "#define BLK_ 0\n";
   s += kJitPrelude;
   char buf[400];
   const std::string minw_s = sh.minw > 0 ? ", " + std::to_string(sh.minw) : std::string();
@@ -604,7 +562,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c0 = (w % NW_) * CW_, g = w / NW_;
-  if (STAGE_ONLY_ == 2) return;
   const int frag = frag_base + (int)blockIdx.y;
   const int u0 = 1 + kFragUnitStart[frag], nu = kFragUnitStart[frag + 1] - kFragUnitStart[frag];
   // tables: wave w stages units w, w + NWT_, ... (one dependent chain per unit and wave,
@@ -681,7 +638,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       }
     }
   }
-  if (STAGE_ONLY_) return;
   const CPd pm = (CPd)(pmats + c0 * 16);
   const double* trow = tab + c0 * (U_ * 4);         // single-tip units
   const double* trow2 = tab + c0 * (U_ * U_ * 4);   // pair units
@@ -766,7 +722,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         fetchers.push_back((int)i);
       }
     auto pref = [&](size_t i) -> std::string {  // P operand of event i
-      snprintf(buf, sizeof(buf), "pm + %lld", sh.same_p ? 0LL : (long long)ev[i].b * C * 16);
+      snprintf(buf, sizeof(buf), "pm + %lld", (long long)ev[i].b * C * 16);
       return buf;
     };
     // Two-stage operand pipeline (L >= 2): a tip's code is read L fetchers ahead (and a
@@ -924,24 +880,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     };
     snprintf(buf, sizeof(buf), "    case %zu: {\n", f);
     s += buf;
-    if (sh.scale && !sh.exact_only) {
-      s += "      int dng = 0;\n";
-      emit_body(false);
-      // the exact pass reads its operands through laundered copies of the base pointers,
-      // so the compiler cannot reuse (and keep live across the vote) the fast pass's loads
-      s += "      if (__syncthreads_or(dng)) {  // a check could have rescaled: redo it exactly\n"
-           "      const CPd pmo_ = pm; const double* trowo_ = trow; const double* trow2o_ = trow2; const u8* crowo_ = crow; const i64 toffo_ = toff;\n"
-           "      {\n"
-           "      const CPd pm = (CPd)launder_s((unsigned long long)pmo_);\n"
-           "      const double* trow = (const double*)launder_s((unsigned long long)trowo_);\n"
-           "      const double* trow2 = (const double*)launder_s((unsigned long long)trow2o_);\n"
-           "      const u8* crow = (const u8*)launder_v((unsigned long long)crowo_);\n"
-           "      const i64 toff = (i64)launder_v((unsigned long long)toffo_);\n";
-      emit_body(true);
-      s += "      }\n      }\n";
-    } else {
-      emit_body(true);
-    }
+    emit_body(true);
     s += "    } break;\n";
   }
   s += "    default: break;\n    }\n  }\n}\n";

@@ -18,3 +18,16 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def root_dir():
     return ROOT
+
+
+def set_tune(monkeypatch, key, value):
+    """Set one of libplk's tuning knobs: they all live in PLK_TUNE="KEY=value,..."
+    (csrc/plk.hip tune_get)."""
+    cur = [kv for kv in os.environ.get("PLK_TUNE", "").split(",") if "=" in kv and kv.split("=", 1)[0] != key]
+    cur.append(f"{key}={value}")
+    monkeypatch.setenv("PLK_TUNE", ",".join(cur))
+
+
+def clear_tune(monkeypatch, key):
+    cur = [kv for kv in os.environ.get("PLK_TUNE", "").split(",") if "=" in kv and kv.split("=", 1)[0] != key]
+    monkeypatch.setenv("PLK_TUNE", ",".join(cur))

@@ -15,6 +15,7 @@ import pytest
 import phylo
 import plk
 import workload
+from conftest import clear_tune, set_tune
 from test_gpu_parity import MODES, _caterpillar, _random_problem, engine_for, oracle_for, run_engine
 
 pytestmark = pytest.mark.gpu
@@ -242,7 +243,7 @@ def test_dr_fused_preorder_equals_levelwise(C, n_taxa, n_pat, amb, monkeypatch):
     br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
     out = {}
     for pre in ("0", "1"):
-        monkeypatch.setenv("PLK_DR_PRE", pre)
+        set_tune(monkeypatch, "DR_PRE", pre)
         eng = engine_for(et, 4, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m],
                          flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | DR)
         eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)

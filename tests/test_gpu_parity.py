@@ -17,6 +17,7 @@ import oracle
 import phylo
 import plk
 import workload
+from conftest import clear_tune, set_tune
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -362,18 +363,16 @@ def test_evaluate_equals_three_calls(S, C, flags):
                                                    (2, False, 130)])
 def test_pmat4_and_kernel_block_sums_bitwise(C, scaling, n_patterns, monkeypatch):
     """The 4-state K4 (pmat4_kernel: a thread per row of P) equals pmat_kernel bitwise -- P,
-    dP, d2P and, through the traversal, the tip tables -- and the JIT kernel's in-kernel
-    block sums (the wave completing a 4096-pattern block adds its 64 wave sums) equal
-    wave_sums_to_blocks' bitwise, for one, several and ragged blocks; a second root
-    reduction without a new traversal returns the same block sums."""
+    dP, d2P and, through the traversal, the tip tables and the block sums, for one, several
+    and ragged blocks; a second root reduction without a new traversal returns the same
+    block sums."""
     et, m, alph, rates, probs, states = _random_problem(4, C, 40, n_patterns, seed=77, amb=True)
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | (plk.PLK_FLAG_SCALING if scaling else 0)
     br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
     ops = phylo.split_ops(et.ops)
     out = {}
     for new in ("0", "1"):
-        monkeypatch.setenv("PLK_PMAT4", new)
-        monkeypatch.setenv("PLK_JIT_BLOCKS", new)
+        set_tune(monkeypatch, "PMAT4", new)
         eng = engine_for(et, 4, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
         eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
         mats = [np.stack([eng.get_pmatrix(int(b)) for b in br]),
@@ -399,9 +398,9 @@ def test_pmat4_and_kernel_block_sums_bitwise(C, scaling, n_patterns, monkeypatch
 
 @pytest.mark.parametrize("S,C", [(4, 4), (20, 2)])
 def test_pmat_request_paths_bitwise(S, C, monkeypatch):
-    """A P(t) request in the kernel arguments, through mapped pinned staging (default for
-    more than 160 branches) and through a stream-ordered copy of the staging give the
-    same transition matrices and lnL bitwise (NH: a model index per branch)."""
+    """A P(t) request in the kernel arguments and through mapped pinned staging (default for
+    more than 160 branches) give the same transition matrices and lnL bitwise (NH: a model
+    index per branch)."""
     et, m, alph, rates, probs, states = _random_problem(S, C, 24, 700, seed=5)
     rng = np.random.default_rng(9)
     models = [m] + [phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5)) for _ in range(2)] \
@@ -410,9 +409,8 @@ def test_pmat_request_paths_bitwise(S, C, monkeypatch):
     br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
     ops = phylo.split_ops(et.ops)
     out = []
-    for staged, mapped in (("0", "1"), ("1", "1"), ("1", "0")):
-        monkeypatch.setenv("PLK_PMAT_STAGED", staged)
-        monkeypatch.setenv("PLK_PMAT_MAPPED", mapped)
+    for staged in ("0", "1"):
+        set_tune(monkeypatch, "PMAT_STAGED", staged)
         eng = engine_for(et, S, C, 700, states, alph.init_table, rates, probs, m.pi, models, model_of_node=mon,
                          flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY)
         res = []
@@ -562,12 +560,12 @@ def test_s4_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling):
 
 
 @pytest.mark.parametrize("mode", sorted(MODES))
-@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,dm", [
-    (4, "balanced64", 700, False, 2), (1, "balanced64", 333, True, 3), (2, "caterpillar30", 400, True, 2),
-    (4, "caterpillar30", 300, False, 4), (3, "balanced100", 257, True, 3)])
-def test_s20_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling, dm, monkeypatch):
-    """20-state fused traversal (treeS_kernel) at every register depth, against the oracle."""
-    monkeypatch.setenv("PLK_TREES_DM", str(dm))
+@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling", [
+    (4, "balanced64", 700, False), (1, "balanced64", 333, True), (2, "caterpillar30", 400, True),
+    (4, "caterpillar30", 300, False), (3, "balanced100", 257, True)])
+def test_s20_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling):
+    """20 states in every traversal mode (jit_treeM lnL-only / materialising, levelwise K2),
+    against the oracle."""
     if tree_kind.startswith("balanced"):
         tree = phylo.balanced_tree(int(tree_kind[8:]), seed=19, lo=0.05, hi=0.4)
     else:
@@ -603,7 +601,6 @@ def test_s20_modes_vs_oracle(mode, C, tree_kind, n_patterns, scaling, dm, monkey
     (2, "balanced64", 700, True, "lnl_only"), (1, "caterpillar40", 300, True, "materialize"),
     (4, "caterpillar40", 900, False, "lnl_only"), (4, "balanced300", 513, True, "lnl_only"),
     (4, "caterpillar200long", 600, True, "lnl_only"), (2, "caterpillar200long", 300, True, "materialize"),
-    (4, "caterpillar200longspec", 600, True, "lnl_only"), (4, "balanced64spec", 500, True, "materialize"),
     # cherry pair tables (every cherry with 4 codes; within a small budget) and G groups per
     # workgroup with a ragged last super-block
     (4, "balanced64", 3000, False, "lnl_only", "acgt"), (4, "balanced64", 1000, False, "materialize", "acgt G=3"),
@@ -618,15 +615,11 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     """The tree-specialised kernel (plk_jit.hpp, hiprtc) against the interpreter
     (tree4_kernel) on the same program: lnL, per-pattern lnL, block sums and every
     interior partial bitwise; and the oracle at 1e-12.  The long-branch caterpillar
-    drives partials below 2^-256, so the speculative no-rescale pass must detect it
-    and fall back to the exact pass."""
+    drives partials below 2^-256 (rescaling in both kernels)."""
     for kv in extra.split():
         if "=" in kv:
             k, v = kv.split("=")
-            monkeypatch.setenv("PLK_JIT_" + k, v)
-    if tree_kind.endswith("spec"):   # the speculative no-rescale pass with its exact fallback
-        monkeypatch.setenv("PLK_JIT_SPECULATE", "1")
-        tree_kind = tree_kind[:-4]
+            set_tune(monkeypatch, "JIT_" + k, v)
     if tree_kind.startswith("balanced"):
         tree = phylo.balanced_tree(int(tree_kind[8:]), seed=23, lo=0.05, hi=0.4)
     elif tree_kind.endswith("long"):
@@ -651,7 +644,7 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
     res = {}
     for kernel in ("0", "1"):
-        monkeypatch.setenv("PLK_JIT", kernel)
+        set_tune(monkeypatch, "JIT", kernel)
         eng = engine_for(et, 4, C, n_patterns, states, init, rates, probs, m.pi, [m], flags=flags)
         lnl, site, blocks = run_engine(eng, et)
         assert eng.kernel_path() == ("jit_tree4" if kernel == "1" else "tree4")
@@ -798,9 +791,9 @@ def test_branch_derivatives_path_equals_kernel(monkeypatch):
     run_engine(eng, et)
     for b in (0, 5, et.n_tips + 2, br[-1]):
         k1, k2 = eng.branch_derivatives(int(b))
-        monkeypatch.setenv("PLK_DERIV_PATH", "1")
+        set_tune(monkeypatch, "DERIV_PATH", "1")
         p1, p2 = eng.branch_derivatives(int(b))
-        monkeypatch.delenv("PLK_DERIV_PATH")
+        clear_tune(monkeypatch, "DERIV_PATH")
         assert abs(k1 - p1) <= 1e-11 * max(1.0, abs(k1)) and abs(k2 - p2) <= 1e-10 * max(1.0, abs(k2)), (b, k1, p1, k2, p2)
 
 
@@ -900,8 +893,8 @@ def test_subtree_patterns_any_state_count(S, C, n_taxa, n_patterns, scaling, amb
     (lnL, per-pattern lnL, block sums and every partial expanded through the links)."""
     et, m, alph, rates, probs, states = _random_problem(S, C, n_taxa, n_patterns, seed=90 + S + C, amb=amb)
     sc = plk.PLK_FLAG_SCALING if scaling else 0
-    monkeypatch.setenv("PLK_GENERIC20", "1")
-    monkeypatch.setenv("PLK_GENERIC64", "1")
+    set_tune(monkeypatch, "GENERIC20", "1")
+    set_tune(monkeypatch, "GENERIC64", "1")
     ref = engine_for(et, S, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m],
                      flags=plk.PLK_FLAG_NONNEG_GUARD | sc | plk.PLK_FLAG_LEVELWISE)
     l0, s0, b0 = run_engine(ref, et)
@@ -960,10 +953,10 @@ def test_treeM_cherry_tables_bitwise(S, C, scaling, variant, monkeypatch):
         rng = np.random.default_rng(7)
         states[rng.random(states.shape) < 0.3] = code
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | (plk.PLK_FLAG_SCALING if scaling else 0)
-    monkeypatch.setenv("PLK_JITM", "0")   # the treeM interpreter (20 states default to jit_treeM)
+    set_tune(monkeypatch, "JITM", "0")   # the treeM interpreter (20 states default to jit_treeM)
     res = {}
     for on in ("0", "1"):
-        monkeypatch.setenv("PLK_TREEM_CHERRY", on)
+        set_tune(monkeypatch, "TREEM_CHERRY", on)
         eng = engine_for(et, S, C, 700, states, init, rates, probs, m.pi, [m], flags=flags)
         res[on] = run_engine(eng, et)
         assert eng.kernel_path() == "treeM"
@@ -983,8 +976,8 @@ def test_pmat64_kernels_bitwise(monkeypatch):
     et, m, alph, rates, probs, states = _random_problem(64, 1, 24, 500, seed=64, amb=True)
     out = {}
     for on, split in (("0", "1"), ("1", "0"), ("1", "1")):  # generic, pmat64_kernel, pmat64s_kernel
-        monkeypatch.setenv("PLK_PMAT64", on)
-        monkeypatch.setenv("PLK_PMAT64_SPLIT", split)
+        set_tune(monkeypatch, "PMAT64", on)
+        set_tune(monkeypatch, "PMAT64_SPLIT", split)
         eng = engine_for(et, 64, 1, 500, states, alph.init_table, rates, probs, m.pi, [m],
                          flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY)
         lnl, site, _ = run_engine(eng, et)
@@ -1005,10 +998,10 @@ def test_treeM_direct_tables_bitwise(S, C, scaling, mode, monkeypatch):
     et, m, alph, rates, probs, states = _random_problem(S, C, 40 if S == 20 else 20, 600, seed=S + 3 * C,
                                                         amb=S == 20)
     flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
-    monkeypatch.setenv("PLK_JITM", "0")
+    set_tune(monkeypatch, "JITM", "0")
     res = {}
     for on in ("0", "1"):
-        monkeypatch.setenv("PLK_TREEM_DIRECT", on)
+        set_tune(monkeypatch, "TREEM_DIRECT", on)
         eng = engine_for(et, S, C, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
         lnl, site, blocks = run_engine(eng, et)
         assert eng.kernel_path() == "treeM"
@@ -1027,10 +1020,10 @@ def test_treeM_32_pattern_workgroups_bitwise(C, scaling, mode, n_pat, monkeypatc
     site_lnl by site_wave_sums_kernel) equal the 64-pattern kernel bitwise."""
     et, m, alph, rates, probs, states = _random_problem(20, C, 40, n_pat, seed=7 * C + n_pat)
     flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
-    monkeypatch.setenv("PLK_JITM", "0")
+    set_tune(monkeypatch, "JITM", "0")
     res = {}
     for g in ("4", "2", "1"):
-        monkeypatch.setenv("PLK_TREEM_G", g)
+        set_tune(monkeypatch, "TREEM_G", g)
         eng = engine_for(et, 20, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
         lnl, site, blocks = run_engine(eng, et)
         assert eng.kernel_path() == "treeM"
@@ -1089,7 +1082,7 @@ def test_jit_treeM_vs_oracle(C, tree_kind, n_patterns, scaling, mode, variant, m
     parts = np.stack([eng.get_partials(p) for p, _ in et.ops[-4:]])
     assert np.all(np.isfinite(parts))
     # the treeM interpreter on the same inputs
-    monkeypatch.setenv("PLK_JITM", "0")
+    set_tune(monkeypatch, "JITM", "0")
     ref = engine_for(et, 20, C, n_patterns, states, init, rates, probs, m.pi, [m], flags=flags)
     lr, sr, _ = run_engine(ref, et)
     assert ref.kernel_path() == "treeM"
@@ -1110,10 +1103,10 @@ def test_jit_treeM_register_depths(dm, L, pd, g, monkeypatch):
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
     l0, s0, _ = run_engine(eng, et)
     del eng
-    monkeypatch.setenv("PLK_JITM_DM", str(dm))
-    monkeypatch.setenv("PLK_JITM_L", str(L))
-    monkeypatch.setenv("PLK_JITM_PD", str(pd))
-    monkeypatch.setenv("PLK_JITM_G", str(g))
+    set_tune(monkeypatch, "JITM_DM", str(dm))
+    set_tune(monkeypatch, "JITM_L", str(L))
+    set_tune(monkeypatch, "JITM_PD", str(pd))
+    set_tune(monkeypatch, "JITM_G", str(g))
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
     l1, s1, _ = run_engine(eng, et)
     assert eng.kernel_path() == "jit_treeM"
@@ -1128,7 +1121,7 @@ def test_jit_treeM_register_depths(dm, L, pd, g, monkeypatch):
 def test_s4_on_matrix_cores_vs_oracle(C, tree_kind, n_patterns, scaling, mode, nh, monkeypatch):
     """4 states through jit_treeM (PLK_S4_JITM=1: one v_mfma_f64_4x4x4_4b block per class
     and 16 patterns) against the oracle at 1e-12, homogeneous and per-branch models."""
-    monkeypatch.setenv("PLK_S4_JITM", "1")
+    set_tune(monkeypatch, "S4_JITM", "1")
     if tree_kind.startswith("balanced"):
         tree = phylo.balanced_tree(int(tree_kind[8:]), seed=41, lo=0.05, hi=0.4)
     elif tree_kind.endswith("long"):
@@ -1158,38 +1151,5 @@ def test_s4_on_matrix_cores_vs_oracle(C, tree_kind, n_patterns, scaling, mode, n
     lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, pi, models, model_of_node=mon,
                         scaling=scaling, pmats=engine_pmats(eng, et))
     check(lnl, site, lo, so)
-    lnl2, site2, _ = run_engine(eng, et)
-    assert lnl2 == lnl and np.array_equal(site2, site)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("C,n_taxa,n_patterns,scaling,mode,variant", [
-    (1, 24, 700, False, "lnl_only", ""), (1, 40, 500, True, "materialize", "amb"), (1, 128, 300, False, "lnl_only", "yn98"),
-    (2, 16, 400, True, "lnl_only", ""), (1, 24, 600, True, "lnl_only", "tiny")])
-def test_jit_treeM_64_states_vs_oracle(C, n_taxa, n_patterns, scaling, mode, variant, monkeypatch):
-    """64 states on jit_treeM (PLK_JITM64=1: 16 x 16 blocks of v_mfma_f64_4x4x4_4b per
-    class and contraction) against the oracle at 1e-12 on the engine's P(t), incl. the YN98
-    codon model of config 4 with its null stop states."""
-    monkeypatch.setenv("PLK_JITM64", "1")
-    et, m, alph, rates, probs, states = _random_problem(64, C, n_taxa, n_patterns, seed=640 + C + n_taxa,
-                                                        amb=variant == "amb")
-    if variant == "yn98":
-        m = phylo.yn98(2.0, 0.3)
-        wl = workload.Workload("y", et, [m], None, rates, probs, m.pi, phylo.CODON, n_patterns, scaling, True, 3)
-        states = wl.simulate(0, n_patterns).astype(np.int32)
-    init = alph.init_table
-    if variant == "tiny":
-        init = np.array(init, dtype=np.float64, copy=True)
-        code = alph.n_codes - 1
-        init[code] = 1e-80
-        states[np.random.default_rng(2).random(states.shape) < 0.3] = code
-    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
-    eng = engine_for(et, 64, C, n_patterns, states, init, rates, probs, m.pi, [m], flags=flags)
-    lnl, site, _ = run_engine(eng, et)
-    assert eng.kernel_path() == "jit_treeM"
-    lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=scaling, pmats=engine_pmats(eng, et))
-    check(lnl, site, lo, so)
-    if variant == "tiny":
-        assert site.min() < -256 * np.log(2)
     lnl2, site2, _ = run_engine(eng, et)
     assert lnl2 == lnl and np.array_equal(site2, site)

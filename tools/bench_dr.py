@@ -9,7 +9,7 @@ duration and their algorithmic HBM rate.  Two engine paths (`dr_path`):
   * fused (4 states without rescaling, dr_pre_s4_kernel): per father f, U_f read (8 C S,
     not at the root), every son's L (8 C S internal, 1 B tip), the U of internal sons
     written (8 C S), the weight (8 B);
-  * levelwise (otherwise, or PLK_DR_PRE=0): every upper vector U_v written once (8 C S)
+  * levelwise (otherwise, or PLK_TUNE=DR_PRE=0): every upper vector U_v written once (8 C S)
     and read by the reduction (8 C S); the preorder update of U_v reads U_father (8 C S,
     not at the root's sons) and every sibling (8 C S internal, 1 B tip); the reduction
     reads L_v (8 C S internal, 1 B tip) and the weight (8 B) -- `reduction_kernel_ms` and
@@ -86,7 +86,7 @@ def main():
         worst = max(worst, abs(p1 - d1[b]) / max(1.0, abs(p1)), abs(p2 - d2[b]) / max(1.0, abs(p2)))
     t_path = (time.perf_counter() - t0) / len(sel) * nb
     up, red = dr_bytes(wl)
-    fused = wl.S == 4 and not wl.scaling and os.environ.get("PLK_DR_PRE", "1") != "0"
+    fused = wl.S == 4 and not wl.scaling and "DR_PRE=0" not in os.environ.get("PLK_TUNE", "")
     fb = dr_fused_bytes(wl)
     rec = {
         "metric": "branch x site-pattern derivative updates/s (d1 and d2 of every branch)",
