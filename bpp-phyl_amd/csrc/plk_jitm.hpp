@@ -112,11 +112,12 @@ struct JitMShape {
   int minw = 2;      // __launch_bounds__ min waves per SIMD
   int pd = 1;        // P(t) staging prefetch distance (contractions ahead)
   int G = 4;         // waves (16-pattern groups) per workgroup: 64 patterns (4) or 128 (8)
+  bool swz = true;   // tile image rotated per Y block (conflict-free staging stores)
   int pb() const { return C * S * S; }  // doubles of P(t) per branch (every class)
   size_t lds_bytes() const { return (size_t)(2 * pb() + 16 * G) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
     return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && pd == o.pd &&
-           G == o.G;
+           G == o.G && swz == o.swz;
   }
 };
 
@@ -132,8 +133,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const int NTH = 64 * sh.G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH;
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
-           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n",
-           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PF, sh.scale ? "true" : "false");
+           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n#define SWZ_ %d\n",
+           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PF, sh.scale ? "true" : "false", sh.swz ? 1 : 0);
   s += buf;
   s += R"PLKJITM(
 // P(t) of branch b (all classes, [c][x][y]) -> registers -> the LDS tile image
@@ -220,12 +221,12 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   // A-operand lane bases, one per tile rotation Y & 3 (lane 16 hi + 4 b + lo reads tile
   // element (hi, lo))
   const double* PA[4];
-  _Pragma("unroll") for (int k = 0; k < 4; ++k) PA[k] = lds + ((hi << 2) | (((lane & 3) + k) & 3));
+  _Pragma("unroll") for (int k = 0; k < 4; ++k) PA[k] = lds + ((hi << 2) | (((lane & 3) + (SWZ_ ? k : 0)) & 3));
   int sidx[PF_];   // this thread's staging elements -> tile slots (-1: past the table)
   _Pragma("unroll") for (int j = 0; j < PF_; ++j) {
     const int e = tid + j * NTH_;
     const int c = e / (S_ * S_), r = e - c * (S_ * S_), x = r / S_, y = r - x * S_;
-    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (((x & 3) + (y >> 2)) & 3) : -1;
+    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (((x & 3) + (SWZ_ ? (y >> 2) : 0)) & 3) : -1;
   }
   double R0[PF_] = {}, R1[PF_] = {}, R2[PF_] = {};
   (void)red; (void)PA; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
