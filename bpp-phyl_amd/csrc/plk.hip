@@ -140,6 +140,8 @@ struct plk_handle_s {
   double* pmats = nullptr;
   double* dpmats = nullptr;
   double* d2pmats = nullptr;
+  double* dpmatsT = nullptr;   // dP^T, d2P^T: the fused 20/64-state DR preorder
+  double* d2pmatsT = nullptr;
   double* V = nullptr;
   double* Vinv = nullptr;
   double* lambda = nullptr;
@@ -944,7 +946,7 @@ int plk_destroy(plk_handle h) {
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
-                  h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
+                  h->d2_sums, h->d_dprog, h->pmatsT, h->dpmatsT, h->d2pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
                   h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -3002,8 +3004,25 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
     }
     if (ops.size() > first) levels.push_back(std::make_pair(first, (int)(ops.size() - first)));
   }
-  const int n_blk = (int)(h->n_pad / kDrThreads);
+  const bool mfma = h->S == 20 || h->S == 64;
+  const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
+  const int n_blk = (int)(h->n_pad / (mfma ? 64 : kDrThreads));
   int rc;
+  if (mfma) {
+    // the sons' dP^T and d2P^T (P^T: ensure_pmatsT) for the matrix-core reduction
+    const size_t bytes = (size_t)nn * C * h->S * h->S * sizeof(double);
+    if (!h->dpmatsT && (rc = dalloc(h, (void**)&h->dpmatsT, bytes))) return rc;
+    if (!h->d2pmatsT && (rc = dalloc(h, (void**)&h->d2pmatsT, bytes))) return rc;
+    const dim3 tg((unsigned)nn, (unsigned)C);
+    if (h->S == 20) {
+      transpose_pmats<20><<<tg, 256, 0, h->stream>>>(h->dpmats, h->dpmatsT, C);
+      transpose_pmats<20><<<tg, 256, 0, h->stream>>>(h->d2pmats, h->d2pmatsT, C);
+    } else {
+      transpose_pmats<64><<<tg, 256, 0, h->stream>>>(h->dpmats, h->dpmatsT, C);
+      transpose_pmats<64><<<tg, 256, 0, h->stream>>>(h->d2pmats, h->d2pmatsT, C);
+    }
+    HIPCHK(h, hipGetLastError());
+  }
   if ((rc = ensure_cap(h, (void**)&h->d_drb, &h->d_drb_cap, br.size() * sizeof(DrBranch)))) return rc;
   if ((rc = ensure_cap(h, (void**)&h->d_drpre, &h->d_drpre_cap, ops.size() * sizeof(DrPreOp)))) return rc;
   if ((rc = ensure_cap(h, (void**)&h->dr_blk, &h->dr_blk_cap, 2 * br.size() * n_blk * sizeof(double)))) return rc;
@@ -3031,6 +3050,7 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
   a.n_patterns = h->n_patterns;
   a.C = C;
   a.n_blk = n_blk;
+  a.uout = h->partials;
   EventPair ev;
   if (h->timing & PLK_TIME_PARTIALS) {
     ev = get_events(h, 0);
@@ -3039,10 +3059,37 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
   for (const auto& l : levels) {
     const dim3 grid((unsigned)n_blk, (unsigned)l.second);
     const DrPreOp* o = h->d_drpre + l.first;
-    switch (C) {
-      case 1: dr_pre_s4_kernel<1><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
-      case 2: dr_pre_s4_kernel<2><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
-      case 4: dr_pre_s4_kernel<4><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+    if (mfma) {
+      const double *pT = h->pmatsT, *dT = h->dpmatsT, *d2T = h->d2pmatsT;
+#define PLK_DRM(S_, C_)                                                                           \
+  (sc ? dr_pre_m_kernel<S_, C_, true><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T)            \
+      : dr_pre_m_kernel<S_, C_, false><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T))
+      if (h->S == 20) {
+        switch (C) {
+          case 1: PLK_DRM(20, 1); break;
+          case 2: PLK_DRM(20, 2); break;
+          case 4: PLK_DRM(20, 4); break;
+        }
+      } else {
+        switch (C) {
+          case 1: PLK_DRM(64, 1); break;
+          case 2: PLK_DRM(64, 2); break;
+          case 4: PLK_DRM(64, 4); break;
+        }
+      }
+#undef PLK_DRM
+    } else if (sc) {
+      switch (C) {
+        case 1: dr_pre_s4_kernel<1, true><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+        case 2: dr_pre_s4_kernel<2, true><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+        case 4: dr_pre_s4_kernel<4, true><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+      }
+    } else {
+      switch (C) {
+        case 1: dr_pre_s4_kernel<1><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+        case 2: dr_pre_s4_kernel<2><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+        case 4: dr_pre_s4_kernel<4><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
+      }
     }
     HIPCHK(h, hipGetLastError());
   }
@@ -3104,10 +3151,10 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   }
   if ((rc = refresh_tip_tables(h))) return rc;
   if ((S == 20 || S == 64) && (rc = ensure_pmatsT(h))) return rc;
-  // 4 states without rescaling: the fused preorder (dr_pre_s4_kernel), one launch per
-  // level of fathers, branch terms reduced where U is formed (PLK_DR_PRE=0: the
-  // levelwise preorder + reduction below)
-  bool pre = S == 4 && !(h->flags & PLK_FLAG_SCALING) && (C == 1 || C == 2 || C == 4) && !tune_is("DR_PRE", '0');
+  // 4, 20 and 64 states (1, 2 or 4 classes, any rescaling): the fused preorder
+  // (dr_pre_s4_kernel / dr_pre_m_kernel), one launch per level of fathers, branch terms
+  // reduced where U is formed (DR_PRE=0: the levelwise preorder + reduction below)
+  bool pre = (S == 4 || S == 20 || S == 64) && (C == 1 || C == 2 || C == 4) && !tune_is("DR_PRE", '0');
   for (size_t d = 0; pre && d < depth.size(); ++d)
     for (int f : depth[d])
       if (f >= nt && (h->topo_kids[f].size() < 2 || h->topo_kids[f].size() > 3)) pre = false;

@@ -80,6 +80,7 @@ struct DrArgs {
   const double* tipP;         // [n_tips][C][n_codes][S] (fused tips' siblings)
   double* blk1;               // [branch][n_blk] block sums of w l'/l
   double* blk2;               // [branch][n_blk] block sums of w (l''/l - (l'/l)^2)
+  double* uout;               // partial slots receiving U (fused preorder)
   int64_t slot_stride;
   int64_t n_pad;
   int64_t n_patterns;
@@ -381,7 +382,11 @@ struct DrPreOp {      // (field order is read as 18 int32 by dr_pre_s4_kernel)
 // scalar loads into SGPRs -- through plain pointers the U stores would make every later
 // matrix read a per-lane vector load, as the compiler cannot rule out aliasing)
 typedef __attribute__((address_space(4))) const double* DrCPd;
-template <int C>
+// With rescaling (SCALE) the stored U of an internal son is rescaled jointly over its
+// states and classes (x 2^256 when that maximum is below 2^-256, the traversal's rule)
+// after the class loop, in place: the lane rewrites its own stores.  The branch terms need
+// no scale bookkeeping: l, l', l'' share U's and L's factors, and only their ratios enter.
+template <int C, bool SCALE = false>
 // (part / uout: the partial slots read (L, U_f) and written (U of internal sons) -- never
 // the same slot within a launch, so both are restrict and the next class's loads may be
 // scheduled above this class's stores)
@@ -408,6 +413,7 @@ __global__ __launch_bounds__(kDrThreads) void dr_pre_s4_kernel(const DrPreOp* __
   const bool live = p < a.n_patterns;
   const int64_t tile = p >> 7, q = p & (kTile - 1);
   double l0[3] = {0.0, 0.0, 0.0}, l1[3] = {0.0, 0.0, 0.0}, l2[3] = {0.0, 0.0, 0.0};
+  double umax[3] = {0.0, 0.0, 0.0};  // SCALE: joint max of each stored U
   // operand sources per son: a tip's code-table row (the same for every class) or the
   // internal son's partial; a missing third son aliases son 0 (loaded, never used).  The
   // next class's operands are loaded before this class's arithmetic and stores.
@@ -488,6 +494,9 @@ __global__ __launch_bounds__(kDrThreads) void dr_pre_s4_kernel(const DrPreOp* __
         double* dst = uout + (int64_t)op.uslot[i] * a.slot_stride + co;
 #pragma unroll
         for (int x = 0; x < S; ++x) dst[(int64_t)x * kTile] = u[x];
+        if (SCALE)
+#pragma unroll
+          for (int x = 0; x < S; ++x) umax[i] = fmax(umax[i], u[x]);
       }
       const DrCPd D1 = (DrCPd)(a.dpmats + ((int64_t)op.son[i] * C + c) * S * S);
       const DrCPd D2 = (DrCPd)(a.d2pmats + ((int64_t)op.son[i] * C + c) * S * S);
@@ -510,6 +519,14 @@ __global__ __launch_bounds__(kDrThreads) void dr_pre_s4_kernel(const DrPreOp* __
       l2[i] = fma(pc, s2, l2[i]);
     }
   }
+  if (SCALE)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (i < op.n && op.uslot[i] >= 0 && umax[i] > 0.0 && umax[i] < kScaleThr) {
+        double* dst = uout + (int64_t)op.uslot[i] * a.slot_stride + tb;
+#pragma unroll
+        for (int e = 0; e < C * S; ++e) dst[(int64_t)e * kTile] *= kScaleUp;
+      }
   const int wv = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -535,6 +552,180 @@ __global__ __launch_bounds__(kDrThreads) void dr_pre_s4_kernel(const DrPreOp* __
     const int i = threadIdx.x;
     double t1 = 0.0, t2 = 0.0;
     for (int k = 0; k < kDrThreads / 64; ++k) {  // fixed order
+      t1 += red[0][i][k];
+      t2 += red[1][i][k];
+    }
+    a.blk1[(size_t)op.bidx[i] * a.n_blk + blockIdx.x] = t1;
+    a.blk2[(size_t)op.bidx[i] * a.n_blk + blockIdx.x] = t2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused preorder for 20 and 64 states (any rescaling): the same per-father op as
+// dr_pre_s4_kernel on fp64 matrix cores, in treeM's v_mfma_f64_16x16x4 layout (a wave owns
+// 16 patterns; lane l holds states 16 xt + (l >> 4) + 4 r of pattern l & 15).  Per class
+//     MU = pi (f the root) or P_f^T U_f,   Q_j = P_j L_j,
+//     U_i = MU (*) prod_{j != i} Q_j   (stored for internal sons),
+//     l += p_c U_i . Q_i,  l' += p_c U_i . (dP_i L_i),  l'' += p_c U_i . (d2P_i L_i),
+// every product a matvec_m whose A operands (the applied matrix, transposed: P_f itself
+// for P_f^T, and P^T, dP^T, d2P^T of the sons) are read from L1/L2 -- the workgroup's four
+// waves share them.  Stored U is rescaled jointly over states and classes after the class
+// loop (in place, as dr_pre_s4_kernel<C, true>).  64-pattern blocks.
+// ---------------------------------------------------------------------------
+template <int S, int C, bool SCALE>
+__global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict__ ops, DrArgs a,
+                                                       const double* __restrict__ pT,
+                                                       const double* __restrict__ dpT,
+                                                       const double* __restrict__ d2pT) {
+  constexpr int XT = MShape<S>::XT, CS = C * S;
+  __shared__ double red[2][3][4];
+  const DrPreOp op = ops[blockIdx.y];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lr = lane >> 4, lc = lane & 15;
+  const int64_t p = (int64_t)blockIdx.x * 64 + 16 * w + lc;
+  const bool live = p < a.n_patterns;
+  const int64_t tile = p >> 7, q = p & (kTile - 1);
+  const int64_t tb = tile * CS * kTile + q;
+  const bool root = op.uf_slot < 0;
+  const size_t SS = (size_t)S * S;
+  double l0[3] = {0.0, 0.0, 0.0}, l1[3] = {0.0, 0.0, 0.0}, l2[3] = {0.0, 0.0, 0.0};
+  double umax[3] = {0.0, 0.0, 0.0};
+  // the son's L of class c in the MFMA layout (padding rows 0)
+  auto loadL = [&](int j, int c, MAcc<S>& v) {
+    if (op.is_tip[j]) {
+      const double* row = a.code_table + (int64_t)a.codes[(int64_t)op.idx[j] * a.n_pad + p] * S;
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[xt][r] = m_valid<S>(xt, r, lr) ? row[16 * xt + lr + 4 * r] : 0.0;
+    } else {
+      const double* L = a.partials + (int64_t)op.idx[j] * a.slot_stride + tb + (int64_t)c * S * kTile;
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[xt][r] = m_valid<S>(xt, r, lr) ? L[(int64_t)(16 * xt + lr + 4 * r) * kTile] : 0.0;
+    }
+  };
+  auto dot = [&](const MAcc<S>& u, const f64x4m (&t)[XT]) {
+    double s = 0.0;
+#pragma unroll
+    for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s = fma(u[xt][r], t[xt][r], s);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    return s;
+  };
+#pragma unroll 1
+  for (int c = 0; c < C; ++c) {
+    MAcc<S> mu;
+    if (root) {
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mu[xt][r] = m_valid<S>(xt, r, lr) ? a.pi[16 * xt + lr + 4 * r] : 0.0;
+    } else {
+      MAcc<S> uf;
+      const double* U = a.partials + (int64_t)op.uf_slot * a.slot_stride + tb + (int64_t)c * S * kTile;
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          uf[xt][r] = m_valid<S>(xt, r, lr) ? U[(int64_t)(16 * xt + lr + 4 * r) * kTile] : 0.0;
+      f64x4m d[XT];
+      matvec_m<S>(d, uf, a.pmats + ((size_t)op.f * C + c) * SS, lr, lc);  // (P_f^T)^T = P_f
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt) mu[xt] = d[xt];
+    }
+    MAcc<S> Q[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j >= op.n) continue;
+      MAcc<S> L;
+      loadL(j, c, L);
+      f64x4m d[XT];
+      matvec_m<S>(d, L, pT + ((size_t)op.son[j] * C + c) * SS, lr, lc);
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt) Q[j][xt] = d[xt];
+    }
+    const double pc = a.probs[c];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i >= op.n) continue;
+      MAcc<S> u;
+#pragma unroll
+      for (int xt = 0; xt < XT; ++xt) {
+        u[xt] = mu[xt];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          if (j != i && j < op.n) u[xt] *= Q[j][xt];
+      }
+      if (op.uslot[i] >= 0) {
+        double* dst = a.uout + (int64_t)op.uslot[i] * a.slot_stride + tb + (int64_t)c * S * kTile;
+#pragma unroll
+        for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (m_valid<S>(xt, r, lr)) {
+              dst[(int64_t)(16 * xt + lr + 4 * r) * kTile] = u[xt][r];
+              if (SCALE) umax[i] = fmax(umax[i], u[xt][r]);
+            }
+      }
+      const double s0 = dot(u, Q[i]);
+      MAcc<S> L;
+      loadL(i, c, L);
+      f64x4m t[XT];
+      matvec_m<S>(t, L, dpT + ((size_t)op.son[i] * C + c) * SS, lr, lc);
+      const double s1 = dot(u, t);
+      matvec_m<S>(t, L, d2pT + ((size_t)op.son[i] * C + c) * SS, lr, lc);
+      const double s2 = dot(u, t);
+      l0[i] = fma(pc, s0, l0[i]);
+      l1[i] = fma(pc, s1, l1[i]);
+      l2[i] = fma(pc, s2, l2[i]);
+    }
+  }
+  if (SCALE)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i >= op.n || op.uslot[i] < 0) continue;
+      double m = umax[i];
+      m = fmax(m, __shfl_xor(m, 16, 64));
+      m = fmax(m, __shfl_xor(m, 32, 64));
+      if (m > 0.0 && m < kScaleThr) {
+        double* dst = a.uout + (int64_t)op.uslot[i] * a.slot_stride + tb;
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int xt = 0; xt < XT; ++xt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (m_valid<S>(xt, r, lr)) dst[(int64_t)(c * S + 16 * xt + lr + 4 * r) * kTile] *= kScaleUp;
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (i >= op.n) continue;
+    double r1 = 0.0, r2 = 0.0;
+    if (live && lr == 0) {
+      const double g = l1[i] / l0[i], hh = l2[i] / l0[i];
+      r1 = a.weights[p] * g;
+      r2 = a.weights[p] * (hh - g * g);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      r1 += __shfl_xor(r1, off, 64);
+      r2 += __shfl_xor(r2, off, 64);
+    }
+    if (lane == 0) {
+      red[0][i][w] = r1;
+      red[1][i][w] = r2;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 && (int)threadIdx.x < op.n) {
+    const int i = threadIdx.x;
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < 4; ++k) {  // fixed order
       t1 += red[0][i][k];
       t2 += red[1][i][k];
     }

@@ -7,7 +7,9 @@
 #include <iostream>
 #include <limits>
 #include <memory>
+#include <algorithm>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../Exceptions.h"
@@ -81,59 +83,82 @@ class Parameter {
   void setConstraint(std::shared_ptr<Constraint> c) { constraint_ = c; }
 };
 
+// An ordered list of parameters.  Name lookups go through a name -> position index that
+// is rebuilt lazily whenever the list changed (or a parameter was renamed through
+// operator[]), so the optimisers' per-evaluation setParameters of every parameter costs
+// O(n), not O(n^2) string comparisons.
 class ParameterList {
   std::vector<Parameter> params_;
+  mutable std::unordered_map<std::string, size_t> index_;
+  mutable bool indexValid_ = false;
+
+  long find(const std::string& name) const {
+    if (!indexValid_ || index_.size() != params_.size()) rebuild();
+    auto it = index_.find(name);
+    if (it == index_.end()) return -1;
+    if (params_[it->second].getName() != name) {  // renamed through operator[]
+      rebuild();
+      it = index_.find(name);
+      return it == index_.end() ? -1 : (long)it->second;
+    }
+    return (long)it->second;
+  }
+  void rebuild() const {
+    index_.clear();
+    for (size_t i = 0; i < params_.size(); i++) index_.emplace(params_[i].getName(), i);  // first wins
+    indexValid_ = true;
+  }
 
  public:
   size_t size() const { return params_.size(); }
   const Parameter& operator[](size_t i) const { return params_[i]; }
-  Parameter& operator[](size_t i) { return params_[i]; }
+  Parameter& operator[](size_t i) {
+    indexValid_ = false;  // the caller may rename it
+    return params_[i];
+  }
   std::vector<std::string> getParameterNames() const {
     std::vector<std::string> v;
     for (auto& p : params_) v.push_back(p.getName());
     return v;
   }
-  bool hasParameter(const std::string& name) const {
-    for (auto& p : params_)
-      if (p.getName() == name) return true;
-    return false;
-  }
+  bool hasParameter(const std::string& name) const { return find(name) >= 0; }
   size_t whichParameterHasName(const std::string& name) const {
-    for (size_t i = 0; i < params_.size(); i++)
-      if (params_[i].getName() == name) return i;
-    throw ParameterNotFoundException("ParameterList::whichParameterHasName", name);
+    const long i = find(name);
+    if (i < 0) throw ParameterNotFoundException("ParameterList::whichParameterHasName", name);
+    return (size_t)i;
   }
   const Parameter& getParameter(const std::string& name) const { return params_[whichParameterHasName(name)]; }
   double getParameterValue(const std::string& name) const { return getParameter(name).getValue(); }
   void addParameter(const Parameter& p) {
     if (hasParameter(p.getName())) throw Exception("ParameterList::addParameter: duplicate " + p.getName());
     params_.push_back(p);
+    index_.emplace(p.getName(), params_.size() - 1);
   }
   void addParameters(const ParameterList& pl) {
     for (size_t i = 0; i < pl.size(); i++) addParameter(pl[i]);
   }
   void includeParameters(const ParameterList& pl) {
     for (size_t i = 0; i < pl.size(); i++) {
-      if (hasParameter(pl[i].getName()))
-        params_[whichParameterHasName(pl[i].getName())].setValue(pl[i].getValue());
+      const long k = find(pl[i].getName());
+      if (k >= 0)
+        params_[(size_t)k].setValue(pl[i].getValue());
       else
-        params_.push_back(pl[i]);
+        addParameter(pl[i]);
     }
   }
   void setParameterValue(const std::string& name, double v) { params_[whichParameterHasName(name)].setValue(v); }
   // Update values of parameters present in both lists; returns true if any changed.
   bool matchParametersValues(const ParameterList& pl, std::vector<size_t>* changed = nullptr) {
     bool any = false;
-    for (size_t i = 0; i < params_.size(); i++) {
-      for (size_t j = 0; j < pl.size(); j++) {
-        if (pl[j].getName() == params_[i].getName()) {
-          if (params_[i].getValue() != pl[j].getValue()) {
-            params_[i].setValue(pl[j].getValue());
-            any = true;
-            if (changed) changed->push_back(i);
-          }
-          break;
-        }
+    for (size_t j = 0; j < pl.size(); j++) {
+      const long i = find(pl[j].getName());
+      if (i < 0) continue;
+      Parameter& p = params_[(size_t)i];
+      if (p.getValue() != pl[j].getValue()) {
+        p.setValue(pl[j].getValue());
+        any = true;
+        if (changed && std::find(changed->begin(), changed->end(), (size_t)i) == changed->end())
+          changed->push_back((size_t)i);
       }
     }
     return any;
@@ -141,7 +166,7 @@ class ParameterList {
   ParameterList getCommonParametersWith(const ParameterList& pl) const {
     ParameterList out;
     for (auto& p : params_)
-      if (pl.hasParameter(p.getName())) out.params_.push_back(p);
+      if (pl.hasParameter(p.getName())) out.addParameter(p);
     return out;
   }
   ParameterList createSubList(const std::vector<std::string>& names) const {
@@ -149,8 +174,15 @@ class ParameterList {
     for (auto& n : names) out.params_.push_back(getParameter(n));
     return out;
   }
-  void deleteParameter(const std::string& name) { params_.erase(params_.begin() + whichParameterHasName(name)); }
-  void reset() { params_.clear(); }
+  void deleteParameter(const std::string& name) {
+    params_.erase(params_.begin() + whichParameterHasName(name));
+    indexValid_ = false;
+  }
+  void reset() {
+    params_.clear();
+    index_.clear();
+    indexValid_ = true;
+  }
   void printParameters(std::ostream& out) const {
     for (auto& p : params_) out << p.getName() << "=" << p.getValue() << std::endl;
   }

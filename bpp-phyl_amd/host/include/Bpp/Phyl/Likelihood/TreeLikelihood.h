@@ -100,6 +100,7 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   double minimumBrLen_ = 0.000001, maximumBrLen_ = 10000.;
   std::shared_ptr<IntervalConstraint> brLenConstraint_;
   ParameterList brLenParameters_;
+  std::vector<std::string> brLenNames_;      // "BrLen<i>" of nodes_[i]
   mutable double minusLogLik_ = -1.;
   mutable std::vector<double> siteLnl_;      // per pattern (fetched lazily)
   mutable bool siteLnlValid_ = false;

@@ -213,8 +213,12 @@ void AbstractPlkTreeLikelihood::initBranchLengthsParameters() {
 
 std::vector<const Node*> AbstractPlkTreeLikelihood::applyBranchLengths() {
   std::vector<const Node*> changed;
+  if (brLenNames_.size() != nodes_.size()) {
+    brLenNames_.clear();
+    for (size_t i = 0; i < nodes_.size(); i++) brLenNames_.push_back("BrLen" + std::to_string(i));
+  }
   for (size_t i = 0; i < nodes_.size(); i++) {
-    const std::string n = "BrLen" + std::to_string(i);
+    const std::string& n = brLenNames_[i];
     if (!parameters_.hasParameter(n)) continue;
     const double v = parameters_.getParameterValue(n);
     if (!nodes_[i]->hasDistanceToFather() || nodes_[i]->getDistanceToFather() != v) {

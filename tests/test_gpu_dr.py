@@ -254,3 +254,47 @@ def test_dr_fused_preorder_equals_levelwise(C, n_taxa, n_pat, amb, monkeypatch):
     for v in br:
         assert _close(a1[v], b1[v], 1e-12), (v, a1[v], b1[v])
         assert _close(a2[v], b2[v], 1e-12), (v, a2[v], b2[v])
+
+
+@pytest.mark.parametrize("S,C,tree_kind,n_pat,scaling", [
+    (20, 4, "balanced40", 500, True), (20, 2, "balanced24", 333, False), (20, 1, "caterpillar120long", 300, True),
+    (64, 1, "balanced24", 300, False), (64, 2, "balanced16", 130, True), (64, 1, "caterpillar60long", 200, True),
+    (4, 4, "caterpillar300long", 600, True), (4, 2, "balanced64", 2000, True)])
+def test_dr_fused_preorder_any_state_count(S, C, tree_kind, n_pat, scaling, monkeypatch):
+    """The fused preorder beyond unscaled DNA: dr_pre_m_kernel (20 / 64 states on fp64
+    matrix cores) and dr_pre_s4_kernel<C, true> (4 states with rescaling; stored upper
+    vectors rescaled jointly over states and classes) against the levelwise preorder +
+    reduction (DR_PRE=0) at 1e-11 and against the path derivatives at 1e-10 (1e-9 through
+    deep rescaling).  "long" caterpillars drive partials and upper vectors below 2^-256."""
+    rng = np.random.default_rng(S * 7 + C + n_pat)
+    if tree_kind.startswith("balanced"):
+        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=S + C, lo=0.05, hi=0.4)
+    else:
+        tree = _caterpillar(int(tree_kind[11:-4]), seed=3, lo=0.1, hi=0.5)
+    et = phylo.engine_tree(tree)
+    if S == 4:
+        m, alph = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5)), phylo.DNA
+    elif S == 20:
+        m, alph = phylo.lg08(), phylo.PROTEIN
+    else:
+        m, alph = phylo.yn98(2.0, 0.3), phylo.CODON
+    rates, probs = phylo.gamma_rates(C, 0.6) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("d", et, [m], None, rates, probs, m.pi, alph, n_pat, scaling, True, 4)
+    states = wl.simulate(0, n_pat).astype(np.int32)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | DR | (plk.PLK_FLAG_SCALING if scaling else 0)
+    out = {}
+    for pre in ("0", "1"):
+        set_tune(monkeypatch, "DR_PRE", pre)
+        eng = engine_for(et, S, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+        eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+        _, site, _ = run_engine(eng, et)
+        if tree_kind.endswith("long"):
+            assert site.min() < -256 * np.log(2)
+        out[pre] = _dr_vs_path(eng, et, rel=1e-9 if tree_kind.endswith("long") else 1e-10) if pre == "1" \
+            else eng.all_branch_derivatives()
+        del eng
+    (a1, a2), (b1, b2) = out["0"], out["1"]
+    for v in br:
+        assert _close(a1[v], b1[v], 1e-11), (v, a1[v], b1[v])
+        assert _close(a2[v], b2[v], 1e-11), (v, a2[v], b2[v])

@@ -6,7 +6,8 @@ what RHomogeneousTreeLikelihood does per BrLen parameter).
 
 One JSON line: branch x pattern derivative updates/s for both, the DR kernels' HIP-event
 duration and their algorithmic HBM rate.  Two engine paths (`dr_path`):
-  * fused (4 states without rescaling, dr_pre_s4_kernel): per father f, U_f read (8 C S,
+  * fused (4 states: dr_pre_s4_kernel; 20 / 64 states: dr_pre_m_kernel on matrix cores;
+    with or without rescaling): per father f, U_f read (8 C S,
     not at the root), every son's L (8 C S internal, 1 B tip), the U of internal sons
     written (8 C S), the weight (8 B);
   * levelwise (otherwise, or PLK_TUNE=DR_PRE=0): every upper vector U_v written once (8 C S)
@@ -51,6 +52,16 @@ def dr_fused_bytes(wl):
     return b
 
 
+def dr_fused_flops(wl):
+    """Contractions of the fused preorder: per father and class, P_f^T U_f (not at the
+    root) and, per son, P L, dP L and d2P L -- 2 S^2 flops each."""
+    et = wl.et
+    n = 0
+    for f, ch in et.ops:
+        n += (1 if f != et.root else 0) + 3 * len(ch)
+    return n * wl.C * 2 * wl.S * wl.S
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="gtr_g4_dna_1M_64")
@@ -86,7 +97,7 @@ def main():
         worst = max(worst, abs(p1 - d1[b]) / max(1.0, abs(p1)), abs(p2 - d2[b]) / max(1.0, abs(p2)))
     t_path = (time.perf_counter() - t0) / len(sel) * nb
     up, red = dr_bytes(wl)
-    fused = wl.S == 4 and not wl.scaling and "DR_PRE=0" not in os.environ.get("PLK_TUNE", "")
+    fused = wl.S in (4, 20, 64) and wl.C in (1, 2, 4) and "DR_PRE=0" not in os.environ.get("PLK_TUNE", "")
     fb = dr_fused_bytes(wl)
     rec = {
         "metric": "branch x site-pattern derivative updates/s (d1 and d2 of every branch)",
@@ -100,6 +111,13 @@ def main():
     }
     if fused:
         rec["fused_kernels_ms"] = red_ms
+        fl = dr_fused_flops(wl)
+        rec["fused_flop_roofline"] = {"bound": "mfma" if wl.S > 4 else "valu", "achieved": fl * P / (red_ms * 1e-3) / 1e12,
+                                      "peak": 78.6, "unit": "TFLOP/s",
+                                      "frac": fl * P / (red_ms * 1e-3) / 1e12 / 78.6,
+                                      "algorithmic_flops_per_pattern": fl,
+                                      "basis": "per father and class: 2 S^2 per contraction (P_f^T U_f below the root, "
+                                               "P_j L_j, dP_i L_i, d2P_i L_i of every son)"}
         rec["fused_roofline"] = {"bound": "hbm", "achieved": fb * P / (red_ms * 1e-3) / 1e9, "peak": 8000.0,
                                  "unit": "GB/s", "frac": fb * P / (red_ms * 1e-3) / 1e9 / 8000.0,
                                  "algorithmic_bytes_per_pattern": fb}
