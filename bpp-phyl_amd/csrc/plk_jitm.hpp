@@ -16,12 +16,14 @@
 // register is exactly the B operand of y-block Y = X of the parent's contraction, so a
 // child feeds its parent straight from registers.  The A operand of block (X, Y) is
 // P[4X + lo][4Y + hi] -- pattern-independent, one 16-double tile per (class, X, Y) in LDS,
-// read with ds_read_b64 at a constant offset (the 4 blocks of a lane group broadcast).
-// Inside a tile the element (hi, lo) sits at 4 hi + ((lo + Y) & 3): the staging stores
-// (ds_write_b64, 16-lane groups, bank (a/4) mod 32) write 16 consecutive y of one x row,
-// which the plain 4 hi + lo image put on 4 bank pairs (4-way conflicts, ~1 extra LDS
-// cycle per LDS instruction of the kernel); rotated by Y they land on 16 distinct pairs,
-// and each A read still covers 8 distinct doubles per 32-lane group (conflict-free).
+// read with ds_read_b64 at a constant offset from one lane base (the 4 blocks of a lane
+// group broadcast).  P(t) is staged in LDS as stored, [c][x][y]: lane (hi, lo) reads row
+// 4X + lo, column 4Y + hi, so a 32-lane group reads rows lo = 0..3 at columns hi = 0, 1 --
+// 8 distinct doubles on 8 distinct bank pairs (conflict-free) -- and the staging is a
+// plain copy whose ds_write_b64 groups store 16 consecutive doubles (conflict-free).  The
+// round-2 16-double tile image [c][X][Y][hi][lo] made those stores 4-way conflicts
+// (~1 extra LDS cycle per LDS instruction of the kernel); JITM_IMG=1 / 2 keep it (and a
+// rotated variant) for A/B.
 //
 // All classes in one wave: the joint (all states, all classes) exact power-of-two
 // rescale of the other kernels is an in-register max plus two shuffles -- no LDS exchange
@@ -112,12 +114,15 @@ struct JitMShape {
   int minw = 2;      // __launch_bounds__ min waves per SIMD
   int pd = 1;        // P(t) staging prefetch distance (contractions ahead)
   int G = 4;         // waves (16-pattern groups) per workgroup: 64 patterns (4) or 128 (8)
-  bool swz = true;   // tile image rotated per Y block (conflict-free staging stores)
+  // LDS image of a staged P(t): 0 = as stored, [c][x][y] (staging is a plain copy; the A
+  // read of block (X, Y) is row 4X + lo, column 4Y + hi from one lane base), 1 = 16-double
+  // tiles [c][X][Y][hi][lo], 2 = tiles rotated per Y block
+  int img = 0;
   int pb() const { return C * S * S; }  // doubles of P(t) per branch (every class)
   size_t lds_bytes() const { return (size_t)(2 * pb() + 16 * G) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
     return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && pd == o.pd &&
-           G == o.G && swz == o.swz;
+           G == o.G && img == o.img;
   }
 };
 
@@ -133,8 +138,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const int NTH = 64 * sh.G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH;
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
-           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n#define SWZ_ %d\n",
-           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PF, sh.scale ? "true" : "false", sh.swz ? 1 : 0);
+           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n#define IMG_ %d\n",
+           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PF, sh.scale ? "true" : "false", sh.img);
   s += buf;
   s += R"PLKJITM(
 // P(t) of branch b (all classes, [c][x][y]) -> registers -> the LDS tile image
@@ -142,14 +147,17 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
 #define PSTAGE_LOAD(R, b) { const double* s_ = a.pmats + (i64)(b) * PB_; \
   _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) { const int e_ = tid + j_ * NTH_; R[j_] = s_[e_ < PB_ ? e_ : PB_ - 1]; } }
 #define PSTAGE_STORE(R, bf) { double* d_ = lds + (bf) * PB_; \
-  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) if (sidx[j_] >= 0) d_[sidx[j_]] = R[j_]; }
+  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) { \
+    if (IMG_ == 0) { const int e_ = tid + j_ * NTH_; if (PB_ % NTH_ == 0 || e_ < PB_) d_[e_] = R[j_]; } \
+    else if (sidx[j_] >= 0) d_[sidx[j_]] = R[j_]; } }
 // D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1); the A read of tile (c, X, Y)
 // goes through the lane base of rotation Y & 3
 #define CONTRIB(D, SRC, bf, SET) { \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
     double d_ = 0.0; \
     _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) \
-      d_ = mfma4(PA[Y_ & 3][(bf) * PB_ + ((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
+      d_ = mfma4(IMG_ == 0 ? PA[0][(bf) * PB_ + (c_ * S_ + 4 * X_) * S_ + 4 * Y_] \
+                           : PA[Y_ & 3][(bf) * PB_ + ((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
     if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } }
 #define ROWMUL(D, F, SET) { _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") \
   for (int X_ = 0; X_ < XB_; ++X_) { if (SET) D[c_][X_] = F[c_][X_]; else D[c_][X_] *= F[c_][X_]; } }
@@ -221,12 +229,13 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   // A-operand lane bases, one per tile rotation Y & 3 (lane 16 hi + 4 b + lo reads tile
   // element (hi, lo))
   const double* PA[4];
-  _Pragma("unroll") for (int k = 0; k < 4; ++k) PA[k] = lds + ((hi << 2) | (((lane & 3) + (SWZ_ ? k : 0)) & 3));
+  _Pragma("unroll") for (int k = 0; k < 4; ++k)
+    PA[k] = IMG_ == 0 ? lds + (lane & 3) * S_ + hi : lds + ((hi << 2) | (((lane & 3) + (IMG_ == 2 ? k : 0)) & 3));
   int sidx[PF_];   // this thread's staging elements -> tile slots (-1: past the table)
   _Pragma("unroll") for (int j = 0; j < PF_; ++j) {
     const int e = tid + j * NTH_;
     const int c = e / (S_ * S_), r = e - c * (S_ * S_), x = r / S_, y = r - x * S_;
-    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (((x & 3) + (SWZ_ ? (y >> 2) : 0)) & 3) : -1;
+    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (((x & 3) + (IMG_ == 2 ? (y >> 2) : 0)) & 3) : -1;
   }
   double R0[PF_] = {}, R1[PF_] = {}, R2[PF_] = {};
   (void)red; (void)PA; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
