@@ -76,11 +76,124 @@ struct PNParam {
 // non-derivable parameters a ThreePointsNumericalDerivative of interval 1e-4 (:311-314,
 // 330-331).  Each step moves every parameter by d1 / |d2| at once (0 if d2 == 0 or the move
 // is NaN), clamped into its constraint; while f grows by more than the tolerance (or is NaN)
-// the Felsenstein-Churchill correction halves all moves, at most 10 times; a step that cannot
-// improve keeps the point.  Stop: |f_new - f_old| < tolerance (FunctionStopCondition) or the
-// evaluation budget.  Deviation: the reference swaps the fourth correction for a
-// conjugate-gradient search (useCG_, :151-170); here the halving continues.
-// f(x) sets every parameter and returns -lnL; evaluations are counted in *nEval.
+// the Felsenstein-Churchill correction halves all moves, at most 10 times, the fourth
+// correction being a conjugate-gradient search from the current point (useCG_, :151-170);
+// a step that cannot improve keeps the point.  Stop: |f_new - f_old| < tolerance
+// (FunctionStopCondition) or the evaluation budget.  f(x) sets every parameter and returns
+// -lnL; evaluations are counted in *nEval.
+// First derivatives at x (the likelihood sits at x on entry and on return): analytic for the
+// derivable parameters, ThreePointsNumericalDerivative (interval 1e-4, one-sided at a
+// constraint) for the others; d2 alike when asked for.
+struct Derivatives {
+  const std::vector<PNParam>& par;
+  const std::function<double(const std::vector<double>&)>& eval;
+  const std::function<void(size_t, double*, double*)>& analytic;
+  void operator()(const std::vector<double>& x, double fx, std::vector<double>& d1, std::vector<double>* d2) const {
+    const size_t n = par.size();
+    const double kInterval = 0.0001;
+    std::vector<double> y(n);
+    bool moved_away = false;
+    for (size_t i = 0; i < n; i++) {
+      double a1 = 0., a2 = 0.;
+      if (par[i].analytic) {
+        if (moved_away) {
+          eval(x);
+          moved_away = false;
+        }
+        analytic(i, &a1, &a2);
+      } else {
+        const double v = x[i], h = (1. + std::fabs(v)) * kInterval;
+        y = x;
+        double fm, fp, f2;
+        if (par[i].correct(v - h) && par[i].correct(v + h)) {
+          y[i] = v - h;
+          fm = eval(y);
+          y[i] = v + h;
+          fp = eval(y);
+          a1 = (fp - fm) / (2. * h);
+          a2 = (fp - 2. * fx + fm) / (h * h);
+        } else if (par[i].correct(v + 2. * h)) {  // left limit: forward
+          y[i] = v + h;
+          fp = eval(y);
+          y[i] = v + 2. * h;
+          f2 = eval(y);
+          a1 = (fp - fx) / h;
+          a2 = (f2 - 2. * fp + fx) / (h * h);
+        } else {  // right limit: backward
+          y[i] = v - h;
+          fm = eval(y);
+          y[i] = v - 2. * h;
+          f2 = eval(y);
+          a1 = (fx - fm) / h;
+          a2 = (fx - 2. * fm + f2) / (h * h);
+        }
+        moved_away = true;
+      }
+      d1[i] = a1;
+      if (d2) (*d2)[i] = a2;
+    }
+    if (moved_away) eval(x);
+  }
+};
+
+// bpp-core ConjugateGradientMultiDimensions as PseudoNewtonOptimizer uses it (Polak-Ribiere
+// directions, a Brent line minimisation along each, FunctionStopCondition |f - f_old| < tol),
+// from x / fx; the constraints bound every line search.  Returns the value at the new x.
+// *nEval is the caller's evaluation counter (eval counts).
+double conjugateGradient(const std::vector<PNParam>& par, std::vector<double>& x, double fx,
+                         const std::function<double(const std::vector<double>&)>& eval, const Derivatives& der,
+                         double tol, unsigned int maxEval, unsigned int* nEval) {
+  const size_t n = par.size();
+  std::vector<double> g(n), h(n), xi(n), y(n);
+  der(x, fx, xi, nullptr);
+  for (size_t j = 0; j < n; j++) g[j] = h[j] = xi[j] = -xi[j];
+  for (int it = 0; it < 200 && *nEval < maxEval; it++) {
+    // the largest step along xi that stays inside every constraint
+    double amax = std::numeric_limits<double>::infinity(), xn = 1., dn = 0.;
+    for (size_t j = 0; j < n; j++) {
+      xn = std::max(xn, std::fabs(x[j]));
+      dn = std::max(dn, std::fabs(xi[j]));
+      if (xi[j] == 0. || !par[j].constraint) continue;
+      const double lo = par[j].constraint->getLowerBound(), hi = par[j].constraint->getUpperBound();
+      const double lim = xi[j] > 0. ? (hi - x[j]) / xi[j] : (lo - x[j]) / xi[j];
+      if (std::isfinite(lim)) amax = std::min(amax, lim * (1. - 1e-9));
+    }
+    if (dn == 0.) break;
+    if (!std::isfinite(amax)) amax = 10. * xn / dn;
+    auto fl = [&](double a) {
+      for (size_t j = 0; j < n; j++) y[j] = par[j].accept(x[j] + a * xi[j]);
+      return eval(y);
+    };
+    double fmin = fx;
+    unsigned int ne = 0;
+    const double a = OptimizationTools::brent(fl, 0., std::max(amax, 0.), std::min(amax, 0.1 * xn / dn), 1e-6, 100,
+                                              &fmin, &ne);
+    const double fold = fx;
+    if (fmin < fx) {
+      for (size_t j = 0; j < n; j++) x[j] = par[j].accept(x[j] + a * xi[j]);
+      fx = eval(x);
+    } else {
+      eval(x);
+    }
+    if (std::fabs(fx - fold) < tol) break;
+    std::vector<double> gn(n);
+    der(x, fx, gn, nullptr);
+    double gg = 0., dgg = 0.;
+    for (size_t j = 0; j < n; j++) {
+      gg += g[j] * g[j];
+      dgg += (gn[j] + g[j]) * gn[j];  // Polak-Ribiere
+    }
+    if (gg == 0.) break;
+    const double gam = dgg / gg;
+    for (size_t j = 0; j < n; j++) {
+      g[j] = -gn[j];
+      h[j] = g[j] + gam * h[j];
+      xi[j] = h[j];
+    }
+  }
+  return fx;
+}
+
 unsigned int pseudoNewton(const std::vector<PNParam>& par, std::vector<double>& x,
                           const std::function<double(const std::vector<double>&)>& f,
                           const std::function<void(size_t, double*, double*)>& analytic, double tolerance,
@@ -88,55 +201,16 @@ unsigned int pseudoNewton(const std::vector<PNParam>& par, std::vector<double>& 
                           const std::function<void(unsigned int, const std::vector<double>&, double)>& onStep) {
   const size_t n = par.size();
   unsigned int nEval = 0, steps = 0;
-  auto eval = [&](const std::vector<double>& y) {
+  std::function<double(const std::vector<double>&)> eval = [&](const std::vector<double>& y) {
     nEval++;
     return f(y);
   };
-  double fcur = eval(x);
+  const Derivatives der{par, eval, analytic};
+  double fcur = eval(x), fprev = 0.;  // previousValue_ starts at 0 (PseudoNewtonOptimizer.cpp:72)
   std::vector<double> d1(n), d2(n), mv(n), y(n);
-  const double kInterval = 0.0001;
   while (nEval < maxEval) {
     steps++;
-    // derivatives at x (the likelihood sits at x)
-    bool moved_away = false;
-    for (size_t i = 0; i < n; i++) {
-      if (par[i].analytic) {
-        if (moved_away) {
-          eval(x);
-          moved_away = false;
-        }
-        analytic(i, &d1[i], &d2[i]);
-        continue;
-      }
-      // ThreePointsNumericalDerivative: central differences, one-sided at a constraint
-      const double v = x[i], h = (1. + std::fabs(v)) * kInterval;
-      y = x;
-      double fm, fp, f2;
-      if (par[i].correct(v - h) && par[i].correct(v + h)) {
-        y[i] = v - h;
-        fm = eval(y);
-        y[i] = v + h;
-        fp = eval(y);
-        d1[i] = (fp - fm) / (2. * h);
-        d2[i] = (fp - 2. * fcur + fm) / (h * h);
-      } else if (par[i].correct(v + 2. * h)) {  // left limit: forward
-        y[i] = v + h;
-        fp = eval(y);
-        y[i] = v + 2. * h;
-        f2 = eval(y);
-        d1[i] = (fp - fcur) / h;
-        d2[i] = (f2 - 2. * fp + fcur) / (h * h);
-      } else {  // right limit: backward
-        y[i] = v - h;
-        fm = eval(y);
-        y[i] = v - 2. * h;
-        f2 = eval(y);
-        d1[i] = (fcur - fm) / h;
-        d2[i] = (fcur - 2. * fm + f2) / (h * h);
-      }
-      moved_away = true;
-    }
-    if (moved_away) eval(x);
+    der(x, fcur, d1, &d2);  // derivatives at x (the likelihood sits at x)
     // Newton moves (PseudoNewtonOptimizer.cpp:108-135)
     for (size_t i = 0; i < n; i++) {
       double m = d2[i] == 0. ? 0. : (d2[i] < 0. ? -d1[i] / d2[i] : d1[i] / d2[i]);
@@ -145,8 +219,15 @@ unsigned int pseudoNewton(const std::vector<PNParam>& par, std::vector<double>& 
       mv[i] = x[i] - y[i];
     }
     double fnew = eval(y);
-    // Felsenstein-Churchill correction (:140-175)
+    // Felsenstein-Churchill correction, the fourth try a conjugate-gradient search (:140-175)
     for (unsigned int count = 0; count < 10 && (fnew > fcur + tolerance || std::isnan(fnew)); count++) {
+      if (count == 3) {
+        const double tol = std::max(std::fabs(fcur - fprev) / 2., tolerance);
+        eval(x);
+        y = x;
+        fnew = conjugateGradient(par, y, fcur, eval, der, tol, maxEval, &nEval);
+        continue;
+      }
       for (size_t i = 0; i < n; i++) {
         mv[i] /= 2.;
         y[i] = par[i].accept(x[i] - mv[i]);
@@ -160,6 +241,7 @@ unsigned int pseudoNewton(const std::vector<PNParam>& par, std::vector<double>& 
       x = y;
     }
     const bool done = std::fabs(fnew - fcur) < tolerance;
+    fprev = fcur;
     fcur = fnew;
     if (onStep) onStep(steps, x, fcur);
     if (done) break;

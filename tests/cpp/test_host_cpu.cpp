@@ -9,6 +9,7 @@
 #include <Bpp/Phyl/Model/SubstitutionModelSet.h>
 #include <Bpp/Phyl/Simulation/NonHomogeneousSequenceSimulator.h>
 #include <Bpp/Numeric/Prob/GammaDiscreteDistribution.h>
+#include <Bpp/Phyl/OptimizationTools.h>
 #include <Bpp/Phyl/TreeTemplate.h>
 #include <Bpp/Seq/Alphabet/AlphabetTools.h>
 
@@ -18,6 +19,53 @@
 #include <vector>
 
 using namespace bpp;
+
+// A host-only "likelihood" (no engine) to drive the optimisers on CPU:
+// f = sqrt(1 + x^2) + sqrt(1 + y^2) from (10, -7), no analytic derivatives.  Far from the
+// minimum the Newton move d1/d2 = x (1 + x^2) overshoots by orders of magnitude, so three
+// Felsenstein-Churchill halvings do not help and the fourth correction -- the
+// conjugate-gradient search -- has to find the way.
+class OvershootLikelihood : public TreeLikelihood {
+  TreeTemplate<Node> tree_;
+  mutable unsigned evals_ = 0;
+
+ public:
+  OvershootLikelihood() : tree_(*TreeTemplateTools::parenthesisToTree("(a:1,b:1);")) {
+    addParameter_(Parameter("x", 10.));
+    addParameter_(Parameter("y", -7.));
+  }
+  unsigned evaluations() const { return evals_; }
+  void initialize() override {}
+  bool isInitialized() const override { return true; }
+  double getValue() const override {
+    evals_++;
+    const double x = parameters_.getParameterValue("x"), y = parameters_.getParameterValue("y");
+    return std::sqrt(1. + x * x) + std::sqrt(1. + y * y);
+  }
+  double getLogLikelihood() const override { return -getValue(); }
+  double getLikelihood() const override { return std::exp(-getValue()); }
+  double getLogLikelihoodForASite(size_t) const override { return -getValue(); }
+  double getLikelihoodForASite(size_t) const override { return getLikelihood(); }
+  size_t getNumberOfSites() const override { return 1; }
+  size_t getNumberOfStates() const override { return 4; }
+  size_t getNumberOfClasses() const override { return 1; }
+  const Tree& getTree() const override { return tree_; }
+  ParameterList getBranchLengthsParameters() const override { return ParameterList(); }
+  ParameterList getSubstitutionModelParameters() const override { return parameters_; }
+  ParameterList getRateDistributionParameters() const override { return ParameterList(); }
+  ParameterList getDerivableParameters() const override { return ParameterList(); }
+  ParameterList getNonDerivableParameters() const override { return parameters_; }
+  void setParameters(const ParameterList& pl) override { parameters_.matchParametersValues(pl); }
+  double f(const ParameterList& pl) override {
+    setParameters(pl);
+    return getValue();
+  }
+  double getFirstOrderDerivative(const std::string&) const override { return 0.; }
+  double getSecondOrderDerivative(const std::string&) const override { return 0.; }
+  void enableDerivatives(bool) override {}
+  void enableFirstOrderDerivatives(bool) override {}
+  void enableSecondOrderDerivatives(bool) override {}
+};
 
 static void printVec(const char* key, const std::vector<double>& v) {
   std::printf("\"%s\": [", key);
@@ -153,6 +201,14 @@ int main() {
     std::printf(", ");
     printVec("expected", want);
     std::printf("}\n");
+  }
+  // PseudoNewton with its conjugate-gradient correction
+  {
+    OvershootLikelihood rl;
+    const unsigned n = OptimizationTools::optimizeNumericalParameters2(&rl, rl.getParameters(), 0, 1e-10, 20000, 0, 0);
+    std::printf("{\"kind\": \"pn_cg\", \"f\": %.17g, \"x\": %.17g, \"y\": %.17g, \"evals\": %u, \"steps\": %u}\n",
+                rl.getValue(), rl.getParameters().getParameterValue("x"), rl.getParameters().getParameterValue("y"), n,
+                OptimizationTools::lastSteps_);
   }
   return 0;
 }

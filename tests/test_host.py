@@ -181,3 +181,13 @@ def test_algorithmic_bytes_cfg2():
     wl = workload.make_workload("gtr_g4_dna_1M_64", n_patterns=10)
     assert wl.algorithmic_bytes_per_pattern() == 15944
     assert abs(wl.algorithmic_bytes_per_pattern() / wl.et.n_internal - 257.16) < 0.01
+
+
+def test_host_pseudonewton_conjugate_gradient(host_records):
+    """optimizeNumericalParameters2 (OPTIMIZATION_NEWTON) on a host-only function whose
+    Newton moves overshoot by orders of magnitude (sqrt(1 + x^2) + sqrt(1 + y^2) from
+    (10, -7)): the fourth Felsenstein-Churchill correction is the conjugate-gradient search
+    of PseudoNewtonOptimizer.cpp:151-170, and the optimiser reaches the minimum (0, 0)."""
+    r = next(x for x in host_records if x["kind"] == "pn_cg")
+    assert abs(r["f"] - 2.0) < 1e-8 and abs(r["x"]) < 1e-3 and abs(r["y"]) < 1e-3, r
+    assert r["evals"] < 2000, r
