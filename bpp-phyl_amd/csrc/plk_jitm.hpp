@@ -20,10 +20,9 @@
 // group broadcast).  P(t) is staged in LDS as stored, [c][x][y]: lane (hi, lo) reads row
 // 4X + lo, column 4Y + hi, so a 32-lane group reads rows lo = 0..3 at columns hi = 0, 1 --
 // 8 distinct doubles on 8 distinct bank pairs (conflict-free) -- and the staging is a
-// plain copy whose ds_write_b64 groups store 16 consecutive doubles (conflict-free).  The
-// round-2 16-double tile image [c][X][Y][hi][lo] made those stores 4-way conflicts
-// (~1 extra LDS cycle per LDS instruction of the kernel); JITM_IMG=1 / 2 keep it (and a
-// rotated variant) for A/B.
+// plain copy whose ds_write_b64 groups store 16 consecutive doubles (conflict-free).
+// SQ_LDS_BANK_CONFLICT on cfg3: 0 (round 2's 16-double tile image [c][X][Y][hi][lo]: 4-way
+// conflicted stores, 43 M conflict cycles per launch, 3.60 vs 3.43 ms; profiles/r03).
 //
 // All classes in one wave: the joint (all states, all classes) exact power-of-two
 // rescale of the other kernels is an in-register max plus two shuffles -- no LDS exchange
@@ -114,15 +113,11 @@ struct JitMShape {
   int minw = 2;      // __launch_bounds__ min waves per SIMD
   int pd = 1;        // P(t) staging prefetch distance (contractions ahead)
   int G = 4;         // waves (16-pattern groups) per workgroup: 64 patterns (4) or 128 (8)
-  // LDS image of a staged P(t): 0 = as stored, [c][x][y] (staging is a plain copy; the A
-  // read of block (X, Y) is row 4X + lo, column 4Y + hi from one lane base), 1 = 16-double
-  // tiles [c][X][Y][hi][lo], 2 = tiles rotated per Y block
-  int img = 0;
   int pb() const { return C * S * S; }  // doubles of P(t) per branch (every class)
   size_t lds_bytes() const { return (size_t)(2 * pb() + 16 * G) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
     return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && pd == o.pd &&
-           G == o.G && img == o.img;
+           G == o.G;
   }
 };
 
@@ -138,26 +133,23 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const int NTH = 64 * sh.G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH;
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
-           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n#define IMG_ %d\n",
-           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PF, sh.scale ? "true" : "false", sh.img);
+           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n",
+           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PF, sh.scale ? "true" : "false");
   s += buf;
   s += R"PLKJITM(
-// P(t) of branch b (all classes, [c][x][y]) -> registers -> the LDS tile image
-// [c][X][Y][16] with P[4X + lo][4Y + hi] at tile position 4 hi + ((lo + Y) & 3)
+// P(t) of branch b (all classes, [c][x][y]) -> registers -> LDS buffer bf, as stored
 #define PSTAGE_LOAD(R, b) { const double* s_ = a.pmats + (i64)(b) * PB_; \
   _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) { const int e_ = tid + j_ * NTH_; R[j_] = s_[e_ < PB_ ? e_ : PB_ - 1]; } }
 #define PSTAGE_STORE(R, bf) { double* d_ = lds + (bf) * PB_; \
   _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) { \
-    if (IMG_ == 0) { const int e_ = tid + j_ * NTH_; if (PB_ % NTH_ == 0 || e_ < PB_) d_[e_] = R[j_]; } \
-    else if (sidx[j_] >= 0) d_[sidx[j_]] = R[j_]; } }
-// D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1); the A read of tile (c, X, Y)
-// goes through the lane base of rotation Y & 3
+    const int e_ = tid + j_ * NTH_; if (PB_ % NTH_ == 0 || e_ < PB_) d_[e_] = R[j_]; } }
+// D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1); lane (hi, lo) reads
+// A(c, X, Y)[lo][hi] = P_c[4X + lo][4Y + hi] at a constant offset from its lane base PA
 #define CONTRIB(D, SRC, bf, SET) { \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
     double d_ = 0.0; \
     _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) \
-      d_ = mfma4(IMG_ == 0 ? PA[0][(bf) * PB_ + (c_ * S_ + 4 * X_) * S_ + 4 * Y_] \
-                           : PA[Y_ & 3][(bf) * PB_ + ((c_ * XB_ + X_) * XB_ + Y_) * 16], SRC[c_][Y_], d_); \
+      d_ = mfma4(PA[(bf) * PB_ + (c_ * S_ + 4 * X_) * S_ + 4 * Y_], SRC[c_][Y_], d_); \
     if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } }
 #define ROWMUL(D, F, SET) { _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") \
   for (int X_ = 0; X_ < XB_; ++X_) { if (SET) D[c_][X_] = F[c_][X_]; else D[c_][X_] *= F[c_][X_]; } }
@@ -226,19 +218,10 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const i64 p0 = (i64)blockIdx.x * (16 * G_);
   const i64 p = p0 + 16 * w + pl;
   const i64 toff = (p >> 7) * (i64)(C_ * S_ * kTile) + (p & (kTile - 1)) + (i64)hi * kTile;
-  // A-operand lane bases, one per tile rotation Y & 3 (lane 16 hi + 4 b + lo reads tile
-  // element (hi, lo))
-  const double* PA[4];
-  _Pragma("unroll") for (int k = 0; k < 4; ++k)
-    PA[k] = IMG_ == 0 ? lds + (lane & 3) * S_ + hi : lds + ((hi << 2) | (((lane & 3) + (IMG_ == 2 ? k : 0)) & 3));
-  int sidx[PF_];   // this thread's staging elements -> tile slots (-1: past the table)
-  _Pragma("unroll") for (int j = 0; j < PF_; ++j) {
-    const int e = tid + j * NTH_;
-    const int c = e / (S_ * S_), r = e - c * (S_ * S_), x = r / S_, y = r - x * S_;
-    sidx[j] = e < PB_ ? ((c * XB_ + (x >> 2)) * XB_ + (y >> 2)) * 16 + ((y & 3) << 2) + (((x & 3) + (IMG_ == 2 ? (y >> 2) : 0)) & 3) : -1;
-  }
+  // A-operand lane base: lane 16 hi + 4 b + lo reads row lo, column hi of a 4x4 block
+  const double* PA = lds + (lane & 3) * S_ + hi;
   double R0[PF_] = {}, R1[PF_] = {}, R2[PF_] = {};
-  (void)red; (void)PA; (void)R0; (void)R1; (void)R2; (void)toff; (void)sidx;
+  (void)red; (void)PA; (void)R0; (void)R1; (void)R2; (void)toff;
   const int frag = frag_base + (int)blockIdx.y;
 )PLKJITM";
   // accumulators per register level and the operand ring

@@ -1,0 +1,81 @@
+// Emit the hiprtc source of the tree-specialised kernels (plk_jit.hpp: jit_tree4_source,
+// plk_jitm.hpp: jit_treeM4_source) for a small two-fragment program, so that
+// tests/test_jit_sources.py can cross-compile it for gfx950 with hipcc on a machine without
+// a GPU (the library compiles these sources only at run time, on the device).
+//   jit_emit <tree4|treeM> <C> <scale 0|1> [S (treeM: 20 | 4)] > kernel.hip
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "plk_jit.hpp"
+#include "plk_jitm.hpp"
+
+using namespace plk;
+
+int main(int argc, char** argv) {
+  const std::string kind = argc > 1 ? argv[1] : "tree4";
+  const int C = argc > 2 ? std::atoi(argv[2]) : 4;
+  const bool scale = argc > 3 && std::atoi(argv[3]) != 0;
+  const int S = argc > 4 ? std::atoi(argv[4]) : 20;
+  // 7 tips (0..6), internal nodes 7..11.  Fragment 0: node 10 = ((t0, t1)8, (t2, t3)9),
+  // stored in slot 0.  Fragment 1 (root 11): (t4, t5)7 unstored, t6, slot 0 via branch 10.
+  // treeM programs carry unstored cherries as T_CHERRY rows instead.
+  std::vector<TInstr> prog;
+  auto add = [&](int op, int d, int a, int b) { prog.push_back(TInstr{op, d, a, b}); };
+  const bool m = kind == "treeM";
+  if (m) {
+    add(T_CHERRY, 0, 0, 8);
+    add(T_CHERRY, 0, 1, 9);
+  } else {
+    add(T_DESCEND, 1, 0, 0);
+    add(T_TIP, 1, 0, 0);
+    add(T_TIP, 1, 1, 1);
+    add(T_ASCEND, 1, -1, 8);
+    add(T_DESCEND, 1, 0, 0);
+    add(T_TIP, 1, 2, 2);
+    add(T_TIP, 1, 3, 3);
+    add(T_ASCEND, 1, -1, 9);
+  }
+  add(T_ROOT, 0, 0, 0);
+  const int start1 = (int)prog.size();
+  if (m) {
+    add(T_CHERRY, 0, 2, 7);
+  } else {
+    add(T_DESCEND, 1, 0, 0);
+    add(T_TIP, 1, 4, 4);
+    add(T_TIP, 1, 5, 5);
+    add(T_ASCEND, 1, -1, 7);
+  }
+  add(T_TIP, 0, 6, 6);
+  add(T_DESCEND, 1, 0, 0);  // a one-child internal level: exercises ASCEND with a store
+  add(T_LOAD, 1, 0, 10);
+  add(T_ASCEND, 1, 1, 11);
+  add(T_ROOT, 0, -1, 1);
+  const std::vector<int32_t> starts = {0, start1};
+  std::string src;
+  if (m) {
+    JitMShape sh;
+    sh.S = S;
+    sh.C = C;
+    sh.U = 16;
+    sh.scale = scale;
+    src = jit_treeM4_source(prog, starts, sh);
+  } else {
+    JitShape sh;
+    sh.C = C;
+    sh.CW = argc > 5 && std::atoi(argv[5]) ? C : 1;
+    sh.U = 16;
+    sh.scale = scale;
+    const JitPlan plan = jit_plan(prog, starts, sh.C, sh.U, 64 * 1024 / 8, scale);
+    sh.NT = plan.NU;
+    sh.TD = plan.tab_doubles;
+    sh.G = 1;
+    sh.PW = 1;
+    sh.L = sh.CW > 1 ? 2 : 3;
+    sh.ppipe = true;
+    src = jit_tree4_source(plan, sh);
+  }
+  std::fwrite(src.data(), 1, src.size(), stdout);
+  return 0;
+}

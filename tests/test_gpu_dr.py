@@ -258,7 +258,7 @@ def test_dr_fused_preorder_equals_levelwise(C, n_taxa, n_pat, amb, monkeypatch):
 
 @pytest.mark.parametrize("S,C,tree_kind,n_pat,scaling", [
     (20, 4, "balanced40", 500, True), (20, 2, "balanced24", 333, False), (20, 1, "caterpillar120long", 300, True),
-    (64, 1, "balanced24", 300, False), (64, 2, "balanced16", 130, True), (64, 1, "caterpillar60long", 200, True),
+    (64, 1, "balanced24", 300, False), (64, 2, "balanced16", 130, True), (64, 1, "caterpillar150long", 200, True),
     (4, 4, "caterpillar300long", 600, True), (4, 2, "balanced64", 2000, True)])
 def test_dr_fused_preorder_any_state_count(S, C, tree_kind, n_pat, scaling, monkeypatch):
     """The fused preorder beyond unscaled DNA: dr_pre_m_kernel (20 / 64 states on fp64

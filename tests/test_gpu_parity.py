@@ -1114,25 +1114,6 @@ def test_jit_treeM_register_depths(dm, L, pd, g, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("img", ["1", "2"])
-def test_jit_treeM_lds_images_bitwise(img, monkeypatch):
-    """The P(t) staging layouts of jit_treeM (JITM_IMG: 0 = as stored, the default; 1 = 16-double
-    tiles; 2 = tiles rotated per Y block) feed the same A operands to the same MFMAs:
-    lnL, per-pattern lnL and block sums bitwise."""
-    et, m, alph, rates, probs, states = _random_problem(20, 4, 60, 700, seed=81, amb=True)
-    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
-    out = []
-    for v in ("0", img):
-        set_tune(monkeypatch, "JITM_IMG", v)
-        eng = engine_for(et, 20, 4, 700, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
-        out.append(run_engine(eng, et))
-        assert eng.kernel_path() == "jit_treeM"
-        del eng
-    (l0, s0, b0), (l1, s1, b1) = out
-    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode,nh", [
     (4, "balanced64", 3000, False, "lnl_only", False), (4, "balanced64", 1000, False, "materialize", False),
     (2, "caterpillar40", 700, True, "lnl_only", False), (4, "balanced300", 513, True, "lnl_only", True),
