@@ -1,6 +1,6 @@
 """The tree-specialised kernels are generated as HIP source at run time and compiled with
 hiprtc on the device (plk_jit.hpp, plk_jitm.hpp).  These CPU tests emit the source of
-both generators for a small two-fragment program (tests/cpp/jit_emit.cpp: stored and
+both generators for a small two-fragment program (tests/jit/jit_emit.cpp: stored and
 unstored cherries, a tip, a loaded fragment root, the root reduction) in the shapes the
 library uses -- one class per wave and every class in the wave, with and without
 rescaling; jit_treeM for 20 and 4 states -- and cross-compile each for gfx950 with hipcc,
@@ -22,7 +22,7 @@ def emitter(tmp_path_factory):
     d = tmp_path_factory.mktemp("jit_emit")
     exe = str(d / "jit_emit")
     subprocess.run([HIPCC, "-std=c++17", "-O1", "--offload-arch=gfx950", "-I" + os.path.join(ROOT, "bpp-phyl_amd", "csrc"),
-                    "-I" + os.path.join(ROOT, "include"), "-o", exe, os.path.join(ROOT, "tests", "cpp", "jit_emit.cpp")],
+                    "-I" + os.path.join(ROOT, "include"), "-o", exe, os.path.join(ROOT, "tests", "jit", "jit_emit.cpp")],
                    check=True, capture_output=True, timeout=600)
     return exe, d
 
