@@ -86,7 +86,8 @@ class Parameter {
 // An ordered list of parameters.  Name lookups go through a name -> position index that
 // is rebuilt lazily whenever the list changed (or a parameter was renamed through
 // operator[]), so the optimisers' per-evaluation setParameters of every parameter costs
-// O(n), not O(n^2) string comparisons.
+// O(n), not O(n^2) string comparisons; a position hint (lists that share an order, the
+// usual case: a sublist handed back to the object it came from) skips the hash.
 class ParameterList {
   std::vector<Parameter> params_;
   mutable std::unordered_map<std::string, size_t> index_;
@@ -102,6 +103,10 @@ class ParameterList {
       return it == index_.end() ? -1 : (long)it->second;
     }
     return (long)it->second;
+  }
+  long find(const std::string& name, size_t hint) const {
+    if (hint < params_.size() && params_[hint].getName() == name) return (long)hint;
+    return find(name);
   }
   void rebuild() const {
     index_.clear();
@@ -122,6 +127,8 @@ class ParameterList {
     return v;
   }
   bool hasParameter(const std::string& name) const { return find(name) >= 0; }
+  // position of `name` (-1: absent), trying position `hint` first (not in the reference API)
+  long indexOf(const std::string& name, size_t hint = (size_t)-1) const { return find(name, hint); }
   size_t whichParameterHasName(const std::string& name) const {
     const long i = find(name);
     if (i < 0) throw ParameterNotFoundException("ParameterList::whichParameterHasName", name);
@@ -148,18 +155,36 @@ class ParameterList {
   }
   void setParameterValue(const std::string& name, double v) { params_[whichParameterHasName(name)].setValue(v); }
   // Update values of parameters present in both lists; returns true if any changed.
+  // `changed` receives the positions that changed (each once).  A much longer `pl` (a
+  // model's few parameters matched against a likelihood's whole list) is probed by this
+  // list's names instead of walking all of it.
   bool matchParametersValues(const ParameterList& pl, std::vector<size_t>* changed = nullptr) {
     bool any = false;
-    for (size_t j = 0; j < pl.size(); j++) {
-      const long i = find(pl[j].getName());
-      if (i < 0) continue;
-      Parameter& p = params_[(size_t)i];
-      if (p.getValue() != pl[j].getValue()) {
-        p.setValue(pl[j].getValue());
-        any = true;
-        if (changed && std::find(changed->begin(), changed->end(), (size_t)i) == changed->end())
-          changed->push_back((size_t)i);
+    std::vector<char> seen;
+    auto set = [&](size_t i, double v) {
+      Parameter& p = params_[i];
+      if (p.getValue() == v) return;
+      p.setValue(v);
+      any = true;
+      if (changed) {
+        if (seen.empty()) seen.assign(params_.size(), 0);
+        if (!seen[i]) changed->push_back(i);
+        seen[i] = 1;
       }
+    };
+    if (pl.size() > 2 * params_.size()) {
+      for (size_t i = 0; i < params_.size(); i++) {
+        const long j = pl.find(params_[i].getName());
+        if (j >= 0) set(i, pl.params_[(size_t)j].getValue());
+      }
+      return any;
+    }
+    size_t hint = 0;
+    for (size_t j = 0; j < pl.size(); j++) {
+      const long i = find(pl.params_[j].getName(), hint);
+      if (i < 0) continue;
+      hint = (size_t)i + 1;
+      set((size_t)i, pl.params_[j].getValue());
     }
     return any;
   }

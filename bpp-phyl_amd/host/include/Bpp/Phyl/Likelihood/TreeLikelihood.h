@@ -101,6 +101,16 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   std::shared_ptr<IntervalConstraint> brLenConstraint_;
   ParameterList brLenParameters_;
   std::vector<std::string> brLenNames_;      // "BrLen<i>" of nodes_[i]
+  std::vector<long> brLenPos_;               // their positions in parameters_ (checked by name)
+  std::vector<int> engineById_;              // engine index by node id (-1: none; engineIndex_ is the reference)
+  int engineOf(const Node* n) const {
+    const int id = n->getId();
+    if (id >= 0 && (size_t)id < engineById_.size() && engineById_[(size_t)id] >= 0 &&
+        nodeById_[(size_t)id] == n)
+      return engineById_[(size_t)id];
+    return engineIndex_.at(n);
+  }
+  std::vector<const Node*> nodeById_;
   mutable double minusLogLik_ = -1.;
   mutable std::vector<double> siteLnl_;      // per pattern (fetched lazily)
   mutable bool siteLnlValid_ = false;

@@ -77,6 +77,22 @@ void AbstractPlkTreeLikelihood::buildEngineLayout() {
   for (Node* n : all)
     if (!n->isLeaf()) engineIndex_[n] = nTips_ + nInternal_++;
   rootEngine_ = engineIndex_[tree_->getRootNode()];
+  engineById_.clear();
+  nodeById_.clear();
+  for (const auto& kv : engineIndex_) {
+    const int id = kv.first->getId();
+    if (id < 0 || id > 16 * (int)all.size() + 1024) continue;  // sparse ids stay on the map
+    if ((size_t)id >= engineById_.size()) {
+      engineById_.resize((size_t)id + 1, -1);
+      nodeById_.resize((size_t)id + 1, nullptr);
+    }
+    if (nodeById_[(size_t)id]) {  // duplicate id: lookups by id are ambiguous
+      engineById_[(size_t)id] = -1;
+      continue;
+    }
+    engineById_[(size_t)id] = kv.second;
+    nodeById_[(size_t)id] = kv.first;
+  }
   opParent_.clear();
   opChildren_.clear();
   opFlags_.clear();
@@ -216,11 +232,14 @@ std::vector<const Node*> AbstractPlkTreeLikelihood::applyBranchLengths() {
   if (brLenNames_.size() != nodes_.size()) {
     brLenNames_.clear();
     for (size_t i = 0; i < nodes_.size(); i++) brLenNames_.push_back("BrLen" + std::to_string(i));
+    brLenPos_.assign(nodes_.size(), -1);
   }
+  const ParameterList& pl = parameters_;
   for (size_t i = 0; i < nodes_.size(); i++) {
-    const std::string& n = brLenNames_[i];
-    if (!parameters_.hasParameter(n)) continue;
-    const double v = parameters_.getParameterValue(n);
+    const long k = pl.indexOf(brLenNames_[i], (size_t)brLenPos_[i]);
+    brLenPos_[i] = k;
+    if (k < 0) continue;
+    const double v = pl[(size_t)k].getValue();
     if (!nodes_[i]->hasDistanceToFather() || nodes_[i]->getDistanceToFather() != v) {
       nodes_[i]->setDistanceToFather(v);
       changed.push_back(nodes_[i]);
@@ -323,7 +342,7 @@ void AbstractPlkTreeLikelihood::evaluateTree(const std::vector<const Node*>& pno
     const Vdouble& rates = rateDistribution_->getCategories();
     std::vector<double> P(nbClasses_ * nbStates_ * nbStates_);
     for (const Node* n : pnodes) {
-      const int e = engineIndex_.at(n), mi = modelIndexForNode(n);
+      const int e = engineOf(n), mi = modelIndexForNode(n);
       const SubstitutionModel* m = modelForIndex(mi);
       if (m && !m->isNonSingular()) {
         hostP_ = true;
@@ -346,7 +365,7 @@ void AbstractPlkTreeLikelihood::evaluateTree(const std::vector<const Node*>& pno
     need.assign((size_t)(nTips_ + nInternal_), 0);
     for (const Node* n : pnodes)
       for (const Node* p = n->getFather(); p; p = p->getFather()) {
-        char& f = need[(size_t)engineIndex_.at(p)];
+        char& f = need[(size_t)engineOf(p)];
         if (f) break;
         f = 1;
       }

@@ -31,3 +31,6 @@ for c in gtr_g4_dna_1M_64 lg08_g4_protein_200k_256 yn98_codon_50k_128 nh_gtr_g4_
 done
 bash tools/gpu_stalls.sh ${P}_cfg3 lg08_g4_protein_200k_256 || exit 1
 bash tools/gpu_stalls.sh ${P}_cfg5 nh_gtr_g4_dna_2M_512 || exit 1
+timeout -k 10 150 bpp-phyl_amd/host/bin/bench_mirror cfg2 > gpurun_out/${P}_mirror_cfg2.json || exit 1
+timeout -k 10 200 python bench.py --patterns 609573 --no-cpu-baseline > gpurun_out/${P}_bench_609k.json 2> gpurun_out/${P}_bench_609k.err || exit 1
+PLK_TUNE=PMAT_STAGED=1 timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/${P}_bench_pmatstaged.json 2> gpurun_out/${P}_bench_pmatstaged.err || exit 1
