@@ -39,6 +39,21 @@ class RowMatrix {
 // d[k] are the eigenvalues and column k of U (row-major) the eigenvectors.
 void symmetricEigen(size_t n, const std::vector<double>& A, std::vector<double>& d, std::vector<double>& U);
 
+// Real eigen-decomposition of a general (nonsymmetric) n x n row-major matrix A, in the
+// layout of the reference's EigenValue (getV / getRealEigenValues / getImagEigenValues,
+// used by Model/AbstractSubstitutionModel.cpp:276-281): a complex pair a +- ib occupies
+// positions k, k+1 with wi[k] = b > 0, wi[k+1] = -b, and columns k, k+1 of V (row-major)
+// hold Re v, Im v of the eigenvector of a + ib, so that A V = V D with D block-diagonal,
+// D(k,k) = D(k+1,k+1) = a, D(k,k+1) = b, D(k+1,k) = -b.  Eigenvalues: complex shifted QR
+// on the Hessenberg form; eigenvectors: inverse iteration (vectors of a repeated
+// eigenvalue deflated against each other).  Returns false if the iteration does not
+// converge.
+bool generalEigen(size_t n, const std::vector<double>& A, std::vector<double>& wr, std::vector<double>& wi,
+                  std::vector<double>& V);
+
+// Inverse of the n x n row-major matrix A (LU with partial pivoting); false if singular.
+bool invertMatrix(size_t n, const std::vector<double>& A, std::vector<double>& Ainv);
+
 }  // namespace bpp
 
 #endif

@@ -78,7 +78,7 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   bool usePatterns_ = true;
   bool verbose_ = true;
   bool initialized_ = false;
-  bool scaling_ = true;
+  int scalingMode_ = -1;  // setUnderflowScaling: 1 on, 0 off, -1 by tree size (createEngine)
   bool incremental_ = true;
   bool compressed_ = false;  // usePatterns: PLK_FLAG_SUBTREE_PATTERNS on the engine
   bool allDirty_ = true;     // next fireParameterChanged recomputes every P(t) (initialize)
@@ -187,8 +187,12 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   const std::vector<unsigned int>& getWeights() const { return rootWeights_; }
   size_t getRootArrayPosition(size_t site) const { return rootPatternLinks_[site]; }
   // Exact power-of-two rescaling of partials (a deviation from the reference, which
-  // has none and underflows on large trees); bit-identical when it never triggers.
-  void setUnderflowScaling(bool yn) { scaling_ = yn; }
+  // has none and underflows on large trees); bit-identical when it never triggers.  By
+  // default it is on when a site's likelihood can approach the double range on long
+  // branches, taken as n_tips * ln(n_states) > 300 (DNA above 216 tips, proteins above
+  // 100, codons above 73), and off otherwise, as in the reference: the kernels without
+  // it are faster (cfg2 one class per wave instead of every class in the wave).
+  void setUnderflowScaling(bool yn) { scalingMode_ = yn ? 1 : 0; }
   // Branch-length-only changes re-evaluate just the ancestors of the changed branches
   // (default); false restores the reference's full traversal on every change.
   void setIncrementalRecompute(bool yn) { incremental_ = yn; }

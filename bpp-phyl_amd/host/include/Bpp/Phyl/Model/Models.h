@@ -34,6 +34,21 @@ class GTR : public AbstractReversibleSubstitutionModel {
   void updateMatrices() override;
 };
 
+// L95 (Lobry 1995) strand-symmetric, non-reversible nucleotide model
+// (Model/Nucleotide/L95.cpp:56-119): generator from alpha, beta, gamma, kappa, theta,
+// frequencies ((1-theta)/2, theta/2, theta/2, (1-theta)/2).  Its eigenvalues can be
+// complex: P(t) then takes the block form (SubstitutionModel::getPij_t) on the host.
+class L95 : public SubstitutionModel {
+  double alpha_, beta_, gamma_, kappa_, theta_;
+
+ public:
+  L95(const NucleicAlphabet* alpha, double a = 0.5, double b = 0.5, double g = 0.5, double kappa = 1.,
+      double theta = 0.5);
+  L95* clone() const override { return new L95(*this); }
+  std::string getName() const override { return "L95"; }
+  void updateMatrices() override;
+};
+
 // LG08 empirical amino-acid model (Model/Protein/LG08.cpp:53-62), fixed frequencies.
 class LG08 : public AbstractReversibleSubstitutionModel {
  public:

@@ -30,6 +30,7 @@ class SubstitutionModel : public AbstractParametrizable {
   RowMatrix<double> exchangeability_;
   Vdouble freq_;
   Vdouble eigenValues_;
+  Vdouble iEigenValues_;                 // imaginary parts (complex pairs: +b, -b)
   RowMatrix<double> leftEigenVectors_;   // V^-1 (rows)
   RowMatrix<double> rightEigenVectors_;  // V (columns)
   bool isDiagonalizable_ = true;
@@ -47,7 +48,7 @@ class SubstitutionModel : public AbstractParametrizable {
   SubstitutionModel(const Alphabet* alpha, size_t size, const std::string& prefix)
       : AbstractParametrizable(prefix), alphabet_(alpha), size_(size), generator_(size, size),
         exchangeability_(size, size), freq_(size, 1. / size), eigenValues_(size, 0.),
-        leftEigenVectors_(size, size), rightEigenVectors_(size, size), pijt_(size, size), dpijt_(size, size),
+        iEigenValues_(size, 0.), leftEigenVectors_(size, size), rightEigenVectors_(size, size), pijt_(size, size), dpijt_(size, size),
         d2pijt_(size, size) {}
   virtual ~SubstitutionModel() {}
   virtual SubstitutionModel* clone() const = 0;
@@ -60,10 +61,14 @@ class SubstitutionModel : public AbstractParametrizable {
   const RowMatrix<double>& getGenerator() const { return generator_; }
   const RowMatrix<double>& getExchangeabilityMatrix() const { return exchangeability_; }
   const Vdouble& getEigenValues() const { return eigenValues_; }
+  const Vdouble& getIEigenValues() const { return iEigenValues_; }
   const RowMatrix<double>& getRowLeftEigenVectors() const { return leftEigenVectors_; }
   const RowMatrix<double>& getColumnRightEigenVectors() const { return rightEigenVectors_; }
   bool isDiagonalizable() const { return isDiagonalizable_; }
   bool isNonSingular() const { return isNonSingular_; }
+  // P(t) from the host (plk_set_pmatrix) instead of the device's real V e^{lambda t} V^-1:
+  // the Taylor branch, and complex eigenvalue pairs (the block form of getPij_t)
+  bool needsHostPij() const { return !isNonSingular_ || !isDiagonalizable_; }
   double getRate() const { return rate_; }
   void setRate(double r) { rate_ = r; }
   bool isScalable() const { return isScalable_; }
@@ -74,7 +79,9 @@ class SubstitutionModel : public AbstractParametrizable {
   // host-computed matrices to the engine with plk_set_pmatrix.
   virtual bool hasClosedFormPij() const { return false; }
 
-  // P(t) = V diag(exp(lambda rate t)) V^-1 (Model/AbstractSubstitutionModel.cpp:426-438)
+  // P(t) = V diag(exp(lambda rate t)) V^-1 (Model/AbstractSubstitutionModel.cpp:426-438);
+  // complex pairs a +- ib: V B V^-1 with 2x2 blocks e^{a r t} [[cos, sin], [-sin, cos]](b r t)
+  // (:440-467), and the derivatives' blocks (:505-537, :581-611)
   virtual const RowMatrix<double>& getPij_t(double t) const;
   virtual const RowMatrix<double>& getdPij_dt(double t) const;
   virtual const RowMatrix<double>& getd2Pij_dt2(double t) const;
@@ -104,6 +111,12 @@ class SubstitutionModel : public AbstractParametrizable {
   // Eigen-system of the current generator (reversible: symmetric form); strips
   // null (stop) states like Model/AbstractSubstitutionModel.cpp:184-273.
   void computeEigen();
+  // Eigen-system of a non-reversible generator (the reference's EigenValue on the
+  // generator, :276-281): real eigenvalues and complex pairs, isDiagonalizable_ = no pair
+  // (:291-303), isNonSingular_ = one null eigenvalue (:306-372), which is set to 0 exactly.
+  void computeEigenGeneral();
+  // out = V T V^-1 with T tridiagonal (diagonal dia, T(k,k+1) = up[k], T(k+1,k) = lo[k])
+  void blockProduct(const Vdouble& dia, const Vdouble& up, const Vdouble& lo, RowMatrix<double>& out) const;
 };
 
 typedef SubstitutionModel TransitionModel;

@@ -2,6 +2,7 @@
 // the discrete Gamma distribution.
 #include <algorithm>
 #include <cmath>
+#include <complex>
 #include <sstream>
 
 #include "Bpp/Numeric/Matrix/Matrix.h"
@@ -377,5 +378,253 @@ GammaDiscreteRateDistribution::GammaDiscreteRateDistribution(size_t n, double al
 }
 
 void GammaDiscreteRateDistribution::fireParameterChanged(const ParameterList&) { discretize(); }
+
+}  // namespace bpp
+
+namespace bpp {
+
+// ---------------------------------------------------------------------------
+// General real eigen-solver (non-reversible generators).
+// ---------------------------------------------------------------------------
+namespace {
+typedef std::complex<double> cd;
+
+// Solve M x = b in place (complex LU with partial pivoting); a zero pivot is replaced by
+// `tiny` (inverse iteration wants the near-singular solve).
+void complexSolve(size_t n, std::vector<cd> M, std::vector<cd>& b, double tiny) {
+  std::vector<size_t> piv(n);
+  for (size_t k = 0; k < n; k++) {
+    size_t p = k;
+    for (size_t i = k + 1; i < n; i++)
+      if (std::abs(M[i * n + k]) > std::abs(M[p * n + k])) p = i;
+    if (p != k) {
+      for (size_t j = 0; j < n; j++) std::swap(M[k * n + j], M[p * n + j]);
+      std::swap(b[k], b[p]);
+    }
+    if (std::abs(M[k * n + k]) < tiny) M[k * n + k] = tiny;
+    for (size_t i = k + 1; i < n; i++) {
+      const cd f = M[i * n + k] / M[k * n + k];
+      if (f == cd(0.)) continue;
+      for (size_t j = k; j < n; j++) M[i * n + j] -= f * M[k * n + j];
+      b[i] -= f * b[k];
+    }
+  }
+  for (size_t k = n; k-- > 0;) {
+    cd s = b[k];
+    for (size_t j = k + 1; j < n; j++) s -= M[k * n + j] * b[j];
+    b[k] = s / M[k * n + k];
+  }
+}
+
+// Eigenvalues of the n x n complex matrix H (row-major, overwritten): Householder reduction
+// to upper Hessenberg form, then single-shift QR with Wilkinson shifts and deflation.
+bool complexEigenvalues(size_t n, std::vector<cd>& H, std::vector<cd>& w) {
+  auto h = [&](size_t i, size_t j) -> cd& { return H[i * n + j]; };
+  for (size_t k = 0; k + 2 < n; k++) {
+    double norm = 0.;
+    for (size_t i = k + 1; i < n; i++) norm += std::norm(h(i, k));
+    norm = std::sqrt(norm);
+    if (norm == 0.) continue;
+    std::vector<cd> v(n, 0.);
+    const cd x0 = h(k + 1, k);
+    const cd alpha = (std::abs(x0) > 0. ? -x0 / std::abs(x0) : cd(-1.)) * norm;
+    for (size_t i = k + 1; i < n; i++) v[i] = h(i, k);
+    v[k + 1] -= alpha;
+    double vn = 0.;
+    for (size_t i = k + 1; i < n; i++) vn += std::norm(v[i]);
+    if (vn == 0.) continue;
+    // H <- (I - 2 v v^H / |v|^2) H (I - 2 v v^H / |v|^2)
+    for (size_t j = 0; j < n; j++) {
+      cd s = 0.;
+      for (size_t i = k + 1; i < n; i++) s += std::conj(v[i]) * h(i, j);
+      s *= 2. / vn;
+      for (size_t i = k + 1; i < n; i++) h(i, j) -= v[i] * s;
+    }
+    for (size_t i = 0; i < n; i++) {
+      cd s = 0.;
+      for (size_t j = k + 1; j < n; j++) s += h(i, j) * v[j];
+      s *= 2. / vn;
+      for (size_t j = k + 1; j < n; j++) h(i, j) -= s * std::conj(v[j]);
+    }
+    for (size_t i = k + 2; i < n; i++) h(i, k) = 0.;
+  }
+  const double eps = 2.220446049250313e-16;
+  size_t hi = n ? n - 1 : 0;
+  int iter = 0, total = 0;
+  while (n && hi > 0) {
+    size_t l = hi;
+    while (l > 0) {
+      const double s = std::abs(h(l - 1, l - 1)) + std::abs(h(l, l));
+      if (std::abs(h(l, l - 1)) <= eps * (s > 0. ? s : 1.)) {
+        h(l, l - 1) = 0.;
+        break;
+      }
+      l--;
+    }
+    if (l == hi) {  // h(hi, hi) is an eigenvalue
+      hi--;
+      iter = 0;
+      continue;
+    }
+    if (++total > 200 * (int)n) return false;
+    const cd a = h(hi - 1, hi - 1), b = h(hi - 1, hi), c = h(hi, hi - 1), d = h(hi, hi);
+    cd mu;
+    if (++iter % 12 == 0) {
+      mu = d + std::abs(c);  // exceptional shift
+    } else {
+      const cd tr = a + d, disc = std::sqrt(tr * tr / 4. - (a * d - b * c));
+      const cd m1 = tr / 2. + disc, m2 = tr / 2. - disc;
+      mu = std::abs(m1 - d) < std::abs(m2 - d) ? m1 : m2;
+    }
+    for (size_t j = l; j <= hi; j++) h(j, j) -= mu;
+    std::vector<cd> cs(hi - l), sn(hi - l);
+    for (size_t k = l; k < hi; k++) {  // H - mu I = Q R (Givens on rows k, k+1)
+      const cd x = h(k, k), y = h(k + 1, k);
+      const double r = std::sqrt(std::norm(x) + std::norm(y));
+      const cd cc = r > 0. ? x / r : cd(1.), ss = r > 0. ? y / r : cd(0.);
+      cs[k - l] = cc;
+      sn[k - l] = ss;
+      for (size_t j = k; j < n; j++) {
+        const cd u = h(k, j), v = h(k + 1, j);
+        h(k, j) = std::conj(cc) * u + std::conj(ss) * v;
+        h(k + 1, j) = -ss * u + cc * v;
+      }
+    }
+    for (size_t k = l; k < hi; k++) {  // R Q (the rotations' adjoints on columns k, k+1)
+      const cd cc = cs[k - l], ss = sn[k - l];
+      const size_t rmax = std::min(k + 2, hi);
+      for (size_t i = 0; i <= rmax; i++) {
+        const cd u = h(i, k), v = h(i, k + 1);
+        h(i, k) = u * cc + v * ss;
+        h(i, k + 1) = -u * std::conj(ss) + v * std::conj(cc);
+      }
+    }
+    for (size_t j = l; j <= hi; j++) h(j, j) += mu;
+  }
+  w.resize(n);
+  for (size_t i = 0; i < n; i++) w[i] = h(i, i);
+  return true;
+}
+}  // namespace
+
+bool invertMatrix(size_t n, const std::vector<double>& A, std::vector<double>& Ainv) {
+  std::vector<double> M(A);
+  Ainv.assign(n * n, 0.);
+  for (size_t i = 0; i < n; i++) Ainv[i * n + i] = 1.;
+  double amax = 0.;
+  for (double x : A) amax = std::max(amax, std::fabs(x));
+  for (size_t k = 0; k < n; k++) {
+    size_t p = k;
+    for (size_t i = k + 1; i < n; i++)
+      if (std::fabs(M[i * n + k]) > std::fabs(M[p * n + k])) p = i;
+    if (!(std::fabs(M[p * n + k]) > 1e-14 * amax)) return false;
+    if (p != k)
+      for (size_t j = 0; j < n; j++) {
+        std::swap(M[k * n + j], M[p * n + j]);
+        std::swap(Ainv[k * n + j], Ainv[p * n + j]);
+      }
+    const double piv = M[k * n + k];
+    for (size_t j = 0; j < n; j++) {
+      M[k * n + j] /= piv;
+      Ainv[k * n + j] /= piv;
+    }
+    for (size_t i = 0; i < n; i++) {
+      if (i == k) continue;
+      const double f = M[i * n + k];
+      if (f == 0.) continue;
+      for (size_t j = 0; j < n; j++) {
+        M[i * n + j] -= f * M[k * n + j];
+        Ainv[i * n + j] -= f * Ainv[k * n + j];
+      }
+    }
+  }
+  return true;
+}
+
+bool generalEigen(size_t n, const std::vector<double>& A, std::vector<double>& wr, std::vector<double>& wi,
+                  std::vector<double>& V) {
+  std::vector<cd> H(A.begin(), A.end()), w;
+  if (!complexEigenvalues(n, H, w)) return false;
+  double anorm = 0.;
+  for (double x : A) anorm = std::max(anorm, std::fabs(x));
+  if (anorm == 0.) anorm = 1.;
+  const double imTol = 1e-10 * anorm;
+  for (cd& z : w)
+    if (std::fabs(z.imag()) <= imTol) z = cd(z.real(), 0.);
+  // order: the Schur diagonal's, each complex pair as (a + ib, a - ib), b > 0
+  std::vector<char> used(n, 0);
+  std::vector<cd> order;
+  for (size_t i = 0; i < n; i++) {
+    if (used[i]) continue;
+    used[i] = 1;
+    if (w[i].imag() == 0.) {
+      order.push_back(w[i]);
+      continue;
+    }
+    size_t best = n;
+    for (size_t j = 0; j < n; j++)
+      if (!used[j] && w[j].imag() != 0. &&
+          (best == n || std::abs(w[j] - std::conj(w[i])) < std::abs(w[best] - std::conj(w[i]))))
+        best = j;
+    if (best == n) return false;  // an unpaired complex eigenvalue of a real matrix
+    used[best] = 1;
+    // the pair's two computed members, averaged into an exact conjugate pair
+    const cd zm(0.5 * (w[i].real() + w[best].real()), 0.5 * (std::fabs(w[i].imag()) + std::fabs(w[best].imag())));
+    order.push_back(zm);
+    order.push_back(std::conj(zm));
+  }
+  wr.assign(n, 0.);
+  wi.assign(n, 0.);
+  V.assign(n * n, 0.);
+  std::vector<std::vector<cd> > found;  // eigenvectors so far (repeated eigenvalues deflate)
+  std::vector<cd> foundVal;
+  unsigned seed = 12345;
+  auto rnd = [&]() {
+    seed = seed * 1103515245u + 12345u;
+    return 0.5 + (double)((seed >> 8) & 0xffff) / 65536.;
+  };
+  for (size_t k = 0; k < n; k++) {
+    const cd lam = order[k];
+    wr[k] = lam.real();
+    wi[k] = lam.imag();
+    if (lam.imag() < 0.) continue;  // second of a pair: its columns were written with the first
+    std::vector<cd> M(n * n);
+    for (size_t i = 0; i < n; i++)
+      for (size_t j = 0; j < n; j++) M[i * n + j] = cd(A[i * n + j]) - (i == j ? lam : cd(0.));
+    std::vector<cd> x(n);
+    for (size_t i = 0; i < n; i++) x[i] = cd(rnd(), 0.);
+    for (int it = 0; it < 4; it++) {
+      complexSolve(n, M, x, 1e-14 * anorm);
+      for (size_t f = 0; f < found.size(); f++) {  // deflate against vectors of the same eigenvalue
+        if (std::abs(foundVal[f] - lam) > 1e-8 * anorm) continue;
+        cd dot = 0.;
+        double nn = 0.;
+        for (size_t i = 0; i < n; i++) {
+          dot += std::conj(found[f][i]) * x[i];
+          nn += std::norm(found[f][i]);
+        }
+        for (size_t i = 0; i < n; i++) x[i] -= dot / nn * found[f][i];
+      }
+      size_t p = 0;
+      for (size_t i = 1; i < n; i++)
+        if (std::abs(x[i]) > std::abs(x[p])) p = i;
+      const cd s = x[p];
+      if (std::abs(s) == 0. || !std::isfinite(std::abs(s))) return false;
+      for (size_t i = 0; i < n; i++) x[i] /= s;  // largest component 1 (real for a real eigenvalue)
+    }
+    found.push_back(x);
+    foundVal.push_back(lam);
+    if (lam.imag() == 0.) {
+      for (size_t i = 0; i < n; i++) V[i * n + k] = x[i].real();
+    } else {
+      if (k + 1 >= n) return false;
+      for (size_t i = 0; i < n; i++) {
+        V[i * n + k] = x[i].real();
+        V[i * n + k + 1] = x[i].imag();
+      }
+    }
+  }
+  return true;
+}
 
 }  // namespace bpp

@@ -169,7 +169,8 @@ void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
     plk_destroy(engine_);
     engine_ = nullptr;
   }
-  unsigned flags = (scaling_ ? (unsigned)PLK_FLAG_SCALING : 0u) | (nonNegGuard ? (unsigned)PLK_FLAG_NONNEG_GUARD : 0u) |
+  const bool scaling = scalingMode_ >= 0 ? scalingMode_ == 1 : nTips_ * std::log((double)nbStates_) > 300.;
+  unsigned flags = (scaling ? (unsigned)PLK_FLAG_SCALING : 0u) | (nonNegGuard ? (unsigned)PLK_FLAG_NONNEG_GUARD : 0u) |
                    extraFlags_;
   // usePatterns (the reference default): per-subtree site-pattern compression on the device
   // (DRASRTreeLikelihoodData.cpp:218-332, PLK_FLAG_SUBTREE_PATTERNS); not for the double-
@@ -288,7 +289,7 @@ void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& 
     std::vector<double> P(nbClasses_ * nbStates_ * nbStates_);
     for (size_t i = 0; i < br.size(); i++) {
       const SubstitutionModel* m = modelForIndex(mod[i]);
-      if (m && !m->isNonSingular()) {
+      if (m && m->needsHostPij()) {
         hostP_ = true;
         for (size_t c = 0; c < nbClasses_; c++) {
           const RowMatrix<double>& Pc = m->getPij_t(t[i] * rates[c]);
@@ -321,7 +322,7 @@ void AbstractPlkTreeLikelihood::refreshDerivativeMatrices() const {
     const int e = engineIndex_.at(n);
     if (!derivStale_[(size_t)e]) continue;
     const SubstitutionModel* m = modelForIndex(modelIndexForNode(n));
-    if (m && !m->isNonSingular()) continue;  // host P(t): numerical derivatives
+    if (m && m->needsHostPij()) continue;  // host P(t): numerical derivatives
     br.push_back(e);
     mod.push_back(modelIndexForNode(n));
     t.push_back(n->getDistanceToFather());
@@ -344,7 +345,7 @@ void AbstractPlkTreeLikelihood::evaluateTree(const std::vector<const Node*>& pno
     for (const Node* n : pnodes) {
       const int e = engineOf(n), mi = modelIndexForNode(n);
       const SubstitutionModel* m = modelForIndex(mi);
-      if (m && !m->isNonSingular()) {
+      if (m && m->needsHostPij()) {
         hostP_ = true;
         for (size_t c = 0; c < nbClasses_; c++) {
           const RowMatrix<double>& Pc = m->getPij_t(n->getDistanceToFather() * rates[c]);

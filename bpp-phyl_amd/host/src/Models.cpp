@@ -39,6 +39,7 @@ void SubstitutionModel::setScale(double scale) {
   for (size_t i = 0; i < size_; i++)
     for (size_t j = 0; j < size_; j++) generator_(i, j) *= scale;
   for (double& l : eigenValues_) l *= scale;
+  for (double& l : iEigenValues_) l *= scale;  // (Model/AbstractSubstitutionModel.cpp:654-662)
 }
 
 void SubstitutionModel::setDiagonal() {
@@ -87,11 +88,18 @@ void SubstitutionModel::checkEigen() {
     double qmax = 0., err = 0.;
     for (size_t i = 0; i < size_; i++)
       for (size_t j = 0; j < size_; j++) qmax = std::max(qmax, std::fabs(generator_(i, j)));
+    // the block-diagonal D of the decomposition (complex pairs as 2x2 blocks)
+    Vdouble up(size_, 0.);
+    for (size_t k = 0; k + 1 < size_; k++)
+      if (iEigenValues_[k] != 0. && iEigenValues_[k] == -iEigenValues_[k + 1]) up[k] = iEigenValues_[k];
     for (size_t i = 0; i < size_ && std::isfinite(err); i++)
       for (size_t j = 0; j < size_; j++) {
         double q = 0., id = 0.;
         for (size_t k = 0; k < size_; k++) {
-          q += rightEigenVectors_(i, k) * eigenValues_[k] * leftEigenVectors_(k, j);
+          double dk = eigenValues_[k] * leftEigenVectors_(k, j);
+          if (k + 1 < size_) dk += up[k] * leftEigenVectors_(k + 1, j);
+          if (k > 0) dk -= up[k - 1] * leftEigenVectors_(k - 1, j);
+          q += rightEigenVectors_(i, k) * dk;
           id += rightEigenVectors_(i, k) * leftEigenVectors_(k, j);
         }
         err = std::max(err, std::fabs(q - generator_(i, j)) / std::max(qmax, 1e-300));
@@ -133,10 +141,43 @@ const RowMatrix<double>& SubstitutionModel::getPij_t(double t) const {
     while (m-- > 0) matMul(pijt_, pijt_, pijt_);
     return pijt_;
   }
+  if (!isDiagonalizable_) {  // complex pairs (Model/AbstractSubstitutionModel.cpp:440-467)
+    Vdouble dia(size_), up(size_, 0.), lo(size_, 0.);
+    const double l = rate_ * t;
+    for (size_t i = 0; i < size_; i++) {
+      dia[i] = std::exp(eigenValues_[i] * l);
+      if (iEigenValues_[i] != 0. && i + 1 < size_) {
+        const double s = std::sin(iEigenValues_[i] * l), c = std::cos(iEigenValues_[i] * l);
+        up[i] = dia[i] * s;
+        lo[i] = -up[i];
+        dia[i] *= c;
+        dia[i + 1] = dia[i];
+        i++;
+      }
+    }
+    blockProduct(dia, up, lo, pijt_);
+    return pijt_;
+  }
   Vdouble w(size_);
   for (size_t k = 0; k < size_; k++) w[k] = std::exp(eigenValues_[k] * rate_ * t);
   eigenProduct(rightEigenVectors_, w, leftEigenVectors_, pijt_);
   return pijt_;
+}
+
+void SubstitutionModel::blockProduct(const Vdouble& dia, const Vdouble& up, const Vdouble& lo,
+                                     RowMatrix<double>& out) const {
+  const size_t n = size_;
+  for (size_t i = 0; i < n; i++)
+    for (size_t j = 0; j < n; j++) {
+      double s = 0.;
+      for (size_t k = 0; k < n; k++) {
+        double tk = dia[k] * leftEigenVectors_(k, j);
+        if (k + 1 < n) tk += up[k] * leftEigenVectors_(k + 1, j);
+        if (k > 0) tk += lo[k - 1] * leftEigenVectors_(k - 1, j);
+        s += rightEigenVectors_(i, k) * tk;
+      }
+      out(i, j) = s;
+    }
 }
 
 const RowMatrix<double>& SubstitutionModel::getdPij_dt(double t) const {
@@ -145,6 +186,26 @@ const RowMatrix<double>& SubstitutionModel::getdPij_dt(double t) const {
     matMul(generator_, P, dpijt_);
     for (size_t i = 0; i < size_; i++)
       for (size_t j = 0; j < size_; j++) dpijt_(i, j) *= rate_;
+    return dpijt_;
+  }
+  if (!isDiagonalizable_) {  // (:505-537)
+    Vdouble dia(size_), up(size_, 0.), lo(size_, 0.);
+    const double l = rate_ * t;
+    for (size_t i = 0; i < size_; i++) {
+      const double e = std::exp(eigenValues_[i] * l);
+      if (iEigenValues_[i] != 0. && i + 1 < size_) {
+        const double a = eigenValues_[i], b = iEigenValues_[i];
+        const double s = std::sin(b * l), c = std::cos(b * l);
+        dia[i] = rate_ * (a * c - b * s) * e;
+        up[i] = rate_ * (a * s + b * c) * e;
+        lo[i] = -up[i];
+        dia[i + 1] = dia[i];
+        i++;
+      } else {
+        dia[i] = rate_ * eigenValues_[i] * e;
+      }
+    }
+    blockProduct(dia, up, lo, dpijt_);
     return dpijt_;
   }
   Vdouble w(size_);
@@ -159,6 +220,28 @@ const RowMatrix<double>& SubstitutionModel::getd2Pij_dt2(double t) const {
     matMul(vPowGen_[2], P, d2pijt_);
     for (size_t i = 0; i < size_; i++)
       for (size_t j = 0; j < size_; j++) d2pijt_(i, j) *= rate_ * rate_;
+    return d2pijt_;
+  }
+  if (!isDiagonalizable_) {
+    // (:581-611), as the reference writes it: the super-diagonal term carries
+    // -2ab cos where the exact second derivative of e^{at} sin(bt) has +2ab cos
+    Vdouble dia(size_), up(size_, 0.), lo(size_, 0.);
+    const double l = rate_ * t, r2 = rate_ * rate_;
+    for (size_t i = 0; i < size_; i++) {
+      const double e = std::exp(eigenValues_[i] * l);
+      if (iEigenValues_[i] != 0. && i + 1 < size_) {
+        const double a = eigenValues_[i], b = iEigenValues_[i];
+        const double s = std::sin(b * l), c = std::cos(b * l);
+        dia[i] = r2 * ((a * a - b * b) * c - 2 * a * b * s) * e;
+        up[i] = r2 * ((a * a - b * b) * s - 2 * a * b * c) * e;
+        lo[i] = -up[i];
+        dia[i + 1] = dia[i];
+        i++;
+      } else {
+        dia[i] = r2 * eigenValues_[i] * eigenValues_[i] * e;
+      }
+    }
+    blockProduct(dia, up, lo, d2pijt_);
     return d2pijt_;
   }
   Vdouble w(size_);
@@ -208,12 +291,47 @@ void SubstitutionModel::computeEigen() {
     }
   }
   if (n > 0) eigenValues_[nullEig] = 0.;  // exact stationary eigenvalue (:358-361)
+  iEigenValues_.assign(size_, 0.);
   for (size_t s = 0; s < null.size(); s++) {
     rightEigenVectors_(null[s], n + s) = 1.;
     leftEigenVectors_(n + s, null[s]) = 1.;
   }
   isDiagonalizable_ = true;
   isNonSingular_ = true;
+  checkEigen();
+}
+
+void SubstitutionModel::computeEigenGeneral() {
+  const size_t n = size_;
+  std::vector<double> A(n * n), wr, wi, V, Vi;
+  for (size_t i = 0; i < n; i++)
+    for (size_t j = 0; j < n; j++) A[i * n + j] = generator_(i, j);
+  isNonSingular_ = isDiagonalizable_ = false;
+  eigenValues_.assign(n, 0.);
+  iEigenValues_.assign(n, 0.);
+  if (generalEigen(n, A, wr, wi, V) && invertMatrix(n, V, Vi)) {
+    for (size_t i = 0; i < n; i++) {
+      eigenValues_[i] = wr[i];
+      iEigenValues_[i] = wi[i];
+      for (size_t j = 0; j < n; j++) {
+        rightEigenVectors_(i, j) = V[i * n + j];
+        leftEigenVectors_(i, j) = Vi[i * n + j];
+      }
+    }
+    isDiagonalizable_ = true;
+    for (double b : iEigenValues_)
+      if (std::fabs(b) > NumConstants::TINY()) isDiagonalizable_ = false;
+    // the null eigenvalue: exactly one with |Re| < fact * SMALL and |Im| < SMALL, fact
+    // = 1, 10, 100, 1000 until one is found (:306-316)
+    std::vector<size_t> nulls;
+    for (double fact = 1.; nulls.empty() && fact <= 1000.; fact *= 10.)
+      for (size_t i = 0; i < n; i++)
+        if (std::fabs(eigenValues_[i]) < fact * NumConstants::SMALL() &&
+            std::fabs(iEigenValues_[i]) < NumConstants::SMALL())
+          nulls.push_back(i);
+    isNonSingular_ = nulls.size() == 1;
+    if (isNonSingular_) eigenValues_[nulls[0]] = iEigenValues_[nulls[0]] = 0.;
+  }
   checkEigen();
 }
 
@@ -288,6 +406,42 @@ const RowMatrix<double>& T92::getPij_t(double d) const {
 
 const RowMatrix<double>& T92::getdPij_dt(double d) const { return SubstitutionModel::getdPij_dt(d); }
 const RowMatrix<double>& T92::getd2Pij_dt2(double d) const { return SubstitutionModel::getd2Pij_dt2(d); }
+
+// ---------------------------------------------------------------------------
+// L95 (Model/Nucleotide/L95.cpp:56-119)
+// ---------------------------------------------------------------------------
+
+L95::L95(const NucleicAlphabet* alpha, double a, double b, double g, double kappa, double theta)
+    : SubstitutionModel(alpha, 4, "L95."), alpha_(a), beta_(b), gamma_(g), kappa_(kappa), theta_(theta) {
+  addParameter_(Parameter("L95.alpha", a, Parameter::PROP_CONSTRAINT_IN));
+  addParameter_(Parameter("L95.beta", b, Parameter::PROP_CONSTRAINT_IN));
+  addParameter_(Parameter("L95.gamma", g, Parameter::PROP_CONSTRAINT_IN));
+  addParameter_(Parameter("L95.kappa", kappa, std::make_shared<IntervalConstraint>(0., 1000., false, false, 1e-3)));
+  addParameter_(Parameter("L95.theta", theta, std::make_shared<IntervalConstraint>(0., 1., false, false, 1e-3)));
+  updateMatrices();
+}
+
+void L95::updateMatrices() {
+  alpha_ = getParameterValue("alpha");
+  beta_ = getParameterValue("beta");
+  gamma_ = getParameterValue("gamma");
+  kappa_ = getParameterValue("kappa");
+  theta_ = getParameterValue("theta");
+  const double a = alpha_, b = beta_, g = gamma_, k = kappa_, th = theta_;
+  freq_ = {(1. - th) / 2., th / 2., th / 2., (1. - th) / 2.};
+  const double Q[4][4] = {{-k * th - g, k * b * th, k * (1. - b) * th, g},
+                          {k * a * (1. - th), -k * (1. - th) + g - 1., 1. - g, k * (1. - th) * (1. - a)},
+                          {k * (1. - th) * (1. - a), 1. - g, -k * (1. - th) + g - 1., k * a * (1. - th)},
+                          {g, k * (1. - b) * th, k * b * th, -k * th - g}};
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) generator_(i, j) = Q[i][j];
+  setScale(1. / (2. * k * th * (1. - th) + g + th - 2. * th * g));
+  // AbstractSubstitutionModel::updateMatrices (:175-418): eigen-system of the generator,
+  // then the normalisation to one substitution per unit time
+  computeEigenGeneral();
+  normalize();
+  if (!isNonSingular_) checkEigen();  // the Taylor powers of the normalised generator
+}
 
 // ---------------------------------------------------------------------------
 // GTR

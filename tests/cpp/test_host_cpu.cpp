@@ -2,6 +2,7 @@
 // tests/test_host.py compares with the oracle and the golden fixtures.
 #include <Bpp/Phyl/Model/Codon/YN98.h>
 #include <Bpp/Phyl/Model/Nucleotide/GTR.h>
+#include <Bpp/Phyl/Model/Nucleotide/L95.h>
 #include <Bpp/Phyl/Model/Nucleotide/T92.h>
 #include <Bpp/Phyl/Model/Protein/LG08.h>
 #include <Bpp/Phyl/Model/RateDistribution/GammaDiscreteRateDistribution.h>
@@ -98,7 +99,29 @@ static void printModel(const char* name, const SubstitutionModel& m, const std::
     for (size_t i = 0; i < p.size(); i++) std::printf("%s%.17g", i ? ", " : "", p[i]);
     std::printf("]");
   }
-  std::printf("]}\n");
+  std::printf("]");
+  auto mats = [&](const char* key, int which) {
+    std::printf(", \"%s\": [", key);
+    for (size_t k = 0; k < ts.size(); k++) {
+      const RowMatrix<double>& P = which == 1 ? m.getdPij_dt(ts[k]) : m.getd2Pij_dt2(ts[k]);
+      std::printf("%s[", k ? ", " : "");
+      for (size_t i = 0; i < S * S; i++) std::printf("%s%.17g", i ? ", " : "", P.data()[i]);
+      std::printf("]");
+    }
+    std::printf("]");
+  };
+  mats("dP", 1);
+  mats("d2P", 2);
+  std::printf(", \"diagonalizable\": %s, \"nonsingular\": %s, ", m.isDiagonalizable() ? "true" : "false",
+              m.isNonSingular() ? "true" : "false");
+  printVec("wr", m.getEigenValues());
+  std::printf(", ");
+  printVec("wi", m.getIEigenValues());
+  std::printf(", ");
+  printVec("V", std::vector<double>(m.getColumnRightEigenVectors().data(), m.getColumnRightEigenVectors().data() + S * S));
+  std::printf(", ");
+  printVec("Vi", std::vector<double>(m.getRowLeftEigenVectors().data(), m.getRowLeftEigenVectors().data() + S * S));
+  std::printf("}\n");
 }
 
 int main() {
@@ -123,6 +146,15 @@ int main() {
     LG08 l(&AlphabetTools::PROTEIN_ALPHABET);
     l.forceTaylorForTests();
     printModel("LG08_taylor", l, ts);
+  }
+  // L95, non-reversible: complex eigenvalue pairs (block form) and a repeated eigenvalue
+  printModel("L95_complex", L95(dna, 0.9, 0.1, 0.3, 2.0, 0.4), ts);
+  printModel("L95_complex2", L95(dna, 0.95, 0.05, 0.9, 5.0, 0.3), ts);
+  printModel("L95_repeated", L95(dna, 0.5, 0.5, 0.5, 1.0, 0.5), ts);
+  {
+    L95 l(dna, 0.1, 0.9, 0.1, 3.0, 0.6);
+    l.setRate(1.7);
+    printModel("L95_rate", l, ts);
   }
   StandardGeneticCode gc(dna);
   printModel("YN98", YN98(&gc, std::vector<double>(), 2.0, 0.3), ts);

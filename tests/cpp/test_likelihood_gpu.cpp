@@ -11,6 +11,7 @@
 #include <Bpp/Phyl/Model/SubstitutionModelSetTools.h>
 #include <Bpp/Phyl/Likelihood/RHomogeneousTreeLikelihood.h>
 #include <Bpp/Phyl/Model/Nucleotide/GTR.h>
+#include <Bpp/Phyl/Model/Nucleotide/L95.h>
 #include <Bpp/Phyl/Model/Nucleotide/T92.h>
 #include <Bpp/Phyl/Model/RateDistribution/GammaDiscreteRateDistribution.h>
 #include <Bpp/Phyl/OptimizationTools.h>
@@ -19,6 +20,7 @@
 #include <Bpp/Seq/Container/VectorSiteContainer.h>
 
 #include <cmath>
+#include <functional>
 #include <string>
 
 #include "plk.h"
@@ -229,6 +231,87 @@ static void taylorModelCase() {
              a.getFirstOrderDerivative(bl[0].getName()), 1e-4);
 }
 
+// Felsenstein's pruning on the host with the model's own getPij_t (an independent check of
+// what the engine computes from host-uploaded P(t))
+static double hostPruningLnl(const TreeTemplate<Node>& tree, const SiteContainer& aln, const SubstitutionModel& m,
+                             const DiscreteDistribution& rd) {
+  const size_t S = m.getNumberOfStates();
+  double lnl = 0.;
+  for (size_t site = 0; site < aln.getNumberOfSites(); site++) {
+    double like = 0.;
+    for (size_t c = 0; c < rd.getNumberOfCategories(); c++) {
+      const double r = rd.getCategories()[c];
+      std::function<std::vector<double>(const Node*)> rec = [&](const Node* n) {
+        std::vector<double> L(S, 1.);
+        if (n->isLeaf()) {
+          const int st = aln.getSequence(n->getName()).getValue(site);
+          for (size_t i = 0; i < S; i++) L[i] = m.getInitValue(i, st);
+          return L;
+        }
+        for (size_t k = 0; k < n->getNumberOfSons(); k++) {
+          const Node* son = n->getSon(k);
+          const std::vector<double> Ls = rec(son);
+          const RowMatrix<double> P = m.getPij_t(son->getDistanceToFather() * r);
+          for (size_t x = 0; x < S; x++) {
+            double s = 0.;
+            for (size_t y = 0; y < S; y++) s += P(x, y) * Ls[y];
+            L[x] *= s;
+          }
+        }
+        return L;
+      };
+      const std::vector<double> L = rec(tree.getRootNode());
+      double s = 0.;
+      for (size_t x = 0; x < S; x++) s += m.freq(x) * L[x];
+      like += rd.getProbability(c) * s;
+    }
+    lnl += std::log(like);
+  }
+  return -lnl;
+}
+
+// A non-reversible model with a complex eigenvalue pair (L95, Model/Nucleotide/L95.cpp):
+// P(t) takes the block form of Model/AbstractSubstitutionModel.cpp:440-467 on the host and
+// reaches the engine through plk_set_pmatrix; checked against host pruning, against the
+// Taylor branch, and its branch-length derivative against a central difference.
+static void complexEigenModelCase() {
+  std::unique_ptr<TreeTemplate<Node> > tree(
+      TreeTemplateTools::parenthesisToTree("((A:0.01, B:0.02):0.03,C:0.01,D:0.1);"));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  const char* names[] = {"A", "B", "C", "D"};
+  const char* seqs[] = {"AAATGGCTGTGCACGTC", "GACTGGATCTGCACGTC", "CTCTGGATGTGCACGTG", "AAATGGCGGTGCGCCTA"};
+  for (int i = 0; i < 4; i++) aln.addSequence(BasicSequence(names[i], seqs[i], dna));
+  L95 blk(dna, 0.95, 0.05, 0.9, 5.0, 0.3);
+  L95 tay(dna, 0.95, 0.05, 0.9, 5.0, 0.3);
+  tay.forceTaylorForTests();
+  std::cout << "L95 diagonalizable " << blk.isDiagonalizable() << " nonsingular " << blk.isNonSingular()
+            << " imag " << blk.getIEigenValues()[0] << " " << blk.getIEigenValues()[1] << " "
+            << blk.getIEigenValues()[2] << " " << blk.getIEigenValues()[3] << std::endl;
+  if (blk.isDiagonalizable() || !blk.isNonSingular()) failures++;  // the block form must be in use
+  GammaDiscreteRateDistribution rdist(4, 0.7);
+  RHomogeneousTreeLikelihood a(*tree, aln, &blk, &rdist, true, false);
+  a.initialize();
+  RHomogeneousTreeLikelihood b(*tree, aln, &tay, &rdist, true, false);
+  b.initialize();
+  const double host = hostPruningLnl(*tree, aln, blk, rdist);
+  expectNear("L95 block-form P(t) through the engine vs host pruning: -lnL", a.getValue(), host, 1e-12 * host);
+  expectNear("L95 block form vs Taylor branch: -lnL", a.getValue(), b.getValue(), 1e-10 * host);
+  ParameterList bl = a.getBranchLengthsParameters();
+  const std::string v = bl[1].getName();
+  const double x = bl[1].getValue(), h = 1e-6;
+  ParameterList p = bl;
+  p[1].setValue(x + h);
+  a.setParameters(p);
+  const double fp = a.getValue();
+  p[1].setValue(x - h);
+  a.setParameters(p);
+  const double fm = a.getValue();
+  p[1].setValue(x);
+  a.setParameters(p);
+  expectNear("L95 d(-lnL)/dBrLen vs central difference", a.getFirstOrderDerivative(v), (fp - fm) / (2 * h), 1e-4);
+}
+
 // gaps are not allowed by the model: BadIntException like getInitValue
 static void gapCase() {
   std::unique_ptr<TreeTemplate<Node> > tree(TreeTemplateTools::parenthesisToTree("((A:0.1,B:0.2):0.1,C:0.3);"));
@@ -256,6 +339,7 @@ int main() {
     doubleRecursiveCase();
     nonHomogeneousDrCase();
     taylorModelCase();
+    complexEigenModelCase();
     gapCase();
   } catch (Exception& e) {
     std::cerr << e.what() << std::endl;

@@ -61,6 +61,60 @@ def test_host_taylor_branch_vs_expm_fixture(host_records, name):
         assert np.allclose(np.array(P).reshape(S, S), Pf, atol=1e-12)
 
 
+@pytest.mark.parametrize("name,complex_pair", [("L95_complex", True), ("L95_complex2", True),
+                                               ("L95_repeated", False), ("L95_rate", True)])
+def test_host_l95_nonreversible_pij(host_records, name, complex_pair):
+    """L95 (Model/Nucleotide/L95.cpp:56-119) is non-reversible: its eigen-system comes from
+    the general real decomposition (complex pairs as (Re v, Im v) column pairs, the
+    reference's EigenValue layout) and P(t), dP/dt take the block form of
+    Model/AbstractSubstitutionModel.cpp:440-467, 505-537 -- checked against scipy's expm
+    of r t Q.  d2P/dt2 follows the reference's block expression (:581-611), restated here
+    from the printed eigen-system; off the pair blocks it is r^2 Q^2 P."""
+    r = _models(host_records)[name]
+    S = 4
+    Q = np.array(r["Q"]).reshape(S, S)
+    pi = np.array(r["pi"])
+    rate = 1.7 if name == "L95_rate" else 1.0
+    assert r["nonsingular"] and r["diagonalizable"] == (not complex_pair)
+    assert abs(-np.dot(np.diag(Q), pi) - 1) < 1e-13        # normalised
+    assert np.allclose(pi @ Q, 0, atol=1e-13)               # pi stationary
+    if complex_pair:  # (the repeated-eigenvalue point is the symmetric corner of L95)
+        assert not np.allclose(pi[:, None] * Q, (pi[:, None] * Q).T)  # not reversible
+    wr, wi = np.array(r["wr"]), np.array(r["wi"])
+    V, Vi = np.array(r["V"]).reshape(S, S), np.array(r["Vi"]).reshape(S, S)
+    assert np.allclose(V @ Vi, np.eye(S), atol=1e-12)
+    ev = list(np.linalg.eigvals(Q))
+    for z in wr + 1j * wi:  # the same spectrum (matched one to one)
+        j = int(np.argmin([abs(z - e) for e in ev]))
+        assert abs(z - ev.pop(j)) < 1e-10
+    if complex_pair:
+        k = int(np.argmax(wi))
+        assert wi[k] > 0 and wi[k + 1] == -wi[k] and wr[k + 1] == wr[k]
+    for t, P, dP, d2P in zip(r["t"], r["P"], r["dP"], r["d2P"]):
+        E = expm(rate * t * Q)
+        assert np.allclose(np.array(P).reshape(S, S), E, atol=1e-12)
+        assert np.allclose(np.array(dP).reshape(S, S), rate * Q @ E, atol=1e-11)
+        # the reference's d2 block form
+        l = rate * t
+        dia, up = np.zeros(S), np.zeros(S - 1)
+        i = 0
+        while i < S:
+            e = np.exp(wr[i] * l)
+            if wi[i] != 0 and i + 1 < S:
+                a, b = wr[i], wi[i]
+                s, c = np.sin(b * l), np.cos(b * l)
+                dia[i] = dia[i + 1] = rate ** 2 * ((a * a - b * b) * c - 2 * a * b * s) * e
+                up[i] = rate ** 2 * ((a * a - b * b) * s - 2 * a * b * c) * e
+                i += 2
+            else:
+                dia[i] = rate ** 2 * wr[i] ** 2 * e
+                i += 1
+        T = np.diag(dia) + np.diag(up, 1) - np.diag(up, -1)
+        assert np.allclose(np.array(d2P).reshape(S, S), V @ T @ Vi, atol=1e-11)
+        if not complex_pair:
+            assert np.allclose(np.array(d2P).reshape(S, S), rate ** 2 * Q @ Q @ E, atol=1e-11)
+
+
 def test_host_yn98_properties(host_records):
     r = _models(host_records)["YN98"]
     Q = np.array(r["Q"]).reshape(64, 64)
