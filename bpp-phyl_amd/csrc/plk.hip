@@ -3007,16 +3007,13 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
   const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   const int n_blk = (int)(h->n_pad / (mfma ? 64 : kDrThreads));
   int rc;
-  if (mfma) {
-    // the sons' dP^T and d2P^T (P^T: ensure_pmatsT) for the matrix-core reduction
+  if (h->S == 64) {
+    // the sons' dP^T and d2P^T (P^T: ensure_pmatsT) for the 16x16x4 matrix-core reduction
     const size_t bytes = (size_t)nn * C * h->S * h->S * sizeof(double);
     if (!h->dpmatsT && (rc = dalloc(h, (void**)&h->dpmatsT, bytes))) return rc;
     if (!h->d2pmatsT && (rc = dalloc(h, (void**)&h->d2pmatsT, bytes))) return rc;
     const dim3 tg((unsigned)nn, (unsigned)C);
-    if (h->S == 20) {
-      transpose_pmats<20><<<tg, 256, 0, h->stream>>>(h->dpmats, h->dpmatsT, C);
-      transpose_pmats<20><<<tg, 256, 0, h->stream>>>(h->d2pmats, h->d2pmatsT, C);
-    } else {
+    if (h->S == 64) {  // (20 states read P, dP, d2P as stored)
       transpose_pmats<64><<<tg, 256, 0, h->stream>>>(h->dpmats, h->dpmatsT, C);
       transpose_pmats<64><<<tg, 256, 0, h->stream>>>(h->d2pmats, h->d2pmatsT, C);
     }
@@ -3063,12 +3060,16 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
 #define PLK_DRM(S_, C_)                                                                           \
   (sc ? dr_pre_m_kernel<S_, C_, true><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T)            \
       : dr_pre_m_kernel<S_, C_, false><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T))
-      if (h->S == 20) {
+      if (h->S == 20) {  // 4x4x4 matrix-core tiles, no padding (plk_dr.hpp: dr_pre_m20_kernel)
+#define PLK_DRM20(C_)                                                                         \
+  (sc ? dr_pre_m20_kernel<C_, true><<<grid, 256, 0, h->stream>>>(o, a)                       \
+      : dr_pre_m20_kernel<C_, false><<<grid, 256, 0, h->stream>>>(o, a))
         switch (C) {
-          case 1: PLK_DRM(20, 1); break;
-          case 2: PLK_DRM(20, 2); break;
-          case 4: PLK_DRM(20, 4); break;
+          case 1: PLK_DRM20(1); break;
+          case 2: PLK_DRM20(2); break;
+          case 4: PLK_DRM20(4); break;
         }
+#undef PLK_DRM20
       } else {
         switch (C) {
           case 1: PLK_DRM(64, 1); break;

@@ -734,6 +734,178 @@ __global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused preorder for 20 states on v_mfma_f64_4x4x4_4b (plk_jitm.hpp's layout): 20 states
+// tile as 5 x 4 with no padding, where dr_pre_m_kernel's 16x16x4 tiles pad 20 to 32 in both
+// dimensions (39 % useful flops).  Lane l = 16 hi + 4 b + lo of wave w holds states
+// 4X + hi (X = 0..4) of pattern 16 w + 4 b + lo; a matvec D = M v is, per X, five MFMAs
+// over Y with A(X, Y)[lo][hi] = M[4X + lo][4Y + hi] read from LDS, and v's register Y as
+// the B operand (D comes out in the same layout, so products chain in registers).  Per
+// class the workgroup stages the matrices of the op -- P_f (read transposed for
+// M_f = P_f^T) and each son's P, dP, d2P, as stored -- in LDS; the products, rescaling
+// and per-block branch terms are dr_pre_m_kernel's (same 64-pattern blocks).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double dr_mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int C, bool SCALE>
+__global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restrict__ ops, DrArgs a) {
+  constexpr int S = 20, XB = 5, SS = S * S, CS = C * S;
+  __shared__ double mats[10 * SS];  // [P_f | P_j, dP_j, d2P_j for j < 3] of one class
+  __shared__ double red[2][3][4];
+  const DrPreOp op = ops[blockIdx.y];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int hi = lane >> 4, lo = lane & 3;
+  const int64_t p = (int64_t)blockIdx.x * 64 + 16 * w + (lane & 15);
+  const bool live = p < a.n_patterns;
+  const int64_t tb = (p >> 7) * CS * kTile + (p & (kTile - 1)) + (int64_t)hi * kTile;
+  const bool root = op.uf_slot < 0;
+  const int nm = 1 + 3 * op.n;
+  double l0[3] = {0.0, 0.0, 0.0}, l1[3] = {0.0, 0.0, 0.0}, l2[3] = {0.0, 0.0, 0.0};
+  double umax[3] = {0.0, 0.0, 0.0};
+  // D = M v for M at LDS matrix m (as stored, or transposed)
+  auto matvec = [&](double (&d)[XB], const double (&v)[XB], int m, bool transposed) {
+    const double* M = mats + m * SS;
+#pragma unroll
+    for (int X = 0; X < XB; ++X) {
+      double acc = 0.0;
+#pragma unroll
+      for (int Y = 0; Y < XB; ++Y)
+        acc = dr_mfma4(transposed ? M[(4 * Y + hi) * S + 4 * X + lo] : M[(4 * X + lo) * S + 4 * Y + hi], v[Y], acc);
+      d[X] = acc;
+    }
+  };
+  auto loadL = [&](int j, int c, double (&v)[XB]) {
+    if (op.is_tip[j]) {
+      const double* row = a.code_table + (int64_t)a.codes[(int64_t)op.idx[j] * a.n_pad + p] * S + hi;
+#pragma unroll
+      for (int X = 0; X < XB; ++X) v[X] = row[4 * X];
+    } else {
+      const double* L = a.partials + (int64_t)op.idx[j] * a.slot_stride + tb + (int64_t)c * S * kTile;
+#pragma unroll
+      for (int X = 0; X < XB; ++X) v[X] = L[(int64_t)(4 * X) * kTile];
+    }
+  };
+  auto dot = [&](const double (&u)[XB], const double (&t)[XB]) {
+    double s = 0.0;
+#pragma unroll
+    for (int X = 0; X < XB; ++X) s = fma(u[X], t[X], s);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    return s;
+  };
+#pragma unroll 1
+  for (int c = 0; c < C; ++c) {
+    __syncthreads();  // the previous class is done with mats
+    for (int e = tid; e < nm * SS; e += 256) {
+      const int m = e / SS, k = e - m * SS;
+      const int j = (m - 1) / 3, kind = (m - 1) - 3 * j;
+      // (selects, not op.son[j]: a runtime index would put the op in scratch memory)
+      const int son = j == 0 ? op.son[0] : j == 1 ? op.son[1] : op.son[2];
+      const double* src = m == 0 ? a.pmats + ((size_t)op.f * C + c) * SS
+                                 : (kind == 0 ? a.pmats : kind == 1 ? a.dpmats : a.d2pmats) +
+                                       ((size_t)son * C + c) * SS;
+      mats[e] = (m == 0 && root) ? 0.0 : src[k];
+    }
+    __syncthreads();
+    double mu[XB];
+    if (root) {
+#pragma unroll
+      for (int X = 0; X < XB; ++X) mu[X] = a.pi[4 * X + hi];
+    } else {
+      const double* U = a.partials + (int64_t)op.uf_slot * a.slot_stride + tb + (int64_t)c * S * kTile;
+      double uf[XB];
+#pragma unroll
+      for (int X = 0; X < XB; ++X) uf[X] = U[(int64_t)(4 * X) * kTile];
+      matvec(mu, uf, 0, true);  // M_f U_f = P_f^T U_f
+    }
+    double Q[3][XB];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j >= op.n) continue;
+      double L[XB];
+      loadL(j, c, L);
+      matvec(Q[j], L, 1 + 3 * j, false);
+    }
+    const double pc = a.probs[c];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i >= op.n) continue;
+      double u[XB];
+#pragma unroll
+      for (int X = 0; X < XB; ++X) {
+        u[X] = mu[X];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          if (j != i && j < op.n) u[X] *= Q[j][X];
+      }
+      if (op.uslot[i] >= 0) {
+        double* dst = a.uout + (int64_t)op.uslot[i] * a.slot_stride + tb + (int64_t)c * S * kTile;
+#pragma unroll
+        for (int X = 0; X < XB; ++X) {
+          dst[(int64_t)(4 * X) * kTile] = u[X];
+          if (SCALE) umax[i] = fmax(umax[i], u[X]);
+        }
+      }
+      const double s0 = dot(u, Q[i]);
+      double L[XB], t[XB];
+      loadL(i, c, L);
+      matvec(t, L, 2 + 3 * i, false);
+      const double s1 = dot(u, t);
+      matvec(t, L, 3 + 3 * i, false);
+      const double s2 = dot(u, t);
+      l0[i] = fma(pc, s0, l0[i]);
+      l1[i] = fma(pc, s1, l1[i]);
+      l2[i] = fma(pc, s2, l2[i]);
+    }
+  }
+  if (SCALE)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i >= op.n || op.uslot[i] < 0) continue;
+      double m = umax[i];
+      m = fmax(m, __shfl_xor(m, 16, 64));
+      m = fmax(m, __shfl_xor(m, 32, 64));
+      if (m > 0.0 && m < kScaleThr) {
+        double* dst = a.uout + (int64_t)op.uslot[i] * a.slot_stride + tb;
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int X = 0; X < XB; ++X) dst[(int64_t)(c * S + 4 * X) * kTile] *= kScaleUp;
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (i >= op.n) continue;
+    double r1 = 0.0, r2 = 0.0;
+    if (live && hi == 0) {
+      const double g = l1[i] / l0[i], hh = l2[i] / l0[i];
+      r1 = a.weights[p] * g;
+      r2 = a.weights[p] * (hh - g * g);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      r1 += __shfl_xor(r1, off, 64);
+      r2 += __shfl_xor(r2, off, 64);
+    }
+    if (lane == 0) {
+      red[0][i][w] = r1;
+      red[1][i][w] = r2;
+    }
+  }
+  __syncthreads();
+  if (tid < 3 && tid < op.n) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < 4; ++k) {  // fixed order
+      t1 += red[0][tid][k];
+      t2 += red[1][tid][k];
+    }
+    const int b = tid == 0 ? op.bidx[0] : tid == 1 ? op.bidx[1] : op.bidx[2];
+    a.blk1[(size_t)b * a.n_blk + blockIdx.x] = t1;
+    a.blk2[(size_t)b * a.n_blk + blockIdx.x] = t2;
+  }
+}
+
 __global__ __launch_bounds__(256) void dr_sum_kernel(const DrBranch* __restrict__ branches, const double* __restrict__ blk1,
                                                      const double* __restrict__ blk2, int n_blk, double* __restrict__ out1,
                                                      double* __restrict__ out2) {
