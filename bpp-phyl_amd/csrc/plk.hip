@@ -1966,6 +1966,10 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.L = tune_int("JITM_L", 1, 1, 4);
     msh.minw = tune_int("JITM_MINW", 2, 1, 8);
     msh.pd = tune_int("JITM_PD", 1, 1, 3);
+    // contraction issue order (plk_jitm.hpp CONTRIB; all orders give the same sums) and the
+    // two-stage operand fetch's code lookahead (0: code and row loaded together)
+    msh.pipe = tune_int("JITM_PIPE", 1, 0, 2);
+    msh.lc = tune_int("JITM_LC", 3, 0, 6);
     // 16-pattern waves per workgroup: 4 (64 patterns) or 8 (128; every P(t) staging and its
     // barrier serve twice the patterns)
     msh.G = tune_int("JITM_G", 4, 4, 8) >= 8 ? 8 : 4;

@@ -113,11 +113,18 @@ struct JitMShape {
   int minw = 2;      // __launch_bounds__ min waves per SIMD
   int pd = 1;        // P(t) staging prefetch distance (contractions ahead)
   int G = 4;         // waves (16-pattern groups) per workgroup: 64 patterns (4) or 128 (8)
+  int lc = 3;        // two-stage fetch: codes lc events ahead, rows L ahead (0: one stage)
+  int pipe = 1;      // contraction order: 0 = per output block, 1 = Y-outer with A read ahead,
+                     // 2 = 1 with the read / MFMA groups pinned (sched_group_barrier)
   int pb() const { return C * S * S; }  // doubles of P(t) per branch (every class)
-  size_t lds_bytes() const { return (size_t)(2 * pb() + 16 * G) * sizeof(double); }
+  // LDS buffer stride: pb() rounded up to whole staging rounds, so that every thread stores
+  // unconditionally (a guarded last store is a divergent branch, and the wait-count pass
+  // then drains every outstanding load, the operand prefetches included, before it)
+  int pbs() const { const int nth = 64 * G; return (pb() + nth - 1) / nth * nth; }
+  size_t lds_bytes() const { return (size_t)(2 * pbs() + 16 * G) * sizeof(double); }
   bool operator==(const JitMShape& o) const {
     return S == o.S && C == o.C && U == o.U && scale == o.scale && L == o.L && minw == o.minw && pd == o.pd &&
-           G == o.G;
+           G == o.G && pipe == o.pipe && lc == o.lc;
   }
 };
 
@@ -133,24 +140,48 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   const int NTH = 64 * sh.G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH;
   snprintf(buf, sizeof(buf),
            "#define S_ %d\n#define C_ %d\n#define XB_ %d\n#define U_ %d\n#define U2_ %d\n#define G_ %d\n"
-           "#define NTH_ %d\n#define PB_ %d\n#define PF_ %d\n#define SC_ %s\n",
-           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, PF, sh.scale ? "true" : "false");
+           "#define NTH_ %d\n#define PB_ %d\n#define PBS_ %d\n#define PF_ %d\n#define SC_ %s\n#define PIPE_ %d\n",
+           S, C, XB, sh.U, sh.U * sh.U, sh.G, NTH, PB, sh.pbs(), PF, sh.scale ? "true" : "false", sh.pipe);
   s += buf;
   s += R"PLKJITM(
 // P(t) of branch b (all classes, [c][x][y]) -> registers -> LDS buffer bf, as stored
 #define PSTAGE_LOAD(R, b) { const double* s_ = a.pmats + (i64)(b) * PB_; \
   _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) { const int e_ = tid + j_ * NTH_; R[j_] = s_[e_ < PB_ ? e_ : PB_ - 1]; } }
-#define PSTAGE_STORE(R, bf) { double* d_ = lds + (bf) * PB_; \
-  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) { \
-    const int e_ = tid + j_ * NTH_; if (PB_ % NTH_ == 0 || e_ < PB_) d_[e_] = R[j_]; } }
+#define PSTAGE_STORE(R, bf) { double* d_ = lds + (bf) * PBS_; \
+  _Pragma("unroll") for (int j_ = 0; j_ < PF_; ++j_) d_[tid + j_ * NTH_] = R[j_]; }
 // D[c][X] (*)= sum_Y A(c, X, Y) . SRC[c][Y]   (SET: D was 1); lane (hi, lo) reads
 // A(c, X, Y)[lo][hi] = P_c[4X + lo][4Y + hi] at a constant offset from its lane base PA
+#if PIPE_ == 0
 #define CONTRIB(D, SRC, bf, SET) { \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { \
     double d_ = 0.0; \
     _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) \
-      d_ = mfma4(PA[(bf) * PB_ + (c_ * S_ + 4 * X_) * S_ + 4 * Y_], SRC[c_][Y_], d_); \
+      d_ = mfma4(PA[(bf) * PBS_ + (c_ * S_ + 4 * X_) * S_ + 4 * Y_], SRC[c_][Y_], d_); \
     if (SET) D[c_][X_] = d_; else D[c_][X_] *= d_; } }
+#else
+// the same sums (each output block accumulates Y = 0..4 in order, so results are bitwise
+// those of PIPE_ 0), issued Y-outer: the five output blocks' MFMAs are independent of each
+// other, and the A operands of step Y + 1 are read from LDS while step Y's MFMAs run
+#define CONTRIB(D, SRC, bf, SET) { \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) { \
+    const double* pa_ = PA + (bf) * PBS_ + c_ * S_ * S_; \
+    double acc_[XB_], an_[XB_]; \
+    _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) an_[X_] = pa_[4 * X_ * S_]; \
+    _Pragma("unroll") for (int Y_ = 0; Y_ < XB_; ++Y_) { \
+      double ac_[XB_]; \
+      _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) ac_[X_] = an_[X_]; \
+      if (Y_ + 1 < XB_) { _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) an_[X_] = pa_[4 * X_ * S_ + 4 * (Y_ + 1)]; } \
+      _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) acc_[X_] = mfma4(ac_[X_], SRC[c_][Y_], Y_ ? acc_[X_] : 0.0); \
+      PIPE_GROUPS(Y_) \
+    } \
+    _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) { if (SET) D[c_][X_] = acc_[X_]; else D[c_][X_] *= acc_[X_]; } } }
+#if PIPE_ == 2
+#define PIPE_GROUPS(Y) { if ((Y) + 1 < XB_) __builtin_amdgcn_sched_group_barrier(0x100, XB_, 0); \
+  __builtin_amdgcn_sched_group_barrier(0x008, XB_, 0); }
+#else
+#define PIPE_GROUPS(Y)
+#endif
+#endif
 #define ROWMUL(D, F, SET) { _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") \
   for (int X_ = 0; X_ < XB_; ++X_) { if (SET) D[c_][X_] = F[c_][X_]; else D[c_][X_] *= F[c_][X_]; } }
 // one row of cherry k's contribution table (combined code of the pattern's two tips)
@@ -160,6 +191,21 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
     F[c_][X_] = r_[(i64)c_ * (U2_ * S_) + 4 * X_]; \
   if (SC_) FK = (int)base_[a.cherry_table_bytes + code_]; }
+// two-stage operand fetch (JitMShape::lc > 0): a table row's code is loaded lc events
+// ahead (CHERRY_CODE / TIP_CODE, one VGPR), its row L events ahead from that code -- so no
+// row load waits on a code load issued just before it (vmcnt counts in issue order: such a
+// wait also drains every load issued earlier, the P(t) staging of the contraction included)
+#define CHERRY_CODE(Q, k) { Q = reinterpret_cast<const u16*>(a.cherry + (i64)(k) * a.cherry_stride + \
+  a.cherry_table_bytes + a.cherry_count_bytes)[p]; }
+#define CHERRY_ROW(F, FK, k, Q) { const u8* base_ = a.cherry + (i64)(k) * a.cherry_stride; \
+  const double* r_ = reinterpret_cast<const double*>(base_) + (i64)(Q) * S_ + hi; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
+    F[c_][X_] = r_[(i64)c_ * (U2_ * S_) + 4 * X_]; \
+  if (SC_) FK = (int)base_[a.cherry_table_bytes + (Q)]; }
+#define TIP_CODE(Q, t) { Q = a.codes[(i64)(t) * a.n_pad + p]; }
+#define TIP_ROW(F, t, Q) { const double* r_ = a.tipP + ((i64)(t) * (C_ * U_) + (Q)) * S_ + hi; \
+  _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
+    F[c_][X_] = r_[(i64)c_ * (U_ * S_) + 4 * X_]; }
 #define TIP_FETCH(F, t) { const int code_ = a.codes[(i64)(t) * a.n_pad + p]; \
   const double* r_ = a.tipP + ((i64)(t) * (C_ * U_) + code_) * S_ + hi; \
   _Pragma("unroll") for (int c_ = 0; c_ < C_; ++c_) _Pragma("unroll") for (int X_ = 0; X_ < XB_; ++X_) \
@@ -210,8 +256,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
            "extern \"C\" __global__ __launch_bounds__(%d, %d) void plk_jit_treeM(JMArgs a, int frag_base) {\n", NTH,
            std::max(sh.minw, 1));
   s += buf;
-  s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PB_] P tiles | red[16 G_]
-  double* red = lds + 2 * PB_;
+  s += R"PLKJITM(  extern __shared__ __attribute__((aligned(16))) double lds[];  // [2][PBS_] P(t) | red[16 G_]
+  double* red = lds + 2 * PBS_;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 4, pl = lane & 15;
@@ -241,6 +287,11 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     snprintf(buf, sizeof(buf), "  double F%d[C_][XB_]; int FK%d = 0; (void)FK%d;\n", r, r, r);
     s += buf;
   }
+  const int LC = sh.lc > L ? sh.lc : 0, NQ = LC ? LC - L + 1 : 0;  // code lookahead, code ring
+  for (int q = 0; q < NQ; ++q) {
+    snprintf(buf, sizeof(buf), "  int QC%d = 0; (void)QC%d;\n", q, q);
+    s += buf;
+  }
   s += "  switch (frag) {\n";
   for (size_t f = 0; f < starts.size(); ++f) {
     std::vector<TInstr> ev;
@@ -258,6 +309,31 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
       }
       if (op == T_LOAD || (op == T_ASCEND && ev[i].b >= 0)) pchain.push_back((int)i);
     }
+    // two-stage: fetcher m's code at fetcher m - LC's event, its row at fetcher m - L's
+    auto emit_code = [&](size_t m) {
+      if (!LC || m >= fetchers.size()) return;
+      const TInstr& e = ev[(size_t)fetchers[m]];
+      const int q = (int)(m % (size_t)NQ);
+      if (e.op == T_CHERRY)
+        snprintf(buf, sizeof(buf), "    CHERRY_CODE(QC%d, %d)\n", q, e.a);
+      else if (e.op == T_TIP)
+        snprintf(buf, sizeof(buf), "    TIP_CODE(QC%d, %d)\n", q, e.a);
+      else
+        return;
+      s += buf;
+    };
+    auto emit_row = [&](size_t m) {
+      if (m >= fetchers.size()) return;
+      const TInstr& e = ev[(size_t)fetchers[m]];
+      const int sl = slot[(size_t)fetchers[m]], q = (int)(m % (size_t)NQ);
+      if (e.op == T_CHERRY)
+        snprintf(buf, sizeof(buf), "    CHERRY_ROW(F%d, FK%d, %d, QC%d)\n", sl, sl, e.a, q);
+      else if (e.op == T_TIP)
+        snprintf(buf, sizeof(buf), "    TIP_ROW(F%d, %d, QC%d)\n", sl, e.a, q);
+      else
+        snprintf(buf, sizeof(buf), "    LOAD_FETCH(F%d, FK%d, %d)\n", sl, sl, e.a);
+      s += buf;
+    };
     auto emit_fetch = [&](int i) {
       const TInstr& e = ev[(size_t)i];
       const int sl = slot[(size_t)i];
@@ -272,7 +348,13 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     snprintf(buf, sizeof(buf), "  case %zu: {\n", f);
     s += buf;
     size_t nf = 0;
-    for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
+    if (LC) {
+      for (size_t m = 0; m < (size_t)LC; ++m) emit_code(m);
+      for (size_t m = 0; m < (size_t)L; ++m) emit_row(m);
+    } else {
+      for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
+    }
+    size_t nfetch = 0;  // fetchers consumed (two-stage)
     int cur = 0;
     size_t np = 0;  // P-chain events consumed
     const int PD = std::min(std::max(sh.pd, 1), 3);
@@ -307,7 +389,13 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     for (size_t i = 0; i < ev.size(); ++i) {
       const TInstr& e = ev[i];
       if (e.op == T_CHERRY || e.op == T_TIP || e.op == T_LOAD) {
-        if (nf < fetchers.size()) emit_fetch(fetchers[nf++]);
+        if (LC) {
+          emit_code(nfetch + (size_t)LC);
+          emit_row(nfetch + (size_t)L);
+          ++nfetch;
+        } else if (nf < fetchers.size()) {
+          emit_fetch(fetchers[nf++]);
+        }
         const int sl = slot[i];
         if (e.op == T_LOAD) {
           snprintf(buf, sizeof(buf), "    CONTRIB(A%d, F%d, %d, %s)\n", d, sl, cur, fresh[(size_t)d] ? "true" : "false");

@@ -5,6 +5,7 @@
 //   jit_emit <tree4|treeM> <C> <scale 0|1> [S (treeM: 20 | 4)] > kernel.hip
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -23,7 +24,7 @@ int main(int argc, char** argv) {
   // treeM programs carry unstored cherries as T_CHERRY rows instead.
   std::vector<TInstr> prog;
   auto add = [&](int op, int d, int a, int b) { prog.push_back(TInstr{op, d, a, b}); };
-  const bool m = kind == "treeM";
+  const bool m = kind == "treeM" || kind == "treeM_deep";
   if (m) {
     add(T_CHERRY, 0, 0, 8);
     add(T_CHERRY, 0, 1, 9);
@@ -52,7 +53,29 @@ int main(int argc, char** argv) {
   add(T_LOAD, 1, 0, 10);
   add(T_ASCEND, 1, 1, 11);
   add(T_ROOT, 0, -1, 1);
-  const std::vector<int32_t> starts = {0, start1};
+  std::vector<int32_t> starts = {0, start1};
+  // treeM_deep <height>: one fragment over a balanced subtree of that height (cherries as
+  // table rows), i.e. height - 1 register levels below the root -- the register pressure of
+  // a real cfg3 fragment (DM 4: height 5)
+  if (kind == "treeM_deep") {
+    prog.clear();
+    const int height = argc > 5 ? std::atoi(argv[5]) : 5;
+    int next_cherry = 0, next_node = 1000;
+    std::function<void(int, int)> sub = [&](int h, int d) {  // a child of height h at level d
+      if (h == 1) {
+        add(T_CHERRY, d, next_cherry++, next_node++);
+        return;
+      }
+      add(T_DESCEND, d + 1, 0, 0);
+      sub(h - 1, d + 1);
+      sub(h - 1, d + 1);
+      add(T_ASCEND, d + 1, -1, next_node++);
+    };
+    sub(height - 1, 0);
+    sub(height - 1, 0);
+    add(T_ROOT, 0, 0, 1);
+    starts = {0};
+  }
   std::string src;
   if (m) {
     JitMShape sh;
@@ -60,6 +83,8 @@ int main(int argc, char** argv) {
     sh.C = C;
     sh.U = 16;
     sh.scale = scale;
+    if (const char* e = std::getenv("JIT_EMIT_PIPE")) sh.pipe = std::atoi(e);
+    if (const char* e = std::getenv("JIT_EMIT_LC")) sh.lc = std::atoi(e);
     src = jit_treeM4_source(prog, starts, sh);
   } else {
     JitShape sh;

@@ -1114,6 +1114,30 @@ def test_jit_treeM_register_depths(dm, L, pd, g, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pipe,lc", [("0", "0"), ("1", "0"), ("2", "3"), ("1", "5"), ("0", "3")])
+def test_jit_treeM_issue_orders_bitwise(pipe, lc, monkeypatch):
+    """jit_treeM's contraction issue orders (JITM_PIPE: per output block / Y-outer with the A
+    operands read ahead / the same with pinned schedule groups) and operand fetch schedules
+    (JITM_LC: code and row together, or the code LC events ahead) run the same operations on
+    the same values: lnL, per-pattern lnL and block sums bitwise equal to the defaults, on a
+    random tree with tips, cherries, fragment roots, ambiguity codes and rescaling."""
+    et, m, alph, rates, probs, states = _random_problem(20, 4, 60, 700, seed=81, amb=True)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
+    out = []
+    for tune in ({}, {"JITM_PIPE": pipe, "JITM_LC": lc}):
+        for k in ("JITM_PIPE", "JITM_LC"):
+            clear_tune(monkeypatch, k)
+        for k, v in tune.items():
+            set_tune(monkeypatch, k, v)
+        eng = engine_for(et, 20, 4, 700, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+        out.append(run_engine(eng, et))
+        assert eng.kernel_path() == "jit_treeM"
+        del eng
+    (l0, s0, b0), (l1, s1, b1) = out
+    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode,nh", [
     (4, "balanced64", 3000, False, "lnl_only", False), (4, "balanced64", 1000, False, "materialize", False),
     (2, "caterpillar40", 700, True, "lnl_only", False), (4, "balanced300", 513, True, "lnl_only", True),
