@@ -2986,27 +2986,34 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
       br.push_back(b);
     }
   std::vector<DrPreOp> ops;
-  std::vector<std::pair<size_t, int> > levels;
-  for (size_t d = 0; d + 1 < depth.size(); ++d) {
-    const size_t first = ops.size();
-    for (int f : depth[d]) {
-      if (f < nt) continue;
-      DrPreOp op;
-      std::memset(&op, 0, sizeof(op));
-      op.f = f;
-      op.uf_slot = f == root ? -1 : h->dr_slot0 + f;
-      for (int v : h->topo_kids[f]) {
-        const int j = op.n++;
-        op.son[j] = v;
-        op.is_tip[j] = v < nt;
-        op.idx[j] = v < nt ? v : v - nt;
-        op.uslot[j] = v < nt ? -1 : h->dr_slot0 + v;
-        op.bidx[j] = bidx[v];
+  struct Level {
+    size_t first;
+    int count;
+    int ns;  // 2: every father of the launch has <= 2 sons (the MFMA kernels' NS)
+  };
+  std::vector<Level> levels;
+  for (size_t d = 0; d + 1 < depth.size(); ++d)
+    for (int ns = 2; ns <= 3; ++ns) {  // fathers of <= 2 sons first, then the others
+      const size_t first = ops.size();
+      for (int f : depth[d]) {
+        if (f < nt) continue;
+        if (((int)h->topo_kids[f].size() <= 2) != (ns == 2)) continue;
+        DrPreOp op;
+        std::memset(&op, 0, sizeof(op));
+        op.f = f;
+        op.uf_slot = f == root ? -1 : h->dr_slot0 + f;
+        for (int v : h->topo_kids[f]) {
+          const int j = op.n++;
+          op.son[j] = v;
+          op.is_tip[j] = v < nt;
+          op.idx[j] = v < nt ? v : v - nt;
+          op.uslot[j] = v < nt ? -1 : h->dr_slot0 + v;
+          op.bidx[j] = bidx[v];
+        }
+        ops.push_back(op);
       }
-      ops.push_back(op);
+      if (ops.size() > first) levels.push_back(Level{first, (int)(ops.size() - first), ns});
     }
-    if (ops.size() > first) levels.push_back(std::make_pair(first, (int)(ops.size() - first)));
-  }
   const bool mfma = h->S == 20 || h->S == 64;
   const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   const int n_blk = (int)(h->n_pad / (mfma ? 64 : kDrThreads));
@@ -3056,24 +3063,33 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
     ev = get_events(h, 0);
     hipEventRecord(ev.a, h->stream);
   }
-  for (const auto& l : levels) {
-    const dim3 grid((unsigned)n_blk, (unsigned)l.second);
+  for (const Level& l : levels) {
+    const dim3 grid((unsigned)n_blk, (unsigned)l.count);
     const DrPreOp* o = h->d_drpre + l.first;
     if (mfma) {
       const double *pT = h->pmatsT, *dT = h->dpmatsT, *d2T = h->d2pmatsT;
-#define PLK_DRM(S_, C_)                                                                           \
-  (sc ? dr_pre_m_kernel<S_, C_, true><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T)            \
-      : dr_pre_m_kernel<S_, C_, false><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T))
+#define PLK_DRM_NS(S_, C_, NS_)                                                                   \
+  (sc ? dr_pre_m_kernel<S_, C_, true, NS_><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T)       \
+      : dr_pre_m_kernel<S_, C_, false, NS_><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T))
+#define PLK_DRM(S_, C_) (l.ns == 2 ? PLK_DRM_NS(S_, C_, 2) : PLK_DRM_NS(S_, C_, 3))
+      // 64 states, one class, binary fathers: PLK_TUNE DR64_W2=1 builds for two waves per SIMD
+      // (256 registers: spills ~260 B per lane) instead of one (342 registers)
+      const bool w2 = h->S == 64 && C == 1 && l.ns == 2 && tune_is("DR64_W2", '1');
       if (h->S == 20) {  // 4x4x4 matrix-core tiles, no padding (plk_dr.hpp: dr_pre_m20_kernel)
-#define PLK_DRM20(C_)                                                                         \
-  (sc ? dr_pre_m20_kernel<C_, true><<<grid, 256, 0, h->stream>>>(o, a)                       \
-      : dr_pre_m20_kernel<C_, false><<<grid, 256, 0, h->stream>>>(o, a))
+#define PLK_DRM20_NS(C_, NS_)                                                                 \
+  (sc ? dr_pre_m20_kernel<C_, true, NS_><<<grid, 256, 0, h->stream>>>(o, a)                  \
+      : dr_pre_m20_kernel<C_, false, NS_><<<grid, 256, 0, h->stream>>>(o, a))
+#define PLK_DRM20(C_) (l.ns == 2 ? PLK_DRM20_NS(C_, 2) : PLK_DRM20_NS(C_, 3))
         switch (C) {
           case 1: PLK_DRM20(1); break;
           case 2: PLK_DRM20(2); break;
           case 4: PLK_DRM20(4); break;
         }
 #undef PLK_DRM20
+#undef PLK_DRM20_NS
+      } else if (w2) {
+        if (sc) dr_pre_m_kernel<64, 1, true, 2, 2><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T);
+        else dr_pre_m_kernel<64, 1, false, 2, 2><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T);
       } else {
         switch (C) {
           case 1: PLK_DRM(64, 1); break;
@@ -3082,6 +3098,7 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
         }
       }
 #undef PLK_DRM
+#undef PLK_DRM_NS
     } else if (sc) {
       switch (C) {
         case 1: dr_pre_s4_kernel<1, true><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;

@@ -572,14 +572,17 @@ __global__ __launch_bounds__(kDrThreads) void dr_pre_s4_kernel(const DrPreOp* __
 // waves share them.  Stored U is rescaled jointly over states and classes after the class
 // loop (in place, as dr_pre_s4_kernel<C, true>).  64-pattern blocks.
 // ---------------------------------------------------------------------------
-template <int S, int C, bool SCALE>
-__global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict__ ops, DrArgs a,
+template <int S, int C, bool SCALE, int NS, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void dr_pre_m_kernel(const DrPreOp* __restrict__ ops, DrArgs a,
                                                        const double* __restrict__ pT,
                                                        const double* __restrict__ dpT,
                                                        const double* __restrict__ d2pT) {
   constexpr int XT = MShape<S>::XT, CS = C * S;
   __shared__ double red[2][3][4];
   const DrPreOp op = ops[blockIdx.y];
+  // sons of the op: NS = 2 launches carry fathers of <= 2 sons, so the third son's
+  // registers and code vanish (64 states: 481 -> fewer registers, two waves per SIMD)
+  const int nsn = NS == 2 ? min(2, op.n) : op.n;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int lr = lane >> 4, lc = lane & 15;
   const int64_t p = (int64_t)blockIdx.x * 64 + 16 * w + lc;
@@ -641,7 +644,7 @@ __global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict
     MAcc<S> Q[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      if (j >= op.n) continue;
+      if (j >= nsn) continue;
       MAcc<S> L;
       loadL(j, c, L);
       f64x4m d[XT];
@@ -652,14 +655,14 @@ __global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict
     const double pc = a.probs[c];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      if (i >= op.n) continue;
+      if (i >= nsn) continue;
       MAcc<S> u;
 #pragma unroll
       for (int xt = 0; xt < XT; ++xt) {
         u[xt] = mu[xt];
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          if (j != i && j < op.n) u[xt] *= Q[j][xt];
+          if (j != i && j < nsn) u[xt] *= Q[j][xt];
       }
       if (op.uslot[i] >= 0) {
         double* dst = a.uout + (int64_t)op.uslot[i] * a.slot_stride + tb + (int64_t)c * S * kTile;
@@ -688,7 +691,7 @@ __global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict
   if (SCALE)
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      if (i >= op.n || op.uslot[i] < 0) continue;
+      if (i >= nsn || op.uslot[i] < 0) continue;
       double m = umax[i];
       m = fmax(m, __shfl_xor(m, 16, 64));
       m = fmax(m, __shfl_xor(m, 32, 64));
@@ -704,7 +707,7 @@ __global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict
     }
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    if (i >= op.n) continue;
+    if (i >= nsn) continue;
     double r1 = 0.0, r2 = 0.0;
     if (live && lr == 0) {
       const double g = l1[i] / l0[i], hh = l2[i] / l0[i];
@@ -722,15 +725,16 @@ __global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict
     }
   }
   __syncthreads();
-  if (threadIdx.x < 3 && (int)threadIdx.x < op.n) {
+  if (threadIdx.x < 3 && (int)threadIdx.x < nsn) {
     const int i = threadIdx.x;
     double t1 = 0.0, t2 = 0.0;
     for (int k = 0; k < 4; ++k) {  // fixed order
       t1 += red[0][i][k];
       t2 += red[1][i][k];
     }
-    a.blk1[(size_t)op.bidx[i] * a.n_blk + blockIdx.x] = t1;
-    a.blk2[(size_t)op.bidx[i] * a.n_blk + blockIdx.x] = t2;
+    const int bi = i == 0 ? op.bidx[0] : i == 1 ? op.bidx[1] : op.bidx[2];  // (no runtime index into op)
+    a.blk1[(size_t)bi * a.n_blk + blockIdx.x] = t1;
+    a.blk2[(size_t)bi * a.n_blk + blockIdx.x] = t2;
   }
 }
 
@@ -749,19 +753,20 @@ __device__ __forceinline__ double dr_mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 
-template <int C, bool SCALE>
+template <int C, bool SCALE, int NS>
 __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restrict__ ops, DrArgs a) {
   constexpr int S = 20, XB = 5, SS = S * S, CS = C * S;
   __shared__ double mats[10 * SS];  // [P_f | P_j, dP_j, d2P_j for j < 3] of one class
   __shared__ double red[2][3][4];
   const DrPreOp op = ops[blockIdx.y];
+  const int nsn = NS == 2 ? min(2, op.n) : op.n;  // (as dr_pre_m_kernel)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int hi = lane >> 4, lo = lane & 3;
   const int64_t p = (int64_t)blockIdx.x * 64 + 16 * w + (lane & 15);
   const bool live = p < a.n_patterns;
   const int64_t tb = (p >> 7) * CS * kTile + (p & (kTile - 1)) + (int64_t)hi * kTile;
   const bool root = op.uf_slot < 0;
-  const int nm = 1 + 3 * op.n;
+  const int nm = 1 + 3 * nsn;
   double l0[3] = {0.0, 0.0, 0.0}, l1[3] = {0.0, 0.0, 0.0}, l2[3] = {0.0, 0.0, 0.0};
   double umax[3] = {0.0, 0.0, 0.0};
   // D = M v for M at LDS matrix m (as stored, or transposed)
@@ -823,7 +828,7 @@ __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restri
     double Q[3][XB];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      if (j >= op.n) continue;
+      if (j >= nsn) continue;
       double L[XB];
       loadL(j, c, L);
       matvec(Q[j], L, 1 + 3 * j, false);
@@ -831,14 +836,14 @@ __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restri
     const double pc = a.probs[c];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      if (i >= op.n) continue;
+      if (i >= nsn) continue;
       double u[XB];
 #pragma unroll
       for (int X = 0; X < XB; ++X) {
         u[X] = mu[X];
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          if (j != i && j < op.n) u[X] *= Q[j][X];
+          if (j != i && j < nsn) u[X] *= Q[j][X];
       }
       if (op.uslot[i] >= 0) {
         double* dst = a.uout + (int64_t)op.uslot[i] * a.slot_stride + tb + (int64_t)c * S * kTile;
@@ -863,7 +868,7 @@ __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restri
   if (SCALE)
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      if (i >= op.n || op.uslot[i] < 0) continue;
+      if (i >= nsn || op.uslot[i] < 0) continue;
       double m = umax[i];
       m = fmax(m, __shfl_xor(m, 16, 64));
       m = fmax(m, __shfl_xor(m, 32, 64));
@@ -876,7 +881,7 @@ __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restri
     }
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    if (i >= op.n) continue;
+    if (i >= nsn) continue;
     double r1 = 0.0, r2 = 0.0;
     if (live && hi == 0) {
       const double g = l1[i] / l0[i], hh = l2[i] / l0[i];
@@ -894,7 +899,7 @@ __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restri
     }
   }
   __syncthreads();
-  if (tid < 3 && tid < op.n) {
+  if (tid < 3 && tid < nsn) {
     double t1 = 0.0, t2 = 0.0;
     for (int k = 0; k < 4; ++k) {  // fixed order
       t1 += red[0][tid][k];

@@ -18,6 +18,9 @@ import json
 for v in ('fused','levelwise'):
     d=json.load(open('gpurun_out/$P/${c}_'+v+'.json')); print('$c', v, round(d['dr_ms'],3), 'ms', d.get('dr_path'), 'maxrel', d['max_rel_diff_dr_vs_path'])"
 done
+PLK_TUNE=DR64_W2=1 timeout -k 10 300 python tools/bench_dr.py --config yn98_codon_50k_128 --reps 3 --path-branches 4 > gpurun_out/$P/cfg4_w2.json 2> gpurun_out/$P/cfg4_w2.err || { tail -5 gpurun_out/$P/cfg4_w2.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('gpurun_out/$P/cfg4_w2.json')); print('cfg4 DR64_W2', round(d['dr_ms'],3), 'ms maxrel', d['max_rel_diff_dr_vs_path'])"
 for c in cfg2 cfg3; do
   timeout -k 10 200 bpp-phyl_amd/host/bin/bench_mirror $c > gpurun_out/$P/mirror_$c.json || exit 1
   cat gpurun_out/$P/mirror_$c.json
