@@ -287,7 +287,9 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     snprintf(buf, sizeof(buf), "  double F%d[C_][XB_]; int FK%d = 0; (void)FK%d;\n", r, r, r);
     s += buf;
   }
-  const int LC = sh.lc > L ? sh.lc : 0, NQ = LC ? LC - L + 1 : 0;  // code lookahead, code ring
+  // code lookahead and code ring: the prologue loads the codes of fetchers 0 .. LC - 1
+  // before the first row, so the ring needs LC slots (LC - L + 1 suffice in steady state)
+  const int LC = sh.lc > L ? sh.lc : 0, NQ = LC;
   for (int q = 0; q < NQ; ++q) {
     snprintf(buf, sizeof(buf), "  int QC%d = 0; (void)QC%d;\n", q, q);
     s += buf;

@@ -85,6 +85,7 @@ int main(int argc, char** argv) {
     tl.setParameters(sets[(i + 1) & 1]);
     v += tl.getValue();
   }
+  plk_reset_timing(tl.getEngine());
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < steps; i++) {
     tl.setParameters(sets[(warmup + i + 1) & 1]);
@@ -92,6 +93,21 @@ int main(int argc, char** argv) {
   }
   const auto t1 = std::chrono::steady_clock::now();
   const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count() / steps;
+  // host segments of plk_evaluate over the timed steps ([5]: the mirror's own time between
+  // evaluations), then the traversal kernel time of the same steps under HIP events
+  plk_timing tm;
+  plk_get_timing_ex(tl.getEngine(), &tm);
+  const double ne = tm.evaluations > 0 ? (double)tm.evaluations : 1.0;
+  plk_set_timing(tl.getEngine(), PLK_TIME_PARTIALS | PLK_TIME_PMAT | PLK_TIME_ROOT | PLK_TIME_TABLES);
+  plk_reset_timing(tl.getEngine());
+  for (int i = 0; i < steps; i++) {
+    tl.setParameters(sets[(warmup + steps + i + 1) & 1]);
+    v += tl.getValue();
+  }
+  plk_timing tk;
+  plk_get_timing_ex(tl.getEngine(), &tk);
+  plk_set_timing(tl.getEngine(), 0);
+  const double nk = tk.evaluations > 0 ? (double)tk.evaluations : 1.0;
   const size_t D = tl.getNumberOfDistinctSites();
   const int internal = taxa - 2;
   const auto& st = tl.getEvaluationStats();
@@ -99,9 +115,13 @@ int main(int argc, char** argv) {
       "{\"bench\": \"mirror\", \"config\": \"%s\", \"taxa\": %d, \"sites\": %zu, \"distinct_patterns\": %zu, "
       "\"internal_nodes\": %d, \"steps\": %d, \"warmup\": %d, \"ms_per_step\": %.5f, \"updates_per_s\": %.6g, "
       "\"kernel_path\": \"%s\", \"minus_lnl\": %.12f, \"full_traversals\": %zu, \"evaluations\": %zu, "
-      "\"simulate_s\": %.2f, \"setup_s\": %.2f, \"checksum\": %.6f}\n",
+      "\"simulate_s\": %.2f, \"setup_s\": %.2f, \"checksum\": %.6f, \"host_us_per_eval\": {\"pmat_call\": %.2f, "
+      "\"traversal_call\": %.2f, \"blocks_call\": %.2f, \"wait\": %.2f, \"sum\": %.2f, \"caller\": %.2f}, "
+      "\"kernel_ms_per_eval\": {\"partials\": %.4f, \"tables\": %.4f, \"pmatrix\": %.4f, \"root\": %.4f}}\n",
       cfg.c_str(), taxa, P, D, internal, steps, warmup, ms, (double)D * internal / (ms * 1e-3),
       plk_kernel_path(tl.getEngine()), tl.getValue(), st.fullTraversals, st.evaluations,
-      std::chrono::duration<double>(c1 - c0).count(), std::chrono::duration<double>(c2 - c1).count(), v);
+      std::chrono::duration<double>(c1 - c0).count(), std::chrono::duration<double>(c2 - c1).count(), v,
+      tm.host_us[0] / ne, tm.host_us[1] / ne, tm.host_us[2] / ne, tm.host_us[3] / ne, tm.host_us[4] / ne,
+      tm.host_us[5] / ne, tk.partials_ms / nk, tk.tables_ms / nk, tk.pmat_ms / nk, tk.root_ms / nk);
   return 0;
 }
