@@ -1968,7 +1968,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.pd = tune_int("JITM_PD", 1, 1, 3);
     // contraction issue order (plk_jitm.hpp CONTRIB; all orders give the same sums) and the
     // two-stage operand fetch's code lookahead (0: code and row loaded together)
-    msh.pipe = tune_int("JITM_PIPE", 1, 0, 2);
+    msh.pipe = tune_int("JITM_PIPE", 2, 0, 2);
     msh.lc = tune_int("JITM_LC", 3, 0, 6);
     // 16-pattern waves per workgroup: 4 (64 patterns) or 8 (128; every P(t) staging and its
     // barrier serve twice the patterns)
@@ -3072,9 +3072,6 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
   (sc ? dr_pre_m_kernel<S_, C_, true, NS_><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T)       \
       : dr_pre_m_kernel<S_, C_, false, NS_><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T))
 #define PLK_DRM(S_, C_) (l.ns == 2 ? PLK_DRM_NS(S_, C_, 2) : PLK_DRM_NS(S_, C_, 3))
-      // 64 states, one class, binary fathers: PLK_TUNE DR64_W2=1 builds for two waves per SIMD
-      // (256 registers: spills ~260 B per lane) instead of one (342 registers)
-      const bool w2 = h->S == 64 && C == 1 && l.ns == 2 && tune_is("DR64_W2", '1');
       if (h->S == 20) {  // 4x4x4 matrix-core tiles, no padding (plk_dr.hpp: dr_pre_m20_kernel)
 #define PLK_DRM20_NS(C_, NS_)                                                                 \
   (sc ? dr_pre_m20_kernel<C_, true, NS_><<<grid, 256, 0, h->stream>>>(o, a)                  \
@@ -3087,9 +3084,6 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
         }
 #undef PLK_DRM20
 #undef PLK_DRM20_NS
-      } else if (w2) {
-        if (sc) dr_pre_m_kernel<64, 1, true, 2, 2><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T);
-        else dr_pre_m_kernel<64, 1, false, 2, 2><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T);
       } else {
         switch (C) {
           case 1: PLK_DRM(64, 1); break;
@@ -3172,10 +3166,15 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   }
   if ((rc = refresh_tip_tables(h))) return rc;
   if ((S == 20 || S == 64) && (rc = ensure_pmatsT(h))) return rc;
-  // 4, 20 and 64 states (1, 2 or 4 classes, any rescaling): the fused preorder
-  // (dr_pre_s4_kernel / dr_pre_m_kernel), one launch per level of fathers, branch terms
-  // reduced where U is formed (DR_PRE=0: the levelwise preorder + reduction below)
-  bool pre = (S == 4 || S == 20 || S == 64) && (C == 1 || C == 2 || C == 4) && !tune_is("DR_PRE", '0');
+  // 4 and 20 states (1, 2 or 4 classes, any rescaling): the fused preorder
+  // (dr_pre_s4_kernel / dr_pre_m20_kernel), one launch per level of fathers, branch terms
+  // reduced where U is formed (DR_PRE=0: the levelwise preorder + reduction below).  64
+  // states: levelwise by default -- dr_pre_m_kernel<64> holds 342 registers (one wave per
+  // SIMD) and ran cfg4's pass in 17.7 ms against 12.7 ms levelwise (profiles/r03/r3e);
+  // DR_PRE=1 selects it
+  const char* pre_key = tune_get("DR_PRE");
+  bool pre = (S == 4 || S == 20 || (S == 64 && pre_key && pre_key[0] == '1')) && (C == 1 || C == 2 || C == 4) &&
+             !(pre_key && pre_key[0] == '0');
   for (size_t d = 0; pre && d < depth.size(); ++d)
     for (int f : depth[d])
       if (f >= nt && (h->topo_kids[f].size() < 2 || h->topo_kids[f].size() > 3)) pre = false;

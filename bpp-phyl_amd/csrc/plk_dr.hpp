@@ -572,8 +572,8 @@ __global__ __launch_bounds__(kDrThreads) void dr_pre_s4_kernel(const DrPreOp* __
 // waves share them.  Stored U is rescaled jointly over states and classes after the class
 // loop (in place, as dr_pre_s4_kernel<C, true>).  64-pattern blocks.
 // ---------------------------------------------------------------------------
-template <int S, int C, bool SCALE, int NS, int MINW = 1>
-__global__ __launch_bounds__(256, MINW) void dr_pre_m_kernel(const DrPreOp* __restrict__ ops, DrArgs a,
+template <int S, int C, bool SCALE, int NS>
+__global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict__ ops, DrArgs a,
                                                        const double* __restrict__ pT,
                                                        const double* __restrict__ dpT,
                                                        const double* __restrict__ d2pT) {

@@ -519,10 +519,12 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   char buf[400];
   const std::string minw_s = sh.minw > 0 ? ", " + std::to_string(sh.minw) : std::string();
   // fragment table units (CSR) as constant data of the module: unit k of fragment f is
-  // entry kFragUnitStart[f] + k of kUnitTA / kUnitTB (-1: single tip) / kUnitOff
-  std::string ua = "};\n__device__ const int kUnitTA[] = {0", ub = "};\n__device__ const int kUnitTB[] = {0",
-              uo = "};\n__device__ const int kUnitOff[] = {0", ur = "};\n__device__ const int kUnitBr[] = {0",
-              uk = "};\n__device__ const int kUnitKOff[] = {0";
+  // entry kFragUnitStart[f] + k of kUnitD, one 32-byte record (ta, tb (-1: single tip), off,
+  // br, koff) read with ONE scalar load -- five separate arrays cost a chain of dependent
+  // scalar loads per unit (the branch on tb placed a wait before the next load), ~2.8 us
+  // per staging round at the start of every launch (profiles/r03/r3d sweep)
+  std::string ud = "};\nstruct __attribute__((aligned(32))) UnitD { int ta, tb, off, br, koff, p0, p1, p2; };\n"
+                   "__device__ const UnitD kUnitD[] = {{0, 0, 0, 0, 0, 0, 0, 0}";
   s += "\n__device__ const int kFragUnitStart[] = {0";
   {
     int acc = 0;
@@ -531,20 +533,12 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       snprintf(buf, sizeof(buf), ",%d", acc);
       s += buf;
       for (const JitUnit& u : un) {
-        snprintf(buf, sizeof(buf), ",%d", u.ta);
-        ua += buf;
-        snprintf(buf, sizeof(buf), ",%d", u.tb);
-        ub += buf;
-        snprintf(buf, sizeof(buf), ",%d", u.off);
-        uo += buf;
-        snprintf(buf, sizeof(buf), ",%d", u.br);
-        ur += buf;
-        snprintf(buf, sizeof(buf), ",%d", u.koff);
-        uk += buf;
+        snprintf(buf, sizeof(buf), ",{%d,%d,%d,%d,%d,0,0,0}", u.ta, u.tb, u.off, u.br, u.koff);
+        ud += buf;
       }
     }
   }
-  s += ua + ub + uo + ur + uk + "};\n";
+  s += ud + "};\n";
   const int CW = sh.CW, NW = C / CW, PW = sh.PW;
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
@@ -567,14 +561,17 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // tables: wave w stages units w, w + NWT_, ... (one dependent chain per unit and wave,
   // the waves' chains overlap)
   for (int k = w; k < nu; k += NWT_) {
-    const int ta = kUnitTA[u0 + k], tb = kUnitTB[u0 + k];
-    double* dst = tab + kUnitOff[u0 + k];
+    const UnitD ud = kUnitD[u0 + k];
+    // every field materialised here: one load and one wait before the branches on them
+    asm volatile("" ::"s"(ud.ta), "s"(ud.tb), "s"(ud.off), "s"(ud.br), "s"(ud.koff));
+    const int ta = ud.ta, tb = ud.tb;
+    double* dst = tab + ud.off;
     const double* ra = a.tipP + (i64)ta * (C_ * U_ * 4);
     if (tb < 0) {
       for (int i = lane; i < C_ * U_ * 4; i += 64) dst[i] = ra[i];
     } else {
       const double* rb = a.tipP + (i64)tb * (C_ * U_ * 4);
-      const int br = kUnitBr[u0 + k], koff = kUnitKOff[u0 + k];
+      const int br = ud.br, koff = ud.koff;
       if (SC_ && koff >= 0) {
         // rescaling contribution unit: one row (all classes) per lane, the cherry's joint
         // check as rescale() makes it, then contrib<.., true>

@@ -298,34 +298,3 @@ def test_dr_fused_preorder_any_state_count(S, C, tree_kind, n_pat, scaling, monk
     for v in br:
         assert _close(a1[v], b1[v], 1e-11), (v, a1[v], b1[v])
         assert _close(a2[v], b2[v], 1e-11), (v, a2[v], b2[v])
-
-
-@pytest.mark.parametrize("tree_kind,scaling", [("balanced24", False), ("caterpillar150long", True)])
-def test_dr_fused_64_two_waves_variant(tree_kind, scaling, monkeypatch):
-    """PLK_TUNE DR64_W2=1 (the 64-state fused preorder built for two waves per SIMD): the
-    same derivatives as the default build to rounding, on binary fathers with and without
-    rescaling."""
-    rng = np.random.default_rng(64)
-    if tree_kind.startswith("balanced"):
-        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=65, lo=0.05, hi=0.4)
-    else:
-        tree = _caterpillar(int(tree_kind[11:-4]), seed=3, lo=0.1, hi=0.5)
-    et = phylo.engine_tree(tree)
-    m, alph = phylo.yn98(2.0, 0.3), phylo.CODON
-    rates, probs = np.ones(1), np.ones(1)
-    wl = workload.Workload("d", et, [m], None, rates, probs, m.pi, alph, 200, scaling, True, 4)
-    states = wl.simulate(0, 200).astype(np.int32)
-    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
-    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | DR | (plk.PLK_FLAG_SCALING if scaling else 0)
-    out = {}
-    for w2 in ("0", "1"):
-        set_tune(monkeypatch, "DR64_W2", w2)
-        eng = engine_for(et, 64, 1, 200, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
-        eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
-        run_engine(eng, et)
-        out[w2] = eng.all_branch_derivatives()
-        del eng
-    (a1, a2), (b1, b2) = out["0"], out["1"]
-    for v in br:
-        assert _close(a1[v], b1[v], 1e-12), (v, a1[v], b1[v])
-        assert _close(a2[v], b2[v], 1e-12), (v, a2[v], b2[v])

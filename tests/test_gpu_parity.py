@@ -1114,7 +1114,7 @@ def test_jit_treeM_register_depths(dm, L, pd, g, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pipe,lc", [("0", "0"), ("1", "0"), ("2", "3"), ("1", "5"), ("0", "3")])
+@pytest.mark.parametrize("pipe,lc", [("0", "0"), ("1", "0"), ("1", "3"), ("2", "5"), ("0", "3")])
 def test_jit_treeM_issue_orders_bitwise(pipe, lc, monkeypatch):
     """jit_treeM's contraction issue orders (JITM_PIPE: per output block / Y-outer with the A
     operands read ahead / the same with pinned schedule groups) and operand fetch schedules

@@ -97,7 +97,10 @@ def main():
         worst = max(worst, abs(p1 - d1[b]) / max(1.0, abs(p1)), abs(p2 - d2[b]) / max(1.0, abs(p2)))
     t_path = (time.perf_counter() - t0) / len(sel) * nb
     up, red = dr_bytes(wl)
-    fused = wl.S in (4, 20, 64) and wl.C in (1, 2, 4) and "DR_PRE=0" not in os.environ.get("PLK_TUNE", "")
+    # the library's choice (plk.hip dr_derivatives): fused for 4 / 20 states, levelwise for 64
+    # unless PLK_TUNE DR_PRE=1; DR_PRE=0 always levelwise
+    tune = os.environ.get("PLK_TUNE", "")
+    fused = wl.C in (1, 2, 4) and "DR_PRE=0" not in tune and (wl.S in (4, 20) or (wl.S == 64 and "DR_PRE=1" in tune))
     fb = dr_fused_bytes(wl)
     rec = {
         "metric": "branch x site-pattern derivative updates/s (d1 and d2 of every branch)",

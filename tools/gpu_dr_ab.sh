@@ -1,7 +1,7 @@
 #!/bin/bash
 # DR pass A/B on one GPU: tests of the fused preorder and the C++ mirror, then
-# tools/bench_dr.py per config with the fused preorder (default) and the levelwise one
-# (PLK_TUNE=DR_PRE=0), and the mirror bench lines.
+# tools/bench_dr.py per config with the default DR path, the levelwise one (DR_PRE=0) and the
+# fused preorder (DR_PRE=1), and the mirror bench lines.
 #   tools/gpu_dr_ab.sh <prefix> [configs...]
 set -o pipefail
 P=${1:-dr}; shift
@@ -11,16 +11,14 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_dr.py tests/test_gpu_host.p
   > gpurun_out/$P/pytest.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/$P/pytest.log; exit 1; }
 tail -1 gpurun_out/$P/pytest.log
 for c in $CFGS; do
-  timeout -k 10 300 python tools/bench_dr.py --config $c --reps 3 --path-branches 4 > gpurun_out/$P/${c}_fused.json 2> gpurun_out/$P/${c}_fused.err || { tail -5 gpurun_out/$P/${c}_fused.err; exit 1; }
-  PLK_TUNE=DR_PRE=0 timeout -k 10 300 python tools/bench_dr.py --config $c --reps 3 --path-branches 4 > gpurun_out/$P/${c}_levelwise.json 2> gpurun_out/$P/${c}_levelwise.err || { tail -5 gpurun_out/$P/${c}_levelwise.err; exit 1; }
-  python3 -c "
+  for v in "default:" "levelwise:DR_PRE=0" "fused:DR_PRE=1"; do
+    n=${v%%:*}; e=${v#*:}
+    PLK_TUNE="$e" timeout -k 10 300 python tools/bench_dr.py --config $c --reps 3 --path-branches 4 > gpurun_out/$P/${c}_$n.json 2> gpurun_out/$P/${c}_$n.err || { tail -5 gpurun_out/$P/${c}_$n.err; exit 1; }
+    python3 -c "
 import json
-for v in ('fused','levelwise'):
-    d=json.load(open('gpurun_out/$P/${c}_'+v+'.json')); print('$c', v, round(d['dr_ms'],3), 'ms', d.get('dr_path'), 'maxrel', d['max_rel_diff_dr_vs_path'])"
+d=json.load(open('gpurun_out/$P/${c}_$n.json')); print('$c', '$n', round(d['dr_ms'],3), 'ms', d.get('dr_path'), 'maxrel', d['max_rel_diff_dr_vs_path'])"
+  done
 done
-PLK_TUNE=DR64_W2=1 timeout -k 10 300 python tools/bench_dr.py --config yn98_codon_50k_128 --reps 3 --path-branches 4 > gpurun_out/$P/cfg4_w2.json 2> gpurun_out/$P/cfg4_w2.err || { tail -5 gpurun_out/$P/cfg4_w2.err; exit 1; }
-python3 -c "
-import json; d=json.load(open('gpurun_out/$P/cfg4_w2.json')); print('cfg4 DR64_W2', round(d['dr_ms'],3), 'ms maxrel', d['max_rel_diff_dr_vs_path'])"
 for c in cfg2 cfg3; do
   timeout -k 10 200 bpp-phyl_amd/host/bin/bench_mirror $c > gpurun_out/$P/mirror_$c.json || exit 1
   cat gpurun_out/$P/mirror_$c.json
