@@ -756,7 +756,7 @@ __device__ __forceinline__ double dr_mfma4(double a, double b, double c) {
 template <int C, bool SCALE, int NS>
 __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restrict__ ops, DrArgs a) {
   constexpr int S = 20, XB = 5, SS = S * S, CS = C * S;
-  __shared__ double mats[10 * SS];  // [P_f | P_j, dP_j, d2P_j for j < 3] of one class
+  __shared__ __attribute__((aligned(16))) double mats[10 * SS];  // [P_f | P_j, dP_j, d2P_j for j < 3] of one class
   __shared__ double red[2][3][4];
   const DrPreOp op = ops[blockIdx.y];
   const int nsn = NS == 2 ? min(2, op.n) : op.n;  // (as dr_pre_m_kernel)
@@ -802,8 +802,17 @@ __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restri
   };
 #pragma unroll 1
   for (int c = 0; c < C; ++c) {
-    __syncthreads();  // the previous class is done with mats
-    for (int e = tid; e < nm * SS; e += 256) {
+    // this class's matrices: every thread's 16-byte loads issued before the first store (a
+    // loop of load -> store paid one L2 round trip per element, ~11 per thread and class);
+    // out-of-range lanes load element 0 and store nothing (matrices are 400 doubles, so no
+    // pair straddles two of them)
+    constexpr int NE2 = ((1 + 3 * NS) * SS / 2 + 255) / 256;
+    double2 mv[NE2];
+    int tq = tid;
+    asm volatile("" : "+v"(tq));  // (opaque per class: the element addresses are not hoisted out of the class loop)
+#pragma unroll
+    for (int q = 0; q < NE2; ++q) {
+      const int e0 = 2 * (tq + 256 * q), e = e0 < nm * SS ? e0 : 0;
       const int m = e / SS, k = e - m * SS;
       const int j = (m - 1) / 3, kind = (m - 1) - 3 * j;
       // (selects, not op.son[j]: a runtime index would put the op in scratch memory)
@@ -811,7 +820,13 @@ __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restri
       const double* src = m == 0 ? a.pmats + ((size_t)op.f * C + c) * SS
                                  : (kind == 0 ? a.pmats : kind == 1 ? a.dpmats : a.d2pmats) +
                                        ((size_t)son * C + c) * SS;
-      mats[e] = (m == 0 && root) ? 0.0 : src[k];
+      mv[q] = *reinterpret_cast<const double2*>(src + k);
+    }
+    __syncthreads();  // the previous class is done with mats
+#pragma unroll
+    for (int q = 0; q < NE2; ++q) {
+      const int e = 2 * (tid + 256 * q);
+      if (e < nm * SS) *reinterpret_cast<double2*>(mats + e) = (e < SS && root) ? make_double2(0.0, 0.0) : mv[q];
     }
     __syncthreads();
     double mu[XB];
