@@ -558,6 +558,27 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   const int c0 = (w % NW_) * CW_, g = w / NW_;
   const int frag = frag_base + (int)blockIdx.y;
   const int u0 = 1 + kFragUnitStart[frag], nu = kFragUnitStart[frag + 1] - kFragUnitStart[frag];
+  // code staging: this thread's items (uint4 column j of group gg in unit k's code row;
+  // JArgs::codes holds one row per unit, unit_codes_kernel), fixed over the super-blocks.
+  // The codes of the next super-block are loaded into registers while this one computes.
+  constexpr int NI_ = (G_ * NT_ * 4 * PW_ + 64 * NWT_ - 1) / (64 * NWT_);
+  const uint4* ucodes = reinterpret_cast<const uint4*>(a.codes);
+  const i64 row16 = a.n_pad / 16;
+  i64 iu_[NI_]; int ic_[NI_], il_[NI_]; uint4 va_[NI_];
+  _Pragma("unroll") for (int m = 0; m < NI_; ++m) {
+    const int i = threadIdx.x + m * (64 * NWT_);
+    const int gg = i / (nu * 4 * PW_), r = i - gg * (nu * 4 * PW_), k = r / (4 * PW_), j = r - k * (4 * PW_);
+    const bool ok = i < G_ * nu * 4 * PW_;
+    ic_[m] = ok ? gg * (64 * PW_) + 16 * j : 0x7fffffff;  // column in the super-block (none: past n_pad)
+    iu_[m] = (i64)(u0 - 1 + k) * row16 + (ic_[m] >> 4);
+    il_[m] = (gg * NT_ + k) * 4 * PW_ + j;
+  }
+  auto fetch_codes = [&](int sb_) {
+    const i64 q0_ = (i64)sb_ * (64 * PW_ * G_);
+    _Pragma("unroll") for (int m = 0; m < NI_; ++m)
+      if (q0_ + ic_[m] < a.n_pad) va_[m] = ucodes[iu_[m] + (q0_ >> 4)];
+  };
+  fetch_codes(blockIdx.x);  // (issued before the table staging below: its loads overlap it)
   // tables: wave w stages units w, w + NWT_, ... (one dependent chain per unit and wave,
   // the waves' chains overlap)
   for (int k = w; k < nu; k += NWT_) {
@@ -661,27 +682,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[4 * CW_ * pw_ + i_] = L_[64 * pw_ + (i64)i_ * kTile]; \
       if (SC_) FK[pw_] = a.scale[sl_ * a.n_pad + p + 64 * pw_]; } }
 #define SB __builtin_amdgcn_sched_barrier(0);
-  // code staging: this thread's items (uint4 column j of group gg in unit k's code row;
-  // JArgs::codes holds one row per unit, unit_codes_kernel), fixed over the super-blocks.
-  // The codes of the next super-block are loaded into registers while this one computes.
-  constexpr int NI_ = (G_ * NT_ * 4 * PW_ + 64 * NWT_ - 1) / (64 * NWT_);
-  const uint4* ucodes = reinterpret_cast<const uint4*>(a.codes);
-  const i64 row16 = a.n_pad / 16;
-  i64 iu_[NI_]; int ic_[NI_], il_[NI_]; uint4 va_[NI_];
-  _Pragma("unroll") for (int m = 0; m < NI_; ++m) {
-    const int i = threadIdx.x + m * (64 * NWT_);
-    const int gg = i / (nu * 4 * PW_), r = i - gg * (nu * 4 * PW_), k = r / (4 * PW_), j = r - k * (4 * PW_);
-    const bool ok = i < G_ * nu * 4 * PW_;
-    ic_[m] = ok ? gg * (64 * PW_) + 16 * j : 0x7fffffff;  // column in the super-block (none: past n_pad)
-    iu_[m] = (i64)(u0 - 1 + k) * row16 + (ic_[m] >> 4);
-    il_[m] = (gg * NT_ + k) * 4 * PW_ + j;
-  }
-  auto fetch_codes = [&](int sb_) {
-    const i64 q0_ = (i64)sb_ * (64 * PW_ * G_);
-    _Pragma("unroll") for (int m = 0; m < NI_; ++m)
-      if (q0_ + ic_[m] < a.n_pad) va_[m] = ucodes[iu_[m] + (q0_ >> 4)];
-  };
-  fetch_codes(blockIdx.x);
   for (int sb = blockIdx.x; sb < a.n_sblocks; sb += gridDim.x) {
     const i64 q0 = (i64)sb * (64 * PW_ * G_);
     // super-blocks of G_ groups; in a ragged last one, groups past n_pad recompute group 0
