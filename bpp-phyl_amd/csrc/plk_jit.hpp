@@ -525,20 +525,40 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // per staging round at the start of every launch (profiles/r03/r3d sweep)
   std::string ud = "};\nstruct __attribute__((aligned(32))) UnitD { int ta, tb, off, br, koff, p0, p1, p2; };\n"
                    "__device__ const UnitD kUnitD[] = {{0, 0, 0, 0, 0, 0, 0, 0}";
+  // With rescaling, a fragment's rescaling contribution units (koff >= 0) are listed apart
+  // (kScUnit, CSR kFragScStart) and staged with one (unit, row) per thread of the whole
+  // workgroup -- such a unit has only U * U rows (16 for DNA), so one unit per wave left 48
+  // of 64 lanes idle and cost one dependent load round per unit and wave; the other units
+  // (kOtherUnit, kFragOtherStart) keep one unit per wave.
+  std::string sc = "};\n__device__ const int kFragScStart[] = {0", scu = "};\n__device__ const int kScUnit[] = {0",
+              ot = "};\n__device__ const int kFragOtherStart[] = {0", otu = "};\n__device__ const int kOtherUnit[] = {0";
   s += "\n__device__ const int kFragUnitStart[] = {0";
   {
-    int acc = 0;
+    int acc = 0, nsc = 0, not_ = 0;
     for (const auto& un : plan.units) {
       acc += (int)un.size();
       snprintf(buf, sizeof(buf), ",%d", acc);
       s += buf;
-      for (const JitUnit& u : un) {
+      for (size_t k = 0; k < un.size(); ++k) {
+        const JitUnit& u = un[k];
         snprintf(buf, sizeof(buf), ",{%d,%d,%d,%d,%d,0,0,0}", u.ta, u.tb, u.off, u.br, u.koff);
         ud += buf;
+        snprintf(buf, sizeof(buf), ",%zu", k);
+        if (sh.scale && u.tb >= 0 && u.koff >= 0) {
+          scu += buf;
+          ++nsc;
+        } else {
+          otu += buf;
+          ++not_;
+        }
       }
+      snprintf(buf, sizeof(buf), ",%d", nsc);
+      sc += buf;
+      snprintf(buf, sizeof(buf), ",%d", not_);
+      ot += buf;
     }
   }
-  s += ud + "};\n";
+  s += ud + sc + scu + ot + otu + "};\n";
   const int CW = sh.CW, NW = C / CW, PW = sh.PW;
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
@@ -579,9 +599,44 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       if (q0_ + ic_[m] < a.n_pad) va_[m] = ucodes[iu_[m] + (q0_ >> 4)];
   };
   fetch_codes(blockIdx.x);  // (issued before the table staging below: its loads overlap it)
-  // tables: wave w stages units w, w + NWT_, ... (one dependent chain per unit and wave,
-  // the waves' chains overlap)
-  for (int k = w; k < nu; k += NWT_) {
+  if (SC_) {
+    // rescaling contribution units: one (unit, row) per thread; each row all classes, the
+    // cherry's joint check as rescale() makes it, then contrib<.., true>
+    const int sc0 = 1 + kFragScStart[frag], nsc = kFragScStart[frag + 1] - kFragScStart[frag];
+    for (int t = threadIdx.x; t < nsc * (U_ * U_); t += 64 * NWT_) {
+      const int kk = t / (U_ * U_), r = t - kk * (U_ * U_);
+      const UnitD ud = kUnitD[u0 + kScUnit[sc0 + kk]];
+      double* dst = tab + ud.off;
+      const double* ra = a.tipP + (i64)ud.ta * (C_ * U_ * 4);
+      const double* rb = a.tipP + (i64)ud.tb * (C_ * U_ * 4);
+      const int ca = r / U_, cb = r - ca * U_;
+      double v[C_][4], m = 0.0;
+      for (int c = 0; c < C_; ++c)
+        for (int y = 0; y < 4; ++y) {
+          v[c][y] = ra[(c * U_ + ca) * 4 + y] * rb[(c * U_ + cb) * 4 + y];
+          m = fmax(m, v[c][y]);
+        }
+      const bool up = m > 0.0 && m < kScaleThr;
+      for (int c = 0; c < C_; ++c) {
+        if (up)
+          for (int y = 0; y < 4; ++y) v[c][y] *= kScaleUp;
+        for (int x = 0; x < 4; ++x) {
+          const double* P = pmats + ((i64)ud.br * C_ + c) * 16 + 4 * x;
+          double t2 = P[0] * v[c][0];
+          t2 = __builtin_fma(P[1], v[c][1], t2);
+          t2 = __builtin_fma(P[2], v[c][2], t2);
+          t2 = __builtin_fma(P[3], v[c][3], t2);
+          dst[(c * U_ * U_ + r) * 4 + x] = t2;
+        }
+      }
+      reinterpret_cast<u8*>(tab + ud.koff)[r] = up ? 1 : 0;
+    }
+  }
+  // the other tables: wave w stages units w, w + NWT_, ... of the fragment's other-unit list
+  // (one dependent chain per unit and wave, the waves' chains overlap)
+  const int ot0 = 1 + kFragOtherStart[frag], not_ = kFragOtherStart[frag + 1] - kFragOtherStart[frag];
+  for (int ko = w; ko < not_; ko += NWT_) {
+    const int k = kOtherUnit[ot0 + ko];
     const UnitD ud = kUnitD[u0 + k];
     // every field materialised here: one load and one wait before the branches on them
     asm volatile("" ::"s"(ud.ta), "s"(ud.tb), "s"(ud.off), "s"(ud.br), "s"(ud.koff));
@@ -592,35 +647,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       for (int i = lane; i < C_ * U_ * 4; i += 64) dst[i] = ra[i];
     } else {
       const double* rb = a.tipP + (i64)tb * (C_ * U_ * 4);
-      const int br = ud.br, koff = ud.koff;
-      if (SC_ && koff >= 0) {
-        // rescaling contribution unit: one row (all classes) per lane, the cherry's joint
-        // check as rescale() makes it, then contrib<.., true>
-        for (int r = lane; r < U_ * U_; r += 64) {
-          const int ca = r / U_, cb = r - ca * U_;
-          double v[C_][4], m = 0.0;
-          for (int c = 0; c < C_; ++c)
-            for (int y = 0; y < 4; ++y) {
-              v[c][y] = ra[(c * U_ + ca) * 4 + y] * rb[(c * U_ + cb) * 4 + y];
-              m = fmax(m, v[c][y]);
-            }
-          const bool up = m > 0.0 && m < kScaleThr;
-          for (int c = 0; c < C_; ++c) {
-            if (up)
-              for (int y = 0; y < 4; ++y) v[c][y] *= kScaleUp;
-            for (int x = 0; x < 4; ++x) {
-              const double* P = pmats + ((i64)br * C_ + c) * 16 + 4 * x;
-              double t = P[0] * v[c][0];
-              t = __builtin_fma(P[1], v[c][1], t);
-              t = __builtin_fma(P[2], v[c][2], t);
-              t = __builtin_fma(P[3], v[c][3], t);
-              dst[(c * U_ * U_ + r) * 4 + x] = t;
-            }
-          }
-          reinterpret_cast<u8*>(tab + koff)[r] = up ? 1 : 0;
-        }
-        continue;
-      }
+      const int br = ud.br;  // (rescaling contribution units were staged above)
       // one row (class c, code pair ca, cb: 4 doubles) per lane, its operands loaded
       // together (16-byte loads), so a unit costs one load latency, not one per double
       for (int r = lane; r < C_ * U_ * U_; r += 64) {
