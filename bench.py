@@ -261,8 +261,19 @@ def roofline(wl, mode, P, ev_steps, tm, work, traffic):
     return main
 
 
+def _json_stdout():
+    """The one JSON line goes to the process's real stdout; everything else written to fd 1
+    (RCCL's version banner, gloo's connection messages, library prints) is sent to stderr, so
+    that stdout under torch.distributed.run carries exactly rank 0's line."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
+
+
 def main():
     args = parse()
+    out = _json_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -422,7 +433,7 @@ def main():
             ns = args.cpu_sample or workload.CONFIGS[args.config]["cpu_sample"]
             _, eng_sites, _ = ev.eng.root_loglik(wl.et.root, want_sites=True)
             rec["cpu_baseline"] = cpu_baseline(wl, min(ns, P), args.cpu_runs, eng_sites)
-        print(json.dumps(rec), flush=True)
+        print(json.dumps(rec), file=out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

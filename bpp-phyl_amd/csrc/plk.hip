@@ -1247,7 +1247,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     ev = get_events(h, 1);
     hipEventRecord(ev.a, h->stream);
   }
-  const size_t lds = (size_t)(h->S + (tips_fused ? 2 : 1) * S2) * sizeof(double);
+  const size_t lds = (size_t)(h->S + (tips_fused ? 3 : 2) * S2) * sizeof(double);
   if (k64 && !tune_is("PMAT64_SPLIT", '0'))
     pmat64s_kernel<<<dim3(n, h->C, 4), dim3(256), (size_t)(64 + 16 * 64 + S2) * sizeof(double), h->stream>>>(a, inl);
   else if (k64)
@@ -1255,7 +1255,15 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   else if (h->S == 4 && !tune_is("PMAT4", '0'))
     pmat4_kernel<<<dim3((unsigned)((n * h->C * 4 + 63) / 64)), dim3(64), 0, h->stream>>>(a, inl);
   else
-    pmat_kernel<<<dim3(n, h->C), dim3(h->S <= 4 ? 64 : 256), lds, h->stream>>>(a, inl);
+  {
+    const int nth = h->S <= 4 ? 64 : 256, ne = (int)((S2 + nth - 1) / nth);
+    const dim3 g(n, h->C);
+    if (ne <= 1) pmat_kernel<1><<<g, dim3(nth), lds, h->stream>>>(a, inl);
+    else if (ne <= 2) pmat_kernel<2><<<g, dim3(nth), lds, h->stream>>>(a, inl);
+    else if (ne <= 4) pmat_kernel<4><<<g, dim3(nth), lds, h->stream>>>(a, inl);
+    else if (ne <= 8) pmat_kernel<8><<<g, dim3(nth), lds, h->stream>>>(a, inl);
+    else pmat_kernel<16><<<g, dim3(nth), lds, h->stream>>>(a, inl);
+  }
   HIPCHK(h, hipGetLastError());
   if (inl.n == 0) HIPCHK(h, hipEventRecord(h->req_done, h->stream));  // the kernel read the staging
   if (h->timing & PLK_TIME_PMAT) {

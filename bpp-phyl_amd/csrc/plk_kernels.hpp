@@ -555,6 +555,28 @@ struct PmatInline {
   int32_t n;  // 0: use PmatArgs' device arrays
 };
 
+// n doubles global -> LDS, the first NE * blockDim.x of them with every thread's loads
+// issued before its first store (a load -> store loop pays one L2 round trip per element and
+// thread); any remainder (n beyond NE * blockDim.x, e.g. more codes than a launch sized for)
+// element by element
+template <int NE>
+__device__ __forceinline__ void stage_lds(double* __restrict__ dst, const double* __restrict__ src, int n) {
+  double r[NE];
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int k = (int)threadIdx.x + (int)blockDim.x * q;
+    r[q] = src[k < n ? k : 0];
+  }
+#pragma unroll
+  for (int q = 0; q < NE; ++q) {
+    const int k = (int)threadIdx.x + (int)blockDim.x * q;
+    if (k < n) dst[k] = r[q];
+  }
+  for (int k = (int)threadIdx.x + (int)blockDim.x * NE; k < n; k += (int)blockDim.x) dst[k] = src[k];
+}
+
+// NE: S * S / blockDim.x rounded up (the staging loads per thread)
+template <int NE>
 __global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a, const PmatInline inl) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int i = blockIdx.x, c = blockIdx.y, S = a.S;
@@ -564,11 +586,12 @@ __global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a, const PmatInline 
   const double tt = (inl.n ? inl.t[i] : a.t[i]) * rc;
   double* e = sm;           // exp(lambda t)
   double* Vm = sm + S;      // V
+  double* Vi = Vm + S * S;  // Vinv
   const double* V = a.V + (size_t)m * S * S;
-  const double* Vi = a.Vinv + (size_t)m * S * S;
   const double* lam = a.lambda + (size_t)m * S;
   for (int k = threadIdx.x; k < S; k += blockDim.x) e[k] = exp(lam[k] * tt);
-  for (int k = threadIdx.x; k < S * S; k += blockDim.x) Vm[k] = V[k];
+  stage_lds<NE>(Vm, V, S * S);
+  stage_lds<NE>(Vi, a.Vinv + (size_t)m * S * S, S * S);
   __syncthreads();
   const size_t off = ((size_t)b * a.C + c) * S * S;
   for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
@@ -588,13 +611,13 @@ __global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a, const PmatInline 
     if (a.mask & 1u) a.P[off + idx] = p;
     if (a.mask & 2u) a.dP[off + idx] = rc * dp;
     if (a.mask & 4u) a.d2P[off + idx] = rc * rc * d2p;
-    if (a.init && b < a.n_tips) Vm[S * S + idx] = p;
+    if (a.init && b < a.n_tips) Vi[S * S + idx] = p;
   }
   // tip branch: its table row tipP[b][c][code][x] = sum_y P[x][y] init[code][y], with
   // tip_table_kernel's arithmetic (the fused kernels read tips through it)
   if (a.init && b < a.n_tips && (a.mask & 1u)) {
     __syncthreads();
-    const double* Pl = Vm + S * S;
+    const double* Pl = Vi + S * S;
     double* out = a.tipP + ((size_t)b * a.C + c) * a.n_codes * S;
     for (int idx = threadIdx.x; idx < a.n_codes * S; idx += blockDim.x) {
       const int code = idx / S, x = idx % S;
@@ -688,10 +711,8 @@ __global__ __launch_bounds__(256) void pmat64_kernel(PmatArgs a, const PmatInlin
   const double* VI = a.Vinv + (size_t)m * S * S;
   const double* lam = a.lambda + (size_t)m * S;
   for (int k = threadIdx.x; k < S; k += blockDim.x) e[k] = exp(lam[k] * tt);
-  for (int k = threadIdx.x; k < S * S; k += blockDim.x) {
-    Vm[k] = V[k];
-    Vi[k] = VI[k];
-  }
+  stage_lds<S * S / 256>(Vm, V, S * S);
+  stage_lds<S * S / 256>(Vi, VI, S * S);
   __syncthreads();
   const int xb = 4 * (threadIdx.x >> 4), yb = threadIdx.x & 15;
   double p[4][4];
@@ -729,7 +750,7 @@ __global__ __launch_bounds__(256) void pmat64_kernel(PmatArgs a, const PmatInlin
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int v = 0; v < 4; ++v) Pl[(xb + u) * S + yb + 16 * v] = p[u][v];
-    for (int k = threadIdx.x; k < a.n_codes * S; k += blockDim.x) In[k] = a.init[k];
+    stage_lds<S * S / 256>(In, a.init, a.n_codes * S);
     __syncthreads();
     double* tout = a.tipP + ((size_t)b * a.C + c) * a.n_codes * S;
     const int xq = 4 * (threadIdx.x & 15), cb = 4 * (threadIdx.x >> 4);
@@ -774,8 +795,8 @@ __global__ __launch_bounds__(256) void pmat64s_kernel(PmatArgs a, const PmatInli
   const double* VI = a.Vinv + (size_t)m * S * S;
   const double* lam = a.lambda + (size_t)m * S;
   for (int k = threadIdx.x; k < S; k += blockDim.x) e[k] = exp(lam[k] * tt);
-  for (int k = threadIdx.x; k < R * S; k += blockDim.x) Vm[k] = V[x0 * S + k];
-  for (int k = threadIdx.x; k < S * S; k += blockDim.x) Vi[k] = VI[k];
+  stage_lds<R * S / 256>(Vm, V + x0 * S, R * S);
+  stage_lds<S * S / 256>(Vi, VI, S * S);
   __syncthreads();
   const int xr = threadIdx.x >> 4, yb = threadIdx.x & 15;
   double p[4] = {0.0, 0.0, 0.0, 0.0};
@@ -802,7 +823,7 @@ __global__ __launch_bounds__(256) void pmat64s_kernel(PmatArgs a, const PmatInli
     double* In = Vi;  // [code][y], n_codes <= 64 (launch guarantees)
 #pragma unroll
     for (int v = 0; v < 4; ++v) Pl[xr * S + yb + 16 * v] = p[v];
-    for (int k = threadIdx.x; k < a.n_codes * S; k += blockDim.x) In[k] = a.init[k];
+    stage_lds<S * S / 256>(In, a.init, a.n_codes * S);
     __syncthreads();
     double* tout = a.tipP + ((size_t)b * a.C + c) * a.n_codes * S;
     const int xl = threadIdx.x & 15, cb = 4 * (threadIdx.x >> 4);
@@ -829,8 +850,8 @@ __global__ __launch_bounds__(256) void tip_table64_kernel(const double* __restri
   double* Pl = sm;           // [x][y]
   double* In = sm + S * S;   // [code][y]
   const double* Pc = P + ((size_t)tip * C + c) * S * S;
-  for (int k = threadIdx.x; k < S * S; k += blockDim.x) Pl[k] = Pc[k];
-  for (int k = threadIdx.x; k < n_codes * S; k += blockDim.x) In[k] = init[k];
+  stage_lds<S * S / 256>(Pl, Pc, S * S);
+  stage_lds<S * S / 256>(In, init, n_codes * S);
   __syncthreads();
   double* out = tipP + ((size_t)tip * C + c) * n_codes * S;
   const int xb = 4 * (threadIdx.x & 15);

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void cherry_table_kernel(const double* __restr
   const int k = blockIdx.y / C, c = blockIdx.y % C, U2 = U * U;
   {
     const double* PT = pmatsT + ((size_t)cherry3[3 * k + 2] * C + c) * S * S;
-    for (int i = threadIdx.x; i < S * S; i += blockDim.x) PTl[i] = PT[i];
+    stage_lds<(S * S + 255) / 256>(PTl, PT, S * S);
     __syncthreads();
   }
   // each workgroup stages P^T once and covers rows_per_wg code pairs, 64 per pass
