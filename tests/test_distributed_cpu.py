@@ -144,3 +144,25 @@ def test_shard_range_properties():
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(a % shard.BLOCK == 0 or a == n for a, _ in rs)
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+
+
+_REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_stdout_is_one_json_line(tmp_path):
+    """Under torch.distributed.run every rank's stdout reaches the driver: RCCL prints a version
+    banner and gloo its connection messages on fd 1.  bench.py moves fd 1 to stderr at start
+    and writes only rank 0's JSON line to the original stdout (bench._json_stdout)."""
+    import subprocess
+    import sys
+    code = (
+        "import importlib.util, os, sys\n"
+        f"spec = importlib.util.spec_from_file_location('bench', {os.path.join(_REPO, 'bench.py')!r})\n"
+        "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+        "out = b._json_stdout()\n"
+        "print('python-level noise'); os.write(1, b'C-level banner\\n')\n"
+        "print('{\"metric\": \"m\"}', file=out, flush=True)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ['{"metric": "m"}']
+    assert "C-level banner" in r.stderr and "python-level noise" in r.stderr
