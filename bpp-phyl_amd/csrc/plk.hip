@@ -1228,6 +1228,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   a.Vinv = h->Vinv;
   a.lambda = h->lambda;
   a.P = h->pmats;
+  a.PT = nullptr;
   a.dP = h->dpmats;
   a.d2P = h->d2pmats;
   a.S = h->S;
@@ -1248,6 +1249,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     hipEventRecord(ev.a, h->stream);
   }
   const size_t lds = (size_t)(h->S + (tips_fused ? 3 : 2) * S2) * sizeof(double);
+  if (k64 && !tune_is("PMAT64_SPLIT", '0')) a.PT = h->pmatsT;  // (allocated by the first transposed-P use)
   if (k64 && !tune_is("PMAT64_SPLIT", '0'))
     pmat64s_kernel<<<dim3(n, h->C, 4), dim3(256), (size_t)(64 + 16 * 64 + S2) * sizeof(double), h->stream>>>(a, inl);
   else if (k64)
@@ -1273,7 +1275,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   if (deriv_mask & PLK_DERIV_P) {
     for (int i = 0; i < n; ++i) {
       h->pmat_valid[branch[i]] = 1;
-      h->pmatsT_dirty = true;
+      if (!a.PT) h->pmatsT_dirty = true;  // pmat64s_kernel wrote the transposed rows too
       if (branch[i] < h->n_tips) h->tip_table_valid[branch[i]] = tips_fused ? 1 : 0;  // row written by pmat_kernel
     }
   }

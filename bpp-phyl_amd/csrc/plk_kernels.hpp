@@ -535,6 +535,7 @@ struct PmatArgs {
   const double* Vinv;      // [n_models][S][S]
   const double* lambda;    // [n_models][S]
   double* P;               // [n_nodes][C][S][S]
+  double* PT;              // P transposed, [n_nodes][C][y][x] (pmat64s_kernel; null: not written)
   double* dP;
   double* d2P;
   const double* init;      // [n_codes][S] code table (null: no tip tables)
@@ -816,6 +817,13 @@ __global__ __launch_bounds__(256) void pmat64s_kernel(PmatArgs a, const PmatInli
     const int y = yb + 16 * v;
     p[v] = tt == 0.0 ? (x == y ? 1.0 : 0.0) : p[v];  // getPij_t: t == 0 -> identity
     out[x * S + y] = p[v];
+  }
+  // the transposed copy the 64-state matrix-core kernels read (transpose_pmats' layout),
+  // written here so that an evaluation needs no transpose launch
+  if (a.PT) {
+    double* outT = a.PT + ((size_t)b * a.C + c) * S * S;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) outT[(yb + 16 * v) * S + x] = p[v];
   }
   if (a.init && b < a.n_tips) {
     __syncthreads();  // done with Vm / Vi
