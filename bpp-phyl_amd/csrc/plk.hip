@@ -1249,7 +1249,10 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     hipEventRecord(ev.a, h->stream);
   }
   const size_t lds = (size_t)(h->S + (tips_fused ? 3 : 2) * S2) * sizeof(double);
-  if (k64 && !tune_is("PMAT64_SPLIT", '0')) a.PT = h->pmatsT;  // (allocated by the first transposed-P use)
+  // pmat64s_kernel and pmat_kernel also write the transposed copy the matrix-core kernels
+  // read (allocated by the first transposed-P use), so an evaluation needs no transpose launch
+  const bool pk_generic = !k64 && !(h->S == 4 && !tune_is("PMAT4", '0'));
+  if (((k64 && !tune_is("PMAT64_SPLIT", '0')) || pk_generic) && (deriv_mask & PLK_DERIV_P)) a.PT = h->pmatsT;
   if (k64 && !tune_is("PMAT64_SPLIT", '0'))
     pmat64s_kernel<<<dim3(n, h->C, 4), dim3(256), (size_t)(64 + 16 * 64 + S2) * sizeof(double), h->stream>>>(a, inl);
   else if (k64)

@@ -610,6 +610,7 @@ __global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a, const PmatInline 
     }
     if (tt == 0.0) p = (x == y) ? 1.0 : 0.0;  // getPij_t: t == 0 -> identity (:428-431)
     if (a.mask & 1u) a.P[off + idx] = p;
+    if (a.PT && (a.mask & 1u)) a.PT[off + (size_t)y * S + x] = p;  // transposed copy (transpose_pmats' layout)
     if (a.mask & 2u) a.dP[off + idx] = rc * dp;
     if (a.mask & 4u) a.d2P[off + idx] = rc * rc * d2p;
     if (a.init && b < a.n_tips) Vi[S * S + idx] = p;
