@@ -1114,6 +1114,7 @@ int plk_set_pattern_weights(plk_handle h, const double* weights) {
   hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hipMemcpy(h->weights, weights, (size_t)h->n_patterns * sizeof(double), hipMemcpyHostToDevice));
+  h->fused_lnl_valid = false;  // a cached fused root reduction used the old weights
   return PLK_OK;
 }
 
@@ -1126,6 +1127,7 @@ int plk_set_category_rates(plk_handle h, const double* rates, const double* prob
   HIPCHK(h, hipMemcpy(h->rates, rates, h->C * sizeof(double), hipMemcpyHostToDevice));
   HIPCHK(h, hipMemcpy(h->probs, probs, h->C * sizeof(double), hipMemcpyHostToDevice));
   h->rates_set = true;
+  h->fused_lnl_valid = false;  // a cached fused root reduction used the old class probabilities
   return PLK_OK;
 }
 
@@ -1137,6 +1139,7 @@ int plk_set_root_frequencies(plk_handle h, const double* pi) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hipMemcpy(h->pi, pi, h->S * sizeof(double), hipMemcpyHostToDevice));
   h->pi_set = true;
+  h->fused_lnl_valid = false;  // a cached fused root reduction used the old frequencies
   return PLK_OK;
 }
 

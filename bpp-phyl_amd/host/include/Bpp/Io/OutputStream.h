@@ -12,8 +12,16 @@
 namespace bpp {
 
 class OutputStream {
+ protected:
+  int precision_ = 6;  // digits of the doubles written (bpp-core AbstractOutputStream default)
+
  public:
   virtual ~OutputStream() {}
+  OutputStream& setPrecision(int digits) {
+    precision_ = digits;
+    return *this;
+  }
+  int getPrecision() const { return precision_; }
   virtual OutputStream& operator<<(const std::string& s) = 0;
   virtual OutputStream& operator<<(double d) = 0;
   virtual OutputStream& operator<<(long d) = 0;
@@ -36,7 +44,7 @@ class StlOutputStream : public OutputStream {
     return *this;
   }
   OutputStream& operator<<(double d) override {
-    if (stream_) *stream_ << std::setprecision(12) << d;
+    if (stream_) *stream_ << std::setprecision(precision_) << d;
     return *this;
   }
   OutputStream& operator<<(long d) override {

@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "../../App/ApplicationTools.h"
 #include "../../Numeric/Prob/DiscreteDistribution.h"
 #include "../../Seq/Container/SiteContainer.h"
 #include "../Model/Models.h"
@@ -57,7 +58,7 @@ class TreeLikelihood : public AbstractParametrizable {
 
 // Common engine plumbing of the R-likelihoods: tree copy, node order, root site
 // patterns, the libplk handle and the postorder op list.
-class AbstractPlkTreeLikelihood : public TreeLikelihood {
+class AbstractPlkTreeLikelihood : public virtual TreeLikelihood {
  protected:
   TreeTemplate<Node>* tree_ = nullptr;
   std::vector<Node*> nodes_;                 // postorder minus root (BrLen<i> = nodes_[i])
@@ -196,6 +197,12 @@ class AbstractPlkTreeLikelihood : public TreeLikelihood {
   // Branch-length-only changes re-evaluate just the ancestors of the changed branches
   // (default); false restores the reference's full traversal on every change.
   void setIncrementalRecompute(bool yn) { incremental_ = yn; }
+  // Branch-length bounds (AbstractHomogeneousTreeLikelihood.h:248-264): the constraint of
+  // every branch-length parameter; the parameters are rebuilt from the tree
+  virtual void setMinimumBranchLength(double minimum);
+  virtual void setMaximumBranchLength(double maximum);
+  double getMinimumBranchLength() const { return minimumBrLen_; }
+  double getMaximumBranchLength() const { return maximumBrLen_; }
   // Partial likelihoods of a node in the reference's [pattern][class][state] order.
   VVVdouble getLikelihoodArray(int nodeId) const;
   plk_handle_s* getEngine() const { return engine_; }

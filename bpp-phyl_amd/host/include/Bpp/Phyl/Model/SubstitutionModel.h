@@ -15,6 +15,8 @@
 #include "../../Numeric/Matrix/Matrix.h"
 #include "../../Numeric/NumConstants.h"
 #include "../../Numeric/Parameter.h"
+#include "../../Numeric/VectorTools.h"
+#include "../../Text/TextTools.h"
 #include "../../Seq/Alphabet/Alphabet.h"
 
 namespace bpp {

@@ -12,7 +12,9 @@
 
 #include <string>
 
+#include "../App/ApplicationTools.h"
 #include "../Io/OutputStream.h"
+#include "Likelihood/ClockTreeLikelihood.h"
 #include "Likelihood/TreeLikelihood.h"
 
 namespace bpp {
@@ -39,6 +41,17 @@ struct OptimizationTools {
                                                    OutputStream* profiler = nullptr, bool reparametrization = false,
                                                    bool useClock = false, unsigned int verbose = 1,
                                                    const std::string& optMethodDeriv = OPTIMIZATION_NEWTON);
+
+  // OptimizationTools.cpp:484-539: every given parameter of a global-clock likelihood
+  // (TotalHeight, HeightP<id>, the model and rate parameters) optimised together,
+  // with numerical derivatives: OPTIMIZATION_GRADIENT (the default) is a conjugate-gradient
+  // descent over TwoPointsNumericalDerivative (interval 1e-7), OPTIMIZATION_NEWTON the
+  // PseudoNewton optimiser over ThreePointsNumericalDerivative (interval 1e-4).
+  static unsigned int optimizeNumericalParametersWithGlobalClock2(
+      DiscreteRatesAcrossSitesClockTreeLikelihood* cl, const ParameterList& parameters,
+      OptimizationListener* listener = nullptr, double tolerance = 0.000001, unsigned int tlEvalMax = 1000000,
+      OutputStream* messageHandler = nullptr, OutputStream* profiler = nullptr, unsigned int verbose = 1,
+      const std::string& optMethodDeriv = OPTIMIZATION_GRADIENT);
 
   // PseudoNewton steps of the last OPTIMIZATION_NEWTON run (diagnostics)
   static unsigned int lastSteps_;

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../Numeric/Prob/DiscreteDistribution.h"
+#include "../../Numeric/Random/RandomTools.h"
 #include "../../Seq/Container/SiteContainer.h"
 #include "../Model/SubstitutionModelSet.h"
 #include "../TreeTemplate.h"
@@ -43,6 +44,7 @@ class NonHomogeneousSequenceSimulator {
   // homogeneous case: the model on every branch, its equilibrium frequencies at the root
   NonHomogeneousSequenceSimulator(const SubstitutionModel* model, const DiscreteDistribution* rate,
                                   const Tree* tree);
+  virtual ~NonHomogeneousSequenceSimulator() {}
   NonHomogeneousSequenceSimulator(const NonHomogeneousSequenceSimulator&) = delete;
   NonHomogeneousSequenceSimulator& operator=(const NonHomogeneousSequenceSimulator&) = delete;
 

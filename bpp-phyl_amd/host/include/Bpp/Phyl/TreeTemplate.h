@@ -8,6 +8,7 @@
 #ifndef BPP_AMD_TREETEMPLATE_H
 #define BPP_AMD_TREETEMPLATE_H
 
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -214,6 +215,27 @@ struct TreeTemplateTools {
                                               const std::string& propertyName = "", bool withId = false,
                                               bool verbose = false);
   static std::string treeToParenthesis(const TreeTemplate<Node>& tree);
+  // TreeTemplateTools.cpp:63-76: a node of more than two sons anywhere below `node`
+  template <class N>
+  static bool isMultifurcating(const N& node) {
+    if (node.getNumberOfSons() > 2) return true;
+    for (size_t i = 0; i < node.getNumberOfSons(); i++)
+      if (isMultifurcating(*node.getSon(i))) return true;
+    return false;
+  }
+  // TreeTemplateTools.cpp:173-186: the height of every node below `node` (the longest path
+  // to a leaf); returns the height of `node`
+  template <class N>
+  static double getHeights(const N& node, std::map<const N*, double>& heights) {
+    double d = 0.;
+    for (size_t i = 0; i < node.getNumberOfSons(); i++) {
+      const N* son = node.getSon(i);
+      const double c = getHeights(*son, heights) + son->getDistanceToFather();
+      if (c > d) d = c;
+    }
+    heights[&node] = d;
+    return d;
+  }
   template <class N>
   static std::vector<const N*> getLeaves(const N& node) {
     std::vector<const N*> out;

@@ -228,6 +228,24 @@ void AbstractPlkTreeLikelihood::initBranchLengthsParameters() {
   }
 }
 
+void AbstractPlkTreeLikelihood::setMinimumBranchLength(double minimum) {
+  if (minimum > maximumBrLen_)
+    throw Exception("AbstractHomogeneousTreeLikelihood::setMinimumBranchLength. Minimum branch length sould be lower "
+                    "than the maximum one: " + TextTools::toString(maximumBrLen_));
+  minimumBrLen_ = minimum;
+  brLenConstraint_ = std::make_shared<IntervalConstraint>(minimumBrLen_, maximumBrLen_, true, true);
+  initBranchLengthsParameters();
+}
+
+void AbstractPlkTreeLikelihood::setMaximumBranchLength(double maximum) {
+  if (maximum < minimumBrLen_)
+    throw Exception("AbstractHomogeneousTreeLikelihood::setMaximumBranchLength. Maximum branch length sould be higher "
+                    "than the minimum one: " + TextTools::toString(minimumBrLen_));
+  maximumBrLen_ = maximum;
+  brLenConstraint_ = std::make_shared<IntervalConstraint>(minimumBrLen_, maximumBrLen_, true, true);
+  initBranchLengthsParameters();
+}
+
 std::vector<const Node*> AbstractPlkTreeLikelihood::applyBranchLengths() {
   std::vector<const Node*> changed;
   if (brLenNames_.size() != nodes_.size()) {

@@ -83,14 +83,18 @@ struct PNParam {
 // -lnL; evaluations are counted in *nEval.
 // First derivatives at x (the likelihood sits at x on entry and on return): analytic for the
 // derivable parameters, ThreePointsNumericalDerivative (interval 1e-4, one-sided at a
-// constraint) for the others; d2 alike when asked for.
+// constraint) for the others; d2 alike when asked for.  With points == 2 the numerical
+// derivatives are bpp-core's TwoPointsNumericalDerivative instead: the forward difference
+// (f(x + h) - f(x)) / h, backward where x + h leaves the constraint, no d2.
 struct Derivatives {
   const std::vector<PNParam>& par;
   const std::function<double(const std::vector<double>&)>& eval;
   const std::function<void(size_t, double*, double*)>& analytic;
+  int points = 3;
+  double interval = 0.0001;
   void operator()(const std::vector<double>& x, double fx, std::vector<double>& d1, std::vector<double>* d2) const {
     const size_t n = par.size();
-    const double kInterval = 0.0001;
+    const double kInterval = interval;
     std::vector<double> y(n);
     bool moved_away = false;
     for (size_t i = 0; i < n; i++) {
@@ -105,7 +109,10 @@ struct Derivatives {
         const double v = x[i], h = (1. + std::fabs(v)) * kInterval;
         y = x;
         double fm, fp, f2;
-        if (par[i].correct(v - h) && par[i].correct(v + h)) {
+        if (points == 2) {
+          y[i] = par[i].correct(v + h) ? v + h : v - h;
+          a1 = (eval(y) - fx) / (y[i] - v);
+        } else if (par[i].correct(v - h) && par[i].correct(v + h)) {
           y[i] = v - h;
           fm = eval(y);
           y[i] = v + h;
@@ -429,6 +436,72 @@ unsigned int OptimizationTools::pseudoNewtonParameters(TreeLikelihood* tl, const
 }
 
 unsigned int OptimizationTools::lastSteps_ = 0;
+
+unsigned int OptimizationTools::optimizeNumericalParametersWithGlobalClock2(
+    DiscreteRatesAcrossSitesClockTreeLikelihood* cl, const ParameterList& parameters, OptimizationListener*,
+    double tolerance, unsigned int tlEvalMax, OutputStream* messenger, OutputStream* profiler, unsigned int,
+    const std::string& optMethodDeriv) {
+  if (optMethodDeriv != OPTIMIZATION_GRADIENT && optMethodDeriv != OPTIMIZATION_NEWTON)
+    throw Exception("OptimizationTools::optimizeBranchLengthsParameters. Unknown optimization method: " +
+                    optMethodDeriv);
+  TreeLikelihood* tl = cl;
+  const ParameterList pl = tl->getParameters().getCommonParametersWith(parameters);
+  std::vector<PNParam> par(pl.size());
+  std::vector<double> x(pl.size());
+  for (size_t i = 0; i < pl.size(); i++) {
+    par[i].name = pl[i].getName();
+    if (pl[i].hasConstraint()) par[i].constraint.reset(pl[i].getConstraint()->clone());
+    x[i] = pl[i].getValue();
+  }
+  ParameterList cur = pl;
+  std::function<double(const std::vector<double>&)> f = [&](const std::vector<double>& y) {
+    for (size_t i = 0; i < y.size(); i++) cur[i].setValue(y[i]);
+    tl->setParameters(cur);
+    return tl->getValue();
+  };
+  const std::function<void(size_t, double*, double*)> none = [](size_t, double*, double*) {
+    throw Exception("optimizeNumericalParametersWithGlobalClock2: no analytic derivative");
+  };
+  if (profiler) {
+    *profiler << "Step";
+    for (auto& p : par) *profiler << "\t" << p.name;
+    *profiler << "\tFunction";
+    profiler->endLine();
+  }
+  auto onStep = [&](unsigned int step, const std::vector<double>& y, double fy) {
+    if (profiler) {
+      *profiler << (long)step;
+      for (double v : y) *profiler << "\t" << v;
+      *profiler << "\t" << fy;
+      profiler->endLine();
+    }
+    if (messenger) {
+      *messenger << "step " << (long)step << ": f = " << fy;
+      messenger->endLine();
+    }
+  };
+  unsigned int nEval = 0, steps = 0;
+  if (optMethodDeriv == OPTIMIZATION_NEWTON) {
+    nEval = pseudoNewton(par, x, f, none, tolerance, tlEvalMax, &steps, onStep);
+  } else {
+    // ConjugateGradientMultiDimensions over TwoPointsNumericalDerivative (interval 1e-7,
+    // OptimizationTools.cpp:499-504), FunctionStopCondition |f - f_old| < tolerance
+    std::function<double(const std::vector<double>&)> eval = [&](const std::vector<double>& y) {
+      nEval++;
+      return f(y);
+    };
+    const Derivatives der{par, eval, none, 2, 0.0000001};
+    const double f0 = eval(x);
+    const double f1 = conjugateGradient(par, x, f0, eval, der, tolerance, tlEvalMax, &nEval);
+    onStep(++steps, x, f1);
+  }
+  f(x);  // leave the likelihood at the accepted point
+  lastSteps_ = steps;
+  if (std::getenv("BPP_AMD_OPT_LOG"))
+    std::fprintf(stderr, "GlobalClock2 (%s): %u function evaluations, -lnL = %.12f\n", optMethodDeriv.c_str(), nEval,
+                 tl->getValue());
+  return nEval;
+}
 
 unsigned int OptimizationTools::optimizeNumericalParameters2(TreeLikelihood* tl, const ParameterList& parameters,
                                                              OptimizationListener*, double tolerance,

@@ -190,6 +190,34 @@ int main() {
     double diff2 = abs(thetas[i] - thetasEst2[i]);
     expect("theta_" + to_string(i + 1) + " recovered within 0.2 (both parametrisations)", diff1 <= 0.2 && diff2 <= 0.2);
   }
+  // a change of the root frequencies only (no model, no branch) re-reduces the root with the
+  // new frequencies on every engine path: the lnL-only kernels, the materialising fused
+  // traversal (BPP_AMD_FUSED=0; its cached root reduction must not be reused) and the
+  // per-subtree-compressed one; checked against a fresh likelihood at the new value
+  {
+    unique_ptr<SiteContainer> sites(simulator.simulate(nsites));
+    for (const char* fused : {"1", "0"})
+      for (bool usePatterns : {false, true}) {
+        setenv("BPP_AMD_FUSED", fused, 1);
+        unique_ptr<SubstitutionModelSet> ms(modelSet->clone());
+        RNonHomogeneousTreeLikelihood tl(*tree, *sites, ms.get(), rdist, false, usePatterns, false);
+        tl.initialize();
+        const double before = tl.getValue();
+        ParameterList gc = tl.getParameters().createSubList(vector<string>(1, "GC.theta"));
+        gc[0].setValue(gc[0].getValue() < 0.5 ? 0.8 : 0.2);
+        tl.setParameters(gc);
+        unique_ptr<SubstitutionModelSet> ms2(modelSet->clone());
+        ms2->setParameterValue("GC.theta", gc[0].getValue());
+        RNonHomogeneousTreeLikelihood fresh(*tree, *sites, ms2.get(), rdist, false, usePatterns, false);
+        fresh.initialize();
+        const string tag = string("root frequencies only (fused=") + fused + ", usePatterns=" +
+                           (usePatterns ? "true" : "false") + ")";
+        expect(tag + ": lnL moved", tl.getValue() != before);
+        expectNear(tag + ": same -lnL as a fresh likelihood", tl.getValue(), fresh.getValue(),
+                   1e-12 * fresh.getValue());
+      }
+    unsetenv("BPP_AMD_FUSED");
+  }
   // the reference's fitModelNH on one more simulated alignment, both root parametrisations
   {
     unique_ptr<SiteContainer> sites(simulator.simulate(nsites));

@@ -38,3 +38,34 @@ def test_cpp_drop_in_nh():
     print(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASSED" in r.stdout
+
+
+@pytest.mark.parametrize("name,goldens", [
+    ("test_likelihood", (85.030942031997312824, 65.72293577214308868406)),
+    ("test_likelihood_clock", (94.3957, 71.2657, 92.3295, 71.2657)),
+    ("test_likelihood_nh", ()),
+])
+def test_reference_likelihood_test_runs_unchanged(name, goldens, tmp_path):
+    """The reference's own test program (/root/reference/test/<name>.cpp, compiled unchanged
+    against the Bio++ mirror by the host Makefile in the build container: bin/ref_<name>) runs
+    on the MI355X and passes its own checks (exit status 0: the goldens at its 0.001 / 0.0001
+    tolerances, the SR vs DR derivatives, the NH theta recovery).  The printed -lnL values are
+    also checked here, in the order the program prints them."""
+    assert plk.device_count() > 0, "no GPU visible"
+    exe = os.path.join(HOST, "bin", "ref_" + name)
+    assert os.path.exists(exe), f"{exe} missing: build it where /root/reference exists (make -C {HOST})"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    print(r.stdout[-6000:])
+    print(r.stderr[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    vals = []
+    for line in r.stdout.splitlines():
+        try:
+            vals.append(float(line.strip()))
+        except ValueError:
+            pass
+    for g in goldens:
+        assert any(abs(v - g) <= 1e-3 for v in vals), (g, vals)
+    if name == "test_likelihood_clock":
+        # the clock half: initial 92.3295 after the unconstrained fit, final 71.2657
+        assert abs(vals[2] - 92.3295) <= 1e-3 and abs(vals[3] - 71.2657) <= 1e-3, vals

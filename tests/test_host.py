@@ -245,3 +245,27 @@ def test_host_pseudonewton_conjugate_gradient(host_records):
     r = next(x for x in host_records if x["kind"] == "pn_cg")
     assert abs(r["f"] - 2.0) < 1e-8 and abs(r["x"]) < 1e-3 and abs(r["y"]) < 1e-3, r
     assert r["evals"] < 2000, r
+
+
+# ------------------------------------------------------------------ the reference's own tests
+
+REF_TESTS = ("test_likelihood", "test_likelihood_clock", "test_likelihood_nh")
+REF_DIR = "/root/reference/test"
+
+
+@pytest.mark.parametrize("name", REF_TESTS)
+def test_reference_likelihood_test_compiles_and_links_unchanged(name, tmp_path):
+    """The drop-in: /root/reference/test/<name>.cpp, read where it lies and never
+    copied, compiles and links against the Bio++ mirror (libbpp_phyl_amd over libplk) with no
+    extra include, define or source.  Running it needs the GPU (tests/test_gpu_host.py)."""
+    src = os.path.join(REF_DIR, name + ".cpp")
+    if not os.path.exists(src):
+        pytest.skip("reference tree absent")
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "bpp-phyl_amd")], check=True)
+    subprocess.run(["make", "-s", "-j8", "-C", HOST, "libbpp_phyl_amd.so"], check=True)
+    exe = str(tmp_path / name)
+    r = subprocess.run(["g++", "-std=c++17", "-O0", "-w", "-I" + os.path.join(HOST, "include"),
+                        "-I" + os.path.join(ROOT, "include"), "-o", exe, src, "-L" + HOST, "-lbpp_phyl_amd",
+                        "-L" + os.path.join(ROOT, "bpp-phyl_amd"), "-lplk"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert os.path.getsize(exe) > 0
