@@ -50,7 +50,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of the job: one rank each under torch.distributed.run (WORLD_SIZE must match), "
+                         "else one process over devices 0..N-1 (plk_create_multi)")
+    ap.add_argument("--devices", default=None,
+                    help="one-process multi-device mode: comma-separated device list of --gpus entries "
+                         "(e.g. 0,0 rehearses two shards on one GPU; the line is then marked a rehearsal)")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the config-5 strong-scaling sub-record of the default line")
+    ap.add_argument("--strong-steps", type=int, default=10, help="timed steps of the strong sub-record")
+    ap.add_argument("--strong-patterns", type=int, default=None,
+                    help="tests only: patterns of the strong sub-record (default config 5's 2M)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=None, choices=sorted(workload.CONFIGS),
@@ -271,16 +281,158 @@ def _json_stdout():
     return os.fdopen(fd, "w")
 
 
+class LaunchError(SystemExit):
+    """Bad --gpus / --devices / launcher combination: exit non-zero before any GPU call."""
+
+    def __init__(self, msg: str):
+        print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+        super().__init__(2)
+
+
+def launch_layout(args):
+    """How the N GPUs are driven.  Under torch.distributed.run (WORLD_SIZE set): one rank
+    per GPU, WORLD_SIZE must equal --gpus.  Without a launcher and --gpus N > 1: ONE process
+    over devices 0..N-1 (or --devices) through one plk_create_multi handle, which shards the
+    patterns in contiguous 4096-aligned ranges, launches every device before the first wait
+    and sums the block sums in global order (bitwise one device).  Never silently fewer GPUs."""
+    world_env = "WORLD_SIZE" in os.environ
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env:
+        if args.devices:
+            raise LaunchError("--devices is the one-process multi-device mode; not under torch.distributed.run")
+        if world != args.gpus:
+            raise LaunchError(f"WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU")
+        return {"kind": "ranks", "world": world, "devices": None}
+    devices = None
+    if args.devices:
+        devices = [int(x) for x in args.devices.split(",") if x.strip() != ""]
+        if len(devices) != args.gpus:
+            raise LaunchError(f"--devices lists {len(devices)} device(s) for --gpus {args.gpus}")
+    elif args.gpus > 1:
+        n = plk.device_count()
+        if args.gpus > n:
+            raise LaunchError(f"--gpus {args.gpus} but only {n} GPU(s) visible")
+        devices = list(range(args.gpus))
+    if args.gpus < 1:
+        raise LaunchError("--gpus must be >= 1")
+    return {"kind": "multi" if devices and len(devices) > 1 else "single", "world": 1, "devices": devices}
+
+
+def measure(args, lay, ctx, config, scaling, patterns=None, classes=None, mode="lnl", steps=None, warmup=None):
+    """Set up one workload over the launch layout and time `steps` evaluations bracketed by
+    a barrier + device synchronisation on both sides (max over ranks).  Returns the record
+    pieces; `value` = the job's P x I per step x steps / time."""
+    import torch
+
+    dist, rank, world = ctx["dist"], ctx["rank"], lay["world"]
+    rehearse = ctx["rehearse"]
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    wl = workload.make_workload(config, n_classes=classes)
+    cfg = workload.CONFIGS[config]
+    P_arg = patterns or (cfg.get("global_patterns", wl.n_patterns) if scaling == "strong" else wl.n_patterns)
+    n_gpu = args.gpus
+    if lay["kind"] == "ranks":
+        start, end, P_job = shard.bench_range(scaling, rank, world, P_arg)
+        device = ctx["device"]
+        P_timed = end - start          # the patterns of the handle whose kernels are timed
+    else:
+        P_job = P_arg * n_gpu if scaling == "weak" else P_arg
+        start, end = 0, P_job
+        device = lay["devices"] if lay["kind"] == "multi" else 0
+        P_timed = shard.shard_range(0, n_gpu, P_job)[1] if lay["kind"] == "multi" else P_job
+    wl.n_patterns = end - start
+    t_setup = time.time()
+    extra = {"lnl": plk.PLK_FLAG_LNL_ONLY, "materialize": 0, "levelwise": plk.PLK_FLAG_LEVELWISE,
+             "subtree": plk.PLK_FLAG_SUBTREE_PATTERNS}[mode]
+    sim_dev = f"cuda:{ctx['device']}" if torch.cuda.is_available() else None
+    ev = workload.Evaluator(wl, device, start, end, extra_flags=extra, sim_device=sim_dev)
+    xchg = None
+    if dist is not None and rehearse:
+        # one GPU, every rank on cuda:0: RCCL cannot put two ranks on one device, so the
+        # rehearsal exchanges the block sums through torch.distributed (gloo)
+        xchg = shard.BlockExchange(dist, ev.n_blocks, device=ctx["coll_dev"])
+    elif dist is not None:
+        # the RCCL communicator inside the handle (plk_comm_init): plk_evaluate all-gathers
+        # every rank's block sums on the engine's stream and returns the global lnL
+        cid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            cid.copy_(torch.frombuffer(bytearray(plk.comm_get_id()), dtype=torch.uint8))
+        dist.broadcast(cid, 0)
+        ev.eng.comm_init(world, rank, bytes(cid.cpu().numpy()))
+    t_setup = time.time() - t_setup
+
+    def one_step():
+        lnl, _, blocks = ev.step()
+        if xchg is None:
+            return lnl  # global: plk_evaluate summed every rank's / device's block sums in global order
+        return xchg.lnl(blocks)
+
+    if dist is not None and not rehearse:
+        # check the in-handle exchange once against torch.distributed's all-gather of the
+        # same per-rank block sums (bitwise), before anything is timed
+        lnl0, _, blocks0 = ev.step()
+        ref = shard.BlockExchange(dist, ev.n_blocks, device=ctx["coll_dev"]).lnl(blocks0)
+        if ref != lnl0:
+            raise RuntimeError(f"rank {rank}: in-handle RCCL lnL {lnl0!r} != torch all-gather {ref!r}")
+    lnl = None
+    for _ in range(warmup):
+        lnl = one_step()
+    ev.eng.reset_timing()
+    # HIP events around the traversal launches and their table builds only (each timed
+    # launch adds an event pair), on every K-th timed step: the kernels' mean durations are
+    # sampled inside the timed region without charging every step the events' stream time
+    k_ev = max(1, args.event_every)
+    mask = 0 if args.no_events else (plk.PLK_TIME_PARTIALS | plk.PLK_TIME_TABLES)
+    ev_steps = 0
+    if dist is not None:
+        dist.barrier()
+    ev.eng.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        if i % k_ev == 0:
+            ev.eng.set_timing(mask)
+            ev_steps += 1
+        elif k_ev > 1 and i % k_ev == 1:
+            ev.eng.set_timing(0)
+        lnl = one_step()
+    if dist is not None:
+        dist.barrier()
+    ev.eng.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    tm = ev.eng.get_timing()
+    ev.eng.set_timing(False)
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=ctx["coll_dev"])
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    units_step = P_job * wl.et.n_internal   # the whole job's node updates per step
+    return {"wl": wl, "ev": ev, "P": P_timed, "P_job": P_job, "lnl": lnl, "elapsed": elapsed, "tm": tm,
+            "ev_steps": ev_steps, "k_ev": k_ev, "steps": steps, "units_step": units_step, "t_setup": t_setup,
+            "value": units_step * steps / elapsed, "ms_step": elapsed * 1e3 / steps}
+
+
+def parallelism(lay, args) -> str:
+    if lay["kind"] == "ranks":
+        return f"pattern-shard x{lay['world']}"
+    if lay["kind"] == "multi":
+        return f"multi-device x{args.gpus}"
+    return "pattern-shard x1"
+
+
 def main():
     args = parse()
+    lay = launch_layout(args)
     out = _json_stdout()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = lay["world"]
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
     dist = None
-    use_dist = world > 1 or (args.force_dist and "WORLD_SIZE" in os.environ)
+    use_dist = lay["kind"] == "ranks" and (world > 1 or args.force_dist)
     rehearse = use_dist and args.dist_backend == "gloo"
     if use_dist:
         import torch.distributed as dist  # noqa: F811
@@ -293,81 +445,14 @@ def main():
     else:
         torch.cuda.set_device(0)
     device = local if use_dist and not rehearse else 0
-    coll_dev = "cpu" if rehearse else "cuda"
+    ctx = {"dist": dist, "rank": rank, "rehearse": rehearse, "device": device,
+           "coll_dev": "cpu" if rehearse else "cuda"}
 
-    wl = workload.make_workload(args.config, n_classes=args.classes)
-    cfg = workload.CONFIGS[args.config]
-    P_arg = args.patterns or (cfg.get("global_patterns", wl.n_patterns) if args.scaling == "strong" else wl.n_patterns)
-    start, end, P_job = shard.bench_range(args.scaling, rank, world, P_arg)
-    P = end - start            # this rank's patterns
-    wl.n_patterns = P
-    t_setup = time.time()
-    extra = {"lnl": plk.PLK_FLAG_LNL_ONLY, "materialize": 0, "levelwise": plk.PLK_FLAG_LEVELWISE,
-             "subtree": plk.PLK_FLAG_SUBTREE_PATTERNS}[args.mode]
-    ev = workload.Evaluator(wl, device, start, end, extra_flags=extra)
-    xchg = None
-    if dist is not None and rehearse:
-        # one GPU, every rank on cuda:0: RCCL cannot put two ranks on one device, so the
-        # rehearsal exchanges the block sums through torch.distributed (gloo)
-        xchg = shard.BlockExchange(dist, ev.n_blocks, device=coll_dev)
-    elif dist is not None:
-        # the RCCL communicator inside the handle (plk_comm_init): plk_evaluate all-gathers
-        # every rank's block sums on the engine's stream and returns the global lnL
-        cid = torch.zeros(128, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            cid.copy_(torch.frombuffer(bytearray(plk.comm_get_id()), dtype=torch.uint8))
-        dist.broadcast(cid, 0)
-        ev.eng.comm_init(world, rank, bytes(cid.cpu().numpy()))
-    t_setup = time.time() - t_setup
-    units_step = P_job * wl.et.n_internal   # the whole job's node updates per step
-
-    def one_step():
-        lnl, _, blocks = ev.step()
-        if xchg is None:
-            return lnl  # global: plk_evaluate summed every rank's block sums in fixed global order
-        return xchg.lnl(blocks)
-
-    if dist is not None and not rehearse:
-        # check the in-handle exchange once against torch.distributed's all-gather of the
-        # same per-rank block sums (bitwise), before anything is timed
-        lnl0, _, blocks0 = ev.step()
-        ref = shard.BlockExchange(dist, ev.n_blocks, device=coll_dev).lnl(blocks0)
-        if ref != lnl0:
-            raise RuntimeError(f"rank {rank}: in-handle RCCL lnL {lnl0!r} != torch all-gather {ref!r}")
-    for _ in range(args.warmup):
-        lnl = one_step()
-    ev.eng.reset_timing()
-    # HIP events around the traversal launches and their table builds only (each timed
-    # launch adds an event pair), on every K-th timed step: the kernels' mean durations are
-    # sampled inside the timed region without charging every step the events' stream time
-    k_ev = max(1, args.event_every)
-    mask = 0 if args.no_events else (plk.PLK_TIME_PARTIALS | plk.PLK_TIME_TABLES)
-    ev_steps = 0
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        if i % k_ev == 0:
-            ev.eng.set_timing(mask)
-            ev_steps += 1
-        elif k_ev > 1 and i % k_ev == 1:
-            ev.eng.set_timing(0)
-        lnl = one_step()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    tm = ev.eng.get_timing()
-    ev.eng.set_timing(False)
-    if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-
+    m = measure(args, lay, ctx, args.config, args.scaling, patterns=args.patterns, classes=args.classes,
+                mode=args.mode)
+    wl, ev, P, P_job, tm, ev_steps, k_ev = m["wl"], m["ev"], m["P"], m["P_job"], m["tm"], m["ev_steps"], m["k_ev"]
+    rec = None
     if rank == 0:
-        ms_step = elapsed * 1e3 / args.steps
-        value = units_step * args.steps / elapsed
         work = ev.eng.traversal_work()
         traffic, traffic_src = measured_traffic(args.config, args.mode, P)
         roof = roofline(wl, args.mode, P, ev_steps, tm, work, traffic) if not args.no_events else None
@@ -375,15 +460,17 @@ def main():
             roof["event_sample"] = f"HIP events on {ev_steps} of {args.steps} timed steps (every {k_ev})"
             if traffic_src:
                 roof["traffic_source"] = traffic_src
+            if lay["kind"] == "multi":
+                roof["timed_shard"] = f"device {lay['devices'][0]} (shard 0 of {args.gpus}, {P} patterns)"
         computed = work["node_updates"]
         rec = {
             "metric": "site-pattern x node partial updates/s",
-            "value": value,
+            "value": m["value"],
             "unit": "updates/s",
-            "n_gpus": world,
+            "n_gpus": args.gpus,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms_step,
+            "ms_per_step": m["ms_step"],
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
@@ -391,7 +478,7 @@ def main():
             "data": "synthetic (seeded counter-based simulation under the model, 1 pattern = 1 column)",
             "config": {
                 "workload": (f"{args.config}: {wl.models[0].name}{'+G%d' % wl.C if wl.C > 1 else ''} "
-                             f"{wl.alphabet.name}, {P_job} patterns in total ({P} on rank 0), "
+                             f"{wl.alphabet.name}, {P_job} patterns in total ({P} on GPU 0), "
                              f"{wl.et.n_tips}-taxon balanced tree "
                              f"({'rooted' if wl.model_of_node is not None else 'unrooted'}, I={wl.et.n_internal})"),
                 "patterns_per_gpu": P,
@@ -401,15 +488,15 @@ def main():
                 "states": wl.S,
                 "classes": wl.C,
                 "mode": args.mode,
-                "parallelism": f"pattern-shard x{world}",
+                "parallelism": parallelism(lay, args),
             },
-            "lnl": lnl,
+            "lnl": m["lnl"],
             "kernel_path": ev.eng.kernel_path(),
             # node updates the kernels compute per pattern (cherry-table nodes and
             # per-subtree compression are lookups / skipped) -- value above is the
             # reference-equivalent ("effective") rate
             "computed_updates_per_step": computed * P_job / P,
-            "computed_updates_per_s": computed * P_job / P * args.steps / elapsed,
+            "computed_updates_per_s": computed * P_job / P * args.steps / m["elapsed"],
             "table_nodes": work["table_nodes"],
             "partials_only_updates_per_s": (P * wl.et.n_internal * ev_steps / (tm["partials_ms"] * 1e-3)
                                             if tm["partials_ms"] > 0 else None),
@@ -425,14 +512,49 @@ def main():
                                       tm["host_us"])} if tm.get("evaluations") else None),
             "table_launches_per_step": tm["table_launches"] / max(ev_steps, 1),
             "roofline": roof,
-            "setup_s": t_setup,
+            "setup_s": m["t_setup"],
         }
+        if args.devices:
+            rec["config"]["devices"] = args.devices
+            if len(set(lay["devices"])) < len(lay["devices"]):
+                rec["rehearsal"] = (f"devices {args.devices}: several shards share a GPU -- the multi-device "
+                                    f"path exercised, not an {args.gpus}-GPU measurement")
         if args.mode == "subtree":
             rec["metric"] += " (EFFECTIVE: per-subtree pattern compression)"
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and lay["kind"] == "single" and not args.no_cpu_baseline:
             ns = args.cpu_sample or workload.CONFIGS[args.config]["cpu_sample"]
             _, eng_sites, _ = ev.eng.root_loglik(wl.et.root, want_sites=True)
             rec["cpu_baseline"] = cpu_baseline(wl, min(ns, P), args.cpu_runs, eng_sites)
+    ev.eng.close()
+    del m, ev
+    if not args.no_strong and args.scaling == "weak" and args.config == "gtr_g4_dna_1M_64":
+        # the strong-scaling curve BASELINE config 5 names, from the same sweep: config 5's 2M
+        # patterns split over the same N GPUs, timed the same way (the N = 1 line is all 2M on
+        # one GPU), so the driver's N = 1, 2, 4, 8 lines carry both curves
+        s = measure(args, lay, ctx, "nh_gtr_g4_dna_2M_512", "strong", patterns=args.strong_patterns,
+                    steps=args.strong_steps, warmup=2)
+        if rank == 0:
+            trav = (s["tm"]["partials_ms"] + s["tm"]["tables_ms"]) / max(s["ev_steps"], 1)
+            flops = s["wl"].algorithmic_flops_per_pattern() * s["P"]
+            rec["strong"] = {
+                "config": "nh_gtr_g4_dna_2M_512 (BASELINE config 5): NH-GTR+G4 DNA, 512-taxon rooted tree, "
+                          f"I={s['wl'].et.n_internal}, {s['P_job']} patterns split over {args.gpus} GPU(s)",
+                "scaling": "strong",
+                "n_gpus": args.gpus,
+                "value": s["value"],
+                "unit": "updates/s",
+                "ms_per_step": s["ms_step"],
+                "steps": s["steps"],
+                "patterns_total": s["P_job"],
+                "patterns_per_gpu": s["P"],
+                "kernel_path": s["ev"].eng.kernel_path(),
+                "traversal_ms": trav,
+                "traversal_frac_fp64": (flops / (trav * 1e-3) / 1e12 / FP64_PEAK_TFS) if trav > 0 else None,
+                "lnl": s["lnl"],
+                "setup_s": s["t_setup"],
+            }
+        s["ev"].eng.close()
+    if rank == 0:
         print(json.dumps(rec), file=out, flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -81,8 +81,12 @@ class Workload:
             f += sum(2 * self.C * S_live * S_live for c in ch if c >= nt) + (len(ch) - 1) * self.C * S_live
         return f
 
-    def simulate(self, start: int, end: int) -> np.ndarray:
-        """States [n_tips][end-start] for sites [start, end)."""
+    def simulate(self, start: int, end: int, device=None) -> np.ndarray:
+        """States [n_tips][end-start] for sites [start, end).  device: a torch device to run
+        the same counter-based generator on (bitwise the same states; config 5's 2M patterns
+        x 1023 nodes take minutes in numpy and well under a second on the GPU)."""
+        if device is not None:
+            return self._simulate_torch(start, end, device)
         et, S = self.et, self.S
         n = end - start
         cls = np.minimum((uniforms(self.seed, 1, start, end) * self.C).astype(np.int64), self.C - 1)
@@ -97,6 +101,52 @@ class Workload:
                 u = uniforms(self.seed, 16 + c, start, end)
                 state[c] = (u[:, None] > rows).sum(axis=1).clip(0, S - 1)
         return state[: et.n_tips]
+
+    def _simulate_torch(self, start: int, end: int, device) -> np.ndarray:
+        """simulate() in torch: uint64 splitmix on int64 tensors (wrapping multiply, logical
+        shifts masked), the same cumulative rows and comparisons, so the states are bitwise
+        those of the numpy generator (tests/test_host.py checks it)."""
+        import torch
+
+        et, S, C = self.et, self.S, self.C
+        n = end - start
+        dev = torch.device(device)
+        idx = torch.arange(start, end, dtype=torch.int64, device=dev)
+
+        def uni(stream):
+            key = idx + _signed(((self.seed * 1000003 + stream) & 0xFFFFFFFF) << 32)
+            z = _splitmix_t(_splitmix_t(key))
+            return _lsr(z, 11).to(torch.float64) * (1.0 / 9007199254740992.0)
+
+        cls = torch.clamp((uni(1) * C).to(torch.int64), max=C - 1)
+        state = torch.empty((et.n_nodes, n), dtype=torch.int16, device=dev)
+        cum0 = torch.from_numpy(np.cumsum(self.root_freqs)).to(dev)
+        state[et.root] = torch.searchsorted(cum0, uni(2), right=True).clamp(0, S - 1)
+        for p, ch in reversed(et.ops):
+            for c in ch:
+                m = self.models[0] if self.model_of_node is None else self.models[self.model_of_node[c]]
+                cum = torch.from_numpy(np.cumsum(np.stack([m.pij(et.brlen[c] * r) for r in self.rates]),
+                                                 axis=2)).to(dev)
+                rows = cum[cls, state[p].long()]
+                state[c] = (uni(16 + c)[:, None] > rows).sum(dim=1).clamp(0, S - 1)
+        return state[: et.n_tips].cpu().numpy()
+
+
+def _signed(v: int) -> int:
+    v &= 0xFFFFFFFFFFFFFFFF
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def _lsr(z, k: int):
+    """Logical right shift of int64 tensors holding uint64 bit patterns."""
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def _splitmix_t(x):
+    z = x + _signed(0x9E3779B97F4A7C15)
+    z = (z ^ _lsr(z, 30)) * _signed(0xBF58476D1CE4E5B9)
+    z = (z ^ _lsr(z, 27)) * _signed(0x94D049BB133111EB)
+    return z ^ _lsr(z, 31)
 
 
 def _gtr_cfg2() -> phylo.Model:
@@ -157,15 +207,18 @@ def make_workload(name: str, n_patterns: Optional[int] = None, seed: int = 42,
 class Evaluator:
     """One libplk engine holding the patterns [start, end) of a workload."""
 
-    def __init__(self, wl: Workload, device: int, start: int, end: int, states: Optional[np.ndarray] = None,
-                 extra_flags: int = 0):
+    def __init__(self, wl: Workload, device, start: int, end: int, states: Optional[np.ndarray] = None,
+                 extra_flags: int = 0, sim_device=None):
+        """device: a HIP device, or a list of them (one plk_create_multi handle sharding the
+        patterns); sim_device: a torch device for the alignment simulation (bitwise the same
+        states as numpy, Workload.simulate)."""
         self.wl = wl
         self.start, self.end = start, end
         et = wl.et
         flags = (plk.PLK_FLAG_SCALING if wl.scaling else 0) | (plk.PLK_FLAG_NONNEG_GUARD if wl.guard else 0) | extra_flags
         self.eng = plk.Engine(device, wl.S, wl.C, end - start, et.n_tips, et.n_internal, len(wl.models), flags)
         self.eng.set_code_table(wl.alphabet.init_table)
-        st = wl.simulate(start, end) if states is None else states
+        st = wl.simulate(start, end, device=sim_device) if states is None else states
         for i in range(et.n_tips):
             self.eng.set_tip_codes(i, phylo.states_to_codes(st[i]))
         self.eng.set_category_rates(wl.rates, wl.probs)

@@ -182,3 +182,35 @@ def test_cpp_drop_in_sharded_goldens():
                        timeout=600, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASSED" in r.stdout
+
+
+def _bench_line(*extra):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--patterns", "50000", "--strong-patterns", "40000", "--strong-steps", "2",
+                        "--no-cpu-baseline", *extra], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_gpus2_one_process_rehearsal():
+    """bench.py --gpus 2 without a launcher: one process, one plk_create_multi handle over the
+    devices (here --devices 0,0, two shards on the one GPU of this box): the line says
+    n_gpus 2, multi-device x2, marks the rehearsal, and its config-5 strong sub-record gives the
+    1-GPU lnL bitwise (the same 40 000 patterns split over two shards)."""
+    one = _bench_line("--gpus", "1")
+    two = _bench_line("--gpus", "2", "--devices", "0,0")
+    assert one["n_gpus"] == 1 and one["config"]["parallelism"] == "pattern-shard x1" and "rehearsal" not in one
+    assert two["n_gpus"] == 2 and two["config"]["parallelism"] == "multi-device x2" and "rehearsal" in two
+    assert two["config"]["patterns_total"] == 100000 and two["config"]["patterns_per_gpu"] == 53248
+    assert one["strong"]["n_gpus"] == 1 and two["strong"]["n_gpus"] == 2
+    assert one["strong"]["patterns_total"] == two["strong"]["patterns_total"] == 40000
+    assert one["strong"]["lnl"] == two["strong"]["lnl"]
+    assert one["kernel_path"] == two["kernel_path"] == "jit_tree4"
