@@ -10,6 +10,7 @@
 #include <Bpp/Phyl/Model/SubstitutionModelSet.h>
 #include <Bpp/Phyl/Simulation/NonHomogeneousSequenceSimulator.h>
 #include <Bpp/Numeric/Prob/GammaDiscreteDistribution.h>
+#include <Bpp/Phyl/Likelihood/ClockTreeLikelihood.h>
 #include <Bpp/Phyl/OptimizationTools.h>
 #include <Bpp/Phyl/TreeTemplate.h>
 #include <Bpp/Seq/Alphabet/AlphabetTools.h>
@@ -26,12 +27,12 @@ using namespace bpp;
 // minimum the Newton move d1/d2 = x (1 + x^2) overshoots by orders of magnitude, so three
 // Felsenstein-Churchill halvings do not help and the fourth correction -- the
 // conjugate-gradient search -- has to find the way.
-class OvershootLikelihood : public TreeLikelihood {
+class OvershootLikelihood : public virtual TreeLikelihood {
   TreeTemplate<Node> tree_;
   mutable unsigned evals_ = 0;
 
  public:
-  OvershootLikelihood() : tree_(*TreeTemplateTools::parenthesisToTree("(a:1,b:1);")) {
+  OvershootLikelihood() : tree_(*std::unique_ptr<TreeTemplate<Node> >(TreeTemplateTools::parenthesisToTree("(a:1,b:1);"))) {
     addParameter_(Parameter("x", 10.));
     addParameter_(Parameter("y", -7.));
   }
@@ -67,6 +68,9 @@ class OvershootLikelihood : public TreeLikelihood {
   void enableFirstOrderDerivatives(bool) override {}
   void enableSecondOrderDerivatives(bool) override {}
 };
+
+// The same function behind the global-clock interface, for optimizeNumericalParametersWithGlobalClock2
+class OvershootClock : public OvershootLikelihood, public DiscreteRatesAcrossSitesClockTreeLikelihood {};
 
 static void printVec(const char* key, const std::vector<double>& v) {
   std::printf("\"%s\": [", key);
@@ -241,6 +245,16 @@ int main() {
     std::printf("{\"kind\": \"pn_cg\", \"f\": %.17g, \"x\": %.17g, \"y\": %.17g, \"evals\": %u, \"steps\": %u}\n",
                 rl.getValue(), rl.getParameters().getParameterValue("x"), rl.getParameters().getParameterValue("y"), n,
                 OptimizationTools::lastSteps_);
+  }
+  // optimizeNumericalParametersWithGlobalClock2: conjugate gradient over two-point numerical
+  // derivatives (the default), and PseudoNewton over three-point ones
+  for (const std::string& method : {OptimizationTools::OPTIMIZATION_GRADIENT, OptimizationTools::OPTIMIZATION_NEWTON}) {
+    OvershootClock rl;
+    const unsigned n = OptimizationTools::optimizeNumericalParametersWithGlobalClock2(&rl, rl.getParameters(), 0, 1e-10,
+                                                                                      20000, 0, 0, 1, method);
+    std::printf("{\"kind\": \"clock2\", \"method\": \"%s\", \"f\": %.17g, \"x\": %.17g, \"y\": %.17g, \"evals\": %u}\n",
+                method.c_str(), rl.getValue(), rl.getParameters().getParameterValue("x"),
+                rl.getParameters().getParameterValue("y"), n);
   }
   return 0;
 }

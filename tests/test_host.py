@@ -247,6 +247,17 @@ def test_host_pseudonewton_conjugate_gradient(host_records):
     assert r["evals"] < 2000, r
 
 
+def test_host_global_clock2_optimisers(host_records):
+    """optimizeNumericalParametersWithGlobalClock2 (OptimizationTools.cpp:484-539) on the same
+    host-only function behind the clock interface: the default OPTIMIZATION_GRADIENT (conjugate
+    gradient over two-point derivatives, interval 1e-7) and OPTIMIZATION_NEWTON both reach (0, 0)."""
+    recs = {r["method"]: r for r in host_records if r["kind"] == "clock2"}
+    assert set(recs) == {"gradient", "newton"}, recs
+    for r in recs.values():
+        assert abs(r["f"] - 2.0) < 1e-7 and abs(r["x"]) < 1e-3 and abs(r["y"]) < 1e-3, r
+        assert r["evals"] < 5000, r
+
+
 # ------------------------------------------------------------------ the reference's own tests
 
 REF_TESTS = ("test_likelihood", "test_likelihood_clock", "test_likelihood_nh")
