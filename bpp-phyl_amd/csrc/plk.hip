@@ -140,8 +140,6 @@ struct plk_handle_s {
   double* pmats = nullptr;
   double* dpmats = nullptr;
   double* d2pmats = nullptr;
-  double* dpmatsT = nullptr;   // dP^T, d2P^T: the fused 20/64-state DR preorder
-  double* d2pmatsT = nullptr;
   double* V = nullptr;
   double* Vinv = nullptr;
   double* lambda = nullptr;
@@ -592,7 +590,7 @@ int ensure_pmatsT(plk_handle h) {
 
 int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs& a) {
   const int S = h->S;
-  if (S == 64 && !tune_get("GENERIC64")) {
+  if (S == 64) {
     // K3: fp64 MFMA, P^T staged in LDS
     int rc = ensure_pmatsT(h);
     if (rc) return rc;
@@ -604,7 +602,7 @@ int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs
       partials_mfma64_kernel<false><<<grid, block, lds, h->stream>>>(d_ops, a, h->pmatsT, h->C);
     return PLK_OK;
   }
-  if (S == 20 && !tune_get("GENERIC20")) {
+  if (S == 20) {
     // K2: P rows through scalar loads, tip tables in LDS
     const size_t lds = 3 * (size_t)h->C * h->n_codes * S * sizeof(double);
     if (lds <= 160 * 1024) {
@@ -624,7 +622,6 @@ int launch_generic(plk_handle h, const KOp* d_ops, int n_ops, const PartialsArgs
     case 3: launch_generic_S<3, 3>(h, d_ops, n_ops, a, lds); break;
     case 4: launch_generic_S<4, 4>(h, d_ops, n_ops, a, lds); break;
     case 20: launch_generic_S<20, 20>(h, d_ops, n_ops, a, lds); break;
-    case 64: launch_generic_S<64, 16>(h, d_ops, n_ops, a, lds); break;
     default: return fail(h, PLK_ERR_UNSUPPORTED, "state count %d has no kernel instance", S);
   }
   return PLK_OK;
@@ -638,7 +635,7 @@ int refresh_tip_tables(plk_handle h) {
     if (!h->pmat_valid[t]) return fail(h, PLK_ERR_STATE, "transition matrix of tip branch %d not set", t);
   if (h->n_tips > 0) {
     dim3 grid(h->n_tips, h->C);
-    if (h->S == 64 && !tune_is("PMAT64", '0'))
+    if (h->S == 64)
       tip_table64_kernel<<<grid, 256, (size_t)(64 * 64 + h->n_codes * 64) * sizeof(double), h->stream>>>(
           h->pmats, h->code_table, h->tipP, h->n_tips, h->C, h->n_codes);
     else
@@ -946,7 +943,7 @@ int plk_destroy(plk_handle h) {
   void* bufs[] = {h->partials, h->scale, h->codes, h->code_table, h->tipP, h->pmats, h->dpmats, h->d2pmats,
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
-                  h->d2_sums, h->d_dprog, h->pmatsT, h->dpmatsT, h->d2pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
+                  h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
                   h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre};
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -1189,8 +1186,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   PmatInline inl;
   inl.n = 0;
   const size_t off_t = 0, off_b = (size_t)n * sizeof(double), off_m = off_b + (size_t)n * sizeof(int32_t);
-  const char* staged_env = tune_get("PMAT_STAGED");
-  if (n <= kPmatInline && !(staged_env && staged_env[0] == '1')) {
+  if (n <= kPmatInline) {
     inl.n = n;
     for (int i = 0; i < n; ++i) {
       inl.t[i] = t[i];
@@ -1240,7 +1236,7 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   a.n_req = n;
   // tip tables ride along for S <= 20 (P of the block staged in LDS; S = 64 keeps the
   // separate tip_table_kernel)
-  const bool k64 = h->S == 64 && deriv_mask == PLK_DERIV_P && !tune_is("PMAT64", '0');
+  const bool k64 = h->S == 64 && deriv_mask == PLK_DERIV_P;
   const bool tips_fused = h->table_set && (h->S <= 20 || (k64 && h->n_codes <= 64));
   a.init = tips_fused ? h->code_table : nullptr;
   a.tipP = h->tipP;
@@ -1254,13 +1250,11 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   const size_t lds = (size_t)(h->S + (tips_fused ? 3 : 2) * S2) * sizeof(double);
   // pmat64s_kernel and pmat_kernel also write the transposed copy the matrix-core kernels
   // read (allocated by the first transposed-P use), so an evaluation needs no transpose launch
-  const bool pk_generic = !k64 && !(h->S == 4 && !tune_is("PMAT4", '0'));
-  if (((k64 && !tune_is("PMAT64_SPLIT", '0')) || pk_generic) && (deriv_mask & PLK_DERIV_P)) a.PT = h->pmatsT;
-  if (k64 && !tune_is("PMAT64_SPLIT", '0'))
+  const bool pk_generic = !k64 && h->S != 4;
+  if ((k64 || pk_generic) && (deriv_mask & PLK_DERIV_P)) a.PT = h->pmatsT;
+  if (k64)
     pmat64s_kernel<<<dim3(n, h->C, 4), dim3(256), (size_t)(64 + 16 * 64 + S2) * sizeof(double), h->stream>>>(a, inl);
-  else if (k64)
-    pmat64_kernel<<<dim3(n, h->C), dim3(256), (size_t)(64 + 2 * S2) * sizeof(double), h->stream>>>(a, inl);
-  else if (h->S == 4 && !tune_is("PMAT4", '0'))
+  else if (h->S == 4)
     pmat4_kernel<<<dim3((unsigned)((n * h->C * 4 + 63) / 64)), dim3(64), 0, h->stream>>>(a, inl);
   else
   {
@@ -1340,16 +1334,10 @@ namespace {
 // ---------------------------------------------------------------------------
 // Fused 4-state traversal: program builder + launches (kernel in plk_tree4.hpp).
 // ---------------------------------------------------------------------------
-constexpr int kTree4Levels(int CW) { return CW >= 4 ? 6 : 8; }
-
-// classes per wave of the fused kernel (PLK_TREE4_CW overrides; default 1 = one
-// wave per rate class, the smallest register footprint and the highest occupancy)
-int tree4_cw(plk_handle h) {
-  int cw = 1;
-  if (const char* e = tune_get("TREE4_CW")) cw = std::atoi(e);
-  if (cw != 1 && cw != 2 && cw != 4) cw = 1;
-  return std::min(cw, h->C);
-}
+// register levels of the interpreter (one wave per rate class: the smallest register
+// footprint and the highest occupancy; the generated kernel also puts every class of a
+// pattern in one wave, with the same results bitwise)
+constexpr int kTree4Levels = 8;
 
 // Fused traversal kernels: 4 states -> the VALU tree kernels (plk_jit.hpp generated per
 // tree, tree4_kernel interpreting the same program); 20 states -> jit_treeM (plk_jitm.hpp,
@@ -1358,9 +1346,8 @@ enum FusedKind { FK_NONE = 0, FK_TREE4, FK_TREEM };
 
 FusedKind fused_kind(plk_handle h) {
   if (h->flags & PLK_FLAG_LEVELWISE) return FK_NONE;
-  // 4 states: the VALU tree kernel (plk_jit.hpp); PLK_S4_JITM=1 runs them on the matrix
-  // cores instead (jit_treeM with one 4x4x4 block per class and 16 patterns)
-  if (h->S == 4 && tune_is("S4_JITM", '1') && !tune_is("JITM", '0') && h->C <= kTreeMaxWaves) return FK_TREEM;
+  // 4 states: the VALU tree kernel (plk_jit.hpp); on the 4x4x4 matrix cores (one block per
+  // class and 16 patterns) it measured slower
   if (h->S == 4) return (h->C == 1 || h->C == 2 || h->C == 4) ? FK_TREE4 : FK_NONE;
   if (h->C > kTreeMaxWaves) return FK_NONE;
   if (h->S == 20) return FK_TREEM;
@@ -1379,13 +1366,13 @@ int tune_int(const char* key, int def, int lo, int hi) {
 
 // 4 states, one class per wave: the tree-specialised kernel (plk_jit.hpp) serves the
 // fused traversal; PLK_JIT=0 keeps the interpreter (tree4_kernel), e.g. for A/B runs.
-bool jit_tree4(plk_handle h) { return fused_kind(h) == FK_TREE4 && tree4_cw(h) == 1 && !tune_is("JIT", '0'); }
+bool jit_tree4(plk_handle h) { return fused_kind(h) == FK_TREE4 && !tune_is("JIT", '0'); }
 
 // 20 states: the tree-specialised kernel on v_mfma_f64_4x4x4_4b (plk_jitm.hpp) serves the
 // fused traversal; PLK_JITM=0 keeps the treeM interpreter (16x16x4 MFMA), e.g. for A/B runs.
 bool jit_treeM(plk_handle h) {
   if (fused_kind(h) != FK_TREEM || tune_is("JITM", '0')) return false;
-  return h->S == 20 || h->S == 4;
+  return h->S == 20;
 }
 
 // Classes in one wave (plk_jit.hpp, CW = C): the joint rescale needs no cross-wave
@@ -1401,15 +1388,12 @@ bool jit_ciw(plk_handle h) {
 
 // tips whose tables (C x codes-in-use x 4 doubles each) fit one fragment's LDS budget
 int jit_tip_cap(plk_handle h) {
-  const int kb = tune_int("JIT_TAB_KB", 48, 4, 120);
+  constexpr int kb = 48;
   return std::max(2, (kb * 1024) / (h->C * std::max(h->n_codes, 1) * 4 * (int)sizeof(double)));
 }
 
-// treeM programs replace unstored cherries by T_CHERRY rows (PLK_TREEM_CHERRY=0: off);
-// combined codes are 16-bit
-bool treeM_cherries(plk_handle h) {
-  return fused_kind(h) == FK_TREEM && h->n_codes * h->n_codes <= 65535 && !tune_is("TREEM_CHERRY", '0');
-}
+// treeM programs replace unstored cherries by T_CHERRY rows; combined codes are 16-bit
+bool treeM_cherries(plk_handle h) { return fused_kind(h) == FK_TREEM && h->n_codes * h->n_codes <= 65535; }
 
 // Cherry contribution tables of the current treeM program (plk_treeM.hpp), rebuilt on
 // every traversal (P(t) and the tip tables may have changed); combined codes only when
@@ -1440,8 +1424,8 @@ int build_cherry_tables(plk_handle h) {
     HIPCHK(h, hipStreamSynchronize(h->stream));  // `tips` goes out of scope
     h->cherry_codes_valid = true;
   }
-  // rows per workgroup: 64-row passes sharing one P^T staging (PLK_CHERRY_ROWS, default 256)
-  const int rows = 64 * std::max(1, tune_int("CHERRY_ROWS", 256, 64, 4096) / 64);
+  // rows per workgroup: 64-row passes sharing one P^T staging
+  constexpr int rows = 256;
   const dim3 grid((unsigned)((U * U + rows - 1) / rows), (unsigned)(nch * C));
   const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   if (S == 20) {
@@ -1464,15 +1448,14 @@ int build_cherry_tables(plk_handle h) {
 int tree_levels(plk_handle h) {
   switch (fused_kind(h)) {
     case FK_TREE4:
-      if (!jit_tree4(h)) return kTree4Levels(tree4_cw(h));
+      if (!jit_tree4(h)) return kTree4Levels;
       // classes in the wave: cfg5 DM 5 / 6 / 7 = 0.70 / 0.55 / 0.84 ms at G = 4
-      return jit_ciw(h) ? tune_int("JIT_CIW_DM", 6, 2, 16) : tune_int("JIT_DM", 10, 2, 32);
-    // S = 20: 3 levels (with cherry tables 7.8 ms on cfg3, 2 levels 8.7 ms although DM = 3
-    // spills a few registers at 128 VGPRs)
+      return jit_ciw(h) ? tune_int("JIT_DM", 6, 2, 16) : tune_int("JIT_DM", 10, 2, 32);
+    // jit_treeM (20 states): 4 levels (DM 3 / 4 = 3.69 / 3.43 ms on cfg3); the treeM
+    // interpreter: 3 (with cherry tables 7.8 ms on cfg3, 2 levels 8.7 ms)
     case FK_TREEM:
-      if (jit_treeM(h))
-        return h->S == 4 ? tune_int("JITM_DM", 8, 2, 16) : tune_int("JITM_DM", h->S == 64 ? 3 : 4, 2, 6);
-      return h->S == 20 ? tune_int("TREEM_DM", 3, 2, 5) : tune_int("TREEM_DM", 3, 2, 3);
+      if (jit_treeM(h)) return tune_int("JITM_DM", 4, 2, 6);
+      return 3;
     default: return 1;
   }
 }
@@ -1517,8 +1500,8 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   // The tree-specialised kernel also bounds the code of a fragment: a workgroup runs
   // one fragment's straight-line code, which must stay within the instruction cache,
   // so a fragment keeps at most EMAX child edges (cutting the largest kept children).
-  const int EMAX = jit_tree4(h) ? tune_int("JIT_EDGES", 160, 8, 1 << 20) : (1 << 30);
-  // ... and its tips' tables must fit the LDS budget (PLK_JIT_TAB_KB, default 48 KiB)
+  const int EMAX = jit_tree4(h) ? 160 : (1 << 30);
+  // ... and its tips' tables must fit the LDS budget (48 KiB)
   const int TMAX = jit_tree4(h) ? jit_tip_cap(h) : (1 << 30);
   // treeM: an unstored cherry (two tip children) is a leaf operand (T_CHERRY)
   std::vector<char> is_cherry(h->n_nodes, 0);
@@ -1700,90 +1683,44 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   return PLK_OK;
 }
 
-template <int CW>
-void launch_tree4_cw(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
-  constexpr int DM = kTree4Levels(CW);
-  const dim3 block(64 * (h->C / CW));
+// the interpreter: one wave per rate class
+void launch_tree4(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
+  const dim3 block(64 * h->C);
   if (h->flags & PLK_FLAG_SCALING)
-    tree4_kernel<CW, DM, true><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
+    tree4_kernel<1, kTree4Levels, true><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
   else
-    tree4_kernel<CW, DM, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
+    tree4_kernel<1, kTree4Levels, false><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, a.pmats);
 }
 
-// treeM tables: staged in LDS behind one barrier per event, or read by every wave straight
-// from L1/L2 (no staging, no barrier).  Measured (profiles/r01/tm1_*): S = 20 (16 waves per
-// workgroup) 7.70 -> 7.48 ms direct; S = 64 (4 waves, 64x64 tables) 0.95 -> 1.35 ms, so
-// direct is the default for 20 states only.  PLK_TREEM_DIRECT=0/1 overrides.
-bool treeM_direct(plk_handle h) {
-  if (tune_is("TREEM_DIRECT", '0')) return false;
-  if (tune_is("TREEM_DIRECT", '1')) return true;
-  return h->S == 20;
-}
+// treeM tables: read by every wave straight from L1/L2 (no staging, no barrier) for 20
+// states, staged in LDS behind one barrier per event for 64.  Measured (profiles/r01/tm1_*):
+// S = 20 (16 waves per workgroup) 7.70 -> 7.48 ms direct; S = 64 (4 waves, 64x64 tables)
+// 0.95 -> 1.35 ms direct.
+bool treeM_direct(plk_handle h) { return h->S == 20; }
 
 // 16-pattern groups per treeM workgroup.  20 states with direct tables: 1 (16 patterns x C
 // classes, four workgroups per CU, so one workgroup's rescale barriers overlap the others'
-// MFMA chains): cfg3 G = 4 / 2 / 1 = 7.40 / 6.87 / 6.43 ms (profiles/r01/g1_*).
-// PLK_TREEM_G overrides; staged tables and 64 states keep 4.
-int treeM_groups(plk_handle h) {
-  if (h->S != 20 || !treeM_direct(h)) return 4;  // staged tables need 64-pattern workgroups
-  const int g = tune_int("TREEM_G", 1, 1, 4);
-  return g == 3 ? 4 : g;
-}
+// MFMA chains): cfg3 G = 4 / 2 / 1 = 7.40 / 6.87 / 6.43 ms (profiles/r01/g1_*); staged
+// tables (64 states) need 64-pattern workgroups.
+int treeM_groups(plk_handle h) { return h->S == 20 ? 1 : 4; }
 
-template <int S, int DM, int G>
-void launch_treeM_g(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
-  const dim3 block(64 * G * h->C);
-  const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
-  if (treeM_direct(h)) {
-    if (sc)
-      treeM_kernel<S, DM, true, true, G><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
-    else
-      treeM_kernel<S, DM, false, true, G><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
-  } else {
-    if (sc)
-      treeM_kernel<S, DM, true, false, G><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
-    else
-      treeM_kernel<S, DM, false, false, G><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
-  }
-}
-
-template <int S, int DM>
-void launch_treeM_dm(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
-  if constexpr (S == 20) {
-    const int g = treeM_groups(h);
-    if (g == 2 || g == 1) {
-      grid.x = (unsigned)(h->n_pad / (16 * g));
-      if (g == 2)
-        launch_treeM_g<S, DM, 2>(h, a, grid, lds);
-      else
-        launch_treeM_g<S, DM, 1>(h, a, grid, lds);
-      return;
-    }
-  }
-  if constexpr (S == 64) {
-    if (treeM_groups(h) == 8) {
-      grid.x = (unsigned)(h->n_pad / (16 * 8));
-      launch_treeM_g<S, DM, 8>(h, a, grid, lds);
-      return;
-    }
-  }
-  launch_treeM_g<S, DM, 4>(h, a, grid, lds);
-}
-
+// 20 states: 3 register levels, one 16-pattern group, direct tables; 64 states: 3 levels,
+// four groups, staged tables
 void launch_treeM(plk_handle h, const TreeArgs& a, dim3 grid, size_t lds) {
+  const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   if (h->S == 20) {
-    switch (h->prog_dm) {
-      case 2: launch_treeM_dm<20, 2>(h, a, grid, lds); break;
-      case 3: launch_treeM_dm<20, 3>(h, a, grid, lds); break;
-      case 5: launch_treeM_dm<20, 5>(h, a, grid, lds); break;
-      case 4: launch_treeM_dm<20, 4>(h, a, grid, lds); break;
-      default: launch_treeM_dm<20, 3>(h, a, grid, lds); break;
-    }
+    grid.x = (unsigned)(h->n_pad / 16);
+    const dim3 block(64 * h->C);
+    if (sc)
+      treeM_kernel<20, 3, true, true, 1><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+    else
+      treeM_kernel<20, 3, false, true, 1><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
   } else {
-    switch (h->prog_dm) {
-      case 3: launch_treeM_dm<64, 3>(h, a, grid, lds); break;
-      default: launch_treeM_dm<64, 2>(h, a, grid, lds); break;
-    }
+    const dim3 block(64 * 4 * h->C);
+    if (sc)
+      treeM_kernel<64, 3, true, false, 4><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
+    else
+      treeM_kernel<64, 3, false, false, 4><<<grid, block, lds, h->stream>>>(a, a.prog, a.frag_start, h->pmatsT);
   }
 }
 
@@ -1851,14 +1788,14 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
                      (a.stage_codes ? (size_t)h->n_tips * 64 : 0);
   a.n_frags = h->prog_nf;
   a.bmask = -1;
-  a.cherry_pairs = tune_is("TREEM_PAIRS", '0') ? 0 : 1;
+  a.cherry_pairs = 1;
   a.n_cherry_staged = 0;
   size_t lds_m = 0;
   if (kind == FK_TREEM) {
     a.buf_doubles = std::max(h->C * h->S * h->S, h->C * h->n_codes * h->S);
     a.buf_doubles = (a.buf_doubles + 1) & ~1;
     const int threads = 64 * treeM_groups(h) * (h->S == 64 ? 1 : h->C);
-    const int pf = h->S == 64 ? (treeM_groups(h) == 8 ? treeM_pf<64, 8>() : treeM_pf<64>()) : treeM_pf<20>();
+    const int pf = h->S == 64 ? treeM_pf<64>() : treeM_pf<20>();
     if (!h->prog_jitm && !treeM_direct(h) && a.buf_doubles > pf * threads)
       return fail(h, PLK_ERR_UNSUPPORTED, "fused MFMA tables (%d doubles) exceed the staging registers",
                   a.buf_doubles);
@@ -1868,13 +1805,10 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     a.stage_codes = (lds_m + (size_t)h->n_tips * 64 <= 76 * 1024) ? 1 : 0;  // two workgroups per CU
     // a program whose tips all sit in cherry tables (balanced trees) has no T_TIP event:
     // staging every tip's codes would only cost each workgroup a load of n_tips x 64 B
-    if (!tune_is("TREEM_STAGE_CODES", '1') &&
-        std::none_of(h->prog_host.begin(), h->prog_host.end(), [](const TInstr& w) { return w.op == T_TIP; }))
+    if (std::none_of(h->prog_host.begin(), h->prog_host.end(), [](const TInstr& w) { return w.op == T_TIP; }))
       a.stage_codes = 0;
-    if (treeM_groups(h) == 8) a.stage_codes = 0;  // the staged code rows cover 64 patterns
     if (a.stage_codes) lds_m += (size_t)h->n_tips * 64;
   }
-  const int cw = tree4_cw(h);
   // 4 states, one class per wave: the tree-specialised kernel (PLK_JIT=0 keeps the
   // interpreter, e.g. for A/B measurements)
   const bool jit = h->prog_jit;
@@ -1883,7 +1817,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   if (jit) {
     sh.C = h->C;
     sh.CW = h->prog_ciw ? h->C : 1;
-    sh.pin = tune_int("JIT_PIN", 1, 0, 1) != 0;  // cfg2 0.244 -> 0.241, cfg5 1.04 -> 0.93 ms
+    sh.pin = true;  // accumulator pinning: cfg2 0.244 -> 0.241, cfg5 1.04 -> 0.93 ms
     sh.U = h->n_codes;
     sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     // cherries read one product table (plk_jit.hpp: JitUnit) while a fragment's tables stay
@@ -1934,11 +1868,11 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // class in the wave a ring slot is C x larger, so there two events ahead (cfg5 0.385 ms
     // at L = 2, 0.391 at L = 1; 1.48 vs 1.04 ms at L = 3 vs 1 before the P(t) stream)
     sh.L = tune_int("JIT_L", h->prog_ciw ? 2 : 3, 1, 8);
-    sh.minw = tune_int("JIT_MINW", 0, 0, 8);
+    sh.minw = 0;
     // speculative no-rescale pass (plk_jit.hpp): a win only where rescaling never
     // fires; on cfg5 it fires in almost every super-block (1.27 vs 1.14 ms), so opt-in
-    // classes in the wave: next class's P(t) loads overlap this class's FMAs (PLK_JIT_PPIPE=0: off)
-    sh.ppipe = !tune_is("JIT_PPIPE", '0');
+    // classes in the wave: next class's P(t) loads overlap this class's FMAs
+    sh.ppipe = true;
     // PLK_JIT_BLOCKS=1: the root fragment forms the block sums (no wave_sums_to_blocks
     // launch).  Measured slower (cfg2 traversal 0.125 -> 0.160 ms): the wave that stores a
     // wave sum must wait for the store and the counter's atomic round trip (~3 us) before
@@ -1980,15 +1914,14 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     msh.U = h->n_codes;
     msh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
     msh.L = tune_int("JITM_L", 1, 1, 4);
-    msh.minw = tune_int("JITM_MINW", 2, 1, 8);
-    msh.pd = tune_int("JITM_PD", 1, 1, 3);
-    // contraction issue order (plk_jitm.hpp CONTRIB; all orders give the same sums) and the
-    // two-stage operand fetch's code lookahead (0: code and row loaded together)
-    msh.pipe = tune_int("JITM_PIPE", 2, 0, 2);
-    msh.lc = tune_int("JITM_LC", 3, 0, 6);
-    // 16-pattern waves per workgroup: 4 (64 patterns) or 8 (128; every P(t) staging and its
-    // barrier serve twice the patterns)
-    msh.G = tune_int("JITM_G", 4, 4, 8) >= 8 ? 8 : 4;
+    msh.minw = 2;
+    msh.pd = 1;
+    // contraction issue order: Y-outer with the A operands read ahead and pinned schedule
+    // groups (plk_jitm.hpp CONTRIB; 3.77 -> 3.26 ms on cfg3); the two-stage operand fetch
+    // loads the code 3 events ahead of its row
+    msh.pipe = 2;
+    msh.lc = 3;
+    msh.G = 4;  // 16-pattern waves per workgroup (64 patterns)
     if (msh.lds_bytes() > 160 * 1024)
       return fail(h, PLK_ERR_UNSUPPORTED, "jit_treeM needs %zu B of LDS", msh.lds_bytes());
     if (!h->jitm_fn || !(msh == h->jitm_shape)) {
@@ -2032,8 +1965,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       void* args[] = {&ja, &pm, &base};
       // persistent grid: as many workgroups as are resident at once (occupancy query), so
       // every workgroup stages its tables once and there is no second dispatch round
-      int wgs = tune_int("JIT_WGS", 0, 0, 1 << 20);
-      if (wgs == 0) {
+      int wgs = 0;
+      {
         if (h->jit_resident <= 0) {
           int per_cu = 0, n_cu = 0;
           HIPCHK(h, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, h->jit_fn, 64 * (h->C / sh.CW) * sh.G,
@@ -2044,8 +1977,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         // every fragment of the tier at once: the resident workgroups split over the
         // fragments (each stages its fragment's tables once and walks many super-blocks)
         // instead of the tier's fragments running one after another with every workgroup
-        // staging tables for a few super-blocks (PLK_JIT_SPLIT_Y=0: the latter)
-        wgs = tune_is("JIT_SPLIT_Y", '0') ? h->jit_resident : std::max(1, h->jit_resident / (int)grid.y);
+        // staging tables for a few super-blocks (cfg5 0.49 -> 0.42 ms)
+        wgs = std::max(1, h->jit_resident / (int)grid.y);
       }
       const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, wgs);
       h->jit_last_gx = (int)gx;
@@ -2067,11 +2000,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
                                                                                  a.wave_sums, a.n_patterns, a.n_pad);
       }
     } else {
-      switch (cw) {
-        case 1: launch_tree4_cw<1>(h, a, grid, lds); break;
-        case 2: launch_tree4_cw<2>(h, a, grid, lds); break;
-        case 4: launch_tree4_cw<4>(h, a, grid, lds); break;
-      }
+      launch_tree4(h, a, grid, lds);
     }
     HIPCHK(h, hipGetLastError());
     if (h->timing & PLK_TIME_PARTIALS) {
@@ -3030,22 +2959,10 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
       }
       if (ops.size() > first) levels.push_back(Level{first, (int)(ops.size() - first), ns});
     }
-  const bool mfma = h->S == 20 || h->S == 64;
+  const bool mfma = h->S == 20;
   const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   const int n_blk = (int)(h->n_pad / (mfma ? 64 : kDrThreads));
   int rc;
-  if (h->S == 64) {
-    // the sons' dP^T and d2P^T (P^T: ensure_pmatsT) for the 16x16x4 matrix-core reduction
-    const size_t bytes = (size_t)nn * C * h->S * h->S * sizeof(double);
-    if (!h->dpmatsT && (rc = dalloc(h, (void**)&h->dpmatsT, bytes))) return rc;
-    if (!h->d2pmatsT && (rc = dalloc(h, (void**)&h->d2pmatsT, bytes))) return rc;
-    const dim3 tg((unsigned)nn, (unsigned)C);
-    if (h->S == 64) {  // (20 states read P, dP, d2P as stored)
-      transpose_pmats<64><<<tg, 256, 0, h->stream>>>(h->dpmats, h->dpmatsT, C);
-      transpose_pmats<64><<<tg, 256, 0, h->stream>>>(h->d2pmats, h->d2pmatsT, C);
-    }
-    HIPCHK(h, hipGetLastError());
-  }
   if ((rc = ensure_cap(h, (void**)&h->d_drb, &h->d_drb_cap, br.size() * sizeof(DrBranch)))) return rc;
   if ((rc = ensure_cap(h, (void**)&h->d_drpre, &h->d_drpre_cap, ops.size() * sizeof(DrPreOp)))) return rc;
   if ((rc = ensure_cap(h, (void**)&h->dr_blk, &h->dr_blk_cap, 2 * br.size() * n_blk * sizeof(double)))) return rc;
@@ -3082,33 +2999,18 @@ int dr_fused_preorder(plk_handle h, const std::vector<std::vector<int> >& depth,
   for (const Level& l : levels) {
     const dim3 grid((unsigned)n_blk, (unsigned)l.count);
     const DrPreOp* o = h->d_drpre + l.first;
-    if (mfma) {
-      const double *pT = h->pmatsT, *dT = h->dpmatsT, *d2T = h->d2pmatsT;
-#define PLK_DRM_NS(S_, C_, NS_)                                                                   \
-  (sc ? dr_pre_m_kernel<S_, C_, true, NS_><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T)       \
-      : dr_pre_m_kernel<S_, C_, false, NS_><<<grid, 256, 0, h->stream>>>(o, a, pT, dT, d2T))
-#define PLK_DRM(S_, C_) (l.ns == 2 ? PLK_DRM_NS(S_, C_, 2) : PLK_DRM_NS(S_, C_, 3))
-      if (h->S == 20) {  // 4x4x4 matrix-core tiles, no padding (plk_dr.hpp: dr_pre_m20_kernel)
+    if (mfma) {  // 20 states: 4x4x4 matrix-core tiles, no padding (plk_dr.hpp: dr_pre_m20_kernel)
 #define PLK_DRM20_NS(C_, NS_)                                                                 \
   (sc ? dr_pre_m20_kernel<C_, true, NS_><<<grid, 256, 0, h->stream>>>(o, a)                  \
       : dr_pre_m20_kernel<C_, false, NS_><<<grid, 256, 0, h->stream>>>(o, a))
 #define PLK_DRM20(C_) (l.ns == 2 ? PLK_DRM20_NS(C_, 2) : PLK_DRM20_NS(C_, 3))
-        switch (C) {
-          case 1: PLK_DRM20(1); break;
-          case 2: PLK_DRM20(2); break;
-          case 4: PLK_DRM20(4); break;
-        }
+      switch (C) {
+        case 1: PLK_DRM20(1); break;
+        case 2: PLK_DRM20(2); break;
+        case 4: PLK_DRM20(4); break;
+      }
 #undef PLK_DRM20
 #undef PLK_DRM20_NS
-      } else {
-        switch (C) {
-          case 1: PLK_DRM(64, 1); break;
-          case 2: PLK_DRM(64, 2); break;
-          case 4: PLK_DRM(64, 4); break;
-        }
-      }
-#undef PLK_DRM
-#undef PLK_DRM_NS
     } else if (sc) {
       switch (C) {
         case 1: dr_pre_s4_kernel<1, true><<<grid, kDrThreads, 0, h->stream>>>(o, a, h->partials, h->partials); break;
@@ -3184,13 +3086,11 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
   if ((S == 20 || S == 64) && (rc = ensure_pmatsT(h))) return rc;
   // 4 and 20 states (1, 2 or 4 classes, any rescaling): the fused preorder
   // (dr_pre_s4_kernel / dr_pre_m20_kernel), one launch per level of fathers, branch terms
-  // reduced where U is formed (DR_PRE=0: the levelwise preorder + reduction below).  64
-  // states: levelwise by default -- dr_pre_m_kernel<64> holds 342 registers (one wave per
-  // SIMD) and ran cfg4's pass in 17.7 ms against 12.7 ms levelwise (profiles/r03/r3e);
-  // DR_PRE=1 selects it
-  const char* pre_key = tune_get("DR_PRE");
-  bool pre = (S == 4 || S == 20 || (S == 64 && pre_key && pre_key[0] == '1')) && (C == 1 || C == 2 || C == 4) &&
-             !(pre_key && pre_key[0] == '0');
+  // reduced where U is formed.  Otherwise (64 states, other class counts, fathers of more
+  // than three sons) the levelwise preorder + reduction below: a fused 64-state preorder on
+  // 16x16x4 tiles held 342 registers (one wave per SIMD) and ran cfg4's pass in 17.7 ms
+  // against 12.7 ms levelwise (profiles/r03/r3e), so it was removed
+  bool pre = (S == 4 || S == 20) && (C == 1 || C == 2 || C == 4);
   for (size_t d = 0; pre && d < depth.size(); ++d)
     for (int f : depth[d])
       if (f >= nt && (h->topo_kids[f].size() < 2 || h->topo_kids[f].size() > 3)) pre = false;
@@ -3208,12 +3108,12 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
         h->pmats, h->pmats, (S == 20 || S == 64) ? h->pmatsT : nullptr, h->pi, h->d_drm, mat_base, C, S);
     HIPCHK(h, hipGetLastError());
   }
-  // S = 20 / 64 reduce on fp64 MFMA (64-pattern blocks) unless PLK_DR_MFMA=0
-  const bool dr_mfma = (S == 20 || S == 64) && !tune_is("DR_MFMA", '0');
+  // S = 20 / 64 reduce on fp64 MFMA (64-pattern blocks)
+  const bool dr_mfma = S == 20 || S == 64;
   // tips whose father has one other son and a father of its own: U_v formed inside the
-  // reduction (S <= 4 kernel), never stored (PLK_DR_FUSE=0 stores every U_v)
+  // reduction (S <= 4 kernel), never stored
   std::vector<char> fused(nn, 0);
-  if (!dr_mfma && S <= 4 && !tune_is("DR_FUSE", '0'))
+  if (!dr_mfma && S <= 4)
     for (int v = 0; v < nt; ++v)
       if (parent[v] >= 0 && parent[v] != root && h->topo_kids[parent[v]].size() == 2) fused[v] = 1;
   // U_v for every non-root node, one launch per (depth, child chunk)
@@ -3321,8 +3221,8 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
     DrArgs am = a;
     am.G = 3 * (size_t)C * S * S * sizeof(double) <= 64 * 1024 ? C : 1;
     const size_t lds_m = 3 * (size_t)am.G * S * S * sizeof(double);
-    // a few workgroups per branch, each looping over pattern blocks (PLK_DR_WGS total)
-    const int want = tune_int("DR_WGS", 4096, 1, 1 << 20);
+    // a few workgroups per branch, each looping over pattern blocks (4096 in total)
+    constexpr int want = 4096;
     grid.x = (unsigned)std::min<int64_t>(n_blk, std::max<int64_t>(1, (want + (int)br.size() - 1) / (int)br.size()));
     if (S == 20)
       dr_branch_mfma_kernel<20><<<grid, kDrmThreads, lds_m, h->stream>>>(h->d_drb, am);
@@ -3333,8 +3233,6 @@ int dr_derivatives(plk_handle h, double* d1, double* d2) {
       case 2: dr_branch_kernel<2><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
       case 3: dr_branch_kernel<3><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
       case 4: dr_branch_kernel<4><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
-      case 20: dr_branch_kernel<20><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
-      case 64: dr_branch_kernel<64><<<grid, kDrThreads, lds, h->stream>>>(h->d_drb, a); break;
     }
   }
   HIPCHK(h, hipGetLastError());
@@ -3611,7 +3509,7 @@ int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   if (h && !h->shards.empty()) return multi_branch_derivatives(h, branch, d1, d2);
   if (!h || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
   if (h->trav_ops.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet (plk_update_partials)");
-  if (h->S != 4 || !(h->C == 1 || h->C == 2 || h->C == 4) || tune_is("DERIV_PATH", '1'))
+  if (h->S != 4 || !(h->C == 1 || h->C == 2 || h->C == 4))
     return path_derivatives(h, branch, d1, d2);
   if (h->deriv_valid.empty() || !h->deriv_valid[branch])
     return fail(h, PLK_ERR_STATE, "dP/d2P of branch %d not computed (PLK_DERIV_DP | PLK_DERIV_D2P)", branch);

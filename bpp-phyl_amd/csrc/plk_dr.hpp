@@ -561,193 +561,19 @@ __global__ __launch_bounds__(kDrThreads) void dr_pre_s4_kernel(const DrPreOp* __
 }
 
 // ---------------------------------------------------------------------------
-// Fused preorder for 20 and 64 states (any rescaling): the same per-father op as
-// dr_pre_s4_kernel on fp64 matrix cores, in treeM's v_mfma_f64_16x16x4 layout (a wave owns
-// 16 patterns; lane l holds states 16 xt + (l >> 4) + 4 r of pattern l & 15).  Per class
-//     MU = pi (f the root) or P_f^T U_f,   Q_j = P_j L_j,
-//     U_i = MU (*) prod_{j != i} Q_j   (stored for internal sons),
-//     l += p_c U_i . Q_i,  l' += p_c U_i . (dP_i L_i),  l'' += p_c U_i . (d2P_i L_i),
-// every product a matvec_m whose A operands (the applied matrix, transposed: P_f itself
-// for P_f^T, and P^T, dP^T, d2P^T of the sons) are read from L1/L2 -- the workgroup's four
-// waves share them.  Stored U is rescaled jointly over states and classes after the class
-// loop (in place, as dr_pre_s4_kernel<C, true>).  64-pattern blocks.
-// ---------------------------------------------------------------------------
-template <int S, int C, bool SCALE, int NS>
-__global__ __launch_bounds__(256) void dr_pre_m_kernel(const DrPreOp* __restrict__ ops, DrArgs a,
-                                                       const double* __restrict__ pT,
-                                                       const double* __restrict__ dpT,
-                                                       const double* __restrict__ d2pT) {
-  constexpr int XT = MShape<S>::XT, CS = C * S;
-  __shared__ double red[2][3][4];
-  const DrPreOp op = ops[blockIdx.y];
-  // sons of the op: NS = 2 launches carry fathers of <= 2 sons, so the third son's
-  // registers and code vanish (64 states: 481 -> fewer registers, two waves per SIMD)
-  const int nsn = NS == 2 ? min(2, op.n) : op.n;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int lr = lane >> 4, lc = lane & 15;
-  const int64_t p = (int64_t)blockIdx.x * 64 + 16 * w + lc;
-  const bool live = p < a.n_patterns;
-  const int64_t tile = p >> 7, q = p & (kTile - 1);
-  const int64_t tb = tile * CS * kTile + q;
-  const bool root = op.uf_slot < 0;
-  const size_t SS = (size_t)S * S;
-  double l0[3] = {0.0, 0.0, 0.0}, l1[3] = {0.0, 0.0, 0.0}, l2[3] = {0.0, 0.0, 0.0};
-  double umax[3] = {0.0, 0.0, 0.0};
-  // the son's L of class c in the MFMA layout (padding rows 0)
-  auto loadL = [&](int j, int c, MAcc<S>& v) {
-    if (op.is_tip[j]) {
-      const double* row = a.code_table + (int64_t)a.codes[(int64_t)op.idx[j] * a.n_pad + p] * S;
-#pragma unroll
-      for (int xt = 0; xt < XT; ++xt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[xt][r] = m_valid<S>(xt, r, lr) ? row[16 * xt + lr + 4 * r] : 0.0;
-    } else {
-      const double* L = a.partials + (int64_t)op.idx[j] * a.slot_stride + tb + (int64_t)c * S * kTile;
-#pragma unroll
-      for (int xt = 0; xt < XT; ++xt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          v[xt][r] = m_valid<S>(xt, r, lr) ? L[(int64_t)(16 * xt + lr + 4 * r) * kTile] : 0.0;
-    }
-  };
-  auto dot = [&](const MAcc<S>& u, const f64x4m (&t)[XT]) {
-    double s = 0.0;
-#pragma unroll
-    for (int xt = 0; xt < XT; ++xt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s = fma(u[xt][r], t[xt][r], s);
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    return s;
-  };
-#pragma unroll 1
-  for (int c = 0; c < C; ++c) {
-    MAcc<S> mu;
-    if (root) {
-#pragma unroll
-      for (int xt = 0; xt < XT; ++xt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mu[xt][r] = m_valid<S>(xt, r, lr) ? a.pi[16 * xt + lr + 4 * r] : 0.0;
-    } else {
-      MAcc<S> uf;
-      const double* U = a.partials + (int64_t)op.uf_slot * a.slot_stride + tb + (int64_t)c * S * kTile;
-#pragma unroll
-      for (int xt = 0; xt < XT; ++xt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          uf[xt][r] = m_valid<S>(xt, r, lr) ? U[(int64_t)(16 * xt + lr + 4 * r) * kTile] : 0.0;
-      f64x4m d[XT];
-      matvec_m<S>(d, uf, a.pmats + ((size_t)op.f * C + c) * SS, lr, lc);  // (P_f^T)^T = P_f
-#pragma unroll
-      for (int xt = 0; xt < XT; ++xt) mu[xt] = d[xt];
-    }
-    MAcc<S> Q[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      if (j >= nsn) continue;
-      MAcc<S> L;
-      loadL(j, c, L);
-      f64x4m d[XT];
-      matvec_m<S>(d, L, pT + ((size_t)op.son[j] * C + c) * SS, lr, lc);
-#pragma unroll
-      for (int xt = 0; xt < XT; ++xt) Q[j][xt] = d[xt];
-    }
-    const double pc = a.probs[c];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      if (i >= nsn) continue;
-      MAcc<S> u;
-#pragma unroll
-      for (int xt = 0; xt < XT; ++xt) {
-        u[xt] = mu[xt];
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-          if (j != i && j < nsn) u[xt] *= Q[j][xt];
-      }
-      if (op.uslot[i] >= 0) {
-        double* dst = a.uout + (int64_t)op.uslot[i] * a.slot_stride + tb + (int64_t)c * S * kTile;
-#pragma unroll
-        for (int xt = 0; xt < XT; ++xt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (m_valid<S>(xt, r, lr)) {
-              dst[(int64_t)(16 * xt + lr + 4 * r) * kTile] = u[xt][r];
-              if (SCALE) umax[i] = fmax(umax[i], u[xt][r]);
-            }
-      }
-      const double s0 = dot(u, Q[i]);
-      MAcc<S> L;
-      loadL(i, c, L);
-      f64x4m t[XT];
-      matvec_m<S>(t, L, dpT + ((size_t)op.son[i] * C + c) * SS, lr, lc);
-      const double s1 = dot(u, t);
-      matvec_m<S>(t, L, d2pT + ((size_t)op.son[i] * C + c) * SS, lr, lc);
-      const double s2 = dot(u, t);
-      l0[i] = fma(pc, s0, l0[i]);
-      l1[i] = fma(pc, s1, l1[i]);
-      l2[i] = fma(pc, s2, l2[i]);
-    }
-  }
-  if (SCALE)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      if (i >= nsn || op.uslot[i] < 0) continue;
-      double m = umax[i];
-      m = fmax(m, __shfl_xor(m, 16, 64));
-      m = fmax(m, __shfl_xor(m, 32, 64));
-      if (m > 0.0 && m < kScaleThr) {
-        double* dst = a.uout + (int64_t)op.uslot[i] * a.slot_stride + tb;
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-          for (int xt = 0; xt < XT; ++xt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (m_valid<S>(xt, r, lr)) dst[(int64_t)(c * S + 16 * xt + lr + 4 * r) * kTile] *= kScaleUp;
-      }
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    if (i >= nsn) continue;
-    double r1 = 0.0, r2 = 0.0;
-    if (live && lr == 0) {
-      const double g = l1[i] / l0[i], hh = l2[i] / l0[i];
-      r1 = a.weights[p] * g;
-      r2 = a.weights[p] * (hh - g * g);
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      r1 += __shfl_xor(r1, off, 64);
-      r2 += __shfl_xor(r2, off, 64);
-    }
-    if (lane == 0) {
-      red[0][i][w] = r1;
-      red[1][i][w] = r2;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < 3 && (int)threadIdx.x < nsn) {
-    const int i = threadIdx.x;
-    double t1 = 0.0, t2 = 0.0;
-    for (int k = 0; k < 4; ++k) {  // fixed order
-      t1 += red[0][i][k];
-      t2 += red[1][i][k];
-    }
-    const int bi = i == 0 ? op.bidx[0] : i == 1 ? op.bidx[1] : op.bidx[2];  // (no runtime index into op)
-    a.blk1[(size_t)bi * a.n_blk + blockIdx.x] = t1;
-    a.blk2[(size_t)bi * a.n_blk + blockIdx.x] = t2;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Fused preorder for 20 states on v_mfma_f64_4x4x4_4b (plk_jitm.hpp's layout): 20 states
-// tile as 5 x 4 with no padding, where dr_pre_m_kernel's 16x16x4 tiles pad 20 to 32 in both
+// tile as 5 x 4 with no padding, where 16x16x4 tiles would pad 20 to 32 in both
 // dimensions (39 % useful flops).  Lane l = 16 hi + 4 b + lo of wave w holds states
 // 4X + hi (X = 0..4) of pattern 16 w + 4 b + lo; a matvec D = M v is, per X, five MFMAs
 // over Y with A(X, Y)[lo][hi] = M[4X + lo][4Y + hi] read from LDS, and v's register Y as
 // the B operand (D comes out in the same layout, so products chain in registers).  Per
 // class the workgroup stages the matrices of the op -- P_f (read transposed for
 // M_f = P_f^T) and each son's P, dP, d2P, as stored -- in LDS; the products, rescaling
-// and per-block branch terms are dr_pre_m_kernel's (same 64-pattern blocks).
+// and per-block branch terms as dr_pre_s4_kernel's, on 64-pattern blocks: per class
+//     MU = pi (f the root) or P_f^T U_f,   Q_j = P_j L_j,
+//     U_i = MU (*) prod_{j != i} Q_j   (stored for internal sons),
+//     l += p_c U_i . Q_i,  l' += p_c U_i . (dP_i L_i),  l'' += p_c U_i . (d2P_i L_i),
+// stored U rescaled jointly over states and classes after the class loop.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double dr_mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
@@ -759,7 +585,7 @@ __global__ __launch_bounds__(256) void dr_pre_m20_kernel(const DrPreOp* __restri
   __shared__ __attribute__((aligned(16))) double mats[10 * SS];  // [P_f | P_j, dP_j, d2P_j for j < 3] of one class
   __shared__ double red[2][3][4];
   const DrPreOp op = ops[blockIdx.y];
-  const int nsn = NS == 2 ? min(2, op.n) : op.n;  // (as dr_pre_m_kernel)
+  const int nsn = NS == 2 ? min(2, op.n) : op.n;  // (the two-son build)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int hi = lane >> 4, lo = lane & 3;
   const int64_t p = (int64_t)blockIdx.x * 64 + 16 * w + (lane & 15);

@@ -271,9 +271,9 @@ __global__ __launch_bounds__(256) void partials_links_s4_kernel(const KOpL* __re
 
 // Any state count: partials_generic_kernel's arithmetic (P and tip tables staged in LDS,
 // XB states per chunk, the same product and FMA order) with the children read through
-// their pattern links -- so values are bitwise those of the uncompressed generic kernel
-// (PLK_FLAG_LEVELWISE with PLK_GENERIC20 / PLK_GENERIC64).  One lane = one distinct
-// pattern j of the parent (its slot entry j).
+// their pattern links (the levelwise 20 / 64-state traversal runs K2 / K3, which sum in
+// another order: 1e-12 apart).  One lane = one distinct pattern j of the parent (its slot
+// entry j).
 template <int S, int XB, bool SCALE>
 __global__ __launch_bounds__(256) void partials_links_generic_kernel(const KOpL* __restrict__ ops, PartialsArgs a,
                                                                      const uint32_t* __restrict__ links, int C) {
@@ -696,93 +696,10 @@ __global__ __launch_bounds__(64) void pmat4_kernel(PmatArgs a, const PmatInline 
 
 // K4 for 64 states (codon models), P only: the same sums as pmat_kernel in the same order
 // (k ascending, w = V[x][k] Vinv[k][y], fma(w, e_k, p)), so bitwise its results, but with
-// V, Vinv and e staged in LDS and a 4 x 4 register block of outputs per thread (16
-// independent FMA chains over 8 LDS reads per k instead of one chain over two reads, one
-// of them from L2).  256 threads = the 64 x 64 outputs.
-__global__ __launch_bounds__(256) void pmat64_kernel(PmatArgs a, const PmatInline inl) {
-  constexpr int S = 64;
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int i = blockIdx.x, c = blockIdx.y;
-  const int b = inl.n ? inl.branch[i] : a.branch[i];
-  const int m = inl.n ? inl.model[i] : (a.model ? a.model[i] : 0);
-  const double tt = (inl.n ? inl.t[i] : a.t[i]) * a.rates[c];
-  double* e = sm;
-  double* Vm = sm + S;
-  double* Vi = Vm + S * S;
-  const double* V = a.V + (size_t)m * S * S;
-  const double* VI = a.Vinv + (size_t)m * S * S;
-  const double* lam = a.lambda + (size_t)m * S;
-  for (int k = threadIdx.x; k < S; k += blockDim.x) e[k] = exp(lam[k] * tt);
-  stage_lds<S * S / 256>(Vm, V, S * S);
-  stage_lds<S * S / 256>(Vi, VI, S * S);
-  __syncthreads();
-  const int xb = 4 * (threadIdx.x >> 4), yb = threadIdx.x & 15;
-  double p[4][4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) p[u][v] = 0.0;
-  for (int k = 0; k < S; ++k) {
-    const double ek = e[k];
-    double vx[4], vy[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) vx[u] = Vm[(xb + u) * S + k];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) vy[v] = Vi[k * S + yb + 16 * v];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) p[u][v] = __builtin_fma(vx[u] * vy[v], ek, p[u][v]);
-  }
-  double* out = a.P + ((size_t)b * a.C + c) * S * S;
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int x = xb + u, y = yb + 16 * v;
-      p[u][v] = tt == 0.0 ? (x == y ? 1.0 : 0.0) : p[u][v];  // getPij_t: t == 0 -> identity
-      out[x * S + y] = p[u][v];
-    }
-  // tip branch: its tip table (tip_table64_kernel's arithmetic) from the P just formed
-  if (a.init && b < a.n_tips) {
-    __syncthreads();  // done with Vm / Vi
-    double* Pl = Vm;  // [x][y]
-    double* In = Vi;  // [code][y], n_codes <= 64 (launch guarantees)
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) Pl[(xb + u) * S + yb + 16 * v] = p[u][v];
-    stage_lds<S * S / 256>(In, a.init, a.n_codes * S);
-    __syncthreads();
-    double* tout = a.tipP + ((size_t)b * a.C + c) * a.n_codes * S;
-    const int xq = 4 * (threadIdx.x & 15), cb = 4 * (threadIdx.x >> 4);
-    double t[4][4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) t[u][v] = 0.0;
-    for (int y = 0; y < S; ++y) {
-      double px[4], iv[4];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) px[v] = Pl[(xq + v) * S + y];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) iv[u] = cb + u < a.n_codes ? In[(cb + u) * S + y] : 0.0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) t[u][v] = __builtin_fma(px[v], iv[u], t[u][v]);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (cb + u < a.n_codes)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) tout[(cb + u) * S + xq + v] = t[u][v];
-  }
-}
-
-// pmat64_kernel split over four 16-row slabs of P (blockIdx.z): 4x the workgroups, so a
-// tree's few hundred branches fill the device several deep instead of one workgroup per CU.
-// Every element is the same sum in the same order as in pmat64_kernel (bitwise).
+// V, Vinv and e staged in LDS and a register block of outputs per thread (independent FMA
+// chains over LDS reads instead of one chain over two reads, one of them from L2), split
+// over four 16-row slabs of P (blockIdx.z): 4x the workgroups, so a tree's few hundred
+// branches fill the device several deep instead of one workgroup per CU.
 __global__ __launch_bounds__(256) void pmat64s_kernel(PmatArgs a, const PmatInline inl) {
   constexpr int S = 64, R = 16;
   extern __shared__ __attribute__((aligned(16))) double sm[];

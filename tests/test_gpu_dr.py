@@ -15,7 +15,7 @@ import pytest
 import phylo
 import plk
 import workload
-from conftest import clear_tune, set_tune
+
 from test_gpu_parity import MODES, _caterpillar, _random_problem, engine_for, oracle_for, run_engine
 
 pytestmark = pytest.mark.gpu
@@ -233,39 +233,30 @@ def test_dr_vs_oracle_restatement(S, C, n_taxa, n_pat):
 
 @pytest.mark.parametrize("C,n_taxa,n_pat,amb", [(4, 64, 5000, True), (1, 9, 700, False), (2, 33, 1300, True),
                                                  (4, 3, 1, False)])
-def test_dr_fused_preorder_equals_levelwise(C, n_taxa, n_pat, amb, monkeypatch):
+def test_dr_fused_preorder_vs_path(C, n_taxa, n_pat, amb):
     """4 states without rescaling: the fused preorder (dr_pre_s4_kernel: father-side vectors
-    in registers, branch terms reduced where they are formed) against the levelwise
-    preorder + reduction pass (PLK_DR_PRE=0) -- relative 1e-12 on d1 and d2 of every
-    branch (pi enters at the root's sons instead of in M_f, so not bitwise) -- and both
-    against the path derivatives."""
+    in registers, branch terms reduced where they are formed) against the path derivatives
+    of every branch."""
     et, m, alph, rates, probs, states = _random_problem(4, C, n_taxa, n_pat, seed=90 + C + n_taxa, amb=amb)
     br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
-    out = {}
-    for pre in ("0", "1"):
-        set_tune(monkeypatch, "DR_PRE", pre)
-        eng = engine_for(et, 4, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m],
-                         flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | DR)
-        eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
-        run_engine(eng, et)
-        out[pre] = _dr_vs_path(eng, et) if pre == "1" else eng.all_branch_derivatives()
-        del eng
-    (a1, a2), (b1, b2) = out["0"], out["1"]
-    for v in br:
-        assert _close(a1[v], b1[v], 1e-12), (v, a1[v], b1[v])
-        assert _close(a2[v], b2[v], 1e-12), (v, a2[v], b2[v])
+    eng = engine_for(et, 4, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m],
+                     flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | DR)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    run_engine(eng, et)
+    _dr_vs_path(eng, et)
 
 
 @pytest.mark.parametrize("S,C,tree_kind,n_pat,scaling", [
     (20, 4, "balanced40", 500, True), (20, 2, "balanced24", 333, False), (20, 1, "caterpillar120long", 300, True),
     (64, 1, "balanced24", 300, False), (64, 2, "balanced16", 130, True), (64, 1, "caterpillar150long", 200, True),
     (4, 4, "caterpillar300long", 600, True), (4, 2, "balanced64", 2000, True)])
-def test_dr_fused_preorder_any_state_count(S, C, tree_kind, n_pat, scaling, monkeypatch):
-    """The fused preorder beyond unscaled DNA: dr_pre_m_kernel (20 / 64 states on fp64
-    matrix cores) and dr_pre_s4_kernel<C, true> (4 states with rescaling; stored upper
-    vectors rescaled jointly over states and classes) against the levelwise preorder +
-    reduction (DR_PRE=0) at 1e-11 and against the path derivatives at 1e-10 (1e-9 through
-    deep rescaling).  "long" caterpillars drive partials and upper vectors below 2^-256."""
+def test_dr_any_state_count_vs_path(S, C, tree_kind, n_pat, scaling):
+    """All-branch derivatives beyond unscaled DNA: the fused preorder for 20 states on fp64
+    matrix cores (dr_pre_m20_kernel) and for 4 states with rescaling (dr_pre_s4_kernel<C,
+    true>; stored upper vectors rescaled jointly over states and classes), the levelwise
+    preorder + MFMA reduction for 64 states, against the path derivatives at 1e-10 (1e-9
+    through deep rescaling).  "long" caterpillars drive partials and upper vectors below
+    2^-256."""
     rng = np.random.default_rng(S * 7 + C + n_pat)
     if tree_kind.startswith("balanced"):
         tree = phylo.balanced_tree(int(tree_kind[8:]), seed=S + C, lo=0.05, hi=0.4)
@@ -283,18 +274,9 @@ def test_dr_fused_preorder_any_state_count(S, C, tree_kind, n_pat, scaling, monk
     states = wl.simulate(0, n_pat).astype(np.int32)
     br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | DR | (plk.PLK_FLAG_SCALING if scaling else 0)
-    out = {}
-    for pre in ("0", "1"):
-        set_tune(monkeypatch, "DR_PRE", pre)
-        eng = engine_for(et, S, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
-        eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
-        _, site, _ = run_engine(eng, et)
-        if tree_kind.endswith("long"):
-            assert site.min() < -256 * np.log(2)
-        out[pre] = _dr_vs_path(eng, et, rel=1e-9 if tree_kind.endswith("long") else 1e-10) if pre == "1" \
-            else eng.all_branch_derivatives()
-        del eng
-    (a1, a2), (b1, b2) = out["0"], out["1"]
-    for v in br:
-        assert _close(a1[v], b1[v], 1e-11), (v, a1[v], b1[v])
-        assert _close(a2[v], b2[v], 1e-11), (v, a2[v], b2[v])
+    eng = engine_for(et, S, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    _, site, _ = run_engine(eng, et)
+    if tree_kind.endswith("long"):
+        assert site.min() < -256 * np.log(2)
+    _dr_vs_path(eng, et, rel=1e-9 if tree_kind.endswith("long") else 1e-10)

@@ -361,67 +361,69 @@ def test_evaluate_equals_three_calls(S, C, flags):
 
 @pytest.mark.parametrize("C,scaling,n_patterns", [(4, False, 9000), (1, False, 4096), (4, True, 5000),
                                                    (2, False, 130)])
-def test_pmat4_and_kernel_block_sums_bitwise(C, scaling, n_patterns, monkeypatch):
-    """The 4-state K4 (pmat4_kernel: a thread per row of P) equals pmat_kernel bitwise -- P,
-    dP, d2P and, through the traversal, the tip tables and the block sums, for one, several
-    and ragged blocks; a second root reduction without a new traversal returns the same
-    block sums."""
+def test_pmat4_and_block_sums(C, scaling, n_patterns):
+    """The 4-state K4 (pmat4_kernel: a thread per row of P): P, r dP, r^2 d2P against
+    V diag(e^{lambda r t}) V^-1 and its derivatives at 1e-13; through the traversal the lnL
+    against the oracle for one, several and ragged blocks; a second root reduction without a
+    new traversal returns the same block sums."""
     et, m, alph, rates, probs, states = _random_problem(4, C, 40, n_patterns, seed=77, amb=True)
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | (plk.PLK_FLAG_SCALING if scaling else 0)
     br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
     ops = phylo.split_ops(et.ops)
-    out = {}
-    for new in ("0", "1"):
-        set_tune(monkeypatch, "PMAT4", new)
-        eng = engine_for(et, 4, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
-        eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
-        mats = [np.stack([eng.get_pmatrix(int(b)) for b in br]),
-                np.stack([eng.get_dpmatrix(int(b), 1) for b in br]),
-                np.stack([eng.get_dpmatrix(int(b), 2) for b in br])]
-        res = []
-        for scale in (1.0, 1.7):
-            lnl, blocks = eng.evaluate(br, et.brlen[br] * scale, ops, et.root)
-            lnl2, _, blocks2 = eng.root_loglik(et.root, want_blocks=True)
-            assert lnl2 == lnl and np.array_equal(blocks2, blocks)
-            res.append((lnl, blocks))
-        assert eng.kernel_path() == "jit_tree4"
-        out[new] = (mats, res)
-        del eng
-    (m0, r0), (m1, r1) = out["0"], out["1"]
-    for a, b in zip(m0, m1):
-        assert np.array_equal(a, b)
-    for (l0, b0), (l1, b1) in zip(r0, r1):
-        assert l0 == l1 and np.array_equal(b0, b1)
+    eng = engine_for(et, 4, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
+    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+    for b in br[:: max(1, len(br) // 7)]:
+        P, dP, d2P = eng.get_pmatrix(int(b)), eng.get_dpmatrix(int(b), 1), eng.get_dpmatrix(int(b), 2)
+        for c in range(C):
+            e = np.exp(m.lam * rates[c] * et.brlen[b])
+            want = (m.V * e) @ m.Vinv
+            wd = (m.V * (e * m.lam * rates[c])) @ m.Vinv
+            wd2 = (m.V * (e * (m.lam * rates[c]) ** 2)) @ m.Vinv
+            assert np.max(np.abs(P[c] - want)) <= 1e-13
+            assert np.max(np.abs(dP[c] - wd)) <= 1e-13 * max(1.0, np.max(np.abs(wd)))
+            assert np.max(np.abs(d2P[c] - wd2)) <= 1e-13 * max(1.0, np.max(np.abs(wd2)))
+    res = []
+    for scale in (1.0, 1.7):
+        lnl, blocks = eng.evaluate(br, et.brlen[br] * scale, ops, et.root)
+        lnl2, _, blocks2 = eng.root_loglik(et.root, want_blocks=True)
+        assert lnl2 == lnl and np.array_equal(blocks2, blocks)
+        assert abs(float(np.add.accumulate(blocks)[-1]) - lnl) <= 1e-12 * abs(lnl)
+        res.append(lnl)
+    assert eng.kernel_path() == "jit_tree4"
+    eng.evaluate(br, et.brlen[br], ops, et.root)
     lo, _ = oracle_for(et, states, alph.init_table, rates, probs, m.pi, [m], scaling=scaling)
-    assert abs(r1[0][0] - lo) <= 1e-10 * abs(lo)
+    assert abs(res[0] - lo) <= 1e-10 * abs(lo)
 
 
 @pytest.mark.parametrize("S,C", [(4, 4), (20, 2)])
-def test_pmat_request_paths_bitwise(S, C, monkeypatch):
-    """A P(t) request in the kernel arguments and through mapped pinned staging (default for
-    more than 160 branches) give the same transition matrices and lnL bitwise (NH: a model
+def test_pmat_request_paths_bitwise(S, C):
+    """A P(t) request of more than 160 branches goes through mapped pinned staging, smaller
+    ones ride in the kernel arguments: the same branches requested at once (staged) and in
+    chunks of 100 (inline) give the same transition matrices and lnL bitwise (NH: a model
     index per branch)."""
-    et, m, alph, rates, probs, states = _random_problem(S, C, 24, 700, seed=5)
+    et, m, alph, rates, probs, states = _random_problem(S, C, 120, 700, seed=5)
     rng = np.random.default_rng(9)
     models = [m] + [phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5)) for _ in range(2)] \
         if S == 4 else [m]
     mon = rng.integers(0, len(models), et.n_nodes).astype(np.int32)
     br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    assert len(br) > 160
     ops = phylo.split_ops(et.ops)
     out = []
-    for staged in ("0", "1"):
-        set_tune(monkeypatch, "PMAT_STAGED", staged)
+    for chunk in (len(br), 100):
         eng = engine_for(et, S, C, 700, states, alph.init_table, rates, probs, m.pi, models, model_of_node=mon,
                          flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY)
         res = []
         for scale in (0.7, 1.4):
-            lnl, blocks = eng.evaluate(br, et.brlen[br] * scale, ops, et.root, mon[br])
+            for k in range(0, len(br), chunk):
+                eng.update_pmatrices(br[k:k + chunk], et.brlen[br[k:k + chunk]] * scale, mon[br[k:k + chunk]])
+            eng.update_partials(ops)
+            lnl, _, blocks = eng.root_loglik(et.root, want_blocks=True)
             res.append((lnl, blocks, np.stack([eng.get_pmatrix(int(b)) for b in br])))
         out.append(res)
         del eng
-    for other in out[1:]:
-        for (l0, b0, p0), (l1, b1, p1) in zip(out[0], other):
-            assert l0 == l1 and np.array_equal(b0, b1) and np.array_equal(p0, p1)
+    for (l0, b0, p0), (l1, b1, p1) in zip(out[0], out[1]):
+        assert l0 == l1 and np.array_equal(b0, b1) and np.array_equal(p0, p1)
 
 
 @pytest.mark.parametrize("S,C,n_taxa,scaling", [(4, 4, 64, False), (4, 4, 40, True), (20, 4, 40, True),
@@ -782,21 +784,6 @@ def test_root_pair_derivatives_vs_oracle_finite_differences(S, C, mode, scaling,
         eng.root_pair_derivatives(int(a), int(a), 0.5, 0.5)
 
 
-def test_branch_derivatives_path_equals_kernel(monkeypatch):
-    """4 states: the levelwise path derivatives equal the register-resident deriv_kernel."""
-    et, m, alph, rates, probs, states = _random_problem(4, 4, 24, 3000, seed=61)
-    eng = engine_for(et, 4, 4, 3000, states, alph.init_table, rates, probs, m.pi, [m])
-    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
-    eng.update_pmatrices(br, et.brlen[br], deriv_mask=7)
-    run_engine(eng, et)
-    for b in (0, 5, et.n_tips + 2, br[-1]):
-        k1, k2 = eng.branch_derivatives(int(b))
-        set_tune(monkeypatch, "DERIV_PATH", "1")
-        p1, p2 = eng.branch_derivatives(int(b))
-        clear_tune(monkeypatch, "DERIV_PATH")
-        assert abs(k1 - p1) <= 1e-11 * max(1.0, abs(k1)) and abs(k2 - p2) <= 1e-10 * max(1.0, abs(k2)), (b, k1, p1, k2, p2)
-
-
 def test_branch_derivatives_require_dp():
     et, m, alph, rates, probs, states = _random_problem(4, 4, 6, 100, seed=3)
     eng = engine_for(et, 4, 4, 100, states, alph.init_table, rates, probs, m.pi, [m])
@@ -886,15 +873,13 @@ def test_subtree_patterns_errors():
 @pytest.mark.parametrize("S,C,n_taxa,n_patterns,scaling,amb", [
     (20, 4, 24, 900, False, True), (20, 2, 40, 700, True, False), (20, 1, 9, 300, False, False),
     (64, 1, 16, 600, False, True), (64, 1, 30, 400, True, False), (64, 1, 8, 300, False, False)])
-def test_subtree_patterns_any_state_count(S, C, n_taxa, n_patterns, scaling, amb, monkeypatch):
+def test_subtree_patterns_any_state_count(S, C, n_taxa, n_patterns, scaling, amb):
     """Row f3 beyond DNA: per-subtree compression for 20 and 64 states
     (partials_links_generic_kernel) against the oracle's own usePatterns = true pruning
-    at 1e-12 and, bitwise, against the uncompressed generic levelwise kernel it restates
-    (lnL, per-pattern lnL, block sums and every partial expanded through the links)."""
+    at 1e-12 and against the uncompressed levelwise kernels (K2 / K3) at 1e-12 (lnL,
+    per-pattern lnL, block sums and every partial expanded through the links)."""
     et, m, alph, rates, probs, states = _random_problem(S, C, n_taxa, n_patterns, seed=90 + S + C, amb=amb)
     sc = plk.PLK_FLAG_SCALING if scaling else 0
-    set_tune(monkeypatch, "GENERIC20", "1")
-    set_tune(monkeypatch, "GENERIC64", "1")
     ref = engine_for(et, S, C, n_patterns, states, alph.init_table, rates, probs, m.pi, [m],
                      flags=plk.PLK_FLAG_NONNEG_GUARD | sc | plk.PLK_FLAG_LEVELWISE)
     l0, s0, b0 = run_engine(ref, et)
@@ -905,7 +890,8 @@ def test_subtree_patterns_any_state_count(S, C, n_taxa, n_patterns, scaling, amb
     l1, s1, b1 = run_engine(eng, et)
     assert eng.kernel_path() == "subtree_patterns"
     p1 = np.stack([eng.get_partials(p) for p, _ in et.ops])
-    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1) and np.array_equal(p0, p1)
+    assert abs(l0 - l1) <= 1e-12 * abs(l0) and np.allclose(s0, s1, rtol=1e-12, atol=0)
+    assert np.allclose(b0, b1, rtol=1e-12, atol=0) and np.allclose(p0, p1, rtol=1e-12, atol=1e-300)
     assert eng.compressed_work() < n_patterns * et.n_internal
     ss, sons, lr = et.son_arrays()
     lo, so, _, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, alph.init_table, engine_pmats(eng, et), probs,
@@ -938,11 +924,10 @@ def test_subtree_patterns_derivatives(S, C):
 @pytest.mark.gpu
 @pytest.mark.parametrize("S,C,scaling,variant", [
     (20, 4, True, ""), (20, 2, False, "amb"), (20, 4, True, "tiny"), (64, 1, False, ""), (64, 1, True, "tiny")])
-def test_treeM_cherry_tables_bitwise(S, C, scaling, variant, monkeypatch):
-    """treeM with cherry contribution tables (T_CHERRY rows, plk_treeM.hpp) against the same
-    traversal without them (PLK_TREEM_CHERRY=0): lnL, per-pattern lnL and block sums
-    bitwise, and the oracle.  "tiny": one code's vector is 1e-80, so cherry partials fall
-    below 2^-256 and the tables' precomputed joint rescale must fire."""
+def test_treeM_cherry_tables_vs_oracle(S, C, scaling, variant, monkeypatch):
+    """treeM with cherry contribution tables (T_CHERRY rows, plk_treeM.hpp) against the
+    oracle.  "tiny": one code's vector is 1e-80, so cherry partials fall below 2^-256 and the
+    tables' precomputed joint rescale must fire."""
     et, m, alph, rates, probs, states = _random_problem(S, C, 48 if S == 20 else 24, 700, seed=S + C,
                                                         amb=variant == "amb")
     init = alph.init_table
@@ -954,15 +939,10 @@ def test_treeM_cherry_tables_bitwise(S, C, scaling, variant, monkeypatch):
         states[rng.random(states.shape) < 0.3] = code
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | (plk.PLK_FLAG_SCALING if scaling else 0)
     set_tune(monkeypatch, "JITM", "0")   # the treeM interpreter (20 states default to jit_treeM)
-    res = {}
-    for on in ("0", "1"):
-        set_tune(monkeypatch, "TREEM_CHERRY", on)
-        eng = engine_for(et, S, C, 700, states, init, rates, probs, m.pi, [m], flags=flags)
-        res[on] = run_engine(eng, et)
-        assert eng.kernel_path() == "treeM"
-        del eng
-    (l0, s0, b0), (l1, s1, b1) = res["0"], res["1"]
-    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1)
+    eng = engine_for(et, S, C, 700, states, init, rates, probs, m.pi, [m], flags=flags)
+    l1, s1, b1 = run_engine(eng, et)
+    assert eng.kernel_path() == "treeM"
+    assert eng.traversal_work()["table_nodes"] > 0
     if variant == "tiny":
         assert s1.min() < -256 * np.log(2)
     lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=scaling)
@@ -970,70 +950,23 @@ def test_treeM_cherry_tables_bitwise(S, C, scaling, variant, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_pmat64_kernels_bitwise(monkeypatch):
-    """The 64-state K4 and tip-table kernels (register-blocked, LDS-staged) give the generic
-    kernels' results bitwise: every P(t) and the traversal's lnL."""
+def test_pmat64s_kernel_bitwise():
+    """The 64-state K4 (pmat64s_kernel: register-blocked, LDS-staged, split in four row slabs)
+    gives the generic kernel's results bitwise (a P-only request runs pmat64s_kernel, a
+    P + dP + d2P request the generic pmat_kernel): every P(t) and the traversal's lnL."""
     et, m, alph, rates, probs, states = _random_problem(64, 1, 24, 500, seed=64, amb=True)
-    out = {}
-    for on, split in (("0", "1"), ("1", "0"), ("1", "1")):  # generic, pmat64_kernel, pmat64s_kernel
-        set_tune(monkeypatch, "PMAT64", on)
-        set_tune(monkeypatch, "PMAT64_SPLIT", split)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    ops = phylo.split_ops(et.ops)
+    out = []
+    for mask in (plk.PLK_DERIV_P, 7):
         eng = engine_for(et, 64, 1, 500, states, alph.init_table, rates, probs, m.pi, [m],
                          flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY)
-        lnl, site, _ = run_engine(eng, et)
-        P = np.stack([eng.get_pmatrix(c) for _, ch in et.ops for c in ch])
-        out[on + split] = (lnl, site, P)
+        eng.update_pmatrices(br, et.brlen[br], deriv_mask=mask)
+        eng.update_partials(ops)
+        lnl, site, _ = eng.root_loglik(et.root, want_sites=True)
+        out.append((lnl, site, np.stack([eng.get_pmatrix(int(b)) for b in br])))
         del eng
-    for k in ("10", "11"):
-        assert out["01"][0] == out[k][0] and np.array_equal(out["01"][1], out[k][1])
-        assert np.array_equal(out["01"][2], out[k][2])
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("S,C,scaling,mode", [(20, 4, True, "lnl_only"), (20, 2, False, "materialize"),
-                                              (64, 1, False, "lnl_only"), (64, 1, True, "materialize")])
-def test_treeM_direct_tables_bitwise(S, C, scaling, mode, monkeypatch):
-    """treeM reading P^T and tip-table rows straight from L1/L2 (PLK_TREEM_DIRECT=1) equals the
-    LDS-staged kernel (=0) bitwise: lnL, per-pattern lnL, block sums and stored partials."""
-    et, m, alph, rates, probs, states = _random_problem(S, C, 40 if S == 20 else 20, 600, seed=S + 3 * C,
-                                                        amb=S == 20)
-    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
-    set_tune(monkeypatch, "JITM", "0")
-    res = {}
-    for on in ("0", "1"):
-        set_tune(monkeypatch, "TREEM_DIRECT", on)
-        eng = engine_for(et, S, C, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
-        lnl, site, blocks = run_engine(eng, et)
-        assert eng.kernel_path() == "treeM"
-        parts = np.stack([eng.get_partials(p) for p, _ in et.ops[-3:]])
-        res[on] = (lnl, site, blocks, parts)
-        del eng
-    a, b = res["0"], res["1"]
-    assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("C,scaling,mode,n_pat", [(4, True, "lnl_only", 700), (2, False, "materialize", 333),
-                                                  (4, False, "lnl_only", 64)])
-def test_treeM_32_pattern_workgroups_bitwise(C, scaling, mode, n_pat, monkeypatch):
-    """20 states with 32- and 16-pattern workgroups (PLK_TREEM_G=2, 1; root wave sums formed from
-    site_lnl by site_wave_sums_kernel) equal the 64-pattern kernel bitwise."""
-    et, m, alph, rates, probs, states = _random_problem(20, C, 40, n_pat, seed=7 * C + n_pat)
-    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
-    set_tune(monkeypatch, "JITM", "0")
-    res = {}
-    for g in ("4", "2", "1"):
-        set_tune(monkeypatch, "TREEM_G", g)
-        eng = engine_for(et, 20, C, n_pat, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
-        lnl, site, blocks = run_engine(eng, et)
-        assert eng.kernel_path() == "treeM"
-        parts = np.stack([eng.get_partials(p) for p, _ in et.ops[-3:]])
-        res[g] = (lnl, site, blocks, parts)
-        del eng
-    a = res["4"]
-    for g in ("2", "1"):
-        b = res[g]
-        assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+    assert out[0][0] == out[1][0] and np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
 
 
 # ---------------------------------------------------------------- jit_treeM (20 states, v_mfma_f64_4x4x4_4b)
@@ -1092,12 +1025,11 @@ def test_jit_treeM_vs_oracle(C, tree_kind, n_patterns, scaling, mode, variant, m
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dm,L,pd,g", [(2, 1, 1, 4), (3, 2, 2, 4), (4, 1, 1, 4), (4, 1, 3, 4), (4, 1, 1, 8),
-                                       (3, 2, 2, 8)])
-def test_jit_treeM_register_depths(dm, L, pd, g, monkeypatch):
-    """Other fragment heights, fetch lookaheads, P(t) staging distances and workgroup sizes
-    (PLK_JITM_G) give the default kernel's results bitwise (different cuts store different
-    partials, but every operation per node is the same)."""
+@pytest.mark.parametrize("dm,L", [(2, 1), (3, 2), (4, 3), (6, 1)])
+def test_jit_treeM_register_depths(dm, L, monkeypatch):
+    """Other fragment heights (JITM_DM) and operand fetch lookaheads (JITM_L) give the default
+    kernel's results bitwise (different cuts store different partials, but every operation
+    per node is the same)."""
     et, m, alph, rates, probs, states = _random_problem(20, 4, 80, 600, seed=77, amb=True)
     flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
@@ -1105,75 +1037,9 @@ def test_jit_treeM_register_depths(dm, L, pd, g, monkeypatch):
     del eng
     set_tune(monkeypatch, "JITM_DM", str(dm))
     set_tune(monkeypatch, "JITM_L", str(L))
-    set_tune(monkeypatch, "JITM_PD", str(pd))
-    set_tune(monkeypatch, "JITM_G", str(g))
     eng = engine_for(et, 20, 4, 600, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
     l1, s1, _ = run_engine(eng, et)
     assert eng.kernel_path() == "jit_treeM"
     assert np.array_equal(s0, s1) and l0 == l1
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("pipe,lc", [("0", "0"), ("1", "0"), ("1", "3"), ("2", "5"), ("0", "3")])
-def test_jit_treeM_issue_orders_bitwise(pipe, lc, monkeypatch):
-    """jit_treeM's contraction issue orders (JITM_PIPE: per output block / Y-outer with the A
-    operands read ahead / the same with pinned schedule groups) and operand fetch schedules
-    (JITM_LC: code and row together, or the code LC events ahead) run the same operations on
-    the same values: lnL, per-pattern lnL and block sums bitwise equal to the defaults, on a
-    random tree with tips, cherries, fragment roots, ambiguity codes and rescaling."""
-    et, m, alph, rates, probs, states = _random_problem(20, 4, 60, 700, seed=81, amb=True)
-    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
-    out = []
-    for tune in ({}, {"JITM_PIPE": pipe, "JITM_LC": lc}):
-        for k in ("JITM_PIPE", "JITM_LC"):
-            clear_tune(monkeypatch, k)
-        for k, v in tune.items():
-            set_tune(monkeypatch, k, v)
-        eng = engine_for(et, 20, 4, 700, states, alph.init_table, rates, probs, m.pi, [m], flags=flags)
-        out.append(run_engine(eng, et))
-        assert eng.kernel_path() == "jit_treeM"
-        del eng
-    (l0, s0, b0), (l1, s1, b1) = out
-    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("C,tree_kind,n_patterns,scaling,mode,nh", [
-    (4, "balanced64", 3000, False, "lnl_only", False), (4, "balanced64", 1000, False, "materialize", False),
-    (2, "caterpillar40", 700, True, "lnl_only", False), (4, "balanced300", 513, True, "lnl_only", True),
-    (1, "balanced64", 333, True, "materialize", False), (4, "caterpillar200long", 600, True, "lnl_only", False)])
-def test_s4_on_matrix_cores_vs_oracle(C, tree_kind, n_patterns, scaling, mode, nh, monkeypatch):
-    """4 states through jit_treeM (PLK_S4_JITM=1: one v_mfma_f64_4x4x4_4b block per class
-    and 16 patterns) against the oracle at 1e-12, homogeneous and per-branch models."""
-    set_tune(monkeypatch, "S4_JITM", "1")
-    if tree_kind.startswith("balanced"):
-        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=41, lo=0.05, hi=0.4)
-    elif tree_kind.endswith("long"):
-        tree = _caterpillar(int(tree_kind[11:-4]), seed=5, lo=0.5, hi=1.5)
-    else:
-        tree = _caterpillar(int(tree_kind[11:]), seed=6)
-    et = phylo.engine_tree(tree, unroot=not nh)
-    rng = np.random.default_rng(C * 17 + n_patterns)
-    rates, probs = phylo.gamma_rates(C, 0.5) if C > 1 else (np.ones(1), np.ones(1))
-    if nh:
-        models = [phylo.gtr(1.2, 0.4, 0.6, 0.8, 0.5, *rng.dirichlet(np.ones(4) * 5)) for _ in range(et.n_nodes)]
-        mon = np.arange(et.n_nodes)
-        pi = np.array([0.3, 0.2, 0.2, 0.3])
-    else:
-        models = [phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))]
-        mon = None
-        pi = models[0].pi
-    wl = workload.Workload("m", et, models, mon, rates, probs, pi, phylo.DNA, n_patterns, scaling, not nh, 5)
-    states = wl.simulate(0, n_patterns).astype(np.int32)
-    mask = rng.random(states.shape) < 0.05
-    states[mask] = rng.integers(4, 15, size=mask.sum())
-    flags = (0 if nh else plk.PLK_FLAG_NONNEG_GUARD) | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
-    eng = engine_for(et, 4, C, n_patterns, states, phylo.DNA.init_table, rates, probs, pi, models,
-                     model_of_node=mon, flags=flags)
-    lnl, site, blocks = run_engine(eng, et)
-    assert eng.kernel_path() == "jit_treeM"
-    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, pi, models, model_of_node=mon,
-                        scaling=scaling, pmats=engine_pmats(eng, et))
-    check(lnl, site, lo, so)
-    lnl2, site2, _ = run_engine(eng, et)
-    assert lnl2 == lnl and np.array_equal(site2, site)
