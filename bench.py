@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--devices", default=None,
                     help="one-process multi-device mode: comma-separated device list of --gpus entries "
                          "(e.g. 0,0 rehearses two shards on one GPU; the line is then marked a rehearsal)")
+    ap.add_argument("--sim-cpu", default=None, help="numpy / torch: simulate the alignment on the host (default: GPU)")
+    ap.add_argument("--empty-cache", action="store_true")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the config-5 strong-scaling sub-record of the default line")
     ap.add_argument("--strong-steps", type=int, default=10, help="timed steps of the strong sub-record")
@@ -345,8 +347,11 @@ def measure(args, lay, ctx, config, scaling, patterns=None, classes=None, mode="
     t_setup = time.time()
     extra = {"lnl": plk.PLK_FLAG_LNL_ONLY, "materialize": 0, "levelwise": plk.PLK_FLAG_LEVELWISE,
              "subtree": plk.PLK_FLAG_SUBTREE_PATTERNS}[mode]
-    sim_dev = f"cuda:{ctx['device']}" if torch.cuda.is_available() else None
+    sim_dev = ("cpu" if args.sim_cpu == "torch" else None) if args.sim_cpu else \
+        (f"cuda:{ctx['device']}" if torch.cuda.is_available() else None)
     ev = workload.Evaluator(wl, device, start, end, extra_flags=extra, sim_device=sim_dev)
+    if args.empty_cache:
+        torch.cuda.empty_cache()
     xchg = None
     if dist is not None and rehearse:
         # one GPU, every rank on cuda:0: RCCL cannot put two ranks on one device, so the

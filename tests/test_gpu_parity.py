@@ -976,7 +976,7 @@ def test_pmat64s_kernel_bitwise():
     (4, "balanced64", 700, False, "lnl_only", ""), (4, "balanced64", 700, True, "materialize", "amb"),
     (1, "balanced64", 333, True, "lnl_only", ""), (2, "caterpillar30", 400, True, "lnl_only", "amb"),
     (3, "balanced100", 257, True, "materialize", ""), (4, "caterpillar30", 300, False, "materialize", ""),
-    (4, "balanced300", 513, True, "lnl_only", "amb"), (4, "balanced64", 900, True, "lnl_only", "tiny"),
+    (4, "balanced160", 513, True, "lnl_only", "amb"), (4, "balanced64", 900, True, "lnl_only", "tiny"),
     (2, "caterpillar30", 500, True, "materialize", "tiny"), (4, "balanced64", 64, False, "lnl_only", "")])
 def test_jit_treeM_vs_oracle(C, tree_kind, n_patterns, scaling, mode, variant, monkeypatch):
     """The tree-specialised 20-state kernel (plk_jitm.hpp) against the oracle on identical
