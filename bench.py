@@ -56,8 +56,8 @@ def parse():
     ap.add_argument("--devices", default=None,
                     help="one-process multi-device mode: comma-separated device list of --gpus entries "
                          "(e.g. 0,0 rehearses two shards on one GPU; the line is then marked a rehearsal)")
-    ap.add_argument("--sim-cpu", default=None, help="numpy / torch: simulate the alignment on the host (default: GPU)")
-    ap.add_argument("--empty-cache", action="store_true")
+    ap.add_argument("--sim-cpu", default=None, choices=["numpy", "torch"],
+                    help="simulate the alignment on the host (default: on the GPU, the same states bitwise)")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the config-5 strong-scaling sub-record of the default line")
     ap.add_argument("--strong-steps", type=int, default=10, help="timed steps of the strong sub-record")
@@ -350,8 +350,9 @@ def measure(args, lay, ctx, config, scaling, patterns=None, classes=None, mode="
     sim_dev = ("cpu" if args.sim_cpu == "torch" else None) if args.sim_cpu else \
         (f"cuda:{ctx['device']}" if torch.cuda.is_available() else None)
     ev = workload.Evaluator(wl, device, start, end, extra_flags=extra, sim_device=sim_dev)
-    if args.empty_cache:
-        torch.cuda.empty_cache()
+    # the simulation's blocks go back to the device: with torch's cache holding them, every
+    # libplk launch / wait call was measured 2-10 us slower (cfg2 step 0.171 vs 0.159 ms)
+    torch.cuda.empty_cache()
     xchg = None
     if dist is not None and rehearse:
         # one GPU, every rank on cuda:0: RCCL cannot put two ranks on one device, so the
@@ -409,6 +410,8 @@ def measure(args, lay, ctx, config, scaling, patterns=None, classes=None, mode="
     elapsed = time.perf_counter() - t0
     tm = ev.eng.get_timing()
     ev.eng.set_timing(False)
+    if os.environ.get("PLK_DEBUG_HOST"):
+        ev.eng.reset_timing()
     if dist is not None:
         e = torch.tensor([elapsed], dtype=torch.float64, device=ctx["coll_dev"])
         dist.all_reduce(e, op=dist.ReduceOp.MAX)

@@ -18,10 +18,12 @@
 #include <hip/hiprtc.h>
 #include <rccl/rccl.h>
 
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <functional>
 #include <map>
@@ -154,8 +156,12 @@ struct plk_handle_s {
   size_t d_ops_cap = 0;
   // pinned host staging: P(t) requests (reused once req_done has passed) and block sums
   char* h_req = nullptr;
-  char* h_req_dev = nullptr;   // device address of the mapped staging (PLK_PMAT_MAPPED)
+  char* h_req_dev = nullptr;   // device address of the staging
   size_t h_req_cap = 0;
+  bool h_req_vram = false;     // staging in host-written fine-grained device memory (else pinned host)
+  bool req_vram_failed = false;
+  bool in_eval = false;        // inside plk_evaluate: the request's reader is waited for by its stream_wait
+  bool req_unrecorded = false; // a staged request's reader has no req_done record (plk_evaluate)
   hipEvent_t req_done = nullptr;
   double* h_blocks = nullptr;
   int64_t slot_stride = 0;
@@ -322,6 +328,50 @@ int ensure_cap(plk_handle h, void** p, size_t* cap, size_t bytes) {
   int rc = dalloc(h, p, nb);
   if (rc) return rc;
   *cap = nb;
+  return PLK_OK;
+}
+
+// Staging of large P(t) requests (plk_update_pmatrices).  Fine-grained device memory that the
+// host writes straight into over the PCIe BAR, so that the P(t) kernel reads its request from
+// HBM (cfg5, 1 022 branches: 3 us less per evaluation than reading pinned host memory over
+// PCIe); it is used only when the allocation is mapped in this process (mincore) and a pattern
+// written by the host reads back through the device, otherwise mapped pinned host memory.
+int req_staging(plk_handle h, size_t bytes) {
+  if (h->h_req_cap >= bytes) return PLK_OK;
+  if (h->h_req) HIPCHK(h, h->h_req_vram ? hipFree(h->h_req) : hipHostFree(h->h_req));
+  h->h_req = nullptr;
+  h->h_req_dev = nullptr;
+  h->h_req_cap = 0;
+  h->h_req_vram = false;
+  bytes = (bytes + 4095) & ~(size_t)4095;
+  void* p = nullptr;
+  if (!h->req_vram_failed && hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) == hipSuccess) {
+    bool ok = false;
+    const long pg = sysconf(_SC_PAGESIZE);
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)(pg - 1);
+    std::vector<unsigned char> vec((bytes + (reinterpret_cast<uintptr_t>(p) - a0) + pg - 1) / pg);
+    if (mincore(reinterpret_cast<void*>(a0), bytes + (reinterpret_cast<uintptr_t>(p) - a0), vec.data()) == 0) {
+      std::vector<uint64_t> pat(bytes / 8), back(bytes / 8);
+      for (size_t i = 0; i < pat.size(); ++i) pat[i] = 0x9E3779B97F4A7C15ull * (i + 1);
+      std::memcpy(p, pat.data(), bytes);
+      std::atomic_thread_fence(std::memory_order_seq_cst);
+      ok = hipMemcpy(back.data(), p, bytes, hipMemcpyDeviceToHost) == hipSuccess &&
+           std::memcmp(back.data(), pat.data(), bytes) == 0;
+    }
+    if (ok) {
+      h->h_req = static_cast<char*>(p);
+      h->h_req_dev = h->h_req;
+      h->h_req_vram = true;
+      h->h_req_cap = bytes;
+      return PLK_OK;
+    }
+    hipFree(p);
+    hipGetLastError();
+    h->req_vram_failed = true;
+  }
+  HIPCHK(h, hipHostMalloc((void**)&h->h_req, bytes, hipHostMallocMapped));
+  HIPCHK(h, hipHostGetDevicePointer((void**)&h->h_req_dev, h->h_req, 0));
+  h->h_req_cap = bytes;
   return PLK_OK;
 }
 
@@ -947,7 +997,7 @@ int plk_destroy(plk_handle h) {
                   h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre};
   for (void* p : bufs)
     if (p) hipFree(p);
-  if (h->h_req) hipHostFree(h->h_req);
+  if (h->h_req) (void)(h->h_req_vram ? hipFree(h->h_req) : hipHostFree(h->h_req));
   if (h->h_blocks) hipHostFree(h->h_blocks);
   if (h->req_done) hipEventDestroy(h->req_done);
   for (auto& e : h->events) {
@@ -1194,28 +1244,30 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
       inl.model[i] = model ? model[i] : 0;
     }
   }
-  // larger requests: pinned staging that the kernel reads through its mapped address over
-  // PCIe (cfg5, 1 022 branches: 8.6 us less per evaluation than a stream-ordered copy into
-  // device memory -- the copy's launch and host API time).  The host rewrites the staging
-  // only after the previous request's reader (req_done) finished.
+  // larger requests: a staging buffer the host writes and the kernel reads (cfg5, 1 022
+  // branches: 8.6 us less per evaluation than a stream-ordered copy into device memory -- the
+  // copy's launch and host API time); see req_staging for where it lives.  The host rewrites
+  // the staging only after the previous request's reader finished (req_done, or the stream
+  // wait that ends plk_evaluate).
   const char* req = nullptr;
   if (inl.n == 0) {
     const size_t bytes = (size_t)n * (2 * sizeof(int32_t) + sizeof(double)) + 64;
     if (!h->req_done) HIPCHK(h, hipEventCreateWithFlags(&h->req_done, hipEventDisableTiming));
-    HIPCHK(h, hipEventSynchronize(h->req_done));
-    if (h->h_req_cap < bytes) {
-      if (h->h_req) HIPCHK(h, hipHostFree(h->h_req));
-      h->h_req = nullptr;
-      h->h_req_dev = nullptr;
-      h->h_req_cap = 0;
-      HIPCHK(h, hipHostMalloc((void**)&h->h_req, bytes, hipHostMallocMapped));
-      HIPCHK(h, hipHostGetDevicePointer((void**)&h->h_req_dev, h->h_req, 0));
-      h->h_req_cap = bytes;
+    if (h->req_unrecorded) {
+      HIPCHK(h, hipStreamSynchronize(h->stream));
+      h->req_unrecorded = false;
+    } else {
+      HIPCHK(h, hipEventSynchronize(h->req_done));
     }
+    int rc = req_staging(h, bytes);
+    if (rc) return rc;
     char* staging = h->h_req;
     std::memcpy(staging + off_t, t, n * sizeof(double));
     std::memcpy(staging + off_b, branch, n * sizeof(int32_t));
     if (model) std::memcpy(staging + off_m, model, n * sizeof(int32_t));
+    // the host's stores reach the staging before the launch's doorbell (a device-memory
+    // staging is write-combined over the BAR)
+    std::atomic_thread_fence(std::memory_order_seq_cst);
     req = h->h_req_dev;
   }
   PmatArgs a;
@@ -1267,7 +1319,14 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     else pmat_kernel<16><<<g, dim3(nth), lds, h->stream>>>(a, inl);
   }
   HIPCHK(h, hipGetLastError());
-  if (inl.n == 0) HIPCHK(h, hipEventRecord(h->req_done, h->stream));  // the kernel read the staging
+  if (inl.n == 0) {
+    // the kernel read the staging: plk_evaluate waits for the whole stream before it returns
+    // (no record needed), other callers record req_done
+    if (h->in_eval)
+      h->req_unrecorded = true;
+    else
+      HIPCHK(h, hipEventRecord(h->req_done, h->stream));
+  }
   if (h->timing & PLK_TIME_PMAT) {
     hipEventRecord(ev.b, h->stream);
     h->events.push_back(ev);
@@ -3696,7 +3755,9 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
   using clk = std::chrono::steady_clock;
   const clk::time_point t0 = clk::now();
   auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+  h->in_eval = true;
   int rc = plk_update_pmatrices(h, n, branch, model, t, PLK_DERIV_P);
+  h->in_eval = false;
   if (rc) return rc;
   const clk::time_point t1 = clk::now();
   rc = plk_update_partials(h, ops, n_ops);
@@ -3706,6 +3767,7 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
   if (rc) return rc;
   const clk::time_point t3 = clk::now();
   if ((rc = stream_wait(h))) return rc;
+  h->req_unrecorded = false;  // the staging's reader is done
   const clk::time_point t4 = clk::now();
   rc = root_finish(h, lnl, block_sums, false);
   if (rc) return rc;
