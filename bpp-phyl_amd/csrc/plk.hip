@@ -3319,11 +3319,20 @@ int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
   if (!h || n_ops < 0 || (n_ops > 0 && !ops)) return fail(h, PLK_ERR_ARG, "bad op list");
   if (n_ops == 0) return PLK_OK;
   hipSetDevice(h->device);
-  int rc = validate_ops(h, ops, n_ops);
-  if (rc) return rc;
-  // merge the op list into the tree (skipped when it repeats the last call's list, the
-  // common case of an optimiser's evaluations)
-  if (h->trav_ops.size() != (size_t)n_ops || std::memcmp(h->trav_ops.data(), ops, n_ops * sizeof(plk_op)) != 0) {
+  // the last call's list again (an optimiser's evaluations): its checks hold still -- every
+  // condition validate_ops tests is monotonic (matrices, tip codes) except the partial an
+  // ACCUMULATE op extends, so only such lists are checked again
+  const bool repeat = h->trav_ops.size() == (size_t)n_ops &&
+                      std::memcmp(h->trav_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
+  bool accumulate = false;
+  if (repeat)
+    for (int i = 0; i < n_ops && !accumulate; ++i) accumulate = (ops[i].flags & PLK_OP_ACCUMULATE) != 0;
+  if (!repeat || accumulate) {
+    int rc = validate_ops(h, ops, n_ops);
+    if (rc) return rc;
+  }
+  // merge the op list into the tree (skipped when it repeats the last call's list)
+  if (!repeat) {
     h->trav_ops.assign(ops, ops + n_ops);
     for (int i = 0; i < n_ops; ++i) {
       std::vector<int>& k = h->topo_kids[ops[i].parent];
