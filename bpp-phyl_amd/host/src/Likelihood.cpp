@@ -565,16 +565,24 @@ double AbstractPlkTreeLikelihood::getFirstOrderDerivative(const std::string& var
   const double t = parameters_.getParameterValue(variable);
   const double h = 1e-5 * std::max(t, 1e-3);
   ParameterList pl = parameters_.createSubList(std::vector<std::string>(1, variable));
-  pl[0].setValue(t + h);
+  // both points inside the parameter's own constraint (BrLen<i>: [min, max] branch length,
+  // RootPosition: (0, 1)); one-sided at a bound
+  double tp = t + h, tm = t - h;
+  if (pl[0].hasConstraint()) {
+    const Constraint& c = *pl[0].getConstraint();
+    if (!c.isCorrect(tp)) tp = t;
+    if (!c.isCorrect(tm)) tm = t;
+  }
+  if (tp == tm) throw Exception("getFirstOrderDerivative: no room for a difference in " + variable);
+  pl[0].setValue(tp);
   self->setParameters(pl);
   const double fp = minusLogLik_;
-  pl[0].setValue(std::max(t - h, minimumBrLen_));
-  const double tm = pl[0].getValue();
+  pl[0].setValue(tm);
   self->setParameters(pl);
   const double fm = minusLogLik_;
   pl[0].setValue(t);
   self->setParameters(pl);
-  return (fp - fm) / (t + h - tm);
+  return (fp - fm) / (tp - tm);
 }
 
 double AbstractPlkTreeLikelihood::getSecondOrderDerivative(const std::string& variable) const {
@@ -588,15 +596,30 @@ double AbstractPlkTreeLikelihood::getSecondOrderDerivative(const std::string& va
   const double h = 1e-4 * std::max(t, 1e-2);
   ParameterList pl = parameters_.createSubList(std::vector<std::string>(1, variable));
   const double f0 = minusLogLik_;
-  pl[0].setValue(t + h);
-  self->setParameters(pl);
-  const double fp = minusLogLik_;
-  pl[0].setValue(std::max(t - h, minimumBrLen_));
-  self->setParameters(pl);
-  const double fm = minusLogLik_;
+  // three equally spaced points inside the parameter's own constraint: centred, or shifted
+  // one step in when t +- h leaves it (one-sided second difference at a bound)
+  double x0 = t - h;
+  if (pl[0].hasConstraint()) {
+    const Constraint& c = *pl[0].getConstraint();
+    if (!c.isCorrect(t - h)) x0 = t;
+    else if (!c.isCorrect(t + h)) x0 = t - 2. * h;
+    if (!c.isCorrect(x0) || !c.isCorrect(x0 + 2. * h))
+      throw Exception("getSecondOrderDerivative: no room for a difference in " + variable);
+  }
+  double f[3];
+  for (int k = 0; k < 3; k++) {
+    const double x = x0 + k * h;
+    if (x == t) {
+      f[k] = f0;
+      continue;
+    }
+    pl[0].setValue(x);
+    self->setParameters(pl);
+    f[k] = minusLogLik_;
+  }
   pl[0].setValue(t);
   self->setParameters(pl);
-  return (fp - 2. * f0 + fm) / (h * h);
+  return (f[2] - 2. * f[1] + f[0]) / (h * h);
 }
 
 // ---------------------------------------------------------------------------

@@ -227,7 +227,11 @@ int plk_block_size(void);
  *   RootPosition: alpha = BrLenRoot,    beta = -BrLenRoot
  * and replaces computeTreeDLikelihood / computeTreeD2Likelihood for those two variables
  * (Likelihood/RNonHomogeneousTreeLikelihood.cpp:391-560, 862-1100).  Requires dP and d2P of
- * both branches.  Any state and class count. */
+ * both branches.  Any state and class count.
+ * Under an RCCL communicator (plk_comm_init) this and plk_branch_derivatives return THIS
+ * RANK'S share (its pattern range) only -- unlike plk_evaluate's lnL, derivatives are not
+ * exchanged: the caller sums d1 and d2 over the ranks (one all-reduce of two doubles).  A
+ * multi-device handle (plk_create_multi) returns the sum over its devices. */
 int plk_root_pair_derivatives(plk_handle h, int a, int b, double alpha, double beta, double* d1, double* d2);
 
 /* Double-recursive derivatives (handle created with PLK_FLAG_DOUBLE_RECURSIVE): d lnL/dt and
