@@ -169,7 +169,12 @@ void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
     plk_destroy(engine_);
     engine_ = nullptr;
   }
-  const bool scaling = scalingMode_ >= 0 ? scalingMode_ == 1 : nTips_ * std::log((double)nbStates_) > 300.;
+  // Default: exact power-of-two rescaling unless the tree is small enough that no site can
+  // leave the double range.  A tip on a minimum-length branch with a mismatch contributes about
+  // ln(1e-6 * rate) ~ -20 to a site's log-likelihood, so 32 tips stay above -708 whatever the
+  // data; beyond that (or for large state spaces) scaling is on.
+  const bool scaling =
+      scalingMode_ >= 0 ? scalingMode_ == 1 : (nTips_ > 32 || nTips_ * std::log((double)nbStates_) > 300.);
   unsigned flags = (scaling ? (unsigned)PLK_FLAG_SCALING : 0u) | (nonNegGuard ? (unsigned)PLK_FLAG_NONNEG_GUARD : 0u) |
                    extraFlags_;
   // usePatterns (the reference default): per-subtree site-pattern compression on the device

@@ -332,6 +332,45 @@ static void gapCase() {
   if (!thrown) failures++;
 }
 
+// Underflow scaling by default on a large tree of very short branches: 150 DNA
+// taxa, every branch 1e-6, random sequences -- each site's likelihood is ~1e-600, far below
+// the double range, so the default rule must switch the exact power-of-two rescaling on (the
+// reference's RHomogeneousTreeLikelihood.cpp sums log site likelihoods without rescaling).
+static std::string comb(int lo, int hi) {
+  if (hi - lo == 1) return "t" + std::to_string(lo) + ":0.000001";
+  const int mid = (lo + hi) / 2;
+  return "(" + comb(lo, mid) + "," + comb(mid, hi) + "):0.000001";
+}
+
+static void shortBranchScalingCase() {
+  const int n = 150, L = 40;
+  std::string nwk = comb(0, n);
+  nwk = nwk.substr(0, nwk.rfind(':')) + ";";
+  std::unique_ptr<TreeTemplate<Node> > tree(TreeTemplateTools::parenthesisToTree(nwk));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  unsigned long long x = 12345;
+  for (int i = 0; i < n; i++) {
+    std::string s;
+    for (int j = 0; j < L; j++) {
+      x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+      s += "ACGT"[(x >> 33) & 3];
+    }
+    aln.addSequence(BasicSequence("t" + std::to_string(i), s, dna));
+  }
+  T92 model(dna, 3.);
+  GammaDiscreteRateDistribution rdist(4, 0.5);
+  RHomogeneousTreeLikelihood def(*tree, aln, &model, &rdist, false, false);
+  def.initialize();
+  RHomogeneousTreeLikelihood on(*tree, aln, &model, &rdist, false, false);
+  on.setUnderflowScaling(true);
+  on.initialize();
+  const double a = def.getValue(), b = on.getValue();
+  std::cout << std::setprecision(17) << "150 taxa, branches 1e-6: default -lnL " << a << ", scaling on " << b << std::endl;
+  if (!std::isfinite(a) || a < 1000.) failures++;
+  expectNear("default rule == scaling on", a, b, 1e-9 * std::fabs(b));
+}
+
 int main() {
   try {
     unrootedGammaCase();
@@ -341,6 +380,7 @@ int main() {
     taylorModelCase();
     complexEigenModelCase();
     gapCase();
+    shortBranchScalingCase();
   } catch (Exception& e) {
     std::cerr << e.what() << std::endl;
     return 1;
