@@ -194,6 +194,9 @@ struct plk_handle_s {
   size_t d_prog_cap = 0;
   int32_t* d_frag = nullptr;
   size_t d_frag_cap = 0;
+  unsigned* d_sbctr = nullptr;          // jit_tree4 dynamic super-block counters, one per fragment
+  size_t d_sbctr_cap = 0;
+  std::vector<unsigned> sb_base;        // each counter's value at the start of its next launch
   std::vector<plk_op> prog_ops;           // op list the cached program was built from
   bool prog_materialize = false;
   bool prog_reduce = false;
@@ -994,7 +997,7 @@ int plk_destroy(plk_handle h) {
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
-                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre};
+                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre, h->d_sbctr};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) (void)(h->h_req_vram ? hipFree(h->h_req) : hipHostFree(h->h_req));
@@ -1714,6 +1717,10 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   HIPCHK(h, hipMemcpyAsync(h->d_frag, start_sorted.data(), 2 * nf * sizeof(int32_t), hipMemcpyHostToDevice,
                            h->stream));
   h->prog_nf = nf;
+  rc = ensure_cap(h, (void**)&h->d_sbctr, &h->d_sbctr_cap, std::max(nf, 1) * sizeof(unsigned));
+  if (rc) return rc;
+  HIPCHK(h, hipMemsetAsync(h->d_sbctr, 0, std::max(nf, 1) * sizeof(unsigned), h->stream));
+  h->sb_base.assign((size_t)std::max(nf, 1), 0u);
   h->prog_host = prog;
   h->frag_starts_host.assign(start_sorted.begin(), start_sorted.begin() + nf);
   h->jit_fn = nullptr;  // specialised kernel of the new program: compiled on first use
@@ -1963,6 +1970,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.n_patterns = a.n_patterns;
     ja.n_sblocks = (int32_t)((h->n_pad + 64 * sh.G * sh.PW - 1) / (64 * sh.G * sh.PW));  // last may be ragged
     ja.guard = a.guard;
+    ja.sb_ctr = h->d_sbctr;
+    ja.dyn = tune_is("JIT_DYN", '0') ? 0 : 1;  // (per launch below)
   }
   const bool jitm = kind == FK_TREEM && h->prog_jitm;
   JMArgs ma;
@@ -2040,12 +2049,28 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         wgs = std::max(1, h->jit_resident / (int)grid.y);
       }
       const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, wgs);
+      // dynamic super-blocks where a workgroup walks several (a tier of 1-2 per workgroup
+      // gains nothing from them and pays the counter's round trips)
+      ja.dyn = (!tune_is("JIT_DYN", '0') && ja.n_sblocks >= 3 * (int64_t)gx) ? 1 : 0;
+      // the tier's fragments take their super-blocks from counters that start this launch
+      // at one common value (every fragment is launched once per traversal with the same
+      // super-block count, so they stay equal; otherwise they are reset here)
+      ja.sb_base = h->sb_base[(size_t)first];
+      for (int k = 1; k < (int)t.size(); ++k)
+        if (h->sb_base[(size_t)(first + k)] != ja.sb_base) {
+          HIPCHK(h, hipMemsetAsync(h->d_sbctr, 0, (size_t)h->prog_nf * sizeof(unsigned), h->stream));
+          std::fill(h->sb_base.begin(), h->sb_base.end(), 0u);
+          ja.sb_base = 0;
+          break;
+        }
       h->jit_last_gx = (int)gx;
       if ((int)h->jit_frag_gx.size() < h->prog_nf) h->jit_frag_gx.resize((size_t)h->prog_nf, 0);
       for (int k = 0; k < (int)t.size(); ++k) h->jit_frag_gx[(size_t)(first + k)] = (int)gx;
       HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
                                       (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
+      if (ja.dyn)
+        for (int k = 0; k < (int)t.size(); ++k) h->sb_base[(size_t)(first + k)] += (unsigned)ja.n_sblocks;
     } else if (jitm) {
       int base = first;
       void* args[] = {&ma, &base};

@@ -53,6 +53,7 @@ struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
   double* partials; i32* scale; const u8* codes; const double* tipP; const double* weights;
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
+  unsigned* sb_ctr; unsigned sb_base; i32 dyn;
 };
 
 // Register vectors hold 4 * CW * PW doubles: vector v = pw * CW + cw is class c0 + cw of
@@ -358,6 +359,12 @@ struct JArgs {
   int64_t n_patterns;
   int32_t n_sblocks;
   int32_t guard;
+  // dynamic super-blocks (dyn != 0): after its first super-block (blockIdx.x) a workgroup
+  // takes the next one from sb_ctr[frag] (a counter that only grows: this launch's values
+  // start at sb_base, and it ends the launch at sb_base + n_sblocks)
+  unsigned* sb_ctr;
+  unsigned sb_base;
+  int32_t dyn;
 };
 
 struct JitShape {
@@ -529,9 +536,32 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // (kScUnit, CSR kFragScStart) and staged with one (unit, row) per thread of the whole
   // workgroup -- such a unit has only U * U rows (16 for DNA), so one unit per wave left 48
   // of 64 lanes idle and cost one dependent load round per unit and wave; the other units
-  // (kOtherUnit, kFragOtherStart) keep one unit per wave.
+  // (kOtherD: their records in that order, CSR kFragOtherStart) keep one unit per wave.
   std::string sc = "};\n__device__ const int kFragScStart[] = {0", scu = "};\n__device__ const int kScUnit[] = {0",
-              ot = "};\n__device__ const int kFragOtherStart[] = {0", otu = "};\n__device__ const int kOtherUnit[] = {0";
+              ot = "};\n__device__ const int kFragOtherStart[] = {0",
+              otu = "};\n__device__ const UnitD kOtherD[] = {{0, 0, 0, 0, 0, 0, 0, 0}";
+  {
+    // the P(t) matrices each fragment reads (CSR kFragPStart / kFragPBr), touched at launch
+    std::string st = "\n__device__ const int kFragPStart[] = {0", br = "};\n__device__ const int kFragPBr[] = {0";
+    int acc = 0;
+    for (size_t f = 0; f < events.size(); ++f) {
+      std::vector<int> b;
+      for (const JitEvent& e : events[f])
+        if ((e.op == T_LOAD || e.op == T_ASCEND) && e.b >= 0) b.push_back(e.b);
+      for (const JitUnit& u : plan.units[f])
+        if (u.br >= 0) b.push_back(u.br);
+      std::sort(b.begin(), b.end());
+      b.erase(std::unique(b.begin(), b.end()), b.end());
+      for (int x : b) {
+        snprintf(buf, sizeof(buf), ",%d", x);
+        br += buf;
+      }
+      acc += (int)b.size();
+      snprintf(buf, sizeof(buf), ",%d", acc);
+      st += buf;
+    }
+    s += st + br + "};\n";
+  }
   s += "\n__device__ const int kFragUnitStart[] = {0";
   {
     int acc = 0, nsc = 0, not_ = 0;
@@ -548,6 +578,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
           scu += buf;
           ++nsc;
         } else {
+          snprintf(buf, sizeof(buf), ",{%d,%d,%d,%d,%d,0,0,0}", u.ta, u.tb, u.off, u.br, u.koff);
           otu += buf;
           ++not_;
         }
@@ -599,6 +630,21 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       if (q0_ + ic_[m] < a.n_pad) va_[m] = ucodes[iu_[m] + (q0_ >> 4)];
   };
   fetch_codes(blockIdx.x);  // (issued before the table staging below: its loads overlap it)
+  // The fragment's P(t) matrices, touched with wide loads while the tables stage: the
+  // traversal reads P(t) through scalar loads one contribution ahead, and their first touch
+  // (the P(t) launch wrote them through another XCD's L2) made the first super-block ~12 us
+  // slower on cfg5 (34 vs 22 us; steady state 19 us)
+  // (with one class per wave (cfg2) the first super-block shows no such penalty and the
+  // touch only lengthened the staging, so there it is left out)
+  double ptouch_ = 0.0;
+  if (CW_ > 1) {
+    const int pb0 = 1 + kFragPStart[frag], npb = kFragPStart[frag + 1] - kFragPStart[frag];
+    const double2* pp_ = reinterpret_cast<const double2*>(pmats);
+    for (int i = threadIdx.x; i < npb * C_ * 8; i += 64 * NWT_) {
+      const int k_ = i / (C_ * 8);
+      ptouch_ += pp_[(i64)kFragPBr[pb0 + k_] * (C_ * 8) + (i - k_ * (C_ * 8))].x;
+    }
+  }
   if (SC_) {
     // rescaling contribution units: one (unit, row) per thread; each row all classes, the
     // cherry's joint check as rescale() makes it, then contrib<.., true>
@@ -635,11 +681,13 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // the other tables: wave w stages units w, w + NWT_, ... of the fragment's other-unit list
   // (one dependent chain per unit and wave, the waves' chains overlap)
   const int ot0 = 1 + kFragOtherStart[frag], not_ = kFragOtherStart[frag + 1] - kFragOtherStart[frag];
+  // (the next unit's record is loaded while this one's rows load and compute)
+  UnitD ud_nx = kOtherD[w < not_ ? ot0 + w : 0];
   for (int ko = w; ko < not_; ko += NWT_) {
-    const int k = kOtherUnit[ot0 + ko];
-    const UnitD ud = kUnitD[u0 + k];
-    // every field materialised here: one load and one wait before the branches on them
+    const UnitD ud = ud_nx;
+    // every field materialised here: one wait before the branches on them
     asm volatile("" ::"s"(ud.ta), "s"(ud.tb), "s"(ud.off), "s"(ud.br), "s"(ud.koff));
+    if (ko + NWT_ < not_) ud_nx = kOtherD[ot0 + ko + NWT_];
     const int ta = ud.ta, tb = ud.tb;
     double* dst = tab + ud.off;
     const double* ra = a.tipP + (i64)ta * (C_ * U_ * 4);
@@ -709,7 +757,18 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[4 * CW_ * pw_ + i_] = L_[64 * pw_ + (i64)i_ * kTile]; \
       if (SC_) FK[pw_] = a.scale[sl_ * a.n_pad + p + 64 * pw_]; } }
 #define SB __builtin_amdgcn_sched_barrier(0);
-  for (int sb = blockIdx.x; sb < a.n_sblocks; sb += gridDim.x) {
+  asm volatile("" ::"v"(ptouch_));  // (keeps the touch loads)
+  // Super-block order.  Static: blockIdx.x, + gridDim.x, ...  Dynamic (a.dyn): the first is
+  // blockIdx.x, every later one comes from the fragment's counter -- thread 0 takes the index
+  // of the super-block after the next one while this one computes, so the atomic's latency is
+  // hidden; a workgroup stops taking after its first index past the end (exactly one such
+  // take per workgroup, so the counter ends at sb_base + n_sblocks).  Which workgroup
+  // computes a super-block does not change its results.
+  __shared__ int sb_next_lds;
+  unsigned sb_pend = 0;
+  if (a.dyn && threadIdx.x == 0)
+    sb_pend = __hip_atomic_fetch_add(a.sb_ctr + frag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int sb = blockIdx.x, sb_nx = 0; sb < a.n_sblocks; sb = sb_nx) {
     const i64 q0 = (i64)sb * (64 * PW_ * G_);
     // super-blocks of G_ groups; in a ragged last one, groups past n_pad recompute group 0
     // (in bounds everywhere) and store nothing
@@ -721,8 +780,15 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     __syncthreads();  // the previous super-block is done with code_lds / xch (and tab is staged)
     _Pragma("unroll") for (int m = 0; m < NI_; ++m)
       if (q0 + ic_[m] < a.n_pad) reinterpret_cast<uint4*>(code_lds)[il_[m]] = va_[m];
+    if (a.dyn && threadIdx.x == 0) {  // (an index outside this launch's range ends the loop)
+      const unsigned d_ = sb_pend - a.sb_base;
+      sb_next_lds = d_ < (unsigned)(a.n_sblocks - (int)gridDim.x) ? (int)gridDim.x + (int)d_ : a.n_sblocks;
+    }
     __syncthreads();
-    fetch_codes(sb + gridDim.x);
+    sb_nx = a.dyn ? __builtin_amdgcn_readfirstlane(sb_next_lds) : sb + (int)gridDim.x;
+    if (a.dyn && threadIdx.x == 0 && sb_nx < a.n_sblocks)
+      sb_pend = __hip_atomic_fetch_add(a.sb_ctr + frag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fetch_codes(sb_nx);
 )PLKJIT";
   int max_level = 0;
   for (const auto& ev : events)

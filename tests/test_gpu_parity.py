@@ -661,6 +661,42 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     check(l1, s1, lo, so)
 
 
+@pytest.mark.parametrize("C,n_taxa,n_patterns,scaling", [(4, 64, 320_000, False), (4, 512, 60_000, True)])
+def test_jit_tree4_dynamic_superblocks_bitwise(C, n_taxa, n_patterns, scaling, monkeypatch):
+    """Dynamic super-blocks (workgroups take super-blocks from a per-fragment counter once
+    they walk >= 3 of them): lnL, per-pattern lnL and block sums bitwise equal to the static
+    order (PLK_TUNE JIT_DYN=0), over repeated lnL-only evaluations of one engine at
+    alternating branch lengths (the counters carry over between launches).  320k patterns
+    of a 64-taxon tree: one fragment, ~1 700 super-blocks on ~512 workgroups; the 512-taxon
+    tree with rescaling: eight 64-tip fragments, 32 workgroups each over 118 super-blocks."""
+    tree = phylo.balanced_tree(n_taxa, seed=29, lo=0.05, hi=0.4)
+    et = phylo.engine_tree(tree)
+    rng = np.random.default_rng(n_taxa)
+    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
+    rates, probs = phylo.gamma_rates(C, 0.5)
+    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, scaling, True, 9)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | (plk.PLK_FLAG_SCALING if scaling else 0)
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    res = {}
+    for dyn in ("0", "1"):
+        set_tune(monkeypatch, "JIT_DYN", dyn)
+        eng = engine_for(et, 4, C, n_patterns, states, phylo.DNA.init_table, rates, probs, m.pi, [m], flags=flags)
+        out = []
+        for k in range(7):
+            eng.update_pmatrices(br, et.brlen[br] * (1.0 + 0.1 * (k % 2)))
+            out.append(run_engine(eng, et))
+        assert eng.kernel_path() == "jit_tree4"
+        res[dyn] = out
+        del eng
+    for (l0, s0, b0), (l1, s1, b1) in zip(res["0"], res["1"]):
+        assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1)
+    assert res["1"][0][0] == res["1"][2][0] and res["1"][1][0] == res["1"][3][0]
+    sub = slice(0, 2000)
+    lo, so = oracle_for(et, states[:, sub], phylo.DNA.init_table, rates, probs, m.pi, [m], scaling=scaling)
+    assert np.allclose(res["1"][0][1][sub], so, rtol=REL, atol=0)
+
+
 def test_fused20_partials_equal_levelwise():
     et, m, alph, rates, probs, states = _random_problem(20, 4, 40, 500, seed=33)
     outs = []
