@@ -227,6 +227,9 @@ struct plk_handle_s {
   std::vector<int32_t> cherry3;
   int32_t* d_cherry3 = nullptr;
   int32_t* d_cherry_tips = nullptr;
+  int32_t* d_cherry_rows = nullptr;       // per cherry: the code pairs it meets (CSR, nch + 1 starts first)
+  size_t cherry_rows_cap = 0;
+  int cherry_rows_max = 0;                // most code pairs of any cherry
   uint8_t* d_cherry = nullptr;
   size_t cherry3_cap = 0, cherry_tips_cap = 0, cherry_cap = 0;
   bool cherry_codes_valid = false;
@@ -997,7 +1000,8 @@ int plk_destroy(plk_handle h) {
                   h->V, h->Vinv, h->lambda, h->weights, h->rates, h->probs, h->pi, h->site_lnl,
                   h->d_ops, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
-                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre, h->d_sbctr};
+                  h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre, h->d_sbctr,
+                  h->d_cherry_rows};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) (void)(h->h_req_vram ? hipFree(h->h_req) : hipHostFree(h->h_req));
@@ -1483,22 +1487,47 @@ int build_cherry_tables(plk_handle h) {
     cherry_codes_kernel<<<dim3((unsigned)((h->n_pad + 255) / 256), (unsigned)nch), 256, 0, h->stream>>>(
         h->codes, h->n_pad, h->d_cherry_tips, U, lay, h->d_cherry);
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipStreamSynchronize(h->stream));  // `tips` goes out of scope
+    // the code pairs each cherry meets: marked on the device, listed here (once per set of
+    // tip codes / program)
+    const size_t U2 = (size_t)U * U;
+    uint8_t* d_mark = nullptr;
+    HIPCHK(h, hipMallocAsync((void**)&d_mark, (size_t)nch * U2, h->stream));
+    HIPCHK(h, hipMemsetAsync(d_mark, 0, (size_t)nch * U2, h->stream));
+    cherry_mark_kernel<<<dim3((unsigned)((h->n_pad + 255) / 256), (unsigned)nch), 256, 0, h->stream>>>(
+        h->n_pad, U, lay, h->d_cherry, d_mark);
+    HIPCHK(h, hipGetLastError());
+    std::vector<uint8_t> mark((size_t)nch * U2);
+    HIPCHK(h, hipMemcpyAsync(mark.data(), d_mark, mark.size(), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipFreeAsync(d_mark, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));  // `tips` goes out of scope, `mark` is read
+    std::vector<int32_t> rl((size_t)nch + 1, 0);
+    h->cherry_rows_max = 0;
+    for (int k = 0; k < nch; ++k) {
+      for (size_t r = 0; r < U2; ++r)
+        if (mark[(size_t)k * U2 + r]) rl.push_back((int32_t)r);
+      rl[(size_t)k + 1] = (int32_t)(rl.size() - (size_t)nch - 1);
+      h->cherry_rows_max = std::max(h->cherry_rows_max, rl[(size_t)k + 1] - rl[(size_t)k]);
+    }
+    rc = ensure_cap(h, (void**)&h->d_cherry_rows, &h->cherry_rows_cap, rl.size() * sizeof(int32_t));
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpy(h->d_cherry_rows, rl.data(), rl.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     h->cherry_codes_valid = true;
   }
   // rows per workgroup: 64-row passes sharing one P^T staging
   constexpr int rows = 256;
-  const dim3 grid((unsigned)((U * U + rows - 1) / rows), (unsigned)(nch * C));
+  const dim3 grid((unsigned)((std::max(h->cherry_rows_max, 1) + rows - 1) / rows), (unsigned)(nch * C));
+  const int32_t* rs = h->d_cherry_rows;
+  const int32_t* rlist = h->d_cherry_rows + nch + 1;
   const bool sc = (h->flags & PLK_FLAG_SCALING) != 0;
   if (S == 20) {
-    if (sc) cherry_table_kernel<20, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
-    else cherry_table_kernel<20, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
+    if (sc) cherry_table_kernel<20, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows, rs, rlist);
+    else cherry_table_kernel<20, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows, rs, rlist);
   } else if (S == 4) {
-    if (sc) cherry_table_kernel<4, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
-    else cherry_table_kernel<4, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
+    if (sc) cherry_table_kernel<4, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows, rs, rlist);
+    else cherry_table_kernel<4, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows, rs, rlist);
   } else if (S == 64) {
-    if (sc) cherry_table_kernel<64, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
-    else cherry_table_kernel<64, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows);
+    if (sc) cherry_table_kernel<64, true><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows, rs, rlist);
+    else cherry_table_kernel<64, false><<<grid, 256, 0, h->stream>>>(h->tipP, h->pmatsT, h->d_cherry3, C, U, lay, h->d_cherry, rows, rs, rlist);
   } else {
     return fail(h, PLK_ERR_UNSUPPORTED, "cherry tables for %d states", S);
   }

@@ -109,15 +109,28 @@ __global__ __launch_bounds__(256) void cherry_codes_kernel(const uint8_t* __rest
   out[i] = (uint16_t)(ca * U + cb);
 }
 
+// mark[k][ca * U + cb] = 1 for every code pair cherry k = blockIdx.y meets (padding included)
+__global__ __launch_bounds__(256) void cherry_mark_kernel(int64_t n_pad, int U, CherryLayout lay,
+                                                          const uint8_t* __restrict__ cherry, uint8_t* __restrict__ mark) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pad) return;
+  const int k = blockIdx.y;
+  const uint16_t* cc = reinterpret_cast<const uint16_t*>(cherry + (size_t)k * lay.stride + lay.table_bytes + lay.count_bytes);
+  mark[(size_t)k * U * U + cc[i]] = 1;
+}
+
 // Four waves per block, one per 16 code pairs (rows) of one cherry and class: blockIdx.x =
 // 64-row block, blockIdx.y = cherry * C + class; P^T of the cherry branch is staged in LDS.
-// cherry3[3k .. 3k+2] = tip a, tip b, cherry node.
+// cherry3[3k .. 3k+2] = tip a, tip b, cherry node.  Only the code pairs the cherry's tips
+// meet are formed (row_list[row_start[k] ..], row_start[k + 1]): the traversal reads no other
+// row (cfg4: ~1/3 of the 61^2 codon pairs occur under the model).
 template <int S, bool SCALE>
 __global__ __launch_bounds__(256) void cherry_table_kernel(const double* __restrict__ tipP,
                                                            const double* __restrict__ pmatsT,
                                                            const int32_t* __restrict__ cherry3, int C, int U,
                                                            CherryLayout lay, uint8_t* __restrict__ cherry,
-                                                           int rows_per_wg) {
+                                                           int rows_per_wg, const int32_t* __restrict__ row_start,
+                                                           const int32_t* __restrict__ row_list) {
   constexpr int XT = MShape<S>::XT;
   __shared__ double PTl[S * S];
   const int lane = threadIdx.x & 63, lr = lane >> 4, lc = lane & 15;
@@ -128,9 +141,11 @@ __global__ __launch_bounds__(256) void cherry_table_kernel(const double* __restr
     __syncthreads();
   }
   // each workgroup stages P^T once and covers rows_per_wg code pairs, 64 per pass
-  for (int r0 = blockIdx.x * rows_per_wg; r0 < min(U2, (int)(blockIdx.x + 1) * rows_per_wg); r0 += 64) {
-  const int r = r0 + (threadIdx.x >> 6) * 16 + lc;  // this lane's row (code pair)
-  const bool rv = r < U2;
+  const int rs = row_start[k], nr = row_start[k + 1] - rs;
+  for (int r0 = blockIdx.x * rows_per_wg; r0 < min(nr, (int)(blockIdx.x + 1) * rows_per_wg); r0 += 64) {
+  const int pos = r0 + (threadIdx.x >> 6) * 16 + lc;  // this lane's entry of the row list
+  const bool rv = pos < nr;
+  const int r = rv ? row_list[rs + pos] : 0;  // its row (code pair)
   const int ca = rv ? r / U : 0, cb = rv ? r % U : 0;
   const int ta = cherry3[3 * k], tb = cherry3[3 * k + 1], node = cherry3[3 * k + 2];
   // the cherry's partial for every class (the joint check needs all of them), own class kept

@@ -8,4 +8,4 @@ export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/t -o run -- \
   python3 $R/bench.py --config yn98_codon_50k_128 --no-cpu-baseline --no-strong --steps 6 > $O/b.json 2> $O/b.err || { tail -5 $O/b.err; exit 1; }
-python3 $R/tools/trace_summary.py $O/t/run_kernel_trace.csv 14 && rm -rf $O/t
+python3 $R/tools/trace_summary.py $O/t/run_kernel_trace.csv 16 && rm -rf $O/t

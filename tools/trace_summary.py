@@ -4,7 +4,7 @@ import csv
 import sys
 
 path, n = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 12
-rows = [r for r in csv.DictReader(open(path)) if r["Kernel_Name"].startswith(("plk", "__amd"))]
+rows = [r for r in csv.DictReader(open(path)) if "plk" in r["Kernel_Name"] or r["Kernel_Name"].startswith("__amd")]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 tail = rows[-n:]
 t0, prev = int(tail[0]["Start_Timestamp"]), None
