@@ -1513,8 +1513,9 @@ int build_cherry_tables(plk_handle h) {
     HIPCHK(h, hipMemcpy(h->d_cherry_rows, rl.data(), rl.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     h->cherry_codes_valid = true;
   }
-  // rows per workgroup: 64-row passes sharing one P^T staging
-  constexpr int rows = 256;
+  // rows per workgroup (64-row passes sharing one P^T staging): one pass (cfg3 tables
+  // 35 us vs 40 at four passes, cfg4 36 vs 38; profiles/r04/ab_runs.md)
+  constexpr int rows = 64;
   const dim3 grid((unsigned)((std::max(h->cherry_rows_max, 1) + rows - 1) / rows), (unsigned)(nch * C));
   const int32_t* rs = h->d_cherry_rows;
   const int32_t* rlist = h->d_cherry_rows + nch + 1;
