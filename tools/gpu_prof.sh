@@ -10,7 +10,7 @@ O=$R/gpurun_out/prof/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 cd /tmp
-B="$R/bench.py --config $CFG --mode $MODE --no-cpu-baseline"
+B="$R/bench.py --config $CFG --mode $MODE --no-cpu-baseline --no-strong"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
   python3 $B --steps $STEPS --warmup 2 > $O/bench.json 2> $O/trace.err || { tail -5 $O/trace.err; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- \
