@@ -90,7 +90,6 @@ class AbstractPlkTreeLikelihood : public virtual TreeLikelihood {
   // per engine node: dP / d2P older than P (evaluations upload P only; the derivative
   // calls bring them up to date first)
   mutable std::vector<char> derivStale_;
-  bool hostP_ = false;       // some branch P(t) came from the host (Taylor branch)
   size_t maxSons_ = 0;
   bool derivFirst_ = true, derivSecond_ = true;
   unsigned extraFlags_ = 0;                  // plk_create flags of the subclass (PLK_FLAG_DOUBLE_RECURSIVE)
@@ -133,6 +132,7 @@ class AbstractPlkTreeLikelihood : public virtual TreeLikelihood {
   virtual int modelIndexForNode(const Node*) const { return 0; }
   // the model behind engine model index m (host P(t) for a model whose eigen-system failed)
   virtual const SubstitutionModel* modelForIndex(int m) const = 0;
+  bool hostPInUse() const;  // a branch's model has no device P(t) (Taylor branch of getPij_t)
   void uploadEigen(int modelIndex, const SubstitutionModel& model);
   void uploadRates();
   void computeTreeLikelihood(const std::vector<const Node*>* changed = nullptr);

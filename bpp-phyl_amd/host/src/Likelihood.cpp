@@ -313,7 +313,6 @@ void AbstractPlkTreeLikelihood::updatePmatrices(const std::vector<const Node*>& 
     for (size_t i = 0; i < br.size(); i++) {
       const SubstitutionModel* m = modelForIndex(mod[i]);
       if (m && m->needsHostPij()) {
-        hostP_ = true;
         for (size_t c = 0; c < nbClasses_; c++) {
           const RowMatrix<double>& Pc = m->getPij_t(t[i] * rates[c]);
           std::copy(Pc.data(), Pc.data() + nbStates_ * nbStates_, P.begin() + c * nbStates_ * nbStates_);
@@ -369,7 +368,6 @@ void AbstractPlkTreeLikelihood::evaluateTree(const std::vector<const Node*>& pno
       const int e = engineOf(n), mi = modelIndexForNode(n);
       const SubstitutionModel* m = modelForIndex(mi);
       if (m && m->needsHostPij()) {
-        hostP_ = true;
         for (size_t c = 0; c < nbClasses_; c++) {
           const RowMatrix<double>& Pc = m->getPij_t(n->getDistanceToFather() * rates[c]);
           std::copy(Pc.data(), Pc.data() + nbStates_ * nbStates_, P.begin() + c * nbStates_ * nbStates_);
@@ -536,8 +534,19 @@ VVVdouble AbstractPlkTreeLikelihood::getLikelihoodArray(int nodeId) const {
 // dL / d2L propagation of Likelihood/RHomogeneousTreeLikelihood.cpp:346-541, 596-791)
 // for every model; central differences of the device log-likelihood only if the
 // engine reports PLK_ERR_UNSUPPORTED (per-subtree pattern compression).
+// some branch's model currently has no device P(t) (its eigen-system failed its check:
+// host Taylor P(t), no dP / d2P on the device); asked per derivative, so a model that
+// recovers a valid eigen-system gets analytic derivatives back
+bool AbstractPlkTreeLikelihood::hostPInUse() const {
+  for (const Node* n : nodes_) {
+    const SubstitutionModel* m = modelForIndex(modelIndexForNode(n));
+    if (m && m->needsHostPij()) return true;
+  }
+  return false;
+}
+
 bool AbstractPlkTreeLikelihood::analyticDerivatives(const std::string& variable, double* d1, double* d2) const {
-  if (!(derivFirst_ || derivSecond_) || hostP_) return false;
+  if (!(derivFirst_ || derivSecond_) || hostPInUse()) return false;
   if (variable.size() <= 5 || variable.find_first_not_of("0123456789", 5) != std::string::npos)
     throw Exception("analyticDerivatives: not a branch-length parameter: " + variable);
   const Node* n = nodes_.at(TextTools::to<size_t>(variable.substr(5)));
@@ -848,7 +857,7 @@ std::vector<const Node*> RNonHomogeneousTreeLikelihood::applyBranchLengths() {
 bool RNonHomogeneousTreeLikelihood::analyticDerivatives(const std::string& variable, double* d1, double* d2) const {
   if (!reparametrizeRoot_ || (variable != "BrLenRoot" && variable != "RootPosition"))
     return AbstractPlkTreeLikelihood::analyticDerivatives(variable, d1, d2);
-  if (!(derivFirst_ || derivSecond_) || hostP_) return false;
+  if (!(derivFirst_ || derivSecond_) || hostPInUse()) return false;
   const double len = parameters_.getParameterValue("BrLenRoot");
   const double pos = parameters_.getParameterValue("RootPosition");
   const double alpha = variable == "BrLenRoot" ? pos : len;
