@@ -10,7 +10,7 @@ O=$R/gpurun_out/stalls/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 cd /tmp
-B="$R/bench.py --config $CFG --mode $MODE --no-cpu-baseline --steps 2 --warmup 1"
+B="$R/bench.py --config $CFG --mode $MODE --no-cpu-baseline --no-strong --steps 2 --warmup 1"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
   SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM --output-format csv -d $O/a -o run -- \
   python3 $B > /dev/null 2> $O/a.err || { tail -5 $O/a.err; exit 1; }
