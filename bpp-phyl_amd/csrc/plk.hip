@@ -1974,7 +1974,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // wave sum must wait for the store and the counter's atomic round trip (~3 us) before
     // its workgroup's next super-block barrier, in every super-block.  Off; the formal
     // release/acquire form (an L2 write-back per wave) was slower still (round 1)
-    if (sh.lds_bytes() > 160 * 1024)
+    if (sh.lds_bytes() > 160 * 1024 - 64)  // (less the kernel's static LDS word)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
     if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW ||
         sh.pin != h->jit_shape.pin ||
