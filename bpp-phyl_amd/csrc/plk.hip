@@ -159,6 +159,7 @@ struct plk_handle_s {
   char* h_req_dev = nullptr;   // device address of the staging
   size_t h_req_cap = 0;
   bool h_req_vram = false;     // staging in host-written fine-grained device memory (else pinned host)
+  std::vector<int32_t> req_shadow;  // branch + model arrays now in the staging (skip rewriting them)
   bool req_vram_failed = false;
   bool in_eval = false;        // inside plk_evaluate: the request's reader is waited for by its stream_wait
   bool req_unrecorded = false; // a staged request's reader has no req_done record (plk_evaluate)
@@ -344,6 +345,7 @@ int ensure_cap(plk_handle h, void** p, size_t* cap, size_t bytes) {
 // written by the host reads back through the device, otherwise mapped pinned host memory.
 int req_staging(plk_handle h, size_t bytes) {
   if (h->h_req_cap >= bytes) return PLK_OK;
+  h->req_shadow.clear();
   if (h->h_req) HIPCHK(h, h->h_req_vram ? hipFree(h->h_req) : hipHostFree(h->h_req));
   h->h_req = nullptr;
   h->h_req_dev = nullptr;
@@ -1270,8 +1272,20 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     if (rc) return rc;
     char* staging = h->h_req;
     std::memcpy(staging + off_t, t, n * sizeof(double));
-    std::memcpy(staging + off_b, branch, n * sizeof(int32_t));
-    if (model) std::memcpy(staging + off_m, model, n * sizeof(int32_t));
+    // an optimiser's evaluations repeat the branch and model arrays: those stores (over the
+    // BAR for a device-memory staging) are skipped when the staging already holds them
+    // (shadow: n, model given, then the arrays as written)
+    const size_t nb = 2 + (size_t)n * (model ? 2 : 1);
+    const bool same = h->req_shadow.size() == nb && h->req_shadow[0] == n && h->req_shadow[1] == (model ? 1 : 0) &&
+                      std::memcmp(h->req_shadow.data() + 2, branch, n * sizeof(int32_t)) == 0 &&
+                      (!model || std::memcmp(h->req_shadow.data() + 2 + n, model, n * sizeof(int32_t)) == 0);
+    if (!same) {
+      std::memcpy(staging + off_b, branch, n * sizeof(int32_t));
+      if (model) std::memcpy(staging + off_m, model, n * sizeof(int32_t));
+      h->req_shadow.assign({n, model ? 1 : 0});
+      h->req_shadow.insert(h->req_shadow.end(), branch, branch + n);
+      if (model) h->req_shadow.insert(h->req_shadow.end(), model, model + n);
+    }
     // the host's stores reach the staging before the launch's doorbell (a device-memory
     // staging is write-combined over the BAR)
     std::atomic_thread_fence(std::memory_order_seq_cst);
