@@ -4,6 +4,13 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# The tree-specialised kernels are compiled by hiprtc at their first use (a 256-taxon protein
+# tree: ~45 s).  The tests share one disk cache inside the repository (`.jit_cache`,
+# git-ignored; filled by a GPU run of the suite and travelling with the tree): an entry is
+# used only when its stored source equals the generated one and its code object's hash
+# checks out, otherwise it is recompiled (csrc/plk.hip jit_compile).  An explicit
+# PLK_JIT_CACHE (a directory, or 0 for none) wins.
+os.environ.setdefault("PLK_JIT_CACHE", os.path.join(ROOT, ".jit_cache"))
 for sub in ("bpp-phyl_amd", "oracle"):
     p = os.path.join(ROOT, sub)
     if p not in sys.path:
