@@ -38,6 +38,9 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# the tree-specialised kernels compile at setup (not timed); the repository's code-object
+# cache (`.jit_cache`, filled by the test suite) spares the compile when it holds them
+os.environ.setdefault("PLK_JIT_CACHE", os.path.join(ROOT, ".jit_cache"))
 sys.path.insert(0, os.path.join(ROOT, "bpp-phyl_amd"))
 
 import phylo  # noqa: E402
