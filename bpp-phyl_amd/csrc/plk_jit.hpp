@@ -562,6 +562,50 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     }
     s += st + br + "};\n";
   }
+  // Fragments of one shape share their code (a balanced tree's eight 64-tip subtrees: one
+  // case instead of eight -- 8x less generated code to compile and to fetch).  The code
+  // differs between such fragments only in the P(t) offsets of their branches and the slots
+  // they load and store; those become a per-fragment base (kFragNB: node, kFragSB: slot) plus
+  // the shared relative offset.  Shape = the event list with node / slot fields relative to
+  // the bases, and the table units' layout (tips and cherry branches are runtime data).
+  std::vector<int> nbase(events.size(), 0), sbase(events.size(), 0), leader(events.size(), -1);
+  {
+    std::vector<std::string> sig(events.size());
+    for (size_t f = 0; f < events.size(); ++f) {
+      int nb = 1 << 30, sb = 1 << 30;
+      for (const JitEvent& e : events[f]) {
+        if ((e.op == T_LOAD || e.op == T_ASCEND) && e.b >= 0) nb = std::min(nb, e.b);
+        if ((e.op == T_LOAD || e.op == T_ASCEND || e.op == T_ROOT) && e.a >= 0) sb = std::min(sb, e.a);
+      }
+      nbase[f] = nb == (1 << 30) ? 0 : nb;
+      sbase[f] = sb == (1 << 30) ? 0 : sb;
+      std::string& g = sig[f];
+      for (const JitEvent& e : events[f]) {
+        const bool node = (e.op == T_LOAD || e.op == T_ASCEND) && e.b >= 0;
+        const bool slt = (e.op == T_LOAD || e.op == T_ASCEND || e.op == T_ROOT) && e.a >= 0;
+        snprintf(buf, sizeof(buf), "%d,%d,%d,%d;", e.op, e.level,
+                 slt ? e.a - sbase[f] : (e.op == T_TIP ? e.a : -1),
+                 node ? e.b - nbase[f] : (e.op == T_ROOT ? e.b : -1));
+        g += buf;
+      }
+      g += "|";
+      for (const JitUnit& u : plan.units[f]) {
+        snprintf(buf, sizeof(buf), "%d,%d,%d,%d;", u.tb < 0 ? 0 : 1, u.br >= 0 ? 1 : 0, u.off, u.koff);
+        g += buf;
+      }
+      for (size_t q = 0; q < f && leader[f] < 0; ++q)
+        if (leader[q] == (int)q && sig[q] == g) leader[f] = (int)q;
+      if (leader[f] < 0) leader[f] = (int)f;
+    }
+    std::string nbs = "\n__device__ const int kFragNB[] = {0", sbs = "};\n__device__ const int kFragSB[] = {0";
+    for (size_t f = 0; f < events.size(); ++f) {
+      snprintf(buf, sizeof(buf), ",%d", nbase[f]);
+      nbs += buf;
+      snprintf(buf, sizeof(buf), ",%d", sbase[f]);
+      sbs += buf;
+    }
+    s += nbs + sbs + "};\n";
+  }
   s += "\n__device__ const int kFragUnitStart[] = {0";
   {
     int acc = 0, nsc = 0, not_ = 0;
@@ -804,6 +848,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   }
   s += "    switch (frag) {\n";
   for (size_t f = 0; f < events.size(); ++f) {
+    if (leader[f] != (int)f) continue;
     const std::vector<JitEvent>& ev = events[f];
     std::vector<int> slot(ev.size(), -1), fetchers;
     for (size_t i = 0; i < ev.size(); ++i)
@@ -811,9 +856,12 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         slot[i] = (int)(fetchers.size() % (size_t)(L + 1));
         fetchers.push_back((int)i);
       }
-    auto pref = [&](size_t i) -> std::string {  // P operand of event i
-      snprintf(buf, sizeof(buf), "pm + %lld", (long long)ev[i].b * C * 16);
+    auto pref = [&](size_t i) -> std::string {  // P operand of event i (relative to the node base)
+      snprintf(buf, sizeof(buf), "pmf_ + %lld", (long long)(ev[i].b - nbase[f]) * C * 16);
       return buf;
+    };
+    auto sref = [&](int a) -> std::string {  // a slot (relative to the slot base)
+      return "sb_ + " + std::to_string(a - sbase[f]);
     };
     // Two-stage operand pipeline (L >= 2): a tip's code is read L fetchers ahead (and a
     // materialised child partial is loaded from HBM L ahead), its table row one ahead, so
@@ -823,7 +871,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       if (e.op == T_TIP)
         snprintf(buf, sizeof(buf), "      CODEF(Q%d, %d)\n", slot[(size_t)i], e.a);
       else
-        snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %d)\n", slot[(size_t)i], slot[(size_t)i], e.a);
+        snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %s)\n", slot[(size_t)i], slot[(size_t)i], sref(e.a).c_str());
       s += buf;
     };
     auto unit_args = [&](const JitEvent& e) -> std::string {  // TB, OFF, R of a unit
@@ -844,7 +892,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         snprintf(buf, sizeof(buf), "      TIPF(F%d, Q%d, %d, %s)\n", slot[(size_t)i], slot[(size_t)i], e.a,
                  unit_args(e).c_str());
       else
-        snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %d)\n", slot[(size_t)i], slot[(size_t)i], e.a);
+        snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %s)\n", slot[(size_t)i], slot[(size_t)i], sref(e.a).c_str());
       s += buf;
     };
     // One pass over the fragment.  exact: the per-node joint rescale of the other
@@ -942,7 +990,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
           if (e.b >= 0) {
             if (sh.scale) check_line(dd);
             if (e.a >= 0) {
-              snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %d, toff, p, c0, A%d, K%d, gv);\n", e.a, dd, dd);
+              snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %s, toff, p, c0, A%d, K%d, gv);\n",
+                       sref(e.a).c_str(), dd, dd);
               s += buf;
             }
           }
@@ -961,15 +1010,21 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         } else {  // T_ROOT
           if (sh.scale) check_line(0);
           if (e.a >= 0) {
-            snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %d, toff, p, c0, A0, K0, gv);\n", e.a);
+            snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %s, toff, p, c0, A0, K0, gv);\n",
+                     sref(e.a).c_str());
             s += buf;
           }
           if (e.b) s += "      reduce_root<C_, CW_, PW_, NWT_, SC_>(a, A0, K0, xch, w, g, c0, p0, p, gv);\n";
         }
       }
     };
-    snprintf(buf, sizeof(buf), "    case %zu: {\n", f);
-    s += buf;
+    for (size_t q = f; q < events.size(); ++q)
+      if (leader[q] == (int)f) {
+        snprintf(buf, sizeof(buf), "    case %zu:\n", q);
+        s += buf;
+      }
+    s += "    {\n      const CPd pmf_ = pm + (i64)kFragNB[frag + 1] * (C_ * 16);\n"
+         "      const int sb_ = __builtin_amdgcn_readfirstlane(kFragSB[frag + 1]); (void)pmf_; (void)sb_;\n";
     emit_body(true);
     s += "    } break;\n";
   }
