@@ -136,6 +136,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   std::string s;
   s.reserve(65536 * std::max<size_t>(starts.size(), 1));
   s += kJitMPrelude;
+  const size_t pre_pos = s.size();  // per-fragment base tables go here (global scope)
+  std::string pre_;
   char buf[512];
   const int NTH = 64 * sh.G, PB = sh.pb(), PF = (PB + NTH - 1) / NTH;
   snprintf(buf, sizeof(buf),
@@ -294,13 +296,66 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     snprintf(buf, sizeof(buf), "  int QC%d = 0; (void)QC%d;\n", q, q);
     s += buf;
   }
+  // Fragments of one shape share one case (a balanced tree's subtrees): per fragment a node
+  // base (P(t) of its branches), a slot base (loads / stores), a tip base and a cherry base,
+  // and the shared code's offsets relative to them (plk_jit.hpp does the same).
+  const size_t NFR = starts.size();
+  std::vector<int> nbase(NFR, 0), sbase(NFR, 0), tbase(NFR, 0), kbase(NFR, 0), leader(NFR, -1);
+  {
+    std::vector<std::string> sig(NFR);
+    for (size_t f = 0; f < NFR; ++f) {
+      int nb = 1 << 30, sb = 1 << 30, tb = 1 << 30, kb = 1 << 30;
+      for (size_t i = (size_t)starts[f];; ++i) {
+        const TInstr& e = prog[i];
+        if ((e.op == T_LOAD || e.op == T_ASCEND) && e.b >= 0) nb = std::min(nb, (int)e.b);
+        if ((e.op == T_LOAD || e.op == T_ASCEND || e.op == T_ROOT) && e.a >= 0) sb = std::min(sb, (int)e.a);
+        if (e.op == T_TIP) tb = std::min(tb, (int)e.a);
+        if (e.op == T_CHERRY) kb = std::min(kb, (int)e.a);
+        if (e.op == T_ROOT) break;
+      }
+      nbase[f] = nb == (1 << 30) ? 0 : nb;
+      sbase[f] = sb == (1 << 30) ? 0 : sb;
+      tbase[f] = tb == (1 << 30) ? 0 : tb;
+      kbase[f] = kb == (1 << 30) ? 0 : kb;
+      std::string& g = sig[f];
+      for (size_t i = (size_t)starts[f];; ++i) {
+        const TInstr& e = prog[i];
+        int ra = -1, rb = -1;
+        if (e.op == T_TIP) ra = e.a - tbase[f];
+        if (e.op == T_CHERRY) ra = e.a - kbase[f];
+        if ((e.op == T_LOAD || e.op == T_ASCEND || e.op == T_ROOT) && e.a >= 0) ra = e.a - sbase[f];
+        if ((e.op == T_LOAD || e.op == T_ASCEND) && e.b >= 0) rb = e.b - nbase[f];
+        if (e.op == T_ROOT) rb = e.b;
+        snprintf(buf, sizeof(buf), "%d,%d,%d;", (int)e.op, ra, rb);
+        g += buf;
+        if (e.op == T_ROOT) break;
+      }
+      for (size_t q = 0; q < f && leader[f] < 0; ++q)
+        if (leader[q] == (int)q && sig[q] == g) leader[f] = (int)q;
+      if (leader[f] < 0) leader[f] = (int)f;
+    }
+    const char* names[4] = {"kFragNB", "kFragSB", "kFragTB", "kFragKB"};
+    const std::vector<int>* vals[4] = {&nbase, &sbase, &tbase, &kbase};
+    for (int t = 0; t < 4; ++t) {
+      std::string arr = std::string("__device__ const int ") + names[t] + "[] = {0";
+      for (size_t f = 0; f < NFR; ++f) {
+        snprintf(buf, sizeof(buf), ",%d", (*vals[t])[f]);
+        arr += buf;
+      }
+      pre_ += arr + "};\n";
+    }
+  }
   s += "  switch (frag) {\n";
   for (size_t f = 0; f < starts.size(); ++f) {
+    if (leader[f] != (int)f) continue;
     std::vector<TInstr> ev;
     for (size_t i = (size_t)starts[f];; ++i) {
       ev.push_back(prog[i]);
       if (prog[i].op == T_ROOT) break;
     }
+    auto rel = [&](const char* base, int v, int b0) -> std::string {
+      return std::string(base) + " + " + std::to_string(v - b0);
+    };
     // operand fetchers (ring slots) and the P chain (events that contract through a branch)
     std::vector<int> slot(ev.size(), -1), fetchers, pchain;
     for (size_t i = 0; i < ev.size(); ++i) {
@@ -317,9 +372,9 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
       const TInstr& e = ev[(size_t)fetchers[m]];
       const int q = (int)(m % (size_t)NQ);
       if (e.op == T_CHERRY)
-        snprintf(buf, sizeof(buf), "    CHERRY_CODE(QC%d, %d)\n", q, e.a);
+        snprintf(buf, sizeof(buf), "    CHERRY_CODE(QC%d, %s)\n", q, rel("kb_", e.a, kbase[f]).c_str());
       else if (e.op == T_TIP)
-        snprintf(buf, sizeof(buf), "    TIP_CODE(QC%d, %d)\n", q, e.a);
+        snprintf(buf, sizeof(buf), "    TIP_CODE(QC%d, %s)\n", q, rel("tb_", e.a, tbase[f]).c_str());
       else
         return;
       s += buf;
@@ -329,26 +384,33 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
       const TInstr& e = ev[(size_t)fetchers[m]];
       const int sl = slot[(size_t)fetchers[m]], q = (int)(m % (size_t)NQ);
       if (e.op == T_CHERRY)
-        snprintf(buf, sizeof(buf), "    CHERRY_ROW(F%d, FK%d, %d, QC%d)\n", sl, sl, e.a, q);
+        snprintf(buf, sizeof(buf), "    CHERRY_ROW(F%d, FK%d, %s, QC%d)\n", sl, sl, rel("kb_", e.a, kbase[f]).c_str(), q);
       else if (e.op == T_TIP)
-        snprintf(buf, sizeof(buf), "    TIP_ROW(F%d, %d, QC%d)\n", sl, e.a, q);
+        snprintf(buf, sizeof(buf), "    TIP_ROW(F%d, %s, QC%d)\n", sl, rel("tb_", e.a, tbase[f]).c_str(), q);
       else
-        snprintf(buf, sizeof(buf), "    LOAD_FETCH(F%d, FK%d, %d)\n", sl, sl, e.a);
+        snprintf(buf, sizeof(buf), "    LOAD_FETCH(F%d, FK%d, %s)\n", sl, sl, rel("sb_", e.a, sbase[f]).c_str());
       s += buf;
     };
     auto emit_fetch = [&](int i) {
       const TInstr& e = ev[(size_t)i];
       const int sl = slot[(size_t)i];
       if (e.op == T_CHERRY)
-        snprintf(buf, sizeof(buf), "    CHERRY_FETCH(F%d, FK%d, %d)\n", sl, sl, e.a);
+        snprintf(buf, sizeof(buf), "    CHERRY_FETCH(F%d, FK%d, %s)\n", sl, sl, rel("kb_", e.a, kbase[f]).c_str());
       else if (e.op == T_TIP)
-        snprintf(buf, sizeof(buf), "    TIP_FETCH(F%d, %d)\n", sl, e.a);
+        snprintf(buf, sizeof(buf), "    TIP_FETCH(F%d, %s)\n", sl, rel("tb_", e.a, tbase[f]).c_str());
       else
-        snprintf(buf, sizeof(buf), "    LOAD_FETCH(F%d, FK%d, %d)\n", sl, sl, e.a);
+        snprintf(buf, sizeof(buf), "    LOAD_FETCH(F%d, FK%d, %s)\n", sl, sl, rel("sb_", e.a, sbase[f]).c_str());
       s += buf;
     };
-    snprintf(buf, sizeof(buf), "  case %zu: {\n", f);
-    s += buf;
+    for (size_t q = f; q < NFR; ++q)
+      if (leader[q] == (int)f) {
+        snprintf(buf, sizeof(buf), "  case %zu:\n", q);
+        s += buf;
+      }
+    s += "  {\n    const int nb_ = __builtin_amdgcn_readfirstlane(kFragNB[frag + 1]), sb_ = "
+         "__builtin_amdgcn_readfirstlane(kFragSB[frag + 1]);\n    const int tb_ = "
+         "__builtin_amdgcn_readfirstlane(kFragTB[frag + 1]), kb_ = __builtin_amdgcn_readfirstlane(kFragKB[frag + 1]);\n"
+         "    (void)nb_; (void)sb_; (void)tb_; (void)kb_;\n";
     size_t nf = 0;
     if (LC) {
       for (size_t m = 0; m < (size_t)LC; ++m) emit_code(m);
@@ -365,7 +427,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     const char* bar = " __syncthreads();";
     auto pload = [&](size_t j) {
       if (j < pchain.size()) {
-        snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R%zu, %d)\n", j % (size_t)PD, ev[(size_t)pchain[j]].b);
+        snprintf(buf, sizeof(buf), "    PSTAGE_LOAD(R%zu, %s)\n", j % (size_t)PD,
+                 rel("nb_", ev[(size_t)pchain[j]].b, nbase[f]).c_str());
         s += buf;
       }
     };
@@ -429,7 +492,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
           s += buf;
         }
         if (e.a >= 0) {
-          snprintf(buf, sizeof(buf), "    STORE(A%d, K%d, %d)\n", d, d, e.a);
+          snprintf(buf, sizeof(buf), "    STORE(A%d, K%d, %s)\n", d, d, rel("sb_", e.a, sbase[f]).c_str());
           s += buf;
         }
         snprintf(buf, sizeof(buf), "    CONTRIB(A%d, A%d, %d, %s)\n", d - 1, d, cur, fresh[(size_t)d - 1] ? "true" : "false");
@@ -445,7 +508,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
       } else {  // T_ROOT
         if (sh.scale) s += "    RESCALE(A0, K0)\n";
         if (e.a >= 0) {
-          snprintf(buf, sizeof(buf), "    STORE(A0, K0, %d)\n", e.a);
+          snprintf(buf, sizeof(buf), "    STORE(A0, K0, %s)\n", rel("sb_", e.a, sbase[f]).c_str());
           s += buf;
         }
         if (e.b) s += "    REDUCE_ROOT(A0, K0)\n";
@@ -454,6 +517,7 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
     s += "  } break;\n";
   }
   s += "  default: break;\n  }\n}\n";
+  s.insert(pre_pos, pre_);
   return s;
 }
 
