@@ -18,7 +18,6 @@
 #include <hip/hiprtc.h>
 #include <rccl/rccl.h>
 
-#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -158,9 +157,7 @@ struct plk_handle_s {
   char* h_req = nullptr;
   char* h_req_dev = nullptr;   // device address of the staging
   size_t h_req_cap = 0;
-  bool h_req_vram = false;     // staging in host-written fine-grained device memory (else pinned host)
   std::vector<int32_t> req_shadow;  // branch + model arrays now in the staging (skip rewriting them)
-  bool req_vram_failed = false;
   bool in_eval = false;        // inside plk_evaluate: the request's reader is waited for by its stream_wait
   bool req_unrecorded = false; // a staged request's reader has no req_done record (plk_evaluate)
   hipEvent_t req_done = nullptr;
@@ -338,45 +335,20 @@ int ensure_cap(plk_handle h, void** p, size_t* cap, size_t bytes) {
   return PLK_OK;
 }
 
-// Staging of large P(t) requests (plk_update_pmatrices).  Fine-grained device memory that the
-// host writes straight into over the PCIe BAR, so that the P(t) kernel reads its request from
-// HBM (cfg5, 1 022 branches: 3 us less per evaluation than reading pinned host memory over
-// PCIe); it is used only when the allocation is mapped in this process (mincore) and a pattern
-// written by the host reads back through the device, otherwise mapped pinned host memory.
+// Staging of large P(t) requests (plk_update_pmatrices): mapped pinned host memory the P(t)
+// kernel reads over PCIe.  (Round 4 measured device memory written by the host over the BAR,
+// 3 us less per cfg5 evaluation, and removed it: a freshly created handle whose staging
+// reused freed device memory had its P(t) kernel read other data than the host had written --
+// a whole shard of -inf in test_multi_device_handle_bitwise[lg08] after other tests in the
+// same process, with fine-grained and with uncached allocations alike; profiles/r04/ab_runs.md.)
 int req_staging(plk_handle h, size_t bytes) {
   if (h->h_req_cap >= bytes) return PLK_OK;
   h->req_shadow.clear();
-  if (h->h_req) HIPCHK(h, h->h_req_vram ? hipFree(h->h_req) : hipHostFree(h->h_req));
+  if (h->h_req) HIPCHK(h, hipHostFree(h->h_req));
   h->h_req = nullptr;
   h->h_req_dev = nullptr;
   h->h_req_cap = 0;
-  h->h_req_vram = false;
   bytes = (bytes + 4095) & ~(size_t)4095;
-  void* p = nullptr;
-  if (!h->req_vram_failed && hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) == hipSuccess) {
-    bool ok = false;
-    const long pg = sysconf(_SC_PAGESIZE);
-    const uintptr_t a0 = reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)(pg - 1);
-    std::vector<unsigned char> vec((bytes + (reinterpret_cast<uintptr_t>(p) - a0) + pg - 1) / pg);
-    if (mincore(reinterpret_cast<void*>(a0), bytes + (reinterpret_cast<uintptr_t>(p) - a0), vec.data()) == 0) {
-      std::vector<uint64_t> pat(bytes / 8), back(bytes / 8);
-      for (size_t i = 0; i < pat.size(); ++i) pat[i] = 0x9E3779B97F4A7C15ull * (i + 1);
-      std::memcpy(p, pat.data(), bytes);
-      std::atomic_thread_fence(std::memory_order_seq_cst);
-      ok = hipMemcpy(back.data(), p, bytes, hipMemcpyDeviceToHost) == hipSuccess &&
-           std::memcmp(back.data(), pat.data(), bytes) == 0;
-    }
-    if (ok) {
-      h->h_req = static_cast<char*>(p);
-      h->h_req_dev = h->h_req;
-      h->h_req_vram = true;
-      h->h_req_cap = bytes;
-      return PLK_OK;
-    }
-    hipFree(p);
-    hipGetLastError();
-    h->req_vram_failed = true;
-  }
   HIPCHK(h, hipHostMalloc((void**)&h->h_req, bytes, hipHostMallocMapped));
   HIPCHK(h, hipHostGetDevicePointer((void**)&h->h_req_dev, h->h_req, 0));
   h->h_req_cap = bytes;
@@ -1006,7 +978,7 @@ int plk_destroy(plk_handle h) {
                   h->d_cherry_rows};
   for (void* p : bufs)
     if (p) hipFree(p);
-  if (h->h_req) (void)(h->h_req_vram ? hipFree(h->h_req) : hipHostFree(h->h_req));
+  if (h->h_req) (void)hipHostFree(h->h_req);
   if (h->h_blocks) hipHostFree(h->h_blocks);
   if (h->req_done) hipEventDestroy(h->req_done);
   for (auto& e : h->events) {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # shape-shared jit_treeM fragments: tests (fresh cache), cfg3 line + compile time
 set -o pipefail
-export PLK_JIT_CACHE=$PWD/gpurun_out/jc_share3; rm -rf $PLK_JIT_CACHE; mkdir -p $PLK_JIT_CACHE
+export PLK_JIT_CACHE=$PWD/gpurun_out/jc_share3_$$; rm -rf $PLK_JIT_CACHE; mkdir -p $PLK_JIT_CACHE
 timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_multi.py -k "jitm or treeM or lg08 or jit_treeM or s20 or cherry" > gpurun_out/share3_tests.log 2>&1; rc=$?
 tail -2 gpurun_out/share3_tests.log; [ $rc -eq 0 ] || { grep -E "Error|error|FAIL" gpurun_out/share3_tests.log | head -20; exit $rc; }
 rm -rf $PLK_JIT_CACHE/*
