@@ -697,6 +697,32 @@ def test_jit_tree4_dynamic_superblocks_bitwise(C, n_taxa, n_patterns, scaling, m
     assert np.allclose(res["1"][0][1][sub], so, rtol=REL, atol=0)
 
 
+def test_jit_same_shape_fragments_share_code(tmp_path, monkeypatch):
+    """A balanced tree's 64-tip fragments have one shape: the generated kernel holds one code
+    block for all of them (plk_jit.hpp: per-fragment node / slot bases), and the result is
+    the oracle's at 1e-12 (the bitwise interpreter tests cover the other shapes)."""
+    monkeypatch.setenv("PLK_JIT_DUMP", str(tmp_path))
+    C, n = 4, 1500
+    tree = phylo.balanced_tree(256, seed=31, lo=0.05, hi=0.4)
+    et = phylo.engine_tree(tree, unroot=False)
+    rng = np.random.default_rng(256)
+    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
+    rates, probs = phylo.gamma_rates(C, 0.5)
+    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n, True, True, 3)
+    states = wl.simulate(0, n).astype(np.int32)
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
+    eng = engine_for(et, 4, C, n, states, phylo.DNA.init_table, rates, probs, m.pi, [m], flags=flags)
+    lnl, site, _ = run_engine(eng, et)
+    assert eng.kernel_path() == "jit_tree4"
+    srcs = [open(os.path.join(tmp_path, f)).read() for f in os.listdir(tmp_path) if f.endswith(".hip")]
+    src = [x for x in srcs if "plk_jit_tree4" in x and "kFragNB" in x][-1]
+    labels = len(__import__("re").findall(r"\n    case \d+:\n", src))
+    blocks = src.count("const CPd pmf_ = ")
+    assert 2 <= blocks < labels, (labels, blocks)   # the same-shape subtrees share a block; the top has its own
+    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m], scaling=True)
+    check(lnl, site, lo, so)
+
+
 def test_fused20_partials_equal_levelwise():
     et, m, alph, rates, probs, states = _random_problem(20, 4, 40, 500, seed=33)
     outs = []
