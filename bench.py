@@ -323,6 +323,12 @@ def launch_layout(args):
     return {"kind": "multi" if devices and len(devices) > 1 else "single", "world": 1, "devices": devices}
 
 
+def single_device(lay) -> int:
+    """The device of a one-GPU, one-process run: --gpus 1 --devices K runs on device K (never
+    silently device 0)."""
+    return lay["devices"][0] if lay["kind"] == "single" and lay["devices"] else 0
+
+
 def measure(args, lay, ctx, config, scaling, patterns=None, classes=None, mode="lnl", steps=None, warmup=None):
     """Set up one workload over the launch layout and time `steps` evaluations bracketed by
     a barrier + device synchronisation on both sides (max over ranks).  Returns the record
@@ -344,7 +350,7 @@ def measure(args, lay, ctx, config, scaling, patterns=None, classes=None, mode="
     else:
         P_job = P_arg * n_gpu if scaling == "weak" else P_arg
         start, end = 0, P_job
-        device = lay["devices"] if lay["kind"] == "multi" else 0
+        device = lay["devices"] if lay["kind"] == "multi" else single_device(lay)
         P_timed = shard.shard_range(0, n_gpu, P_job)[1] if lay["kind"] == "multi" else P_job
     wl.n_patterns = end - start
     t_setup = time.time()
@@ -420,7 +426,8 @@ def measure(args, lay, ctx, config, scaling, patterns=None, classes=None, mode="
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     units_step = P_job * wl.et.n_internal   # the whole job's node updates per step
-    return {"wl": wl, "ev": ev, "P": P_timed, "P_job": P_job, "lnl": lnl, "elapsed": elapsed, "tm": tm,
+    fan = ev.eng.fanout() if lay["kind"] == "multi" else None
+    return {"wl": wl, "ev": ev, "P": P_timed, "P_job": P_job, "lnl": lnl, "elapsed": elapsed, "tm": tm, "fanout": fan,
             "ev_steps": ev_steps, "k_ev": k_ev, "steps": steps, "units_step": units_step, "t_setup": t_setup,
             "value": units_step * steps / elapsed, "ms_step": elapsed * 1e3 / steps}
 
@@ -454,8 +461,8 @@ def main():
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
-        torch.cuda.set_device(0)
-    device = local if use_dist and not rehearse else 0
+        torch.cuda.set_device(single_device(lay))
+    device = local if use_dist and not rehearse else single_device(lay)
     ctx = {"dist": dist, "rank": rank, "rehearse": rehearse, "device": device,
            "coll_dev": "cpu" if rehearse else "cuda"}
 
@@ -525,6 +532,11 @@ def main():
             "roofline": roof,
             "setup_s": m["t_setup"],
         }
+        if m["fanout"]:
+            # host fan-out of the multi-device handle over the timed steps (plk_get_fanout): per shard
+            # the mean offsets from posting an evaluation to its worker starting, its traversal
+            # launch call returning and its completion wait returning
+            rec["fanout"] = m["fanout"]
         if args.devices:
             rec["config"]["devices"] = args.devices
             if len(set(lay["devices"])) < len(lay["devices"]):
@@ -564,6 +576,8 @@ def main():
                 "lnl": s["lnl"],
                 "setup_s": s["t_setup"],
             }
+            if s["fanout"]:
+                rec["strong"]["fanout"] = s["fanout"]
         s["ev"].eng.close()
     if rank == 0:
         print(json.dumps(rec), file=out, flush=True)

@@ -24,9 +24,12 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -106,11 +109,90 @@ bool tune_is(const char* key, char v) {
   return e && e[0] == v;
 }
 
-std::string g_last_error;
+// per host thread (like errno): the shard workers of a multi-device handle fail on their own
+thread_local std::string g_last_error;
 
 struct EventPair {
   hipEvent_t a, b;
   int kind;  // 0 partials, 1 pmat, 2 root, 3 tables
+};
+
+using clk = std::chrono::steady_clock;
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// Host workers of a multi-device handle (plk_create_multi).  Every shard after the first has a
+// persistent thread; the caller runs shard 0 itself, so all shards' launch calls and stream
+// waits run side by side instead of one shard after another (one thread issuing eight
+// shards' launches put the last device ~8 x 8.5 us behind the first).  A job is posted by
+// bumping `seq`; a worker spins on it for kSpinIdle after its last job (an evaluation loop
+// posts every ~0.2 ms, so the workers never sleep there) and then sleeps on the condition
+// variable; the caller spins on `done`.  Results are per-shard slots reduced by the caller in
+// shard order, so every sum keeps the single-thread order.
+struct ShardPool {
+  static constexpr std::chrono::milliseconds kSpinIdle{20};
+  std::vector<std::thread> threads;
+  std::atomic<uint64_t> seq{0};
+  std::atomic<int> done{0};
+  std::atomic<int> sleepers{0};
+  std::atomic<bool> stop{false};
+  std::mutex m;
+  std::condition_variable cv;
+  const std::function<int(size_t)>* job = nullptr;
+  std::vector<int> rc;
+  clk::time_point t_post;
+  std::vector<clk::time_point> t_start;  // per shard: the job began
+
+  explicit ShardPool(size_t n) : rc(n, 0), t_start(n) {
+    for (size_t i = 1; i < n; ++i) threads.emplace_back([this, i] { worker(i); });
+  }
+  ~ShardPool() {
+    stop.store(true);
+    {
+      std::lock_guard<std::mutex> lk(m);
+      cv.notify_all();
+    }
+    for (auto& t : threads) t.join();
+  }
+  void worker(size_t i) {
+    uint64_t seen = 0;
+    for (;;) {
+      uint64_t s = seq.load(std::memory_order_acquire);
+      const clk::time_point t0 = clk::now();
+      for (int k = 1; s == seen && !stop.load(std::memory_order_relaxed); ++k) {
+        cpu_relax();
+        if ((k & 255) == 0 && clk::now() - t0 > kSpinIdle) {
+          // idle: sleep (sleepers and seq are seq_cst on both sides, so a post either sees
+          // this sleeper and notifies under the mutex, or this check sees the post)
+          std::unique_lock<std::mutex> lk(m);
+          sleepers.fetch_add(1);
+          cv.wait(lk, [&] { return seq.load() != seen || stop.load(); });
+          sleepers.fetch_sub(1);
+        }
+        s = seq.load(std::memory_order_acquire);
+      }
+      if (stop.load()) return;
+      seen = s;
+      t_start[i] = clk::now();
+      rc[i] = (*job)(i);
+      done.fetch_add(1, std::memory_order_release);
+    }
+  }
+  // f(i) for every shard i, concurrently; returns when all are done
+  void run(const std::function<int(size_t)>& f) {
+    job = &f;
+    done.store(0, std::memory_order_relaxed);
+    t_post = clk::now();
+    seq.fetch_add(1);
+    if (sleepers.load() > 0) {
+      std::lock_guard<std::mutex> lk(m);
+      cv.notify_all();
+    }
+    t_start[0] = clk::now();
+    rc[0] = f(0);
+    const int others = (int)rc.size() - 1;
+    while (done.load(std::memory_order_acquire) < others) cpu_relax();
+  }
 };
 
 }  // namespace
@@ -192,9 +274,8 @@ struct plk_handle_s {
   size_t d_prog_cap = 0;
   int32_t* d_frag = nullptr;
   size_t d_frag_cap = 0;
-  unsigned* d_sbctr = nullptr;          // jit_tree4 dynamic super-block counters, one per fragment
-  size_t d_sbctr_cap = 0;
-  std::vector<unsigned> sb_base;        // each counter's value at the start of its next launch
+  unsigned* d_sbctr = nullptr;          // jit_tree4 dynamic super-block counters, one per fragment,
+  size_t d_sbctr_cap = 0;               // then the exit-ticket counter (all 0 between launches)
   std::vector<plk_op> prog_ops;           // op list the cached program was built from
   bool prog_materialize = false;
   bool prog_reduce = false;
@@ -277,6 +358,15 @@ struct plk_handle_s {
   // block-aligned pattern ranges; the parent owns no device memory
   std::vector<plk_handle> shards;
   std::vector<int64_t> shard_start;       // first pattern of each shard (+ n_patterns at the end)
+  std::unique_ptr<ShardPool> pool;        // host workers of the shards (started by the first call)
+  // fan-out of the multi-device evaluations since plk_reset_timing (plk_get_fanout): per shard
+  // the summed offsets (us) from the caller's post to the worker's start, to its traversal
+  // launch call returning and to its completion wait returning; spread of the launches
+  std::vector<double> fan_us;             // [shard][3]
+  double fan_spread_sum = 0.0, fan_spread_max = 0.0;
+  int64_t fan_n = 0;
+  // single-device handle: when the last plk_evaluate's traversal launch call and stream wait returned
+  clk::time_point t_launched{}, t_waited{};
   // RCCL communicator of a sharded multi-process run (plk_comm_init): block sums all-gathered
   // on the handle's stream and summed in global order on the device
   ncclComm_t comm = nullptr;
@@ -289,6 +379,9 @@ struct plk_handle_s {
   int64_t* d_comm_counts = nullptr;       // block sums per rank
   double* h_total = nullptr;              // mapped pinned: the global lnL
   double* d_total = nullptr;              // its device address
+  double* d_xch = nullptr;                // derivative sums exchanged under the communicator
+  double* d_xch_all = nullptr;
+  size_t d_xch_cap = 0, d_xch_all_cap = 0;
 };
 
 namespace {
@@ -467,10 +560,17 @@ int jit_compile(plk_handle h, const std::string& src, std::vector<char>* code, b
   std::string dir = jit_cache_dir(), stem;
   if (!dir.empty()) {
     char hx[17];
-    int maj = 0, mnr = 0;
-    hiprtcVersion(&maj, &mnr);  // a compiler update invalidates every entry
+    // the key: the source, the options, the device's full architecture name (with its
+    // target features) and the hiprtc and HIP runtime versions -- a compiler or runtime update
+    // or another device variant invalidates every entry
+    int maj = 0, mnr = 0, rt = 0;
+    hiprtcVersion(&maj, &mnr);
+    hipRuntimeGetVersion(&rt);
+    hipDeviceProp_t prop;
+    const std::string arch = hipGetDeviceProperties(&prop, h->device) == hipSuccess ? prop.gcnArchName : "?";
     snprintf(hx, sizeof(hx), "%016llx",
-             (unsigned long long)fnv1a64(src + opts[0] + opts[1] + std::to_string(maj) + "." + std::to_string(mnr)));
+             (unsigned long long)fnv1a64(src + opts[0] + opts[1] + std::to_string(maj) + "." + std::to_string(mnr) +
+                                         "/" + std::to_string(rt) + "/" + arch));
     stem = dir + "/" + hx;
     std::vector<char> stored, sum;
     // an entry is used only if its stored source equals the generated one and the code
@@ -706,21 +806,30 @@ int multi_forward(plk_handle h, int rc) {
   return rc;
 }
 
-int multi_each(plk_handle h, const std::function<int(plk_handle)>& f) {
-  for (size_t i = 0; i < h->shards.size(); ++i) {
-    const int rc = f(h->shards[i]);
-    if (rc) return fail(h, rc, "shard %zu (device %d): %s", i, h->shards[i]->device, h->shards[i]->last_error.c_str());
+// f(i) for every shard i, on the shards' host workers (ShardPool); the first failing shard in
+// shard order is reported
+int multi_run(plk_handle h, const std::function<int(size_t)>& f) {
+  const size_t n = h->shards.size();
+  if (n == 1) {
+    const int rc = f(0);
+    if (rc) return fail(h, rc, "shard 0 (device %d): %s", h->shards[0]->device, h->shards[0]->last_error.c_str());
+    return PLK_OK;
   }
+  if (!h->pool) h->pool.reset(new ShardPool(n));
+  h->pool->run(f);
+  for (size_t i = 0; i < n; ++i)
+    if (const int rc = h->pool->rc[i])
+      return fail(h, rc, "shard %zu (device %d): %s", i, h->shards[i]->device, h->shards[i]->last_error.c_str());
   return PLK_OK;
+}
+
+int multi_each(plk_handle h, const std::function<int(plk_handle)>& f) {
+  return multi_run(h, [&](size_t i) { return f(h->shards[i]); });
 }
 
 // f(shard, first pattern of the shard): per-pattern arrays are sliced at the shard starts
 int multi_slices(plk_handle h, const std::function<int(plk_handle, int64_t)>& f) {
-  for (size_t i = 0; i < h->shards.size(); ++i) {
-    const int rc = f(h->shards[i], h->shard_start[i]);
-    if (rc) return fail(h, rc, "shard %zu (device %d): %s", i, h->shards[i]->device, h->shards[i]->last_error.c_str());
-  }
-  return PLK_OK;
+  return multi_run(h, [&](size_t i) { return f(h->shards[i], h->shard_start[i]); });
 }
 
 }  // namespace
@@ -733,70 +842,85 @@ int root_finish_c(plk_handle h, double* lnl, double* block_sums);
 namespace {
 double* block_target(plk_handle h);
 
-// every device's root reduction in flight, then one wait per device; the lnL is the sum of
-// all block sums in global block order (bitwise the single-device value)
-int multi_root_finish_all(plk_handle h, double* lnl, double* block_sums) {
-  std::vector<double> all;
-  all.reserve((size_t)h->n_blocks);
-  for (size_t i = 0; i < h->shards.size(); ++i) {
-    plk_handle x = h->shards[i];
-    std::vector<double> b((size_t)x->n_blocks);
-    const int rc = root_finish_c(x, nullptr, b.data());
-    if (rc) return fail(h, rc, "shard %zu: %s", i, x->last_error.c_str());
-    all.insert(all.end(), b.begin(), b.end());
-  }
+// first block sum of each shard in the handle's global block order
+size_t shard_block0(plk_handle h, size_t i) { return (size_t)(h->shard_start[i] / kRootBlock); }
+
+// the lnL is the sum of all block sums in global block order (bitwise the single-device value)
+void sum_blocks(const std::vector<double>& all, double* lnl, double* block_sums) {
   double s = 0.0;
   for (double v : all) s += v;
   if (lnl) *lnl = s;
   if (block_sums) std::memcpy(block_sums, all.data(), all.size() * sizeof(double));
-  return PLK_OK;
 }
 
 int multi_root_loglik_impl(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums) {
-  const int rc = multi_slices(h, [&](plk_handle x, int64_t a) { return root_launch_c(x, root, site_lnl ? site_lnl + a : nullptr); });
+  std::vector<double> all((size_t)h->n_blocks);
+  const int rc = multi_run(h, [&](size_t i) {
+    plk_handle x = h->shards[i];
+    const int r = root_launch_c(x, root, site_lnl ? site_lnl + h->shard_start[i] : nullptr);
+    return r ? r : root_finish_c(x, nullptr, all.data() + shard_block0(h, i));
+  });
   if (rc) return rc;
-  return multi_root_finish_all(h, lnl, block_sums);
+  sum_blocks(all, lnl, block_sums);
+  return PLK_OK;
 }
 
+// every shard's whole evaluation (P(t), traversal, block sums, its stream wait) on its own host
+// worker; the fan-out timestamps of plk_get_fanout are taken here
 int multi_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* model, const double* t,
                    const plk_op* ops, int n_ops, int root, double* lnl, double* block_sums) {
-  const int rc = multi_each(h, [&](plk_handle x) {
-    int r = plk_update_pmatrices(x, n, branch, model, t, PLK_DERIV_P);
-    if (!r) r = plk_update_partials(x, ops, n_ops);
-    if (!r) r = root_launch_c(x, root, nullptr);
-    return r;
+  std::vector<double> all((size_t)h->n_blocks);
+  const int rc = multi_run(h, [&](size_t i) {
+    return plk_evaluate(h->shards[i], n, branch, model, t, ops, n_ops, root, nullptr, all.data() + shard_block0(h, i));
   });
   if (rc) return rc;
-  return multi_root_finish_all(h, lnl, block_sums);
+  sum_blocks(all, lnl, block_sums);
+  const size_t ns = h->shards.size();
+  if (ns > 1) {
+    const ShardPool& p = *h->pool;
+    auto us = [&](clk::time_point b) { return std::chrono::duration<double, std::micro>(b - p.t_post).count(); };
+    h->fan_us.resize(3 * ns, 0.0);
+    double lo = 1e300, hi = -1e300;
+    for (size_t i = 0; i < ns; ++i) {
+      const double l = us(h->shards[i]->t_launched);
+      h->fan_us[3 * i] += us(p.t_start[i]);
+      h->fan_us[3 * i + 1] += l;
+      h->fan_us[3 * i + 2] += us(h->shards[i]->t_waited);
+      lo = std::min(lo, l);
+      hi = std::max(hi, l);
+    }
+    h->fan_spread_sum += hi - lo;
+    h->fan_spread_max = std::max(h->fan_spread_max, hi - lo);
+    h->fan_n++;
+  }
+  return PLK_OK;
 }
 
+// per-shard values summed in shard order (the order of the former one-thread loop)
 int multi_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
-  double s1 = 0.0, s2 = 0.0;
-  const int rc = multi_each(h, [&](plk_handle x) {
-    double a = 0.0, b = 0.0;
-    const int r = plk_branch_derivatives(x, branch, &a, &b);
-    s1 += a;
-    s2 += b;
-    return r;
-  });
+  std::vector<double> a(h->shards.size()), b(h->shards.size());
+  const int rc = multi_run(h, [&](size_t i) { return plk_branch_derivatives(h->shards[i], branch, &a[i], &b[i]); });
   if (rc) return rc;
+  double s1 = 0.0, s2 = 0.0;
+  for (size_t i = 0; i < a.size(); ++i) {
+    s1 += a[i];
+    s2 += b[i];
+  }
   if (d1) *d1 = s1;
   if (d2) *d2 = s2;
   return PLK_OK;
 }
 
 int multi_all_branch_derivatives(plk_handle h, double* d1, double* d2) {
-  const size_t n = (size_t)h->n_nodes;
-  std::vector<double> s1(n, 0.0), s2(n, 0.0), a(n), b(n);
-  const int rc = multi_each(h, [&](plk_handle x) {
-    const int r = plk_all_branch_derivatives(x, a.data(), b.data());
-    for (size_t i = 0; i < n; ++i) {
-      s1[i] += a[i];
-      s2[i] += b[i];
-    }
-    return r;
-  });
+  const size_t n = (size_t)h->n_nodes, ns = h->shards.size();
+  std::vector<double> a(n * ns), b(n * ns), s1(n, 0.0), s2(n, 0.0);
+  const int rc = multi_run(h, [&](size_t k) { return plk_all_branch_derivatives(h->shards[k], &a[k * n], &b[k * n]); });
   if (rc) return rc;
+  for (size_t k = 0; k < ns; ++k)
+    for (size_t i = 0; i < n; ++i) {
+      s1[i] += a[k * n + i];
+      s2[i] += b[k * n + i];
+    }
   if (d1) std::memcpy(d1, s1.data(), n * sizeof(double));
   if (d2) std::memcpy(d2, s2.data(), n * sizeof(double));
   return PLK_OK;
@@ -804,13 +928,11 @@ int multi_all_branch_derivatives(plk_handle h, double* d1, double* d2) {
 
 int multi_compressed_work(plk_handle h, int64_t* updates) {
   int64_t s = 0;
-  const int rc = multi_each(h, [&](plk_handle x) {
+  for (size_t i = 0; i < h->shards.size(); ++i) {
     int64_t u = 0;
-    const int r = plk_compressed_work(x, &u);
+    if (const int r = plk_compressed_work(h->shards[i], &u)) return fail(h, r, "shard %zu: %s", i, h->shards[i]->last_error.c_str());
     s += u;
-    return r;
-  });
-  if (rc) return rc;
+  }
   if (updates) *updates = s;
   return PLK_OK;
 }
@@ -819,10 +941,9 @@ int multi_traversal_work(plk_handle h, plk_work* out) {
   plk_work sum;
   std::memset(&sum, 0, sizeof(sum));
   sum.exact = 1;
-  const int rc = multi_each(h, [&](plk_handle x) {
+  for (size_t i = 0; i < h->shards.size(); ++i) {
     plk_work w;
-    const int r = plk_traversal_work(x, &w);
-    if (r) return r;
+    if (const int r = plk_traversal_work(h->shards[i], &w)) return fail(h, r, "shard %zu: %s", i, h->shards[i]->last_error.c_str());
     sum.patterns += w.patterns;
     sum.node_updates += w.node_updates;
     sum.table_nodes = w.table_nodes;
@@ -832,9 +953,7 @@ int multi_traversal_work(plk_handle h, plk_work* out) {
     sum.table_flops += w.table_flops;
     sum.exact = sum.exact && w.exact;
     sum.internal_nodes = w.internal_nodes;
-    return 0;
-  });
-  if (rc) return rc;
+  }
   if (out) *out = sum;
   return PLK_OK;
 }
@@ -963,6 +1082,7 @@ void comm_release(plk_handle h);
 int plk_destroy(plk_handle h) {
   if (!h) return PLK_OK;
   if (!h->shards.empty()) {
+    h->pool.reset();  // workers joined before their shards go
     for (plk_handle s : h->shards) plk_destroy(s);
     delete h;
     return PLK_OK;
@@ -1009,9 +1129,11 @@ int plk_comm_get_id(plk_comm_id* id) {
 void comm_release(plk_handle h) {
   if (h->comm) ncclCommDestroy(h->comm);
   h->comm = nullptr;
-  for (void* p : {(void*)h->d_blk_local, (void*)h->d_blk_all, (void*)h->d_comm_counts})
+  for (void* p : {(void*)h->d_blk_local, (void*)h->d_blk_all, (void*)h->d_comm_counts, (void*)h->d_xch,
+                  (void*)h->d_xch_all})
     if (p) hipFree(p);
-  h->d_blk_local = h->d_blk_all = nullptr;
+  h->d_blk_local = h->d_blk_all = h->d_xch = h->d_xch_all = nullptr;
+  h->d_xch_cap = h->d_xch_all_cap = 0;
   h->d_comm_counts = nullptr;
   if (h->h_total) hipHostFree(h->h_total);
   h->h_total = nullptr;
@@ -1733,10 +1855,9 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   HIPCHK(h, hipMemcpyAsync(h->d_frag, start_sorted.data(), 2 * nf * sizeof(int32_t), hipMemcpyHostToDevice,
                            h->stream));
   h->prog_nf = nf;
-  rc = ensure_cap(h, (void**)&h->d_sbctr, &h->d_sbctr_cap, std::max(nf, 1) * sizeof(unsigned));
+  rc = ensure_cap(h, (void**)&h->d_sbctr, &h->d_sbctr_cap, (size_t)(nf + 1) * sizeof(unsigned));
   if (rc) return rc;
-  HIPCHK(h, hipMemsetAsync(h->d_sbctr, 0, std::max(nf, 1) * sizeof(unsigned), h->stream));
-  h->sb_base.assign((size_t)std::max(nf, 1), 0u);
+  HIPCHK(h, hipMemsetAsync(h->d_sbctr, 0, (size_t)(nf + 1) * sizeof(unsigned), h->stream));
   h->prog_host = prog;
   h->frag_starts_host.assign(start_sorted.begin(), start_sorted.begin() + nf);
   h->jit_fn = nullptr;  // specialised kernel of the new program: compiled on first use
@@ -1988,6 +2109,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.guard = a.guard;
     ja.sb_ctr = h->d_sbctr;
     ja.dyn = tune_is("JIT_DYN", '0') ? 0 : 1;  // (per launch below)
+    ja.exit_ctr = h->d_sbctr + h->prog_nf;  // (null per launch below when not dynamic)
   }
   const bool jitm = kind == FK_TREEM && h->prog_jitm;
   JMArgs ma;
@@ -2068,25 +2190,14 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       // dynamic super-blocks where a workgroup walks several (a tier of 1-2 per workgroup
       // gains nothing from them and pays the counter's round trips)
       ja.dyn = (!tune_is("JIT_DYN", '0') && ja.n_sblocks >= 3 * (int64_t)gx) ? 1 : 0;
-      // the tier's fragments take their super-blocks from counters that start this launch
-      // at one common value (every fragment is launched once per traversal with the same
-      // super-block count, so they stay equal; otherwise they are reset here)
-      ja.sb_base = h->sb_base[(size_t)first];
-      for (int k = 1; k < (int)t.size(); ++k)
-        if (h->sb_base[(size_t)(first + k)] != ja.sb_base) {
-          HIPCHK(h, hipMemsetAsync(h->d_sbctr, 0, (size_t)h->prog_nf * sizeof(unsigned), h->stream));
-          std::fill(h->sb_base.begin(), h->sb_base.end(), 0u);
-          ja.sb_base = 0;
-          break;
-        }
+      // the launch's counters start at 0; its last workgroup leaves them at 0 (exit ticket)
+      ja.exit_ctr = ja.dyn ? h->d_sbctr + h->prog_nf : nullptr;
       h->jit_last_gx = (int)gx;
       if ((int)h->jit_frag_gx.size() < h->prog_nf) h->jit_frag_gx.resize((size_t)h->prog_nf, 0);
       for (int k = 0; k < (int)t.size(); ++k) h->jit_frag_gx[(size_t)(first + k)] = (int)gx;
       HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
                                       (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
-      if (ja.dyn)
-        for (int k = 0; k < (int)t.size(); ++k) h->sb_base[(size_t)(first + k)] += (unsigned)ja.n_sblocks;
     } else if (jitm) {
       int base = first;
       void* args[] = {&ma, &base};
@@ -3513,6 +3624,31 @@ int root_finish(plk_handle h, double* lnl, double* block_sums, bool wait = true)
   return PLK_OK;
 }
 
+// Under a communicator: v[0..n) (this rank's derivative sums) becomes the sum over all ranks
+// in rank order -- one ncclAllGather of n doubles per rank on the handle's stream, then the
+// same chain of adds on every rank, so all ranks return the same doubles (an all-reduce's
+// order depends on the ring).  Without a communicator v is left as it is.
+int comm_sum_values(plk_handle h, double* v, size_t n) {
+  if (!h->comm || n == 0) return PLK_OK;
+  hipSetDevice(h->device);
+  const size_t R = (size_t)h->comm_ranks;
+  int rc = ensure_cap(h, (void**)&h->d_xch, &h->d_xch_cap, n * sizeof(double));
+  if (!rc) rc = ensure_cap(h, (void**)&h->d_xch_all, &h->d_xch_all_cap, R * n * sizeof(double));
+  if (rc) return rc;
+  HIPCHK(h, hipMemcpyAsync(h->d_xch, v, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  if (ncclAllGather(h->d_xch, h->d_xch_all, n, ncclFloat64, h->comm, h->stream) != ncclSuccess)
+    return fail(h, PLK_ERR_DEVICE, "ncclAllGather of the derivative sums failed");
+  std::vector<double> all(R * n);
+  HIPCHK(h, hipMemcpyAsync(all.data(), h->d_xch_all, all.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (size_t i = 0; i < n; ++i) {
+    double s = 0.0;
+    for (size_t r = 0; r < R; ++r) s += all[r * n + i];
+    v[i] = s;
+  }
+  return PLK_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -3613,9 +3749,22 @@ static int launch_root(plk_handle h, int root) {
   return PLK_OK;
 }
 
+static int branch_derivatives_local(plk_handle h, int branch, double* d1, double* d2);
+
 int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
   env_refresh();
   if (h && !h->shards.empty()) return multi_branch_derivatives(h, branch, d1, d2);
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  double v[2] = {0.0, 0.0};
+  int rc = branch_derivatives_local(h, branch, &v[0], &v[1]);
+  if (!rc) rc = comm_sum_values(h, v, 2);  // global under a communicator
+  if (rc) return rc;
+  if (d1) *d1 = v[0];
+  if (d2) *d2 = v[1];
+  return PLK_OK;
+}
+
+static int branch_derivatives_local(plk_handle h, int branch, double* d1, double* d2) {
   if (!h || branch < 0 || branch >= h->n_nodes) return fail(h, PLK_ERR_ARG, "bad branch %d", branch);
   if (h->trav_ops.empty()) return fail(h, PLK_ERR_STATE, "no traversal yet (plk_update_partials)");
   if (h->S != 4 || !(h->C == 1 || h->C == 2 || h->C == 4))
@@ -3714,21 +3863,26 @@ int plk_branch_derivatives(plk_handle h, int branch, double* d1, double* d2) {
 int plk_root_pair_derivatives(plk_handle h, int a, int b, double alpha, double beta, double* d1, double* d2) {
   env_refresh();
   if (h && !h->shards.empty()) {
-    double s1 = 0.0, s2 = 0.0;
-    const int rc = multi_each(h, [&](plk_handle x) {
-      double u = 0.0, v = 0.0;
-      const int r = plk_root_pair_derivatives(x, a, b, alpha, beta, &u, &v);
-      s1 += u;
-      s2 += v;
-      return r;
-    });
+    std::vector<double> u(h->shards.size()), v(h->shards.size());
+    const int rc = multi_run(h, [&](size_t i) { return plk_root_pair_derivatives(h->shards[i], a, b, alpha, beta, &u[i], &v[i]); });
     if (rc) return rc;
+    double s1 = 0.0, s2 = 0.0;
+    for (size_t i = 0; i < u.size(); ++i) {  // shard order
+      s1 += u[i];
+      s2 += v[i];
+    }
     if (d1) *d1 = s1;
     if (d2) *d2 = s2;
     return PLK_OK;
   }
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
-  return root_pair_derivatives(h, a, b, alpha, beta, d1, d2);
+  double v[2] = {0.0, 0.0};
+  int rc = root_pair_derivatives(h, a, b, alpha, beta, &v[0], &v[1]);
+  if (!rc) rc = comm_sum_values(h, v, 2);
+  if (rc) return rc;
+  if (d1) *d1 = v[0];
+  if (d2) *d2 = v[1];
+  return PLK_OK;
 }
 
 int plk_set_timing(plk_handle h, int enable) {
@@ -3752,7 +3906,12 @@ int plk_get_timing(plk_handle h, int64_t* n_launches, double* partials_ms, doubl
 }
 
 int plk_reset_timing(plk_handle h) {
-  if (h && !h->shards.empty()) return multi_each(h, [&](plk_handle x) { return plk_reset_timing(x); });
+  if (h && !h->shards.empty()) {
+    h->fan_us.assign(h->fan_us.size(), 0.0);
+    h->fan_spread_sum = h->fan_spread_max = 0.0;
+    h->fan_n = 0;
+    return multi_each(h, [&](plk_handle x) { return plk_reset_timing(x); });
+  }
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
   int rc = collect_events(h);
   if (rc) return rc;
@@ -3802,7 +3961,6 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
   env_refresh();
   if (h && !h->shards.empty()) return multi_evaluate(h, n, branch, model, t, ops, n_ops, root, lnl, block_sums);
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
-  using clk = std::chrono::steady_clock;
   const clk::time_point t0 = clk::now();
   auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
   h->in_eval = true;
@@ -3830,6 +3988,23 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
   if (h->n_evals > 0) h->host_us[5] += us(h->last_eval_end, t0);
   h->n_evals++;
   h->last_eval_end = t5;
+  h->t_launched = t2;
+  h->t_waited = t4;
+  return PLK_OK;
+}
+
+int plk_get_fanout(plk_handle h, int n_shards, double* offsets_us, double* spread_us, int64_t* evaluations) {
+  if (!h) return fail(h, PLK_ERR_ARG, "null handle");
+  const int ns = h->shards.empty() ? 1 : (int)h->shards.size();
+  if (n_shards != ns) return fail(h, PLK_ERR_ARG, "handle has %d shard(s), not %d", ns, n_shards);
+  const double k = h->fan_n > 0 ? 1.0 / (double)h->fan_n : 0.0;
+  for (int i = 0; i < 3 * ns; ++i)
+    if (offsets_us) offsets_us[i] = (size_t)i < h->fan_us.size() ? h->fan_us[i] * k : 0.0;
+  if (spread_us) {
+    spread_us[0] = h->fan_spread_sum * k;
+    spread_us[1] = h->fan_spread_max;
+  }
+  if (evaluations) *evaluations = h->fan_n;
   return PLK_OK;
 }
 
@@ -3837,7 +4012,15 @@ int plk_all_branch_derivatives(plk_handle h, double* d1, double* d2) {
   env_refresh();
   if (h && !h->shards.empty()) return multi_all_branch_derivatives(h, d1, d2);
   if (!h) return fail(h, PLK_ERR_ARG, "null handle");
-  return dr_derivatives(h, d1, d2);
+  if (!h->comm) return dr_derivatives(h, d1, d2);
+  const size_t n = (size_t)h->n_nodes;
+  std::vector<double> v(2 * n, 0.0);
+  int rc = dr_derivatives(h, v.data(), v.data() + n);
+  if (!rc) rc = comm_sum_values(h, v.data(), 2 * n);
+  if (rc) return rc;
+  if (d1) std::memcpy(d1, v.data(), n * sizeof(double));
+  if (d2) std::memcpy(d2, v.data() + n, n * sizeof(double));
+  return PLK_OK;
 }
 
 const char* plk_kernel_path(plk_handle h) {

@@ -53,7 +53,7 @@ struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
   double* partials; i32* scale; const u8* codes; const double* tipP; const double* weights;
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
-  unsigned* sb_ctr; unsigned sb_base; i32 dyn;
+  unsigned* sb_ctr; i32 dyn; unsigned* exit_ctr;
 };
 
 // Register vectors hold 4 * CW * PW doubles: vector v = pw * CW + cw is class c0 + cw of
@@ -360,11 +360,13 @@ struct JArgs {
   int32_t n_sblocks;
   int32_t guard;
   // dynamic super-blocks (dyn != 0): after its first super-block (blockIdx.x) a workgroup
-  // takes the next one from sb_ctr[frag] (a counter that only grows: this launch's values
-  // start at sb_base, and it ends the launch at sb_base + n_sblocks)
+  // takes the next one from sb_ctr[frag], which is 0 when the launch starts (the last
+  // workgroup to exit resets it)
   unsigned* sb_ctr;
-  unsigned sb_base;
   int32_t dyn;
+  // exit ticket (with dyn): every workgroup takes one ticket as it exits; the last one resets
+  // the launch's super-block counters and the ticket counter to 0
+  unsigned* exit_ctr;
 };
 
 struct JitShape {
@@ -805,9 +807,9 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // Super-block order.  Static: blockIdx.x, + gridDim.x, ...  Dynamic (a.dyn): the first is
   // blockIdx.x, every later one comes from the fragment's counter -- thread 0 takes the index
   // of the super-block after the next one while this one computes, so the atomic's latency is
-  // hidden; a workgroup stops taking after its first index past the end (exactly one such
-  // take per workgroup, so the counter ends at sb_base + n_sblocks).  Which workgroup
-  // computes a super-block does not change its results.
+  // hidden; a workgroup stops taking after its first index past the end.  The counter starts
+  // the launch at 0 (the exit ticket below resets it).  Which workgroup computes a
+  // super-block does not change its results.
   __shared__ int sb_next_lds;
   unsigned sb_pend = 0;
   if (a.dyn && threadIdx.x == 0)
@@ -825,7 +827,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     _Pragma("unroll") for (int m = 0; m < NI_; ++m)
       if (q0 + ic_[m] < a.n_pad) reinterpret_cast<uint4*>(code_lds)[il_[m]] = va_[m];
     if (a.dyn && threadIdx.x == 0) {  // (an index outside this launch's range ends the loop)
-      const unsigned d_ = sb_pend - a.sb_base;
+      const unsigned d_ = sb_pend;
       sb_next_lds = d_ < (unsigned)(a.n_sblocks - (int)gridDim.x) ? (int)gridDim.x + (int)d_ : a.n_sblocks;
     }
     __syncthreads();
@@ -1028,7 +1030,23 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     emit_body(true);
     s += "    } break;\n";
   }
-  s += "    default: break;\n    }\n  }\n}\n";
+  s += "    default: break;\n    }\n  }\n";
+  // Exit ticket (dynamic super-blocks): thread 0 of every workgroup takes one ticket after its
+  // last super-block -- its own counter atomics have returned by then -- and the last one
+  // leaves the launch's counters and the ticket counter at 0 for the next launch, so the host
+  // keeps no copy of them.  (Forming the block sums in the last workgroup as well was measured
+  // 8 us slower per cfg2 traversal than wave_sums_to_blocks: the wave sums must then cross the
+  // XCDs' L2s, as sc1 stores and loads or behind L2 write-backs -- profiles/r05/ab_runs.md.)
+  s += R"PLKJIT(  if (a.exit_ctr && threadIdx.x == 0) {
+    const unsigned t_ = __hip_atomic_fetch_add(a.exit_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t_ == gridDim.x * gridDim.y - 1u) {
+      for (unsigned f_ = 0; f_ < gridDim.y; ++f_)
+        __hip_atomic_store(a.sb_ctr + frag_base + f_, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.exit_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+)PLKJIT";
   return s;
 }
 

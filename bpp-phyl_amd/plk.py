@@ -37,7 +37,7 @@ EXPORTS = [
     "plk_set_timing", "plk_get_timing", "plk_reset_timing", "plk_synchronize", "plk_branch_derivatives",
     "plk_kernel_path", "plk_evaluate", "plk_compressed_work", "plk_all_branch_derivatives",
     "plk_get_timing_ex", "plk_traversal_work", "plk_create_multi", "plk_shard_count", "plk_comm_get_id",
-    "plk_comm_init", "plk_get_dpmatrix", "plk_root_pair_derivatives",
+    "plk_comm_init", "plk_get_dpmatrix", "plk_root_pair_derivatives", "plk_get_fanout",
 ]
 
 
@@ -92,6 +92,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_create_multi": ([P(ct.c_int), ct.c_int, ct.c_int, ct.c_int, ct.c_int64, ct.c_int, ct.c_int, ct.c_int,
                               ct.c_uint, P(ct.c_void_p)], ct.c_int),
         "plk_shard_count": ([ct.c_void_p, P(ct.c_int)], ct.c_int),
+        "plk_get_fanout": ([ct.c_void_p, ct.c_int, dp, dp, P(ct.c_int64)], ct.c_int),
         "plk_comm_get_id": ([P(plk_comm_id)], ct.c_int),
         "plk_comm_init": ([ct.c_void_p, ct.c_int, ct.c_int, P(plk_comm_id)], ct.c_int),
         "plk_set_code_table": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
@@ -122,7 +123,11 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_evaluate": ([ct.c_void_p, ct.c_int, ip, ip, dp, P(plk_op), ct.c_int, ct.c_int, dp, dp], ct.c_int),
     }
     for name, (args, res) in sig.items():
-        f = getattr(lib, name)
+        f = getattr(lib, name, None)
+        if f is None and os.environ.get("PLK_LIB"):
+            continue  # an older A/B build (PLK_LIB) without this entry point
+        if f is None:
+            raise AttributeError(f"{path}: missing {name}")
         f.argtypes = args
         f.restype = res
     if lib.plk_abi_version() != ABI_VERSION:  # the structs above mirror this version of plk.h
@@ -386,6 +391,18 @@ class Engine:
         n = ct.c_int(0)
         self._chk(self.lib.plk_shard_count(self.h, ct.byref(n)))
         return n.value
+
+    def fanout(self) -> dict:
+        """plk_get_fanout: per shard, the mean offsets (us) from posting an evaluation to the
+        shard's worker starting it, to its traversal launch call returning and to its stream
+        wait returning; the spread (last - first traversal launch), mean and max."""
+        ns = self.shard_count()
+        off, spread, n = np.zeros(3 * ns), np.zeros(2), ct.c_int64(0)
+        self._chk(self.lib.plk_get_fanout(self.h, ns, _d(off), _d(spread), ct.byref(n)))
+        o = off.reshape(ns, 3)
+        return {"evaluations": n.value, "start_us": o[:, 0].tolist(), "traversal_launched_us": o[:, 1].tolist(),
+                "waited_us": o[:, 2].tolist(), "launch_spread_mean_us": float(spread[0]),
+                "launch_spread_max_us": float(spread[1])}
 
     def comm_init(self, n_ranks: int, rank: int, comm_id: bytes):
         """plk_comm_init: RCCL communicator inside the handle; evaluations then return the

@@ -141,14 +141,23 @@ int plk_destroy(plk_handle h);
  * One process, several devices: plk_create_multi takes the device list (a device may be
  * listed twice: two shards on one GPU, for tests) and the TOTAL pattern count; the handle
  * it returns accepts every call of this header with whole-alignment arguments (tip codes,
- * weights, per-pattern outputs span all patterns) and fans them out: launches on all
- * devices first, then one wait per device; each device's block sums arrive in mapped host
- * memory and the host sums them in global order (the result is needed on the host, so an
- * in-process collective would only add a hop).  Derivatives are summed over shards.  Timing
- * and plk_kernel_path report shard 0; plk_traversal_work sums the shards. */
+ * weights, per-pattern outputs span all patterns) and fans them out: every shard after the
+ * first has a persistent host worker thread (the caller's thread runs the first), so the
+ * shards' launch calls and stream waits run side by side; each device's block sums arrive in
+ * mapped host memory and the caller sums them in global order (the result is needed on the
+ * host, so an in-process collective would only add a hop).  Derivatives are summed over
+ * shards in shard order.  Timing and plk_kernel_path report shard 0; plk_traversal_work sums
+ * the shards. */
 int plk_create_multi(const int* devices, int n_devices, int n_states, int n_classes, int64_t n_patterns, int n_tips,
                      int n_internal, int n_models, unsigned flags, plk_handle* out);
 int plk_shard_count(plk_handle h, int* n_shards);
+/* Fan-out of a multi-device handle's plk_evaluate calls since plk_reset_timing: for each of its
+ * n_shards shards (plk_shard_count), the mean offset in microseconds from the caller posting
+ * the evaluation to [3i] the shard's worker starting it, [3i+1] its traversal launch call
+ * returning and [3i+2] its completion wait returning; spread_us[0] / [1] = mean / max over the
+ * evaluations of the last minus the first shard's traversal launch.  A single-device handle
+ * reports zeros (n_shards = 1). */
+int plk_get_fanout(plk_handle h, int n_shards, double* offsets_us, double* spread_us, int64_t* evaluations);
 
 /* One process per GPU (torch.distributed / MPI launch): rank r creates its handle with
  * plk_create for ITS pattern range, one rank gets an id with plk_comm_get_id and shares
@@ -228,10 +237,11 @@ int plk_block_size(void);
  * and replaces computeTreeDLikelihood / computeTreeD2Likelihood for those two variables
  * (Likelihood/RNonHomogeneousTreeLikelihood.cpp:391-560, 862-1100).  Requires dP and d2P of
  * both branches.  Any state and class count.
- * Under an RCCL communicator (plk_comm_init) this and plk_branch_derivatives return THIS
- * RANK'S share (its pattern range) only -- unlike plk_evaluate's lnL, derivatives are not
- * exchanged: the caller sums d1 and d2 over the ranks (one all-reduce of two doubles).  A
- * multi-device handle (plk_create_multi) returns the sum over its devices. */
+ * Under an RCCL communicator (plk_comm_init) this, plk_branch_derivatives and
+ * plk_all_branch_derivatives return GLOBAL values on every rank: each rank's d1 and d2 are
+ * all-gathered (one fixed-size ncclAllGather on the handle's stream) and summed in rank
+ * order, so every rank holds the same doubles.  A multi-device handle (plk_create_multi)
+ * returns the sum over its devices in shard order. */
 int plk_root_pair_derivatives(plk_handle h, int a, int b, double alpha, double beta, double* d1, double* d2);
 
 /* Double-recursive derivatives (handle created with PLK_FLAG_DOUBLE_RECURSIVE): d lnL/dt and

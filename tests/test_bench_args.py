@@ -61,6 +61,16 @@ def test_explicit_devices(bench):
     assert bench.parallelism(lay, _args(gpus=2)) == "multi-device x2"
 
 
+def test_single_gpu_explicit_device(bench):
+    """--gpus 1 --devices K: one process on device K, not device 0."""
+    lay = bench.launch_layout(_args(gpus=1, devices="3"))
+    assert lay == {"kind": "single", "world": 1, "devices": [3]}
+    assert bench.single_device(lay) == 3
+    assert bench.single_device(bench.launch_layout(_args())) == 0
+    with pytest.raises(SystemExit):
+        bench.launch_layout(_args(gpus=1, devices="0,1"))
+
+
 def test_cli_exits_nonzero_without_gpus(tmp_path):
     """`python bench.py --gpus 2` with no launcher on a box with fewer GPUs: exit status 2 and a
     message, before any GPU work (this container has none)."""

@@ -113,6 +113,15 @@ def test_comm_single_rank_bitwise(config, flags):
     s0 = ref.root_loglik(et.root, want_sites=True)
     s1 = eng.root_loglik(et.root, want_sites=True)
     assert s0[0] == s1[0] and np.array_equal(s0[1], s1[1])
+    if wl.S == 4:
+        # derivatives are global under a communicator (all-gathered, summed in rank order):
+        # at one rank they are the handle's own values bitwise
+        for e in (ref, eng):
+            e.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+            e.update_partials(ops)
+            e.root_loglik(et.root)
+        for b in (0, int(br[-1])):
+            assert ref.branch_derivatives(b) == eng.branch_derivatives(b)
 
 
 def test_comm_init_failure_leaves_single_rank_path(monkeypatch):
@@ -214,3 +223,41 @@ def test_bench_gpus2_one_process_rehearsal():
     assert one["strong"]["patterns_total"] == two["strong"]["patterns_total"] == 40000
     assert one["strong"]["lnl"] == two["strong"]["lnl"]
     assert one["kernel_path"] == two["kernel_path"] == "jit_tree4"
+
+
+def test_multi_device_fanout_eight_shards():
+    """Eight shards of one plk_create_multi handle (all on the one GPU of this box): every
+    shard runs on its own host worker; lnL and block sums equal one handle bitwise evaluation
+    after evaluation, derivatives agree, and plk_get_fanout reports every shard's offsets."""
+    n = 8 * 4096 + 123
+    wl = workload.make_workload("gtr_g4_dna_1M_64", n_patterns=n)
+    et = wl.et
+    states = wl.simulate(0, n)
+    base = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY
+    one = _setup(plk.Engine(0, wl.S, wl.C, n, et.n_tips, et.n_internal, 1, base), wl, states)
+    multi = _setup(plk.Engine([0] * 8, wl.S, wl.C, n, et.n_tips, et.n_internal, 1, base), wl, states)
+    assert multi.shard_count() == 8
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    ops = phylo.split_ops(et.ops)
+    multi.reset_timing()
+    for k in range(12):
+        t = et.brlen[br] * (1.0 + 0.05 * k)
+        l1, b1 = one.evaluate(br, t, ops, et.root)
+        lm, bm = multi.evaluate(br, t, ops, et.root)
+        assert l1 == lm and np.array_equal(b1, bm)
+    f = multi.fanout()
+    assert f["evaluations"] == 12 and len(f["traversal_launched_us"]) == 8
+    assert all(0.0 <= a <= b <= c for a, b, c in zip(f["start_us"], f["traversal_launched_us"], f["waited_us"]))
+    assert 0.0 <= f["launch_spread_mean_us"] <= f["launch_spread_max_us"]
+    assert one.fanout()["evaluations"] == 0
+    r1 = one.root_loglik(et.root, want_sites=True, want_blocks=True)
+    rm = multi.root_loglik(et.root, want_sites=True, want_blocks=True)
+    assert r1[0] == rm[0] and np.array_equal(r1[1], rm[1]) and np.array_equal(r1[2], rm[2])
+    for e in (one, multi):
+        e.update_pmatrices(br, et.brlen[br], deriv_mask=7)
+        e.update_partials(ops)
+        e.root_loglik(et.root)
+    for b in (0, et.n_tips, int(br[-1])):
+        a1, a2 = one.branch_derivatives(b)
+        m1, m2 = multi.branch_derivatives(b)
+        assert abs(a1 - m1) <= 1e-12 * abs(a1) and abs(a2 - m2) <= 1e-12 * abs(a2)
