@@ -377,6 +377,8 @@ struct plk_handle_s {
   size_t d_drpre_cap = 0;
   double* d_blk_all = nullptr;            // [comm_ranks][comm_cmax]
   int64_t* d_comm_counts = nullptr;       // block sums per rank
+  int32_t* h_uflow = nullptr;             // mapped pinned: root-reduction underflow flag (plk_root_underflow)
+  int32_t* d_uflow = nullptr;             // its device address
   double* h_total = nullptr;              // mapped pinned: the global lnL
   double* d_total = nullptr;              // its device address
   double* d_xch = nullptr;                // derivative sums exchanged under the communicator
@@ -842,6 +844,15 @@ int root_finish_c(plk_handle h, double* lnl, double* block_sums);
 namespace {
 double* block_target(plk_handle h);
 
+// The root reductions of an unscaled handle flag a site likelihood below 2^-255 (or <= 0, or
+// NaN) in mapped host memory (plk_root_underflow); a scaled handle's reductions see rescaled
+// values, so they get no flag.  The host clears it before a launch that reduces the root.
+int32_t* uflow_arm(plk_handle h) {
+  if (h->flags & PLK_FLAG_SCALING) return nullptr;
+  *(volatile int32_t*)h->h_uflow = 0;
+  return h->d_uflow;
+}
+
 // first block sum of each shard in the handle's global block order
 size_t shard_block0(plk_handle h, size_t i) { return (size_t)(h->shard_start[i] / kRootBlock); }
 
@@ -1063,6 +1074,10 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
       hipHostGetDevicePointer((void**)&h->block_sums, h->h_blocks, 0) != hipSuccess)
     return bail(fail(h, PLK_ERR_OOM, "pinned block-sum buffer"));
   if ((rc = dalloc(h, (void**)&h->wave_sums, (size_t)(h->n_pad / 64) * sizeof(double)))) return bail(rc);
+  if (hipHostMalloc((void**)&h->h_uflow, 64, hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&h->d_uflow, h->h_uflow, 0) != hipSuccess)
+    return bail(fail(h, PLK_ERR_OOM, "pinned underflow flag"));
+  *h->h_uflow = 0;
   h->materialized.assign(n_internal, 0);
   // default weights 1 for real patterns, 0 for padding
   std::vector<double> w(h->n_pad, 0.0);
@@ -1100,6 +1115,7 @@ int plk_destroy(plk_handle h) {
     if (p) hipFree(p);
   if (h->h_req) (void)hipHostFree(h->h_req);
   if (h->h_blocks) hipHostFree(h->h_blocks);
+  if (h->h_uflow) hipHostFree(h->h_uflow);
   if (h->req_done) hipEventDestroy(h->req_done);
   for (auto& e : h->events) {
     hipEventDestroy(e.a);
@@ -1966,6 +1982,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     }
   }
   TreeArgs a;
+  a.uflow = h->prog_root >= 0 ? uflow_arm(h) : nullptr;
   a.cherry = h->d_cherry;
   a.prog = h->d_prog;
   a.partials = h->partials;
@@ -2110,6 +2127,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.sb_ctr = h->d_sbctr;
     ja.dyn = tune_is("JIT_DYN", '0') ? 0 : 1;  // (per launch below)
     ja.exit_ctr = h->d_sbctr + h->prog_nf;  // (null per launch below when not dynamic)
+    ja.uflow = a.uflow;
   }
   const bool jitm = kind == FK_TREEM && h->prog_jitm;
   JMArgs ma;
@@ -2154,6 +2172,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ma.cherry_table_bytes = (int64_t)lay.table_bytes;
     ma.cherry_count_bytes = (int64_t)lay.count_bytes;
     ma.guard = a.guard;
+    ma.uflow = a.uflow;
   }
   h->kernel_path = jit ? "jit_tree4" : jitm ? "jit_treeM" : kind == FK_TREEM ? "treeM" : "tree4";
   int first = 0;
@@ -3703,6 +3722,19 @@ int plk_create_multi(const int* devices, int n_devices, int n_states, int n_clas
   return PLK_OK;
 }
 
+int plk_root_underflow(plk_handle h, int* flag) {
+  if (!h || !flag) return fail(h, PLK_ERR_ARG, "null argument");
+  if (h->flags & PLK_FLAG_SCALING) return fail(h, PLK_ERR_STATE, "a scaled handle's reduction has no underflow flag");
+  int f = 0;
+  if (!h->shards.empty()) {
+    for (plk_handle x : h->shards) f |= *(volatile int32_t*)x->h_uflow;
+  } else {
+    f = *(volatile int32_t*)h->h_uflow;
+  }
+  *flag = f ? 1 : 0;
+  return PLK_OK;
+}
+
 int plk_shard_count(plk_handle h, int* n_shards) {
   if (!h || !n_shards) return fail(h, PLK_ERR_ARG, "null argument");
   *n_shards = h->shards.empty() ? 1 : (int)h->shards.size();
@@ -3731,6 +3763,7 @@ static int launch_root(plk_handle h, int root) {
   a.S = h->S;
   a.C = h->C;
   a.guard = (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0;
+  a.uflow = uflow_arm(h);
   EventPair ev;
   if (h->timing & PLK_TIME_ROOT) {
     ev = get_events(h, 2);

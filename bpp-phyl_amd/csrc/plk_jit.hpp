@@ -53,7 +53,7 @@ struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
   double* partials; i32* scale; const u8* codes; const double* tipP; const double* weights;
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
-  unsigned* sb_ctr; i32 dyn; unsigned* exit_ctr;
+  unsigned* sb_ctr; i32 dyn; unsigned* exit_ctr; i32* uflow;
 };
 
 // Register vectors hold 4 * CW * PW doubles: vector v = pw * CW + cw is class c0 + cw of
@@ -332,6 +332,7 @@ __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[
       double wr = 0.0;
       const i64 pp = p + 64 * pw;
       if (gv && pp < a.n_patterns) {
+        if (a.uflow && !(l >= 2.0 * kScaleThr)) *a.uflow = 1;  // plk_root_underflow
         a.site_lnl[pp] = r;
         wr = a.weights[pp] * r;
       }
@@ -367,6 +368,7 @@ struct JArgs {
   // exit ticket (with dyn): every workgroup takes one ticket as it exits; the last one resets
   // the launch's super-block counters and the ticket counter to 0
   unsigned* exit_ctr;
+  int32_t* uflow;  // unscaled handles: set to 1 when a site likelihood is < 2^-255 (or null)
 };
 
 struct JitShape {

@@ -65,7 +65,7 @@ struct JMArgs {
   double* partials; i32* scale; const u8* codes; const double* tipP; const u8* cherry; const double* pmats;
   const double* weights; const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i64 cherry_stride; i64 cherry_table_bytes; i64 cherry_count_bytes;
-  i32 guard;
+  i32 guard; i32* uflow;
 };
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
@@ -102,6 +102,7 @@ struct JMArgs {
   int64_t cherry_table_bytes;
   int64_t cherry_count_bytes;
   int32_t guard;
+  int32_t* uflow;  // unscaled handles: set to 1 when a site likelihood is < 2^-255 (or null)
 };
 
 struct JitMShape {
@@ -246,7 +247,8 @@ inline std::string jit_treeM4_source(const std::vector<TInstr>& prog, const std:
   double rr_ = jitm_log(l_); \
   if (SC_) rr_ -= (double)K * kLn2x256; \
   double wr_ = 0.0; \
-  if (p < a.n_patterns) { if (hi == 0) a.site_lnl[p] = rr_; wr_ = a.weights[p] * rr_; } \
+  if (p < a.n_patterns) { if (hi == 0) a.site_lnl[p] = rr_; wr_ = a.weights[p] * rr_; \
+    if (a.uflow && hi == 0 && !(l_ >= 2.0 * kScaleThr)) *a.uflow = 1; } \
   if (hi == 0) red[16 * w + pl] = wr_; \
   __syncthreads(); \
   if (w < G_ / 4) { double v_ = red[64 * w + lane]; \

@@ -863,6 +863,7 @@ struct RootArgs {
   int64_t n_patterns;
   int S, C;
   int guard;               // 1: homogeneous guards, 0: NH clamp
+  int32_t* uflow;          // unscaled handles: set to 1 when a site likelihood is < 2^-255 (or null)
 };
 
 __global__ __launch_bounds__(64) void root_kernel(RootArgs a) {
@@ -894,6 +895,7 @@ __global__ __launch_bounds__(64) void root_kernel(RootArgs a) {
   if (a.scale) r -= (double)a.scale[p] * kLn2x256;
   double wr = 0.0;
   if (p < a.n_patterns) {
+    if (a.uflow && !(l >= 2.0 * kScaleThr)) *a.uflow = 1;  // plk_root_underflow
     a.site_lnl[p] = r;
     wr = a.weights[p] * r;
   }

@@ -69,6 +69,7 @@ struct TreeArgs {
   const uint8_t* cherry;      // treeM: per cherry [table | counts | codes] (plk_treeM.hpp: CherryLayout)
   int32_t cherry_pairs;       // treeM: two consecutive T_CHERRY rows gathered together
   int32_t n_cherry_staged;    // treeM: cherries whose combined codes are staged in LDS (0: none)
+  int32_t* uflow;             // unscaled handles: set to 1 when a site likelihood is < 2^-255 (or null)
 };
 
 constexpr int kTreeMaxWaves = 4;
@@ -278,6 +279,7 @@ __global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a, const TInstr* __
       if (SCALE) r -= (double)cnt * kLn2x256;
       double wr = 0.0;
       if (p < a.n_patterns) {
+        if (a.uflow && !(l >= 2.0 * kScaleThr)) *a.uflow = 1;  // plk_root_underflow
         a.site_lnl[p] = r;
         wr = a.weights[p] * r;
       }

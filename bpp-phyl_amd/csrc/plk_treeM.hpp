@@ -503,6 +503,7 @@ __global__ __launch_bounds__((treeM_threads<S, G>()), (S == 64 ? 1 : 4)) void tr
       if (SCALE) rr -= (double)cnt * kLn2x256;
       double wr = 0.0;
       if (p < a.n_patterns) {
+        if (a.uflow && !(l >= 2.0 * kScaleThr)) *a.uflow = 1;  // plk_root_underflow
         a.site_lnl[p] = rr;
         wr = a.weights[p] * rr;
       }

@@ -79,7 +79,11 @@ class AbstractPlkTreeLikelihood : public virtual TreeLikelihood {
   bool usePatterns_ = true;
   bool verbose_ = true;
   bool initialized_ = false;
-  int scalingMode_ = -1;  // setUnderflowScaling: 1 on, 0 off, -1 by tree size (createEngine)
+  int scalingMode_ = -1;  // setUnderflowScaling: 1 on, 0 off, -1 unscaled first with an exact fallback
+  bool scaledNow_ = false;   // scalingMode_ -1: an evaluation flagged underflow, the engine rescales since
+  size_t engineModels_ = 1;  // createEngine's arguments (kept for the fallback's new engine)
+  bool engineGuard_ = true;
+  bool engineScaled_ = false;  // the current engine was created with PLK_FLAG_SCALING
   bool incremental_ = true;
   bool compressed_ = false;  // usePatterns: PLK_FLAG_SUBTREE_PATTERNS on the engine
   bool allDirty_ = true;     // next fireParameterChanged recomputes every P(t) (initialize)
@@ -124,6 +128,15 @@ class AbstractPlkTreeLikelihood : public virtual TreeLikelihood {
   void buildEngineLayout();
   void setDataImpl(const SiteContainer& sites, const Alphabet* alphabet, const SubstitutionModel& model);
   void createEngine(size_t nModels, bool nonNegGuard);
+  // the subclass's uploads after createEngine: tip codes, code table and weights (uploadData);
+  // eigen-systems, rates and root frequencies (uploadModels)
+  virtual void uploadData() = 0;
+  virtual void uploadModels() = 0;
+  // scalingMode_ -1: the engine flagged a site likelihood below 2^-255 (plk_root_underflow), so
+  // a rescaling engine could differ: re-create the engine with PLK_FLAG_SCALING, re-upload and
+  // re-evaluate every branch (from then on every evaluation is scaled)
+  void switchToScaledEngine();
+  bool underflowed() const;
   virtual void initBranchLengthsParameters();
   // set the nodes' lengths from the parameters; returns the nodes whose length changed
   virtual std::vector<const Node*> applyBranchLengths();
@@ -154,6 +167,7 @@ class AbstractPlkTreeLikelihood : public virtual TreeLikelihood {
     size_t eigenUploads = 0;     // eigen-systems handed to the engine
     size_t pmatBranches = 0;     // branches whose P(t) was recomputed
     size_t fullTraversals = 0;   // traversals over every internal node
+    size_t scaledFallbacks = 0;  // unscaled evaluations redone on a rescaling engine (0 or 1)
   };
   EvaluationStats stats_;
 
@@ -189,11 +203,16 @@ class AbstractPlkTreeLikelihood : public virtual TreeLikelihood {
   size_t getRootArrayPosition(size_t site) const { return rootPatternLinks_[site]; }
   // Exact power-of-two rescaling of partials (a deviation from the reference, which
   // has none and underflows on large trees); bit-identical when it never triggers.  By
-  // default it is on when a site's likelihood can approach the double range on long
-  // branches, taken as n_tips * ln(n_states) > 300 (DNA above 216 tips, proteins above
-  // 100, codons above 73), and off otherwise, as in the reference: the kernels without
-  // it are faster (cfg2 one class per wave instead of every class in the wave).
-  void setUnderflowScaling(bool yn) { scalingMode_ = yn ? 1 : 0; }
+  // default every evaluation runs unscaled first -- the faster kernels, one class per wave on
+  // cfg2 -- and the engine reports whether any site likelihood fell below 2^-255
+  // (plk_root_underflow, include/plk.h: otherwise no rescale could have fired, and the result
+  // is bitwise the scaled one); on the first such evaluation the engine is re-created with
+  // rescaling and the evaluation redone, and it stays scaled.  setUnderflowScaling(true / false)
+  // forces it on / off (off: the reference's arithmetic, which may underflow); a call after
+  // the data are set re-creates the engine when the choice changes it (and re-evaluates an
+  // initialized object).
+  void setUnderflowScaling(bool yn);
+  bool underflowScalingActive() const { return scalingMode_ == 1 || (scalingMode_ < 0 && scaledNow_); }
   // Branch-length-only changes re-evaluate just the ancestors of the changed branches
   // (default); false restores the reference's full traversal on every change.
   void setIncrementalRecompute(bool yn) { incremental_ = yn; }
@@ -212,6 +231,10 @@ class AbstractPlkTreeLikelihood : public virtual TreeLikelihood {
 
 class RHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
   SubstitutionModel* model_;  // not owned
+
+ protected:
+  void uploadData() override;
+  void uploadModels() override;
 
  public:
   RHomogeneousTreeLikelihood(const Tree& tree, SubstitutionModel* model, DiscreteDistribution* rDist,
@@ -264,6 +287,8 @@ class RNonHomogeneousTreeLikelihood : public AbstractPlkTreeLikelihood {
   void initBranchLengthsParameters() override;
   std::vector<const Node*> applyBranchLengths() override;
   bool analyticDerivatives(const std::string& variable, double* d1, double* d2) const override;
+  void uploadData() override;
+  void uploadModels() override;
 
  public:
   RNonHomogeneousTreeLikelihood(const Tree& tree, const SiteContainer& data, SubstitutionModelSet* modelSet,

@@ -162,6 +162,7 @@ void AbstractPlkTreeLikelihood::setDataImpl(const SiteContainer& sites, const Al
   data_.reset(sites.clone());
   nbStates_ = model.getNumberOfStates();
   initialized_ = false;
+  scaledNow_ = false;  // new data: unscaled first again
 }
 
 void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
@@ -169,12 +170,12 @@ void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
     plk_destroy(engine_);
     engine_ = nullptr;
   }
-  // Default: exact power-of-two rescaling unless the tree is small enough that no site can
-  // leave the double range.  A tip on a minimum-length branch with a mismatch contributes about
-  // ln(1e-6 * rate) ~ -20 to a site's log-likelihood, so 32 tips stay above -708 whatever the
-  // data; beyond that (or for large state spaces) scaling is on.
-  const bool scaling =
-      scalingMode_ >= 0 ? scalingMode_ == 1 : (nTips_ > 32 || nTips_ * std::log((double)nbStates_) > 300.);
+  // Exact power-of-two rescaling when forced, or after an unscaled evaluation flagged underflow
+  // (setUnderflowScaling, switchToScaledEngine)
+  engineModels_ = nModels;
+  engineGuard_ = nonNegGuard;
+  const bool scaling = underflowScalingActive();
+  engineScaled_ = scaling;
   unsigned flags = (scaling ? (unsigned)PLK_FLAG_SCALING : 0u) | (nonNegGuard ? (unsigned)PLK_FLAG_NONNEG_GUARD : 0u) |
                    extraFlags_;
   // usePatterns (the reference default): per-subtree site-pattern compression on the device
@@ -412,6 +413,7 @@ void AbstractPlkTreeLikelihood::evaluateTree(const std::vector<const Node*>& pno
     check(plk_update_pmatrices(engine_, (int)br.size(), br.data(), mod.data(), t.data(), PLK_DERIV_P),
           "plk_update_pmatrices");
     minusLogLik_ = -reduceRoot();
+    if (underflowed()) switchToScaledEngine();
     return;
   }
   double lnl = 0.;
@@ -419,6 +421,35 @@ void AbstractPlkTreeLikelihood::evaluateTree(const std::vector<const Node*>& pno
                      rootEngine_, &lnl, nullptr),
         "plk_evaluate");
   minusLogLik_ = -lnl;
+  if (underflowed()) switchToScaledEngine();
+}
+
+// plk_root_underflow after an unscaled evaluation in the default mode (include/plk.h: a 0 proves
+// the rescaling engine would have returned bitwise the same lnL)
+bool AbstractPlkTreeLikelihood::underflowed() const {
+  if (scalingMode_ >= 0 || scaledNow_) return false;
+  int flag = 0;
+  check(plk_root_underflow(engine_, &flag), "plk_root_underflow");
+  return flag != 0;
+}
+
+void AbstractPlkTreeLikelihood::setUnderflowScaling(bool yn) {
+  scalingMode_ = yn ? 1 : 0;
+  scaledNow_ = false;
+  if (!engine_ || engineScaled_ == underflowScalingActive()) return;
+  createEngine(engineModels_, engineGuard_);
+  uploadData();
+  allDirty_ = true;
+  if (initialized_) fireParameterChanged(getParameters());
+}
+
+void AbstractPlkTreeLikelihood::switchToScaledEngine() {
+  scaledNow_ = true;
+  stats_.scaledFallbacks++;
+  createEngine(engineModels_, engineGuard_);
+  uploadData();
+  uploadModels();
+  evaluateTree(std::vector<const Node*>(nodes_.begin(), nodes_.end()), false);
 }
 
 // Full postorder traversal (Likelihood/RHomogeneousTreeLikelihood.cpp:795-798), or,
@@ -659,7 +690,15 @@ void RHomogeneousTreeLikelihood::setData(const SiteContainer& sites) {
   if (verbose_) ApplicationTools::displayTask("Initializing data structure");
   setDataImpl(sites, model_->getAlphabet(), *model_);
   createEngine(1, true);
-  // leaf codes and init values (getInitValue) on the device
+  uploadData();
+  if (verbose_) {
+    ApplicationTools::displayTaskDone();
+    ApplicationTools::displayResult("Number of distinct sites", nbDistinctSites_);
+  }
+}
+
+// leaf codes and init values (getInitValue), pattern weights
+void RHomogeneousTreeLikelihood::uploadData() {
   const Alphabet* a = model_->getAlphabet();
   const int nc = a->getNumberOfCodes();
   std::vector<double> table((size_t)nc * nbStates_);
@@ -673,10 +712,12 @@ void RHomogeneousTreeLikelihood::setData(const SiteContainer& sites) {
   }
   std::vector<double> w(rootWeights_.begin(), rootWeights_.end());
   check(plk_set_pattern_weights(engine_, w.data()), "plk_set_pattern_weights");
-  if (verbose_) {
-    ApplicationTools::displayTaskDone();
-    ApplicationTools::displayResult("Number of distinct sites", nbDistinctSites_);
-  }
+}
+
+void RHomogeneousTreeLikelihood::uploadModels() {
+  uploadEigen(0, *model_);
+  uploadRates();
+  uploadRootFrequencies(model_->getFrequencies());
 }
 
 void RHomogeneousTreeLikelihood::initialize() {
@@ -717,9 +758,7 @@ void RHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList&) {
   const bool rateChanged = rateDistribution_->matchParametersValues(getParameters());
   if (allDirty_ || modelChanged || rateChanged) {
     allDirty_ = false;
-    uploadEigen(0, *model_);
-    uploadRates();
-    uploadRootFrequencies(model_->getFrequencies());
+    uploadModels();
     evaluateTree(std::vector<const Node*>(nodes_.begin(), nodes_.end()), false);
   } else {
     evaluateTree(changed, true);
@@ -792,6 +831,11 @@ void RNonHomogeneousTreeLikelihood::setData(const SiteContainer& sites) {
   const SubstitutionModel& m0 = *modelSet_->getModel(0);
   setDataImpl(sites, modelSet_->getAlphabet(), m0);
   createEngine(modelSet_->getNumberOfModels(), false);
+  uploadData();
+}
+
+void RNonHomogeneousTreeLikelihood::uploadData() {
+  const SubstitutionModel& m0 = *modelSet_->getModel(0);
   const Alphabet* a = modelSet_->getAlphabet();
   const int nc = a->getNumberOfCodes();
   std::vector<double> table((size_t)nc * nbStates_);
@@ -888,6 +932,12 @@ ParameterList RNonHomogeneousTreeLikelihood::getSubstitutionModelParameters() co
   return modelSet_->getParameters().getCommonParametersWith(getParameters());
 }
 
+void RNonHomogeneousTreeLikelihood::uploadModels() {
+  for (size_t m = 0; m < modelSet_->getNumberOfModels(); m++) uploadEigen((int)m, *modelSet_->getModel(m));
+  uploadRates();
+  uploadRootFrequencies(modelSet_->getRootFrequencies());
+}
+
 void RNonHomogeneousTreeLikelihood::computeAllTransitionProbabilities() {
   for (size_t m = 0; m < modelSet_->getNumberOfModels(); m++) uploadEigen((int)m, *modelSet_->getModel(m));
   uploadRates();
@@ -908,9 +958,7 @@ void RNonHomogeneousTreeLikelihood::fireParameterChanged(const ParameterList&) {
   const bool rateChanged = rateDistribution_->matchParametersValues(getParameters());
   if (allDirty_ || rateChanged) {
     allDirty_ = false;
-    for (size_t m = 0; m < modelSet_->getNumberOfModels(); m++) uploadEigen((int)m, *modelSet_->getModel(m));
-    uploadRates();
-    uploadRootFrequencies(modelSet_->getRootFrequencies());
+    uploadModels();
     evaluateTree(std::vector<const Node*>(nodes_.begin(), nodes_.end()), false);
     return;
   }

@@ -38,6 +38,7 @@ EXPORTS = [
     "plk_kernel_path", "plk_evaluate", "plk_compressed_work", "plk_all_branch_derivatives",
     "plk_get_timing_ex", "plk_traversal_work", "plk_create_multi", "plk_shard_count", "plk_comm_get_id",
     "plk_comm_init", "plk_get_dpmatrix", "plk_root_pair_derivatives", "plk_get_fanout",
+    "plk_root_underflow",
 ]
 
 
@@ -93,6 +94,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
                               ct.c_uint, P(ct.c_void_p)], ct.c_int),
         "plk_shard_count": ([ct.c_void_p, P(ct.c_int)], ct.c_int),
         "plk_get_fanout": ([ct.c_void_p, ct.c_int, dp, dp, P(ct.c_int64)], ct.c_int),
+        "plk_root_underflow": ([ct.c_void_p, P(ct.c_int)], ct.c_int),
         "plk_comm_get_id": ([P(plk_comm_id)], ct.c_int),
         "plk_comm_init": ([ct.c_void_p, ct.c_int, ct.c_int, P(plk_comm_id)], ct.c_int),
         "plk_set_code_table": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
@@ -335,6 +337,14 @@ class Engine:
         self._chk(self.lib.plk_root_loglik(self.h, root, ct.byref(lnl), _d(sites) if want_sites else None,
                                            _d(blocks) if want_blocks else None))
         return lnl.value, sites, blocks
+
+    def root_underflow(self) -> bool:
+        """plk_root_underflow (unscaled handles): did the last root reduction meet a site
+        likelihood below 2^-255 (or <= 0, or NaN)?  False proves a scaled handle would have
+        returned bitwise the same lnL."""
+        f = ct.c_int(0)
+        self._chk(self.lib.plk_root_underflow(self.h, ct.byref(f)))
+        return bool(f.value)
 
     def branch_derivatives(self, branch: int):
         """(d lnL/dt, d2 lnL/dt2) for the branch above node `branch`."""

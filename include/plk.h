@@ -207,6 +207,19 @@ int plk_get_partials(plk_handle h, int node, double* out /* n_patterns x C x S, 
  * gives a result independent of how patterns are sharded across devices. */
 int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, double* block_sums);
 
+/* Underflow check of an UNSCALED handle (created without PLK_FLAG_SCALING): *flag = 1 when the
+ * last root reduction (plk_evaluate, plk_root_loglik, or a fused traversal's) met a site
+ * likelihood below 2^-255, or <= 0, or NaN; 0 otherwise.  Call it after the evaluation
+ * returned (plk_evaluate and plk_root_loglik synchronise).  A 0 proves that a handle with
+ * PLK_FLAG_SCALING would have returned bitwise the same lnL: partials are <= 1 and every
+ * node's joint maximum over (class, state) is <= each of its children's (P rows sum to 1), and
+ * a site's likelihood is <= its root's joint maximum, so every node's maximum was >= 2^-255
+ * (one bit of rounding margin above the 2^-256 rescaling threshold) and no rescale would have
+ * fired.  The Bio++ mirror evaluates unscaled first and falls back to a scaled handle only when
+ * the flag is set.  PLK_ERR_STATE on a scaled handle.  Replaces nothing in the reference, which
+ * has no scaling. */
+int plk_root_underflow(plk_handle h, int* flag);
+
 /* One likelihood evaluation as RHomogeneousTreeLikelihood::fireParameterChanged does it
  * (Likelihood/RHomogeneousTreeLikelihood.cpp:255-283): P(t) of the listed branches
  * (plk_update_pmatrices, P only), the postorder traversal (plk_update_partials) and the

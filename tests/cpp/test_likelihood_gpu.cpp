@@ -366,9 +366,71 @@ static void shortBranchScalingCase() {
   on.setUnderflowScaling(true);
   on.initialize();
   const double a = def.getValue(), b = on.getValue();
-  std::cout << std::setprecision(17) << "150 taxa, branches 1e-6: default -lnL " << a << ", scaling on " << b << std::endl;
+  std::cout << std::setprecision(17) << "150 taxa, branches 1e-6: default -lnL " << a << ", scaling on " << b
+            << ", fallbacks " << def.getEvaluationStats().scaledFallbacks << std::endl;
   if (!std::isfinite(a) || a < 1000.) failures++;
-  expectNear("default rule == scaling on", a, b, 1e-9 * std::fabs(b));
+  // the unscaled first evaluation underflows: the default falls back to the rescaling engine
+  // once and returns the forced-scaling value bitwise
+  if (def.getEvaluationStats().scaledFallbacks != 1 || !def.underflowScalingActive()) failures++;
+  if (a != b) {
+    std::cout << "FAIL default (fallback) != scaling on, bitwise" << std::endl;
+    failures++;
+  }
+}
+
+// 64 taxa (a balanced tree, branches 0.02-0.1, 300 random DNA sites): no site likelihood comes
+// near 2^-255, so the default stays on the unscaled engine -- no fallback -- and every value
+// equals the forced-scaling engine's bitwise, through branch-length changes
+static void unscaledFirstCase() {
+  const int n = 64, L = 300;
+  std::string nwk = "t0:0.05";
+  {
+    std::vector<std::string> level;
+    unsigned long long x = 777;
+    auto len = [&]() {
+      x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+      return std::to_string(0.02 + 0.08 * (double)((x >> 33) & 0xffff) / 65536.0);
+    };
+    for (int i = 0; i < n; i++) level.push_back("t" + std::to_string(i));
+    while (level.size() > 1) {
+      std::vector<std::string> next;
+      for (size_t i = 0; i + 1 < level.size(); i += 2)
+        next.push_back("(" + level[i] + ":" + len() + "," + level[i + 1] + ":" + len() + ")");
+      level = next;
+    }
+    nwk = level[0] + ";";
+  }
+  std::unique_ptr<TreeTemplate<Node> > tree(TreeTemplateTools::parenthesisToTree(nwk));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  unsigned long long x = 4242;
+  for (int i = 0; i < n; i++) {
+    std::string s;
+    for (int j = 0; j < L; j++) {
+      x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+      s += "ACGT"[(x >> 33) & 3];
+    }
+    aln.addSequence(BasicSequence("t" + std::to_string(i), s, dna));
+  }
+  GTR model(dna, 1.2, 0.4, 0.6, 0.8, 0.5, 0.30, 0.20, 0.25, 0.25);
+  GammaDiscreteRateDistribution rdist(4, 0.5);
+  RHomogeneousTreeLikelihood def(*tree, aln, &model, &rdist, true, false);
+  def.initialize();
+  RHomogeneousTreeLikelihood on(*tree, aln, &model, &rdist, true, false);
+  on.setUnderflowScaling(true);
+  on.initialize();
+  int mismatches = def.getValue() != on.getValue();
+  ParameterList bl = def.getBranchLengthsParameters();
+  for (int k = 1; k <= 3; k++) {
+    for (size_t i = 0; i < bl.size(); i++) bl[i].setValue(bl[i].getValue() * (1.0 + 0.1 * k));
+    def.setParameters(bl);
+    on.setParameters(bl);
+    mismatches += def.getValue() != on.getValue();
+  }
+  std::cout << std::setprecision(17) << "64 taxa: default -lnL " << def.getValue() << ", scaling on " << on.getValue()
+            << ", fallbacks " << def.getEvaluationStats().scaledFallbacks << ", bitwise mismatches " << mismatches
+            << std::endl;
+  if (mismatches || def.getEvaluationStats().scaledFallbacks != 0 || def.underflowScalingActive()) failures++;
 }
 
 int main() {
@@ -381,6 +443,7 @@ int main() {
     complexEigenModelCase();
     gapCase();
     shortBranchScalingCase();
+    unscaledFirstCase();
   } catch (Exception& e) {
     std::cerr << e.what() << std::endl;
     return 1;

@@ -76,6 +76,12 @@ int main(int argc, char** argv) {
   RHomogeneousTreeLikelihood tl(*tree, *sites, model.get(), rdist.get(), true, false);
   tl.initialize();
   const auto c2 = std::chrono::steady_clock::now();
+  // the same likelihood with rescaling forced on: the default (unscaled first, exact fallback)
+  // must return its values bitwise (checked after the timed steps)
+  std::unique_ptr<RHomogeneousTreeLikelihood> forced(
+      new RHomogeneousTreeLikelihood(*tree, *sites, model.get(), rdist.get(), true, false));
+  forced->setUnderflowScaling(true);
+  forced->initialize();
   sites.reset();
   ParameterList bl = tl.getBranchLengthsParameters();
   std::vector<ParameterList> sets(2, bl);
@@ -108,6 +114,13 @@ int main(int argc, char** argv) {
   plk_get_timing_ex(tl.getEngine(), &tk);
   plk_set_timing(tl.getEngine(), 0);
   const double nk = tk.evaluations > 0 ? (double)tk.evaluations : 1.0;
+  int mismatches = 0;
+  for (int k = 0; k < 2; k++) {
+    tl.setParameters(sets[k]);
+    forced->setParameters(sets[k]);
+    mismatches += tl.getValue() != forced->getValue();
+  }
+  forced.reset();
   const size_t D = tl.getNumberOfDistinctSites();
   const int internal = taxa - 2;
   const auto& st = tl.getEvaluationStats();
@@ -115,11 +128,13 @@ int main(int argc, char** argv) {
       "{\"bench\": \"mirror\", \"config\": \"%s\", \"taxa\": %d, \"sites\": %zu, \"distinct_patterns\": %zu, "
       "\"internal_nodes\": %d, \"steps\": %d, \"warmup\": %d, \"ms_per_step\": %.5f, \"updates_per_s\": %.6g, "
       "\"kernel_path\": \"%s\", \"minus_lnl\": %.12f, \"full_traversals\": %zu, \"evaluations\": %zu, "
+      "\"scaled_fallbacks\": %zu, \"scaling_active\": %s, \"bitwise_mismatches_vs_forced_scaling\": %d, "
       "\"simulate_s\": %.2f, \"setup_s\": %.2f, \"checksum\": %.6f, \"host_us_per_eval\": {\"pmat_call\": %.2f, "
       "\"traversal_call\": %.2f, \"blocks_call\": %.2f, \"wait\": %.2f, \"sum\": %.2f, \"caller\": %.2f}, "
       "\"kernel_ms_per_eval\": {\"partials\": %.4f, \"tables\": %.4f, \"pmatrix\": %.4f, \"root\": %.4f}}\n",
       cfg.c_str(), taxa, P, D, internal, steps, warmup, ms, (double)D * internal / (ms * 1e-3),
-      plk_kernel_path(tl.getEngine()), tl.getValue(), st.fullTraversals, st.evaluations,
+      plk_kernel_path(tl.getEngine()), tl.getValue(), st.fullTraversals, st.evaluations, st.scaledFallbacks,
+      tl.underflowScalingActive() ? "true" : "false", mismatches,
       std::chrono::duration<double>(c1 - c0).count(), std::chrono::duration<double>(c2 - c1).count(), v,
       tm.host_us[0] / ne, tm.host_us[1] / ne, tm.host_us[2] / ne, tm.host_us[3] / ne, tm.host_us[4] / ne,
       tm.host_us[5] / ne, tk.partials_ms / nk, tk.tables_ms / nk, tk.pmat_ms / nk, tk.root_ms / nk);
