@@ -282,7 +282,6 @@ struct plk_handle_s {
   int prog_dm = 0;                        // register levels the program was cut for
   bool prog_jit = false;                  // program cut for the tree-specialised kernel
   bool prog_ciw = false;                  // ... with every class of a pattern in one wave
-  bool prog_pcs = false;                  // ... one class per wave with per-class scaling (jit_pcs)
   int prog_tmax = 0;                      // tips per fragment the program was cut for
   int prog_nf = 0;                        // fragments of the cached program
   std::vector<std::vector<int> > prog_tiers;  // fragment ids per tier
@@ -323,7 +322,6 @@ struct plk_handle_s {
   JitPlan jit_plan;            // table units / events of the current program (plk_jit.hpp)
   bool jit_plan_valid = false;
   int jit_plan_U = 0, jit_plan_budget = -1;
-  bool jit_plan_pcs = false;
   uint8_t* d_ucodes = nullptr;  // code row of every table unit of jit_plan (unit_codes_kernel)
   int2* d_units = nullptr;      // (ta, tb) of every unit
   size_t ucodes_cap = 0, units_cap = 0;
@@ -1058,9 +1056,7 @@ int plk_create(int device, int n_states, int n_classes, int64_t n_patterns, int 
   // with PLK_FLAG_DOUBLE_RECURSIVE one more slot and matrix per node (U_v, M_f)
   if ((rc = dalloc(h, (void**)&h->partials, (size_t)n_slots * h->slot_stride * sizeof(double)))) return bail(rc);
   if (flags & PLK_FLAG_SCALING) {
-    // (4 states, several classes: room for per-class counts [slot][C][n_pad], jit_pcs)
-    const size_t per_slot = (size_t)h->n_pad * ((n_states == 4 && n_classes > 1) ? n_classes : 1);
-    if ((rc = dalloc(h, (void**)&h->scale, (size_t)n_slots * per_slot * sizeof(int32_t)))) return bail(rc);
+    if ((rc = dalloc(h, (void**)&h->scale, (size_t)n_slots * h->n_pad * sizeof(int32_t)))) return bail(rc);
   }
   if ((rc = dalloc(h, (void**)&h->codes, (size_t)(n_tips + kScratchTips) * h->n_pad))) return bail(rc);
   if ((rc = dalloc(h, (void**)&h->pmats, (size_t)h->n_mats * n_classes * S2 * sizeof(double)))) return bail(rc);
@@ -1573,28 +1569,11 @@ bool jit_treeM(plk_handle h) {
 // exchange (the per-node barrier of the one-class-per-wave layout costs ~2x on cfg5),
 // at the price of C x the registers per level (so a lower fragment height).  Default
 // for scaling runs; PLK_JIT_CIW=0/1 overrides.
-bool jit_pcs(plk_handle h);
-
 bool jit_ciw(plk_handle h) {
-  if (!jit_tree4(h) || h->C == 1 || jit_pcs(h)) return false;
+  if (!jit_tree4(h) || h->C == 1) return false;
   const char* e = tune_get("JIT_CIW");
   if (e) return e[0] == '1';
   return (h->flags & PLK_FLAG_SCALING) != 0;
-}
-
-// Per-class scaling (plk_jit.hpp PCS_): with rescaling, one class per wave and each class
-// rescaled on its own (its own power-of-two count per pattern), the classes meeting only at
-// the root reduction -- no cross-wave exchange or barrier per node (what one class per wave
-// with the joint rescale pays) and a quarter of the registers per level of every class in
-// the wave.  Exact like the joint convention: the partials differ from it only by powers of
-// two, so without any rescale the result is bitwise the same, and with rescales it agrees to
-// the last bits of the final log (tested against the oracle at 1e-12).  lnL-only traversals
-// only: the fragment roots they store carry per-class counts, which no other kernel reads
-// (a materialising traversal -- plk_get_partials, derivatives -- uses the joint convention).
-// PLK_TUNE JIT_PCS=0 keeps classes in the wave.
-bool jit_pcs(plk_handle h) {
-  if (!jit_tree4(h) || h->C == 1 || !(h->flags & PLK_FLAG_SCALING) || !(h->flags & PLK_FLAG_LNL_ONLY)) return false;
-  return !tune_is("JIT_PCS", '0');
 }
 
 // tips whose tables (C x codes-in-use x 4 doubles each) fit one fragment's LDS budget
@@ -1687,9 +1666,7 @@ int tree_levels(plk_handle h) {
     case FK_TREE4:
       if (!jit_tree4(h)) return kTree4Levels;
       // classes in the wave: cfg5 DM 5 / 6 / 7 = 0.70 / 0.55 / 0.84 ms at G = 4
-      // per-class scaling takes the same cut (at DM 10 the edge and tip caps cut the 512-taxon
-      // tree into four tiers instead of two: 0.63 vs 0.36 ms at 250 k patterns)
-      return (jit_ciw(h) || jit_pcs(h)) ? tune_int("JIT_DM", 6, 2, 16) : tune_int("JIT_DM", 10, 2, 32);
+      return jit_ciw(h) ? tune_int("JIT_DM", 6, 2, 16) : tune_int("JIT_DM", 10, 2, 32);
     // jit_treeM (20 states): 4 levels (DM 3 / 4 = 3.69 / 3.43 ms on cfg3); the treeM
     // interpreter: 3 (with cherry tables 7.8 ms on cfg3, 2 levels 8.7 ms)
     case FK_TREEM:
@@ -1910,7 +1887,6 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   h->prog_jit = jit_tree4(h);
   h->prog_jitm = jit_treeM(h);
   h->prog_ciw = jit_ciw(h);
-  h->prog_pcs = jit_pcs(h);
   h->prog_tmax = TMAX;
   h->prog_root = root_reduce;
   h->cherry3.swap(cherry3);
@@ -1920,8 +1896,7 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   for (int n = nt; n < h->n_nodes; ++n)
     if (produced[n]) {
       const bool cut = frag_of[n] >= 0 && frag_roots[frag_of[n]] == n;
-      // (a per-class scaled fragment root serves only this program's later tiers)
-      h->prog_mat_after[n - nt] = (materialize || (cut && n != root_reduce && !h->prog_pcs)) ? 1 : 0;
+      h->prog_mat_after[n - nt] = (materialize || (cut && n != root_reduce)) ? 1 : 0;
       h->materialized[n - nt] = (char)h->prog_mat_after[n - nt];
     }
   return PLK_OK;
@@ -1973,7 +1948,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   const bool reduce = h->pi_set && h->rates_set;
   const bool same = h->prog_ops.size() == (size_t)n_ops && h->prog_materialize == materialize &&
                     h->prog_reduce == reduce && h->prog_dm == tree_levels(h) && h->prog_jit == jit_tree4(h) && h->prog_ciw == jit_ciw(h) &&
-                    h->prog_pcs == jit_pcs(h) &&
                     h->prog_jitm == jit_treeM(h) &&
                     (!h->prog_jit || h->prog_tmax == jit_tip_cap(h)) &&
                     std::memcmp(h->prog_ops.data(), ops, n_ops * sizeof(plk_op)) == 0;
@@ -2066,13 +2040,11 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.pin = true;  // accumulator pinning: cfg2 0.244 -> 0.241, cfg5 1.04 -> 0.93 ms
     sh.U = h->n_codes;
     sh.scale = (h->flags & PLK_FLAG_SCALING) != 0;
-    sh.pcs = h->prog_pcs;
     // cherries read one product table (plk_jit.hpp: JitUnit) while a fragment's tables stay
     // within PLK_JIT_PAIR_KB (0: no pairs)
     const int budget = tune_int("JIT_PAIR_KB", 64, 0, 150) * 1024 / (int)sizeof(double);
-    if (!h->jit_plan_valid || h->jit_plan_U != sh.U || h->jit_plan_budget != budget || h->jit_plan_pcs != sh.pcs) {
-      h->jit_plan = jit_plan(h->prog_host, h->frag_starts_host, sh.C, sh.U, budget, sh.scale, sh.pcs);
-      h->jit_plan_pcs = sh.pcs;
+    if (!h->jit_plan_valid || h->jit_plan_U != sh.U || h->jit_plan_budget != budget) {
+      h->jit_plan = jit_plan(h->prog_host, h->frag_starts_host, sh.C, sh.U, budget, sh.scale);
       h->jit_plan_valid = true;
       h->jit_plan_U = sh.U;
       h->jit_plan_budget = budget;
@@ -2108,8 +2080,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // otherwise the G with the most resident waves (jit_auto_groups; cfg2 with cherry
     // tables: G = 3, 0.140 ms, G = 2 0.150, G = 4 0.162)
     sh.G = tune_int("JIT_G", 0, 0, 8);
-    // (per-class scaling has no per-node barrier: the G with the most resident waves)
-    if (sh.G == 0) sh.G = h->prog_ciw ? 8 : (sh.scale && !sh.pcs) ? 1 : jit_auto_groups(sh);
+    if (sh.G == 0) sh.G = h->prog_ciw ? 8 : sh.scale ? 1 : jit_auto_groups(sh);
     // two patterns per lane halve the P(t) reads per FMA but double the registers:
     // measured slower (cfg2 0.255-0.301 vs 0.241 ms), so opt-in; not with speculation
     sh.PW = 1;
@@ -2133,7 +2104,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.pin != h->jit_shape.pin ||
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
-        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.pcs != h->jit_shape.pcs) {
+        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;

@@ -213,9 +213,7 @@ __device__ __forceinline__ void flag_risky(int& dng, const double (&v)[N]) {
 template <int C, int CW, int PW, int NWT>
 __device__ __forceinline__ void rescale(double (&v)[4 * CW * PW], int (&cnt)[PW], double* xch, int w, int g) {
   constexpr int NW = C / CW;
-  // one wave holds every class of its patterns (the joint check in registers), or per-class
-  // scaling (PCS_: each class wave rescales its own class and keeps its own count)
-  if (NW == 1 || PCS_) {
+  if (NW == 1) {
 #pragma unroll
     for (int pw = 0; pw < PW; ++pw) {
       int mh = 0;
@@ -268,9 +266,8 @@ __device__ __forceinline__ void rescale(double (&v)[4 * CW * PW], int (&cnt)[PW]
     }
 }
 
-// off: the lane's first pattern in the slot (tile layout); pattern pw is 64 further.  Scale
-// counts: one per pattern (joint), or one per class and pattern (PCS_: [slot][C][n_pad])
-template <int C, int CW, int PW, bool SCALE>
+// off: the lane's first pattern in the slot (tile layout); pattern pw is 64 further
+template <int CW, int PW, bool SCALE>
 __device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0,
                                       const double (&v)[4 * CW * PW], const int (&cnt)[PW], bool gv) {
   if (!gv) return;  // a group past the last pattern (ragged last super-block) recomputes group 0
@@ -280,10 +277,7 @@ __device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, 
   for (int pw = 0; pw < PW; ++pw)
 #pragma unroll
     for (int i = 0; i < 4 * CW; ++i) __builtin_nontemporal_store(v[4 * CW * pw + i], dst + 64 * pw + (i64)i * kTile);
-  if (SCALE && PCS_)
-#pragma unroll
-    for (int pw = 0; pw < PW; ++pw) a.scale[((i64)slot * C + c0) * a.n_pad + p + 64 * pw] = cnt[pw];
-  else if (SCALE && c0 == 0)
+  if (SCALE && c0 == 0)
 #pragma unroll
     for (int pw = 0; pw < PW; ++pw) a.scale[(i64)slot * a.n_pad + p + 64 * pw] = cnt[pw];
 }
@@ -314,32 +308,18 @@ __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[
       }
       t[pw][cw] = lc * a.probs[c0 + cw];
     }
-  // per-class scaling: the classes' counts travel beside their terms (second exchange
-  // buffer); each term is brought to the smallest count's scale, 2^-256 per count above it
-  // (exact while the product stays normal), and that count is taken off the log
-  double* xk = xch + PW * NWT * 64;
   if (NW > 1) {
     __syncthreads();
 #pragma unroll
-    for (int pw = 0; pw < PW; ++pw) {
-      xch[(pw * NWT + w) * 64 + lane] = t[pw][0];
-      if (PCS_) xk[(pw * NWT + w) * 64 + lane] = (double)cnt[pw];
-    }
+    for (int pw = 0; pw < PW; ++pw) xch[(pw * NWT + w) * 64 + lane] = t[pw][0];
     __syncthreads();
   }
   if (c0 == 0) {
 #pragma unroll
     for (int pw = 0; pw < PW; ++pw) {
       double l = 0.0;
-      int kmin = 0;
-      if (PCS_ && NW > 1) {
-        kmin = (int)xk[(pw * NWT + g * NW) * 64 + lane];
-        for (int c = 1; c < C; ++c) kmin = min(kmin, (int)xk[(pw * NWT + g * NW + c) * 64 + lane]);
-      }
       for (int c = 0; c < C; ++c) {
-        double li = NW > 1 ? xch[(pw * NWT + g * NW + c) * 64 + lane] : t[pw][c < CW ? c : 0];
-        if (PCS_ && NW > 1)
-          for (int k = (int)xk[(pw * NWT + g * NW + c) * 64 + lane]; k > kmin; --k) li *= kScaleThr;
+        const double li = NW > 1 ? xch[(pw * NWT + g * NW + c) * 64 + lane] : t[pw][c < CW ? c : 0];
         if (a.guard) {
           if (li > 0.0) l += li;
         } else {
@@ -348,7 +328,7 @@ __device__ __forceinline__ void reduce_root(const JArgs& a, const double (&acc)[
       }
       if (!a.guard && l < 0.0) l = 0.0;
       double r = jit_log(l);
-      if (SCALE) r -= (double)(PCS_ && NW > 1 ? kmin : cnt[pw]) * kLn2x256;
+      if (SCALE) r -= (double)cnt[pw] * kLn2x256;
       double wr = 0.0;
       const i64 pp = p + 64 * pw;
       if (gv && pp < a.n_patterns) {
@@ -404,7 +384,6 @@ struct JitShape {
   int L = 1;        // operand fetch lookahead (events)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
-  bool pcs = false;         // per-class scaling (one class per wave, no cross-wave rescale; see rescale)
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     // the second exchange buffer only serves the per-node rescale
@@ -471,7 +450,7 @@ struct JitPlan {
 // Cherries become pair units while the fragment's tables stay within pair_budget
 // doubles (0: no pairs; pairs need U * U <= 256 so that a combined code is one byte).
 inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts, int C, int U,
-                        int pair_budget, bool scale, bool pcs = false) {
+                        int pair_budget, bool scale) {
   JitPlan plan;
   plan.events.assign(starts.size(), {});
   plan.units.assign(starts.size(), {});
@@ -530,7 +509,7 @@ inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32
       off += u.tb < 0 ? single : C * U * U * 4;
       if (u.koff >= 0) {
         u.koff = off;
-        off += ((pcs ? C : 1) * U * U + 31) / 32 * 4;  // count bytes (per class with pcs), whole 32-byte rows
+        off += (U * U + 31) / 32 * 4;  // count bytes, whole 32-byte rows
       }
     }
     plan.NU = std::max(plan.NU, (int)un.size());
@@ -547,7 +526,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   std::string s;
   s.reserve(4096 * events.size() + 16384);
   s += sh.ppipe ? "#define PPIPE_ 1\n" : "#define PPIPE_ 0\n";  // read by the prelude's contrib
-  s += sh.pcs ? "#define PCS_ 1\n" : "#define PCS_ 0\n";        // ... rescale, store, reduce_root
   s += kJitPrelude;
   char buf[400];
   const std::string minw_s = sh.minw > 0 ? ", " + std::to_string(sh.minw) : std::string();
@@ -726,21 +704,16 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       const double* ra = a.tipP + (i64)ud.ta * (C_ * U_ * 4);
       const double* rb = a.tipP + (i64)ud.tb * (C_ * U_ * 4);
       const int ca = r / U_, cb = r - ca * U_;
-      double v[C_][4], m = 0.0, mc[C_];
-      for (int c = 0; c < C_; ++c) {
-        mc[c] = 0.0;
+      double v[C_][4], m = 0.0;
+      for (int c = 0; c < C_; ++c)
         for (int y = 0; y < 4; ++y) {
           v[c][y] = ra[(c * U_ + ca) * 4 + y] * rb[(c * U_ + cb) * 4 + y];
           m = fmax(m, v[c][y]);
-          mc[c] = fmax(mc[c], v[c][y]);
         }
-      }
-      const bool up = m > 0.0 && m < kScaleThr;  // the joint check (per class with PCS_)
+      const bool up = m > 0.0 && m < kScaleThr;
       for (int c = 0; c < C_; ++c) {
-        const bool upc = PCS_ ? (mc[c] > 0.0 && mc[c] < kScaleThr) : up;
-        if (upc)
+        if (up)
           for (int y = 0; y < 4; ++y) v[c][y] *= kScaleUp;
-        if (PCS_) reinterpret_cast<u8*>(tab + ud.koff)[c * (U_ * U_) + r] = upc ? 1 : 0;
         for (int x = 0; x < 4; ++x) {
           const double* P = pmats + ((i64)ud.br * C_ + c) * 16 + 4 * x;
           double t2 = P[0] * v[c][0];
@@ -750,7 +723,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
           dst[(c * U_ * U_ + r) * 4 + x] = t2;
         }
       }
-      if (!PCS_) reinterpret_cast<u8*>(tab + ud.koff)[r] = up ? 1 : 0;
+      reinterpret_cast<u8*>(tab + ud.koff)[r] = up ? 1 : 0;
     }
   }
   // the other tables: wave w stages units w, w + NWT_, ... of the fragment's other-unit list
@@ -823,14 +796,14 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
 #define TIPF(F, Q, k, TB, OFF, R) { CODEF(Q, k) ROWF(F, TB, OFF, R, Q) }
 // count bytes of a rescaling contribution unit
 #define KTF(K, KOFF, Q) { _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) \
-    K[pw_] += (int)reinterpret_cast<const u8*>(tab + (KOFF))[(PCS_ ? c0 * (U_ * U_) : 0) + (((Q) >> (8 * pw_)) & 255)]; }
+    K[pw_] += (int)reinterpret_cast<const u8*>(tab + (KOFF))[((Q) >> (8 * pw_)) & 255]; }
 // (slot numbers are laundered: otherwise every slot's base address is hoisted out of the
 // super-block loop into its own SGPR pair, and they spill)
 #define LOADF(F, FK, slot) { const i64 sl_ = (i64)launder_s(slot); \
     const double* L_ = a.partials + sl_ * a.slot_stride + toff; \
     _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
       _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[4 * CW_ * pw_ + i_] = L_[64 * pw_ + (i64)i_ * kTile]; \
-      if (SC_) FK[pw_] = a.scale[(PCS_ ? sl_ * C_ + c0 : sl_) * a.n_pad + p + 64 * pw_]; } }
+      if (SC_) FK[pw_] = a.scale[sl_ * a.n_pad + p + 64 * pw_]; } }
 #define SB __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::"v"(ptouch_));  // (keeps the touch loads)
   // Super-block order.  Static: blockIdx.x, + gridDim.x, ...  Dynamic (a.dyn): the first is
@@ -1021,7 +994,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
           if (e.b >= 0) {
             if (sh.scale) check_line(dd);
             if (e.a >= 0) {
-              snprintf(buf, sizeof(buf), "      store<C_, CW_, PW_, SC_>(a, %s, toff, p, c0, A%d, K%d, gv);\n",
+              snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %s, toff, p, c0, A%d, K%d, gv);\n",
                        sref(e.a).c_str(), dd, dd);
               s += buf;
             }
@@ -1041,7 +1014,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         } else {  // T_ROOT
           if (sh.scale) check_line(0);
           if (e.a >= 0) {
-            snprintf(buf, sizeof(buf), "      store<C_, CW_, PW_, SC_>(a, %s, toff, p, c0, A0, K0, gv);\n",
+            snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %s, toff, p, c0, A0, K0, gv);\n",
                      sref(e.a).c_str());
             s += buf;
           }

@@ -92,8 +92,7 @@ int main(int argc, char** argv) {
     sh.CW = argc > 5 && std::atoi(argv[5]) ? C : 1;
     sh.U = 16;
     sh.scale = scale;
-    sh.pcs = scale && sh.CW == 1 && argc > 6 && std::atoi(argv[6]) != 0;  // per-class scaling
-    const JitPlan plan = jit_plan(prog, starts, sh.C, sh.U, 64 * 1024 / 8, scale, sh.pcs);
+    const JitPlan plan = jit_plan(prog, starts, sh.C, sh.U, 64 * 1024 / 8, scale);
     sh.NT = plan.NU;
     sh.TD = plan.tab_doubles;
     sh.G = 1;

@@ -644,10 +644,6 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
         mask = rng.random(states.shape) < 0.05
         states[mask] = rng.integers(4, 15, size=mask.sum())
     flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | (plk.PLK_FLAG_SCALING if scaling else 0)
-    if scaling and mode == "lnl_only" and C > 1 and "PCS" not in extra:
-        # the interpreter rescales jointly; per-class scaling (the lnL-only default) agrees with
-        # it to the last bits of the log, not bitwise (test_jit_tree4_per_class_scaling)
-        set_tune(monkeypatch, "JIT_PCS", "0")
     res = {}
     for kernel in ("0", "1"):
         set_tune(monkeypatch, "JIT", kernel)
@@ -662,61 +658,6 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     if tree_kind.endswith("long") or "tiny" in extra.split():
         assert s1.min() < -256 * np.log(2)   # partials did go through rescaling
     lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=scaling)
-    check(l1, s1, lo, so)
-
-
-@pytest.mark.parametrize("C,tree_kind,n_patterns,extra", [
-    (4, "balanced64", 3000, ""), (2, "balanced300", 900, ""), (4, "balanced512", 2000, ""),
-    (4, "caterpillar200long", 600, ""), (2, "caterpillar200long", 300, "G=3"),
-    (4, "balanced64", 1500, "tiny"), (4, "balanced300", 900, "tiny acgt")])
-def test_jit_tree4_per_class_scaling(C, tree_kind, n_patterns, extra, monkeypatch):
-    """Per-class scaling (plk.hip jit_pcs, plk_jit.hpp PCS_: one class per wave, each class
-    rescaled on its own, classes brought to one scale at the root): the oracle's lnL and every
-    per-pattern lnL at 1e-12; the classes-in-the-wave kernel's (joint rescale, PLK_TUNE
-    JIT_PCS=0) agree to ~1e-15 per pattern, and bitwise when nothing was rescaled.  The long
-    caterpillar and the 1e-80 code ("tiny": the cherry tables' per-class checks) rescale."""
-    for kv in extra.split():
-        if "=" in kv:
-            k, v = kv.split("=")
-            set_tune(monkeypatch, "JIT_" + k, v)
-    if tree_kind.startswith("balanced"):
-        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=23, lo=0.05, hi=0.4)
-    else:
-        tree = _caterpillar(int(tree_kind[11:-4]), seed=5, lo=0.5, hi=1.5)
-    et = phylo.engine_tree(tree, unroot=not tree_kind.endswith("512"))
-    rng = np.random.default_rng(C * 7 + n_patterns)
-    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
-    rates, probs = phylo.gamma_rates(C, 0.5)
-    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, True, True, 5)
-    states = wl.simulate(0, n_patterns).astype(np.int32)
-    init = phylo.DNA.init_table
-    if "tiny" in extra.split():
-        init = np.array(init, dtype=np.float64, copy=True)
-        init[4] = 1e-80
-        mask = rng.random(states.shape) < 0.3
-        states[mask] = 4
-    elif "acgt" not in extra.split():
-        mask = rng.random(states.shape) < 0.05
-        states[mask] = rng.integers(4, 15, size=mask.sum())
-    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
-    res = {}
-    for pcs in ("0", "1"):
-        set_tune(monkeypatch, "JIT_PCS", pcs)
-        eng = engine_for(et, 4, C, n_patterns, states, init, rates, probs, m.pi, [m], flags=flags)
-        res[pcs] = run_engine(eng, et)
-        assert eng.kernel_path() == "jit_tree4"
-        if pcs == "1":
-            # a later materialising call (plk_get_partials) takes the joint kernel
-            node = et.ops[len(et.ops) // 2][0]
-            assert np.all(np.isfinite(eng.get_partials(node)))
-            assert run_engine(eng, et)[0] == res["1"][0]
-        del eng
-    (l0, s0, _), (l1, s1, _) = res["0"], res["1"]
-    assert np.allclose(s1, s0, rtol=1e-14, atol=0)
-    rescaled = s1.min() < -256 * np.log(2) or "tiny" in extra.split()
-    if not rescaled:
-        assert l0 == l1 and np.array_equal(s0, s1)
-    lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=True)
     check(l1, s1, lo, so)
 
 
@@ -761,7 +702,6 @@ def test_jit_same_shape_fragments_share_code(tmp_path, monkeypatch):
     block for all of them (plk_jit.hpp: per-fragment node / slot bases), and the result is
     the oracle's at 1e-12 (the bitwise interpreter tests cover the other shapes)."""
     monkeypatch.setenv("PLK_JIT_DUMP", str(tmp_path))
-    set_tune(monkeypatch, "JIT_PCS", "0")  # (every class in the wave: eight 64-tip fragments of one shape)
     C, n = 4, 1500
     tree = phylo.balanced_tree(256, seed=31, lo=0.05, hi=0.4)
     et = phylo.engine_tree(tree, unroot=False)
