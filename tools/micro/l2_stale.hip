@@ -94,5 +94,48 @@ int main() {
                   mode == 0 ? "read at once" : mode == 1 ? "L2 thrashed before the read" : "L2 flushed after free",
                   trials, reused, bad);
     }
+  // Bulk reuse: the round-4 staging was a small fine-grained allocation made after many other
+  // buffers were freed.  Free 64 coarse 256 KB buffers a kernel filled with OLD, then make 512
+  // small (16 KB) fine-grained / uncached allocations, write NEW into each from the host,
+  // thrash the L2s (or not), and read them all back in one kernel per buffer.
+  // (mode 2: the fix -- a system-scope release in workgroups on every XCD writes the freed
+  // buffers' dirty lines back before the host writes, then the L2s are thrashed)
+  for (int fl = 0; fl < 2; ++fl)
+    for (int thr_first = 0; thr_first < 3; ++thr_first) {
+      const size_t big_n = 32768, small_n = 2048;  // 256 KB, 16 KB
+      std::vector<unsigned long long*> xs(64), fs(512);
+      for (auto& x : xs) {
+        CK(hipMalloc(&x, big_n * 8));
+        fill<<<64, 256>>>(x, big_n, OLD);
+      }
+      CK(hipDeviceSynchronize());
+      for (auto& x : xs) CK(hipFree(x));
+      if (thr_first == 2) {
+        flush_l2<<<2048, 64>>>();
+        CK(hipDeviceSynchronize());
+      }
+      for (auto& f : fs) {
+        CK(hipExtMallocWithFlags((void**)&f, small_n * 8, flags[fl]));
+        for (size_t i = 0; i < small_n; ++i) f[i] = NEW;
+      }
+      __atomic_thread_fence(__ATOMIC_SEQ_CST);
+      if (thr_first) {
+        thrash<<<2048, 256>>>(thr, big / 8);
+        CK(hipDeviceSynchronize());
+      }
+      long long bad = 0, overlap = 0;
+      for (auto& f : fs) {
+        copy<<<8, 256>>>(f, out, small_n);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h.data(), out, small_n * 8, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < small_n; ++i) bad += h[i] != NEW;
+        for (auto& x : xs) overlap += (char*)f >= (char*)x && (char*)f < (char*)x + big_n * 8;
+      }
+      std::printf("bulk %s, %s: 512 x 16 KB after 64 x 256 KB freed, %lld inside a freed range, %lld words not NEW\n",
+                  fl == 0 ? "fine-grained" : "uncached",
+                  thr_first == 2 ? "L2 written back after the free, then thrashed" : thr_first ? "L2 thrashed" : "read at once",
+                  overlap, bad);
+      for (auto& f : fs) CK(hipFree(f));
+    }
   return 0;
 }
