@@ -276,9 +276,6 @@ struct plk_handle_s {
   size_t d_frag_cap = 0;
   unsigned* d_sbctr = nullptr;          // jit_tree4 dynamic super-block counters, one per fragment,
   size_t d_sbctr_cap = 0;               // then the exit-ticket counter (all 0 between launches)
-  unsigned* d_sbtk = nullptr;           // fused root fragment: one counter per super-block (0 between launches)
-  size_t d_sbtk_cap = 0;
-  unsigned long long* d_fdbg = nullptr;  // (measurement only, PLK_TUNE JIT_FUSEDBG=5) cycle sums
   std::vector<plk_op> prog_ops;           // op list the cached program was built from
   bool prog_materialize = false;
   bool prog_reduce = false;
@@ -1113,8 +1110,7 @@ int plk_destroy(plk_handle h) {
                   h->d_ops, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
                   h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre, h->d_sbctr,
-                  h->d_cherry_rows, h->d_sbtk, h->d_fdbg};
-
+                  h->d_cherry_rows};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) (void)hipHostFree(h->h_req);
@@ -2102,29 +2098,13 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // wave sum must wait for the store and the counter's atomic round trip (~3 us) before
     // its workgroup's next super-block barrier, in every super-block.  Off; the formal
     // release/acquire form (an L2 write-back per wave) was slower still (round 1)
-    // (Experiment, opt-in PLK_TUNE JIT_FUSE=1, measured slower and removed in the next commit:
-    // profiles/r05/ab_runs.md.)  A second and last tier of one table-free fragment (cfg5: the
-    // root fragment over the eight stored 64-tip subtree roots) runs inside the first tier's
-    // launch: per super-block, the workgroup that finishes its last first-tier fragment reads
-    // the roots back with sc1 loads and reduces the root (plk_jit.hpp JitShape::fuse_root).
-    sh.fuse_root = -1;
-    sh.fuse_nf = 0;
-    if (h->prog_tiers.size() == 2 && h->prog_tiers[1].size() == 1 && tune_is("JIT_FUSE", '1')) {
-      const int fr = h->prog_tiers[1][0];
-      if (h->jit_plan.units[(size_t)fr].empty()) {
-        sh.fuse_root = fr;
-        sh.fuse_nf = (int)h->prog_tiers[0].size();
-        sh.fuse_dbg = tune_int("JIT_FUSEDBG", 0, 0, 5);
-      }
-    }
     if (sh.lds_bytes() > 160 * 1024 - 64)  // (less the kernel's static LDS word)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
     if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW ||
         sh.pin != h->jit_shape.pin ||
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
-        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.fuse_root != h->jit_shape.fuse_root ||
-        sh.fuse_nf != h->jit_shape.fuse_nf || sh.fuse_dbg != h->jit_shape.fuse_dbg) {
+        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
@@ -2148,25 +2128,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.dyn = tune_is("JIT_DYN", '0') ? 0 : 1;  // (per launch below)
     ja.exit_ctr = h->d_sbctr + h->prog_nf;  // (null per launch below when not dynamic)
     ja.uflow = a.uflow;
-    ja.sb_tk = nullptr;
-    if (sh.fuse_root >= 0) {
-      const size_t need = (size_t)ja.n_sblocks * sizeof(unsigned);
-      if (h->d_sbtk_cap < need) {
-        int rc = ensure_cap(h, (void**)&h->d_sbtk, &h->d_sbtk_cap, need);
-        if (rc) return rc;
-        HIPCHK(h, hipMemsetAsync(h->d_sbtk, 0, h->d_sbtk_cap, h->stream));  // the kernel leaves them at 0
-      }
-      ja.sb_tk = h->d_sbtk;
-    }
-    ja.dbg = nullptr;
-    if (sh.fuse_dbg == 5) {
-      if (!h->d_fdbg) {
-        int rc = dalloc(h, (void**)&h->d_fdbg, 8 * sizeof(unsigned long long));
-        if (rc) return rc;
-        HIPCHK(h, hipMemsetAsync(h->d_fdbg, 0, 8 * sizeof(unsigned long long), h->stream));
-      }
-      ja.dbg = h->d_fdbg;
-    }
   }
   const bool jitm = kind == FK_TREEM && h->prog_jitm;
   JMArgs ma;
@@ -2216,12 +2177,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   h->kernel_path = jit ? "jit_tree4" : jitm ? "jit_treeM" : kind == FK_TREEM ? "treeM" : "tree4";
   int first = 0;
   for (const auto& t : h->prog_tiers) {
-    if (jit && sh.fuse_root >= 0 && first == sh.fuse_root) {
-      // (ran inside the first tier's launch)
-      if ((int)h->jit_frag_gx.size() > first) h->jit_frag_gx[(size_t)first] = h->jit_last_gx;
-      first += (int)t.size();
-      continue;
-    }
     a.frag_start = h->d_frag + first;
     dim3 grid((unsigned)(h->n_pad / 64), (unsigned)t.size());
     EventPair ev;
@@ -4007,12 +3962,6 @@ int plk_get_timing_ex(plk_handle h, plk_timing* out) {
   hipSetDevice(h->device);
   int rc = collect_events(h);
   if (rc) return rc;
-  if (h->d_fdbg) {  // (measurement only, PLK_TUNE JIT_FUSEDBG=5)
-    unsigned long long d[5] = {};
-    if (hipMemcpy(d, h->d_fdbg, sizeof(d), hipMemcpyDeviceToHost) == hipSuccess && d[3] > 0)
-      std::fprintf(stderr, "plk fuse dbg: %llu iterations, body %.0f cycles/iter, hand-off+root %.0f cycles/iter, %llu root runs, root %.0f cycles/run\n",
-                   d[3], (double)d[0] / d[3], (double)d[1] / d[3], d[4], d[4] ? (double)d[2] / d[4] : 0.0);
-  }
   out->partials_launches = h->n_launches;
   out->partials_ms = h->acc_ms[0];
   out->pmat_ms = h->acc_ms[1];

@@ -53,7 +53,7 @@ struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
   double* partials; i32* scale; const u8* codes; const double* tipP; const double* weights;
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
-  unsigned* sb_ctr; i32 dyn; unsigned* exit_ctr; i32* uflow; unsigned* sb_tk; unsigned long long* dbg;
+  unsigned* sb_ctr; i32 dyn; unsigned* exit_ctr; i32* uflow;
 };
 
 // Register vectors hold 4 * CW * PW doubles: vector v = pw * CW + cw is class c0 + cw of
@@ -267,18 +267,7 @@ __device__ __forceinline__ void rescale(double (&v)[4 * CW * PW], int (&cnt)[PW]
 }
 
 // off: the lane's first pattern in the slot (tile layout); pattern pw is 64 further
-// Hand-off of a fragment root to the workgroup that finishes its super-block last (FUSE_,
-// MI355X_MICROARCH.md "inter-workgroup visibility", first hand-off row): every byte stored
-// write-through (sc1: agent-scope relaxed atomic stores), every storing wave waits for its
-// stores before the workgroup's one counter add, and the reader loads every byte with sc1
-// loads (agent-scope relaxed atomic loads: they bypass the reader CU's L1)
-__device__ __forceinline__ double ldwt(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int ldwt(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// WT: write-through (sc1) stores of a handed-off fragment root
-template <int CW, int PW, bool SCALE, bool WT = false>
+template <int CW, int PW, bool SCALE>
 __device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0,
                                       const double (&v)[4 * CW * PW], const int (&cnt)[PW], bool gv) {
   if (!gv) return;  // a group past the last pattern (ragged last super-block) recomputes group 0
@@ -287,20 +276,10 @@ __device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, 
 #pragma unroll
   for (int pw = 0; pw < PW; ++pw)
 #pragma unroll
-    for (int i = 0; i < 4 * CW; ++i) {
-      if (WT)
-        __hip_atomic_store(dst + 64 * pw + (i64)i * kTile, v[4 * CW * pw + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        __builtin_nontemporal_store(v[4 * CW * pw + i], dst + 64 * pw + (i64)i * kTile);
-    }
+    for (int i = 0; i < 4 * CW; ++i) __builtin_nontemporal_store(v[4 * CW * pw + i], dst + 64 * pw + (i64)i * kTile);
   if (SCALE && c0 == 0)
 #pragma unroll
-    for (int pw = 0; pw < PW; ++pw) {
-      if (WT)
-        __hip_atomic_store(a.scale + (i64)slot * a.n_pad + p + 64 * pw, cnt[pw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        a.scale[(i64)slot * a.n_pad + p + 64 * pw] = cnt[pw];
-    }
+    for (int pw = 0; pw < PW; ++pw) a.scale[(i64)slot * a.n_pad + p + 64 * pw] = cnt[pw];
 }
 
 // log() out of line: inlined into the persistent loop, its polynomial constants are
@@ -390,10 +369,6 @@ struct JArgs {
   // the launch's super-block counters and the ticket counter to 0
   unsigned* exit_ctr;
   int32_t* uflow;  // unscaled handles: set to 1 when a site likelihood is < 2^-255 (or null)
-  // fused root fragment (JitShape::fuse_root): one counter per super-block, 0 between launches
-  // (the workgroup that takes the last count resets it)
-  unsigned* sb_tk;
-  unsigned long long* dbg;  // (measurement only, fuse_dbg 5) cycle sums of the loop's parts
 };
 
 struct JitShape {
@@ -409,13 +384,6 @@ struct JitShape {
   int L = 1;        // operand fetch lookahead (events)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
-  // >= 0: the program's second and last tier is this one fragment, which reads only the
-  // first tier's fragment roots (no tables); it runs inside the first tier's launch, per
-  // super-block, in the workgroup that finishes that super-block's last first-tier fragment
-  // (fuse_nf of them) -- no second launch, and the roots it reads are fresh in L2 / MALL
-  int fuse_root = -1;
-  int fuse_nf = 0;
-  int fuse_dbg = 0;  // (measurement only) 1: the hand-off without the root fragment's body
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     // the second exchange buffer only serves the per-node rescale
@@ -679,15 +647,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
            C, CW, NW, PW, sh.G, NW * sh.G, U, std::max(sh.NT, 1), std::max(sh.TD, 4), sh.scale ? "true" : "false",
            64 * NW * sh.G, minw_s.c_str());
   s += buf;
-  // Fused root fragment: first-tier fragment k walks the super-blocks from k * n / nf on
-  // (wrapping), so the last of the nf fragments to reach a super-block -- the workgroup that
-  // runs its root -- is a different fragment in each eighth of the range, and every fragment
-  // gets 1 / nf of the root runs (from a common start, the slowest fragment was last at almost
-  // every super-block and took nearly all of them: cfg5 2M 4.5 ms against 2.7 unfused)
-  if (sh.fuse_root >= 0)
-    s += "#define ROT_(x) ((x) + rot_off_ < a.n_sblocks ? (x) + rot_off_ : (x) + rot_off_ - a.n_sblocks)\n";
-  else
-    s += "#define ROT_(x) (x)\n";
   s += R"PLKJIT(  extern __shared__ __attribute__((aligned(16))) double lds[];
   double* tab = lds;                                          // units: [C_][U_ or U_ * U_][4] each
   double* xch = tab + TD_;                                    // [2][PW_][NWT_][64] (rescale alternates)
@@ -697,8 +656,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c0 = (w % NW_) * CW_, g = w / NW_;
   const int frag = frag_base + (int)blockIdx.y;
-  const int rot_off_ = (int)(((i64)blockIdx.y * a.n_sblocks) / (int)gridDim.y);  // (ROT_)
-  (void)rot_off_;
   const int u0 = 1 + kFragUnitStart[frag], nu = kFragUnitStart[frag + 1] - kFragUnitStart[frag];
   // code staging: this thread's items (uint4 column j of group gg in unit k's code row;
   // JArgs::codes holds one row per unit, unit_codes_kernel), fixed over the super-blocks.
@@ -716,7 +673,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     il_[m] = (gg * NT_ + k) * 4 * PW_ + j;
   }
   auto fetch_codes = [&](int sb_) {
-    const i64 q0_ = (i64)ROT_(sb_) * (64 * PW_ * G_);
+    const i64 q0_ = (i64)sb_ * (64 * PW_ * G_);
     _Pragma("unroll") for (int m = 0; m < NI_; ++m)
       if (q0_ + ic_[m] < a.n_pad) va_[m] = ucodes[iu_[m] + (q0_ >> 4)];
   };
@@ -847,12 +804,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
       _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[4 * CW_ * pw_ + i_] = L_[64 * pw_ + (i64)i_ * kTile]; \
       if (SC_) FK[pw_] = a.scale[sl_ * a.n_pad + p + 64 * pw_]; } }
-// LOADF with sc1 loads: a fragment root handed off inside the launch (FUSE_)
-#define LOADW(F, FK, slot) { const i64 sl_ = (i64)launder_s(slot); \
-    const double* L_ = a.partials + sl_ * a.slot_stride + toff; \
-    _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
-      _Pragma("unroll") for (int i_ = 0; i_ < 4 * CW_; ++i_) F[4 * CW_ * pw_ + i_] = ldwt(L_ + 64 * pw_ + (i64)i_ * kTile); \
-      if (SC_) FK[pw_] = ldwt(a.scale + sl_ * a.n_pad + p + 64 * pw_); } }
 #define SB __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::"v"(ptouch_));  // (keeps the touch loads)
   // Super-block order.  Static: blockIdx.x, + gridDim.x, ...  Dynamic (a.dyn): the first is
@@ -862,16 +813,11 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // the launch at 0 (the exit ticket below resets it).  Which workgroup computes a
   // super-block does not change its results.
   __shared__ int sb_next_lds;
-  __shared__ int fuse_last_lds;  // (FUSE_) this workgroup runs the root fragment of the super-block
-  (void)fuse_last_lds;
-  unsigned long long cy_b_ = 0, cy_h_ = 0, cy_r_ = 0, cy_ru_ = 0; unsigned n_b_ = 0, n_r_ = 0;
-  (void)cy_b_; (void)cy_h_; (void)cy_r_; (void)cy_ru_; (void)n_b_; (void)n_r_;
   unsigned sb_pend = 0;
   if (a.dyn && threadIdx.x == 0)
     sb_pend = __hip_atomic_fetch_add(a.sb_ctr + frag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int sb = blockIdx.x, sb_nx = 0; sb < a.n_sblocks; sb = sb_nx) {
-    const int sbr_ = ROT_(sb);  // (the super-block this iteration computes)
-    const i64 q0 = (i64)sbr_ * (64 * PW_ * G_);
+    const i64 q0 = (i64)sb * (64 * PW_ * G_);
     // super-blocks of G_ groups; in a ragged last one, groups past n_pad recompute group 0
     // (in bounds everywhere) and store nothing
     const bool gv = q0 + g * (64 * PW_) < a.n_pad;
@@ -904,11 +850,10 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
              r, r, r);
     s += buf;
   }
-  const int FR = sh.fuse_root;
-  // one fragment's body; wt: the fused root fragment (sc1 loads of the handed-off roots)
-  auto emit_fragment = [&](size_t f, bool wt) {
+  s += "    switch (frag) {\n";
+  for (size_t f = 0; f < events.size(); ++f) {
+    if (leader[f] != (int)f) continue;
     const std::vector<JitEvent>& ev = events[f];
-    const char* loadm = wt ? "LOADW" : "LOADF";
     std::vector<int> slot(ev.size(), -1), fetchers;
     for (size_t i = 0; i < ev.size(); ++i)
       if (ev[i].op == T_TIP || ev[i].op == T_LOAD) {
@@ -916,7 +861,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         fetchers.push_back((int)i);
       }
     auto pref = [&](size_t i) -> std::string {  // P operand of event i (relative to the node base)
-      snprintf(buf, sizeof(buf), "pmf_ + %lld", wt && sh.fuse_dbg == 3 ? 0ll : (long long)(ev[i].b - nbase[f]) * C * 16);
+      snprintf(buf, sizeof(buf), "pmf_ + %lld", (long long)(ev[i].b - nbase[f]) * C * 16);
       return buf;
     };
     auto sref = [&](int a) -> std::string {  // a slot (relative to the slot base)
@@ -930,7 +875,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       if (e.op == T_TIP)
         snprintf(buf, sizeof(buf), "      CODEF(Q%d, %d)\n", slot[(size_t)i], e.a);
       else
-        snprintf(buf, sizeof(buf), "      %s(F%d, FK%d, %s)\n", loadm, slot[(size_t)i], slot[(size_t)i], sref(e.a).c_str());
+        snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %s)\n", slot[(size_t)i], slot[(size_t)i], sref(e.a).c_str());
       s += buf;
     };
     auto unit_args = [&](const JitEvent& e) -> std::string {  // TB, OFF, R of a unit
@@ -951,7 +896,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         snprintf(buf, sizeof(buf), "      TIPF(F%d, Q%d, %d, %s)\n", slot[(size_t)i], slot[(size_t)i], e.a,
                  unit_args(e).c_str());
       else
-        snprintf(buf, sizeof(buf), "      %s(F%d, FK%d, %s)\n", loadm, slot[(size_t)i], slot[(size_t)i], sref(e.a).c_str());
+        snprintf(buf, sizeof(buf), "      LOADF(F%d, FK%d, %s)\n", slot[(size_t)i], slot[(size_t)i], sref(e.a).c_str());
       s += buf;
     };
     // One pass over the fragment.  exact: the per-node joint rescale of the other
@@ -1069,21 +1014,14 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         } else {  // T_ROOT
           if (sh.scale) check_line(0);
           if (e.a >= 0) {
-            // (a first-tier root the fused root fragment reads: write-through)
-            snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_, %s>(a, %s, toff, p, c0, A0, K0, gv);\n",
-                     FR >= 0 && !wt ? "true" : "false", sref(e.a).c_str());
+            snprintf(buf, sizeof(buf), "      store<CW_, PW_, SC_>(a, %s, toff, p, c0, A0, K0, gv);\n",
+                     sref(e.a).c_str());
             s += buf;
           }
           if (e.b) s += "      reduce_root<C_, CW_, PW_, NWT_, SC_>(a, A0, K0, xch, w, g, c0, p0, p, gv);\n";
         }
       }
     };
-    emit_body(true);
-  };
-  if (sh.fuse_dbg == 5) s += "    const unsigned long long cy0_ = __builtin_readcyclecounter();\n";
-  s += "    switch (frag) {\n";
-  for (size_t f = 0; f < events.size(); ++f) {
-    if (leader[f] != (int)f || (int)f == FR) continue;
     for (size_t q = f; q < events.size(); ++q)
       if (leader[q] == (int)f) {
         snprintf(buf, sizeof(buf), "    case %zu:\n", q);
@@ -1091,62 +1029,16 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       }
     s += "    {\n      const CPd pmf_ = pm + (i64)kFragNB[frag + 1] * (C_ * 16);\n"
          "      const int sb_ = __builtin_amdgcn_readfirstlane(kFragSB[frag + 1]); (void)pmf_; (void)sb_;\n";
-    emit_fragment(f, false);
+    emit_body(true);
     s += "    } break;\n";
   }
-  s += "    default: break;\n    }\n";
-  if (FR >= 0) {
-    // The fused root fragment.  Every wave waits for its write-through root stores, the
-    // workgroup takes one count of the super-block's counter behind a barrier, and the
-    // workgroup that takes the last one (the super-block's fuse_nf roots are then all in
-    // memory) runs the root fragment over the same patterns, reading the roots with sc1
-    // loads, and leaves the counter at 0 for the next launch.
-    const std::string nf1 = std::to_string(sh.fuse_nf - 1), nfs = std::to_string(sh.fuse_nf);
-    if (sh.fuse_dbg == 5) s += "    const unsigned long long cy_ru0_ = __builtin_readcyclecounter();\n";
-    s += "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
-         "    __syncthreads();\n"
-         "    if (threadIdx.x == 0) {\n"
-         "      const unsigned t_ = __hip_atomic_fetch_add(a.sb_tk + sbr_, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n";
-    if (sh.fuse_dbg == 4) {
-      // (measurement only) the super-block's root runs in the workgroup of first-tier
-      // fragment sb % fuse_nf, which polls the counter until every root is in
-      s += "      int last_ = (sbr_ % " + nfs + ") == (int)blockIdx.y;\n"
-           "      if (last_) {\n"
-           "        unsigned v_ = t_ + 1u;\n"
-           "        for (int it_ = 0; v_ < " + nfs + "u && it_ < (1 << 22); ++it_) {\n"
-           "          __builtin_amdgcn_s_sleep(1);\n"
-           "          v_ = __hip_atomic_load(a.sb_tk + sbr_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-           "        }\n"
-           "        __hip_atomic_store(a.sb_tk + sbr_, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-           "      }\n";
-    } else {
-      s += "      const int last_ = t_ == " + nf1 + "u;\n"
-           "      if (last_) __hip_atomic_store(a.sb_tk + sbr_, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n";
-    }
-    s += "      fuse_last_lds = last_;\n"
-         "    }\n"
-         "    __syncthreads();\n"
-         "    if (fuse_last_lds) {\n"
-         "      const CPd pmf_ = pm + (i64)kFragNB[" + std::to_string(FR + 1) + "] * (C_ * 16);\n"
-         "      const int sb_ = kFragSB[" + std::to_string(FR + 1) + "]; (void)pmf_; (void)sb_;\n";
-    if (sh.fuse_dbg == 5) s += "      cy_ru_ = __builtin_readcyclecounter();\n";
-    if (sh.fuse_dbg != 1) emit_fragment((size_t)FR, true);
-    if (sh.fuse_dbg == 5) s += "      cy_r_ += __builtin_readcyclecounter() - cy_ru_; ++n_r_;\n";
-    s += "    }\n";
-    if (sh.fuse_dbg == 5) s += "    cy_b_ += cy_ru0_ - cy0_; cy_h_ += __builtin_readcyclecounter() - cy_ru0_; ++n_b_;\n";
-  }
-  s += "  }\n";
+  s += "    default: break;\n    }\n  }\n";
   // Exit ticket (dynamic super-blocks): thread 0 of every workgroup takes one ticket after its
   // last super-block -- its own counter atomics have returned by then -- and the last one
   // leaves the launch's counters and the ticket counter at 0 for the next launch, so the host
   // keeps no copy of them.  (Forming the block sums in the last workgroup as well was measured
   // 8 us slower per cfg2 traversal than wave_sums_to_blocks: the wave sums must then cross the
   // XCDs' L2s, as sc1 stores and loads or behind L2 write-backs -- profiles/r05/ab_runs.md.)
-  if (sh.fuse_dbg == 5)
-    s += "  if (threadIdx.x == 0 && a.dbg) {\n"
-         "    atomicAdd(a.dbg + 0, cy_b_); atomicAdd(a.dbg + 1, cy_h_); atomicAdd(a.dbg + 2, cy_r_);\n"
-         "    atomicAdd(a.dbg + 3, (unsigned long long)n_b_); atomicAdd(a.dbg + 4, (unsigned long long)n_r_);\n"
-         "  }\n";
   s += R"PLKJIT(  if (a.exit_ctr && threadIdx.x == 0) {
     const unsigned t_ = __hip_atomic_fetch_add(a.exit_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t_ == gridDim.x * gridDim.y - 1u) {

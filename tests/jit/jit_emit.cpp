@@ -76,28 +76,6 @@ int main(int argc, char** argv) {
     add(T_ROOT, 0, 0, 1);
     starts = {0};
   }
-  // tree4_fuse: two first-tier fragments (each ((t, t), (t, t)) stored in slots 0 / 1) and a
-  // root fragment that loads both and reduces the root -- the shape of the fused second tier
-  // (JitShape::fuse_root)
-  const bool fuse = kind == "tree4_fuse";
-  if (fuse) {
-    prog.clear();
-    for (int k = 0; k < 2; ++k) {
-      add(T_DESCEND, 1, 0, 0);
-      add(T_TIP, 1, 4 * k, 4 * k);
-      add(T_TIP, 1, 4 * k + 1, 4 * k + 1);
-      add(T_ASCEND, 1, -1, 8 + 3 * k);
-      add(T_DESCEND, 1, 0, 0);
-      add(T_TIP, 1, 4 * k + 2, 4 * k + 2);
-      add(T_TIP, 1, 4 * k + 3, 4 * k + 3);
-      add(T_ASCEND, 1, -1, 9 + 3 * k);
-      add(T_ROOT, 0, k, 0);
-    }
-    starts = {0, 9, 18};
-    add(T_LOAD, 0, 0, 10);
-    add(T_LOAD, 0, 1, 13);
-    add(T_ROOT, 0, -1, 1);
-  }
   std::string src;
   if (m) {
     JitMShape sh;
@@ -121,11 +99,6 @@ int main(int argc, char** argv) {
     sh.PW = 1;
     sh.L = sh.CW > 1 ? 2 : 3;
     sh.ppipe = true;
-    if (fuse) {
-      sh.fuse_root = 2;
-      sh.fuse_nf = 2;
-      if (const char* e = std::getenv("JIT_EMIT_FUSEDBG")) sh.fuse_dbg = std::atoi(e);
-    }
     src = jit_tree4_source(plan, sh);
   }
   std::fwrite(src.data(), 1, src.size(), stdout);

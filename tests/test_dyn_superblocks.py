@@ -71,28 +71,3 @@ def test_stale_counter_never_leaves_the_range():
         assert all(0 <= d < n for d in done)
         assert len(done) == len(set(done))
         assert ctr == 0  # and the launch's last workgroup repairs the counter
-
-
-@pytest.mark.parametrize("seed", range(8))
-def test_fused_root_ticket_one_last_per_superblock(seed):
-    """The fused root fragment's hand-off (plk_jit.hpp, FUSE_): each of the nf first-tier
-    workgroups that computes super-block sb stores its root, waits for the stores, then adds 1
-    to tk[sb]; the one whose add returns nf - 1 runs the root over sb and stores 0.  Under any
-    interleaving: exactly one root run per super-block, it sees all nf roots stored, and every
-    counter ends at 0 for the next launch."""
-    rng = random.Random(100 + seed)
-    n, nf = rng.randint(1, 60), rng.randint(1, 9)
-    tk = [0] * n
-    for _launch in range(3):
-        stored = [set() for _ in range(n)]
-        runs = [0] * n
-        todo = [(f, sb) for f in range(nf) for sb in range(n)]
-        rng.shuffle(todo)
-        for f, sb in todo:
-            stored[sb].add(f)
-            t, tk[sb] = tk[sb], tk[sb] + 1
-            if t == nf - 1:
-                assert stored[sb] == set(range(nf))
-                runs[sb] += 1
-                tk[sb] = 0
-        assert runs == [1] * n and tk == [0] * n

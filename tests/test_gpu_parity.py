@@ -697,47 +697,6 @@ def test_jit_tree4_dynamic_superblocks_bitwise(C, n_taxa, n_patterns, scaling, m
     assert np.allclose(res["1"][0][1][sub], so, rtol=REL, atol=0)
 
 
-@pytest.mark.parametrize("n_patterns,unroot", [(60_000, False), (1_000, False), (20_000, True)])
-def test_jit_tree4_fused_root_bitwise(n_patterns, unroot, monkeypatch):
-    """A second tier of one table-free fragment (a balanced 512-taxon tree: the root fragment
-    over the eight stored 64-tip subtree roots) runs inside the first tier's launch, in the
-    workgroup that finishes each super-block's last subtree (plk_jit.hpp JitShape::fuse_root):
-    lnL, per-pattern lnL and block sums bitwise equal to the two-launch form (PLK_TUNE
-    JIT_FUSE=0) over repeated evaluations at alternating branch lengths -- a root read from a
-    stale line (the previous evaluation's value, or another XCD's unwritten one) changes the
-    result -- with dynamic super-blocks (60k), a static ragged order (1k) and an unrooted tree;
-    and the oracle at 1e-12 on a slice."""
-    tree = phylo.balanced_tree(512, seed=37, lo=0.05, hi=0.4)
-    et = phylo.engine_tree(tree, unroot=unroot)
-    rng = np.random.default_rng(512)
-    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
-    rates, probs = phylo.gamma_rates(4, 0.5)
-    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, True, True, 11)
-    states = wl.simulate(0, n_patterns).astype(np.int32)
-    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
-    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
-    res, launches = {}, {}
-    for fuse in ("0", "1"):
-        set_tune(monkeypatch, "JIT_FUSE", fuse)
-        eng = engine_for(et, 4, 4, n_patterns, states, phylo.DNA.init_table, rates, probs, m.pi, [m], flags=flags)
-        eng.set_timing(True)
-        out = []
-        for k in range(7):
-            eng.update_pmatrices(br, et.brlen[br] * (1.0 + 0.15 * (k % 2)))
-            out.append(run_engine(eng, et))
-        assert eng.kernel_path() == "jit_tree4"
-        launches[fuse] = eng.get_timing()["launches"]  # traversal launches
-        res[fuse] = out
-        del eng
-    assert launches["1"] == launches["0"] - 7, launches  # one launch fewer per evaluation
-    for (l0, s0, b0), (l1, s1, b1) in zip(res["0"], res["1"]):
-        assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1)
-    assert res["1"][0][0] == res["1"][2][0] and res["1"][1][0] == res["1"][3][0] != res["1"][0][0]
-    sub = slice(n_patterns - 1500, n_patterns)
-    lo, so = oracle_for(et, states[:, sub], phylo.DNA.init_table, rates, probs, m.pi, [m], scaling=True)
-    assert np.allclose(res["1"][0][1][sub], so, rtol=REL, atol=0)
-
-
 def test_jit_same_shape_fragments_share_code(tmp_path, monkeypatch):
     """A balanced tree's 64-tip fragments have one shape: the generated kernel holds one code
     block for all of them (plk_jit.hpp: per-fragment node / slot bases), and the result is
@@ -759,9 +718,7 @@ def test_jit_same_shape_fragments_share_code(tmp_path, monkeypatch):
     src = [x for x in srcs if "plk_jit_tree4" in x and "kFragNB" in x][-1]
     labels = len(__import__("re").findall(r"^    case \d+:$", src, __import__("re").M))
     blocks = src.count("const CPd pmf_ = ")
-    # the same-shape subtrees share a block; the top has its own (in the switch, or after it
-    # as the fused root fragment)
-    assert 2 <= blocks < labels + 1, (labels, blocks)
+    assert 2 <= blocks < labels, (labels, blocks)   # the same-shape subtrees share a block; the top has its own
     lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m], scaling=True)
     check(lnl, site, lo, so)
 
