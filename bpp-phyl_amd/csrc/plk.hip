@@ -315,11 +315,6 @@ struct plk_handle_s {
   std::vector<int32_t> frag_starts_host;  // fragment start offsets, tier order
   hipFunction_t jit_fn = nullptr;
   JitShape jit_shape;
-  hipFunction_t jit_fn_fpm = nullptr;  // the same program with the P(t) prologue (JitShape::fpm)
-  JitShape jit_shape_fpm;
-  // plk_evaluate's P(t) request when the traversal computes it (fpm_req.n > 0 until then)
-  PmatInline fpm_req{};
-  bool fpm_defer = false;  // set by plk_evaluate around its plk_update_pmatrices call
   // tree-specialised 20-state kernel on v_mfma_f64_4x4x4_4b (plk_jitm.hpp); null: not compiled yet
   hipFunction_t jitm_fn = nullptr;
   JitMShape jitm_shape;
@@ -332,7 +327,6 @@ struct plk_handle_s {
   size_t ucodes_cap = 0, units_cap = 0;
   bool ucodes_valid = false;    // cleared by new tip codes and by a new plan
   int jit_resident = 0;  // workgroups of jit_fn resident at once on the device
-  int jit_resident_fpm = 0;  // (of jit_fn_fpm)
   std::string kernel_path;                // what served the last plk_update_partials
   // per-subtree pattern compression (PLK_FLAG_SUBTREE_PATTERNS)
   std::vector<std::vector<uint8_t> > tip_codes_host;  // compact codes per tip
@@ -1407,20 +1401,6 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
     std::atomic_thread_fence(std::memory_order_seq_cst);
     req = h->h_req_dev;
   }
-  // plk_evaluate on a one-launch jit_tree4 program: the traversal computes the request in its
-  // prologue (fpm_defer, decided by the caller); here only the bookkeeping below
-  const bool defer = h->fpm_defer && inl.n > 0 && deriv_mask == PLK_DERIV_P && h->S == 4 && h->table_set;
-  if (defer) {
-    h->fpm_req = inl;
-    for (int i = 0; i < n; ++i) {
-      h->pmat_valid[branch[i]] = 1;
-      h->pmatsT_dirty = true;
-      if (branch[i] < h->n_tips) h->tip_table_valid[branch[i]] = 1;  // rows written by the prologue
-    }
-    if (h->deriv_valid.empty()) h->deriv_valid.assign(h->n_nodes, 0);
-    for (int i = 0; i < n; ++i) h->deriv_valid[branch[i]] = 0;
-    return PLK_OK;
-  }
   PmatArgs a;
   a.t = inl.n ? nullptr : reinterpret_cast<const double*>(req + off_t);
   a.branch = inl.n ? nullptr : reinterpret_cast<const int32_t*>(req + off_b);
@@ -1495,19 +1475,6 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
                     (PLK_DERIV_P | PLK_DERIV_DP | PLK_DERIV_D2P);
   for (int i = 0; i < n; ++i) h->deriv_valid[branch[i]] = both ? 1 : 0;
   return PLK_OK;
-}
-
-// A deferred P(t) request (plk_evaluate, JitShape::fpm) whose traversal will not compute it:
-// launch it as plk_update_pmatrices would have.
-static int flush_fpm(plk_handle h) {
-  if (h->fpm_req.n <= 0) return PLK_OK;
-  const PmatInline q = h->fpm_req;
-  h->fpm_req.n = 0;
-  const bool saved = h->fpm_defer;
-  h->fpm_defer = false;
-  const int rc = plk_update_pmatrices(h, q.n, q.branch, q.model, q.t, PLK_DERIV_P);
-  h->fpm_defer = saved;
-  return rc;
 }
 
 int plk_set_pmatrix(plk_handle h, int branch, const double* P) {
@@ -1910,7 +1877,6 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   h->prog_host = prog;
   h->frag_starts_host.assign(start_sorted.begin(), start_sorted.begin() + nf);
   h->jit_fn = nullptr;  // specialised kernel of the new program: compiled on first use
-  h->jit_fn_fpm = nullptr;
   h->jitm_fn = nullptr;
   h->jit_plan_valid = false;
   HIPCHK(h, hipStreamSynchronize(h->stream));  // host staging vectors go out of scope
@@ -2083,7 +2049,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       h->jit_plan_U = sh.U;
       h->jit_plan_budget = budget;
       h->jit_fn = nullptr;
-      h->jit_fn_fpm = nullptr;
       h->ucodes_valid = false;
     }
     if (!h->ucodes_valid) {
@@ -2135,29 +2100,16 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // release/acquire form (an L2 write-back per wave) was slower still (round 1)
     if (sh.lds_bytes() > 160 * 1024 - 64)  // (less the kernel's static LDS word)
       return fail(h, PLK_ERR_UNSUPPORTED, "tree kernel needs %zu B of LDS", sh.lds_bytes());
-    // plk_evaluate's deferred P(t) request: computed in the prologue of the first tier's launch
-    // (its exp table fits the table area, which the prologue borrows; the later tiers read the
-    // matrices after the launch boundary); otherwise launched on its own now
-    const bool fpm = h->fpm_req.n > 0 && h->fpm_req.n * sh.C * 4 <= std::max(sh.TD, 4);
-    if (h->fpm_req.n > 0 && !fpm) {
-      int rc = flush_fpm(h);
+    if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW ||
+        sh.pin != h->jit_shape.pin ||
+        sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
+        sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
+        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe) {
+      int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
+      h->jit_shape = sh;
+      h->jit_resident = 0;
     }
-    for (int v = 0; v < 2; ++v) {  // the kernels this traversal launches: without / with the prologue
-      if (v == 0 ? (fpm && h->prog_tiers.size() == 1) : !fpm) continue;
-      sh.fpm = v == 1;
-      hipFunction_t& jfn = sh.fpm ? h->jit_fn_fpm : h->jit_fn;
-      JitShape& jsh = sh.fpm ? h->jit_shape_fpm : h->jit_shape;
-      if (!jfn || sh.C != jsh.C || sh.CW != jsh.CW || sh.pin != jsh.pin || sh.G != jsh.G || sh.U != jsh.U ||
-          sh.NT != jsh.NT || sh.TD != jsh.TD || sh.scale != jsh.scale || sh.L != jsh.L || sh.minw != jsh.minw ||
-          sh.ppipe != jsh.ppipe) {
-        int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &jfn);
-        if (rc) return rc;
-        jsh = sh;
-        (sh.fpm ? h->jit_resident_fpm : h->jit_resident) = 0;
-      }
-    }
-    sh.fpm = fpm;
     ja.partials = a.partials;
     ja.scale = a.scale;
     ja.codes = h->d_ucodes;
@@ -2176,15 +2128,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.dyn = tune_is("JIT_DYN", '0') ? 0 : 1;  // (per launch below)
     ja.exit_ctr = h->d_sbctr + h->prog_nf;  // (null per launch below when not dynamic)
     ja.uflow = a.uflow;
-    ja.V = h->V;
-    ja.Vinv = h->Vinv;
-    ja.lambda = h->lambda;
-    ja.rates = h->rates;
-    ja.init = h->code_table;
-    ja.pmats_w = h->pmats;
-    ja.tipP_w = h->tipP;
-    ja.n_codes = h->n_codes;
-    ja.n_tips = h->n_tips;
   }
   const bool jitm = kind == FK_TREEM && h->prog_jitm;
   JMArgs ma;
@@ -2244,26 +2187,23 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     if (jit) {
       const double* pm = h->pmats;
       int base = first;
-      void* args[] = {&ja, &pm, &base, &h->fpm_req};
-      const bool fp = sh.fpm && first == 0;  // (the first tier's launch computes the request)
-      hipFunction_t jfn = fp ? h->jit_fn_fpm : h->jit_fn;
+      void* args[] = {&ja, &pm, &base};
       // persistent grid: as many workgroups as are resident at once (occupancy query), so
       // every workgroup stages its tables once and there is no second dispatch round
       int wgs = 0;
       {
-        int& jres = fp ? h->jit_resident_fpm : h->jit_resident;
-        if (jres <= 0) {
+        if (h->jit_resident <= 0) {
           int per_cu = 0, n_cu = 0;
-          HIPCHK(h, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jfn, 64 * (h->C / sh.CW) * sh.G,
+          HIPCHK(h, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, h->jit_fn, 64 * (h->C / sh.CW) * sh.G,
                                                                        sh.lds_bytes()));
           HIPCHK(h, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, h->device));
-          jres = std::max(1, per_cu) * std::max(1, n_cu);
+          h->jit_resident = std::max(1, per_cu) * std::max(1, n_cu);
         }
         // every fragment of the tier at once: the resident workgroups split over the
         // fragments (each stages its fragment's tables once and walks many super-blocks)
         // instead of the tier's fragments running one after another with every workgroup
         // staging tables for a few super-blocks (cfg5 0.49 -> 0.42 ms)
-        wgs = std::max(1, jres / (int)grid.y);
+        wgs = std::max(1, h->jit_resident / (int)grid.y);
       }
       const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, wgs);
       // dynamic super-blocks where a workgroup walks several (a tier of 1-2 per workgroup
@@ -2274,10 +2214,9 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       h->jit_last_gx = (int)gx;
       if ((int)h->jit_frag_gx.size() < h->prog_nf) h->jit_frag_gx.resize((size_t)h->prog_nf, 0);
       for (int k = 0; k < (int)t.size(); ++k) h->jit_frag_gx[(size_t)(first + k)] = (int)gx;
-      HIPCHK(h, hipModuleLaunchKernel(jfn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
+      HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
                                       (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
-      if (fp) h->fpm_req.n = 0;  // (computed by this launch)
     } else if (jitm) {
       int base = first;
       void* args[] = {&ma, &base};
@@ -3572,13 +3511,8 @@ int plk_update_partials(plk_handle h, const plk_op* ops, int n_ops) {
       k.insert(k.end(), ops[i].child, ops[i].child + ops[i].n_children);
     }
   }
-  const bool t4 = !(h->flags & PLK_FLAG_SUBTREE_PATTERNS) && tree4_supported(h) && fusable(ops, n_ops);
-  if (h->fpm_req.n > 0 && !(t4 && jit_tree4(h))) {  // (only the jit_tree4 traversal computes a deferred request)
-    int rc = flush_fpm(h);
-    if (rc) return rc;
-  }
   if (h->flags & PLK_FLAG_SUBTREE_PATTERNS) return update_compressed(h, ops, n_ops);
-  if (t4) return update_tree4(h, ops, n_ops);
+  if (tree4_supported(h) && fusable(ops, n_ops)) return update_tree4(h, ops, n_ops);
   return update_levelwise(h, ops, n_ops);
 }
 
@@ -4063,19 +3997,11 @@ int plk_evaluate(plk_handle h, int n, const int32_t* branch, const int32_t* mode
   const clk::time_point t0 = clk::now();
   auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
   h->in_eval = true;
-  // jit_tree4: the traversal computes the P(t) request in its prologue (JitShape::fpm; the
-  // traversal launches it, or it is launched on its own when the program does not allow it)
-  h->fpm_defer = jit_tree4(h) && !tune_is("JIT_FPM", '0');
   int rc = plk_update_pmatrices(h, n, branch, model, t, PLK_DERIV_P);
-  h->fpm_defer = false;
   h->in_eval = false;
   if (rc) return rc;
   const clk::time_point t1 = clk::now();
   rc = plk_update_partials(h, ops, n_ops);
-  if (h->fpm_req.n > 0) {  // (a failed traversal: the matrices the bookkeeping promised)
-    const int rc2 = flush_fpm(h);
-    if (!rc) rc = rc2;
-  }
   if (rc) return rc;
   const clk::time_point t2 = clk::now();
   rc = root_launch(h, root, nullptr);

@@ -54,13 +54,7 @@ struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
   unsigned* sb_ctr; i32 dyn; unsigned* exit_ctr; i32* uflow;
-  // FPM_: the evaluation's P(t) request, computed by every workgroup before its tables stage
-  const double* V; const double* Vinv; const double* lambda; const double* rates; const double* init;
-  double* pmats_w; double* tipP_w; i32 n_codes; i32 n_tips;
 };
-// (FPM_) the request as plk::PmatInline lays it out: branch lengths, branches, models, count
-#define kReqMax 160
-struct PmatReqJ { double t[kReqMax]; int branch[kReqMax]; int model[kReqMax]; int n; };
 
 // Register vectors hold 4 * CW * PW doubles: vector v = pw * CW + cw is class c0 + cw of
 // the lane's pattern pw (patterns p and p + 64 of a 128-pattern tile when PW = 2).
@@ -375,17 +369,6 @@ struct JArgs {
   // the launch's super-block counters and the ticket counter to 0
   unsigned* exit_ctr;
   int32_t* uflow;  // unscaled handles: set to 1 when a site likelihood is < 2^-255 (or null)
-  // JitShape::fpm: the P(t) request of the evaluation (a PmatInline kernel argument) is computed
-  // inside the traversal, from these, into pmats_w / tipP_w (pmat4_kernel's operations)
-  const double* V;
-  const double* Vinv;
-  const double* lambda;
-  const double* rates;
-  const double* init;
-  double* pmats_w;
-  double* tipP_w;
-  int32_t n_codes;
-  int32_t n_tips;
 };
 
 struct JitShape {
@@ -401,10 +384,6 @@ struct JitShape {
   int L = 1;        // operand fetch lookahead (events)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
-  // the evaluation's P(t) matrices and tip tables computed by every workgroup in the kernel's
-  // prologue (plk_evaluate, one-launch programs, requests of <= kPmatInline branches): no
-  // P(t) launch and no kernel boundary in front of the traversal
-  bool fpm = false;
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     // the second exchange buffer only serves the per-node rescale
@@ -663,11 +642,10 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
            "#define U_ %d\n#define NT_ %d\n#define TD_ %d\n#define SC_ %s\n#define V_ (4 * CW_ * PW_)\n"
-           "#define FPM_ %d\n"
            "extern \"C\" __global__ __launch_bounds__(%d%s) void plk_jit_tree4(JArgs a, const double* __restrict__ "
-           "pmats, int frag_base%s) {\n",
+           "pmats, int frag_base) {\n",
            C, CW, NW, PW, sh.G, NW * sh.G, U, std::max(sh.NT, 1), std::max(sh.TD, 4), sh.scale ? "true" : "false",
-           sh.fpm ? 1 : 0, 64 * NW * sh.G, minw_s.c_str(), sh.fpm ? ", const PmatReqJ q" : "");
+           64 * NW * sh.G, minw_s.c_str());
   s += buf;
   s += R"PLKJIT(  extern __shared__ __attribute__((aligned(16))) double lds[];
   double* tab = lds;                                          // units: [C_][U_ or U_ * U_][4] each
@@ -700,60 +678,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       if (q0_ + ic_[m] < a.n_pad) va_[m] = ucodes[iu_[m] + (q0_ >> 4)];
   };
   fetch_codes(blockIdx.x);  // (issued before the table staging below: its loads overlap it)
-#if FPM_
-  {
-    // The evaluation's P(t) request, in every workgroup (the same values, so the stores of
-    // different workgroups to one line agree), with pmat4_kernel's operations in its order:
-    // e_k = exp(lambda_k t r_c) per (branch, class) -- staged in the table area, which the
-    // tables only fill below -- then per (branch, class, row x) P[x][y] = sum_k (V[x][k]
-    // Vinv[k][y]) e_k and, for a tip branch, its table entries sum_y P[x][y] init[code][y].
-    double* eL = tab;
-    const int nq = q.n, nt_ = 64 * NWT_;
-    for (int it = threadIdx.x; it < nq * C_ * 4; it += nt_) {
-      const int k = it & 3, ic = it >> 2, i = ic / C_, c = ic - i * C_;
-      const double tt = q.t[i] * a.rates[c];
-      eL[it] = exp(a.lambda[q.model[i] * 4 + k] * tt);
-    }
-    __syncthreads();
-    for (int it = threadIdx.x; it < nq * C_ * 4; it += nt_) {
-      const int x = it & 3, ic = it >> 2, i = ic / C_, c = ic - i * C_;
-      const int b = q.branch[i], m = q.model[i];
-      const double tt = q.t[i] * a.rates[c];
-      const double* V = a.V + m * 16;
-      const double* Vi = a.Vinv + m * 16;
-      double e[4], vx[4], vi[16], p[4];
-      _Pragma("unroll") for (int k = 0; k < 4; ++k) {
-        vx[k] = V[x * 4 + k];
-        e[k] = eL[ic * 4 + k];
-      }
-      _Pragma("unroll") for (int k = 0; k < 16; ++k) vi[k] = Vi[k];
-      _Pragma("unroll") for (int y = 0; y < 4; ++y) {
-        p[y] = 0.0;
-        _Pragma("unroll") for (int k = 0; k < 4; ++k) {
-          const double w_ = vx[k] * vi[k * 4 + y];
-          p[y] = __builtin_fma(w_, e[k], p[y]);
-        }
-        if (tt == 0.0) p[y] = (x == y) ? 1.0 : 0.0;  // getPij_t: t == 0 -> identity
-      }
-      double* P_ = a.pmats_w + ((i64)b * C_ + c) * 16 + x * 4;
-      _Pragma("unroll") for (int y = 0; y < 4; ++y) P_[y] = p[y];
-      if (b < a.n_tips) {
-        double* o_ = a.tipP_w + ((i64)b * C_ + c) * a.n_codes * 4 + x;
-        for (int code = 0; code < a.n_codes; ++code) {
-          double t_ = 0.0;
-          _Pragma("unroll") for (int y = 0; y < 4; ++y) t_ = __builtin_fma(p[y], a.init[code * 4 + y], t_);
-          o_[code * 4] = t_;
-        }
-      }
-    }
-    // every store of this workgroup is in its XCD's L2 before any of its waves reads the
-    // matrices back (the staging below; the traversal's scalar loads through the laundered
-    // base, which the compiler cannot hoist above this point)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    pmats = reinterpret_cast<const double*>(launder_s(reinterpret_cast<unsigned long long>(pmats)));
-  }
-#endif
   // The fragment's P(t) matrices, touched with wide loads while the tables stage: the
   // traversal reads P(t) through scalar loads one contribution ahead, and their first touch
   // (the P(t) launch wrote them through another XCD's L2) made the first super-block ~12 us

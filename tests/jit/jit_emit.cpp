@@ -2,7 +2,7 @@
 // plk_jitm.hpp: jit_treeM4_source) for a small two-fragment program, so that
 // tests/test_jit_sources.py can cross-compile it for gfx950 with hipcc on a machine without
 // a GPU (the library compiles these sources only at run time, on the device).
-//   jit_emit <tree4|treeM> <C> <scale 0|1> [S (treeM: 20 | 4)] [classes in wave] [P(t) prologue] > kernel.hip
+//   jit_emit <tree4|treeM> <C> <scale 0|1> [S (treeM: 20 | 4)] > kernel.hip
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
@@ -99,7 +99,6 @@ int main(int argc, char** argv) {
     sh.PW = 1;
     sh.L = sh.CW > 1 ? 2 : 3;
     sh.ppipe = true;
-    sh.fpm = argc > 6 && std::atoi(argv[6]) != 0;  // the P(t) prologue (plk_evaluate)
     src = jit_tree4_source(plan, sh);
   }
   std::fwrite(src.data(), 1, src.size(), stdout);

@@ -359,45 +359,6 @@ def test_evaluate_equals_three_calls(S, C, flags):
         assert abs(lnl_e - lo) <= REL * abs(lo)
 
 
-@pytest.mark.parametrize("C,flags", [(4, plk.PLK_FLAG_LNL_ONLY), (2, plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING),
-                                     (4, 0)])
-def test_evaluate_fused_pmatrices_bitwise(C, flags, monkeypatch):
-    """plk_evaluate on a one-launch jit_tree4 program computes its P(t) request in the
-    traversal's prologue (JitShape::fpm, no pmat4_kernel launch): the matrices it leaves in
-    HBM, the lnL and the block sums are bitwise those of the separate P(t) launch (PLK_TUNE
-    JIT_FPM=0) -- two rate models over the branches, ambiguity codes (tip tables of 16
-    codes), a zero-length branch (identity), a request of a subset of the branches, and a
-    materialising handle."""
-    et, m, alph, rates, probs, states = _random_problem(4, C, 32, 7000, seed=91, amb=True)
-    rng = np.random.default_rng(91)
-    m2 = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
-    mon = rng.integers(0, 2, et.n_nodes).astype(np.int32)
-    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
-    t = et.brlen[br].copy()
-    t[3] = 0.0
-    ops = phylo.split_ops(et.ops)
-    sub = br[::3].copy()
-    res = {}
-    for fpm in ("0", "1"):
-        set_tune(monkeypatch, "JIT_FPM", fpm)
-        eng = engine_for(et, 4, C, 7000, states, alph.init_table, rates, probs, m.pi, [m, m2], model_of_node=mon,
-                         flags=plk.PLK_FLAG_NONNEG_GUARD | flags)
-        eng.set_timing(True)
-        out = []
-        for k, (b, tt) in enumerate([(br, t), (br, t * 1.2), (sub, t[::3] * 0.7)]):
-            lnl, blocks = eng.evaluate(b, tt, ops, et.root, mon[b])
-            P = np.stack([eng.get_pmatrix(int(x)) for x in br])
-            out.append((lnl, blocks.copy(), P))
-        assert eng.kernel_path() == "jit_tree4"
-        tm = eng.get_timing()
-        assert (tm["pmat_ms"] == 0.0) == (fpm == "1"), tm   # no P(t) launch when fused
-        res[fpm] = out
-        del eng
-    for (l0, b0, p0), (l1, b1, p1) in zip(res["0"], res["1"]):
-        assert l0 == l1 and np.array_equal(b0, b1) and np.array_equal(p0, p1)
-    assert np.array_equal(res["1"][0][2][3], np.broadcast_to(np.eye(4), (C, 4, 4)))
-
-
 @pytest.mark.parametrize("C,scaling,n_patterns", [(4, False, 9000), (1, False, 4096), (4, True, 5000),
                                                    (2, False, 130)])
 def test_pmat4_and_block_sums(C, scaling, n_patterns):

@@ -28,7 +28,7 @@ def emitter(tmp_path_factory):
 
 
 @pytest.mark.parametrize("args", [
-    ("tree4", "4", "0"), ("tree4", "4", "1", "0", "1"), ("tree4", "1", "1"), ("tree4", "4", "0", "0", "0", "1"),
+    ("tree4", "4", "0"), ("tree4", "4", "1", "0", "1"), ("tree4", "1", "1"),
     ("treeM", "4", "1", "20"), ("treeM", "1", "0", "20"), ("treeM", "4", "0", "4"),
     ("treeM_deep", "4", "1", "20", "5")])
 def test_emitted_kernel_compiles_for_gfx950(emitter, args):
