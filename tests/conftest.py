@@ -27,6 +27,18 @@ def root_dir():
     return ROOT
 
 
+def run_make(*args):
+    """`make *args` under an exclusive lock: pytest-xdist workers share the build trees, and a
+    worker's make once rewrote a binary another worker was executing (ETXTBSY).  After the
+    first build the others find nothing to do."""
+    import fcntl
+    import subprocess
+    import tempfile
+    with open(os.path.join(tempfile.gettempdir(), "plk_tests_make.lock"), "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        subprocess.run(["make", *args], check=True)
+
+
 def set_tune(monkeypatch, key, value):
     """Set one of libplk's tuning knobs: they all live in PLK_TUNE="KEY=value,..."
     (csrc/plk.hip tune_get)."""

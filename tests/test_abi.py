@@ -7,6 +7,7 @@ import subprocess
 import pytest
 
 import plk
+from conftest import run_make
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -19,7 +20,7 @@ def _declared():
 
 def _ensure_built():
     if not os.path.exists(plk.LIB_PATH):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "bpp-phyl_amd")], check=True)
+        run_make("-s", "-C", os.path.join(ROOT, "bpp-phyl_amd"))
 
 
 def test_header_symbols_listed_in_binding():

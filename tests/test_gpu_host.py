@@ -7,6 +7,7 @@ import subprocess
 import pytest
 
 import plk
+from conftest import run_make
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -15,7 +16,7 @@ HOST = os.path.join(ROOT, "bpp-phyl_amd", "host")
 
 def test_cpp_drop_in_goldens():
     assert plk.device_count() > 0, "no GPU visible"
-    subprocess.run(["make", "-s", "-j8", "-C", HOST], check=True)
+    run_make("-s", "-j8", "-C", HOST)
     r = subprocess.run([os.path.join(HOST, "bin", "test_likelihood_gpu")], capture_output=True, text=True,
                        timeout=600)
     print(r.stdout)
@@ -30,7 +31,7 @@ def test_cpp_drop_in_nh():
     parametrisations), per-theta evaluations recomputing one eigen-system, and the
     BrLenRoot / RootPosition derivatives against central differences."""
     assert plk.device_count() > 0, "no GPU visible"
-    subprocess.run(["make", "-s", "-j8", "-C", HOST], check=True)
+    run_make("-s", "-j8", "-C", HOST)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     r = subprocess.run([os.path.join(HOST, "bin", "test_likelihood_nh_gpu")], capture_output=True, text=True,
                        timeout=600, cwd=ROOT)

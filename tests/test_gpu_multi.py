@@ -20,6 +20,7 @@ import pytest
 import phylo
 import plk
 import workload
+from conftest import run_make
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -185,7 +186,7 @@ def test_cpp_drop_in_sharded_goldens():
     """The Bio++ mirror's drop-in program with the patterns sharded over two handles on the
     GPU (BPP_AMD_DEVICES=0,0): the reference goldens, optimisers included."""
     host = os.path.join(ROOT, "bpp-phyl_amd", "host")
-    subprocess.run(["make", "-s", "-j8", "-C", host], check=True)
+    run_make("-s", "-j8", "-C", host)
     env = dict(os.environ, BPP_AMD_DEVICES="0,0")
     r = subprocess.run([os.path.join(host, "bin", "test_likelihood_gpu")], capture_output=True, text=True,
                        timeout=600, env=env)

@@ -12,6 +12,7 @@ from scipy.linalg import expm
 import oracle
 import phylo
 import workload
+from conftest import run_make
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
@@ -20,8 +21,8 @@ HOST = os.path.join(ROOT, "bpp-phyl_amd", "host")
 
 @pytest.fixture(scope="module")
 def host_records():
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "bpp-phyl_amd")], check=True)
-    subprocess.run(["make", "-s", "-j8", "-C", HOST], check=True)
+    run_make("-s", "-C", os.path.join(ROOT, "bpp-phyl_amd"))
+    run_make("-s", "-j8", "-C", HOST)
     out = subprocess.run([os.path.join(HOST, "bin", "test_host_cpu")], check=True, capture_output=True,
                          text=True).stdout
     return [json.loads(line) for line in out.splitlines() if line.strip()]
@@ -272,8 +273,8 @@ def test_reference_likelihood_test_compiles_and_links_unchanged(name, tmp_path):
     src = os.path.join(REF_DIR, name + ".cpp")
     if not os.path.exists(src):
         pytest.skip("reference tree absent")
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "bpp-phyl_amd")], check=True)
-    subprocess.run(["make", "-s", "-j8", "-C", HOST, "libbpp_phyl_amd.so"], check=True)
+    run_make("-s", "-C", os.path.join(ROOT, "bpp-phyl_amd"))
+    run_make("-s", "-j8", "-C", HOST, "libbpp_phyl_amd.so")
     exe = str(tmp_path / name)
     r = subprocess.run(["g++", "-std=c++17", "-O0", "-w", "-I" + os.path.join(HOST, "include"),
                         "-I" + os.path.join(ROOT, "include"), "-o", exe, src, "-L" + HOST, "-lbpp_phyl_amd",

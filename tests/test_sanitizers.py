@@ -7,6 +7,7 @@ results as the ordinary builds.  Host code only: GPU sanitizers are not availabl
 import json
 import os
 import subprocess
+from conftest import run_make
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HOST = os.path.join(ROOT, "bpp-phyl_amd", "host")
@@ -23,14 +24,14 @@ def _run(exe, tmp_path):
 
 
 def test_oracle_asan_ubsan_clean(tmp_path):
-    subprocess.run(["make", "-s", "-C", ORACLE, "asan"], check=True)
+    run_make("-s", "-C", ORACLE, "asan")
     out = _run(os.path.join(ORACLE, "_san", "oracle_check"), tmp_path)
     assert out.strip().endswith("PASSED"), out
 
 
 def test_host_mirror_asan_ubsan_clean(tmp_path):
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "bpp-phyl_amd")], check=True)
-    subprocess.run(["make", "-s", "-j8", "-C", HOST, "asan", "bin/test_host_cpu"], check=True)
+    run_make("-s", "-C", os.path.join(ROOT, "bpp-phyl_amd"))
+    run_make("-s", "-j8", "-C", HOST, "asan", "bin/test_host_cpu")
     san = [json.loads(x) for x in _run(os.path.join(HOST, "san", "test_host_cpu"), tmp_path).splitlines() if x.strip()]
     ref = subprocess.run([os.path.join(HOST, "bin", "test_host_cpu")], check=True, capture_output=True,
                          text=True, timeout=300).stdout
