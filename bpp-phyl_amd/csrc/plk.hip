@@ -2088,7 +2088,6 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // class in the wave a ring slot is C x larger, so there two events ahead (cfg5 0.385 ms
     // at L = 2, 0.391 at L = 1; 1.48 vs 1.04 ms at L = 3 vs 1 before the P(t) stream)
     sh.L = tune_int("JIT_L", h->prog_ciw ? 2 : 3, 1, 8);
-    sh.Lr = tune_int("JIT_LR", 0, 0, 8);
     sh.minw = 0;
     // speculative no-rescale pass (plk_jit.hpp): a win only where rescaling never
     // fires; on cfg5 it fires in almost every super-block (1.27 vs 1.14 ms), so opt-in
@@ -2104,7 +2103,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     if (!h->jit_fn || sh.C != h->jit_shape.C || sh.CW != h->jit_shape.CW ||
         sh.pin != h->jit_shape.pin ||
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
-        sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L || sh.Lr != h->jit_shape.Lr ||
+        sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
         sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;

@@ -382,7 +382,6 @@ struct JitShape {
   int TD = 0;       // most table doubles of any fragment (JitPlan::tab_doubles)
   bool scale = false;
   int L = 1;        // operand fetch lookahead (events)
-  int Lr = 0;       // the lookahead of fragments without tip tables (0: L)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
   size_t lds_bytes() const {
@@ -846,17 +845,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     snprintf(buf, sizeof(buf), "    double A%d[V_]; int K%d[PW_] = {}; (void)K%d;\n", d, d, d);
     s += buf;
   }
-  // A fragment without tip tables (one that only loads stored partials: cfg5's root fragment
-  // over the eight subtree roots) streams its operands from HBM; it fetches them Lr events
-  // ahead (JitShape::Lr), the others L
-  auto frag_L = [&](size_t f) {
-    for (const JitEvent& e : events[f])
-      if (e.op == T_TIP) return L;
-    return std::max(L, sh.Lr);
-  };
-  int Lmax = L;
-  for (size_t f = 0; f < events.size(); ++f) Lmax = std::max(Lmax, frag_L(f));
-  for (int r = 0; r <= Lmax; ++r) {
+  for (int r = 0; r <= L; ++r) {
     snprintf(buf, sizeof(buf), "    double F%d[V_]; int FK%d[PW_] = {}; (void)FK%d; int Q%d = 0; (void)Q%d;\n", r, r,
              r, r, r);
     s += buf;
@@ -864,7 +853,6 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   s += "    switch (frag) {\n";
   for (size_t f = 0; f < events.size(); ++f) {
     if (leader[f] != (int)f) continue;
-    const int L = frag_L(f);
     const std::vector<JitEvent>& ev = events[f];
     std::vector<int> slot(ev.size(), -1), fetchers;
     for (size_t i = 0; i < ev.size(); ++i)
