@@ -73,6 +73,46 @@ def test_multi_device_handle_bitwise(config, n, flags, devs):
     assert wm["patterns"] == n and wm["node_updates"] == w1["node_updates"]
 
 
+def test_shard_request_staging_after_allocation_churn():
+    """The round-4 -inf shard (profiles/r05/ab_runs.md): a fresh shard handle's
+    P(t) request, staged in host-written device memory, read back as other data after many
+    device buffers had been freed and the caches thrashed (tools/micro/l2_stale.hip
+    reproduces it).  The staging is pinned host memory now; here the same conditions -- 48
+    handles with their buffers created and destroyed, a 1.6 GB write -- come before fresh
+    two- and three-shard handles whose 1 022-branch requests take the staging path, and
+    their lnL and block sums must equal one handle's bitwise, evaluation after evaluation."""
+    n = 3 * 4096 + 9
+    wl = workload.make_workload("nh_gtr_g4_dna_2M_512", n_patterns=n)
+    et = wl.et
+    states = wl.simulate(0, n)
+    base = plk.PLK_FLAG_SCALING | plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    mi = wl.model_of_node[br].astype(np.int32)
+    ops = phylo.split_ops(et.ops)
+    for k in range(48):  # freed device buffers of many sizes, with kernels' data in them
+        m = 4096 * (1 + k % 5)
+        e = _setup(plk.Engine(0, wl.S, wl.C, m, et.n_tips, et.n_internal, len(wl.models), base), wl,
+                   wl.simulate(k, k + m))
+        e.evaluate(br, et.brlen[br] * (1.0 + 0.01 * k), ops, et.root, mi)
+        e.close()
+    # a cache thrash: a materialising 64-taxon traversal writes 62 partials x 200k x 128 B
+    wl2 = workload.make_workload("gtr_g4_dna_1M_64", n_patterns=200_000)
+    big = _setup(plk.Engine(0, 4, 4, 200_000, wl2.et.n_tips, wl2.et.n_internal, 1, plk.PLK_FLAG_NONNEG_GUARD), wl2,
+                 wl2.simulate(0, 200_000))
+    br2 = np.array([v for v in range(wl2.et.n_nodes) if v != wl2.et.root], dtype=np.int32)
+    big.evaluate(br2, wl2.et.brlen[br2], phylo.split_ops(wl2.et.ops), wl2.et.root)
+    big.close()
+    one = _setup(plk.Engine(0, wl.S, wl.C, n, et.n_tips, et.n_internal, len(wl.models), base), wl, states)
+    for devs in ([0, 0], [0, 0, 0]):
+        multi = _setup(plk.Engine(devs, wl.S, wl.C, n, et.n_tips, et.n_internal, len(wl.models), base), wl, states)
+        for scale in (1.0, 0.7, 1.3):
+            t = et.brlen[br] * scale
+            l1, b1 = one.evaluate(br, t, ops, et.root, mi)
+            lm, bm = multi.evaluate(br, t, ops, et.root, mi)
+            assert np.isfinite(lm) and l1 == lm and np.array_equal(b1, bm)
+        multi.close()
+
+
 def test_multi_device_branch_derivatives():
     wl = workload.make_workload("gtr_g4_dna_1M_64", n_patterns=2 * 4096 + 11)
     et, n = wl.et, wl.n_patterns
