@@ -379,8 +379,9 @@ struct plk_handle_s {
   int64_t* d_comm_counts = nullptr;       // block sums per rank
   int32_t* h_uflow = nullptr;             // mapped pinned: root-reduction underflow flag (plk_root_underflow)
   int32_t* d_uflow = nullptr;             // its device address
-  double* h_total = nullptr;              // mapped pinned: the global lnL
-  double* d_total = nullptr;              // its device address
+  double* h_blk_all = nullptr;            // mapped pinned: every rank's block sums [comm_ranks][comm_cmax]
+  double* d_blk_all_map = nullptr;        // its device address
+  std::vector<int64_t> comm_counts;       // block sums per rank (host copy)
   double* d_xch = nullptr;                // derivative sums exchanged under the communicator
   double* d_xch_all = nullptr;
   size_t d_xch_cap = 0, d_xch_all_cap = 0;
@@ -1151,9 +1152,10 @@ void comm_release(plk_handle h) {
   h->d_blk_local = h->d_blk_all = h->d_xch = h->d_xch_all = nullptr;
   h->d_xch_cap = h->d_xch_all_cap = 0;
   h->d_comm_counts = nullptr;
-  if (h->h_total) hipHostFree(h->h_total);
-  h->h_total = nullptr;
-  h->d_total = nullptr;
+  if (h->h_blk_all) hipHostFree(h->h_blk_all);
+  h->h_blk_all = nullptr;
+  h->d_blk_all_map = nullptr;
+  h->comm_counts.clear();
   h->comm_ranks = 0;
   h->comm_rank = 0;
   h->comm_cmax = 0;
@@ -1190,10 +1192,12 @@ int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id) {
     if ((rc = dalloc(h, (void**)&h->d_blk_local, (size_t)cmax * sizeof(double)))) return rc;
     if ((rc = dalloc(h, (void**)&h->d_blk_all, (size_t)n_ranks * cmax * sizeof(double)))) return rc;
     HIPCHK(h, hipMemset(h->d_blk_local, 0, (size_t)cmax * sizeof(double)));
-    if (hipHostMalloc((void**)&h->h_total, sizeof(double), hipHostMallocMapped) != hipSuccess ||
-        hipHostGetDevicePointer((void**)&h->d_total, h->h_total, 0) != hipSuccess)
-      return fail(h, PLK_ERR_OOM, "pinned total");
+    if (hipHostMalloc((void**)&h->h_blk_all, (size_t)n_ranks * cmax * sizeof(double), hipHostMallocMapped) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void**)&h->d_blk_all_map, h->h_blk_all, 0) != hipSuccess)
+      return fail(h, PLK_ERR_OOM, "pinned block sums of every rank");
     h->comm_cmax = cmax;
+    h->comm_counts = counts;
     return PLK_OK;
   };
   int rc = env_is("PLK_TEST_COMM_FAIL", '1') ? fail(h, PLK_ERR_OOM, "forced exchange-setup failure (test)") : setup();
@@ -3558,35 +3562,21 @@ static int multi_root_loglik(plk_handle h, int root, double* lnl, double* site_l
 
 namespace {
 
-// global lnL of a communicator run: every rank's block sums in rank order (ranks hold
-// consecutive pattern ranges), each rank's in block order -- the same sequence of adds as
-// one process over all patterns; this rank's own block sums are copied to the mapped host
-// buffer beside it.  The sequence is one dependent chain of adds, so the workgroup stages
-// the block sums in LDS (coalesced, in chunks) and one thread runs the chain from LDS: the
-// loads leave the chain (a thread walking global memory paid a load latency per add --
-// ~20 us per evaluation at one rank, 8x that at eight)
-constexpr int kCommChunk = 4096;
-__global__ void comm_sum_kernel(const double* __restrict__ all, const int64_t* __restrict__ counts, int n_ranks,
-                                int64_t cmax, const double* __restrict__ local, int64_t n_local,
-                                double* __restrict__ local_out, double* __restrict__ total_out) {
-  __shared__ double buf[kCommChunk];
-  double s = 0.0;
-  for (int r = 0; r < n_ranks; ++r) {
-    const int64_t n = counts[r];
-    const double* src = all + (int64_t)r * cmax;
-    for (int64_t b0 = 0; b0 < n; b0 += kCommChunk) {
-      const int m = (int)(n - b0 < kCommChunk ? n - b0 : kCommChunk);
-      __syncthreads();  // the previous chunk is summed
-      for (int i = threadIdx.x; i < m; i += blockDim.x) buf[i] = src[b0 + i];
-      __syncthreads();
-      if (threadIdx.x == 0) {
-#pragma unroll 16
-        for (int i = 0; i < m; ++i) s += buf[i];
-      }
-    }
+// A communicator run's global lnL is every rank's block sums in rank order (ranks hold
+// consecutive pattern ranges), each rank's in block order -- the same sequence of adds as one
+// process over all patterns.  That sequence is one dependent chain of adds, which the host
+// runs faster than one GPU thread (~4 vs ~10 cycles per add at a few GHz: 1 960 adds at eight
+// ranks of 1 M patterns); this kernel only moves the gathered block sums, and this rank's
+// own, into mapped host memory, every thread a share.
+__global__ void comm_copy_kernel(const double* __restrict__ all, int64_t n_all, const double* __restrict__ local,
+                                 int64_t n_local, double* __restrict__ all_out, double* __restrict__ local_out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_all + n_local;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n_all)
+      all_out[i] = all[i];
+    else
+      local_out[i - n_all] = local[i - n_all];
   }
-  if (threadIdx.x == 0) *total_out = s;
-  for (int64_t i = threadIdx.x; i < n_local; i += blockDim.x) local_out[i] = local[i];
 }
 
 // block sums land in mapped host memory, or in the all-gather's send buffer under a communicator
@@ -3618,8 +3608,9 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
     if (ncclAllGather(h->d_blk_local, h->d_blk_all, (size_t)h->comm_cmax, ncclFloat64, h->comm, h->stream) !=
         ncclSuccess)
       return fail(h, PLK_ERR_DEVICE, "ncclAllGather of the block sums failed");
-    comm_sum_kernel<<<1, 256, 0, h->stream>>>(h->d_blk_all, h->d_comm_counts, h->comm_ranks, h->comm_cmax,
-                                              h->d_blk_local, h->n_blocks, h->block_sums, h->d_total);
+    const int64_t n_all = (int64_t)h->comm_ranks * h->comm_cmax;
+    comm_copy_kernel<<<(unsigned)((n_all + h->n_blocks + 255) / 256), 256, 0, h->stream>>>(
+        h->d_blk_all, n_all, h->d_blk_local, h->n_blocks, h->d_blk_all_map, h->block_sums);
     HIPCHK(h, hipGetLastError());
   }
   if (site_lnl)
@@ -3634,7 +3625,10 @@ int root_finish(plk_handle h, double* lnl, double* block_sums, bool wait = true)
     if (int rc = stream_wait(h)) return rc;
   double s = 0.0;
   if (h->comm) {
-    s = *h->h_total;
+    for (int r = 0; r < h->comm_ranks; ++r) {  // rank order, block order (comm_copy_kernel)
+      const double* b = h->h_blk_all + (size_t)r * h->comm_cmax;
+      for (int64_t i = 0; i < h->comm_counts[(size_t)r]; ++i) s += b[i];
+    }
   } else {
     for (int b = 0; b < h->n_blocks; ++b) s += h->h_blocks[b];  // fixed order: block 0, 1, 2, ...
   }
