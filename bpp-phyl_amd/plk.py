@@ -205,6 +205,7 @@ class Engine:
         self.n_tips, self.n_internal = n_tips, n_internal
         self._ops_cache = None
         self._eval_cache = None
+        self._eval_call = None
         if isinstance(device, (list, tuple)):
             devs = (ct.c_int * len(device))(*device)
             rc = self.lib.plk_create_multi(devs, len(device), n_states, n_classes, n_patterns, n_tips, n_internal,
@@ -315,13 +316,24 @@ class Engine:
             self._eval_cache = (branches, models, b, m, b.ctypes.data_as(ct.POINTER(ct.c_int32)),
                                 None if m is None else m.ctypes.data_as(ct.POINTER(ct.c_int32)), blocks,
                                 _d(blocks), tbuf, _d(tbuf), ct.c_double(0.0))
-        _, _, b, _, bp, mp, blocks_buf, blocks_p, tbuf, tbuf_p, lnl = self._eval_cache
-        if np.shape(t) != tbuf.shape:
+        c = self._eval_cache
+        _, _, b, _, bp, mp, blocks_buf, blocks_p, tbuf, tbuf_p, lnl = c
+        if getattr(t, "shape", None) != tbuf.shape and np.shape(t) != tbuf.shape:
             raise ValueError(f"branch lengths: {np.shape(t)} for {tbuf.shape[0]} branches")
         tbuf[:] = t  # (float64 conversion included)
-        arr = self._op_array(ops)
-        self._chk(self.lib.plk_evaluate(self.h, len(b), bp, mp, tbuf_p, arr, len(arr), root, ct.byref(lnl),
-                                        blocks_p))
+        # The call's arguments are the same ctypes objects from one evaluation to the next
+        # (same op list object, root and index arrays): they are made once, and passed to an
+        # entry point without argtypes -- ctypes' per-call argument conversion cost ~2 of the
+        # ~3 us of a ten-argument call (the objects are already the C types plk.h declares)
+        call = self._eval_call
+        if call is None or call[0] is not ops or call[1] != root or call[2] is not c:
+            arr = self._op_array(ops)
+            fn = self.lib["plk_evaluate"]  # (a fresh function object: lib.plk_evaluate keeps its argtypes)
+            fn.restype = ct.c_int
+            args = (self.h, ct.c_int(len(b)), bp, mp, tbuf_p, ct.cast(arr, ct.POINTER(plk_op)), ct.c_int(len(arr)),
+                    ct.c_int(root), ct.byref(lnl), blocks_p)
+            call = self._eval_call = (ops, root, c, fn, args, arr)
+        self._chk(call[3](*call[4]))
         return lnl.value, blocks_buf.copy()
 
     def get_partials(self, node: int) -> np.ndarray:
