@@ -339,6 +339,8 @@ struct plk_handle_s {
   uint32_t* d_links = nullptr;
   size_t d_links_cap = 0;
   KOpL* d_opsl = nullptr;
+  KKid* d_kidsl = nullptr;  // the compressed ops' child records
+  size_t d_kidsl_cap = 0;
   size_t d_opsl_cap = 0;
   int64_t cmp_work = 0;                               // sum over nodes of distinct patterns
   // tree of the traversals so far: sons per node, merged over plk_update_partials calls
@@ -1111,7 +1113,7 @@ int plk_destroy(plk_handle h) {
                   h->d_ops, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
                   h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre, h->d_sbctr,
-                  h->d_cherry_rows};
+                  h->d_cherry_rows, h->d_kidsl};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) (void)hipHostFree(h->h_req);
@@ -2437,7 +2439,6 @@ int build_compression(plk_handle h, const plk_op* ops, int n_ops) {
   }
   std::vector<char> produced(h->n_nodes, 0), is_child(h->n_nodes, 0);
   for (const auto& n : nodes) {
-    if (n.kids.size() > 3) return fail(h, PLK_ERR_UNSUPPORTED, "pattern compression: node %d has > 3 children", n.node);
     for (int c : n.kids) {
       if (c >= nt && !produced[c])
         return fail(h, PLK_ERR_STATE, "pattern compression: child %d of node %d not produced by this call", c, n.node);
@@ -2528,6 +2529,7 @@ int build_compression(plk_handle h, const plk_op* ops, int n_ops) {
   for (int l = 0; l <= max_level; ++l) start[l + 1] += start[l];
   std::vector<int> fill(start.begin(), start.end() - 1);
   std::vector<KOpL> kops(nodes.size());
+  std::vector<KKid> kid_recs;
   std::vector<int64_t> link_off(nodes.size());
   int64_t total = 0;
   for (size_t ni = 0; ni < nodes.size(); ++ni) {
@@ -2541,12 +2543,16 @@ int build_compression(plk_handle h, const plk_op* ops, int n_ops) {
     k.parent = nodes[ni].node - nt;
     k.n = (int32_t)nodes[ni].kids.size();
     k.D = (int32_t)nodeD[ni];
+    k.k0 = (int32_t)kid_recs.size();
     for (int j = 0; j < k.n; ++j) {
       const int c = nodes[ni].kids[(size_t)j];
-      k.branch[j] = c;
-      k.is_tip[j] = c < nt;
-      k.child[j] = c < nt ? c : c - nt;
-      k.link[j] = link_off[ni] + (int64_t)j * nodeD[ni];
+      KKid kd;
+      std::memset(&kd, 0, sizeof(kd));
+      kd.branch = c;
+      kd.is_tip = c < nt;
+      kd.child = c < nt ? c : c - nt;
+      kd.link = link_off[ni] + (int64_t)j * nodeD[ni];
+      kid_recs.push_back(kd);
     }
     kops[(size_t)fill[nlev[ni]]++] = k;
     h->cmp_level_maxD[nlev[ni]] = std::max<int>(h->cmp_level_maxD[nlev[ni]], k.D);
@@ -2555,6 +2561,9 @@ int build_compression(plk_handle h, const plk_op* ops, int n_ops) {
   if (rc) return rc;
   rc = ensure_cap(h, (void**)&h->d_opsl, &h->d_opsl_cap, kops.size() * sizeof(KOpL));
   if (rc) return rc;
+  rc = ensure_cap(h, (void**)&h->d_kidsl, &h->d_kidsl_cap, std::max<size_t>(kid_recs.size(), 1) * sizeof(KKid));
+  if (rc) return rc;
+  HIPCHK(h, hipMemcpy(h->d_kidsl, kid_recs.data(), kid_recs.size() * sizeof(KKid), hipMemcpyHostToDevice));
   for (size_t ni = 0; ni < nodes.size(); ++ni)
     HIPCHK(h, hipMemcpy(h->d_links + link_off[ni], node_links[ni].data(), node_links[ni].size() * sizeof(uint32_t),
                         hipMemcpyHostToDevice));
@@ -2569,18 +2578,18 @@ template <int C>
 void launch_links(plk_handle h, const KOpL* d, int cnt, int maxD, const PartialsArgs& a) {
   const dim3 grid((unsigned)((maxD + 255) / 256), (unsigned)cnt), block(256);
   if (h->flags & PLK_FLAG_SCALING)
-    partials_links_s4_kernel<C, true><<<grid, block, 0, h->stream>>>(d, a, h->d_links);
+    partials_links_s4_kernel<C, true><<<grid, block, 0, h->stream>>>(d, h->d_kidsl, a, h->d_links);
   else
-    partials_links_s4_kernel<C, false><<<grid, block, 0, h->stream>>>(d, a, h->d_links);
+    partials_links_s4_kernel<C, false><<<grid, block, 0, h->stream>>>(d, h->d_kidsl, a, h->d_links);
 }
 
 template <int S, int XB>
 void launch_links_generic_S(plk_handle h, const KOpL* d, int cnt, int maxD, const PartialsArgs& a, size_t lds) {
   const dim3 grid((unsigned)((maxD + 255) / 256), (unsigned)cnt), block(256);
   if (h->flags & PLK_FLAG_SCALING)
-    partials_links_generic_kernel<S, XB, true><<<grid, block, lds, h->stream>>>(d, a, h->d_links, h->C);
+    partials_links_generic_kernel<S, XB, true><<<grid, block, lds, h->stream>>>(d, h->d_kidsl, a, h->d_links, h->C);
   else
-    partials_links_generic_kernel<S, XB, false><<<grid, block, lds, h->stream>>>(d, a, h->d_links, h->C);
+    partials_links_generic_kernel<S, XB, false><<<grid, block, lds, h->stream>>>(d, h->d_kidsl, a, h->d_links, h->C);
 }
 
 int launch_links_generic(plk_handle h, const KOpL* d, int cnt, int maxD, const PartialsArgs& a) {

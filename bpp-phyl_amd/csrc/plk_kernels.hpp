@@ -183,70 +183,83 @@ __global__ __launch_bounds__(256) void partials_s4_kernel(const KOp* __restrict_
 // ---------------------------------------------------------------------------
 struct KOpL {
   int32_t parent;    // internal slot
-  int32_t n;         // children (1..3)
+  int32_t n;         // children (any number: a polytomy's whole list)
   int32_t D;         // distinct patterns of the parent's subtree
-  int32_t pad_;
-  int32_t child[3];  // tip index or internal slot
-  int32_t branch[3]; // node index of the child = transition-matrix index
-  int32_t is_tip[3];
-  int32_t pad2_;
-  int64_t link[3];   // offset of the child's link array (D uint32) in the link pool
+  int32_t k0;        // its first child record (KKid)
 };
+struct KKid {
+  int32_t child;     // tip index or internal slot
+  int32_t branch;    // node index of the child = transition-matrix index
+  int32_t is_tip;
+  int32_t pad_;
+  int64_t link;      // offset of the child's link array (D uint32) in the link pool
+};
+// The links kernels stage the tables of three children at a time in LDS; a node with more
+// (a polytomy) takes them three by three, its product in the children's order.
+constexpr int kLinkGroup = 3;
 
 template <int C, bool SCALE>
-__global__ __launch_bounds__(256) void partials_links_s4_kernel(const KOpL* __restrict__ ops, PartialsArgs a,
-                                                                const uint32_t* __restrict__ links) {
+__global__ __launch_bounds__(256) void partials_links_s4_kernel(const KOpL* __restrict__ ops, const KKid* __restrict__ kids,
+                                                                PartialsArgs a, const uint32_t* __restrict__ links) {
   constexpr int S = 4;
   constexpr int CS = C * S;
-  __shared__ double tipT[3][C * kMaxCodes4 * S];
+  __shared__ double tipT[kLinkGroup][C * kMaxCodes4 * S];
   const KOpL& op = ops[blockIdx.y];
   const int n = op.n;
   const int nc = a.n_codes;
   if ((int)(blockIdx.x * blockDim.x) >= op.D) return;  // whole workgroup past this op's patterns
-  for (int k = 0; k < n; ++k)
-    if (op.is_tip[k]) {
-      const double* src = a.tipP + (size_t)op.child[k] * (C * nc * S);
-      for (int i = threadIdx.x; i < C * nc * S; i += blockDim.x) tipT[k][i] = src[i];
-    }
-  __syncthreads();
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= op.D) return;
   double acc[C][S];
   int cnt = 0;
 #pragma unroll
   for (int c = 0; c < C; ++c)
 #pragma unroll
     for (int x = 0; x < S; ++x) acc[c][x] = 1.0;
-  for (int k = 0; k < n; ++k) {
-    const uint32_t l = links[op.link[k] + j];
-    if (op.is_tip[k]) {
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const double* t = &tipT[k][(c * nc + (int)l) * S];
-#pragma unroll
-        for (int x = 0; x < S; ++x) acc[c][x] *= t[x];
+  for (int g0 = 0; g0 < n; g0 += kLinkGroup) {
+    const int gn = n - g0 < kLinkGroup ? n - g0 : kLinkGroup;
+    if (g0 > 0) __syncthreads();  // the previous group's tables are read
+    for (int k = 0; k < gn; ++k) {
+      const KKid& kd = kids[op.k0 + g0 + k];
+      if (kd.is_tip) {
+        const double* src = a.tipP + (size_t)kd.child * (C * nc * S);
+        for (int i = threadIdx.x; i < C * nc * S; i += blockDim.x) tipT[k][i] = src[i];
       }
-    } else {
-      const double* __restrict__ P = a.pmats + (size_t)op.branch[k] * (C * S * S);
-      const double* L = a.partials + (size_t)op.child[k] * a.slot_stride + (size_t)(l >> 7) * (CS * kTile) + (l & 127);
-      double v[C][S];
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int y = 0; y < S; ++y) v[c][y] = L[(c * S + y) * kTile];
-#pragma unroll
-      for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int x = 0; x < S; ++x) {
-          const double* Px = P + (c * S + x) * S;
-          double s = Px[0] * v[c][0];
-#pragma unroll
-          for (int y = 1; y < S; ++y) s = __builtin_fma(Px[y], v[c][y], s);
-          acc[c][x] *= s;
-        }
-      if (SCALE) cnt += a.scale[(size_t)op.child[k] * a.n_pad + l];
     }
+    __syncthreads();
+    if (j < op.D)
+      for (int k = 0; k < gn; ++k) {
+        const KKid& kd = kids[op.k0 + g0 + k];
+        const uint32_t l = links[kd.link + j];
+        if (kd.is_tip) {
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            const double* t = &tipT[k][(c * nc + (int)l) * S];
+#pragma unroll
+            for (int x = 0; x < S; ++x) acc[c][x] *= t[x];
+          }
+        } else {
+          const double* __restrict__ P = a.pmats + (size_t)kd.branch * (C * S * S);
+          const double* L = a.partials + (size_t)kd.child * a.slot_stride + (size_t)(l >> 7) * (CS * kTile) + (l & 127);
+          double v[C][S];
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int y = 0; y < S; ++y) v[c][y] = L[(c * S + y) * kTile];
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int x = 0; x < S; ++x) {
+              const double* Px = P + (c * S + x) * S;
+              double s = Px[0] * v[c][0];
+#pragma unroll
+              for (int y = 1; y < S; ++y) s = __builtin_fma(Px[y], v[c][y], s);
+              acc[c][x] *= s;
+            }
+          if (SCALE) cnt += a.scale[(size_t)kd.child * a.n_pad + l];
+        }
+      }
   }
+  if (j >= op.D) return;
   if (SCALE) {
     double m = 0.0;
 #pragma unroll
@@ -275,7 +288,8 @@ __global__ __launch_bounds__(256) void partials_links_s4_kernel(const KOpL* __re
 // another order: 1e-12 apart).  One lane = one distinct pattern j of the parent (its slot
 // entry j).
 template <int S, int XB, bool SCALE>
-__global__ __launch_bounds__(256) void partials_links_generic_kernel(const KOpL* __restrict__ ops, PartialsArgs a,
+__global__ __launch_bounds__(256) void partials_links_generic_kernel(const KOpL* __restrict__ ops,
+                                                                     const KKid* __restrict__ kids, PartialsArgs a,
                                                                      const uint32_t* __restrict__ links, int C) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const KOpL& op = ops[blockIdx.y];
@@ -284,60 +298,71 @@ __global__ __launch_bounds__(256) void partials_links_generic_kernel(const KOpL*
   const int CS = C * S;
   if ((int)(blockIdx.x * blockDim.x) >= op.D) return;  // whole workgroup past this op's patterns
   const int per = C * S * ((S > nc) ? S : nc);
-  for (int k = 0; k < n; ++k) {
-    const double* src = op.is_tip[k] ? a.tipP + (size_t)op.child[k] * (C * nc * S)
-                                     : a.pmats + (size_t)op.branch[k] * (C * S * S);
-    const int cnt = op.is_tip[k] ? C * nc * S : C * S * S;
-    for (int i = threadIdx.x; i < cnt; i += blockDim.x) lds[k * per + i] = src[i];
-  }
-  __syncthreads();
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= op.D) return;
   double* outp = a.partials + (size_t)op.parent * a.slot_stride + (size_t)(j >> 7) * ((size_t)CS * kTile) + (j & 127);
-  uint32_t l[3] = {0u, 0u, 0u};
-  for (int k = 0; k < n; ++k) l[k] = links[op.link[k] + j];
   int cnt = 0;
-  if (SCALE)
-    for (int k = 0; k < n; ++k)
-      if (!op.is_tip[k]) cnt += a.scale[(size_t)op.child[k] * a.n_pad + l[k]];
   double m = 0.0;
-  for (int c = 0; c < C; ++c) {
-    for (int x0 = 0; x0 < S; x0 += XB) {
-      double acc[XB];
-#pragma unroll
-      for (int xb = 0; xb < XB; ++xb) acc[xb] = 1.0;
-      for (int k = 0; k < n; ++k) {
-        if (op.is_tip[k]) {
-          const double* t = &lds[k * per + (c * nc + (int)l[k]) * S + x0];
-#pragma unroll
-          for (int xb = 0; xb < XB; ++xb) acc[xb] *= t[xb];
-        } else {
-          const double* L = a.partials + (size_t)op.child[k] * a.slot_stride +
-                            (size_t)(l[k] >> 7) * ((size_t)CS * kTile) + (l[k] & 127) + (size_t)c * S * kTile;
-          const double* Pc = &lds[k * per + (c * S + x0) * S];
-          double s[XB];
-          {
-            const double l0 = L[0];
-#pragma unroll
-            for (int xb = 0; xb < XB; ++xb) s[xb] = Pc[xb * S] * l0;
-          }
-#pragma unroll 4
-          for (int y = 1; y < S; ++y) {
-            const double ly = L[(size_t)y * kTile];
-#pragma unroll
-            for (int xb = 0; xb < XB; ++xb) s[xb] = __builtin_fma(Pc[xb * S + y], ly, s[xb]);
-          }
-#pragma unroll
-          for (int xb = 0; xb < XB; ++xb) acc[xb] *= s[xb];
-        }
+  // children three at a time (their tables in LDS); after the first group the product so
+  // far is read back from the parent's slot and extended in the children's order
+  for (int g0 = 0; g0 < n; g0 += kLinkGroup) {
+    const int gn = n - g0 < kLinkGroup ? n - g0 : kLinkGroup;
+    const bool last = g0 + gn == n;
+    if (g0 > 0) __syncthreads();  // the previous group's tables are read
+    for (int k = 0; k < gn; ++k) {
+      const KKid& kd = kids[op.k0 + g0 + k];
+      const double* src = kd.is_tip ? a.tipP + (size_t)kd.child * (C * nc * S) : a.pmats + (size_t)kd.branch * (C * S * S);
+      const int nel = kd.is_tip ? C * nc * S : C * S * S;
+      for (int i = threadIdx.x; i < nel; i += blockDim.x) lds[k * per + i] = src[i];
+    }
+    __syncthreads();
+    if (j >= op.D) continue;
+    uint32_t l[kLinkGroup] = {0u, 0u, 0u};
+    for (int k = 0; k < gn; ++k) l[k] = links[kids[op.k0 + g0 + k].link + j];
+    if (SCALE)
+      for (int k = 0; k < gn; ++k) {
+        const KKid& kd = kids[op.k0 + g0 + k];
+        if (!kd.is_tip) cnt += a.scale[(size_t)kd.child * a.n_pad + l[k]];
       }
+    for (int c = 0; c < C; ++c) {
+      for (int x0 = 0; x0 < S; x0 += XB) {
+        double acc[XB];
 #pragma unroll
-      for (int xb = 0; xb < XB; ++xb) {
-        if (SCALE) m = fmax(m, acc[xb]);
-        outp[(size_t)(c * S + x0 + xb) * kTile] = acc[xb];
+        for (int xb = 0; xb < XB; ++xb) acc[xb] = g0 == 0 ? 1.0 : outp[(size_t)(c * S + x0 + xb) * kTile];
+        for (int k = 0; k < gn; ++k) {
+          const KKid& kd = kids[op.k0 + g0 + k];
+          if (kd.is_tip) {
+            const double* t = &lds[k * per + (c * nc + (int)l[k]) * S + x0];
+#pragma unroll
+            for (int xb = 0; xb < XB; ++xb) acc[xb] *= t[xb];
+          } else {
+            const double* L = a.partials + (size_t)kd.child * a.slot_stride +
+                              (size_t)(l[k] >> 7) * ((size_t)CS * kTile) + (l[k] & 127) + (size_t)c * S * kTile;
+            const double* Pc = &lds[k * per + (c * S + x0) * S];
+            double s[XB];
+            {
+              const double l0 = L[0];
+#pragma unroll
+              for (int xb = 0; xb < XB; ++xb) s[xb] = Pc[xb * S] * l0;
+            }
+#pragma unroll 4
+            for (int y = 1; y < S; ++y) {
+              const double ly = L[(size_t)y * kTile];
+#pragma unroll
+              for (int xb = 0; xb < XB; ++xb) s[xb] = __builtin_fma(Pc[xb * S + y], ly, s[xb]);
+            }
+#pragma unroll
+            for (int xb = 0; xb < XB; ++xb) acc[xb] *= s[xb];
+          }
+        }
+#pragma unroll
+        for (int xb = 0; xb < XB; ++xb) {
+          if (SCALE && last) m = fmax(m, acc[xb]);
+          outp[(size_t)(c * S + x0 + xb) * kTile] = acc[xb];
+        }
       }
     }
   }
+  if (j >= op.D) return;
   if (SCALE) {
     if (m > 0.0 && m < kScaleThr) {
       for (int i = 0; i < CS; ++i) outp[(size_t)i * kTile] *= kScaleUp;

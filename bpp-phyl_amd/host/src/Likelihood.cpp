@@ -180,9 +180,9 @@ void AbstractPlkTreeLikelihood::createEngine(size_t nModels, bool nonNegGuard) {
                    extraFlags_;
   // usePatterns (the reference default): per-subtree site-pattern compression on the device
   // (DRASRTreeLikelihoodData.cpp:218-332, PLK_FLAG_SUBTREE_PATTERNS); not for the double-
-  // recursive classes (their data class has no compression either, DRASDRTreeLikelihoodData)
-  // nor for nodes of more than 3 sons, and BPP_AMD_USE_PATTERNS=0 switches it off
-  compressed_ = usePatterns_ && !(extraFlags_ & PLK_FLAG_DOUBLE_RECURSIVE) && maxSons_ <= 3;
+  // recursive classes (their data class has no compression either, DRASDRTreeLikelihoodData);
+  // BPP_AMD_USE_PATTERNS=0 switches it off
+  compressed_ = usePatterns_ && !(extraFlags_ & PLK_FLAG_DOUBLE_RECURSIVE);
   if (const char* e = std::getenv("BPP_AMD_USE_PATTERNS"))
     if (e[0] == '0') compressed_ = false;
   // Shapes the fused tree kernels serve (4 states with 1, 2 or 4 classes: plk_jit_tree4;

@@ -87,8 +87,8 @@ enum {
                                     each internal node is computed once per distinct pattern of
                                     its subtree and read through pattern links.  Links are
                                     built on the host from the tip codes and the op list (all
-                                    internal children must be produced by the same call);
-                                    4-state models only */,
+                                    internal children must be produced by the same call); any
+                                    state count, polytomies of any degree */,
   PLK_FLAG_DOUBLE_RECURSIVE = 1u << 5 /* DRHomogeneousTreeLikelihood: keep one "upper" conditional
                                     likelihood per branch (the reference's father-side arrays,
                                     DRHomogeneousTreeLikelihood.cpp:543-651) so that

@@ -262,6 +262,65 @@ def test_random_vs_oracle(S, C, n_taxa, n_patterns):
     check(lnl, site, lo, so)
 
 
+def _random_topology(n, rng, lo, hi, poly=0.1):
+    """A random rooted tree: subtrees joined at random (a coalescent-like shape, unbalanced),
+    now and then three or four at once (a polytomy), branch lengths uniform in [lo, hi]."""
+    parts = [f"t{i}" for i in range(n)]
+    while len(parts) > 1:
+        k = 2 if len(parts) < 4 or rng.random() > poly else int(rng.integers(3, 5))
+        idx = sorted(rng.choice(len(parts), size=min(k, len(parts)), replace=False), reverse=True)
+        kids = [parts.pop(int(i)) for i in idx]
+        parts.append("(" + ",".join(f"{c}:{rng.uniform(lo, hi):.5f}" for c in kids) + ")")
+    return phylo.Tree.from_newick(parts[0] + ";")
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_random_topologies_vs_oracle(seed):
+    """Random unbalanced trees (random joins, polytomies, rooted or unrooted), random
+    GTR / LG08 / YN98 models with one to three of them over the branches, 1-4 rate classes,
+    every traversal mode (per-subtree compression for one model), with and without
+    rescaling (long branches) and ambiguity codes, against the oracle at 1e-12 per pattern
+    on the engine's own P(t) -- the fragment cutting, tiers, cherry tables and shape sharing
+    of the generated kernels on shapes no config has."""
+    rng = np.random.default_rng(1000 + seed)
+    S = 20 if seed % 4 == 3 else 64 if seed % 8 == 5 else 4
+    C = 1 if S == 64 else int(rng.choice([1, 2, 3, 4]))
+    n_taxa = int(rng.integers(3, 41 if S == 20 else 31 if S == 64 else 301))
+    n = int(rng.choice([1, 77, 700, 2500]))
+    scaling = bool(rng.random() < 0.4)
+    lo, hi = (0.3, 1.2) if scaling else (0.01, 0.3)
+    tree = _random_topology(n_taxa, rng, lo, hi)
+    unroot = bool(rng.random() < 0.5)
+    et = phylo.engine_tree(tree, unroot=unroot)
+    n_models = int(rng.integers(1, 4))
+    if S == 4:
+        models = [phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5)) for _ in range(n_models)]
+        alph = phylo.DNA
+    elif S == 20:
+        models, alph = [phylo.lg08()] * n_models, phylo.PROTEIN
+    else:
+        models = [phylo.yn98(float(rng.uniform(1.0, 4.0)), float(rng.uniform(0.1, 1.0))) for _ in range(n_models)]
+        alph = phylo.CODON
+    mon = rng.integers(0, n_models, et.n_nodes).astype(np.int32) if n_models > 1 else None
+    rates, probs = phylo.gamma_rates(C, float(rng.uniform(0.3, 2.0))) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("f", et, models, mon, rates, probs, models[0].pi, alph, n, scaling, True, seed)
+    states = wl.simulate(0, n).astype(np.int32)
+    if rng.random() < 0.5:  # ambiguity / gap codes
+        mask = rng.random(states.shape) < 0.1
+        states[mask] = rng.integers(S, alph.n_codes, size=mask.sum())
+    mode = ["lnl_only", "materialize", "levelwise", "subtree"][seed % 4 if n_models == 1 else seed % 3]
+    flags = plk.PLK_FLAG_NONNEG_GUARD | (plk.PLK_FLAG_SUBTREE_PATTERNS if mode == "subtree" else MODES[mode]) | \
+        (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, S, C, n, states, alph.init_table, rates, probs, models[0].pi, models, model_of_node=mon,
+                     flags=flags)
+    lnl, site, _ = run_engine(eng, et)
+    lo_, so = oracle_for(et, states, alph.init_table, rates, probs, models[0].pi, models, model_of_node=mon,
+                         scaling=scaling, pmats=engine_pmats(eng, et))
+    check(lnl, site, lo_, so)
+    lnl2, site2, _ = run_engine(eng, et)  # a second traversal: the same doubles
+    assert lnl2 == lnl and np.array_equal(site2, site)
+
+
 def test_ambiguity_codes_vs_oracle():
     et, m, alph, rates, probs, states = _random_problem(4, 4, 20, 3000, seed=5, amb=True)
     eng = engine_for(et, 4, 4, 3000, states, alph.init_table, rates, probs, m.pi, [m])
@@ -917,6 +976,40 @@ def test_subtree_patterns_follow_new_tip_codes():
     ref = engine_for(et, 4, 4, 2000, states2, alph.init_table, rates, probs, m.pi, [m])
     l0, s0, _ = run_engine(ref, et)
     assert l0 == l1 and np.array_equal(s0, s1)
+
+
+@pytest.mark.parametrize("S,C,scaling", [(4, 4, False), (4, 2, True), (20, 2, False), (64, 1, True)])
+def test_subtree_patterns_polytomy(S, C, scaling):
+    """Per-subtree compression on polytomies of five and four children (the links kernels take
+    the children three at a time, their product in order): against the oracle at 1e-12 and
+    the uncompressed traversal's lnL (the same products; rescaling can only fire at other
+    points, by exact powers of two)."""
+    t = phylo.Tree.from_newick("((a:0.1,b:0.2,c:0.05,d:0.3,e:0.12):0.1,(f:0.2,g:0.1,h:0.4,i:0.3):0.05,j:0.3,k:0.2);")
+    et = phylo.engine_tree(t)
+    assert max(len(ch) for _, ch in et.ops) >= 5
+    rng = np.random.default_rng(S + C)
+    m = {4: lambda: phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5)), 20: phylo.lg08,
+         64: lambda: phylo.yn98(2.0, 0.4)}[S]()
+    alph = {4: phylo.DNA, 20: phylo.PROTEIN, 64: phylo.CODON}[S]
+    rates, probs = phylo.gamma_rates(C, 0.6) if C > 1 else (np.ones(1), np.ones(1))
+    n = 1500
+    if scaling:
+        et.brlen = et.brlen * 8.0
+    wl = workload.Workload("p", et, [m], None, rates, probs, m.pi, alph, n, scaling, True, 17)
+    states = wl.simulate(0, n).astype(np.int32)
+    sc = plk.PLK_FLAG_SCALING if scaling else 0
+    res = []
+    for mode in (plk.PLK_FLAG_SUBTREE_PATTERNS, plk.PLK_FLAG_LEVELWISE):
+        eng = engine_for(et, S, C, n, states, alph.init_table, rates, probs, m.pi, [m],
+                         flags=plk.PLK_FLAG_NONNEG_GUARD | mode | sc)
+        res.append(run_engine(eng, et))
+        if mode == plk.PLK_FLAG_SUBTREE_PATTERNS:
+            assert eng.kernel_path() == "subtree_patterns"
+            pm = engine_pmats(eng, et)
+    (l1, s1, _), (l2, s2, _) = res
+    lo, so = oracle_for(et, states, alph.init_table, rates, probs, m.pi, [m], scaling=scaling, pmats=pm)
+    check(l1, s1, lo, so)
+    assert np.allclose(s1, s2, rtol=1e-13, atol=0)
 
 
 def test_subtree_patterns_errors():
