@@ -280,3 +280,56 @@ def test_dr_any_state_count_vs_path(S, C, tree_kind, n_pat, scaling):
     if tree_kind.endswith("long"):
         assert site.min() < -256 * np.log(2)
     _dr_vs_path(eng, et, rel=1e-9 if tree_kind.endswith("long") else 1e-10)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_dr_random_topologies(seed):
+    """Random unbalanced trees with polytomies (test_gpu_parity._random_topology), one or two
+    rate models over the branches, 4 / 20 / 64 states, every traversal mode, with and without
+    rescaling: every branch's double-recursive derivatives against the single-traversal path
+    derivatives (1e-10), and two branches' first derivatives against central differences of
+    the oracle's lnL."""
+    from test_gpu_parity import _random_topology
+    rng = np.random.default_rng(2000 + seed)
+    S = 20 if seed % 4 == 3 else 64 if seed % 8 == 5 else 4
+    C = 1 if S == 64 else int(rng.choice([1, 2, 4]))
+    n_taxa = int(rng.integers(3, 25 if S != 4 else 90))
+    n = int(rng.choice([1, 300, 1500]))
+    scaling = bool(rng.random() < 0.35)
+    lo, hi = (0.3, 1.0) if scaling else (0.02, 0.3)
+    et = phylo.engine_tree(_random_topology(n_taxa, rng, lo, hi), unroot=bool(rng.random() < 0.5))
+    n_models = int(rng.integers(1, 3))
+    if S == 4:
+        models = [phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5)) for _ in range(n_models)]
+        alph = phylo.DNA
+    elif S == 20:
+        models, alph = [phylo.lg08()] * n_models, phylo.PROTEIN
+    else:
+        models = [phylo.yn98(float(rng.uniform(1.0, 4.0)), float(rng.uniform(0.1, 1.0))) for _ in range(n_models)]
+        alph = phylo.CODON
+    mon = rng.integers(0, n_models, et.n_nodes).astype(np.int32) if n_models > 1 else None
+    rates, probs = phylo.gamma_rates(C, float(rng.uniform(0.3, 2.0))) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("d", et, models, mon, rates, probs, models[0].pi, alph, n, scaling, True, seed)
+    states = wl.simulate(0, n).astype(np.int32)
+    mode = ["lnl_only", "materialize", "levelwise"][seed % 3]
+    flags = plk.PLK_FLAG_NONNEG_GUARD | MODES[mode] | DR | (plk.PLK_FLAG_SCALING if scaling else 0)
+    eng = engine_for(et, S, C, n, states, alph.init_table, rates, probs, models[0].pi, models, model_of_node=mon,
+                     flags=flags)
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    eng.update_pmatrices(br, et.brlen[br], None if mon is None else mon[br], deriv_mask=7)
+    lnl0 = abs(run_engine(eng, et)[0])
+    d1, _ = _dr_vs_path(eng, et)
+    for b in rng.choice(br, size=min(2, len(br)), replace=False):
+        b = int(b)
+        h = 1e-5 * max(1.0, et.brlen[b])
+
+        def lnl_at(t):
+            bl = et.brlen.copy()
+            bl[b] = t
+            e2 = phylo.EngineTree(et.n_tips, et.n_internal, et.root, et.tip_names, et.ops, bl, {}, [], [])
+            return oracle_for(e2, states, alph.init_table, rates, probs, models[0].pi, models, model_of_node=mon,
+                              scaling=scaling)[0]
+
+        fd1 = (lnl_at(et.brlen[b] + h) - lnl_at(et.brlen[b] - h)) / (2 * h)
+        # central-difference error: truncation O(h^2) plus the lnL round-off amplified by 1/h
+        assert abs(d1[b] - fd1) <= 1e-5 * max(1.0, abs(fd1)) + 64 * 2.2e-16 * lnl0 / h, (b, d1[b], fd1)

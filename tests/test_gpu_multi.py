@@ -302,3 +302,74 @@ def test_multi_device_fanout_eight_shards():
         a1, a2 = one.branch_derivatives(b)
         m1, m2 = multi.branch_derivatives(b)
         assert abs(a1 - m1) <= 1e-12 * abs(a1) and abs(a2 - m2) <= 1e-12 * abs(a2)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_multi_device_random_topologies_incremental(seed):
+    """Random unbalanced trees (polytomies, rooted or unrooted, 1-3 models, 4 / 20 / 64
+    states) on two- and three-shard handles, every traversal mode: the sharded handle equals
+    one handle bitwise (lnL, block sums, per-pattern lnL) after a full traversal and after
+    incremental ones (the changed branches' P(t) and the ancestors' ops only), and the
+    incremental result equals a full re-traversal bitwise."""
+    from test_gpu_parity import MODES, _random_topology
+    rng = np.random.default_rng(5000 + seed)
+    S = 20 if seed % 4 == 3 else 64 if seed % 8 == 5 else 4
+    C = 1 if S == 64 else int(rng.choice([1, 2, 4]))
+    n = int(rng.choice([4096 + 1, 2 * 4096 + 333, 3 * 4096 + 17]))
+    devs = [0, 0] if rng.random() < 0.5 else [0, 0, 0]
+    scaling = bool(rng.random() < 0.4)
+    lo, hi = (0.3, 1.2) if scaling else (0.01, 0.3)
+    et = phylo.engine_tree(_random_topology(int(rng.integers(4, 24 if S == 64 else 60)), rng, lo, hi),
+                           unroot=bool(rng.random() < 0.5))
+    n_models = int(rng.integers(1, 4))
+    if S == 4:
+        models = [phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5)) for _ in range(n_models)]
+        alph = phylo.DNA
+    elif S == 20:
+        models, alph = [phylo.lg08()] * n_models, phylo.PROTEIN
+    else:
+        models = [phylo.yn98(float(rng.uniform(1.0, 4.0)), float(rng.uniform(0.1, 1.0))) for _ in range(n_models)]
+        alph = phylo.CODON
+    mon = rng.integers(0, n_models, et.n_nodes).astype(np.int32) if n_models > 1 else None
+    rates, probs = phylo.gamma_rates(C, float(rng.uniform(0.3, 2.0))) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("m", et, models, mon, rates, probs, models[0].pi, alph, n, scaling, True, seed)
+    states = wl.simulate(0, n)
+    mode = ["lnl_only", "materialize", "levelwise", "subtree"][seed % 4 if n_models == 1 else seed % 3]
+    flags = plk.PLK_FLAG_NONNEG_GUARD | (plk.PLK_FLAG_SUBTREE_PATTERNS if mode == "subtree" else MODES[mode]) | \
+        (plk.PLK_FLAG_SCALING if scaling else 0)
+    mk = lambda d: _setup(plk.Engine(d, S, C, n, et.n_tips, et.n_internal, n_models, flags), wl, states)  # noqa: E731
+    one, multi = mk(0), mk(devs)
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    mi = None if mon is None else mon[br]
+    ops = phylo.split_ops(et.ops)
+    parents = {c: p for p, ch in et.ops for c in ch}
+    bl = et.brlen.copy()
+
+    def both(fn):
+        r = [fn(e) for e in (one, multi)]
+        for e in (one, multi):
+            r.append(e.root_loglik(et.root, want_sites=True, want_blocks=True))
+        (l1, b1), (lm, bm), s1, sm = r
+        assert np.isfinite(l1) and l1 == lm and np.array_equal(b1, bm)
+        assert s1[0] == l1 and sm[0] == lm and np.array_equal(s1[1], sm[1]) and np.array_equal(s1[2], sm[2])
+        return l1
+
+    both(lambda e: e.evaluate(br, bl[br], ops, et.root, mi))
+    for _ in range(2):
+        ch = rng.choice(br, size=min(2, len(br)), replace=False).astype(np.int32)
+        bl[ch] *= rng.uniform(0.5, 1.5, size=len(ch))
+        if mode == "lnl_only":  # nothing is stored: every call is a full traversal
+            inc = both(lambda e: e.evaluate(br, bl[br], ops, et.root, mi))
+        else:
+            anc = set()
+            for b in ch:
+                v = int(b)
+                while v in parents:
+                    v = parents[v]
+                    anc.add(v)
+            sub = phylo.split_ops([(p, c) for p, c in et.ops if p in anc])
+            inc = both(lambda e: e.evaluate(ch, bl[ch], sub, et.root, None if mon is None else mon[ch]))
+        fresh = mk(0)
+        full, _ = fresh.evaluate(br, bl[br], ops, et.root, mi)
+        fresh.close()
+        assert inc == full
