@@ -109,6 +109,8 @@ bool tune_is(const char* key, char v) {
   return e && e[0] == v;
 }
 
+int tune_int(const char* key, int def, int lo, int hi);
+
 // per host thread (like errno): the shard workers of a multi-device handle fail on their own
 thread_local std::string g_last_error;
 
@@ -1423,6 +1425,12 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   a.C = h->C;
   a.mask = deriv_mask;
   a.n_req = n;
+  a.uni_model = -1;
+  if (h->S == 64) {
+    a.uni_model = model ? model[0] : 0;
+    for (int i = 1; model && i < n; ++i)
+      if (model[i] != a.uni_model) a.uni_model = -1;
+  }
   // tip tables ride along for S <= 20 (P of the block staged in LDS; S = 64 keeps the
   // separate tip_table_kernel)
   const bool k64 = h->S == 64 && deriv_mask == PLK_DERIV_P;
@@ -1441,9 +1449,22 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
   // read (allocated by the first transposed-P use), so an evaluation needs no transpose launch
   const bool pk_generic = !k64 && h->S != 4;
   if ((k64 || pk_generic) && (deriv_mask & PLK_DERIV_P)) a.PT = h->pmatsT;
-  if (k64)
-    pmat64s_kernel<<<dim3(n, h->C, 4), dim3(256), (size_t)(64 + 16 * 64 + S2) * sizeof(double), h->stream>>>(a, inl);
-  else if (h->S == 4)
+  if (k64) {
+    // several matrices per workgroup (pmat64w_kernel); PLK_TUNE P64RX=0 keeps pmat64s_kernel
+    const int rx = tune_int("P64RX", 4, 0, 4), nb = tune_int("P64NB", 2, 1, 4);
+    if (rx == 0) {
+      pmat64s_kernel<<<dim3(n, h->C, 4), dim3(256), (size_t)(64 + 16 * 64 + S2) * sizeof(double), h->stream>>>(a, inl);
+    } else {
+      const int rr = rx <= 1 ? 1 : rx <= 2 ? 2 : 4, nn = nb <= 1 ? 1 : nb <= 2 ? 2 : 4;
+      const dim3 g((unsigned)((n * h->C + nn - 1) / nn), (unsigned)(64 / (4 * rr)));
+      const size_t lds = (size_t)(64 * kP64Pad + nn * 64 + nn * 4 * rr * kP64Pad) * sizeof(double);
+#define PLK_P64W(RX_, NB_) \
+  if (rr == RX_ && nn == NB_) pmat64w_kernel<RX_, NB_><<<g, dim3(256), lds, h->stream>>>(a, inl);
+      PLK_P64W(1, 1) PLK_P64W(1, 2) PLK_P64W(1, 4) PLK_P64W(2, 1) PLK_P64W(2, 2) PLK_P64W(2, 4)
+      PLK_P64W(4, 1) PLK_P64W(4, 2) PLK_P64W(4, 4)
+#undef PLK_P64W
+    }
+  } else if (h->S == 4)
     pmat4_kernel<<<dim3((unsigned)((n * h->C * 4 + 63) / 64)), dim3(64), 0, h->stream>>>(a, inl);
   else
   {

@@ -569,6 +569,7 @@ struct PmatArgs {
   int S, C;
   unsigned mask;
   int n_req;               // branches in the request
+  int uni_model;           // every entry of the request uses this model (-1: mixed or unknown)
 };
 
 // Requests of up to kPmatInline branches travel in the kernel arguments (no staging
@@ -787,6 +788,160 @@ __global__ __launch_bounds__(256) void pmat64s_kernel(PmatArgs a, const PmatInli
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (cb + u < a.n_codes) tout[(cb + u) * S + x0 + xl] = t[u];
+  }
+}
+
+// K4 for 64 states, several matrices per workgroup, one P row per wave register: lane y of
+// a wave holds P[x][y] of its rows x.  w = V[x][k] Vinv[k][y] does not depend on the branch
+// length or the rate class, so the NB matrices of a workgroup (request entry i, class c, in
+// i-major order) that share a model share every w: per (x, y, k) one multiply and NB FMAs.
+// Per k a lane reads Vinv[k][y] from LDS (consecutive, no conflicts); V[x][k] and
+// e_q[k] = exp(lambda_k r_c t_i) come by v_readlane from lane k of a register.  The sums
+// are pmat_kernel's in its order (k ascending, fma(w, e_k, p)), so the results are bitwise
+// pmat64s_kernel's.  A workgroup covers rows x0 .. x0 + 4 RX - 1 (blockIdx.y, RX per wave);
+// its matrices form runs of one model (a non-homogeneous request can change model inside the
+// group), each staged and computed in turn; a request of one model (a.uni_model >= 0, known
+// to the host) stages Vinv while the request entries -- in pinned host memory for requests
+// over kPmatInline branches, a bus round trip -- are on their way.  cfg4 (254 branches):
+// 31 us against pmat64s_kernel's 36-37; in-kernel stamps put ~4.7 us in the prologue
+// (request, staging), ~6 us in the k loop and ~10 us in the P / P^T stores
+// (profiles/r05/ab_runs.md).
+constexpr int kP64Pad = 65;
+__device__ __forceinline__ double readlane_f64(double v, int k) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, k), hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int RX, int NB>
+__global__ __launch_bounds__(256) void pmat64w_kernel(PmatArgs a, const PmatInline inl) {
+  constexpr int S = 64, R = 4 * RX;
+  static_assert(NB * S <= 256 && R <= 64, "NB exponential rows over 256 threads; R rows");
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* Vi = sm;               // [S][S] Vinv; tip phase: the code table [code][kP64Pad]
+  double* e = Vi + S * kP64Pad;  // [NB][S]
+  double* Pl = e + NB * S;       // [NB][R][kP64Pad]: the workgroup's P rows
+  __shared__ int s_b[NB], s_m[NB];
+  __shared__ double s_t[NB];
+  const int n_mat = a.n_req * a.C;
+  const int j0 = blockIdx.x * NB, jn = min(n_mat, j0 + NB), x0 = R * blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int xw = x0 + RX * __builtin_amdgcn_readfirstlane(tid >> 6);  // the wave's first row
+  if (tid < NB && j0 + tid < jn) {
+    const int j = j0 + tid, i = j / a.C;
+    s_b[tid] = inl.n ? inl.branch[i] : a.branch[i];
+    s_m[tid] = inl.n ? inl.model[i] : (a.model ? a.model[i] : 0);
+    s_t[tid] = (inl.n ? inl.t[i] : a.t[i]) * a.rates[j - i * a.C];
+  }
+  int staged = -1;
+  if (a.uni_model >= 0) {
+    stage_lds<S * S / 256>(Vi, a.Vinv + (size_t)a.uni_model * S * S, S * S);
+    staged = a.uni_model;
+  }
+  __syncthreads();
+  for (int r0 = j0; r0 < jn;) {
+    const int m = __builtin_amdgcn_readfirstlane(s_m[r0 - j0]);
+    int r1 = r0 + 1;
+    while (r1 < jn && s_m[r1 - j0] == m) ++r1;
+    if (staged != m) {
+      if (staged >= 0) __syncthreads();  // the previous run is done with Vi
+      stage_lds<S * S / 256>(Vi, a.Vinv + (size_t)m * S * S, S * S);
+      staged = m;
+    }
+    const double* lam = a.lambda + (size_t)m * S;
+    if (tid < NB * S) {
+      const int q = tid / S;
+      e[tid] = r0 + q < r1 ? exp(lam[tid % S] * s_t[r0 + q - j0]) : 0.0;
+    }
+    __syncthreads();
+    double ek[NB], vxl[RX];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) ek[q] = e[q * S + lane];  // lane k holds e_q[k]
+#pragma unroll
+    for (int r = 0; r < RX; ++r) vxl[r] = a.V[((size_t)m * S + xw + r) * S + lane];  // lane k holds V[x][k]
+    double p[RX][NB];
+#pragma unroll
+    for (int r = 0; r < RX; ++r)
+#pragma unroll
+      for (int q = 0; q < NB; ++q) p[r][q] = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < S; ++k) {
+      const double vi = Vi[k * S + lane];
+      double w[RX];
+#pragma unroll
+      for (int r = 0; r < RX; ++r) w[r] = readlane_f64(vxl[r], k) * vi;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const double eq = readlane_f64(ek[q], k);
+#pragma unroll
+        for (int r = 0; r < RX; ++r) p[r][q] = __builtin_fma(w[r], eq, p[r][q]);
+      }
+    }
+    // P rows straight from the registers (lane y: 512-byte rows); the workgroup's rows of
+    // every matrix also go to LDS, from where P^T leaves as whole 128-byte lines of R
+    // consecutive x per y (a store of column y from the registers scatters 64 lanes over
+    // 64 lines -- 16 K such stores per cfg4 request ran ~20 us)
+    bool any_tip = false;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int j = r0 + q;
+      if (j >= r1) break;
+      const int b = s_b[j - j0], c = j % a.C;
+      const bool ident = s_t[j - j0] == 0.0;  // getPij_t: t == 0 -> identity
+      double* out = a.P + ((size_t)b * a.C + c) * S * S;
+#pragma unroll
+      for (int r = 0; r < RX; ++r) {
+        const int x = xw + r;
+        p[r][q] = ident ? (x == lane ? 1.0 : 0.0) : p[r][q];
+        out[x * S + lane] = p[r][q];
+        Pl[(q * R + xw - x0 + r) * kP64Pad + lane] = p[r][q];
+      }
+      any_tip |= a.init && b < a.n_tips;
+    }
+    __syncthreads();
+    if (a.PT) {
+      const int y = tid >> 2, xq = (tid & 3) * RX;  // 4 threads per y, RX consecutive x each
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int j = r0 + q;
+        if (j >= r1) break;
+        const int b = s_b[j - j0], c = j % a.C;
+        double* outT = a.PT + ((size_t)b * a.C + c) * S * S + (size_t)y * S + x0 + xq;
+#pragma unroll
+        for (int u = 0; u < RX; ++u) outT[u] = Pl[(q * R + xq + u) * kP64Pad + y];
+      }
+    }
+    if (any_tip) {
+      // tip rows tipP[b][c][code][x0 + xl] = sum_y P[x][y] init[code][y] (tip_table64_kernel's
+      // sums, y ascending) from the P rows in LDS
+      constexpr int NC = R / 4;  // codes per thread
+      const int xl = tid % R, cb = NC * (tid / R);
+      for (int k = tid; k < a.n_codes * S; k += 256) Vi[(k / S) * kP64Pad + k % S] = a.init[k];
+      staged = -1;
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int j = r0 + q;
+        if (j >= r1) break;
+        const int b = s_b[j - j0], c = j % a.C;
+        if (b >= a.n_tips) continue;
+        double t[NC];
+#pragma unroll
+        for (int u = 0; u < NC; ++u) t[u] = 0.0;
+#pragma unroll 4
+        for (int y = 0; y < S; ++y) {
+          const double px = Pl[(q * R + xl) * kP64Pad + y];
+#pragma unroll
+          for (int u = 0; u < NC; ++u)
+            t[u] = __builtin_fma(px, cb + u < a.n_codes ? Vi[(cb + u) * kP64Pad + y] : 0.0, t[u]);
+        }
+        double* tout = a.tipP + ((size_t)b * a.C + c) * a.n_codes * S;
+#pragma unroll
+        for (int u = 0; u < NC; ++u)
+          if (cb + u < a.n_codes) tout[(cb + u) * S + x0 + xl] = t[u];
+      }
+    }
+    r0 = r1;
+    if (r0 < jn) __syncthreads();  // the next run rewrites e
   }
 }
 

@@ -1124,6 +1124,47 @@ def test_pmat64s_kernel_bitwise():
     assert out[0][0] == out[1][0] and np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
 
 
+@pytest.mark.parametrize("RX,NB,C,n_taxa,nh", [
+    (4, 4, 1, 24, False), (4, 4, 3, 24, True), (4, 4, 1, 100, True), (2, 4, 2, 100, False),
+    (2, 2, 1, 24, True), (1, 1, 4, 24, False), (4, 2, 1, 100, False), (1, 4, 1, 100, True),
+    (4, 1, 1, 24, True)])
+def test_pmat64w_kernel_bitwise(RX, NB, C, n_taxa, nh, monkeypatch):
+    """pmat64w_kernel (NB matrices of one model per workgroup sharing every V Vinv product,
+    RX rows per wave, PLK_TUNE P64RX / P64NB) against the generic kernel (a P + dP + d2P request)
+    and pmat64s_kernel (P64RX=0), bitwise: every P(t), the fused tip tables (through the
+    traversal's lnL and site lnL) -- one class or several, one model or a different model
+    per branch (runs of one model inside a workgroup), inline requests (<= 160 branches)
+    and staged ones (198), and a zero-length branch (identity)."""
+    # a 64-code table (n_codes <= 64: the P(t) kernel writes the tip tables) for most cases,
+    # the codon alphabet's 65 (the separate tip-table kernel) when NB == 2
+    et, m, alph, rates, probs, states = _random_problem(64, C, n_taxa, 300, seed=640 + n_taxa + C, amb=NB == 2)
+    if NB != 2:
+        alph = phylo.Alphabet("R", 64, {}, np.eye(64))
+    models = [m] + ([_random_problem(64, 1, 4, 10, seed=650 + k)[1] for k in range(2)] if nh else [])
+    mon = np.random.default_rng(7).integers(0, len(models), et.n_nodes).astype(np.int32) if nh else None
+    br = np.array([n for n in range(et.n_nodes) if n != et.root], dtype=np.int32)
+    t = et.brlen[br].copy()
+    t[len(t) // 3] = 0.0
+    ops = phylo.split_ops(et.ops)
+    out = []
+    for mask, tune in ((7, None), (plk.PLK_DERIV_P, {"P64RX": 0}), (plk.PLK_DERIV_P, {"P64RX": RX, "P64NB": NB})):
+        clear_tune(monkeypatch, "P64RX")
+        clear_tune(monkeypatch, "P64NB")
+        for k, v in (tune or {}).items():
+            set_tune(monkeypatch, k, v)
+        eng = engine_for(et, 64, C, 300, states, alph.init_table, rates, probs, m.pi, models, model_of_node=mon,
+                         flags=plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY)
+        eng.update_pmatrices(br, t, None if mon is None else mon[br], deriv_mask=mask)
+        eng.update_partials(ops)
+        lnl, site, _ = eng.root_loglik(et.root, want_sites=True)
+        out.append((lnl, site, np.stack([eng.get_pmatrix(int(b)) for b in br])))
+        eng.close()
+    assert np.isfinite(out[0][0])
+    assert np.array_equal(out[0][2][len(t) // 3], np.stack([np.eye(64)] * C))
+    for o in out[1:]:
+        assert o[0] == out[0][0] and np.array_equal(o[1], out[0][1]) and np.array_equal(o[2], out[0][2])
+
+
 # ---------------------------------------------------------------- jit_treeM (20 states, v_mfma_f64_4x4x4_4b)
 
 @pytest.mark.gpu
