@@ -66,8 +66,11 @@ def parse():
     ap.add_argument("--strong-steps", type=int, default=10, help="timed steps of the strong sub-record")
     ap.add_argument("--strong-patterns", type=int, default=None,
                     help="tests only: patterns of the strong sub-record (default config 5's 2M)")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 200 timed steps of config 2 are ~30 ms: a 20-step window (3 ms) after 3 warmup steps
+    # times the GPU before its clock has settled -- the same box gave 0.156-0.165 ms per step
+    # over 20 steps and 0.143-0.145 over 200 (profiles/r05/warm/)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default=None, choices=sorted(workload.CONFIGS),
                     help="default: gtr_g4_dna_1M_64 (config 2); with --scaling strong nh_gtr_g4_dna_2M_512 (config 5)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
