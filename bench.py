@@ -63,7 +63,7 @@ def parse():
                     help="simulate the alignment on the host (default: on the GPU, the same states bitwise)")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the config-5 strong-scaling sub-record of the default line")
-    ap.add_argument("--strong-steps", type=int, default=10, help="timed steps of the strong sub-record")
+    ap.add_argument("--strong-steps", type=int, default=40, help="timed steps of the strong sub-record (~0.1 s)")
     ap.add_argument("--strong-patterns", type=int, default=None,
                     help="tests only: patterns of the strong sub-record (default config 5's 2M)")
     # 200 timed steps of config 2 are ~30 ms: a 20-step window (3 ms) after 3 warmup steps
@@ -558,7 +558,7 @@ def main():
         # patterns split over the same N GPUs, timed the same way (the N = 1 line is all 2M on
         # one GPU), so the driver's N = 1, 2, 4, 8 lines carry both curves
         s = measure(args, lay, ctx, "nh_gtr_g4_dna_2M_512", "strong", patterns=args.strong_patterns,
-                    steps=args.strong_steps, warmup=2)
+                    steps=args.strong_steps, warmup=5)
         if rank == 0:
             trav = (s["tm"]["partials_ms"] + s["tm"]["tables_ms"]) / max(s["ev_steps"], 1)
             flops = s["wl"].algorithmic_flops_per_pattern() * s["P"]

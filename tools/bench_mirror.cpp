@@ -52,7 +52,8 @@ int main(int argc, char** argv) {
   const int taxa = cfg == "cfg3" ? 256 : cfg == "cfg4" ? 128 : 64;
   const size_t defP = cfg == "cfg3" ? 200000 : cfg == "cfg4" ? 50000 : 1000000;
   const size_t P = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : defP;
-  const int steps = argc > 3 ? std::atoi(argv[3]) : 20, warmup = argc > 4 ? std::atoi(argv[4]) : 3;
+  // 200 steps after 50 warmup: the GPU clock settles (bench.py, profiles/r05/ab_runs.md "window")
+  const int steps = argc > 3 ? std::atoi(argv[3]) : 200, warmup = argc > 4 ? std::atoi(argv[4]) : 50;
   ApplicationTools::verbosity() = 0;
   std::mt19937_64 rng(42);
   std::unique_ptr<TreeTemplate<Node> > tree(TreeTemplateTools::parenthesisToTree(balancedNewick(taxa, rng)));
