@@ -304,13 +304,9 @@ def test_multi_device_fanout_eight_shards():
         assert abs(a1 - m1) <= 1e-12 * abs(a1) and abs(a2 - m2) <= 1e-12 * abs(a2)
 
 
-@pytest.mark.parametrize("seed", range(16))
-def test_multi_device_random_topologies_incremental(seed):
-    """Random unbalanced trees (polytomies, rooted or unrooted, 1-3 models, 4 / 20 / 64
-    states) on two- and three-shard handles, every traversal mode: the sharded handle equals
-    one handle bitwise (lnL, block sums, per-pattern lnL) after a full traversal and after
-    incremental ones (the changed branches' P(t) and the ancestors' ops only), and the
-    incremental result equals a full re-traversal bitwise."""
+def _random_sharded_problem(seed):
+    """A random unbalanced tree (polytomies, rooted or unrooted), 1-3 GTR / LG08 / YN98 models,
+    1-4 classes, rescaling or not, a traversal mode, 1-3 blocks of 4096 patterns and a few."""
     from test_gpu_parity import MODES, _random_topology
     rng = np.random.default_rng(5000 + seed)
     S = 20 if seed % 4 == 3 else 64 if seed % 8 == 5 else 4
@@ -337,6 +333,17 @@ def test_multi_device_random_topologies_incremental(seed):
     mode = ["lnl_only", "materialize", "levelwise", "subtree"][seed % 4 if n_models == 1 else seed % 3]
     flags = plk.PLK_FLAG_NONNEG_GUARD | (plk.PLK_FLAG_SUBTREE_PATTERNS if mode == "subtree" else MODES[mode]) | \
         (plk.PLK_FLAG_SCALING if scaling else 0)
+    return rng, S, C, n, devs, et, n_models, mon, wl, states, mode, flags
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_multi_device_random_topologies_incremental(seed):
+    """Random unbalanced trees (polytomies, rooted or unrooted, 1-3 models, 4 / 20 / 64
+    states) on two- and three-shard handles, every traversal mode: the sharded handle equals
+    one handle bitwise (lnL, block sums, per-pattern lnL) after a full traversal and after
+    incremental ones (the changed branches' P(t) and the ancestors' ops only), and the
+    incremental result equals a full re-traversal bitwise."""
+    rng, S, C, n, devs, et, n_models, mon, wl, states, mode, flags = _random_sharded_problem(seed)
     mk = lambda d: _setup(plk.Engine(d, S, C, n, et.n_tips, et.n_internal, n_models, flags), wl, states)  # noqa: E731
     one, multi = mk(0), mk(devs)
     br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
@@ -373,3 +380,30 @@ def test_multi_device_random_topologies_incremental(seed):
         full, _ = fresh.evaluate(br, bl[br], ops, et.root, mi)
         fresh.close()
         assert inc == full
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_comm_random_topologies(seed):
+    """plk_comm_init at one rank on random trees (the sharded fuzz's problems): lnL, block
+    sums and per-pattern lnL equal the handle without a communicator bitwise, after a full
+    and an incremental evaluation, and -- where partials are stored -- so do the branch
+    derivatives (all-gathered and summed in rank order)."""
+    rng, S, C, n, devs, et, n_models, mon, wl, states, mode, flags = _random_sharded_problem(100 + seed)
+    ref = _setup(plk.Engine(0, S, C, n, et.n_tips, et.n_internal, n_models, flags), wl, states)
+    eng = _setup(plk.Engine(0, S, C, n, et.n_tips, et.n_internal, n_models, flags), wl, states)
+    eng.comm_init(1, 0, plk.comm_get_id())
+    br = np.array([v for v in range(et.n_nodes) if v != et.root], dtype=np.int32)
+    mi = None if mon is None else mon[br]
+    ops = phylo.split_ops(et.ops)
+    for scale in (1.0, 1.1):
+        r = [e.evaluate(br, et.brlen[br] * scale, ops, et.root, mi) for e in (ref, eng)]
+        assert np.isfinite(r[0][0]) and r[0][0] == r[1][0] and np.array_equal(r[0][1], r[1][1])
+    s0, s1 = (e.root_loglik(et.root, want_sites=True) for e in (ref, eng))
+    assert s0[0] == s1[0] and np.array_equal(s0[1], s1[1])
+    if mode != "lnl_only" and mode != "subtree":
+        for e in (ref, eng):
+            e.update_pmatrices(br, et.brlen[br], mi, deriv_mask=7)
+            e.update_partials(ops)
+            e.root_loglik(et.root)
+        for b in rng.choice(br, size=min(3, len(br)), replace=False):
+            assert ref.branch_derivatives(int(b)) == eng.branch_derivatives(int(b))
