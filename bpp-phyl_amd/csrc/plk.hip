@@ -1465,7 +1465,20 @@ int plk_update_pmatrices(plk_handle h, int n, const int32_t* branch, const int32
 #undef PLK_P64W
     }
   } else if (h->S == 4)
-    pmat4_kernel<<<dim3((unsigned)((n * h->C * 4 + 63) / 64)), dim3(64), 0, h->stream>>>(a, inl);
+  {
+    const dim3 g4((unsigned)((n * h->C * 4 + 63) / 64));
+    // <= 64 branches: the 1 KB argument block (cfg2: 0.7 us per evaluation, profiles/r05/ab_runs.md)
+    if (inl.n > 0 && inl.n <= kPmatInlineSmall) {
+      PmatInlineSmall sm;
+      sm.n = inl.n;
+      std::copy(inl.t, inl.t + inl.n, sm.t);
+      std::copy(inl.branch, inl.branch + inl.n, sm.branch);
+      std::copy(inl.model, inl.model + inl.n, sm.model);
+      pmat4_kernel<PmatInlineSmall><<<g4, dim3(64), 0, h->stream>>>(a, sm);
+    } else {
+      pmat4_kernel<PmatInline><<<g4, dim3(64), 0, h->stream>>>(a, inl);
+    }
+  }
   else
   {
     const int nth = h->S <= 4 ? 64 : 256, ne = (int)((S2 + nth - 1) / nth);

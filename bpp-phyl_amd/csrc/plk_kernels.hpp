@@ -581,6 +581,15 @@ struct PmatInline {
   int32_t model[kPmatInline];
   int32_t n;  // 0: use PmatArgs' device arrays
 };
+// the same for requests of up to 64 branches (cfg2: 62): a 1 KB argument block instead of
+// 2.5 KB -- the launch copies every argument byte into the kernel-argument buffer
+constexpr int kPmatInlineSmall = 64;
+struct PmatInlineSmall {
+  double t[kPmatInlineSmall];
+  int32_t branch[kPmatInlineSmall];
+  int32_t model[kPmatInlineSmall];
+  int32_t n;
+};
 
 // n doubles global -> LDS, the first NE * blockDim.x of them with every thread's loads
 // issued before its first store (a load -> store loop pays one L2 round trip per element and
@@ -661,7 +670,8 @@ __global__ __launch_bounds__(256) void pmat_kernel(PmatArgs a, const PmatInline 
 // (bitwise its results).  pmat_kernel's workgroup per (branch, class) ran a chain of
 // dependent loads, LDS staging and barriers for 16 outputs; here each thread issues its
 // loads at once and the launch is n * C * 4 threads.
-__global__ __launch_bounds__(64) void pmat4_kernel(PmatArgs a, const PmatInline inl) {
+template <class Inl>
+__global__ __launch_bounds__(64) void pmat4_kernel(PmatArgs a, const Inl inl) {
   constexpr int S = 4;
   const int gid = blockIdx.x * 64 + threadIdx.x;
   if (gid >= a.n_req * a.C * S) return;
