@@ -7,7 +7,7 @@ model and rate classes, against the CPU oracle.
   - end to end (the oracle's independent Jacobi P(t), oracle.reversible_pij on the
     model's generator): total lnL relative 1e-10 (north_star), per pattern 1e-9;
   - the kernel that served the traversal is the one the bench line names;
-  - at full size: the oracle on a pattern prefix (patterns are independent), bitwise
+  - at full size: the oracle on every pattern (per pattern and the total), bitwise
     determinism, and bitwise invariance of the block sums under a 2-way shard.
 
 Config 4 (YN98, 64 stored states with TAA/TAG/TGA as null states, C = 1) runs the
@@ -51,7 +51,7 @@ def _model_of(wl, n):
     return wl.models[0] if wl.model_of_node is None else wl.models[wl.model_of_node[n]]
 
 
-def _oracle(wl, states, pmats=None, brlen=None):
+def _oracle(wl, states, pmats=None, brlen=None, use_patterns=False):
     et = wl.et
     bl = et.brlen if brlen is None else brlen
     if pmats is None:
@@ -63,7 +63,7 @@ def _oracle(wl, states, pmats=None, brlen=None):
                     pmats[n, c] = oracle.reversible_pij(m.Q, m.pi, bl[n] * wl.rates[c])
     ss, sons, lr = et.son_arrays()
     lnl, site, _, _ = oracle.tree_loglik(ss, sons, lr, et.root, states, wl.alphabet.init_table, pmats, wl.probs,
-                                         wl.root_freqs, use_patterns=False, scaling=wl.scaling, want_sites=True)
+                                         wl.root_freqs, use_patterns=use_patterns, scaling=wl.scaling, want_sites=True)
     return lnl, site
 
 
@@ -99,11 +99,13 @@ def test_bench_mode_vs_oracle(config):
         assert np.allclose(sites, so2, rtol=1e-9, atol=0)
 
 
+# the oracle over every pattern of the full-size workload (the reference's per-subtree
+# compression keeps it at a few seconds per config on the box's host core)
 FULL = {
-    "gtr_g4_dna_1M_64": 20000,
-    "lg08_g4_protein_200k_256": 800,
-    "yn98_codon_50k_128": 1500,
-    "nh_gtr_g4_dna_2M_512": 3000,
+    "gtr_g4_dna_1M_64": None,
+    "lg08_g4_protein_200k_256": None,
+    "yn98_codon_50k_128": None,
+    "nh_gtr_g4_dna_2M_512": None,
 }
 
 
@@ -111,10 +113,9 @@ FULL = {
 @pytest.mark.parametrize("config", sorted(FULL))
 def test_bench_mode_full_size(config):
     """The bench's workload at its full per-GPU size in the bench's mode: finite and
-    deterministic, the oracle on patterns spread over the whole range -- the first and the
-    last ones (the ragged last super-block and block) and a seeded sample between them --
-    and block sums bitwise invariant under a 2-way shard at a block boundary (the multi-GPU
-    exchange's premise)."""
+    deterministic, the oracle on every pattern (1e-12 per pattern and on the total, the
+    ragged last super-block and block included), and block sums bitwise invariant under a
+    2-way shard at a block boundary (the multi-GPU exchange's premise)."""
     wl = workload.make_workload(config)
     P = wl.n_patterns
     states = wl.simulate(0, P)
@@ -124,12 +125,14 @@ def test_bench_mode_full_size(config):
     assert np.isfinite(lnl) and lnl == lnl2 and np.array_equal(blocks, blocks2)
     assert ev.eng.kernel_path() == CASES[config][1]
     _, sites, _ = ev.eng.root_loglik(wl.et.root, want_sites=True)
-    n = FULL[config]
+    n = FULL[config] or P
     edge = min(256, n // 4)
     mid = np.random.default_rng(11).choice(np.arange(edge, P - edge), size=n - 2 * edge, replace=False)
     idx = np.sort(np.concatenate([np.arange(edge), mid, np.arange(P - edge, P)]))
-    lo, so = _oracle(wl, states[:, idx].astype(np.int32), pmats=_engine_pmats(ev.eng, wl.et))
+    lo, so = _oracle(wl, states[:, idx].astype(np.int32), pmats=_engine_pmats(ev.eng, wl.et), use_patterns=True)
     assert np.allclose(sites[idx], so, rtol=REL, atol=0)
+    if n == P:  # every pattern: the total too
+        assert abs(lnl - lo) <= REL * abs(lo), (lnl, lo)
     del ev
     cut = (P // 4096 // 2) * 4096
     parts = []
