@@ -11,7 +11,7 @@ model and rate classes, against the CPU oracle.
     determinism, and bitwise invariance of the block sums under a 2-way shard.
 
 Config 4 (YN98, 64 stored states with TAA/TAG/TGA as null states, C = 1) runs the
-treeM<64> traversal, the cherry contribution tables and pmat64s_kernel, i.e. the path
+treeM<64> traversal, the cherry contribution tables and pmat64w_kernel, i.e. the path
 that profiles/*cfg4* time; reference chain Model/Codon/YN98.cpp:51-78 ->
 Model/Codon/AbstractCodonSubstitutionModel.cpp:174-190.
 """
