@@ -13,6 +13,7 @@
 #include "plk_jit.hpp"
 #include "plk_jitm.hpp"
 #include "plk_dr.hpp"
+#include "plk_exchange.hpp"
 
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
@@ -176,8 +177,21 @@ struct ShardPool {
       if (stop.load()) return;
       seen = s;
       t_start[i] = clk::now();
-      rc[i] = (*job)(i);
+      rc[i] = guarded(*job, i);
       done.fetch_add(1, std::memory_order_release);
+    }
+  }
+  // A shard job runs plk_* code that can throw (std::vector growth): on a worker thread an
+  // escaping exception would call std::terminate, on the caller's it would unwind while the
+  // workers still use `f` -- so every job's exception becomes its error code, and run()
+  // returns only after every worker has finished.
+  static int guarded(const std::function<int(size_t)>& f, size_t i) {
+    try {
+      return f(i);
+    } catch (const std::bad_alloc&) {
+      return PLK_ERR_OOM;
+    } catch (...) {
+      return PLK_ERR_DEVICE;
     }
   }
   // f(i) for every shard i, concurrently; returns when all are done
@@ -191,7 +205,7 @@ struct ShardPool {
       cv.notify_all();
     }
     t_start[0] = clk::now();
-    rc[0] = f(0);
+    rc[0] = guarded(f, 0);
     const int others = (int)rc.size() - 1;
     while (done.load(std::memory_order_acquire) < others) cpu_relax();
   }
@@ -375,15 +389,16 @@ struct plk_handle_s {
   // on the handle's stream and summed in global order on the device
   ncclComm_t comm = nullptr;
   int comm_ranks = 0, comm_rank = 0;
-  int64_t comm_cmax = 0;                  // block sums per rank in the all-gather (max over ranks)
-  double* d_blk_local = nullptr;          // [comm_cmax] this rank's block sums (zero padded)
+  int64_t comm_stride = 0;                // doubles per rank record in the all-gather (plk_exchange.hpp)
+  int comm_uflow = 0;                     // OR of every rank's underflow flag, last evaluation
+  double* d_blk_local = nullptr;          // [comm_stride] this rank's record: block sums, zeros, flag
   DrPreOp* d_drpre = nullptr;             // fused DR preorder ops (dr_pre_s4_kernel)
   size_t d_drpre_cap = 0;
-  double* d_blk_all = nullptr;            // [comm_ranks][comm_cmax]
+  double* d_blk_all = nullptr;            // [comm_ranks][comm_stride]
   int64_t* d_comm_counts = nullptr;       // block sums per rank
   int32_t* h_uflow = nullptr;             // mapped pinned: root-reduction underflow flag (plk_root_underflow)
   int32_t* d_uflow = nullptr;             // its device address
-  double* h_blk_all = nullptr;            // mapped pinned: every rank's block sums [comm_ranks][comm_cmax]
+  double* h_blk_all = nullptr;            // mapped pinned: every rank's record [comm_ranks][comm_stride]
   double* d_blk_all_map = nullptr;        // its device address
   std::vector<int64_t> comm_counts;       // block sums per rank (host copy)
   double* d_xch = nullptr;                // derivative sums exchanged under the communicator
@@ -1162,7 +1177,8 @@ void comm_release(plk_handle h) {
   h->comm_counts.clear();
   h->comm_ranks = 0;
   h->comm_rank = 0;
-  h->comm_cmax = 0;
+  h->comm_stride = 0;
+  h->comm_uflow = 0;
 }
 
 int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id) {
@@ -1192,15 +1208,19 @@ int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id) {
     HIPCHK(h, hipMemcpyAsync(counts.data(), h->d_comm_counts, counts.size() * sizeof(int64_t),
                              hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    const int64_t cmax = *std::max_element(counts.begin(), counts.end());
-    if ((rc = dalloc(h, (void**)&h->d_blk_local, (size_t)cmax * sizeof(double)))) return rc;
-    if ((rc = dalloc(h, (void**)&h->d_blk_all, (size_t)n_ranks * cmax * sizeof(double)))) return rc;
-    HIPCHK(h, hipMemset(h->d_blk_local, 0, (size_t)cmax * sizeof(double)));
-    if (hipHostMalloc((void**)&h->h_blk_all, (size_t)n_ranks * cmax * sizeof(double), hipHostMallocMapped) !=
+    // PLK_TEST_COMM_PAD=k (test hook): k more padding doubles per record, so that a one-rank
+    // run exercises the zero padding a rank with fewer blocks than another carries
+    const char* pad = env_get("PLK_TEST_COMM_PAD");
+    const int64_t stride = xchg::stride(counts.data(), n_ranks) + (pad ? std::max(0, std::atoi(pad)) : 0);
+    if (stride < 1) return fail(h, PLK_ERR_ARG, "bad block counts in the exchange");
+    if ((rc = dalloc(h, (void**)&h->d_blk_local, (size_t)stride * sizeof(double)))) return rc;
+    if ((rc = dalloc(h, (void**)&h->d_blk_all, (size_t)n_ranks * stride * sizeof(double)))) return rc;
+    HIPCHK(h, hipMemset(h->d_blk_local, 0, (size_t)stride * sizeof(double)));
+    if (hipHostMalloc((void**)&h->h_blk_all, (size_t)n_ranks * stride * sizeof(double), hipHostMallocMapped) !=
             hipSuccess ||
         hipHostGetDevicePointer((void**)&h->d_blk_all_map, h->h_blk_all, 0) != hipSuccess)
       return fail(h, PLK_ERR_OOM, "pinned block sums of every rank");
-    h->comm_cmax = cmax;
+    h->comm_stride = stride;
     h->comm_counts = counts;
     return PLK_OK;
   };
@@ -3625,6 +3645,17 @@ __global__ void comm_copy_kernel(const double* __restrict__ all, int64_t n_all, 
 // block sums land in mapped host memory, or in the all-gather's send buffer under a communicator
 double* block_target(plk_handle h) { return h->comm ? h->d_blk_local : h->block_sums; }
 
+// The fixed-order 4096-pattern block sums of the wave sums; under a communicator also the
+// underflow flag into this rank's exchange record (plk_exchange.hpp layout).
+int launch_block_sums(plk_handle h) {
+  const int n_waves = (int)((h->n_patterns + 63) / 64);
+  wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(
+      h->wave_sums, block_target(h), n_waves, h->n_blocks, h->comm ? h->d_uflow : nullptr,
+      h->comm ? h->d_blk_local + h->comm_stride - 1 : nullptr);
+  HIPCHK(h, hipGetLastError());
+  return PLK_OK;
+}
+
 // Enqueue the root reduction of `root` (fused traversals already did it), the fixed-order
 // 4096-pattern block sums, the RCCL exchange under a communicator, and the per-pattern lnL
 // copy; root_finish waits and sums.  Split so that a multi-device handle can have every
@@ -3635,10 +3666,8 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
   hipSetDevice(h->device);
   if (h->fused_lnl_valid && h->fused_lnl_root == root) {
     // the fused traversal already reduced the root: only the block sums remain
-    const int n_waves = (int)((h->n_patterns + 63) / 64);
-    wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, block_target(h), n_waves,
-                                                                          h->n_blocks);
-    HIPCHK(h, hipGetLastError());
+    int rc = launch_block_sums(h);
+    if (rc) return rc;
   } else {
     if (!h->materialized[root - h->n_tips]) return fail(h, PLK_ERR_STATE, "root %d has no partial", root);
     int rc = launch_root(h, root);
@@ -3648,10 +3677,10 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
     }
   if (h->comm) {
     // the one cross-GPU exchange of an evaluation: a fixed-size all-gather of block sums
-    if (ncclAllGather(h->d_blk_local, h->d_blk_all, (size_t)h->comm_cmax, ncclFloat64, h->comm, h->stream) !=
+    if (ncclAllGather(h->d_blk_local, h->d_blk_all, (size_t)h->comm_stride, ncclFloat64, h->comm, h->stream) !=
         ncclSuccess)
       return fail(h, PLK_ERR_DEVICE, "ncclAllGather of the block sums failed");
-    const int64_t n_all = (int64_t)h->comm_ranks * h->comm_cmax;
+    const int64_t n_all = (int64_t)h->comm_ranks * h->comm_stride;
     comm_copy_kernel<<<(unsigned)((n_all + h->n_blocks + 255) / 256), 256, 0, h->stream>>>(
         h->d_blk_all, n_all, h->d_blk_local, h->n_blocks, h->d_blk_all_map, h->block_sums);
     HIPCHK(h, hipGetLastError());
@@ -3668,10 +3697,8 @@ int root_finish(plk_handle h, double* lnl, double* block_sums, bool wait = true)
     if (int rc = stream_wait(h)) return rc;
   double s = 0.0;
   if (h->comm) {
-    for (int r = 0; r < h->comm_ranks; ++r) {  // rank order, block order (comm_copy_kernel)
-      const double* b = h->h_blk_all + (size_t)r * h->comm_cmax;
-      for (int64_t i = 0; i < h->comm_counts[(size_t)r]; ++i) s += b[i];
-    }
+    // rank order, block order (comm_copy_kernel moved the records), and every rank's flag
+    s = xchg::reduce(h->h_blk_all, h->comm_counts.data(), h->comm_ranks, h->comm_stride, &h->comm_uflow);
   } else {
     for (int b = 0; b < h->n_blocks; ++b) s += h->h_blocks[b];  // fixed order: block 0, 1, 2, ...
   }
@@ -3697,11 +3724,7 @@ int comm_sum_values(plk_handle h, double* v, size_t n) {
   std::vector<double> all(R * n);
   HIPCHK(h, hipMemcpyAsync(all.data(), h->d_xch_all, all.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  for (size_t i = 0; i < n; ++i) {
-    double s = 0.0;
-    for (size_t r = 0; r < R; ++r) s += all[r * n + i];
-    v[i] = s;
-  }
+  xchg::rank_sums(all.data(), (int)R, n, v);
   return PLK_OK;
 }
 
@@ -3759,12 +3782,47 @@ int plk_create_multi(const int* devices, int n_devices, int n_states, int n_clas
   return PLK_OK;
 }
 
+int plk_exchange_stride(const int64_t* counts, int n_ranks, int64_t* stride) {
+  if (!counts || !stride || n_ranks < 1) return fail(nullptr, PLK_ERR_ARG, "bad exchange layout arguments");
+  const int64_t s = xchg::stride(counts, n_ranks);
+  if (s < 1) return fail(nullptr, PLK_ERR_ARG, "negative block count");
+  *stride = s;
+  return PLK_OK;
+}
+
+int plk_exchange_pack(const double* block_sums, int64_t n_blocks, int uflow, int64_t stride, double* record) {
+  if (!record || n_blocks < 0 || (n_blocks > 0 && !block_sums) || stride < n_blocks + 1)
+    return fail(nullptr, PLK_ERR_ARG, "bad exchange record (%lld blocks, stride %lld)", (long long)n_blocks,
+                (long long)stride);
+  xchg::pack(block_sums, n_blocks, uflow, stride, record);
+  return PLK_OK;
+}
+
+int plk_exchange_reduce(const double* gathered, const int64_t* counts, int n_ranks, int64_t stride, double* lnl,
+                        int* uflow) {
+  if (!gathered || !counts || !lnl || n_ranks < 1) return fail(nullptr, PLK_ERR_ARG, "bad exchange reduce arguments");
+  for (int r = 0; r < n_ranks; ++r)
+    if (counts[r] < 0 || counts[r] > stride - 1)
+      return fail(nullptr, PLK_ERR_ARG, "rank %d: %lld blocks in a record of stride %lld", r, (long long)counts[r],
+                  (long long)stride);
+  *lnl = xchg::reduce(gathered, counts, n_ranks, stride, uflow);
+  return PLK_OK;
+}
+
+int plk_exchange_rank_sums(const double* gathered, int n_ranks, int64_t n, double* v) {
+  if (!gathered || !v || n_ranks < 1 || n < 0) return fail(nullptr, PLK_ERR_ARG, "bad rank-sum arguments");
+  xchg::rank_sums(gathered, n_ranks, (size_t)n, v);
+  return PLK_OK;
+}
+
 int plk_root_underflow(plk_handle h, int* flag) {
   if (!h || !flag) return fail(h, PLK_ERR_ARG, "null argument");
   if (h->flags & PLK_FLAG_SCALING) return fail(h, PLK_ERR_STATE, "a scaled handle's reduction has no underflow flag");
   int f = 0;
   if (!h->shards.empty()) {
     for (plk_handle x : h->shards) f |= *(volatile int32_t*)x->h_uflow;
+  } else if (h->comm) {
+    f = h->comm_uflow;  // every rank's flag, carried in the block-sum all-gather
   } else {
     f = *(volatile int32_t*)h->h_uflow;
   }
@@ -3808,10 +3866,7 @@ static int launch_root(plk_handle h, int root) {
   }
   root_kernel<<<(unsigned)(h->n_pad / 64), 64, 0, h->stream>>>(a);
   HIPCHK(h, hipGetLastError());
-  const int n_waves = (int)((h->n_patterns + 63) / 64);
-  wave_sums_to_blocks<<<(h->n_blocks + 3) / 4, 256, 0, h->stream>>>(h->wave_sums, block_target(h), n_waves,
-                                                                        h->n_blocks);
-  HIPCHK(h, hipGetLastError());
+  if (int rc = launch_block_sums(h)) return rc;
   if (h->timing & PLK_TIME_ROOT) {
     hipEventRecord(ev.b, h->stream);
     h->events.push_back(ev);

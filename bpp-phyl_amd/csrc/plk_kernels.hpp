@@ -258,23 +258,25 @@ __global__ __launch_bounds__(256) void partials_links_s4_kernel(const KOpL* __re
           if (SCALE) cnt += a.scale[(size_t)kd.child * a.n_pad + l];
         }
       }
-  }
-  if (j >= op.D) return;
-  if (SCALE) {
-    double m = 0.0;
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-      for (int x = 0; x < S; ++x) m = fmax(m, acc[c][x]);
-    if (m > 0.0 && m < kScaleThr) {
+    // the joint rescale after every group of three, as the uncompressed traversal's
+    // ACCUMULATE ops do (a wide polytomy's running product never drifts below 2^-256)
+    if (SCALE && j < op.D) {
+      double m = 0.0;
 #pragma unroll
       for (int c = 0; c < C; ++c)
 #pragma unroll
-        for (int x = 0; x < S; ++x) acc[c][x] *= kScaleUp;
-      cnt += 1;
+        for (int x = 0; x < S; ++x) m = fmax(m, acc[c][x]);
+      if (m > 0.0 && m < kScaleThr) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int x = 0; x < S; ++x) acc[c][x] *= kScaleUp;
+        cnt += 1;
+      }
     }
-    a.scale[(size_t)op.parent * a.n_pad + j] = cnt;
   }
+  if (j >= op.D) return;
+  if (SCALE) a.scale[(size_t)op.parent * a.n_pad + j] = cnt;
   double* out = a.partials + (size_t)op.parent * a.slot_stride + (size_t)(j >> 7) * (CS * kTile) + (j & 127);
 #pragma unroll
   for (int c = 0; c < C; ++c)
@@ -301,12 +303,12 @@ __global__ __launch_bounds__(256) void partials_links_generic_kernel(const KOpL*
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double* outp = a.partials + (size_t)op.parent * a.slot_stride + (size_t)(j >> 7) * ((size_t)CS * kTile) + (j & 127);
   int cnt = 0;
-  double m = 0.0;
   // children three at a time (their tables in LDS); after the first group the product so
-  // far is read back from the parent's slot and extended in the children's order
+  // far is read back from the parent's slot and extended in the children's order, and
+  // each group ends with the joint rescale, as the uncompressed traversal's ACCUMULATE ops
   for (int g0 = 0; g0 < n; g0 += kLinkGroup) {
     const int gn = n - g0 < kLinkGroup ? n - g0 : kLinkGroup;
-    const bool last = g0 + gn == n;
+    double m = 0.0;
     if (g0 > 0) __syncthreads();  // the previous group's tables are read
     for (int k = 0; k < gn; ++k) {
       const KKid& kd = kids[op.k0 + g0 + k];
@@ -356,20 +358,18 @@ __global__ __launch_bounds__(256) void partials_links_generic_kernel(const KOpL*
         }
 #pragma unroll
         for (int xb = 0; xb < XB; ++xb) {
-          if (SCALE && last) m = fmax(m, acc[xb]);
+          if (SCALE) m = fmax(m, acc[xb]);
           outp[(size_t)(c * S + x0 + xb) * kTile] = acc[xb];
         }
       }
     }
-  }
-  if (j >= op.D) return;
-  if (SCALE) {
-    if (m > 0.0 && m < kScaleThr) {
+    if (SCALE && m > 0.0 && m < kScaleThr) {
       for (int i = 0; i < CS; ++i) outp[(size_t)i * kTile] *= kScaleUp;
       cnt += 1;
     }
-    a.scale[(size_t)op.parent * a.n_pad + j] = cnt;
   }
+  if (j >= op.D) return;
+  if (SCALE) a.scale[(size_t)op.parent * a.n_pad + j] = cnt;
 }
 
 // ---------------------------------------------------------------------------

@@ -295,11 +295,16 @@ __global__ __launch_bounds__(256) void tree4_kernel(TreeArgs a, const TInstr* __
 // wave order.  One wave per block: the 64 loads are issued together (one per lane),
 // then lane 0 adds them in order through shuffles, so the result is the plain
 // sequential sum without 64 dependent memory round trips.
+// Under a communicator flag_out is the underflow slot of this rank's exchange record
+// (plk_exchange.hpp): the root reduction's flag travels in the same all-gather.
 __global__ __launch_bounds__(256) void wave_sums_to_blocks(const double* __restrict__ wave_sums,
                                                            double* __restrict__ block_sums, int n_waves,
-                                                           int n_blocks) {
+                                                           int n_blocks, const int32_t* uflow,
+                                                           double* __restrict__ flag_out) {
   const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  if (flag_out && b == 0 && lane == 0)
+    *flag_out = __hip_atomic_load(uflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ? 1.0 : 0.0;
   if (b >= n_blocks) return;
   const int w = b * (kRootBlock / 64) + lane;
   const double v = w < n_waves ? wave_sums[w] : 0.0;

@@ -38,7 +38,8 @@ EXPORTS = [
     "plk_kernel_path", "plk_evaluate", "plk_compressed_work", "plk_all_branch_derivatives",
     "plk_get_timing_ex", "plk_traversal_work", "plk_create_multi", "plk_shard_count", "plk_comm_get_id",
     "plk_comm_init", "plk_get_dpmatrix", "plk_root_pair_derivatives", "plk_get_fanout",
-    "plk_root_underflow",
+    "plk_root_underflow", "plk_exchange_stride", "plk_exchange_pack", "plk_exchange_reduce",
+    "plk_exchange_rank_sums",
 ]
 
 
@@ -96,6 +97,10 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_get_fanout": ([ct.c_void_p, ct.c_int, dp, dp, P(ct.c_int64)], ct.c_int),
         "plk_root_underflow": ([ct.c_void_p, P(ct.c_int)], ct.c_int),
         "plk_comm_get_id": ([P(plk_comm_id)], ct.c_int),
+        "plk_exchange_stride": ([P(ct.c_int64), ct.c_int, P(ct.c_int64)], ct.c_int),
+        "plk_exchange_pack": ([dp, ct.c_int64, ct.c_int, ct.c_int64, dp], ct.c_int),
+        "plk_exchange_reduce": ([dp, P(ct.c_int64), ct.c_int, ct.c_int64, dp, P(ct.c_int)], ct.c_int),
+        "plk_exchange_rank_sums": ([dp, ct.c_int, ct.c_int64, dp], ct.c_int),
         "plk_comm_init": ([ct.c_void_p, ct.c_int, ct.c_int, P(plk_comm_id)], ct.c_int),
         "plk_set_code_table": ([ct.c_void_p, ct.c_int, dp], ct.c_int),
         "plk_set_tip_codes": ([ct.c_void_p, ct.c_int, P(ct.c_uint8)], ct.c_int),
@@ -163,6 +168,45 @@ def comm_get_id() -> bytes:
     if rc != PLK_OK:
         raise PlkError(rc, lib.plk_last_error(None).decode())
     return ct.string_at(ct.addressof(cid), 128)   # all 128 bytes (a c_char field stops at NUL)
+
+
+def _chk(rc: int):
+    if rc != PLK_OK:
+        raise PlkError(rc, load().plk_last_error(None).decode())
+
+
+# The exchange bookkeeping of the communicator path (csrc/plk_exchange.hpp): host only, usable
+# without a GPU.  Record of a rank = its block sums, zero padding, its underflow flag.
+
+def exchange_stride(counts: Sequence[int]) -> int:
+    c = np.ascontiguousarray(counts, dtype=np.int64)
+    out = ct.c_int64(0)
+    _chk(load().plk_exchange_stride(c.ctypes.data_as(ct.POINTER(ct.c_int64)), len(c), ct.byref(out)))
+    return out.value
+
+
+def exchange_pack(block_sums: np.ndarray, uflow: bool, stride: int) -> np.ndarray:
+    b = np.ascontiguousarray(block_sums, dtype=np.float64)
+    rec = np.full(stride, np.nan)
+    _chk(load().plk_exchange_pack(_d(b), len(b), int(bool(uflow)), stride, _d(rec)))
+    return rec
+
+
+def exchange_reduce(gathered: np.ndarray, counts: Sequence[int], stride: int) -> Tuple[float, bool]:
+    g = np.ascontiguousarray(gathered, dtype=np.float64).ravel()
+    c = np.ascontiguousarray(counts, dtype=np.int64)
+    lnl, f = ct.c_double(0), ct.c_int(0)
+    _chk(load().plk_exchange_reduce(_d(g), c.ctypes.data_as(ct.POINTER(ct.c_int64)), len(c), stride, ct.byref(lnl),
+                                    ct.byref(f)))
+    return lnl.value, bool(f.value)
+
+
+def exchange_rank_sums(gathered: np.ndarray, n_ranks: int) -> np.ndarray:
+    g = np.ascontiguousarray(gathered, dtype=np.float64).ravel()
+    n = len(g) // n_ranks
+    v = np.empty(n)
+    _chk(load().plk_exchange_rank_sums(_d(g), n_ranks, n, _d(v)))
+    return v
 
 
 def build_id() -> str:

@@ -173,6 +173,21 @@ typedef struct plk_comm_id {
 int plk_comm_get_id(plk_comm_id* id);
 int plk_comm_init(plk_handle h, int n_ranks, int rank, const plk_comm_id* id);
 
+/* The exchange's host-side bookkeeping, the same code the communicator path runs
+ * (csrc/plk_exchange.hpp); host only, no GPU needed -- for callers with their own
+ * collective (MPI, gloo) and for the CPU tests.  Rank r's record is `stride` doubles:
+ * its block sums, zero padding, its underflow flag (1.0 / 0.0); stride = max block
+ * count + 1.  reduce: the global lnL as ONE chain of adds in rank order then block order
+ * (the one-process fixed-order sum of RNonHomogeneousTreeLikelihood.cpp:168-182, bitwise
+ * for any rank count) and the OR of the flags.  rank_sums: v[i] = sum over ranks in rank
+ * order of gathered[r * n + i] (the derivative sums). */
+int plk_exchange_stride(const int64_t* counts /* n_ranks */, int n_ranks, int64_t* stride);
+int plk_exchange_pack(const double* block_sums, int64_t n_blocks, int uflow, int64_t stride,
+                      double* record /* stride */);
+int plk_exchange_reduce(const double* gathered /* n_ranks x stride */, const int64_t* counts, int n_ranks,
+                        int64_t stride, double* lnl, int* uflow);
+int plk_exchange_rank_sums(const double* gathered /* n_ranks x n */, int n_ranks, int64_t n, double* v /* n */);
+
 /* Data */
 int plk_set_code_table(plk_handle h, int n_codes, const double* code_to_vec /* n_codes x S */);
 int plk_set_tip_codes(plk_handle h, int tip, const uint8_t* codes /* n_patterns */);
@@ -216,8 +231,9 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
  * a site's likelihood is <= its root's joint maximum, so every node's maximum was >= 2^-255
  * (one bit of rounding margin above the 2^-256 rescaling threshold) and no rescale would have
  * fired.  The Bio++ mirror evaluates unscaled first and falls back to a scaled handle only when
- * the flag is set.  PLK_ERR_STATE on a scaled handle.  Replaces nothing in the reference, which
- * has no scaling. */
+ * the flag is set.  Under a communicator the flag is global (every rank's, carried in the
+ * block-sum all-gather), so all ranks take the same fallback decision.  PLK_ERR_STATE on a
+ * scaled handle.  Replaces nothing in the reference, which has no scaling. */
 int plk_root_underflow(plk_handle h, int* flag);
 
 /* One likelihood evaluation as RHomogeneousTreeLikelihood::fireParameterChanged does it

@@ -526,25 +526,33 @@ void computeSubtreeLikelihood(OLik& L, int node) {
       }
       if (L.scaling && !L.tree->sons[son].empty()) L.nscale[node][i] += L.nscale[son][(*links)[i]];
     }
-  }
-  if (L.scaling) {
-    for (size_t i = 0; i < nbSites; i++) {
-      double m = 0.;
-      for (int c = 0; c < L.C; c++)
-        for (int x = 0; x < L.S; x++) m = std::max(m, (*likNode)[i][c][x]);
-      if (m > 0. && m < kScaleThreshold) {
+    // The rescale runs after every third son and after the last: the engine's ABI takes
+    // at most three children per op (a polytomy is several ACCUMULATE ops, each ending
+    // with the check), so a wide polytomy's running product is kept above 2^-256 the same way.
+    if (L.scaling && ((l + 1) % 3 == 0 || l + 1 == sons.size())) {
+      for (size_t i = 0; i < nbSites; i++) {
+        double m = 0.;
         for (int c = 0; c < L.C; c++)
-          for (int x = 0; x < L.S; x++) (*likNode)[i][c][x] *= kScaleUp;
-        L.nscale[node][i] += 1;
+          for (int x = 0; x < L.S; x++) m = std::max(m, (*likNode)[i][c][x]);
+        if (m > 0. && m < kScaleThreshold) {
+          for (int c = 0; c < L.C; c++)
+            for (int x = 0; x < L.S; x++) (*likNode)[i][c][x] *= kScaleUp;
+          L.nscale[node][i] += 1;
+        }
       }
     }
   }
 }
 
 // Root reduction: getLogLikelihood / getLogLikelihoodForASite /
-// getLikelihoodForASiteForARateClass, L/RHomogeneousTreeLikelihood.cpp:162-216
-// (the <= 0 guards at :197-198 and :212-213; sorted sum at :170-174).
-double rootLogLikForSite(const OLik& L, size_t site, const double* classProbs, const double* rootFreqs) {
+// getLikelihoodForASiteForARateClass.
+//  - homogeneous (nh == false), L/RHomogeneousTreeLikelihood.cpp:162-216: terms <= 0 are
+//    dropped at both levels (the guards at :197-198 and :212-213);
+//  - non-homogeneous (nh == true), L/RNonHomogeneousTreeLikelihood.cpp:168-233: every term
+//    is added (getLikelihoodForASiteForARateClass :212-221 has no guard), and the site sum
+//    l is clamped l < 0 -> 0 before the log (getLogLikelihoodForASite :198-208, clamp :206).
+// Both sort the site values and sum from the largest (homogeneous :170-174, NH :168-180).
+double rootLogLikForSite(const OLik& L, size_t site, const double* classProbs, const double* rootFreqs, bool nh) {
   size_t p = L.rootLinks[site];
   const VVdouble& la = L.lik[L.tree->root][p];
   double l = 0;
@@ -552,11 +560,12 @@ double rootLogLikForSite(const OLik& L, size_t site, const double* classProbs, c
     double lc = 0;
     for (int s = 0; s < L.S; s++) {
       double li = la[c][s] * rootFreqs[s];
-      if (li > 0) lc += li;
+      if (nh || li > 0) lc += li;
     }
     double li = lc * classProbs[c];
-    if (li > 0) l += li;
+    if (nh || li > 0) l += li;
   }
+  if (nh && l < 0) l = 0;
   double r = std::log(l);
   if (L.scaling) r -= L.nscale[L.tree->root][p] * 256. * 0.69314718055994530942;
   return r;
@@ -577,11 +586,13 @@ extern "C" {
 //   out: lnl (= getLogLikelihood()), site_lnl[n_sites] (nullable),
 //        t_traversal (seconds per traversal, nullable), t_reduce (nullable)
 // Returns 0, or < 0 on error (-2: state code not allowed by the model).
-int orc_tree_loglik(int n_nodes, int root, const int* son_start, const int* sons, const int* leaf_row,
-                    int n_sites, const int* states, int S, int C, int n_codes, const double* init_values,
-                    const double* pmats, const double* class_probs, const double* root_freqs, int use_patterns,
-                    int scaling, int n_rep, double* lnl, double* site_lnl, double* t_traversal,
-                    double* t_reduce) {
+//   nh_root: 0 = the homogeneous root rule (<= 0 terms dropped), 1 = the NH rule (no
+//            per-term guard, class sum clamped at 0), see rootLogLikForSite
+int orc_tree_loglik_rule(int n_nodes, int root, const int* son_start, const int* sons, const int* leaf_row,
+                         int n_sites, const int* states, int S, int C, int n_codes, const double* init_values,
+                         const double* pmats, const double* class_probs, const double* root_freqs,
+                         int use_patterns, int scaling, int nh_root, int n_rep, double* lnl, double* site_lnl,
+                         double* t_traversal, double* t_reduce) {
   OTree T;
   T.n_nodes = n_nodes;
   T.root = root;
@@ -639,7 +650,7 @@ int orc_tree_loglik(int n_nodes, int root, const int* son_start, const int* sons
   for (int r = 0; r < n_rep; r++) computeSubtreeLikelihood(L, root);  // computeTreeLikelihood :795-798
   auto t1 = std::chrono::steady_clock::now();
   std::vector<double> la(n_sites);
-  for (int i = 0; i < n_sites; i++) la[i] = rootLogLikForSite(L, i, class_probs, root_freqs);
+  for (int i = 0; i < n_sites; i++) la[i] = rootLogLikForSite(L, i, class_probs, root_freqs, nh_root != 0);
   if (site_lnl)
     for (int i = 0; i < n_sites; i++) site_lnl[i] = la[i];
   std::sort(la.begin(), la.end());
@@ -650,6 +661,17 @@ int orc_tree_loglik(int n_nodes, int root, const int* son_start, const int* sons
   if (t_traversal) *t_traversal = std::chrono::duration<double>(t1 - t0).count() / n_rep;
   if (t_reduce) *t_reduce = std::chrono::duration<double>(t2 - t1).count();
   return 0;
+}
+
+// The homogeneous entry (RHomogeneousTreeLikelihood's root rule).
+int orc_tree_loglik(int n_nodes, int root, const int* son_start, const int* sons, const int* leaf_row,
+                    int n_sites, const int* states, int S, int C, int n_codes, const double* init_values,
+                    const double* pmats, const double* class_probs, const double* root_freqs, int use_patterns,
+                    int scaling, int n_rep, double* lnl, double* site_lnl, double* t_traversal,
+                    double* t_reduce) {
+  return orc_tree_loglik_rule(n_nodes, root, son_start, sons, leaf_row, n_sites, states, S, C, n_codes, init_values,
+                              pmats, class_probs, root_freqs, use_patterns, scaling, 0, n_rep, lnl, site_lnl,
+                              t_traversal, t_reduce);
 }
 
 // Double-recursive branch derivatives, restating DRHomogeneousTreeLikelihood

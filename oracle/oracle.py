@@ -37,6 +37,8 @@ def load() -> ct.CDLL:
     lib.orc_reversible_pij.argtypes = [ct.c_int, dp, dp, ct.c_double, dp]
     lib.orc_tree_loglik.argtypes = [ct.c_int, ct.c_int, ip, ip, ip, ct.c_int, ip, ct.c_int, ct.c_int, ct.c_int, dp,
                                     dp, dp, dp, ct.c_int, ct.c_int, ct.c_int, dp, dp, dp, dp]
+    lib.orc_tree_loglik_rule.argtypes = [ct.c_int, ct.c_int, ip, ip, ip, ct.c_int, ip, ct.c_int, ct.c_int, ct.c_int,
+                                         dp, dp, dp, dp, ct.c_int, ct.c_int, ct.c_int, ct.c_int, dp, dp, dp, dp]
     lib.orc_count_patterns.argtypes = [ct.c_int, ct.c_int, ip]
     lib.orc_dr_derivatives.argtypes = [ct.c_int, ct.c_int, ip, ip, ip, ct.c_int, ip, ct.c_int, ct.c_int, ct.c_int,
                                        dp, dp, dp, dp, dp, dp, dp, dp]
@@ -97,8 +99,10 @@ def reversible_pij(Q: np.ndarray, pi: np.ndarray, t: float) -> np.ndarray:
 
 
 def tree_loglik(son_start, sons, leaf_row, root, states, init_table, pmats, class_probs, root_freqs,
-                use_patterns=True, scaling=False, n_rep=1, want_sites=False):
+                use_patterns=True, scaling=False, n_rep=1, want_sites=False, nh_root=False):
     """pmats: [n_nodes][C][S][S]; states: [n_leaf_rows][n_sites] ints.
+    nh_root: RNonHomogeneousTreeLikelihood's root rule (no <= 0 guards, site sum clamped at
+    0) instead of RHomogeneousTreeLikelihood's (terms <= 0 dropped).
     Returns (lnL, site_lnl or None, seconds per traversal, seconds for the reduction)."""
     lib = load()
     n_nodes = len(leaf_row)
@@ -114,9 +118,10 @@ def tree_loglik(son_start, sons, leaf_row, root, states, init_table, pmats, clas
     pm = np.ascontiguousarray(pmats, dtype=np.float64)
     cp = np.ascontiguousarray(class_probs, dtype=np.float64)
     rf = np.ascontiguousarray(root_freqs, dtype=np.float64)
-    rc = lib.orc_tree_loglik(n_nodes, root, _i(args[0]), _i(args[1]), _i(args[2]), n_sites, _i(states), S, C,
-                             it.shape[0], _d(it), _d(pm), _d(cp), _d(rf), int(use_patterns), int(scaling), n_rep,
-                             ct.byref(lnl), _d(sites) if want_sites else None, ct.byref(tt), ct.byref(tr))
+    rc = lib.orc_tree_loglik_rule(n_nodes, root, _i(args[0]), _i(args[1]), _i(args[2]), n_sites, _i(states), S, C,
+                                  it.shape[0], _d(it), _d(pm), _d(cp), _d(rf), int(use_patterns), int(scaling),
+                                  int(nh_root), n_rep, ct.byref(lnl), _d(sites) if want_sites else None,
+                                  ct.byref(tt), ct.byref(tr))
     if rc != 0:
         raise ValueError(f"oracle error {rc} (state code not allowed by the model?)")
     return lnl.value, sites, tt.value, tr.value

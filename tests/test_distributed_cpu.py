@@ -166,3 +166,96 @@ def test_bench_stdout_is_one_json_line(tmp_path):
     assert r.returncode == 0, r.stderr
     assert r.stdout.splitlines() == ['{"metric": "m"}']
     assert "C-level banner" in r.stderr and "python-level noise" in r.stderr
+
+
+# ---------------------------------------------------------------- libplk's own exchange bookkeeping
+
+def _exchange_worker(rank, world, port, counts, flags, n_deriv, q):
+    """One rank of plk_comm_init's exchange with gloo standing in for RCCL: its record packed
+    by libplk (plk_exchange_pack), the fixed-size all-gather, then libplk's reduction
+    (plk_exchange_reduce) and rank-order derivative sums (plk_exchange_rank_sums) -- the code
+    root_finish / comm_sum_values run on the gathered buffers."""
+    import torch
+    import plk
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    blocks_all, deriv_all = _exchange_data(counts, world, n_deriv)
+    a = sum(counts[:rank])
+    mine = blocks_all[a:a + counts[rank]]
+    # the block counts are exchanged once, as plk_comm_init does
+    cnt = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(cnt, torch.tensor([len(mine)], dtype=torch.int64))
+    got_counts = [int(c.item()) for c in cnt]
+    stride = plk.exchange_stride(got_counts)
+    rec = plk.exchange_pack(mine, flags[rank], stride)
+    parts = [torch.zeros(stride, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(parts, torch.from_numpy(rec))
+    gathered = torch.stack(parts).numpy()
+    lnl, uflow = plk.exchange_reduce(gathered, got_counts, stride)
+    dv = [torch.zeros(n_deriv, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(dv, torch.from_numpy(deriv_all[rank].copy()))
+    d = plk.exchange_rank_sums(torch.stack(dv).numpy(), world)
+    q.put((rank, got_counts, stride, rec.tolist(), lnl, uflow, d.tolist()))
+    dist.destroy_process_group()
+
+
+def _exchange_data(counts, world, n_deriv):
+    """Block sums over a wide dynamic range, so that any other order of adds changes the
+    total's low bits; per-rank derivative sums likewise."""
+    rng = np.random.default_rng(sum(counts) * 31 + world)
+    blocks = -rng.gamma(2.0, 1.0, size=sum(counts)) * 10.0 ** rng.uniform(-2, 7, size=sum(counts))
+    deriv = rng.normal(size=(world, n_deriv)) * 10.0 ** rng.uniform(-3, 6, size=(world, n_deriv))
+    return blocks, deriv
+
+
+@pytest.mark.parametrize("counts,flags", [
+    ([5, 3], [0, 0]),                    # the last rank has fewer blocks than the widest
+    ([2, 7, 4], [0, 1, 0]),              # a flag on a middle rank reaches every rank
+    ([245, 245, 245, 245, 245, 245, 245, 244], [0] * 7 + [1]),   # config 5's 2 M over 8 ranks
+    ([9, 1, 1, 6, 3, 8, 2, 1], [0] * 8),  # ragged, world 8
+    ([1, 0, 4], [0, 0, 0])])             # a rank with no blocks
+def test_libplk_exchange_multi_rank_bitwise(counts, flags):
+    """libplk's exchange bookkeeping at world 2 / 3 / 8 over gloo with uneven per-rank block
+    counts (padding to the widest rank's count): every rank gets the one-process fixed-order
+    sum of all blocks bitwise (RNonHomogeneousTreeLikelihood.cpp:168-182 summed as one chain),
+    the OR of the underflow flags, and the rank-order derivative sums; the record is the
+    documented layout (block sums, zeros, flag)."""
+    world = len(counts)
+    n_deriv = 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, counts, flags, n_deriv, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    blocks, deriv = _exchange_data(counts, world, n_deriv)
+    whole = 0.0
+    for b in blocks:          # one process over every block, block order
+        whole += b
+    dsum = np.zeros(n_deriv)
+    for r in range(world):    # rank order
+        dsum = dsum + deriv[r]
+    stride = max(counts) + 1
+    a = 0
+    for rank, got_counts, st, rec, lnl, uflow, d in res:
+        assert got_counts == counts and st == stride
+        exp_rec = list(blocks[a:a + counts[rank]]) + [0.0] * (stride - 1 - counts[rank]) + [float(flags[rank])]
+        assert rec == exp_rec
+        a += counts[rank]
+        assert lnl == whole, (rank, lnl, whole)
+        assert uflow == any(flags)
+        assert np.array_equal(np.array(d), dsum)
+
+
+def test_libplk_exchange_argument_checks():
+    import plk
+    with pytest.raises(plk.PlkError):
+        plk.exchange_stride([3, -1])
+    with pytest.raises(plk.PlkError):
+        plk.exchange_pack(np.ones(4), False, 4)             # 4 blocks + the flag need stride 5
+    with pytest.raises(plk.PlkError):
+        plk.exchange_reduce(np.zeros((2, 3)), [2, 3], 3)    # rank 1's 3 blocks exceed its record

@@ -1012,6 +1012,45 @@ def test_subtree_patterns_polytomy(S, C, scaling):
     assert np.allclose(s1, s2, rtol=1e-13, atol=0)
 
 
+@pytest.mark.parametrize("S,C", [(4, 2), (20, 1)])
+def test_subtree_patterns_wide_polytomy_rescale(S, C):
+    """A root polytomy of nine cherries whose partials sit near 2^-150 (a code whose vector is
+    1e-23 on 80 % of the cells): the running product must be rescaled after every
+    group of three children in the compressed links kernels as in the uncompressed
+    traversal's ACCUMULATE ops -- checked once at the end it underflows to 0 (-inf sites).
+    Compressed == uncompressed (bitwise for 4 states: the same arithmetic; 1e-13 for 20),
+    both == the oracle (which rescales after every third son the same way) at 1e-12."""
+    rng = np.random.default_rng(90 + S)
+    clade = lambda k: f"(t{k}a:0.3,t{k}b:0.4):0.2"
+    et = phylo.engine_tree(phylo.Tree.from_newick("(" + ",".join(clade(k) for k in range(9)) + ");"))
+    assert max(len(ch) for _, ch in et.ops) == 9
+    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5)) if S == 4 else phylo.lg08()
+    alph = phylo.DNA if S == 4 else phylo.PROTEIN
+    rates, probs = phylo.gamma_rates(C, 0.6) if C > 1 else (np.ones(1), np.ones(1))
+    n = 900
+    states = rng.choice(S, size=(et.n_tips, n), p=m.pi).astype(np.int32)
+    init = np.array(alph.init_table, dtype=np.float64, copy=True)
+    code = alph.n_codes - 1
+    init[code] = 1e-23
+    states[rng.random(states.shape) < 0.8] = code
+    res = []
+    for mode in (plk.PLK_FLAG_SUBTREE_PATTERNS, plk.PLK_FLAG_LEVELWISE):
+        eng = engine_for(et, S, C, n, states, init, rates, probs, m.pi, [m],
+                         flags=plk.PLK_FLAG_NONNEG_GUARD | mode | plk.PLK_FLAG_SCALING)
+        res.append(run_engine(eng, et))
+        if mode == plk.PLK_FLAG_SUBTREE_PATTERNS:
+            assert eng.kernel_path() == "subtree_patterns"
+            pm = engine_pmats(eng, et)
+    (l1, s1, _), (l2, s2, _) = res
+    assert np.all(np.isfinite(s1)) and s1.min() < -3 * 256 * np.log(2)   # several rescales per site
+    if S == 4:
+        assert l1 == l2 and np.array_equal(s1, s2)
+    else:
+        assert np.allclose(s1, s2, rtol=1e-13, atol=0)
+    lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=True, pmats=pm)
+    check(l1, s1, lo, so)
+
+
 def test_subtree_patterns_errors():
     et, m, alph, rates, probs, states = _random_problem(4, 2, 12, 300, seed=43)
     with pytest.raises(plk.PlkError):   # no compressed double-recursive passes

@@ -223,3 +223,55 @@ def test_oracle_dr_derivatives_vs_central_differences(seed):
         fd2 = (lnl_at(t + 1e-4) - 2 * lnl_at(t) + lnl_at(t - 1e-4)) / 1e-8
         assert abs(d1[v] - fd1) <= 1e-6 * max(1.0, abs(fd1)), (v, d1[v], fd1)
         assert abs(d2[v] - fd2) <= 1e-4 * max(1.0, abs(fd2)), (v, d2[v], fd2)
+
+
+# ---------------------------------------------------------------- the two root rules (row a10)
+
+def test_root_rules_agree_without_nonpositive_terms():
+    """On positive root partials the NH rule (no guards, clamp) and the homogeneous rule
+    (terms <= 0 dropped) are the same sum: the golden holds under both."""
+    case = _ref()["test_likelihood"]
+    et = phylo.engine_tree(phylo.Tree.from_newick(case["newick"]), unroot=case["unroot"])
+    states = np.stack([phylo.DNA.encode(case["sequences"][n]) for n in et.tip_names])
+    m = case["model"]
+    r, p = oracle.gamma_rates(case["rates"]["n"], case["rates"]["alpha"])
+    pm = np.zeros((et.n_nodes, len(r), 4, 4))
+    for n in range(et.n_nodes):
+        if n != et.root:
+            pm[n] = np.stack([oracle.t92_pij(m["kappa"], m["theta"], et.brlen[n] * rc) for rc in r])
+    pi = oracle.t92_freqs(m["theta"])
+    import negroot
+    lh, sh = negroot.oracle_sites(et, states, phylo.DNA.init_table, pm, p, pi, False, False)
+    ln, sn = negroot.oracle_sites(et, states, phylo.DNA.init_table, pm, p, pi, False, True)
+    assert lh == ln and np.array_equal(sh, sn)
+    assert abs(-ln - 85.030942031997312824) < 1e-9
+
+
+@pytest.mark.parametrize("S,C", [(4, 4), (20, 2), (64, 1)])
+@pytest.mark.parametrize("kind", ["mixed", "clamp"])
+def test_root_rules_oracle_vs_numpy(S, C, kind):
+    """The oracle's two root rules (orc_tree_loglik_rule) against a numpy restatement of
+    L/RHomogeneousTreeLikelihood.cpp:192-216 and L/RNonHomogeneousTreeLikelihood.cpp:198-221
+    on inputs with root terms <= 0: per site (-inf at the same sites, no NaN), and the two
+    rules differ where the census says they must."""
+    import negroot
+    et, m, init, states, rates, probs, pi, pm = negroot.problem(S, C, 16 if S < 64 else 8, 400, seed=S + C)
+    delta, pm2, census = negroot.choose(et, states, init, pm, pi, probs, kind)
+    assert census["neg_terms"] > 0
+    Lr, lf = negroot.root_partials_signed(et, states, init, pm2)
+    l_h, l_nh = negroot.rule_sums(Lr, pi, probs)
+    with np.errstate(divide="ignore"):
+        want_h = np.log(l_h) + lf
+        want_nh = np.log(np.maximum(l_nh, 0.0)) + lf
+    lh, sh = negroot.oracle_sites(et, states, init, pm2, probs, pi, False, False)
+    ln, sn = negroot.oracle_sites(et, states, init, pm2, probs, pi, False, True)
+    # sums in a different order: cancellation in the NH sum near 0 costs digits there
+    negroot.same_sites(sh, want_h, rel=1e-11)
+    negroot.same_sites(sn, want_nh, rel=1e-8)
+    fin = np.isfinite(sn)
+    assert np.any(sh[fin] != sn[fin])                    # the guards fired
+    if kind == "clamp":
+        assert census["clamp_sites"] > 0 and np.isneginf(ln)
+        assert np.any(np.isneginf(sn) & np.isfinite(sh))  # the clamp fired (log 0, not NaN)
+    else:
+        assert np.isfinite(ln) and np.isfinite(lh) and ln < lh
