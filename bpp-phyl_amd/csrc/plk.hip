@@ -396,6 +396,13 @@ struct plk_handle_s {
   size_t d_drpre_cap = 0;
   double* d_blk_all = nullptr;            // [comm_ranks][comm_stride]
   int64_t* d_comm_counts = nullptr;       // block sums per rank
+  // PLK_DEBUG_CLOCK: per-workgroup clock stamps of the last jit_tree4 traversal (mapped pinned,
+  // 4 u64 per workgroup) and one summary record per traversal (plk_clock_records)
+  unsigned long long* h_clk = nullptr;
+  unsigned long long* d_clk = nullptr;
+  size_t clk_cap = 0;                     // workgroups the stamp buffer holds
+  size_t clk_n = 0;                       // workgroups stamped by the pending traversal
+  std::vector<double> clk_rec;
   int32_t* h_uflow = nullptr;             // mapped pinned: root-reduction underflow flag (plk_root_underflow)
   int32_t* d_uflow = nullptr;             // its device address
   double* h_blk_all = nullptr;            // mapped pinned: every rank's record [comm_ranks][comm_stride]
@@ -1136,6 +1143,7 @@ int plk_destroy(plk_handle h) {
   if (h->h_req) (void)hipHostFree(h->h_req);
   if (h->h_blocks) hipHostFree(h->h_blocks);
   if (h->h_uflow) hipHostFree(h->h_uflow);
+  if (h->h_clk) hipHostFree(h->h_clk);
   if (h->req_done) hipEventDestroy(h->req_done);
   for (auto& e : h->events) {
     hipEventDestroy(e.a);
@@ -2153,6 +2161,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // fires; on cfg5 it fires in almost every super-block (1.27 vs 1.14 ms), so opt-in
     // classes in the wave: next class's P(t) loads overlap this class's FMAs
     sh.ppipe = true;
+    sh.clk = env_is("PLK_DEBUG_CLOCK", '1');
     // PLK_JIT_BLOCKS=1: the root fragment forms the block sums (no wave_sums_to_blocks
     // launch).  Measured slower (cfg2 traversal 0.125 -> 0.160 ms): the wave that stores a
     // wave sum must wait for the store and the counter's atomic round trip (~3 us) before
@@ -2164,7 +2173,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.pin != h->jit_shape.pin ||
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
-        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe) {
+        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.clk != h->jit_shape.clk) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
@@ -2236,6 +2245,21 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
   }
   h->kernel_path = jit ? "jit_tree4" : jitm ? "jit_treeM" : kind == FK_TREEM ? "treeM" : "tree4";
   int first = 0;
+  if (jit && h->jit_shape.clk) {
+    // stamp buffer for every workgroup of every tier's launch (grids below: at most
+    // jit_resident workgroups per fragment of a tier)
+    size_t need = 0;
+    for (const auto& t : h->prog_tiers) need += (size_t)(h->n_pad / 64) * t.size();
+    if (need > h->clk_cap) {
+      if (h->h_clk) hipHostFree(h->h_clk);
+      h->h_clk = nullptr;
+      if (hipHostMalloc((void**)&h->h_clk, need * 4 * sizeof(unsigned long long), hipHostMallocMapped) != hipSuccess ||
+          hipHostGetDevicePointer((void**)&h->d_clk, h->h_clk, 0) != hipSuccess)
+        return fail(h, PLK_ERR_OOM, "clock stamp buffer");
+      h->clk_cap = need;
+    }
+    h->clk_n = 0;
+  }
   for (const auto& t : h->prog_tiers) {
     a.frag_start = h->d_frag + first;
     dim3 grid((unsigned)(h->n_pad / 64), (unsigned)t.size());
@@ -2247,7 +2271,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     if (jit) {
       const double* pm = h->pmats;
       int base = first;
-      void* args[] = {&ja, &pm, &base};
+      unsigned long long* clkp = h->d_clk ? h->d_clk + 4 * h->clk_n : nullptr;
+      void* args[] = {&ja, &pm, &base, &clkp};  // (the 4th only exists in a PLK_DEBUG_CLOCK build)
       // persistent grid: as many workgroups as are resident at once (occupancy query), so
       // every workgroup stages its tables once and there is no second dispatch round
       int wgs = 0;
@@ -2277,6 +2302,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
                                       (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
+      if (sh.clk) h->clk_n += (size_t)gx * grid.y;
     } else if (jitm) {
       int base = first;
       void* args[] = {&ma, &base};
@@ -3691,10 +3717,35 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
   return PLK_OK;
 }
 
+// PLK_DEBUG_CLOCK: one record per stamped traversal, from its workgroups' stamps --
+// [0] shader clock in MHz over all workgroups (sum of clock ticks / sum of 100 MHz ticks),
+// [1] / [2] the slowest / fastest workgroup's, [3] first start to last end in us, [4] workgroups
+void clock_summary(plk_handle h) {
+  if (!h->clk_n) return;
+  double sc = 0.0, sw = 0.0, lo = 1e30, hi = 0.0;
+  unsigned long long w0 = ~0ull, w1 = 0;
+  for (size_t i = 0; i < h->clk_n; ++i) {
+    const volatile unsigned long long* q = h->h_clk + 4 * i;
+    const double dc = (double)(q[2] - q[0]), dw = (double)(q[3] - q[1]);
+    if (dw <= 0.0) continue;
+    sc += dc;
+    sw += dw;
+    lo = std::min(lo, 100.0 * dc / dw);
+    hi = std::max(hi, 100.0 * dc / dw);
+    w0 = std::min<unsigned long long>(w0, (unsigned long long)q[1]);
+    w1 = std::max<unsigned long long>(w1, (unsigned long long)q[3]);
+  }
+  const double rec[5] = {sw > 0 ? 100.0 * sc / sw : 0.0, lo, hi, w1 > w0 ? (double)(w1 - w0) / 100.0 : 0.0,
+                         (double)h->clk_n};
+  h->clk_rec.insert(h->clk_rec.end(), rec, rec + 5);
+  h->clk_n = 0;
+}
+
 int root_finish(plk_handle h, double* lnl, double* block_sums, bool wait = true) {
   hipSetDevice(h->device);
   if (wait)
     if (int rc = stream_wait(h)) return rc;
+  clock_summary(h);  // (the stream has drained: root_finish reads the block sums below)
   double s = 0.0;
   if (h->comm) {
     // rank order, block order (comm_copy_kernel moved the records), and every rank's flag
@@ -3812,6 +3863,15 @@ int plk_exchange_reduce(const double* gathered, const int64_t* counts, int n_ran
 int plk_exchange_rank_sums(const double* gathered, int n_ranks, int64_t n, double* v) {
   if (!gathered || !v || n_ranks < 1 || n < 0) return fail(nullptr, PLK_ERR_ARG, "bad rank-sum arguments");
   xchg::rank_sums(gathered, n_ranks, (size_t)n, v);
+  return PLK_OK;
+}
+
+int plk_clock_records(plk_handle h, double* out, int cap, int* n) {
+  if (!h || !n || cap < 0 || (cap > 0 && !out)) return fail(h, PLK_ERR_ARG, "bad clock-record arguments");
+  const int have = (int)(h->clk_rec.size() / 5);
+  *n = have;
+  if (out) std::memcpy(out, h->clk_rec.data(), (size_t)std::min(cap, have) * 5 * sizeof(double));
+  if (cap >= have) h->clk_rec.clear();
   return PLK_OK;
 }
 

@@ -384,6 +384,7 @@ struct JitShape {
   int L = 1;        // operand fetch lookahead (events)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
+  bool clk = false;         // PLK_DEBUG_CLOCK: per-workgroup shader-clock / constant-clock stamps (diagnostic)
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
     // the second exchange buffer only serves the per-node rescale
@@ -643,10 +644,14 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
            "#define U_ %d\n#define NT_ %d\n#define TD_ %d\n#define SC_ %s\n#define V_ (4 * CW_ * PW_)\n"
            "extern \"C\" __global__ __launch_bounds__(%d%s) void plk_jit_tree4(JArgs a, const double* __restrict__ "
-           "pmats, int frag_base) {\n",
+           "pmats, int frag_base%s) {\n",
            C, CW, NW, PW, sh.G, NW * sh.G, U, std::max(sh.NT, 1), std::max(sh.TD, 4), sh.scale ? "true" : "false",
-           64 * NW * sh.G, minw_s.c_str());
+           64 * NW * sh.G, minw_s.c_str(), sh.clk ? ", unsigned long long* __restrict__ clk_" : "");
   s += buf;
+  // PLK_DEBUG_CLOCK (diagnostic build of the same program): thread 0 of every workgroup records
+  // the shader clock counter (clock64) and the constant 100 MHz counter (wall_clock64) at its
+  // start and end, so the host can tell the shader clock the launch ran at
+  if (sh.clk) s += "  const unsigned long long clk_c0_ = clock64(), clk_w0_ = wall_clock64();\n";
   s += R"PLKJIT(  extern __shared__ __attribute__((aligned(16))) double lds[];
   double* tab = lds;                                          // units: [C_][U_ or U_ * U_][4] each
   double* xch = tab + TD_;                                    // [2][PW_][NWT_][64] (rescale alternates)
@@ -1033,6 +1038,11 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     s += "    } break;\n";
   }
   s += "    default: break;\n    }\n  }\n";
+  if (sh.clk)
+    s += "  if (threadIdx.x == 0) {\n"
+         "    unsigned long long* q_ = clk_ + 4 * ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x);\n"
+         "    const unsigned long long c1_ = clock64(), w1_ = wall_clock64();\n"
+         "    q_[0] = clk_c0_; q_[1] = clk_w0_; q_[2] = c1_; q_[3] = w1_;\n  }\n";
   // Exit ticket (dynamic super-blocks): thread 0 of every workgroup takes one ticket after its
   // last super-block -- its own counter atomics have returned by then -- and the last one
   // leaves the launch's counters and the ticket counter at 0 for the next launch, so the host

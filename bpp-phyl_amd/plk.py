@@ -39,7 +39,7 @@ EXPORTS = [
     "plk_get_timing_ex", "plk_traversal_work", "plk_create_multi", "plk_shard_count", "plk_comm_get_id",
     "plk_comm_init", "plk_get_dpmatrix", "plk_root_pair_derivatives", "plk_get_fanout",
     "plk_root_underflow", "plk_exchange_stride", "plk_exchange_pack", "plk_exchange_reduce",
-    "plk_exchange_rank_sums",
+    "plk_exchange_rank_sums", "plk_clock_records",
 ]
 
 
@@ -96,6 +96,7 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
         "plk_shard_count": ([ct.c_void_p, P(ct.c_int)], ct.c_int),
         "plk_get_fanout": ([ct.c_void_p, ct.c_int, dp, dp, P(ct.c_int64)], ct.c_int),
         "plk_root_underflow": ([ct.c_void_p, P(ct.c_int)], ct.c_int),
+        "plk_clock_records": ([ct.c_void_p, dp, ct.c_int, P(ct.c_int)], ct.c_int),
         "plk_comm_get_id": ([P(plk_comm_id)], ct.c_int),
         "plk_exchange_stride": ([P(ct.c_int64), ct.c_int, P(ct.c_int64)], ct.c_int),
         "plk_exchange_pack": ([dp, ct.c_int64, ct.c_int, ct.c_int64, dp], ct.c_int),
@@ -401,6 +402,16 @@ class Engine:
         f = ct.c_int(0)
         self._chk(self.lib.plk_root_underflow(self.h, ct.byref(f)))
         return bool(f.value)
+
+    def clock_records(self) -> np.ndarray:
+        """plk_clock_records (PLK_DEBUG_CLOCK=1): per stamped traversal [shader MHz over all
+        workgroups, slowest / fastest workgroup MHz, span us, workgroups]; clears them."""
+        n = ct.c_int(0)
+        self._chk(self.lib.plk_clock_records(self.h, None, 0, ct.byref(n)))
+        out = np.zeros((n.value, 5))
+        if n.value:
+            self._chk(self.lib.plk_clock_records(self.h, _d(out), n.value, ct.byref(n)))
+        return out
 
     def branch_derivatives(self, branch: int):
         """(d lnL/dt, d2 lnL/dt2) for the branch above node `branch`."""

@@ -236,6 +236,14 @@ int plk_root_loglik(plk_handle h, int root, double* lnl, double* site_lnl, doubl
  * scaled handle.  Replaces nothing in the reference, which has no scaling. */
 int plk_root_underflow(plk_handle h, int* flag);
 
+/* Diagnostic (PLK_DEBUG_CLOCK=1 when the traversal kernel is generated): every jit_tree4
+ * workgroup stamps the shader clock counter and the constant 100 MHz counter at its start and
+ * end, and each evaluation leaves one record of 5 doubles: the shader clock in MHz over all
+ * workgroups, the slowest and fastest workgroup's MHz, the traversal's first-start-to-last-end
+ * span in us, and the workgroup count.  *n = records held; up to cap are copied to out, and
+ * the held records are cleared when all fit.  Replaces nothing in the reference. */
+int plk_clock_records(plk_handle h, double* out /* cap x 5 */, int cap, int* n);
+
 /* One likelihood evaluation as RHomogeneousTreeLikelihood::fireParameterChanged does it
  * (Likelihood/RHomogeneousTreeLikelihood.cpp:255-283): P(t) of the listed branches
  * (plk_update_pmatrices, P only), the postorder traversal (plk_update_partials) and the
