@@ -338,8 +338,13 @@ struct plk_handle_s {
   JitPlan jit_plan;            // table units / events of the current program (plk_jit.hpp)
   bool jit_plan_valid = false;
   int jit_plan_U = 0, jit_plan_budget = -1;
+  int jit_plan_qb = -1;                 // quad budget the plan was built with (0: none)
+  bool jit_plan_cls = false;            // the plan is one class per workgroup (it has quad units)
+  double* d_cls = nullptr;              // JitShape::cls: every class's root term, [C][n_pad]
+  size_t d_cls_cap = 0;
+  double* fused_cls_blocks = nullptr;   // the last traversal formed its block sums here (cls_blocks_kernel)
   uint8_t* d_ucodes = nullptr;  // code row of every table unit of jit_plan (unit_codes_kernel)
-  int2* d_units = nullptr;      // (ta, tb) of every unit
+  int4* d_units = nullptr;      // (ta, tb) of every unit
   size_t ucodes_cap = 0, units_cap = 0;
   bool ucodes_valid = false;    // cleared by new tip codes and by a new plan
   int jit_resident = 0;  // workgroups of jit_fn resident at once on the device
@@ -1137,7 +1142,7 @@ int plk_destroy(plk_handle h) {
                   h->d_ops, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
                   h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre, h->d_sbctr,
-                  h->d_cherry_rows, h->d_kidsl};
+                  h->d_cherry_rows, h->d_kidsl, h->d_cls};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) (void)hipHostFree(h->h_req);
@@ -1939,9 +1944,11 @@ int build_tree4_program(plk_handle h, const plk_op* ops, int n_ops, bool materia
   HIPCHK(h, hipMemcpyAsync(h->d_frag, start_sorted.data(), 2 * nf * sizeof(int32_t), hipMemcpyHostToDevice,
                            h->stream));
   h->prog_nf = nf;
-  rc = ensure_cap(h, (void**)&h->d_sbctr, &h->d_sbctr_cap, (size_t)(nf + 1) * sizeof(unsigned));
+  // one counter per fragment and class (one class per workgroup, plk_jit.hpp JitShape::cls),
+  // then the exit ticket
+  rc = ensure_cap(h, (void**)&h->d_sbctr, &h->d_sbctr_cap, (size_t)(nf * h->C + 1) * sizeof(unsigned));
   if (rc) return rc;
-  HIPCHK(h, hipMemsetAsync(h->d_sbctr, 0, (size_t)(nf + 1) * sizeof(unsigned), h->stream));
+  HIPCHK(h, hipMemsetAsync(h->d_sbctr, 0, (size_t)(nf * h->C + 1) * sizeof(unsigned), h->stream));
   h->prog_host = prog;
   h->frag_starts_host.assign(start_sorted.begin(), start_sorted.begin() + nf);
   h->jit_fn = nullptr;  // specialised kernel of the new program: compiled on first use
@@ -2111,23 +2118,38 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // cherries read one product table (plk_jit.hpp: JitUnit) while a fragment's tables stay
     // within PLK_JIT_PAIR_KB (0: no pairs)
     const int budget = tune_int("JIT_PAIR_KB", 64, 0, 150) * 1024 / (int)sizeof(double);
-    if (!h->jit_plan_valid || h->jit_plan_U != sh.U || h->jit_plan_budget != budget) {
-      h->jit_plan = jit_plan(h->prog_host, h->frag_starts_host, sh.C, sh.U, budget, sh.scale);
+    // One class per workgroup with quad units (plk_jit.hpp JitUnit, JitShape::cls): tables of
+    // one class, so a fragment's cherries fit as 4-tip subtree tables -- for one class per wave,
+    // no rescaling, lnL only (quads are never stored) and at most 4 codes in use (U^4 <= 256).
+    // PLK_TUNE JIT_QUAD_KB bounds the tables (0: off); the plan is rebuilt as usual when it
+    // gets no quad.
+    const bool cls_ok = !h->prog_ciw && !sh.scale && (h->flags & PLK_FLAG_LNL_ONLY) && sh.U <= 4;
+    const int qb = cls_ok ? tune_int("JIT_QUAD_KB", 136, 0, 150) * 1024 / (int)sizeof(double) : 0;
+    if (!h->jit_plan_valid || h->jit_plan_U != sh.U || h->jit_plan_budget != budget || h->jit_plan_qb != qb) {
+      h->jit_plan_cls = false;
+      if (qb > 0) {
+        h->jit_plan = jit_plan(h->prog_host, h->frag_starts_host, sh.C, sh.U, std::max(qb, budget), sh.scale, true, qb);
+        for (const auto& un : h->jit_plan.units)
+          for (const JitUnit& u : un) h->jit_plan_cls |= u.tc >= 0;
+      }
+      if (!h->jit_plan_cls) h->jit_plan = jit_plan(h->prog_host, h->frag_starts_host, sh.C, sh.U, budget, sh.scale);
       h->jit_plan_valid = true;
       h->jit_plan_U = sh.U;
       h->jit_plan_budget = budget;
+      h->jit_plan_qb = qb;
       h->jit_fn = nullptr;
       h->ucodes_valid = false;
     }
+    sh.cls = h->jit_plan_cls;
     if (!h->ucodes_valid) {
-      std::vector<int2> units;
+      std::vector<int4> units;
       for (const auto& un : h->jit_plan.units)
-        for (const JitUnit& u : un) units.push_back(make_int2(u.ta, u.tb));
+        for (const JitUnit& u : un) units.push_back(make_int4(u.ta, u.tb, u.tc, u.td));
       int rc = ensure_cap(h, (void**)&h->d_ucodes, &h->ucodes_cap, std::max<size_t>(units.size(), 1) * h->n_pad);
-      if (!rc) rc = ensure_cap(h, (void**)&h->d_units, &h->units_cap, std::max<size_t>(units.size(), 1) * sizeof(int2));
+      if (!rc) rc = ensure_cap(h, (void**)&h->d_units, &h->units_cap, std::max<size_t>(units.size(), 1) * sizeof(int4));
       if (rc) return rc;
       if (!units.empty()) {
-        HIPCHK(h, hipMemcpyAsync(h->d_units, units.data(), units.size() * sizeof(int2), hipMemcpyHostToDevice,
+        HIPCHK(h, hipMemcpyAsync(h->d_units, units.data(), units.size() * sizeof(int4), hipMemcpyHostToDevice,
                                  h->stream));
         const dim3 ug((unsigned)((h->n_pad / 16 + 255) / 256), (unsigned)units.size());
         hipLaunchKernelGGL(unit_codes_kernel, ug, dim3(256), 0, h->stream, h->codes, h->n_pad, h->d_units, sh.U,
@@ -2139,6 +2161,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     }
     sh.NT = h->jit_plan.NU;
     sh.TD = h->jit_plan.tab_doubles;
+    sh.QT = h->jit_plan.quad_tmp;
     // pattern groups per workgroup (they share the staged tables): with per-node rescaling
     // and one class per wave every node has two workgroup barriers, whose cost grows with
     // the waves that meet there (cfg5: 1.93 ms at G = 2, 1.16 ms at G = 1), so one group;
@@ -2147,11 +2170,20 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // with the tier's fragments side by side: G = 6 / 7 / 8 = 0.48 / 0.43 / 0.39 ms);
     // otherwise the G with the most resident waves (jit_auto_groups; cfg2 with cherry
     // tables: G = 3, 0.140 ms, G = 2 0.150, G = 4 0.162)
-    sh.G = tune_int("JIT_G", 0, 0, 8);
-    if (sh.G == 0) sh.G = h->prog_ciw ? 8 : sh.scale ? 1 : jit_auto_groups(sh);
+    sh.PW = tune_int("JIT_PW", 1, 1, 2);  // (before G: the code rows take G x PW)
+    sh.G = tune_int("JIT_G", 0, 0, 16);
+    if (sh.G == 0) {
+      if (sh.cls) {
+        // one class per workgroup: the tables take most of the LDS, so one workgroup per CU
+        // and as many groups as fit (at most 16: 1024 threads)
+        sh.G = 16;
+        while (sh.G > 1 && sh.lds_bytes() > 160 * 1024 - 64) --sh.G;
+      } else {
+        sh.G = h->prog_ciw ? 8 : sh.scale ? 1 : jit_auto_groups(sh);
+      }
+    }
     // two patterns per lane halve the P(t) reads per FMA but double the registers:
     // measured slower (cfg2 0.255-0.301 vs 0.241 ms), so opt-in; not with speculation
-    sh.PW = 1;
     // two-stage pipeline, codes / HBM loads 3 ahead (cfg2 0.274 -> 0.259 ms); with every
     // class in the wave a ring slot is C x larger, so there two events ahead (cfg5 0.385 ms
     // at L = 2, 0.391 at L = 1; 1.48 vs 1.04 ms at L = 3 vs 1 before the P(t) stream)
@@ -2173,7 +2205,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.pin != h->jit_shape.pin ||
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
-        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.clk != h->jit_shape.clk) {
+        sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.clk != h->jit_shape.clk ||
+        sh.cls != h->jit_shape.cls) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
@@ -2195,8 +2228,14 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ja.guard = a.guard;
     ja.sb_ctr = h->d_sbctr;
     ja.dyn = tune_is("JIT_DYN", '0') ? 0 : 1;  // (per launch below)
-    ja.exit_ctr = h->d_sbctr + h->prog_nf;  // (null per launch below when not dynamic)
+    ja.exit_ctr = h->d_sbctr + (size_t)h->prog_nf * h->C;  // (null per launch below when not dynamic)
     ja.uflow = a.uflow;
+    ja.cls_sum = nullptr;
+    if (sh.cls) {
+      int rc = ensure_cap(h, (void**)&h->d_cls, &h->d_cls_cap, (size_t)h->C * h->n_pad * sizeof(double));
+      if (rc) return rc;
+      ja.cls_sum = h->d_cls;
+    }
   }
   const bool jitm = kind == FK_TREEM && h->prog_jitm;
   JMArgs ma;
@@ -2244,12 +2283,13 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     ma.uflow = a.uflow;
   }
   h->kernel_path = jit ? "jit_tree4" : jitm ? "jit_treeM" : kind == FK_TREEM ? "treeM" : "tree4";
+  h->fused_cls_blocks = nullptr;
   int first = 0;
   if (jit && h->jit_shape.clk) {
     // stamp buffer for every workgroup of every tier's launch (grids below: at most
     // jit_resident workgroups per fragment of a tier)
     size_t need = 0;
-    for (const auto& t : h->prog_tiers) need += (size_t)(h->n_pad / 64) * t.size();
+    for (const auto& t : h->prog_tiers) need += (size_t)(h->n_pad / 64) * t.size() * (h->jit_shape.cls ? h->C : 1);
     if (need > h->clk_cap) {
       if (h->h_clk) hipHostFree(h->h_clk);
       h->h_clk = nullptr;
@@ -2271,6 +2311,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     if (jit) {
       const double* pm = h->pmats;
       int base = first;
+      const int gz = sh.cls ? h->C : 1;  // one class per workgroup: grid.z = class
       unsigned long long* clkp = h->d_clk ? h->d_clk + 4 * h->clk_n : nullptr;
       void* args[] = {&ja, &pm, &base, &clkp};  // (the 4th only exists in a PLK_DEBUG_CLOCK build)
       // persistent grid: as many workgroups as are resident at once (occupancy query), so
@@ -2279,7 +2320,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
       {
         if (h->jit_resident <= 0) {
           int per_cu = 0, n_cu = 0;
-          HIPCHK(h, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, h->jit_fn, 64 * (h->C / sh.CW) * sh.G,
+          HIPCHK(h, hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, h->jit_fn, 64 * sh.nw() * sh.G,
                                                                        sh.lds_bytes()));
           HIPCHK(h, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, h->device));
           h->jit_resident = std::max(1, per_cu) * std::max(1, n_cu);
@@ -2288,21 +2329,29 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         // fragments (each stages its fragment's tables once and walks many super-blocks)
         // instead of the tier's fragments running one after another with every workgroup
         // staging tables for a few super-blocks (cfg5 0.49 -> 0.42 ms)
-        wgs = std::max(1, h->jit_resident / (int)grid.y);
+        wgs = std::max(1, h->jit_resident / ((int)grid.y * gz));
       }
       const unsigned gx = (unsigned)std::min<int64_t>(ja.n_sblocks, wgs);
       // dynamic super-blocks where a workgroup walks several (a tier of 1-2 per workgroup
       // gains nothing from them and pays the counter's round trips)
       ja.dyn = (!tune_is("JIT_DYN", '0') && ja.n_sblocks >= 3 * (int64_t)gx) ? 1 : 0;
       // the launch's counters start at 0; its last workgroup leaves them at 0 (exit ticket)
-      ja.exit_ctr = ja.dyn ? h->d_sbctr + h->prog_nf : nullptr;
+      ja.exit_ctr = ja.dyn ? h->d_sbctr + (size_t)h->prog_nf * h->C : nullptr;
       h->jit_last_gx = (int)gx;
       if ((int)h->jit_frag_gx.size() < h->prog_nf) h->jit_frag_gx.resize((size_t)h->prog_nf, 0);
       for (int k = 0; k < (int)t.size(); ++k) h->jit_frag_gx[(size_t)(first + k)] = (int)gx;
-      HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, 1, 64 * (h->C / sh.CW) * sh.G, 1, 1,
+      HIPCHK(h, hipModuleLaunchKernel(h->jit_fn, gx, grid.y, (unsigned)gz, 64 * sh.nw() * sh.G, 1, 1,
                                       (unsigned)sh.lds_bytes(),
                                       h->stream, args, nullptr));
-      if (sh.clk) h->clk_n += (size_t)gx * grid.y;
+      if (sh.clk) h->clk_n += (size_t)gx * grid.y * gz;
+      if (sh.cls && h->prog_root >= 0 && first + (int)t.size() == h->prog_nf) {
+        // the classes' root terms meet here: log, site lnL, wave and block sums (the work of
+        // reduce_root and wave_sums_to_blocks), inside the traversal's timing
+        h->fused_cls_blocks = block_target(h);
+        cls_blocks_kernel<<<(unsigned)h->n_blocks, 1024, 0, h->stream>>>(
+            h->d_cls, h->C, h->n_pad, h->weights, h->site_lnl, h->fused_cls_blocks, h->n_patterns,
+            (int)((h->n_patterns + 63) / 64), ja.guard, ja.uflow);
+      }
     } else if (jitm) {
       int base = first;
       void* args[] = {&ma, &base};
@@ -2835,6 +2884,15 @@ void traversal_work(plk_handle h, plk_work* w) {
       const int gx = f < h->jit_frag_gx.size() && h->jit_frag_gx[f] > 0 ? h->jit_frag_gx[f] : std::max(h->jit_last_gx, 1);
       for (const JitUnit& u : h->jit_plan.units[f]) {
         if (u.tb < 0) continue;
+        if (u.tc >= 0) {
+          // a quad replaces three nodes (two cherries and Q); per row and class: two pair
+          // products, two cherry contribs, the product, Q's contrib.  With one class per
+          // workgroup each of the gx x C workgroups builds its class's rows.
+          tnodes += 3;
+          rows += (int64_t)U * U * U * U * C;
+          tab += (double)gx * C * U * U * U * U * (3.0 * S + 3.0 * S * (2 * S - 1));
+          continue;
+        }
         tnodes++;
         rows += (int64_t)U * U * C;
         tab += (double)gx * C * U * U * (S + (u.br >= 0 ? (double)S * (2 * S - 1) : 0.0));
@@ -3691,9 +3749,25 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
   if (!h->pi_set || !h->rates_set) return fail(h, PLK_ERR_STATE, "root frequencies / category rates not set");
   hipSetDevice(h->device);
   if (h->fused_lnl_valid && h->fused_lnl_root == root) {
-    // the fused traversal already reduced the root: only the block sums remain
-    int rc = launch_block_sums(h);
-    if (rc) return rc;
+    // the fused traversal already reduced the root: only the block sums remain (with one class
+    // per workgroup they are formed too -- again if the communicator changed where they go)
+    if (h->fused_cls_blocks && h->fused_cls_blocks == block_target(h)) {
+      if (h->comm) {
+        flag_slot_kernel<<<1, 1, 0, h->stream>>>(h->d_uflow, h->d_blk_local + h->comm_stride - 1);
+        HIPCHK(h, hipGetLastError());
+      }
+    } else if (h->fused_cls_blocks) {
+      h->fused_cls_blocks = block_target(h);
+      cls_blocks_kernel<<<(unsigned)h->n_blocks, 1024, 0, h->stream>>>(
+          h->d_cls, h->C, h->n_pad, h->weights, h->site_lnl, h->fused_cls_blocks, h->n_patterns,
+          (int)((h->n_patterns + 63) / 64), (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0,
+          (h->flags & PLK_FLAG_SCALING) ? nullptr : h->d_uflow);
+      HIPCHK(h, hipGetLastError());
+      if (h->comm) flag_slot_kernel<<<1, 1, 0, h->stream>>>(h->d_uflow, h->d_blk_local + h->comm_stride - 1);
+    } else {
+      int rc = launch_block_sums(h);
+      if (rc) return rc;
+    }
   } else {
     if (!h->materialized[root - h->n_tips]) return fail(h, PLK_ERR_STATE, "root %d has no partial", root);
     int rc = launch_root(h, root);

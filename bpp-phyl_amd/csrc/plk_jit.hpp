@@ -54,6 +54,7 @@ struct JArgs {  // codes: one row per table unit (unit_codes_kernel)
   const double* pi; const double* probs; double* site_lnl; double* wave_sums;
   i64 slot_stride; i64 n_pad; i64 n_patterns; i32 n_sblocks; i32 guard;
   unsigned* sb_ctr; i32 dyn; unsigned* exit_ctr; i32* uflow;
+  double* cls_sum;  // workgroups of one class (CLS_): per class and pattern, its root term [C][n_pad]
 };
 
 // Register vectors hold 4 * CW * PW doubles: vector v = pw * CW + cw is class c0 + cw of
@@ -266,6 +267,29 @@ __device__ __forceinline__ void rescale(double (&v)[4 * CW * PW], int (&cnt)[PW]
     }
 }
 
+// One class per workgroup (JitShape::cls): this class's root term of each of the lane's patterns,
+// t_c = (sum_s L[c][s] pi_s, terms <= 0 dropped under the guards) * prob_c -- reduce_root's
+// t[pw][0] -- goes to cls_sum[c][p]; class_sums_to_blocks adds the classes in class order with
+// the guard or clamp, takes the log and forms the block sums as reduce_root + wave_sums_to_blocks.
+template <int PW>
+__device__ __forceinline__ void reduce_root_cls(const JArgs& a, const double (&acc)[4 * PW], int c0, i64 p, bool gv) {
+  if (!gv) return;
+#pragma unroll
+  for (int pw = 0; pw < PW; ++pw) {
+    double lc = 0.0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const double li = acc[4 * pw + s] * a.pi[s];
+      if (a.guard) {
+        if (li > 0.0) lc += li;
+      } else {
+        lc += li;
+      }
+    }
+    a.cls_sum[(i64)c0 * a.n_pad + p + 64 * pw] = lc * a.probs[c0];
+  }
+}
+
 // off: the lane's first pattern in the slot (tile layout); pattern pw is 64 further
 template <int CW, int PW, bool SCALE>
 __device__ __forceinline__ void store(const JArgs& a, int slot, i64 off, i64 p, int c0,
@@ -369,6 +393,7 @@ struct JArgs {
   // the launch's super-block counters and the ticket counter to 0
   unsigned* exit_ctr;
   int32_t* uflow;  // unscaled handles: set to 1 when a site likelihood is < 2^-255 (or null)
+  double* cls_sum;  // JitShape::cls: every class's root term per pattern, [C][n_pad] (class_sums_to_blocks)
 };
 
 struct JitShape {
@@ -385,11 +410,20 @@ struct JitShape {
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
   bool clk = false;         // PLK_DEBUG_CLOCK: per-workgroup shader-clock / constant-clock stamps (diagnostic)
+  // one class per workgroup (grid.z = class): the tables hold that class only (C x smaller, so
+  // a fragment's cherries fit as quad units, JitUnit), and the root terms of the classes meet
+  // in HBM (class_sums_to_blocks) instead of an LDS exchange.  One class per wave, no scaling.
+  bool cls = false;
+  int QT = 0;       // quad build scratch doubles (JitPlan::quad_tmp), in the code rows' LDS
+  int nw() const { return cls ? 1 : C / CW; }  // waves per pattern group
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
-    // the second exchange buffer only serves the per-node rescale
-    return (size_t)std::max(TD, 4) * sizeof(double) + (scale ? 2 : 1) * (size_t)PW * G * (C / CW) * 64 * sizeof(double) +
-           (size_t)G * nt * 64 * PW;
+    // the class exchange (root reduction, per-node rescale; the second buffer only serves the
+    // rescale) -- none with one class per workgroup
+    const size_t xch = cls ? 0 : (scale ? 2 : 1) * (size_t)PW * G * nw() * 64 * sizeof(double);
+    // the code rows' space also holds the quad build's cherry rows before the first super-block
+    return (size_t)std::max(TD, 4) * sizeof(double) + xch +
+           std::max((size_t)G * nt * 64 * PW, (size_t)QT * sizeof(double));
   }
 };
 
@@ -401,7 +435,7 @@ inline int jit_auto_groups(const JitShape& base) {
   for (int g = 1; g <= 4; ++g) {
     JitShape t = base;
     t.G = g;
-    const int waves_wg = (t.C / t.CW) * g;
+    const int waves_wg = t.nw() * g;
     const int by_lds = (int)((160 * 1024) / std::max<size_t>(t.lds_bytes(), 1));
     const int by_vgpr = (4 * 7) / waves_wg;
     const int waves = std::min(by_lds, by_vgpr) * waves_wg;
@@ -433,11 +467,20 @@ struct JitEvent {
 // With rescaling, the cherry's joint check depends on its row alone: the row is rescaled
 // before the product exactly as the kernel would, and its count (0 / 1) is kept in U * U
 // bytes at koff, added to the parent's count with the contribution.
+// A quad (one class per workgroup, no scaling) goes one level further: a node Q whose two
+// children are unstored cherries (a, b) and (c, d), itself not stored, is one unit whose rows
+// hold Q's contribution to its parent, quad[((ca U + cb) U + cc) U + cd][x] =
+// sum_y P_Q[x][y] (contA[ca U + cb][y] * contB[cc U + cd][y]) with contA / contB the cherries'
+// contribution rows -- the operations of the interpreter in its order (Q's accumulator is
+// contA, then *= contB; then contrib), read with one combined code (U^4 <= 256).  A 4-tip
+// subtree then costs one LDS row read instead of two reads, 4 multiplies and a 4x4 matvec.
 struct JitUnit {
   int ta, tb;
   int off;
   int br = -1;    // >= 0: contribution unit through P of node br
   int koff = -1;  // rescaling contribution unit: doubles offset of its count bytes
+  int tc = -1, td = -1;    // quad: tips of the second cherry (ta, tb: the first)
+  int brA = -1, brB = -1;  // quad: the two cherry nodes (br: the quad node Q)
 };
 
 struct JitPlan {
@@ -445,18 +488,23 @@ struct JitPlan {
   std::vector<std::vector<JitUnit> > units;    // per fragment: its tables, in event order
   int NU = 0;           // most units of any fragment
   int tab_doubles = 0;  // most table doubles of any fragment
+  int quad_tmp = 0;     // most doubles of any fragment's quad build scratch (its cherries' rows)
 };
 
 // Per fragment: its events with TIP events renumbered to fragment-local table units.
 // Cherries become pair units while the fragment's tables stay within pair_budget
 // doubles (0: no pairs; pairs need U * U <= 256 so that a combined code is one byte).
+// cls: one class per workgroup (tables of one class); quad_budget > 0 (doubles, cls only): pairs
+// of unstored cherries under an unstored node become quad units while the tables fit.
 inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32_t>& starts, int C, int U,
-                        int pair_budget, bool scale) {
+                        int pair_budget, bool scale, bool cls = false, int quad_budget = 0) {
   JitPlan plan;
   plan.events.assign(starts.size(), {});
   plan.units.assign(starts.size(), {});
+  const int CT = cls ? 1 : C;  // classes in the tables
   const bool pairs = pair_budget > 0 && U * U <= 256;
-  const int single = C * U * 4, grow = C * U * 4 * (U - 1);
+  const bool quads = cls && !scale && pairs && quad_budget > 0 && U * U * U * U <= 256;
+  const int single = CT * U * 4, grow = CT * U * 4 * (U - 1), pair = CT * U * U * 4, quad = CT * U * U * U * U * 4;
   for (size_t f = 0; f < starts.size(); ++f) {
     std::vector<JitEvent>& ev = plan.events[f];
     std::vector<JitUnit>& un = plan.units[f];
@@ -497,6 +545,29 @@ inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32
           ev.push_back({T_TIP, d, k, w.b});
           continue;
         }
+        auto cherry_unit = [&](size_t i) {  // event i: a contribution unit of an unstored cherry at level d
+          if (ev[i].op != T_TIP || ev[i].level != d) return false;
+          const JitUnit& u = un[(size_t)ev[i].a];
+          return u.tb >= 0 && u.br >= 0 && u.tc < 0 && u.koff < 0;
+        };
+        if (quads && w.a < 0 && w.b >= 0 && n >= 3 && cherry_unit(n - 1) && cherry_unit(n - 2) &&
+            ev[n - 3].op == T_DESCEND && ev[n - 3].level == d && ev[n - 1].a == (int)un.size() - 1 &&
+            total + quad - 2 * pair <= quad_budget) {
+          // a quad: the node's two children are unstored cherries, the node is not stored
+          const int k1 = ev[n - 2].a, k2 = ev[n - 1].a;
+          JitUnit& q = un[(size_t)k1];
+          q.tc = un[(size_t)k2].ta;
+          q.td = un[(size_t)k2].tb;
+          q.brA = q.br;
+          q.brB = un[(size_t)k2].br;
+          q.br = w.b;
+          un.pop_back();
+          total += quad - 2 * pair;
+          ev.resize(n - 3);
+          --d;
+          ev.push_back({T_TIP, d, k1, w.b});
+          continue;
+        }
         ev.push_back({T_ASCEND, d, w.a, w.b});
         --d;
       } else if (w.op == T_ROOT) {
@@ -507,7 +578,7 @@ inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32
     int off = 0;
     for (JitUnit& u : un) {
       u.off = off;
-      off += u.tb < 0 ? single : C * U * U * 4;
+      off += u.tb < 0 ? single : u.tc >= 0 ? quad : pair;
       if (u.koff >= 0) {
         u.koff = off;
         off += (U * U + 31) / 32 * 4;  // count bytes, whole 32-byte rows
@@ -515,6 +586,9 @@ inline JitPlan jit_plan(const std::vector<TInstr>& prog, const std::vector<int32
     }
     plan.NU = std::max(plan.NU, (int)un.size());
     plan.tab_doubles = std::max(plan.tab_doubles, off);
+    int nq = 0;
+    for (const JitUnit& u : un) nq += u.tc >= 0;
+    plan.quad_tmp = std::max(plan.quad_tmp, 2 * nq * U * U * 4);
   }
   return plan;
 }
@@ -545,6 +619,10 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   std::string sc = "};\n__device__ const int kFragScStart[] = {0", scu = "};\n__device__ const int kScUnit[] = {0",
               ot = "};\n__device__ const int kFragOtherStart[] = {0",
               otu = "};\n__device__ const UnitD kOtherD[] = {{0, 0, 0, 0, 0, 0, 0, 0}";
+  // quad units (JitUnit): their own list (kQuadD, CSR kFragQuadStart), staged one row per thread
+  std::string qs = "};\nstruct QuadD { int ta, tb, tc, td, brA, brB, brQ, off; };\n"
+                   "__device__ const int kFragQuadStart[] = {0",
+              qd = "};\n__device__ const QuadD kQuadD[] = {{0, 0, 0, 0, 0, 0, 0, 0}";
   {
     // the P(t) matrices each fragment reads (CSR kFragPStart / kFragPBr), touched at launch
     std::string st = "\n__device__ const int kFragPStart[] = {0", br = "};\n__device__ const int kFragPBr[] = {0";
@@ -613,7 +691,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   }
   s += "\n__device__ const int kFragUnitStart[] = {0";
   {
-    int acc = 0, nsc = 0, not_ = 0;
+    int acc = 0, nsc = 0, not_ = 0, nq = 0;
     for (const auto& un : plan.units) {
       acc += (int)un.size();
       snprintf(buf, sizeof(buf), ",%d", acc);
@@ -623,7 +701,11 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         snprintf(buf, sizeof(buf), ",{%d,%d,%d,%d,%d,0,0,0}", u.ta, u.tb, u.off, u.br, u.koff);
         ud += buf;
         snprintf(buf, sizeof(buf), ",%zu", k);
-        if (sh.scale && u.tb >= 0 && u.koff >= 0) {
+        if (u.tc >= 0) {
+          snprintf(buf, sizeof(buf), ",{%d,%d,%d,%d,%d,%d,%d,%d}", u.ta, u.tb, u.tc, u.td, u.brA, u.brB, u.br, u.off);
+          qd += buf;
+          ++nq;
+        } else if (sh.scale && u.tb >= 0 && u.koff >= 0) {
           scu += buf;
           ++nsc;
         } else {
@@ -636,10 +718,14 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       sc += buf;
       snprintf(buf, sizeof(buf), ",%d", not_);
       ot += buf;
+      snprintf(buf, sizeof(buf), ",%d", nq);
+      qs += buf;
     }
   }
-  s += ud + sc + scu + ot + otu + "};\n";
-  const int CW = sh.CW, NW = C / CW, PW = sh.PW;
+  s += ud + sc + scu + ot + otu + qs + qd + "};\n";
+  const int CW = sh.CW, NW = sh.nw(), PW = sh.PW;
+  snprintf(buf, sizeof(buf), "#define CLS_ %d\n#define CT_ %d\n", sh.cls ? 1 : 0, sh.cls ? 1 : C);
+  s += buf;
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
            "#define U_ %d\n#define NT_ %d\n#define TD_ %d\n#define SC_ %s\n#define V_ (4 * CW_ * PW_)\n"
@@ -656,11 +742,15 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   double* tab = lds;                                          // units: [C_][U_ or U_ * U_][4] each
   double* xch = tab + TD_;                                    // [2][PW_][NWT_][64] (rescale alternates)
   double* xch2 = xch + PW_ * NWT_ * 64;
-  u8* code_lds = reinterpret_cast<u8*>(xch + (SC_ ? 2 : 1) * PW_ * NWT_ * 64); // [G_][NT_][64 * PW_]
+  u8* code_lds = reinterpret_cast<u8*>(xch + (CLS_ ? 0 : (SC_ ? 2 : 1) * PW_ * NWT_ * 64)); // [G_][NT_][64 * PW_]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c0 = (w % NW_) * CW_, g = w / NW_;
+  // (CLS_: the workgroup's class is blockIdx.z; TC0_ = the class of table class 0)
+  const int c0 = CLS_ ? (int)blockIdx.z : (w % NW_) * CW_, g = w / NW_;
+  const int TC0_ = CLS_ ? c0 : 0;
   const int frag = frag_base + (int)blockIdx.y;
+  // dynamic super-block counter of this fragment (and class)
+  unsigned* const sbc_ = a.sb_ctr + frag * (int)gridDim.z + (int)blockIdx.z;
   const int u0 = 1 + kFragUnitStart[frag], nu = kFragUnitStart[frag + 1] - kFragUnitStart[frag];
   // code staging: this thread's items (uint4 column j of group gg in unit k's code row;
   // JArgs::codes holds one row per unit, unit_codes_kernel), fixed over the super-blocks.
@@ -743,15 +833,15 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     if (ko + NWT_ < not_) ud_nx = kOtherD[ot0 + ko + NWT_];
     const int ta = ud.ta, tb = ud.tb;
     double* dst = tab + ud.off;
-    const double* ra = a.tipP + (i64)ta * (C_ * U_ * 4);
+    const double* ra = a.tipP + (i64)ta * (C_ * U_ * 4) + TC0_ * (U_ * 4);
     if (tb < 0) {
-      for (int i = lane; i < C_ * U_ * 4; i += 64) dst[i] = ra[i];
+      for (int i = lane; i < CT_ * U_ * 4; i += 64) dst[i] = ra[i];
     } else {
-      const double* rb = a.tipP + (i64)tb * (C_ * U_ * 4);
+      const double* rb = a.tipP + (i64)tb * (C_ * U_ * 4) + TC0_ * (U_ * 4);
       const int br = ud.br;  // (rescaling contribution units were staged above)
       // one row (class c, code pair ca, cb: 4 doubles) per lane, its operands loaded
       // together (16-byte loads), so a unit costs one load latency, not one per double
-      for (int r = lane; r < C_ * U_ * U_; r += 64) {
+      for (int r = lane; r < CT_ * U_ * U_; r += 64) {
         const int c = r / (U_ * U_), q = r - c * (U_ * U_), ca = q / U_, cb = q - ca * U_;
         const double2* pa = reinterpret_cast<const double2*>(ra + (c * U_ + ca) * 4);
         const double2* pb = reinterpret_cast<const double2*>(rb + (c * U_ + cb) * 4);
@@ -762,7 +852,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
           o[0] = make_double2(v[0], v[1]);
           o[1] = make_double2(v[2], v[3]);
         } else {  // contrib<.., true>: the same operations in the same order
-          const double2* P2 = reinterpret_cast<const double2*>(pmats + ((i64)br * C_ + c) * 16);
+          const double2* P2 = reinterpret_cast<const double2*>(pmats + ((i64)br * C_ + TC0_ + c) * 16);
           double P[16];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -784,10 +874,69 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       }
     }
   }
+  if (CLS_) {
+    // quad units: one (unit, row) per thread of the workgroup.  The interpreter's operations
+    // in its order: each cherry's pair product and contrib<.., true> through the cherry's P,
+    // Q's accumulator = contA, *= contB, then contrib<.., true> through P_Q.
+    constexpr int U4_ = U_ * U_ * U_ * U_;
+    const int q0_ = 1 + kFragQuadStart[frag], nq_ = kFragQuadStart[frag + 1] - kFragQuadStart[frag];
+    auto pcon = [&](int br_, const double (&v_)[4], double (&t_)[4]) {
+      const double2* P2 = reinterpret_cast<const double2*>(pmats + ((i64)br_ * C_ + c0) * 16);
+      double P[16];
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) { const double2 pj = P2[j]; P[2 * j] = pj.x; P[2 * j + 1] = pj.y; }
+      _Pragma("unroll") for (int x = 0; x < 4; ++x) {
+        t_[x] = P[4 * x] * v_[0];
+        t_[x] = __builtin_fma(P[4 * x + 1], v_[1], t_[x]);
+        t_[x] = __builtin_fma(P[4 * x + 2], v_[2], t_[x]);
+        t_[x] = __builtin_fma(P[4 * x + 3], v_[3], t_[x]);
+      }
+    };
+    auto prow = [&](int t1_, int k1_, int t2_, int k2_, double (&v_)[4]) {
+      const double2* pa = reinterpret_cast<const double2*>(a.tipP + ((i64)t1_ * C_ + c0) * (U_ * 4) + k1_ * 4);
+      const double2* pb = reinterpret_cast<const double2*>(a.tipP + ((i64)t2_ * C_ + c0) * (U_ * 4) + k2_ * 4);
+      const double2 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+      v_[0] = a0.x * b0.x; v_[1] = a0.y * b0.y; v_[2] = a1.x * b1.x; v_[3] = a1.y * b1.y;
+    };
+    // phase 1: the two cherries' contribution rows of every quad (U^2 rows each), in the code
+    // rows' LDS space (staged only at the first super-block); phase 2: the quad rows from them
+    double* qtmp = reinterpret_cast<double*>(code_lds);
+    for (int t = threadIdx.x; t < nq_ * 2 * (U_ * U_); t += 64 * NWT_) {
+      const int kk = t / (2 * U_ * U_), hr = t - kk * (2 * U_ * U_), which = hr / (U_ * U_), r = hr - which * (U_ * U_);
+      const QuadD qd_ = kQuadD[q0_ + kk];
+      const int ca = r / U_, cb = r - ca * U_;
+      double v[4], o[4];
+      if (which == 0) {
+        prow(qd_.ta, ca, qd_.tb, cb, v);
+        pcon(qd_.brA, v, o);
+      } else {
+        prow(qd_.tc, ca, qd_.td, cb, v);
+        pcon(qd_.brB, v, o);
+      }
+      double2* od = reinterpret_cast<double2*>(qtmp + (i64)t * 4);
+      od[0] = make_double2(o[0], o[1]);
+      od[1] = make_double2(o[2], o[3]);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < nq_ * U4_; t += 64 * NWT_) {
+      const int kk = t / U4_, r = t - kk * U4_;
+      const QuadD qd_ = kQuadD[q0_ + kk];
+      const int ab = r / (U_ * U_), cd = r - ab * (U_ * U_);
+      const double2* pa = reinterpret_cast<const double2*>(qtmp + ((i64)(2 * kk) * (U_ * U_) + ab) * 4);
+      const double2* pb = reinterpret_cast<const double2*>(qtmp + ((i64)(2 * kk + 1) * (U_ * U_) + cd) * 4);
+      const double2 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+      double acc[4] = {a0.x, a0.y, a1.x, a1.y}, o[4];
+      acc[0] *= b0.x; acc[1] *= b0.y; acc[2] *= b1.x; acc[3] *= b1.y;
+      pcon(qd_.brQ, acc, o);
+      double2* od = reinterpret_cast<double2*>(tab + qd_.off + (i64)r * 4);
+      od[0] = make_double2(o[0], o[1]);
+      od[1] = make_double2(o[2], o[3]);
+    }
+  }
   const CPd pm = (CPd)(pmats + c0 * 16);
-  const double* trow = tab + c0 * (U_ * 4);         // single-tip units
-  const double* trow2 = tab + c0 * (U_ * U_ * 4);   // pair units
-  (void)xch; (void)xch2; (void)trow; (void)trow2;
+  const double* trow = tab + (CLS_ ? 0 : c0 * (U_ * 4));         // single-tip units
+  const double* trow2 = tab + (CLS_ ? 0 : c0 * (U_ * U_ * 4));   // pair units
+  const double* trow4 = tab;                                      // quad units (CLS_ only)
+  (void)xch; (void)xch2; (void)trow; (void)trow2; (void)trow4;
 // unit k: codes of the lane's patterns (4 per int), then their table rows (R rows per
 // class at OFF doubles from the class base TB)
 #define CODEF(Q, k) { Q = 0; _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) \
@@ -820,7 +969,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   __shared__ int sb_next_lds;
   unsigned sb_pend = 0;
   if (a.dyn && threadIdx.x == 0)
-    sb_pend = __hip_atomic_fetch_add(a.sb_ctr + frag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sb_pend = __hip_atomic_fetch_add(sbc_, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int sb = blockIdx.x, sb_nx = 0; sb < a.n_sblocks; sb = sb_nx) {
     const i64 q0 = (i64)sb * (64 * PW_ * G_);
     // super-blocks of G_ groups; in a ragged last one, groups past n_pad recompute group 0
@@ -840,7 +989,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     __syncthreads();
     sb_nx = a.dyn ? __builtin_amdgcn_readfirstlane(sb_next_lds) : sb + (int)gridDim.x;
     if (a.dyn && threadIdx.x == 0 && sb_nx < a.n_sblocks)
-      sb_pend = __hip_atomic_fetch_add(a.sb_ctr + frag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sb_pend = __hip_atomic_fetch_add(sbc_, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     fetch_codes(sb_nx);
 )PLKJIT";
   int max_level = 0;
@@ -886,7 +1035,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     auto unit_args = [&](const JitEvent& e) -> std::string {  // TB, OFF, R of a unit
       const JitUnit& u = plan.units[f][(size_t)e.a];
       char ubuf[96];
-      snprintf(ubuf, sizeof(ubuf), "%s, %d, %d", u.tb < 0 ? "trow" : "trow2", u.off, u.tb < 0 ? U : U * U);
+      snprintf(ubuf, sizeof(ubuf), "%s, %d, %d", u.tb < 0 ? "trow" : u.tc >= 0 ? "trow4" : "trow2", u.off,
+               u.tb < 0 ? U : u.tc >= 0 ? U * U * U * U : U * U);
       return ubuf;
     };
     auto emit_stage2 = [&](int i) {
@@ -1023,7 +1173,9 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
                      sref(e.a).c_str());
             s += buf;
           }
-          if (e.b) s += "      reduce_root<C_, CW_, PW_, NWT_, SC_>(a, A0, K0, xch, w, g, c0, p0, p, gv);\n";
+          if (e.b)
+            s += sh.cls ? "      reduce_root_cls<PW_>(a, A0, c0, p, gv);\n"
+                        : "      reduce_root<C_, CW_, PW_, NWT_, SC_>(a, A0, K0, xch, w, g, c0, p0, p, gv);\n";
         }
       }
     };
@@ -1040,7 +1192,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   s += "    default: break;\n    }\n  }\n";
   if (sh.clk)
     s += "  if (threadIdx.x == 0) {\n"
-         "    unsigned long long* q_ = clk_ + 4 * ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x);\n"
+         "    unsigned long long* q_ = clk_ + 4 * (((unsigned long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + "
+         "blockIdx.x);\n"
          "    const unsigned long long c1_ = clock64(), w1_ = wall_clock64();\n"
          "    q_[0] = clk_c0_; q_[1] = clk_w0_; q_[2] = c1_; q_[3] = w1_;\n  }\n";
   // Exit ticket (dynamic super-blocks): thread 0 of every workgroup takes one ticket after its
@@ -1051,9 +1204,9 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // XCDs' L2s, as sc1 stores and loads or behind L2 write-backs -- profiles/r05/ab_runs.md.)
   s += R"PLKJIT(  if (a.exit_ctr && threadIdx.x == 0) {
     const unsigned t_ = __hip_atomic_fetch_add(a.exit_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t_ == gridDim.x * gridDim.y - 1u) {
-      for (unsigned f_ = 0; f_ < gridDim.y; ++f_)
-        __hip_atomic_store(a.sb_ctr + frag_base + f_, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t_ == gridDim.x * gridDim.y * gridDim.z - 1u) {
+      for (unsigned f_ = 0; f_ < gridDim.y * gridDim.z; ++f_)
+        __hip_atomic_store(a.sb_ctr + frag_base * gridDim.z + f_, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(a.exit_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

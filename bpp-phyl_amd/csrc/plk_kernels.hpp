@@ -1016,15 +1016,19 @@ __global__ __launch_bounds__(256) void tip_table_kernel(const double* __restrict
 // reads codes[ta] (tb < 0) or the combined code codes[ta] * U + codes[tb] of a cherry's
 // product table.  Rebuilt when tip codes or the unit list change, not per evaluation.
 // Bytes are combined four to a word: a byte times U plus a byte < U stays below 256.
+// units[k] = (ta, tb, tc, td): a tip (tb < 0), a cherry (ca U + cb) or a quad
+// (((ca U + cb) U + cc) U + cd, plk_jit.hpp JitUnit); 4 codes per 32-bit word, bytes stay < 256
 __global__ __launch_bounds__(256) void unit_codes_kernel(const uint8_t* __restrict__ codes, int64_t n_pad,
-                                                         const int2* __restrict__ units, int U,
+                                                         const int4* __restrict__ units, int U,
                                                          uint8_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // uint4 index in the row
   if (i * 16 >= n_pad) return;
-  const int2 u = units[blockIdx.y];
+  const int4 u = units[blockIdx.y];
   uint4 v = reinterpret_cast<const uint4*>(codes + (int64_t)u.x * n_pad)[i];
-  if (u.y >= 0) {
-    const uint4 b = reinterpret_cast<const uint4*>(codes + (int64_t)u.y * n_pad)[i];
+  const int more[3] = {u.y, u.z, u.w};
+  for (int k = 0; k < 3; ++k) {
+    if (more[k] < 0) break;
+    const uint4 b = reinterpret_cast<const uint4*>(codes + (int64_t)more[k] * n_pad)[i];
     v.x = v.x * U + b.x;
     v.y = v.y * U + b.y;
     v.z = v.z * U + b.z;
@@ -1055,6 +1059,78 @@ struct RootArgs {
   int guard;               // 1: homogeneous guards, 0: NH clamp
   int32_t* uflow;          // unscaled handles: set to 1 when a site likelihood is < 2^-255 (or null)
 };
+
+// The root reduction of a traversal run with one class per workgroup (plk_jit.hpp, JitShape::cls):
+// cls_sum[c][p] holds each class's term t_c = l_c prob_c (the per-state guards applied); the
+// classes are added in class order with the class-level guard or the NH clamp, then log, the
+// underflow flag, site lnL, the 64-pattern wave sums (the same butterfly) and the 4096-pattern
+// block sum (the same chain of adds as wave_sums_to_blocks) -- reduce_root's and
+// wave_sums_to_blocks' operations in their order, so the block sums are bitwise those of the
+// classes-in-one-workgroup kernel.  One workgroup of 16 waves per block, each wave four of its
+// 64-pattern waves with every load issued before the first log (one memory round trip).
+__global__ __launch_bounds__(1024) void cls_blocks_kernel(const double* __restrict__ cls_sum, int C, int64_t n_pad,
+                                                          const double* __restrict__ weights,
+                                                          double* __restrict__ site_lnl, double* __restrict__ block_sums,
+                                                          int64_t n_patterns, int n_waves, int guard, int32_t* uflow) {
+  constexpr int kW = kRootBlock / 64;  // 64-pattern waves per block
+  constexpr int kPer = kW / 16;        // per hardware wave
+  __shared__ double ws[kW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.x;
+  double l[kPer], wt[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t p = ((int64_t)b * kW + wv + 16 * j) * 64 + lane;
+    l[j] = 0.0;
+    wt[j] = 0.0;
+    if (p < n_pad) {
+      for (int c = 0; c < C; ++c) {
+        const double li = cls_sum[(int64_t)c * n_pad + p];
+        if (guard) {
+          if (li > 0.0) l[j] += li;
+        } else {
+          l[j] += li;
+        }
+      }
+      if (p < n_patterns) wt[j] = weights[p];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = wv + 16 * j;
+    const int64_t p0 = ((int64_t)b * kW + k) * 64, p = p0 + lane;
+    double wr = 0.0;
+    if (p0 < n_pad) {
+      double lj = l[j];
+      if (!guard && lj < 0.0) lj = 0.0;
+      const double r = log(lj);
+      if (p < n_patterns) {
+        if (uflow && !(lj >= 2.0 * kScaleThr)) *uflow = 1;  // plk_root_underflow
+        site_lnl[p] = r;
+        wr = wt[j] * r;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+    }
+    if (lane == 0) ws[k] = wr;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const double v = ws[lane];
+    double s = 0.0;
+    for (int k = 0; k < kW; ++k) {
+      const double x = __shfl(v, k, 64);
+      if (b * kW + k < n_waves) s += x;
+    }
+    if (lane == 0) block_sums[b] = s;
+  }
+}
+
+// Under a communicator: the underflow flag into this rank's exchange record once every block of
+// cls_blocks_kernel has set it (plk_exchange.hpp layout; wave_sums_to_blocks does this itself).
+__global__ void flag_slot_kernel(const int32_t* uflow, double* __restrict__ slot) {
+  *slot = __hip_atomic_load(uflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ? 1.0 : 0.0;
+}
 
 __global__ __launch_bounds__(64) void root_kernel(RootArgs a) {
   const int lane = threadIdx.x;

@@ -3,6 +3,7 @@
 // tests/test_jit_sources.py can cross-compile it for gfx950 with hipcc on a machine without
 // a GPU (the library compiles these sources only at run time, on the device).
 //   jit_emit <tree4|treeM> <C> <scale 0|1> [S (treeM: 20 | 4)] > kernel.hip
+//   jit_emit tree4q <C> 0 > kernel.hip: one class per workgroup with a quad unit (JitShape::cls)
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
@@ -57,6 +58,27 @@ int main(int argc, char** argv) {
   // treeM_deep <height>: one fragment over a balanced subtree of that height (cherries as
   // table rows), i.e. height - 1 register levels below the root -- the register pressure of
   // a real cfg3 fragment (DM 4: height 5)
+  if (kind == "tree4q") {
+    // one fragment, root 11 = (Q 10 = ((t0, t1)8, (t2, t3)9), (t4, t5)7, t6): a quad, a cherry, a tip
+    prog.clear();
+    add(T_DESCEND, 1, 0, 0);
+    add(T_DESCEND, 2, 0, 0);
+    add(T_TIP, 2, 0, 0);
+    add(T_TIP, 2, 1, 1);
+    add(T_ASCEND, 2, -1, 8);
+    add(T_DESCEND, 2, 0, 0);
+    add(T_TIP, 2, 2, 2);
+    add(T_TIP, 2, 3, 3);
+    add(T_ASCEND, 2, -1, 9);
+    add(T_ASCEND, 1, -1, 10);
+    add(T_DESCEND, 1, 0, 0);
+    add(T_TIP, 1, 4, 4);
+    add(T_TIP, 1, 5, 5);
+    add(T_ASCEND, 1, -1, 7);
+    add(T_TIP, 0, 6, 6);
+    add(T_ROOT, 0, -1, 1);
+    starts = {0};
+  }
   if (kind == "treeM_deep") {
     prog.clear();
     const int height = argc > 5 ? std::atoi(argv[5]) : 5;
@@ -92,9 +114,21 @@ int main(int argc, char** argv) {
     sh.CW = argc > 5 && std::atoi(argv[5]) ? C : 1;
     sh.U = 16;
     sh.scale = scale;
-    const JitPlan plan = jit_plan(prog, starts, sh.C, sh.U, 64 * 1024 / 8, scale);
+    sh.cls = kind == "tree4q";
+    if (sh.cls) sh.U = 4;
+    const JitPlan plan = sh.cls ? jit_plan(prog, starts, sh.C, sh.U, 136 * 1024 / 8, false, true, 136 * 1024 / 8)
+                                : jit_plan(prog, starts, sh.C, sh.U, 64 * 1024 / 8, scale);
+    if (sh.cls) {
+      int nq = 0;
+      for (const JitUnit& u : plan.units[0]) nq += u.tc >= 0;
+      if (nq != 1) {
+        std::fprintf(stderr, "expected one quad unit, got %d\n", nq);
+        return 1;
+      }
+    }
     sh.NT = plan.NU;
     sh.TD = plan.tab_doubles;
+    sh.QT = plan.quad_tmp;
     sh.G = 1;
     sh.PW = 1;
     sh.L = sh.CW > 1 ? 2 : 3;

@@ -720,6 +720,50 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     check(l1, s1, lo, so)
 
 
+@pytest.mark.parametrize("C,tree_kind,n_patterns,guard,tune", [
+    (4, "balanced64", 3000, True, ""), (4, "balanced64", 777, False, ""), (2, "balanced64", 5000, True, "JIT_G=8"),
+    (1, "balanced64", 1500, True, ""), (4, "balanced64", 4100, True, "JIT_QUAD_KB=40"),
+    (4, "balanced300", 2000, True, ""), (2, "balanced64", 600, True, "JIT_G=3"), (4, "caterpillar40", 900, True, ""),
+    (4, "random120", 2500, True, ""), (2, "balanced64", 70000, True, "")])
+def test_jit_tree4_quads_bitwise(C, tree_kind, n_patterns, guard, tune, monkeypatch):
+    """One class per workgroup with quad units (plk_jit.hpp JitUnit / JitShape::cls: a node whose
+    two children are unstored cherries is one table of U^4 rows, the classes' root terms meet in
+    cls_root_kernel): lnL, per-pattern lnL and block sums bitwise those of the interpreter
+    (tree4_kernel) and of the classes-in-one-workgroup kernel without quads (JIT_QUAD_KB=0), on
+    balanced, multi-tier, caterpillar (no quads) and random trees, a partial quad budget, both
+    root rules; the oracle at 1e-12.  ACGT data (4 codes in use: U^4 = 256 rows)."""
+    if tree_kind.startswith("balanced"):
+        tree = phylo.balanced_tree(int(tree_kind[8:]), seed=23, lo=0.05, hi=0.4)
+    elif tree_kind.startswith("random"):
+        tree = _random_topology(int(tree_kind[6:]), np.random.default_rng(5), 0.05, 0.4, poly=0.0)
+    else:
+        tree = _caterpillar(int(tree_kind[11:]), seed=5)
+    et = phylo.engine_tree(tree)
+    rng = np.random.default_rng(C * 13 + n_patterns)
+    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
+    rates, probs = phylo.gamma_rates(C, 0.5) if C > 1 else (np.ones(1), np.ones(1))
+    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, False, True, 5)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    flags = (plk.PLK_FLAG_NONNEG_GUARD if guard else 0) | plk.PLK_FLAG_LNL_ONLY
+    res = {}
+    for name, extra in (("quads", ""), ("noquads", "JIT_QUAD_KB=0"), ("interp", "JIT=0")):
+        monkeypatch.setenv("PLK_TUNE", ",".join(x for x in (tune.replace(" ", ","), extra) if x))
+        eng = engine_for(et, 4, C, n_patterns, states, phylo.DNA.init_table, rates, probs, m.pi, [m], flags=flags)
+        lnl, site, blocks = run_engine(eng, et)
+        lnl2, site2, blocks2 = run_engine(eng, et)    # a second evaluation: the counters reset
+        assert lnl2 == lnl and np.array_equal(site2, site) and np.array_equal(blocks2, blocks)
+        res[name] = (lnl, site, blocks, eng.traversal_work()["table_nodes"], eng.kernel_path())
+        eng.close()
+    (lq, sq, bq, tq, pq), (ln, sn, bn, tn, pn), (li, si, bi, ti, pi_) = res["quads"], res["noquads"], res["interp"]
+    assert pq == pn == "jit_tree4" and pi_ == "tree4"
+    assert lq == ln == li and np.array_equal(sq, sn) and np.array_equal(sq, si)
+    assert np.array_equal(bq, bn) and np.array_equal(bq, bi)
+    if not tree_kind.startswith("caterpillar"):
+        assert tq > tn   # quads replace three table nodes each where cherries replaced one
+    lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m])
+    check(lq, sq, lo, so)   # (positive partials: both root rules are the same sum here)
+
+
 @pytest.mark.parametrize("C,n_taxa,n_patterns,scaling", [(4, 64, 320_000, False), (4, 512, 60_000, True)])
 def test_jit_tree4_dynamic_superblocks_bitwise(C, n_taxa, n_patterns, scaling, monkeypatch):
     """Dynamic super-blocks (workgroups take super-blocks from a per-fragment counter once

@@ -28,13 +28,15 @@ def emitter(tmp_path_factory):
 
 
 @pytest.mark.parametrize("args", [
-    ("tree4", "4", "0"), ("tree4", "4", "1", "0", "1"), ("tree4", "1", "1"),
+    ("tree4", "4", "0"), ("tree4", "4", "1", "0", "1"), ("tree4", "1", "1"), ("tree4q", "4", "0"), ("tree4q", "2", "0"),
     ("treeM", "4", "1", "20"), ("treeM", "1", "0", "20"), ("treeM", "4", "0", "4"),
     ("treeM_deep", "4", "1", "20", "5")])
 def test_emitted_kernel_compiles_for_gfx950(emitter, args):
     exe, d = emitter
     src = subprocess.run([exe, *args], check=True, capture_output=True, timeout=60).stdout.decode()
     name = "plk_jit_treeM" if args[0].startswith("treeM") else "plk_jit_tree4"
+    if args[0] == "tree4q":
+        assert "kQuadD[] = {{0, 0, 0, 0, 0, 0, 0, 0},{0,1,2,3,8,9,10," in src   # the quad unit's record
     assert f"void {name}(" in src
     path = d / ("k_" + "_".join(args) + ".hip")
     # hiprtc includes the HIP device runtime implicitly; hipcc needs the header
