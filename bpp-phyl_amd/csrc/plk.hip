@@ -2162,6 +2162,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.NT = h->jit_plan.NU;
     sh.TD = h->jit_plan.tab_doubles;
     sh.QT = h->jit_plan.quad_tmp;
+    sh.soa = tune_int("JIT_SOA", 1, 0, 1) != 0;
+    sh.ps1 = tune_int("JIT_PS1", 0, 0, 1) != 0;
     // pattern groups per workgroup (they share the staged tables): with per-node rescaling
     // and one class per wave every node has two workgroup barriers, whose cost grows with
     // the waves that meet there (cfg5: 1.93 ms at G = 2, 1.16 ms at G = 1), so one group;
@@ -2206,7 +2208,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
         sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.clk != h->jit_shape.clk ||
-        sh.cls != h->jit_shape.cls) {
+        sh.cls != h->jit_shape.cls || sh.soa != h->jit_shape.soa || sh.ps1 != h->jit_shape.ps1) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;

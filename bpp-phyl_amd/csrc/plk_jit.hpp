@@ -179,6 +179,8 @@ __device__ __forceinline__ unsigned long long launder_s(unsigned long long x) {
   asm volatile("" : "+s"(x));
   return x;
 }
+// Table element x of row r (R rows per class block): [row][4] or, with SOA_, [half][row][2]
+#define TABIX(R, r, x) (SOA_ ? ((x) >> 1) * ((R) * 2) + (r) * 2 + ((x) & 1) : (r) * 4 + (x))
 __device__ __forceinline__ unsigned long long launder_v(unsigned long long x) {
   asm volatile("" : "+v"(x));
   return x;
@@ -415,6 +417,10 @@ struct JitShape {
   // in HBM (class_sums_to_blocks) instead of an LDS exchange.  One class per wave, no scaling.
   bool cls = false;
   int QT = 0;       // quad build scratch doubles (JitPlan::quad_tmp), in the code rows' LDS
+  // table rows as two planes of 16-byte halves ([half][row] per class) instead of 32-byte rows:
+  // a ds_read_b128 of random rows then spreads over all 16 four-bank windows, not 8
+  bool soa = false;
+  bool ps1 = false;  // one class per wave: the P(t) stream (contrib_s) too
   int nw() const { return cls ? 1 : C / CW; }  // waves per pattern group
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
@@ -724,7 +730,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   }
   s += ud + sc + scu + ot + otu + qs + qd + "};\n";
   const int CW = sh.CW, NW = sh.nw(), PW = sh.PW;
-  snprintf(buf, sizeof(buf), "#define CLS_ %d\n#define CT_ %d\n", sh.cls ? 1 : 0, sh.cls ? 1 : C);
+  snprintf(buf, sizeof(buf), "#define CLS_ %d\n#define CT_ %d\n#define SOA_ %d\n", sh.cls ? 1 : 0, sh.cls ? 1 : C,
+           sh.soa ? 1 : 0);
   s += buf;
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
@@ -815,7 +822,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
           t2 = __builtin_fma(P[1], v[c][1], t2);
           t2 = __builtin_fma(P[2], v[c][2], t2);
           t2 = __builtin_fma(P[3], v[c][3], t2);
-          dst[(c * U_ * U_ + r) * 4 + x] = t2;
+          dst[c * (U_ * U_ * 4) + TABIX(U_ * U_, r, x)] = t2;
         }
       }
       reinterpret_cast<u8*>(tab + ud.koff)[r] = up ? 1 : 0;
@@ -835,7 +842,10 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     double* dst = tab + ud.off;
     const double* ra = a.tipP + (i64)ta * (C_ * U_ * 4) + TC0_ * (U_ * 4);
     if (tb < 0) {
-      for (int i = lane; i < CT_ * U_ * 4; i += 64) dst[i] = ra[i];
+      for (int i = lane; i < CT_ * U_ * 4; i += 64) {
+        const int c = i / (U_ * 4), q = i - c * (U_ * 4);
+        dst[c * (U_ * 4) + TABIX(U_, q >> 2, q & 3)] = ra[i];
+      }
     } else {
       const double* rb = a.tipP + (i64)tb * (C_ * U_ * 4) + TC0_ * (U_ * 4);
       const int br = ud.br;  // (rescaling contribution units were staged above)
@@ -847,10 +857,11 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         const double2* pb = reinterpret_cast<const double2*>(rb + (c * U_ + cb) * 4);
         const double2 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
         double v[4] = {a0.x * b0.x, a0.y * b0.y, a1.x * b1.x, a1.y * b1.y};
-        double2* o = reinterpret_cast<double2*>(dst + (i64)r * 4);
+        double2* o0 = reinterpret_cast<double2*>(dst + c * (U_ * U_ * 4) + TABIX(U_ * U_, q, 0));
+        double2* o1 = reinterpret_cast<double2*>(dst + c * (U_ * U_ * 4) + TABIX(U_ * U_, q, 2));
         if (br < 0) {
-          o[0] = make_double2(v[0], v[1]);
-          o[1] = make_double2(v[2], v[3]);
+          *o0 = make_double2(v[0], v[1]);
+          *o1 = make_double2(v[2], v[3]);
         } else {  // contrib<.., true>: the same operations in the same order
           const double2* P2 = reinterpret_cast<const double2*>(pmats + ((i64)br * C_ + TC0_ + c) * 16);
           double P[16];
@@ -868,8 +879,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
             t[x] = __builtin_fma(P[4 * x + 2], v[2], t[x]);
             t[x] = __builtin_fma(P[4 * x + 3], v[3], t[x]);
           }
-          o[0] = make_double2(t[0], t[1]);
-          o[1] = make_double2(t[2], t[3]);
+          *o0 = make_double2(t[0], t[1]);
+          *o1 = make_double2(t[2], t[3]);
         }
       }
     }
@@ -927,9 +938,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       double acc[4] = {a0.x, a0.y, a1.x, a1.y}, o[4];
       acc[0] *= b0.x; acc[1] *= b0.y; acc[2] *= b1.x; acc[3] *= b1.y;
       pcon(qd_.brQ, acc, o);
-      double2* od = reinterpret_cast<double2*>(tab + qd_.off + (i64)r * 4);
-      od[0] = make_double2(o[0], o[1]);
-      od[1] = make_double2(o[2], o[3]);
+      *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, r, 0)) = make_double2(o[0], o[1]);
+      *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, r, 2)) = make_double2(o[2], o[3]);
     }
   }
   const CPd pm = (CPd)(pmats + c0 * 16);
@@ -942,10 +952,10 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
 #define CODEF(Q, k) { Q = 0; _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) \
     Q |= (int)crow[(k) * (64 * PW_) + 64 * pw_] << (8 * pw_); }
 #define ROWF(F, TB, OFF, R, Q) { _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
-    const double* r0_ = TB + (OFF) + (((Q) >> (8 * pw_)) & 255) * 4; \
+    const double* r0_ = TB + (OFF) + TABIX(R, ((Q) >> (8 * pw_)) & 255, 0); \
     _Pragma("unroll") for (int cw_ = 0; cw_ < CW_; ++cw_) { \
       const double2* r_ = reinterpret_cast<const double2*>(r0_ + cw_ * ((R) * 4)); \
-      const double2 x_ = r_[0], y_ = r_[1]; const int v_ = 4 * (pw_ * CW_ + cw_); \
+      const double2 x_ = r_[0], y_ = r_[SOA_ ? (R) : 1]; const int v_ = 4 * (pw_ * CW_ + cw_); \
       F[v_] = x_.x; F[v_ + 1] = x_.y; F[v_ + 2] = y_.x; F[v_ + 3] = y_.y; } } }
 #define TIPF(F, Q, k, TB, OFF, R) { CODEF(Q, k) ROWF(F, TB, OFF, R, Q) }
 // count bytes of a rescaling contribution unit
@@ -1061,7 +1071,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     // every check, no rescale would happen, and this pass IS the exact result.
     // classes in the wave with pipelined P(t): the fragment's contributions form one
     // stream of class loads (contrib_s), the first loaded ahead of the body
-    const bool pstream = sh.ppipe && CW > 1;
+    const bool pstream = sh.ppipe && (CW > 1 || sh.ps1);
     std::vector<size_t> cev;  // events with a contribution, in order
     for (size_t i = 0; i < ev.size(); ++i)
       if (ev[i].op == T_LOAD || ev[i].op == T_ASCEND) cev.push_back(i);

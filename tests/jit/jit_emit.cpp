@@ -129,6 +129,7 @@ int main(int argc, char** argv) {
     sh.NT = plan.NU;
     sh.TD = plan.tab_doubles;
     sh.QT = plan.quad_tmp;
+    sh.soa = std::getenv("JIT_EMIT_SOA") != nullptr;
     sh.G = 1;
     sh.PW = 1;
     sh.L = sh.CW > 1 ? 2 : 3;
