@@ -433,6 +433,82 @@ static void unscaledFirstCase() {
   if (mismatches || def.getEvaluationStats().scaledFallbacks != 0 || def.underflowScalingActive()) failures++;
 }
 
+// The NH mirror (RNonHomogeneousTreeLikelihood: NH root rule, no non-negative guards) on a
+// 64-taxon rooted tree with per-branch T92 theta: unscaled first, no fallback, every value equal
+// to the forced-scaling engine's bitwise, through branch-length and model-parameter changes
+// (the clear-flag proof on the NH path)
+static void unscaledFirstNhCase() {
+  const int n = 64, L = 300;
+  std::string nwk;
+  {
+    std::vector<std::string> level;
+    unsigned long long x = 991;
+    auto len = [&]() {
+      x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+      return std::to_string(0.02 + 0.08 * (double)((x >> 33) & 0xffff) / 65536.0);
+    };
+    for (int i = 0; i < n; i++) level.push_back("t" + std::to_string(i));
+    while (level.size() > 1) {
+      std::vector<std::string> next;
+      for (size_t i = 0; i + 1 < level.size(); i += 2)
+        next.push_back("(" + level[i] + ":" + len() + "," + level[i + 1] + ":" + len() + ")");
+      level = next;
+    }
+    nwk = level[0] + ";";
+  }
+  std::unique_ptr<TreeTemplate<Node> > tree(TreeTemplateTools::parenthesisToTree(nwk));
+  const NucleicAlphabet* dna = &AlphabetTools::DNA_ALPHABET;
+  VectorSiteContainer aln(dna);
+  unsigned long long x = 5151;
+  for (int i = 0; i < n; i++) {
+    std::string s;
+    for (int j = 0; j < L; j++) {
+      x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+      s += "ACGT"[(x >> 33) & 3];
+    }
+    aln.addSequence(BasicSequence("t" + std::to_string(i), s, dna));
+  }
+  std::map<std::string, std::vector<Vint> > globals;
+  globals["T92.kappa"] = {};
+  std::map<std::string, std::string> alias;
+  // one model set per likelihood: a set shared by two would report a parameter change only to
+  // the first of them (matchParametersValues), as in the reference
+  std::unique_ptr<SubstitutionModelSet> sets[2];
+  for (auto& set : sets) {
+    set.reset(SubstitutionModelSetTools::createNonHomogeneousModelSet(new T92(dna, 3.), new GCFrequencySet(dna),
+                                                                       tree.get(), alias, globals));
+    for (size_t k = 0; k < set->getNumberOfModels(); k++)
+      set->setParameterValue("T92.theta_" + std::to_string(k + 1), 0.3 + 0.4 * (double)(k % 7) / 6.0);
+  }
+  GammaDiscreteRateDistribution rdist(4, 0.8);
+  RNonHomogeneousTreeLikelihood def(*tree, aln, sets[0].get(), &rdist, false);
+  def.initialize();
+  RNonHomogeneousTreeLikelihood on(*tree, aln, sets[1].get(), &rdist, false);
+  on.setUnderflowScaling(true);
+  on.initialize();
+  int mismatches = def.getValue() != on.getValue();
+  ParameterList bl = def.getBranchLengthsParameters();
+  for (int k = 1; k <= 3; k++) {
+    for (size_t i = 0; i < bl.size(); i++) bl[i].setValue(bl[i].getValue() * (1.0 + 0.1 * k));
+    def.setParameters(bl);
+    on.setParameters(bl);
+    mismatches += def.getValue() != on.getValue();
+  }
+  // a root-frequency parameter (GC.theta) and a branch model's theta
+  for (const char* key : {"GC.theta", "T92.theta_3"}) {
+    ParameterList th = def.getParameters();
+    for (size_t i = 0; i < th.size(); i++)
+      if (th[i].getName() == key) th[i].setValue(0.45);
+    def.setParameters(th);
+    on.setParameters(th);
+    mismatches += def.getValue() != on.getValue();
+  }
+  std::cout << std::setprecision(17) << "NH 64 taxa: default -lnL " << def.getValue() << ", scaling on "
+            << on.getValue() << ", fallbacks " << def.getEvaluationStats().scaledFallbacks << ", bitwise mismatches "
+            << mismatches << std::endl;
+  if (mismatches || def.getEvaluationStats().scaledFallbacks != 0 || def.underflowScalingActive()) failures++;
+}
+
 int main() {
   try {
     unrootedGammaCase();
@@ -444,6 +520,7 @@ int main() {
     gapCase();
     shortBranchScalingCase();
     unscaledFirstCase();
+    unscaledFirstNhCase();
   } catch (Exception& e) {
     std::cerr << e.what() << std::endl;
     return 1;
