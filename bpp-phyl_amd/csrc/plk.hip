@@ -343,6 +343,11 @@ struct plk_handle_s {
   double* d_cls = nullptr;              // JitShape::cls: every class's root term, [C][n_pad]
   size_t d_cls_cap = 0;
   double* fused_cls_blocks = nullptr;   // the last traversal formed its block sums here (cls_blocks_kernel)
+  uint8_t* d_ucodes_dc = nullptr;       // JitShape::dc: [fragment][pattern][16] unit codes
+  size_t ucodes_dc_cap = 0;
+  bool ucodes_dc_valid = false;
+  int32_t* d_units_start = nullptr;     // CSR of the plan's units per fragment (unit_codes_dc_kernel)
+  size_t units_start_cap = 0;
   uint8_t* d_ucodes = nullptr;  // code row of every table unit of jit_plan (unit_codes_kernel)
   int4* d_units = nullptr;      // (ta, tb) of every unit
   size_t ucodes_cap = 0, units_cap = 0;
@@ -1142,7 +1147,7 @@ int plk_destroy(plk_handle h) {
                   h->d_ops, h->wave_sums, h->d_links, h->d_opsl, h->d_prog, h->d_frag, h->d1_sums,
                   h->d2_sums, h->d_dprog, h->pmatsT, h->d_ucodes, h->d_units, h->d_cherry3,
                   h->d_cherry_tips, h->d_cherry, h->d_drb, h->d_drm, h->dr_blk, h->dr_out, h->d_drpre, h->d_sbctr,
-                  h->d_cherry_rows, h->d_kidsl, h->d_cls};
+                  h->d_cherry_rows, h->d_kidsl, h->d_cls, h->d_ucodes_dc, h->d_units_start};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (h->h_req) (void)hipHostFree(h->h_req);
@@ -2158,11 +2163,30 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         HIPCHK(h, hipStreamSynchronize(h->stream));  // `units` goes out of scope
       }
       h->ucodes_valid = true;
+      h->ucodes_dc_valid = false;
     }
     sh.NT = h->jit_plan.NU;
     sh.TD = h->jit_plan.tab_doubles;
     sh.QT = h->jit_plan.quad_tmp;
     sh.soa = tune_int("JIT_SOA", 1, 0, 1) != 0;
+    // direct codes where a fragment has at most 16 units (cfg2, 0.099 vs 0.111 ms traversal)
+    sh.dc = sh.cls && sh.NT <= 16 && tune_int("JIT_DC", 1, 0, 1) != 0;
+    if (sh.dc && !h->ucodes_dc_valid) {
+      const int nfr = (int)h->jit_plan.units.size();
+      std::vector<int32_t> us(1, 0);
+      for (const auto& un : h->jit_plan.units) us.push_back(us.back() + (int)un.size());
+      int rc = ensure_cap(h, (void**)&h->d_ucodes_dc, &h->ucodes_dc_cap, (size_t)nfr * h->n_pad * 16);
+      if (!rc) rc = ensure_cap(h, (void**)&h->d_units_start, &h->units_start_cap, us.size() * sizeof(int32_t));
+      if (rc) return rc;
+      HIPCHK(h, hipMemcpyAsync(h->d_units_start, us.data(), us.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                               h->stream));
+      const dim3 dg((unsigned)((h->n_pad + 255) / 256), (unsigned)nfr);
+      hipLaunchKernelGGL(unit_codes_dc_kernel, dg, dim3(256), 0, h->stream, h->d_ucodes, h->n_pad, h->d_units_start,
+                         reinterpret_cast<uint4*>(h->d_ucodes_dc));
+      HIPCHK(h, hipGetLastError());
+      HIPCHK(h, hipStreamSynchronize(h->stream));  // `us` goes out of scope
+      h->ucodes_dc_valid = true;
+    }
     sh.ps1 = tune_int("JIT_PS1", 0, 0, 1) != 0;
     // pattern groups per workgroup (they share the staged tables): with per-node rescaling
     // and one class per wave every node has two workgroup barriers, whose cost grows with
@@ -2172,7 +2196,10 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // with the tier's fragments side by side: G = 6 / 7 / 8 = 0.48 / 0.43 / 0.39 ms);
     // otherwise the G with the most resident waves (jit_auto_groups; cfg2 with cherry
     // tables: G = 3, 0.140 ms, G = 2 0.150, G = 4 0.162)
-    sh.PW = tune_int("JIT_PW", 1, 1, 2);  // (before G: the code rows take G x PW)
+    // (before G: the code rows take G x PW).  With direct codes (one class per workgroup, no code
+    // rows in LDS) two patterns per lane: twice the independent work per wave at four waves
+    // per SIMD (cfg2 traversal 0.093 vs 0.099 ms)
+    sh.PW = tune_int("JIT_PW", sh.dc ? 2 : 1, 1, 2);
     sh.G = tune_int("JIT_G", 0, 0, 16);
     if (sh.G == 0) {
       if (sh.cls) {
@@ -2184,6 +2211,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.G = h->prog_ciw ? 8 : sh.scale ? 1 : jit_auto_groups(sh);
       }
     }
+    sh.G = std::max(1, std::min(sh.G, 1024 / (64 * sh.nw())));  // (a JIT_G past 1024 threads)
     // two patterns per lane halve the P(t) reads per FMA but double the registers:
     // measured slower (cfg2 0.255-0.301 vs 0.241 ms), so opt-in; not with speculation
     // two-stage pipeline, codes / HBM loads 3 ahead (cfg2 0.274 -> 0.259 ms); with every
@@ -2208,7 +2236,8 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
         sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.clk != h->jit_shape.clk ||
-        sh.cls != h->jit_shape.cls || sh.soa != h->jit_shape.soa || sh.ps1 != h->jit_shape.ps1) {
+        sh.cls != h->jit_shape.cls || sh.soa != h->jit_shape.soa || sh.ps1 != h->jit_shape.ps1 ||
+        sh.dc != h->jit_shape.dc) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
@@ -2216,7 +2245,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     }
     ja.partials = a.partials;
     ja.scale = a.scale;
-    ja.codes = h->d_ucodes;
+    ja.codes = sh.dc ? h->d_ucodes_dc : h->d_ucodes;
     ja.tipP = h->tipP;
     ja.weights = a.weights;
     ja.pi = a.pi;

@@ -179,6 +179,8 @@ __device__ __forceinline__ unsigned long long launder_s(unsigned long long x) {
   asm volatile("" : "+s"(x));
   return x;
 }
+// component j of a uint4 (j a constant)
+__device__ __forceinline__ unsigned cvw(const uint4& v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
 // Table element x of row r (R rows per class block): [row][4] or, with SOA_, [half][row][2]
 #define TABIX(R, r, x) (SOA_ ? ((x) >> 1) * ((R) * 2) + (r) * 2 + ((x) & 1) : (r) * 4 + (x))
 __device__ __forceinline__ unsigned long long launder_v(unsigned long long x) {
@@ -421,6 +423,10 @@ struct JitShape {
   // a ds_read_b128 of random rows then spreads over all 16 four-bank windows, not 8
   bool soa = false;
   bool ps1 = false;  // one class per wave: the P(t) stream (contrib_s) too
+  // direct codes (cls, at most 16 units per fragment): every wave loads its own patterns' unit
+  // codes, 16 bytes per pattern ([fragment][pattern][16], unit_codes_dc_kernel), into
+  // registers one super-block ahead -- no code rows in LDS and one barrier per super-block
+  bool dc = false;
   int nw() const { return cls ? 1 : C / CW; }  // waves per pattern group
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
@@ -429,7 +435,7 @@ struct JitShape {
     const size_t xch = cls ? 0 : (scale ? 2 : 1) * (size_t)PW * G * nw() * 64 * sizeof(double);
     // the code rows' space also holds the quad build's cherry rows before the first super-block
     return (size_t)std::max(TD, 4) * sizeof(double) + xch +
-           std::max((size_t)G * nt * 64 * PW, (size_t)QT * sizeof(double));
+           std::max(dc ? (size_t)0 : (size_t)G * nt * 64 * PW, (size_t)QT * sizeof(double));
   }
 };
 
@@ -730,8 +736,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   }
   s += ud + sc + scu + ot + otu + qs + qd + "};\n";
   const int CW = sh.CW, NW = sh.nw(), PW = sh.PW;
-  snprintf(buf, sizeof(buf), "#define CLS_ %d\n#define CT_ %d\n#define SOA_ %d\n", sh.cls ? 1 : 0, sh.cls ? 1 : C,
-           sh.soa ? 1 : 0);
+  snprintf(buf, sizeof(buf), "#define CLS_ %d\n#define CT_ %d\n#define SOA_ %d\n#define DC_ %d\n", sh.cls ? 1 : 0,
+           sh.cls ? 1 : C, sh.soa ? 1 : 0, sh.dc ? 1 : 0);
   s += buf;
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
@@ -779,7 +785,17 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     _Pragma("unroll") for (int m = 0; m < NI_; ++m)
       if (q0_ + ic_[m] < a.n_pad) va_[m] = ucodes[iu_[m] + (q0_ >> 4)];
   };
-  fetch_codes(blockIdx.x);  // (issued before the table staging below: its loads overlap it)
+  // DC_: this wave's own patterns' codes (16 unit bytes per pattern), next super-block's
+  uint4 cv_[PW_], cvn_[PW_];
+  const uint4* dcodes = reinterpret_cast<const uint4*>(a.codes) + (i64)frag * a.n_pad;
+  auto fetch_dc = [&](int sb_) {
+    const i64 q0_ = (i64)sb_ * (64 * PW_ * G_);
+    const i64 pp_ = (q0_ + g * (64 * PW_) < a.n_pad ? q0_ + g * (64 * PW_) : q0_) + lane;
+    if (sb_ < a.n_sblocks) _Pragma("unroll") for (int pw = 0; pw < PW_; ++pw) cvn_[pw] = dcodes[pp_ + 64 * pw];
+  };
+  (void)cv_; (void)cvn_; (void)dcodes;
+  // (issued before the table staging below: its loads overlap it)
+  if (DC_) fetch_dc(blockIdx.x); else fetch_codes(blockIdx.x);
   // The fragment's P(t) matrices, touched with wide loads while the tables stage: the
   // traversal reads P(t) through scalar loads one contribution ahead, and their first touch
   // (the P(t) launch wrote them through another XCD's L2) made the first super-block ~12 us
@@ -950,7 +966,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
 // unit k: codes of the lane's patterns (4 per int), then their table rows (R rows per
 // class at OFF doubles from the class base TB)
 #define CODEF(Q, k) { Q = 0; _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) \
-    Q |= (int)crow[(k) * (64 * PW_) + 64 * pw_] << (8 * pw_); }
+    Q |= (DC_ ? (int)((cvw(cv_[pw_], (k) >> 2) >> (8 * ((k) & 3))) & 255) : (int)crow[(k) * (64 * PW_) + 64 * pw_]) << (8 * pw_); }
 #define ROWF(F, TB, OFF, R, Q) { _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
     const double* r0_ = TB + (OFF) + TABIX(R, ((Q) >> (8 * pw_)) & 255, 0); \
     _Pragma("unroll") for (int cw_ = 0; cw_ < CW_; ++cw_) { \
@@ -976,8 +992,9 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   // hidden; a workgroup stops taking after its first index past the end.  The counter starts
   // the launch at 0 (the exit ticket below resets it).  Which workgroup computes a
   // super-block does not change its results.
-  __shared__ int sb_next_lds;
+  __shared__ int sb_next_lds[2];  // (DC_: alternating, one barrier per super-block)
   unsigned sb_pend = 0;
+  int it_ = 0;
   if (a.dyn && threadIdx.x == 0)
     sb_pend = __hip_atomic_fetch_add(sbc_, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int sb = blockIdx.x, sb_nx = 0; sb < a.n_sblocks; sb = sb_nx) {
@@ -987,20 +1004,27 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     const bool gv = q0 + g * (64 * PW_) < a.n_pad;
     const i64 p0 = gv ? q0 + g * (64 * PW_) : q0, p = p0 + lane;
     const u8* crow = code_lds + (gv ? g : 0) * (NT_ * 64 * PW_) + lane;
+    (void)crow;
     const i64 toff = (p >> 7) * (C_ * 4 * kTile) + (i64)c0 * 4 * kTile + (p & (kTile - 1));
     (void)toff;
-    __syncthreads();  // the previous super-block is done with code_lds / xch (and tab is staged)
-    _Pragma("unroll") for (int m = 0; m < NI_; ++m)
-      if (q0 + ic_[m] < a.n_pad) reinterpret_cast<uint4*>(code_lds)[il_[m]] = va_[m];
+    const int sl_ = DC_ ? (it_ & 1) : 0;
+    if (DC_) {
+      _Pragma("unroll") for (int pw = 0; pw < PW_; ++pw) cv_[pw] = cvn_[pw];
+    } else {
+      __syncthreads();  // the previous super-block is done with code_lds / xch (and tab is staged)
+      _Pragma("unroll") for (int m = 0; m < NI_; ++m)
+        if (q0 + ic_[m] < a.n_pad) reinterpret_cast<uint4*>(code_lds)[il_[m]] = va_[m];
+    }
     if (a.dyn && threadIdx.x == 0) {  // (an index outside this launch's range ends the loop)
       const unsigned d_ = sb_pend;
-      sb_next_lds = d_ < (unsigned)(a.n_sblocks - (int)gridDim.x) ? (int)gridDim.x + (int)d_ : a.n_sblocks;
+      sb_next_lds[sl_] = d_ < (unsigned)(a.n_sblocks - (int)gridDim.x) ? (int)gridDim.x + (int)d_ : a.n_sblocks;
     }
-    __syncthreads();
-    sb_nx = a.dyn ? __builtin_amdgcn_readfirstlane(sb_next_lds) : sb + (int)gridDim.x;
+    __syncthreads();  // (DC_: also the tables' staging before the first super-block)
+    sb_nx = a.dyn ? __builtin_amdgcn_readfirstlane(sb_next_lds[sl_]) : sb + (int)gridDim.x;
+    ++it_;
     if (a.dyn && threadIdx.x == 0 && sb_nx < a.n_sblocks)
       sb_pend = __hip_atomic_fetch_add(sbc_, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    fetch_codes(sb_nx);
+    if (DC_) fetch_dc(sb_nx); else fetch_codes(sb_nx);
 )PLKJIT";
   int max_level = 0;
   for (const auto& ev : events)

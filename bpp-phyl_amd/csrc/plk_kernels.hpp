@@ -1060,6 +1060,20 @@ struct RootArgs {
   int32_t* uflow;          // unscaled handles: set to 1 when a site likelihood is < 2^-255 (or null)
 };
 
+// Direct-code layout of the generated 4-state kernel (plk_jit.hpp JitShape::dc): fragment f's
+// unit codes of pattern p as 16 bytes, byte k = unit k (at most 16 units), from the per-unit
+// rows of unit_codes_kernel.  units_start: CSR of the fragments' units (n_frag + 1 entries).
+__global__ __launch_bounds__(256) void unit_codes_dc_kernel(const uint8_t* __restrict__ rows, int64_t n_pad,
+                                                            const int32_t* __restrict__ units_start,
+                                                            uint4* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pad) return;
+  const int f = blockIdx.y, u0 = units_start[f], nu = units_start[f + 1] - u0;
+  unsigned w[4] = {0u, 0u, 0u, 0u};
+  for (int k = 0; k < nu && k < 16; ++k) w[k >> 2] |= (unsigned)rows[(int64_t)(u0 + k) * n_pad + p] << (8 * (k & 3));
+  out[(int64_t)f * n_pad + p] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // The root reduction of a traversal run with one class per workgroup (plk_jit.hpp, JitShape::cls):
 // cls_sum[c][p] holds each class's term t_c = l_c prob_c (the per-state guards applied); the
 // classes are added in class order with the class-level guard or the NH clamp, then log, the

@@ -130,6 +130,7 @@ int main(int argc, char** argv) {
     sh.TD = plan.tab_doubles;
     sh.QT = plan.quad_tmp;
     sh.soa = std::getenv("JIT_EMIT_SOA") != nullptr;
+    sh.dc = sh.cls && std::getenv("JIT_EMIT_DC") != nullptr;
     sh.G = 1;
     sh.PW = 1;
     sh.L = sh.CW > 1 ? 2 : 3;

@@ -724,14 +724,18 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     (4, "balanced64", 3000, True, ""), (4, "balanced64", 777, False, ""), (2, "balanced64", 5000, True, "JIT_G=8"),
     (1, "balanced64", 1500, True, ""), (4, "balanced64", 4100, True, "JIT_QUAD_KB=40"),
     (4, "balanced300", 2000, True, ""), (2, "balanced64", 600, True, "JIT_G=3"), (4, "caterpillar40", 900, True, ""),
-    (4, "random120", 2500, True, ""), (2, "balanced64", 70000, True, "")])
+    (4, "random120", 2500, True, ""), (2, "balanced64", 70000, True, ""),
+    # staged code rows and one pattern per lane (the shapes before direct codes)
+    (4, "balanced64", 3000, True, "JIT_DC=0 JIT_PW=1"), (2, "balanced300", 2000, True, "JIT_DC=0"),
+    (4, "balanced64", 5000, False, "JIT_PW=1"), (4, "balanced64", 9000, True, "JIT_G=5")])
 def test_jit_tree4_quads_bitwise(C, tree_kind, n_patterns, guard, tune, monkeypatch):
     """One class per workgroup with quad units (plk_jit.hpp JitUnit / JitShape::cls: a node whose
     two children are unstored cherries is one table of U^4 rows, the classes' root terms meet in
     cls_root_kernel): lnL, per-pattern lnL and block sums bitwise those of the interpreter
     (tree4_kernel) and of the classes-in-one-workgroup kernel without quads (JIT_QUAD_KB=0), on
     balanced, multi-tier, caterpillar (no quads) and random trees, a partial quad budget, both
-    root rules; the oracle at 1e-12.  ACGT data (4 codes in use: U^4 = 256 rows)."""
+    root rules, direct codes (DC, two patterns per lane: the default) and staged code rows; the
+    oracle at 1e-12.  ACGT data (4 codes in use: U^4 = 256 rows)."""
     if tree_kind.startswith("balanced"):
         tree = phylo.balanced_tree(int(tree_kind[8:]), seed=23, lo=0.05, hi=0.4)
     elif tree_kind.startswith("random"):
