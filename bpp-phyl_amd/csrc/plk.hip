@@ -880,6 +880,7 @@ int root_finish_c(plk_handle h, double* lnl, double* block_sums);
 
 namespace {
 double* block_target(plk_handle h);
+void launch_cls_blocks(plk_handle h, int guard, int32_t* uflow);
 
 // The root reductions of an unscaled handle flag a site likelihood below 2^-255 (or <= 0, or
 // NaN) in mapped host memory (plk_root_underflow); a scaled handle's reductions see rescaled
@@ -2379,9 +2380,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         // the classes' root terms meet here: log, site lnL, wave and block sums (the work of
         // reduce_root and wave_sums_to_blocks), inside the traversal's timing
         h->fused_cls_blocks = block_target(h);
-        cls_blocks_kernel<<<(unsigned)h->n_blocks, 1024, 0, h->stream>>>(
-            h->d_cls, h->C, h->n_pad, h->weights, h->site_lnl, h->fused_cls_blocks, h->n_patterns,
-            (int)((h->n_patterns + 63) / 64), ja.guard, ja.uflow);
+        launch_cls_blocks(h, ja.guard, ja.uflow);
       }
     } else if (jitm) {
       int base = first;
@@ -3760,6 +3759,21 @@ __global__ void comm_copy_kernel(const double* __restrict__ all, int64_t n_all, 
 // block sums land in mapped host memory, or in the all-gather's send buffer under a communicator
 double* block_target(plk_handle h) { return h->comm ? h->d_blk_local : h->block_sums; }
 
+// The classes' root terms of a one-class-per-workgroup traversal -> site lnL and block sums
+// (cls_blocks_kernel) into h->fused_cls_blocks
+void launch_cls_blocks(plk_handle h, int guard, int32_t* uflow) {
+  const int n_waves = (int)((h->n_patterns + 63) / 64);
+  const dim3 g((unsigned)h->n_blocks), b(1024);
+  switch (h->C) {
+    case 1: cls_blocks_kernel<1><<<g, b, 0, h->stream>>>(h->d_cls, h->n_pad, h->weights, h->site_lnl,
+                                                        h->fused_cls_blocks, h->n_patterns, n_waves, guard, uflow); break;
+    case 2: cls_blocks_kernel<2><<<g, b, 0, h->stream>>>(h->d_cls, h->n_pad, h->weights, h->site_lnl,
+                                                        h->fused_cls_blocks, h->n_patterns, n_waves, guard, uflow); break;
+    default: cls_blocks_kernel<4><<<g, b, 0, h->stream>>>(h->d_cls, h->n_pad, h->weights, h->site_lnl,
+                                                         h->fused_cls_blocks, h->n_patterns, n_waves, guard, uflow);
+  }
+}
+
 // The fixed-order 4096-pattern block sums of the wave sums; under a communicator also the
 // underflow flag into this rank's exchange record (plk_exchange.hpp layout).
 int launch_block_sums(plk_handle h) {
@@ -3789,10 +3803,8 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
       }
     } else if (h->fused_cls_blocks) {
       h->fused_cls_blocks = block_target(h);
-      cls_blocks_kernel<<<(unsigned)h->n_blocks, 1024, 0, h->stream>>>(
-          h->d_cls, h->C, h->n_pad, h->weights, h->site_lnl, h->fused_cls_blocks, h->n_patterns,
-          (int)((h->n_patterns + 63) / 64), (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0,
-          (h->flags & PLK_FLAG_SCALING) ? nullptr : h->d_uflow);
+      launch_cls_blocks(h, (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0,
+                        (h->flags & PLK_FLAG_SCALING) ? nullptr : h->d_uflow);
       HIPCHK(h, hipGetLastError());
       if (h->comm) flag_slot_kernel<<<1, 1, 0, h->stream>>>(h->d_uflow, h->d_blk_local + h->comm_stride - 1);
     } else {

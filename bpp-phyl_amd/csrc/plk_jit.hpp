@@ -290,7 +290,7 @@ __device__ __forceinline__ void reduce_root_cls(const JArgs& a, const double (&a
         lc += li;
       }
     }
-    a.cls_sum[(i64)c0 * a.n_pad + p + 64 * pw] = lc * a.probs[c0];
+    __builtin_nontemporal_store(lc * a.probs[c0], a.cls_sum + (i64)c0 * a.n_pad + p + 64 * pw);
   }
 }
 
@@ -945,7 +945,9 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     }
     __syncthreads();
     for (int t = threadIdx.x; t < nq_ * U4_; t += 64 * NWT_) {
-      const int kk = t / U4_, r = t - kk * U4_;
+      // (U4_ a multiple of 64: the wave's rows belong to one quad, so its record and P(t) are
+      // wave-uniform -- scalar loads)
+      const int kk = U4_ % 64 == 0 ? __builtin_amdgcn_readfirstlane(t / U4_) : t / U4_, r = t - kk * U4_;
       const QuadD qd_ = kQuadD[q0_ + kk];
       const int ab = r / (U_ * U_), cd = r - ab * (U_ * U_);
       const double2* pa = reinterpret_cast<const double2*>(qtmp + ((i64)(2 * kk) * (U_ * U_) + ab) * 4);
