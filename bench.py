@@ -190,7 +190,7 @@ def cpu_baseline(wl, n_sample: int, runs: int, eng_sites=None):
 
 FP64_PEAK_TFS = 78.6   # MI355X fp64 peak, vector and matrix alike (AMD spec sheet; the guide lists no fp64 row)
 RIDGE = FP64_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop/B
-TRAFFIC_FILES = ("profiles/r05/close/traffic.json", "profiles/r05/final/traffic.json", "profiles/r04/final/traffic.json", "profiles/r03/final/traffic.json", "profiles/r03/traffic.json", "profiles/r02/traffic.json", "profiles/traffic.json")
+TRAFFIC_FILES = ("profiles/r06/final/traffic.json", "profiles/r05/close/traffic.json", "profiles/r05/final/traffic.json", "profiles/r04/final/traffic.json", "profiles/r03/final/traffic.json", "profiles/r03/traffic.json", "profiles/r02/traffic.json", "profiles/traffic.json")
 
 
 def measured_traffic(config, mode, P):

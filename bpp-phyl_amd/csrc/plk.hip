@@ -343,6 +343,7 @@ struct plk_handle_s {
   double* d_cls = nullptr;              // JitShape::cls: every class's root term, [C][n_pad]
   size_t d_cls_cap = 0;
   double* fused_cls_blocks = nullptr;   // the last traversal formed its block sums here (cls_blocks_kernel)
+  bool cls_site_written = false;        // ... and its per-pattern lnL (only when asked for: 8 B per pattern)
   uint8_t* d_ucodes_dc = nullptr;       // JitShape::dc: [fragment][pattern][16] unit codes
   size_t ucodes_dc_cap = 0;
   bool ucodes_dc_valid = false;
@@ -880,7 +881,7 @@ int root_finish_c(plk_handle h, double* lnl, double* block_sums);
 
 namespace {
 double* block_target(plk_handle h);
-void launch_cls_blocks(plk_handle h, int guard, int32_t* uflow);
+void launch_cls_blocks(plk_handle h, int guard, int32_t* uflow, bool site);
 
 // The root reductions of an unscaled handle flag a site likelihood below 2^-255 (or <= 0, or
 // NaN) in mapped host memory (plk_root_underflow); a scaled handle's reductions see rescaled
@@ -2380,7 +2381,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         // the classes' root terms meet here: log, site lnL, wave and block sums (the work of
         // reduce_root and wave_sums_to_blocks), inside the traversal's timing
         h->fused_cls_blocks = block_target(h);
-        launch_cls_blocks(h, ja.guard, ja.uflow);
+        launch_cls_blocks(h, ja.guard, ja.uflow, false);
       }
     } else if (jitm) {
       int base = first;
@@ -3761,15 +3762,18 @@ double* block_target(plk_handle h) { return h->comm ? h->d_blk_local : h->block_
 
 // The classes' root terms of a one-class-per-workgroup traversal -> site lnL and block sums
 // (cls_blocks_kernel) into h->fused_cls_blocks
-void launch_cls_blocks(plk_handle h, int guard, int32_t* uflow) {
+// (site: also the per-pattern lnL -- an evaluation that returns only the lnL skips those stores)
+void launch_cls_blocks(plk_handle h, int guard, int32_t* uflow, bool site) {
   const int n_waves = (int)((h->n_patterns + 63) / 64);
   const dim3 g((unsigned)h->n_blocks), b(1024);
+  double* sl = site ? h->site_lnl : nullptr;
+  h->cls_site_written = site;
   switch (h->C) {
-    case 1: cls_blocks_kernel<1><<<g, b, 0, h->stream>>>(h->d_cls, h->n_pad, h->weights, h->site_lnl,
+    case 1: cls_blocks_kernel<1><<<g, b, 0, h->stream>>>(h->d_cls, h->n_pad, h->weights, sl,
                                                         h->fused_cls_blocks, h->n_patterns, n_waves, guard, uflow); break;
-    case 2: cls_blocks_kernel<2><<<g, b, 0, h->stream>>>(h->d_cls, h->n_pad, h->weights, h->site_lnl,
+    case 2: cls_blocks_kernel<2><<<g, b, 0, h->stream>>>(h->d_cls, h->n_pad, h->weights, sl,
                                                         h->fused_cls_blocks, h->n_patterns, n_waves, guard, uflow); break;
-    default: cls_blocks_kernel<4><<<g, b, 0, h->stream>>>(h->d_cls, h->n_pad, h->weights, h->site_lnl,
+    default: cls_blocks_kernel<4><<<g, b, 0, h->stream>>>(h->d_cls, h->n_pad, h->weights, sl,
                                                          h->fused_cls_blocks, h->n_patterns, n_waves, guard, uflow);
   }
 }
@@ -3796,15 +3800,16 @@ int root_launch(plk_handle h, int root, double* site_lnl) {
   if (h->fused_lnl_valid && h->fused_lnl_root == root) {
     // the fused traversal already reduced the root: only the block sums remain (with one class
     // per workgroup they are formed too -- again if the communicator changed where they go)
-    if (h->fused_cls_blocks && h->fused_cls_blocks == block_target(h)) {
+    if (h->fused_cls_blocks && h->fused_cls_blocks == block_target(h) && (h->cls_site_written || !site_lnl)) {
       if (h->comm) {
         flag_slot_kernel<<<1, 1, 0, h->stream>>>(h->d_uflow, h->d_blk_local + h->comm_stride - 1);
         HIPCHK(h, hipGetLastError());
       }
     } else if (h->fused_cls_blocks) {
+      // again: block sums to the communicator's buffer, or the per-pattern lnL asked for
       h->fused_cls_blocks = block_target(h);
       launch_cls_blocks(h, (h->flags & PLK_FLAG_NONNEG_GUARD) ? 1 : 0,
-                        (h->flags & PLK_FLAG_SCALING) ? nullptr : h->d_uflow);
+                        (h->flags & PLK_FLAG_SCALING) ? nullptr : h->d_uflow, site_lnl != nullptr);
       HIPCHK(h, hipGetLastError());
       if (h->comm) flag_slot_kernel<<<1, 1, 0, h->stream>>>(h->d_uflow, h->d_blk_local + h->comm_stride - 1);
     } else {

@@ -1127,7 +1127,7 @@ __global__ __launch_bounds__(1024) void cls_blocks_kernel(const double* __restri
       const double r = log(lj);
       if (p < n_patterns) {
         if (uflow && !(lj >= 2.0 * kScaleThr)) *uflow = 1;  // plk_root_underflow
-        site_lnl[p] = r;
+        if (site_lnl) site_lnl[p] = r;
         wr = wt[j] * r;
       }
 #pragma unroll

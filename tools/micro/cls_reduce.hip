@@ -1,0 +1,126 @@
+// Micro-benchmark of the class-sum root reduction of the one-class-per-workgroup 4-state
+// traversal (plk_kernels.hpp cls_blocks_kernel): C = 4 class terms per pattern -> log, site
+// lnL, weighted sums, 4096-pattern block sums, at 1M patterns.  Variants:
+//   0: cls_blocks_kernel's shape (1024 threads per block, 4 pattern-waves per wave)
+//   1: 0 without the log (memory floor of the same access pattern)
+//   2: 0 without the site lnL stores
+//   3: 256-thread blocks, one pattern-wave per wave, wave sums to HBM (no block sums)
+//   4: pure streaming read of the same bytes (sum only)
+// hipcc -O3 --offload-arch=gfx950 -o cls_reduce cls_reduce.hip
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      std::printf("%s failed: %s\n", #x, hipGetErrorString(e_));               \
+      return 1;                                                                \
+    }                                                                          \
+  } while (0)
+
+constexpr int kBlock = 4096;
+
+template <int V>
+__global__ __launch_bounds__(1024) void red1024(const double* __restrict__ cls, int64_t n_pad, const double* __restrict__ w,
+                                                double* __restrict__ site, double* __restrict__ blocks, int64_t n) {
+  constexpr int kW = kBlock / 64, kPer = kW / 16, C = 4;
+  __shared__ double ws[kW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, b = blockIdx.x;
+  double t[kPer][C], wt[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t p = ((int64_t)b * kW + wv + 16 * j) * 64 + lane;
+#pragma unroll
+    for (int c = 0; c < C; ++c) t[j][c] = cls[(int64_t)c * n_pad + p];
+    wt[j] = w[p];
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = wv + 16 * j;
+    const int64_t p = ((int64_t)b * kW + k) * 64 + lane;
+    double l = 0.0;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (t[j][c] > 0.0) l += t[j][c];
+    const double r = V == 1 ? l : log(l);
+    if (V != 2 && p < n) site[p] = r;
+    double wr = wt[j] * r;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+    if (lane == 0) ws[k] = wr;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const double v = ws[lane];
+    double s = 0.0;
+    for (int k = 0; k < kW; ++k) s += __shfl(v, k, 64);
+    if (lane == 0) blocks[b] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void red256(const double* __restrict__ cls, int64_t n_pad, const double* __restrict__ w,
+                                              double* __restrict__ site, double* __restrict__ wsums, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64, p = p0 + lane;
+  double l = 0.0;
+  double t[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) t[c] = cls[(int64_t)c * n_pad + p];
+  const double wt = w[p];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (t[c] > 0.0) l += t[c];
+  const double r = log(l);
+  if (p < n) site[p] = r;
+  double wr = wt * r;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+  if (lane == 0) wsums[p0 >> 6] = wr;
+}
+
+__global__ __launch_bounds__(256) void stream(const double* __restrict__ cls, int64_t total, double* __restrict__ out) {
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+    s += cls[i];
+  if (s == 12345.0) out[0] = s;
+}
+
+int main() {
+  const int64_t n = 1000000, n_pad = (n + kBlock - 1) / kBlock * kBlock;
+  const int nb = (int)(n_pad / kBlock);
+  double *cls, *w, *site, *blocks, *wsums;
+  CK(hipMalloc(&cls, 4 * n_pad * 8));
+  CK(hipMalloc(&w, n_pad * 8));
+  CK(hipMalloc(&site, n_pad * 8));
+  CK(hipMalloc(&blocks, nb * 8));
+  CK(hipMalloc(&wsums, n_pad / 64 * 8));
+  std::vector<double> h(4 * n_pad, 0.1);
+  CK(hipMemcpy(cls, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(w, h.data(), n_pad * 8, hipMemcpyHostToDevice));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int v = 0; v < 5; ++v) {
+    auto run = [&]() {
+      if (v == 0) red1024<0><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 1) red1024<1><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 2) red1024<2><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 3) red256<<<(unsigned)(n_pad / 256), 256>>>(cls, n_pad, w, site, wsums, n);
+      if (v == 4) stream<<<1024, 256>>>(cls, 5 * n_pad, site);
+    };
+    for (int i = 0; i < 20; ++i) run();
+    CK(hipEventRecord(a));
+    const int reps = 200;
+    for (int i = 0; i < reps; ++i) run();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::printf("variant %d: %.2f us per launch\n", v, ms * 1000.0 / reps);
+  }
+  return 0;
+}

@@ -18,7 +18,7 @@ from collections import OrderedDict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PARTIALS = ("tree4_kernel", "treeS_kernel", "treeM_kernel", "partials_", "plk_jit_tree4", "plk_jit_treeM",
-            "cherry_table_kernel")  # partials_links_ included
+            "cherry_table_kernel", "cls_blocks_kernel")  # partials_links_ included
 
 
 def rows(d):
@@ -53,6 +53,10 @@ def main():
     bench = json.load(open(os.path.join(src, "bench.json")))
     # the traversal's launches plus the table builds that feed it (cherry_table_kernel)
     n_launch = int(round(bench["partials_launches_per_step"] + bench.get("table_launches_per_step", 0)))
+    # one class per workgroup: the classes' root reduction (cls_blocks_kernel) is part of the
+    # traversal (inside its HIP events), one launch after it
+    if any("cls_blocks_kernel" in n for n, _ in per_dispatch(rows(os.path.join(src, "fetch"))).values()):
+        n_launch += 1
     P = bench["config"]["patterns_per_gpu"]
     fetch = last_traversal(per_dispatch(rows(os.path.join(src, "fetch"))), n_launch)
     write = last_traversal(per_dispatch(rows(os.path.join(src, "write"))), n_launch)
