@@ -105,7 +105,7 @@ def parse():
                          "subtree: per-subtree pattern compression (reference usePatterns=true) -- value is then "
                          "an EFFECTIVE rate (SURVEY 8d), reported beside the computed updates")
     args = ap.parse_args()
-    if args.clock_json:
+    if args.clock_json and os.environ.get("PLK_DEBUG_CLOCK") != "2":  # (2: stamps end at the prologue)
         os.environ["PLK_DEBUG_CLOCK"] = "1"
     if args.config is None:
         args.config = "nh_gtr_g4_dna_2M_512" if args.scaling == "strong" else "gtr_g4_dna_1M_64"

@@ -5,12 +5,15 @@
 //   1: 0 without the log (memory floor of the same access pattern)
 //   2: 0 without the site lnL stores
 //   3: 256-thread blocks, one pattern-wave per wave, wave sums to HBM (no block sums)
-//   4: pure streaming read of the same bytes (sum only)
-// hipcc -O3 --offload-arch=gfx950 -o cls_reduce cls_reduce.hip
+//   4: pure streaming read of the class terms (sum only)
+//   5: 0 with the block chain read from LDS (broadcast reads, then the 64 adds)
+//   6: 0 without the block chain (wave sums left in LDS)
+// hipcc -O3 --offload-arch=gfx950 -o cls_reduce cls_reduce.hip; ./cls_reduce [patterns]
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #define CK(x)                                                                  \
@@ -54,6 +57,19 @@ __global__ __launch_bounds__(1024) void red1024(const double* __restrict__ cls, 
     if (lane == 0) ws[k] = wr;
   }
   __syncthreads();
+  if (V == 6) return;
+  if (V == 5) {  // the chain from LDS: broadcast reads, then the 64 dependent adds
+    if (wv == 0) {
+      double x[kW];
+#pragma unroll
+      for (int k = 0; k < kW; ++k) x[k] = ws[k];
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < kW; ++k) s += x[k];
+      if (lane == 0) blocks[b] = s;
+    }
+    return;
+  }
   if (wv == 0) {
     const double v = ws[lane];
     double s = 0.0;
@@ -89,8 +105,8 @@ __global__ __launch_bounds__(256) void stream(const double* __restrict__ cls, in
   if (s == 12345.0) out[0] = s;
 }
 
-int main() {
-  const int64_t n = 1000000, n_pad = (n + kBlock - 1) / kBlock * kBlock;
+int main(int argc, char** argv) {
+  const int64_t n = argc > 1 ? std::atoll(argv[1]) : 1000000, n_pad = (n + kBlock - 1) / kBlock * kBlock;
   const int nb = (int)(n_pad / kBlock);
   double *cls, *w, *site, *blocks, *wsums;
   CK(hipMalloc(&cls, 4 * n_pad * 8));
@@ -104,13 +120,15 @@ int main() {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int v = 0; v < 5; ++v) {
+  for (int v = 0; v < 7; ++v) {
     auto run = [&]() {
       if (v == 0) red1024<0><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
       if (v == 1) red1024<1><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
       if (v == 2) red1024<2><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
       if (v == 3) red256<<<(unsigned)(n_pad / 256), 256>>>(cls, n_pad, w, site, wsums, n);
-      if (v == 4) stream<<<1024, 256>>>(cls, 5 * n_pad, site);
+      if (v == 5) red1024<5><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 6) red1024<6><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 4) stream<<<1024, 256>>>(cls, 4 * n_pad, site);  // the class terms only (4 * n_pad doubles)
     };
     for (int i = 0; i < 20; ++i) run();
     CK(hipEventRecord(a));
@@ -120,7 +138,7 @@ int main() {
     CK(hipEventSynchronize(b));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, a, b));
-    std::printf("variant %d: %.2f us per launch\n", v, ms * 1000.0 / reps);
+    std::printf("n %lld variant %d: %.2f us per launch\n", (long long)n, v, ms * 1000.0 / reps);
   }
   return 0;
 }
