@@ -2225,7 +2225,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // fires; on cfg5 it fires in almost every super-block (1.27 vs 1.14 ms), so opt-in
     // classes in the wave: next class's P(t) loads overlap this class's FMAs
     sh.ppipe = true;
-    sh.clk = env_is("PLK_DEBUG_CLOCK", '1');
+    sh.clk = env_is("PLK_DEBUG_CLOCK", '1') ? 1 : env_is("PLK_DEBUG_CLOCK", '2') ? 2 : 0;
     // PLK_JIT_BLOCKS=1: the root fragment forms the block sums (no wave_sums_to_blocks
     // launch).  Measured slower (cfg2 traversal 0.125 -> 0.160 ms): the wave that stores a
     // wave sum must wait for the store and the counter's atomic round trip (~3 us) before

@@ -413,7 +413,7 @@ struct JitShape {
   int L = 1;        // operand fetch lookahead (events)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
-  bool clk = false;         // PLK_DEBUG_CLOCK: per-workgroup shader-clock / constant-clock stamps (diagnostic)
+  int clk = 0;              // PLK_DEBUG_CLOCK: per-workgroup shader-clock / constant-clock stamps (diagnostic; 2: prologue only)
   // one class per workgroup (grid.z = class): the tables hold that class only (C x smaller, so
   // a fragment's cherries fit as quad units, JitUnit), and the root terms of the classes meet
   // in HBM (class_sums_to_blocks) instead of an LDS exchange.  One class per wave, no scaling.
@@ -907,10 +907,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     // Q's accumulator = contA, *= contB, then contrib<.., true> through P_Q.
     constexpr int U4_ = U_ * U_ * U_ * U_;
     const int q0_ = 1 + kFragQuadStart[frag], nq_ = kFragQuadStart[frag + 1] - kFragQuadStart[frag];
-    auto pcon = [&](int br_, const double (&v_)[4], double (&t_)[4]) {
-      const double2* P2 = reinterpret_cast<const double2*>(pmats + ((i64)br_ * C_ + c0) * 16);
-      double P[16];
-      _Pragma("unroll") for (int j = 0; j < 8; ++j) { const double2 pj = P2[j]; P[2 * j] = pj.x; P[2 * j + 1] = pj.y; }
+    auto pcon = [&](const double (&P)[16], const double (&v_)[4], double (&t_)[4]) {
       _Pragma("unroll") for (int x = 0; x < 4; ++x) {
         t_[x] = P[4 * x] * v_[0];
         t_[x] = __builtin_fma(P[4 * x + 1], v_[1], t_[x]);
@@ -918,46 +915,53 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         t_[x] = __builtin_fma(P[4 * x + 3], v_[3], t_[x]);
       }
     };
-    auto prow = [&](int t1_, int k1_, int t2_, int k2_, double (&v_)[4]) {
-      const double2* pa = reinterpret_cast<const double2*>(a.tipP + ((i64)t1_ * C_ + c0) * (U_ * 4) + k1_ * 4);
-      const double2* pb = reinterpret_cast<const double2*>(a.tipP + ((i64)t2_ * C_ + c0) * (U_ * 4) + k2_ * 4);
-      const double2 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
-      v_[0] = a0.x * b0.x; v_[1] = a0.y * b0.y; v_[2] = a1.x * b1.x; v_[3] = a1.y * b1.y;
+    auto pload = [&](int br_, double (&P)[16]) {  // (br_ wave-uniform: scalar loads)
+      const double* P1 = pmats + ((i64)br_ * C_ + c0) * 16;
+      _Pragma("unroll") for (int j = 0; j < 16; ++j) P[j] = P1[j];
     };
-    // phase 1: the two cherries' contribution rows of every quad (U^2 rows each), in the code
-    // rows' LDS space (staged only at the first super-block); phase 2: the quad rows from them
+    // One wave per quad (quads w, w + NWT_, ...), every load of the quad issued before its
+    // arithmetic: the quad's record and its three P(t) (the two cherries', Q's) wave-uniform.
+    // Phase 1: lanes [0, 2 U^2) form the two cherries' contribution rows (U^2 rows each) in the
+    // code rows' LDS space (staged only at the first super-block); phase 2: the wave's lanes
+    // form the quad rows from them.  The same operations per row as before (the interpreter's
+    // order: each cherry's pair product and contrib<.., true> through the cherry's P, Q's
+    // accumulator = contA, *= contB, then contrib<.., true> through P_Q).
     double* qtmp = reinterpret_cast<double*>(code_lds);
-    for (int t = threadIdx.x; t < nq_ * 2 * (U_ * U_); t += 64 * NWT_) {
-      const int kk = t / (2 * U_ * U_), hr = t - kk * (2 * U_ * U_), which = hr / (U_ * U_), r = hr - which * (U_ * U_);
+    for (int kk = w; kk < nq_; kk += NWT_) {
       const QuadD qd_ = kQuadD[q0_ + kk];
-      const int ca = r / U_, cb = r - ca * U_;
-      double v[4], o[4];
-      if (which == 0) {
-        prow(qd_.ta, ca, qd_.tb, cb, v);
-        pcon(qd_.brA, v, o);
-      } else {
-        prow(qd_.tc, ca, qd_.td, cb, v);
-        pcon(qd_.brB, v, o);
+      double PA[16], PB[16], PQ[16];
+      pload(qd_.brA, PA);
+      pload(qd_.brB, PB);
+      pload(qd_.brQ, PQ);
+      for (int hr = lane; hr < 2 * U_ * U_; hr += 64) {
+        const int which = hr / (U_ * U_), r = hr - which * (U_ * U_), ca = r / U_, cb = r - ca * U_;
+        const int t1 = which ? qd_.tc : qd_.ta, t2 = which ? qd_.td : qd_.tb;
+        const double2* pa = reinterpret_cast<const double2*>(a.tipP + ((i64)t1 * C_ + c0) * (U_ * 4) + ca * 4);
+        const double2* pb = reinterpret_cast<const double2*>(a.tipP + ((i64)t2 * C_ + c0) * (U_ * 4) + cb * 4);
+        const double2 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+        const double v[4] = {a0.x * b0.x, a0.y * b0.y, a1.x * b1.x, a1.y * b1.y};
+        double P[16], o[4];
+        _Pragma("unroll") for (int j = 0; j < 16; ++j) P[j] = which ? PB[j] : PA[j];
+        pcon(P, v, o);
+        double2* od = reinterpret_cast<double2*>(qtmp + ((i64)(2 * kk) * (U_ * U_) + hr) * 4);
+        od[0] = make_double2(o[0], o[1]);
+        od[1] = make_double2(o[2], o[3]);
       }
-      double2* od = reinterpret_cast<double2*>(qtmp + (i64)t * 4);
-      od[0] = make_double2(o[0], o[1]);
-      od[1] = make_double2(o[2], o[3]);
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < nq_ * U4_; t += 64 * NWT_) {
-      // (U4_ a multiple of 64: the wave's rows belong to one quad, so its record and P(t) are
-      // wave-uniform -- scalar loads)
-      const int kk = U4_ % 64 == 0 ? __builtin_amdgcn_readfirstlane(t / U4_) : t / U4_, r = t - kk * U4_;
-      const QuadD qd_ = kQuadD[q0_ + kk];
-      const int ab = r / (U_ * U_), cd = r - ab * (U_ * U_);
-      const double2* pa = reinterpret_cast<const double2*>(qtmp + ((i64)(2 * kk) * (U_ * U_) + ab) * 4);
-      const double2* pb = reinterpret_cast<const double2*>(qtmp + ((i64)(2 * kk + 1) * (U_ * U_) + cd) * 4);
-      const double2 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
-      double acc[4] = {a0.x, a0.y, a1.x, a1.y}, o[4];
-      acc[0] *= b0.x; acc[1] *= b0.y; acc[2] *= b1.x; acc[3] *= b1.y;
-      pcon(qd_.brQ, acc, o);
-      *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, r, 0)) = make_double2(o[0], o[1]);
-      *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, r, 2)) = make_double2(o[2], o[3]);
+      // (the rows just written are read by other lanes of this wave)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      _Pragma("unroll") for (int r = lane; r < U4_; r += 64) {
+        const int ab = r / (U_ * U_), cd = r - ab * (U_ * U_);
+        const double2* pa = reinterpret_cast<const double2*>(qtmp + ((i64)(2 * kk) * (U_ * U_) + ab) * 4);
+        const double2* pb = reinterpret_cast<const double2*>(qtmp + ((i64)(2 * kk + 1) * (U_ * U_) + cd) * 4);
+        const double2 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+        double acc[4] = {a0.x, a0.y, a1.x, a1.y}, o[4];
+        acc[0] *= b0.x; acc[1] *= b0.y; acc[2] *= b1.x; acc[3] *= b1.y;
+        pcon(PQ, acc, o);
+        *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, r, 0)) = make_double2(o[0], o[1]);
+        *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, r, 2)) = make_double2(o[2], o[3]);
+      }
     }
   }
   const CPd pm = (CPd)(pmats + c0 * 16);
@@ -1226,7 +1230,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     s += "    } break;\n";
   }
   s += "    default: break;\n    }\n  }\n";
-  if (sh.clk)
+  if (sh.clk == 1)
     s += "  if (threadIdx.x == 0) {\n"
          "    unsigned long long* q_ = clk_ + 4 * (((unsigned long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + "
          "blockIdx.x);\n"
@@ -1248,6 +1252,17 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   }
 }
 )PLKJIT";
+  if (sh.clk == 2) {
+    // PLK_DEBUG_CLOCK=2: the end stamp is taken where the super-block loop starts (the prologue:
+    // code fetch, table staging, quad build), not at the kernel's end.  (Inserted into the
+    // generated text, so that the ordinary programs' sources -- and their cached code -- do not change.)
+    const std::string anchor = "  for (int sb = blockIdx.x, sb_nx = 0; sb < a.n_sblocks; sb = sb_nx) {";
+    const size_t at = s.find(anchor);
+    if (at != std::string::npos)
+      s.insert(at, "  if (threadIdx.x == 0) { unsigned long long* q_ = clk_ + 4 * (((unsigned long long)blockIdx.z * "
+                   "gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x); const unsigned long long c1_ = clock64(), w1_ = "
+                   "wall_clock64(); q_[0] = clk_c0_; q_[1] = clk_w0_; q_[2] = c1_; q_[3] = w1_; }\n");
+  }
   return s;
 }
 

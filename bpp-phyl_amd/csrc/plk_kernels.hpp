@@ -1137,12 +1137,15 @@ __global__ __launch_bounds__(1024) void cls_blocks_kernel(const double* __restri
   }
   __syncthreads();
   if (wv == 0) {
-    const double v = ws[lane];
+    // the chain of adds in wave order, its operands read from LDS (broadcast reads, issued ahead
+    // of the adds; a shuffle per operand put a cross-lane round trip before every add)
+    double x[kW];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) x[k] = ws[k];
     double s = 0.0;
-    for (int k = 0; k < kW; ++k) {
-      const double x = __shfl(v, k, 64);
-      if (b * kW + k < n_waves) s += x;
-    }
+#pragma unroll
+    for (int k = 0; k < kW; ++k)
+      if (b * kW + k < n_waves) s += x[k];
     if (lane == 0) block_sums[b] = s;
   }
 }

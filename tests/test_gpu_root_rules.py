@@ -30,7 +30,8 @@ REL = 1e-12
 
 # path -> (S, C, n_taxa, traversal flags, PLK_TUNE keys)
 PATHS = {
-    "jit_tree4": (4, 4, 16, plk.PLK_FLAG_LNL_ONLY, {}),
+    "jit_tree4": (4, 4, 16, plk.PLK_FLAG_LNL_ONLY, {}),              # unscaled: one class per workgroup, quads
+    "jit_tree4_noquad": (4, 4, 16, plk.PLK_FLAG_LNL_ONLY, {"JIT_QUAD_KB": "0"}),   # every class in the wave
     "tree4": (4, 4, 16, plk.PLK_FLAG_LNL_ONLY, {"JIT": "0"}),
     "levelwise": (4, 3, 16, plk.PLK_FLAG_LEVELWISE, {}),
     "subtree_patterns": (4, 2, 16, plk.PLK_FLAG_SUBTREE_PATTERNS, {}),
@@ -72,7 +73,7 @@ def test_root_rules_vs_oracle(path, scaling, kind, monkeypatch):
                                                                  tiny=scaling)
     delta, pm2, census = negroot.choose(et, states, init, pm, pi, probs, kind)
     assert census["neg_terms"] > 0                       # the root saw terms <= 0
-    expect_path = {"levelwise20": "levelwise", "treeM64": "treeM"}.get(path, path)
+    expect_path = {"levelwise20": "levelwise", "treeM64": "treeM", "jit_tree4_noquad": "jit_tree4"}.get(path, path)
     got = {}
     for guard in (True, False):
         flags = tflags | (plk.PLK_FLAG_NONNEG_GUARD if guard else 0) | (plk.PLK_FLAG_SCALING if scaling else 0)
@@ -80,6 +81,8 @@ def test_root_rules_vs_oracle(path, scaling, kind, monkeypatch):
         eng.update_partials(phylo.split_ops(et.ops))
         lnl, site, _ = eng.root_loglik(et.root, want_sites=True, want_blocks=True)
         assert eng.kernel_path() == expect_path
+        if path == "jit_tree4" and not scaling:   # quads ran (three table nodes each; 8 cherries here)
+            assert eng.traversal_work()["table_nodes"] > et.n_tips // 2
         eng.close()
         lo, so = negroot.oracle_sites(et, states, init, pm2, probs, pi, scaling, nh_root=not guard)
         negroot.same_sites(site, so, REL)

@@ -8,6 +8,8 @@
 //   4: pure streaming read of the class terms (sum only)
 //   5: 0 with the block chain read from LDS (broadcast reads, then the 64 adds)
 //   6: 0 without the block chain (wave sums left in LDS)
+//   7-10: red_pipe<waves per block, batch>: <8,4>, <4,4>, <4,2>, <16,2> (next batch's loads
+//         issued before the current batch's log and reduction)
 // hipcc -O3 --offload-arch=gfx950 -o cls_reduce cls_reduce.hip; ./cls_reduce [patterns]
 #include <hip/hip_runtime.h>
 
@@ -78,6 +80,60 @@ __global__ __launch_bounds__(1024) void red1024(const double* __restrict__ cls, 
   }
 }
 
+
+// Pipelined: NWV waves per 4096-pattern block, each wave 64 / NWV pattern-waves in batches of B,
+// the next batch's loads issued before the current batch's log / reduction (double buffer);
+// the block chain from LDS.
+template <int NWV, int B>
+__global__ __launch_bounds__(64 * NWV) void red_pipe(const double* __restrict__ cls, int64_t n_pad,
+                                                     const double* __restrict__ w, double* __restrict__ site,
+                                                     double* __restrict__ blocks, int64_t n) {
+  constexpr int kW = kBlock / 64, KPW = kW / NWV, NB = KPW / B, C = 4;
+  __shared__ double ws[kW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, b = blockIdx.x;
+  double t[2][B][C + 1];
+  auto load = [&](int buf, int bi) {
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int k = wv + NWV * (bi * B + j);
+      const int64_t p = ((int64_t)b * kW + k) * 64 + lane;
+#pragma unroll
+      for (int c = 0; c < C; ++c) t[buf][j][c] = cls[(int64_t)c * n_pad + p];
+      t[buf][j][C] = w[p];
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int bi = 0; bi < NB; ++bi) {
+    if (bi + 1 < NB) load((bi + 1) & 1, bi + 1);
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int k = wv + NWV * (bi * B + j);
+      const int64_t p = ((int64_t)b * kW + k) * 64 + lane;
+      double l = 0.0;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        if (t[bi & 1][j][c] > 0.0) l += t[bi & 1][j][c];
+      const double r = log(l);
+      if (p < n) site[p] = r;
+      double wr = t[bi & 1][j][C] * r;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+      if (lane == 0) ws[k] = wr;
+    }
+  }
+  __syncthreads();
+  if (wv == 0) {
+    double x[kW];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) x[k] = ws[k];
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kW; ++k) s += x[k];
+    if (lane == 0) blocks[b] = s;
+  }
+}
+
 __global__ __launch_bounds__(256) void red256(const double* __restrict__ cls, int64_t n_pad, const double* __restrict__ w,
                                               double* __restrict__ site, double* __restrict__ wsums, int64_t n) {
   const int lane = threadIdx.x & 63;
@@ -120,7 +176,7 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int v = 0; v < 7; ++v) {
+  for (int v = 0; v < 11; ++v) {
     auto run = [&]() {
       if (v == 0) red1024<0><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
       if (v == 1) red1024<1><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
@@ -128,6 +184,10 @@ int main(int argc, char** argv) {
       if (v == 3) red256<<<(unsigned)(n_pad / 256), 256>>>(cls, n_pad, w, site, wsums, n);
       if (v == 5) red1024<5><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
       if (v == 6) red1024<6><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 7) red_pipe<8, 4><<<nb, 512>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 8) red_pipe<4, 4><<<nb, 256>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 9) red_pipe<4, 2><<<nb, 256>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 10) red_pipe<16, 2><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
       if (v == 4) stream<<<1024, 256>>>(cls, 4 * n_pad, site);  // the class terms only (4 * n_pad doubles)
     };
     for (int i = 0; i < 20; ++i) run();
