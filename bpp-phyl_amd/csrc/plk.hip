@@ -2220,6 +2220,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // class in the wave a ring slot is C x larger, so there two events ahead (cfg5 0.385 ms
     // at L = 2, 0.391 at L = 1; 1.48 vs 1.04 ms at L = 3 vs 1 before the P(t) stream)
     sh.L = tune_int("JIT_L", h->prog_ciw ? 2 : 3, 1, 8);
+    sh.RD = tune_int("JIT_RD", 1, 1, 8);  // table rows this many fetchers ahead (<= JIT_L)
     sh.minw = 0;
     // speculative no-rescale pass (plk_jit.hpp): a win only where rescaling never
     // fires; on cfg5 it fires in almost every super-block (1.27 vs 1.14 ms), so opt-in
@@ -2238,7 +2239,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.G != h->jit_shape.G || sh.U != h->jit_shape.U ||
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
         sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.clk != h->jit_shape.clk ||
-        sh.cls != h->jit_shape.cls || sh.soa != h->jit_shape.soa || sh.ps1 != h->jit_shape.ps1 ||
+        sh.cls != h->jit_shape.cls || sh.soa != h->jit_shape.soa || sh.ps1 != h->jit_shape.ps1 || sh.RD != h->jit_shape.RD ||
         sh.dc != h->jit_shape.dc) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
       if (rc) return rc;

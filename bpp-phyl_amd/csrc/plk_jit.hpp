@@ -411,6 +411,7 @@ struct JitShape {
   int TD = 0;       // most table doubles of any fragment (JitPlan::tab_doubles)
   bool scale = false;
   int L = 1;        // operand fetch lookahead (events)
+  int RD = 1;       // two-stage fetch: table rows RD fetchers ahead (codes L ahead; RD <= L)
   int minw = 0;     // __launch_bounds__ min waves per SIMD (0: compiler default)
   bool ppipe = true;        // classes in the wave: P(t) of the next class loaded during this one (contrib)
   int clk = 0;              // PLK_DEBUG_CLOCK: per-workgroup shader-clock / constant-clock stamps (diagnostic; 2: prologue only)
@@ -1135,7 +1136,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
       size_t n1 = 0, n2 = 0;  // two-stage pipeline: stage-1 / stage-2 fetches emitted
       if (L >= 2) {
         for (; n1 < fetchers.size() && n1 < (size_t)L; ++n1) emit_stage1(fetchers[n1]);
-        if (n2 < fetchers.size()) emit_stage2(fetchers[n2++]);
+        const size_t rd = (size_t)std::max(1, std::min(sh.RD, L));  // (a slot's row is used before its reuse)
+        for (; n2 < fetchers.size() && n2 < rd; ++n2) emit_stage2(fetchers[n2]);
       } else {
         for (; nf < fetchers.size() && nf < (size_t)L; ++nf) emit_fetch(fetchers[nf]);
       }
