@@ -10,6 +10,9 @@
 //   6: 0 without the block chain (wave sums left in LDS)
 //   7-10: red_pipe<waves per block, batch>: <8,4>, <4,4>, <4,2>, <16,2> (next batch's loads
 //         issued before the current batch's log and reduction)
+//   11, 12: 5 with the class terms interleaved per 64-pattern group ([group][C][64]); 12 with the
+//         weights as a fifth row of each group
+//   13: the product's loads alone (no log, no stores, no reduction)
 // hipcc -O3 --offload-arch=gfx950 -o cls_reduce cls_reduce.hip; ./cls_reduce [patterns]
 #include <hip/hip_runtime.h>
 
@@ -134,6 +137,73 @@ __global__ __launch_bounds__(64 * NWV) void red_pipe(const double* __restrict__ 
   }
 }
 
+
+// Interleaved layout: per 64-pattern group the class terms (and with W the weights too) as
+// consecutive 512-byte rows, [group][C (+1)][64] -- one contiguous chunk per pattern-wave
+template <bool W>
+__global__ __launch_bounds__(1024) void red_il(const double* __restrict__ cls, const double* __restrict__ w,
+                                               double* __restrict__ site, double* __restrict__ blocks, int64_t n) {
+  constexpr int kW = kBlock / 64, kPer = kW / 16, C = 4, R = W ? C + 1 : C;
+  __shared__ double ws[kW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, b = blockIdx.x;
+  double t[kPer][C], wt[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t g = (int64_t)b * kW + wv + 16 * j, p = g * 64 + lane;
+#pragma unroll
+    for (int c = 0; c < C; ++c) t[j][c] = cls[(g * R + c) * 64 + lane];
+    wt[j] = W ? cls[(g * R + C) * 64 + lane] : w[p];
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = wv + 16 * j;
+    const int64_t p = ((int64_t)b * kW + k) * 64 + lane;
+    double l = 0.0;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (t[j][c] > 0.0) l += t[j][c];
+    const double r = log(l);
+    if (p < n) site[p] = r;
+    double wr = wt[j] * r;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wr += __shfl_xor(wr, off, 64);
+    if (lane == 0) ws[k] = wr;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    double x[kW];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) x[k] = ws[k];
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kW; ++k) s += x[k];
+    if (lane == 0) blocks[b] = s;
+  }
+}
+
+
+// The product's access pattern with no arithmetic beyond one sum per lane (memory floor of
+// the shape): every load issued first, then one store per block
+__global__ __launch_bounds__(1024) void red_loads(const double* __restrict__ cls, int64_t n_pad,
+                                                  const double* __restrict__ w, double* __restrict__ blocks) {
+  constexpr int kW = kBlock / 64, kPer = kW / 16, C = 4;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, b = blockIdx.x;
+  double t[kPer][C + 1];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t p = ((int64_t)b * kW + wv + 16 * j) * 64 + lane;
+#pragma unroll
+    for (int c = 0; c < C; ++c) t[j][c] = cls[(int64_t)c * n_pad + p];
+    t[j][C] = w[p];
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+#pragma unroll
+    for (int c = 0; c <= C; ++c) s += t[j][c];
+  if (s == 12345.0) blocks[b] = s;
+}
+
 __global__ __launch_bounds__(256) void red256(const double* __restrict__ cls, int64_t n_pad, const double* __restrict__ w,
                                               double* __restrict__ site, double* __restrict__ wsums, int64_t n) {
   const int lane = threadIdx.x & 63;
@@ -165,7 +235,7 @@ int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? std::atoll(argv[1]) : 1000000, n_pad = (n + kBlock - 1) / kBlock * kBlock;
   const int nb = (int)(n_pad / kBlock);
   double *cls, *w, *site, *blocks, *wsums;
-  CK(hipMalloc(&cls, 4 * n_pad * 8));
+  CK(hipMalloc(&cls, 5 * n_pad * 8));  // (variant 12 reads a fifth row per group)
   CK(hipMalloc(&w, n_pad * 8));
   CK(hipMalloc(&site, n_pad * 8));
   CK(hipMalloc(&blocks, nb * 8));
@@ -176,7 +246,7 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int v = 0; v < 11; ++v) {
+  for (int v = 0; v < 14; ++v) {
     auto run = [&]() {
       if (v == 0) red1024<0><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
       if (v == 1) red1024<1><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
@@ -188,6 +258,9 @@ int main(int argc, char** argv) {
       if (v == 8) red_pipe<4, 4><<<nb, 256>>>(cls, n_pad, w, site, blocks, n);
       if (v == 9) red_pipe<4, 2><<<nb, 256>>>(cls, n_pad, w, site, blocks, n);
       if (v == 10) red_pipe<16, 2><<<nb, 1024>>>(cls, n_pad, w, site, blocks, n);
+      if (v == 11) red_il<false><<<nb, 1024>>>(cls, w, site, blocks, n);
+      if (v == 12) red_il<true><<<nb, 1024>>>(cls, w, site, blocks, n);
+      if (v == 13) red_loads<<<nb, 1024>>>(cls, n_pad, w, blocks);
       if (v == 4) stream<<<1024, 256>>>(cls, 4 * n_pad, site);  // the class terms only (4 * n_pad doubles)
     };
     for (int i = 0; i < 20; ++i) run();
