@@ -2241,7 +2241,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.clk != h->jit_shape.clk ||
         sh.cls != h->jit_shape.cls || sh.soa != h->jit_shape.soa || sh.ps1 != h->jit_shape.ps1 || sh.RD != h->jit_shape.RD ||
         sh.dc != h->jit_shape.dc) {
-      int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), "plk_jit_tree4", &h->jit_fn);
+      int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), jit_tree4_name(sh), &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;
       h->jit_resident = 0;

@@ -440,6 +440,10 @@ struct JitShape {
   }
 };
 
+// The generated kernel's name: one class per workgroup is plk_jit_tree4c, so that kernel-trace
+// statistics keep it apart from the classes-in-the-wave kernel (plk_jit_tree4) of other configs
+inline const char* jit_tree4_name(const JitShape& sh) { return sh.cls ? "plk_jit_tree4c" : "plk_jit_tree4"; }
+
 // Pattern groups per workgroup with the most waves resident per CU: LDS (160 KiB per CU)
 // against the tables every workgroup stages once, and VGPRs at the ~72 registers these
 // kernels take (7 waves per SIMD); ties go to fewer groups.
@@ -743,10 +747,10 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
            "#define U_ %d\n#define NT_ %d\n#define TD_ %d\n#define SC_ %s\n#define V_ (4 * CW_ * PW_)\n"
-           "extern \"C\" __global__ __launch_bounds__(%d%s) void plk_jit_tree4(JArgs a, const double* __restrict__ "
+           "extern \"C\" __global__ __launch_bounds__(%d%s) void %s(JArgs a, const double* __restrict__ "
            "pmats, int frag_base%s) {\n",
            C, CW, NW, PW, sh.G, NW * sh.G, U, std::max(sh.NT, 1), std::max(sh.TD, 4), sh.scale ? "true" : "false",
-           64 * NW * sh.G, minw_s.c_str(), sh.clk ? ", unsigned long long* __restrict__ clk_" : "");
+           64 * NW * sh.G, minw_s.c_str(), jit_tree4_name(sh), sh.clk ? ", unsigned long long* __restrict__ clk_" : "");
   s += buf;
   // PLK_DEBUG_CLOCK (diagnostic build of the same program): thread 0 of every workgroup records
   // the shader clock counter (clock64) and the constant 100 MHz counter (wall_clock64) at its

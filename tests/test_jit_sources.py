@@ -34,7 +34,7 @@ def emitter(tmp_path_factory):
 def test_emitted_kernel_compiles_for_gfx950(emitter, args):
     exe, d = emitter
     src = subprocess.run([exe, *args], check=True, capture_output=True, timeout=60).stdout.decode()
-    name = "plk_jit_treeM" if args[0].startswith("treeM") else "plk_jit_tree4"
+    name = "plk_jit_treeM" if args[0].startswith("treeM") else "plk_jit_tree4c" if args[0] == "tree4q" else "plk_jit_tree4"
     if args[0] == "tree4q":
         assert "kQuadD[] = {{0, 0, 0, 0, 0, 0, 0, 0},{0,1,2,3,8,9,10," in src   # the quad unit's record
     assert f"void {name}(" in src
