@@ -729,7 +729,9 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     (4, "balanced64", 3000, True, "JIT_DC=0 JIT_PW=1"), (2, "balanced300", 2000, True, "JIT_DC=0"),
     (4, "balanced64", 5000, False, "JIT_PW=1"), (4, "balanced64", 9000, True, "JIT_G=5"),
     # table rows two / three fetchers ahead (PLK_TUNE JIT_RD)
-    (4, "balanced64", 3000, True, "JIT_RD=2"), (2, "balanced300", 2000, False, "JIT_RD=3")])
+    (4, "balanced64", 3000, True, "JIT_RD=2"), (2, "balanced300", 2000, False, "JIT_RD=3"),
+    # fewer patterns than one super-block / one group (the idle groups recompute group 0, store nothing)
+    (4, "balanced64", 7, True, ""), (2, "balanced64", 129, False, ""), (1, "balanced64", 1, True, "")])
 def test_jit_tree4_quads_bitwise(C, tree_kind, n_patterns, guard, tune, monkeypatch):
     """One class per workgroup with quad units (plk_jit.hpp JitUnit / JitShape::cls: a node whose
     two children are unstored cherries is one table of U^4 rows, the classes' root terms meet in
