@@ -347,6 +347,7 @@ struct plk_handle_s {
   uint8_t* d_ucodes_dc = nullptr;       // JitShape::dc: [fragment][pattern][16] unit codes
   size_t ucodes_dc_cap = 0;
   bool ucodes_dc_valid = false;
+  int ucodes_dc_w = 0;                  // its 16-byte words per pattern (JitShape::dcw)
   int32_t* d_units_start = nullptr;     // CSR of the plan's units per fragment (unit_codes_dc_kernel)
   size_t units_start_cap = 0;
   uint8_t* d_ucodes = nullptr;  // code row of every table unit of jit_plan (unit_codes_kernel)
@@ -2171,23 +2172,28 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     sh.TD = h->jit_plan.tab_doubles;
     sh.QT = h->jit_plan.quad_tmp;
     sh.soa = tune_int("JIT_SOA", 1, 0, 1) != 0;
-    // direct codes where a fragment has at most 16 units (cfg2, 0.099 vs 0.111 ms traversal)
-    sh.dc = sh.cls && sh.NT <= 16 && tune_int("JIT_DC", 1, 0, 1) != 0;
-    if (sh.dc && !h->ucodes_dc_valid) {
+    // direct codes where a fragment has at most 16 units (cfg2, 0.099 vs 0.111 ms traversal);
+    // every class in the wave: up to 32 units in two 16-byte words (cfg5 shard traversal
+    // 345-353 vs 367-368 us; PLK_TUNE JIT_DC_CIW=0 keeps the code rows in LDS)
+    sh.dc = sh.cls ? sh.NT <= 16 && tune_int("JIT_DC", 1, 0, 1) != 0
+                   : h->prog_ciw && sh.NT <= 32 && tune_int("JIT_DC_CIW", 1, 0, 1) != 0;
+    sh.dcw = sh.NT <= 16 ? 1 : 2;
+    if (sh.dc && (!h->ucodes_dc_valid || h->ucodes_dc_w != sh.dcw)) {
       const int nfr = (int)h->jit_plan.units.size();
       std::vector<int32_t> us(1, 0);
       for (const auto& un : h->jit_plan.units) us.push_back(us.back() + (int)un.size());
-      int rc = ensure_cap(h, (void**)&h->d_ucodes_dc, &h->ucodes_dc_cap, (size_t)nfr * h->n_pad * 16);
+      int rc = ensure_cap(h, (void**)&h->d_ucodes_dc, &h->ucodes_dc_cap, (size_t)nfr * h->n_pad * 16 * sh.dcw);
       if (!rc) rc = ensure_cap(h, (void**)&h->d_units_start, &h->units_start_cap, us.size() * sizeof(int32_t));
       if (rc) return rc;
       HIPCHK(h, hipMemcpyAsync(h->d_units_start, us.data(), us.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                                h->stream));
       const dim3 dg((unsigned)((h->n_pad + 255) / 256), (unsigned)nfr);
       hipLaunchKernelGGL(unit_codes_dc_kernel, dg, dim3(256), 0, h->stream, h->d_ucodes, h->n_pad, h->d_units_start,
-                         reinterpret_cast<uint4*>(h->d_ucodes_dc));
+                         sh.dcw, reinterpret_cast<uint4*>(h->d_ucodes_dc));
       HIPCHK(h, hipGetLastError());
       HIPCHK(h, hipStreamSynchronize(h->stream));  // `us` goes out of scope
       h->ucodes_dc_valid = true;
+      h->ucodes_dc_w = sh.dcw;
     }
     sh.ps1 = tune_int("JIT_PS1", 0, 0, 1) != 0;
     // pattern groups per workgroup (they share the staged tables): with per-node rescaling
@@ -2201,7 +2207,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
     // (before G: the code rows take G x PW).  With direct codes (one class per workgroup, no code
     // rows in LDS) two patterns per lane: twice the independent work per wave at four waves
     // per SIMD (cfg2 traversal 0.093 vs 0.099 ms)
-    sh.PW = tune_int("JIT_PW", sh.dc ? 2 : 1, 1, 2);
+    sh.PW = tune_int("JIT_PW", sh.dc && sh.cls ? 2 : 1, 1, 2);
     sh.G = tune_int("JIT_G", 0, 0, 16);
     if (sh.G == 0) {
       if (sh.cls) {
@@ -2240,7 +2246,7 @@ int update_tree4(plk_handle h, const plk_op* ops, int n_ops) {
         sh.NT != h->jit_shape.NT || sh.TD != h->jit_shape.TD || sh.scale != h->jit_shape.scale || sh.L != h->jit_shape.L ||
         sh.minw != h->jit_shape.minw || sh.ppipe != h->jit_shape.ppipe || sh.clk != h->jit_shape.clk ||
         sh.cls != h->jit_shape.cls || sh.soa != h->jit_shape.soa || sh.ps1 != h->jit_shape.ps1 || sh.RD != h->jit_shape.RD ||
-        sh.dc != h->jit_shape.dc) {
+        sh.dc != h->jit_shape.dc || sh.dcw != h->jit_shape.dcw) {
       int rc = jit_function(h, jit_tree4_source(h->jit_plan, sh), jit_tree4_name(sh), &h->jit_fn);
       if (rc) return rc;
       h->jit_shape = sh;

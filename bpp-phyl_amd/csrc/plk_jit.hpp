@@ -428,6 +428,7 @@ struct JitShape {
   // codes, 16 bytes per pattern ([fragment][pattern][16], unit_codes_dc_kernel), into
   // registers one super-block ahead -- no code rows in LDS and one barrier per super-block
   bool dc = false;
+  int dcw = 1;       // direct codes: 16-byte words per pattern (16 units each; 2 for up to 32 units)
   int nw() const { return cls ? 1 : C / CW; }  // waves per pattern group
   size_t lds_bytes() const {
     const size_t nt = (size_t)std::max(NT, 1);
@@ -741,8 +742,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
   }
   s += ud + sc + scu + ot + otu + qs + qd + "};\n";
   const int CW = sh.CW, NW = sh.nw(), PW = sh.PW;
-  snprintf(buf, sizeof(buf), "#define CLS_ %d\n#define CT_ %d\n#define SOA_ %d\n#define DC_ %d\n", sh.cls ? 1 : 0,
-           sh.cls ? 1 : C, sh.soa ? 1 : 0, sh.dc ? 1 : 0);
+  snprintf(buf, sizeof(buf), "#define CLS_ %d\n#define CT_ %d\n#define SOA_ %d\n#define DC_ %d\n#define DCW_ %d\n",
+           sh.cls ? 1 : 0, sh.cls ? 1 : C, sh.soa ? 1 : 0, sh.dc ? 1 : 0, sh.dc ? sh.dcw : 1);
   s += buf;
   snprintf(buf, sizeof(buf),
            "#define C_ %d\n#define CW_ %d\n#define NW_ %d\n#define PW_ %d\n#define G_ %d\n#define NWT_ %d\n"
@@ -790,13 +791,16 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     _Pragma("unroll") for (int m = 0; m < NI_; ++m)
       if (q0_ + ic_[m] < a.n_pad) va_[m] = ucodes[iu_[m] + (q0_ >> 4)];
   };
-  // DC_: this wave's own patterns' codes (16 unit bytes per pattern), next super-block's
-  uint4 cv_[PW_], cvn_[PW_];
-  const uint4* dcodes = reinterpret_cast<const uint4*>(a.codes) + (i64)frag * a.n_pad;
+  // DC_: this wave's own patterns' codes (DCW_ 16-byte words per pattern: unit k is byte k),
+  // next super-block's
+  uint4 cv_[PW_][DCW_], cvn_[PW_][DCW_];
+  const uint4* dcodes = reinterpret_cast<const uint4*>(a.codes) + (i64)frag * a.n_pad * DCW_;
   auto fetch_dc = [&](int sb_) {
     const i64 q0_ = (i64)sb_ * (64 * PW_ * G_);
     const i64 pp_ = (q0_ + g * (64 * PW_) < a.n_pad ? q0_ + g * (64 * PW_) : q0_) + lane;
-    if (sb_ < a.n_sblocks) _Pragma("unroll") for (int pw = 0; pw < PW_; ++pw) cvn_[pw] = dcodes[pp_ + 64 * pw];
+    if (sb_ < a.n_sblocks)
+      _Pragma("unroll") for (int pw = 0; pw < PW_; ++pw)
+        _Pragma("unroll") for (int w_ = 0; w_ < DCW_; ++w_) cvn_[pw][w_] = dcodes[(pp_ + 64 * pw) * DCW_ + w_];
   };
   (void)cv_; (void)cvn_; (void)dcodes;
   // (issued before the table staging below: its loads overlap it)
@@ -977,7 +981,7 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
 // unit k: codes of the lane's patterns (4 per int), then their table rows (R rows per
 // class at OFF doubles from the class base TB)
 #define CODEF(Q, k) { Q = 0; _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) \
-    Q |= (DC_ ? (int)((cvw(cv_[pw_], (k) >> 2) >> (8 * ((k) & 3))) & 255) : (int)crow[(k) * (64 * PW_) + 64 * pw_]) << (8 * pw_); }
+    Q |= (DC_ ? (int)((cvw(cv_[pw_][(k) >> 4], ((k) >> 2) & 3) >> (8 * ((k) & 3))) & 255) : (int)crow[(k) * (64 * PW_) + 64 * pw_]) << (8 * pw_); }
 #define ROWF(F, TB, OFF, R, Q) { _Pragma("unroll") for (int pw_ = 0; pw_ < PW_; ++pw_) { \
     const double* r0_ = TB + (OFF) + TABIX(R, ((Q) >> (8 * pw_)) & 255, 0); \
     _Pragma("unroll") for (int cw_ = 0; cw_ < CW_; ++cw_) { \
@@ -1020,7 +1024,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
     (void)toff;
     const int sl_ = DC_ ? (it_ & 1) : 0;
     if (DC_) {
-      _Pragma("unroll") for (int pw = 0; pw < PW_; ++pw) cv_[pw] = cvn_[pw];
+      _Pragma("unroll") for (int pw = 0; pw < PW_; ++pw)
+        _Pragma("unroll") for (int w_ = 0; w_ < DCW_; ++w_) cv_[pw][w_] = cvn_[pw][w_];
     } else {
       __syncthreads();  // the previous super-block is done with code_lds / xch (and tab is staged)
       _Pragma("unroll") for (int m = 0; m < NI_; ++m)

@@ -1061,17 +1061,19 @@ struct RootArgs {
 };
 
 // Direct-code layout of the generated 4-state kernel (plk_jit.hpp JitShape::dc): fragment f's
-// unit codes of pattern p as 16 bytes, byte k = unit k (at most 16 units), from the per-unit
-// rows of unit_codes_kernel.  units_start: CSR of the fragments' units (n_frag + 1 entries).
+// unit codes of pattern p as dw 16-byte words, byte k = unit k (at most 16 dw units), from the
+// per-unit rows of unit_codes_kernel.  units_start: CSR of the fragments' units (n_frag + 1 entries).
 __global__ __launch_bounds__(256) void unit_codes_dc_kernel(const uint8_t* __restrict__ rows, int64_t n_pad,
-                                                            const int32_t* __restrict__ units_start,
+                                                            const int32_t* __restrict__ units_start, int dw,
                                                             uint4* __restrict__ out) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pad) return;
   const int f = blockIdx.y, u0 = units_start[f], nu = units_start[f + 1] - u0;
-  unsigned w[4] = {0u, 0u, 0u, 0u};
-  for (int k = 0; k < nu && k < 16; ++k) w[k >> 2] |= (unsigned)rows[(int64_t)(u0 + k) * n_pad + p] << (8 * (k & 3));
-  out[(int64_t)f * n_pad + p] = make_uint4(w[0], w[1], w[2], w[3]);
+  unsigned w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  for (int k = 0; k < nu && k < 16 * dw && k < 32; ++k)
+    w[k >> 2] |= (unsigned)rows[(int64_t)(u0 + k) * n_pad + p] << (8 * (k & 3));
+  for (int j = 0; j < dw && j < 2; ++j)
+    out[((int64_t)f * n_pad + p) * dw + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
 }
 
 // The root reduction of a traversal run with one class per workgroup (plk_jit.hpp, JitShape::cls):

@@ -4,6 +4,7 @@
 // a GPU (the library compiles these sources only at run time, on the device).
 //   jit_emit <tree4|treeM> <C> <scale 0|1> [S (treeM: 20 | 4)] > kernel.hip
 //   jit_emit tree4q <C> 0 > kernel.hip: one class per workgroup with a quad unit (JitShape::cls)
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
@@ -130,7 +131,10 @@ int main(int argc, char** argv) {
     sh.TD = plan.tab_doubles;
     sh.QT = plan.quad_tmp;
     sh.soa = std::getenv("JIT_EMIT_SOA") != nullptr;
-    sh.dc = sh.cls && std::getenv("JIT_EMIT_DC") != nullptr;
+    // JIT_EMIT_DC=<words>: direct codes (one class per workgroup; or every class in the wave, with
+    // the given 16-byte words per pattern)
+    sh.dc = (sh.cls || sh.CW > 1) && std::getenv("JIT_EMIT_DC") != nullptr;
+    if (sh.dc) sh.dcw = std::max(1, std::atoi(std::getenv("JIT_EMIT_DC")));
     sh.G = 1;
     sh.PW = 1;
     sh.L = sh.CW > 1 ? 2 : 3;

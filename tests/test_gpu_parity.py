@@ -731,7 +731,9 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     # table rows two / three fetchers ahead (PLK_TUNE JIT_RD)
     (4, "balanced64", 3000, True, "JIT_RD=2"), (2, "balanced300", 2000, False, "JIT_RD=3"),
     # fewer patterns than one super-block / one group (the idle groups recompute group 0, store nothing)
-    (4, "balanced64", 7, True, ""), (2, "balanced64", 129, False, ""), (1, "balanced64", 1, True, "")])
+    (4, "balanced64", 7, True, ""), (2, "balanced64", 129, False, ""), (1, "balanced64", 1, True, ""),
+    # the P(t) load stream of the classes-in-the-wave kernel with one class per wave
+    (4, "balanced64", 3000, True, "JIT_PS1=1")])
 def test_jit_tree4_quads_bitwise(C, tree_kind, n_patterns, guard, tune, monkeypatch):
     """One class per workgroup with quad units (plk_jit.hpp JitUnit / JitShape::cls: a node whose
     two children are unstored cherries is one table of U^4 rows, the classes' root terms meet in
@@ -770,6 +772,48 @@ def test_jit_tree4_quads_bitwise(C, tree_kind, n_patterns, guard, tune, monkeypa
         assert tq > tn   # quads replace three table nodes each where cherries replaced one
     lo, so = oracle_for(et, states, phylo.DNA.init_table, rates, probs, m.pi, [m])
     check(lq, sq, lo, so)   # (positive partials: both root rules are the same sum here)
+
+
+@pytest.mark.parametrize("C,n_taxa,n_patterns,extra", [(4, 512, 30_000, ""), (4, 64, 5_000, "tiny"),
+                                                       (2, 150, 3_000, ""), (4, 64, 700, "ambig")])
+def test_jit_tree4_direct_codes_classes_in_wave_bitwise(C, n_taxa, n_patterns, extra, monkeypatch):
+    """Every class in the wave (rescaling) with direct codes (PLK_TUNE JIT_DC_CIW=1: each wave
+    loads its own patterns' unit codes, up to 32 units in two 16-byte words, one barrier per
+    super-block): lnL, per-pattern lnL and block sums bitwise those of the staged code rows,
+    over two evaluations; the oracle at 1e-12."""
+    tree = phylo.balanced_tree(n_taxa, seed=31, lo=0.05, hi=0.4) if n_taxa != 150 else \
+        _random_topology(150, np.random.default_rng(8), 0.05, 0.4, poly=0.0)
+    et = phylo.engine_tree(tree)
+    rng = np.random.default_rng(C * 17 + n_patterns)
+    m = phylo.gtr(*rng.uniform(0.3, 2.0, 5), *rng.dirichlet(np.ones(4) * 5))
+    rates, probs = phylo.gamma_rates(C, 0.5)
+    wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, True, True, 5)
+    states = wl.simulate(0, n_patterns).astype(np.int32)
+    init = phylo.DNA.init_table
+    if extra == "tiny":
+        init = np.array(init, dtype=np.float64, copy=True)
+        init[4] = 1e-80
+        states[rng.random(states.shape) < 0.3] = 4
+    elif extra == "ambig":
+        mask = rng.random(states.shape) < 0.05
+        states[mask] = rng.integers(4, 15, size=mask.sum())
+    flags = plk.PLK_FLAG_NONNEG_GUARD | plk.PLK_FLAG_LNL_ONLY | plk.PLK_FLAG_SCALING
+    res = {}
+    for name, tune in (("rows", "JIT_DC_CIW=0"), ("dc", "JIT_DC_CIW=1")):
+        monkeypatch.setenv("PLK_TUNE", tune)
+        eng = engine_for(et, 4, C, n_patterns, states, init, rates, probs, m.pi, [m], flags=flags)
+        a = run_engine(eng, et)
+        b = run_engine(eng, et)
+        assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+        assert eng.kernel_path() == "jit_tree4"
+        res[name] = a
+        eng.close()
+    (l0, s0, b0), (l1, s1, b1) = res["rows"], res["dc"]
+    assert l0 == l1 and np.array_equal(s0, s1) and np.array_equal(b0, b1)
+    if extra == "tiny":
+        assert s1.min() < -256 * np.log(2)   # rescaling fired
+    lo, so = oracle_for(et, states, init, rates, probs, m.pi, [m], scaling=True)
+    check(l1, s1, lo, so)
 
 
 @pytest.mark.parametrize("C,n_taxa,n_patterns,scaling", [(4, 64, 320_000, False), (4, 512, 60_000, True)])

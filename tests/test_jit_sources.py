@@ -31,14 +31,20 @@ def emitter(tmp_path_factory):
     ("tree4", "4", "0"), ("tree4", "4", "1", "0", "1"), ("tree4", "1", "1"), ("tree4q", "4", "0"), ("tree4q", "2", "0"),
     ("treeM", "4", "1", "20"), ("treeM", "1", "0", "20"), ("treeM", "4", "0", "4"),
     ("treeM_deep", "4", "1", "20", "5")])
-def test_emitted_kernel_compiles_for_gfx950(emitter, args):
+@pytest.mark.parametrize("dc", [None, "2"])
+def test_emitted_kernel_compiles_for_gfx950(emitter, args, dc):
     exe, d = emitter
-    src = subprocess.run([exe, *args], check=True, capture_output=True, timeout=60).stdout.decode()
+    if dc and not (args[0] == "tree4q" or (args[0] == "tree4" and len(args) > 4 and args[4] == "1")):
+        pytest.skip("direct codes: one class per workgroup or every class in the wave")
+    env = dict(os.environ, **({"JIT_EMIT_DC": dc} if dc else {}))
+    src = subprocess.run([exe, *args], check=True, capture_output=True, timeout=60, env=env).stdout.decode()
+    if dc:
+        assert "#define DC_ 1\n#define DCW_ 2" in src
     name = "plk_jit_treeM" if args[0].startswith("treeM") else "plk_jit_tree4c" if args[0] == "tree4q" else "plk_jit_tree4"
     if args[0] == "tree4q":
         assert "kQuadD[] = {{0, 0, 0, 0, 0, 0, 0, 0},{0,1,2,3,8,9,10," in src   # the quad unit's record
     assert f"void {name}(" in src
-    path = d / ("k_" + "_".join(args) + ".hip")
+    path = d / ("k_" + "_".join(args) + ("_dc" if dc else "") + ".hip")
     # hiprtc includes the HIP device runtime implicitly; hipcc needs the header
     path.write_text("#include <hip/hip_runtime.h>\n" + src)
     r = subprocess.run([HIPCC, "-x", "hip", "--offload-arch=gfx950", "--cuda-device-only", "-O3", "-c", "-o",
