@@ -31,11 +31,18 @@ def emitter(tmp_path_factory):
     ("tree4", "4", "0"), ("tree4", "4", "1", "0", "1"), ("tree4", "1", "1"), ("tree4q", "4", "0"), ("tree4q", "2", "0"),
     ("treeM", "4", "1", "20"), ("treeM", "1", "0", "20"), ("treeM", "4", "0", "4"),
     ("treeM_deep", "4", "1", "20", "5")])
-@pytest.mark.parametrize("dc", [None, "2"])
-def test_emitted_kernel_compiles_for_gfx950(emitter, args, dc):
+def test_emitted_kernel_compiles_for_gfx950(emitter, args):
+    _compile_emitted(emitter, args, None)
+
+
+# direct codes (two 16-byte words per pattern): one class per workgroup, every class in the wave
+@pytest.mark.parametrize("args", [("tree4q", "4", "0"), ("tree4", "4", "1", "0", "1")])
+def test_emitted_direct_codes_kernel_compiles_for_gfx950(emitter, args):
+    _compile_emitted(emitter, args, "2")
+
+
+def _compile_emitted(emitter, args, dc):
     exe, d = emitter
-    if dc and not (args[0] == "tree4q" or (args[0] == "tree4" and len(args) > 4 and args[4] == "1")):
-        pytest.skip("direct codes: one class per workgroup or every class in the wave")
     env = dict(os.environ, **({"JIT_EMIT_DC": dc} if dc else {}))
     src = subprocess.run([exe, *args], check=True, capture_output=True, timeout=60, env=env).stdout.decode()
     if dc:
