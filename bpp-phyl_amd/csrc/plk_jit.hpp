@@ -183,6 +183,8 @@ __device__ __forceinline__ unsigned long long launder_s(unsigned long long x) {
 __device__ __forceinline__ unsigned cvw(const uint4& v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
 // Table element x of row r (R rows per class block): [row][4] or, with SOA_, [half][row][2]
 #define TABIX(R, r, x) (SOA_ ? ((x) >> 1) * ((R) * 2) + (r) * 2 + ((x) & 1) : (r) * 4 + (x))
+// a quad table's row position (plk_kernels.hpp quad_row: unit_codes_kernel stores it as the code)
+#define QROW_(r) (U_ == 4 ? (((r) & ~15) | (((r) + 7 * (((r) >> 6) & 3) + 7 * (((r) >> 4) & 3)) & 15)) : (r))
 __device__ __forceinline__ unsigned long long launder_v(unsigned long long x) {
   asm volatile("" : "+v"(x));
   return x;
@@ -968,8 +970,8 @@ inline std::string jit_tree4_source(const JitPlan& plan, const JitShape& sh) {
         double acc[4] = {a0.x, a0.y, a1.x, a1.y}, o[4];
         acc[0] *= b0.x; acc[1] *= b0.y; acc[2] *= b1.x; acc[3] *= b1.y;
         pcon(PQ, acc, o);
-        *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, r, 0)) = make_double2(o[0], o[1]);
-        *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, r, 2)) = make_double2(o[2], o[3]);
+        *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, QROW_(r), 0)) = make_double2(o[0], o[1]);
+        *reinterpret_cast<double2*>(tab + qd_.off + TABIX(U4_, QROW_(r), 2)) = make_double2(o[2], o[3]);
       }
     }
   }

@@ -1018,6 +1018,16 @@ __global__ __launch_bounds__(256) void tip_table_kernel(const double* __restrict
 // Bytes are combined four to a word: a byte times U plus a byte < U stays below 256.
 // units[k] = (ta, tb, tc, td): a tip (tb < 0), a cherry (ca U + cb) or a quad
 // (((ca U + cb) U + cc) U + cd, plk_jit.hpp JitUnit); 4 codes per 32-bit word, bytes stay < 256
+// Position of row r (combined code ((ca 4 + cb) 4 + cc) 4 + cd) in a quad table of 256 rows:
+// each 16-row block is rotated by 7 (ca + cb), so that the 16-byte half-rows that one
+// ds_read_b128 lane group gathers land on distinct bank slots more often -- sibling tips tend to
+// share a code, which the plain order (slot = 4 cc + cd) maps onto 4 of the 16 slots (cfg2's
+// data: 2.29 -> 1.47 LDS cycles per 16-lane group, tools/lds_conflict_sim.py).  The generated
+// kernel's quad build places rows the same way (plk_jit.hpp QROW_).
+__host__ __device__ inline int quad_row(int r) {
+  return (r & ~15) | ((r + 7 * ((r >> 6) & 3) + 7 * ((r >> 4) & 3)) & 15);
+}
+
 __global__ __launch_bounds__(256) void unit_codes_kernel(const uint8_t* __restrict__ codes, int64_t n_pad,
                                                          const int4* __restrict__ units, int U,
                                                          uint8_t* __restrict__ out) {
@@ -1033,6 +1043,18 @@ __global__ __launch_bounds__(256) void unit_codes_kernel(const uint8_t* __restri
     v.y = v.y * U + b.y;
     v.z = v.z * U + b.z;
     v.w = v.w * U + b.w;
+  }
+  if (u.w >= 0 && U == 4) {
+    // quad rows are placed by quad_row (one class per workgroup's tables), so the code is the
+    // row's position
+    unsigned* wv = &v.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      unsigned o = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) o |= (unsigned)quad_row((int)((wv[j] >> (8 * b)) & 255u)) << (8 * b);
+      wv[j] = o;
+    }
   }
   reinterpret_cast<uint4*>(out + (int64_t)blockIdx.y * n_pad)[i] = v;
 }
