@@ -733,7 +733,9 @@ def test_jit_tree4_bitwise_equals_interpreter(C, tree_kind, n_patterns, scaling,
     # fewer patterns than one super-block / one group (the idle groups recompute group 0, store nothing)
     (4, "balanced64", 7, True, ""), (2, "balanced64", 129, False, ""), (1, "balanced64", 1, True, ""),
     # the P(t) load stream of the classes-in-the-wave kernel with one class per wave
-    (4, "balanced64", 3000, True, "JIT_PS1=1")])
+    (4, "balanced64", 3000, True, "JIT_PS1=1"),
+    # 3 / 2 codes in use (U^4 = 81 / 16 rows: quad rows in the plain order)
+    (4, "balanced64:u3", 3000, True, ""), (2, "balanced64:u2", 2000, False, "")])
 def test_jit_tree4_quads_bitwise(C, tree_kind, n_patterns, guard, tune, monkeypatch):
     """One class per workgroup with quad units (plk_jit.hpp JitUnit / JitShape::cls: a node whose
     two children are unstored cherries is one table of U^4 rows, the classes' root terms meet in
@@ -742,6 +744,7 @@ def test_jit_tree4_quads_bitwise(C, tree_kind, n_patterns, guard, tune, monkeypa
     balanced, multi-tier, caterpillar (no quads) and random trees, a partial quad budget, both
     root rules, direct codes (DC, two patterns per lane: the default) and staged code rows; the
     oracle at 1e-12.  ACGT data (4 codes in use: U^4 = 256 rows)."""
+    tree_kind, _, ucodes = tree_kind.partition(":u")
     if tree_kind.startswith("balanced"):
         tree = phylo.balanced_tree(int(tree_kind[8:]), seed=23, lo=0.05, hi=0.4)
     elif tree_kind.startswith("random"):
@@ -754,6 +757,8 @@ def test_jit_tree4_quads_bitwise(C, tree_kind, n_patterns, guard, tune, monkeypa
     rates, probs = phylo.gamma_rates(C, 0.5) if C > 1 else (np.ones(1), np.ones(1))
     wl = workload.Workload("m", et, [m], None, rates, probs, m.pi, phylo.DNA, n_patterns, False, True, 5)
     states = wl.simulate(0, n_patterns).astype(np.int32)
+    if ucodes:
+        states %= int(ucodes)   # only the first ucodes nucleotide codes in use
     flags = (plk.PLK_FLAG_NONNEG_GUARD if guard else 0) | plk.PLK_FLAG_LNL_ONLY
     res = {}
     for name, extra in (("quads", ""), ("noquads", "JIT_QUAD_KB=0"), ("interp", "JIT=0")):
